@@ -1,0 +1,237 @@
+// K4 prefill_attn_varlen (causal, GQA) and K9c encoder_attn (bidirectional) — one flash-attention
+// forward for packed variable-length sequences (cu_seqlens), head_dim 64 or 128, bf16 in/out.
+//
+// Workgroup = 4 waves = 64 query rows of one (sequence, query head); each wave owns 16 rows and
+// walks 32-key tiles that all 4 waves share through a double-buffered, XOR-swizzled LDS image
+// (register-staged: next tile's global loads are issued before the current tile's MFMAs and written
+// to LDS after them — cdna_hip_programming.md T14).
+//
+// Per wave and key tile (mfma_f32_16x16x32_bf16; lane l: r16 = l & 15, g = l >> 4):
+//   S^T = K Q^T :  A = K rows from LDS (ds_read_b128, chunk XOR row swizzle: T2),
+//                  B = Q^T held in registers for the whole kernel;
+//                  C: lane reg r = S^T[key 4g + r][query r16]   (two 16-key subtiles)
+//   O  += P V   :  A = the softmaxed S^T registers themselves (k permuted {4g+0..3, 16+4g+0..3}),
+//                  B = V columns by ds_read_b64_tr_b16 (T10 hardware transpose), same permutation;
+//                  C: lane reg r = O[query 4g + r][dim 16n + r16]
+// so P never leaves registers.  Online softmax in the log2 domain; rows are finite-initialised
+// (-1e30) so fully-masked tiles cannot produce NaN.
+#include "common.h"
+
+namespace lwc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+LWC_DEVICE float4v mfma16p(const short8& a, const short8& b, const float4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+constexpr int kQT = 64;  // query rows per workgroup
+constexpr int kKT = 32;  // keys per tile
+
+struct PrefillParams {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* out;
+  const int* cu_seqlens;
+  int q_stride, k_stride, v_stride, o_stride;  // elements per token row
+  int Hq, Hkv, nseq, max_tiles;
+  float scale;
+  int causal;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
+  constexpr int CPR = D / 8;                // 16-byte chunks per row
+  constexpr int KS = D / 32;                // k-steps for S
+  constexpr int NS = D / 16;                // n-subtiles for O
+  constexpr int TILE_BYTES = kKT * D * 2;   // one K or V tile
+  constexpr int CH_PER_THREAD = kKT * CPR / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];  // [buf][K|V]
+
+  const int seq = blockIdx.x / p.max_tiles, qtile = blockIdx.x % p.max_tiles;
+  const int hq = blockIdx.y, kvh = hq / (p.Hq / p.Hkv);
+  const int s0 = p.cu_seqlens[seq], len = p.cu_seqlens[seq + 1] - s0;
+  const int q0 = qtile * kQT;
+  if (q0 >= len) return;  // whole workgroup exits together (uniform)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int qrow = q0 + wid * 16 + r16;  // this lane's query (as B-operand column)
+
+  short8 qf[KS];
+  {
+    const int qr = qrow < len ? qrow : len - 1;
+    const bf16_t* qp = p.q + (size_t)(s0 + qr) * p.q_stride + hq * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const short8*>(qp + 32 * s + 8 * g);
+  }
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const int q_last = min(len, q0 + kQT) - 1;
+  const int kv_end = p.causal ? q_last + 1 : len;
+  const int ntiles = (kv_end + kKT - 1) / kKT;
+
+  // staging registers
+  uint4v stk[CH_PER_THREAD], stv[CH_PER_THREAD];
+  auto gload = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < CH_PER_THREAD; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c / CPR, ch = c % CPR;
+      const int key = tile * kKT + row;
+      if (key < len) {
+        stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(s0 + key) * p.k_stride + kvh * D + ch * 8);
+        stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(s0 + key) * p.v_stride + kvh * D + ch * 8);
+      } else {
+        stk[i] = uint4v{0, 0, 0, 0};
+        stv[i] = uint4v{0, 0, 0, 0};
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* kb = smem + buf * 2 * TILE_BYTES;
+    char* vb = kb + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < CH_PER_THREAD; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c / CPR, ch = c % CPR;
+      const int off = (row * CPR + (ch ^ (row & (CPR - 1)))) * 16;
+      *reinterpret_cast<uint4v*>(kb + off) = stk[i];
+      *reinterpret_cast<uint4v*>(vb + off) = stv[i];
+    }
+  };
+
+  float4v o[NS];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) o[n] = float4v{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);  // issue next tile's loads before the MFMAs (T14)
+    const char* kb = smem + buf * 2 * TILE_BYTES;
+    const char* vb = kb + TILE_BYTES;
+    // ---- S^T for the two 16-key subtiles ----
+    float4v sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int ch = 4 * s + g;
+      const int rA = r16, rB = 16 + r16;
+      const short8 ka = *reinterpret_cast<const short8*>(kb + (rA * CPR + (ch ^ (rA & (CPR - 1)))) * 16);
+      const short8 kbv = *reinterpret_cast<const short8*>(kb + (rB * CPR + (ch ^ (rB & (CPR - 1)))) * 16);
+      sa = mfma16p(ka, qf[s], sa);
+      sb = mfma16p(kbv, qf[s], sb);
+    }
+    // ---- mask + online softmax (per query r16) ----
+    float pa[4], pb[4];
+    float mx = -1e30f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ka_ = t * kKT + 4 * g + r, kb_ = ka_ + 16;
+      const bool va = ka_ < len && (!p.causal || ka_ <= qrow);
+      const bool vbk = kb_ < len && (!p.causal || kb_ <= qrow);
+      pa[r] = va ? sa[r] * sl2 : -INFINITY;
+      pb[r] = vbk ? sb[r] * sl2 : -INFINITY;
+      mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = exp2f(m - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pa[r] = exp2f(pa[r] - m_new);
+      pb[r] = exp2f(pb[r] - m_new);
+      rs += pa[r] + pb[r];
+    }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = m_new;
+    float al[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) al[r] = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+    for (int n = 0; n < NS; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[n][r] *= al[r];
+    short8 pf;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pf[r] = (short)f2bf(pa[r]);
+      pf[4 + r] = (short)f2bf(pb[r]);
+    }
+    // ---- O += P V, V columns via the hardware transpose read ----
+    const int qq = r16 >> 2, pp = r16 & 3;
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const int chunk = 2 * n + (pp >> 1);
+      const int rowA = 4 * g + qq, rowB = 16 + 4 * g + qq;
+      const int offA = (rowA * CPR + (chunk ^ (rowA & (CPR - 1)))) * 16 + (pp & 1) * 8;
+      const int offB = (rowB * CPR + (chunk ^ (rowB & (CPR - 1)))) * 16 + (pp & 1) * 8;
+      const short4v va4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vb + offA));
+      const short4v vb4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vb + offB));
+      short8 vf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        vf[r] = va4[r];
+        vf[4 + r] = vb4[r];
+      }
+      o[n] = mfma16p(pf, vf, o[n]);
+    }
+    if (t + 1 < ntiles) {
+      __syncthreads();  // everyone done reading buf^1 from the previous iteration
+      lstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: normalise, stage the wave's 16 x D tile through LDS, 16 B stores ----
+  float linv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float lr = __shfl(l, 4 * g + r, 64);
+    linv[r] = lr > 0.f ? 1.f / lr : 0.f;
+  }
+  __syncthreads();
+  bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 16 * D;
+#pragma unroll
+  for (int n = 0; n < NS; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ot[(4 * g + r) * D + 16 * n + r16] = f2bf(o[n][r] * linv[r]);
+  __syncthreads();
+  for (int c = lane; c < 16 * CPR; c += 64) {
+    const int row = c / CPR, ch = c % CPR;
+    const int qr = q0 + wid * 16 + row;
+    if (qr < len)
+      *reinterpret_cast<uint4v*>(p.out + (size_t)(s0 + qr) * p.o_stride + hq * D + ch * 8) =
+          *reinterpret_cast<const uint4v*>(ot + row * D + ch * 8);
+  }
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v, void* out, const int* cu_seqlens,
+                                     int nseq, int max_seqlen, int q_stride, int k_stride, int v_stride, int o_stride,
+                                     int Hq, int Hkv, int D, float scale, int causal, hipStream_t s) {
+  using namespace lwc;
+  if (Hq % Hkv != 0) return -1;
+  if (nseq == 0 || max_seqlen == 0) return 0;
+  const int max_tiles = (max_seqlen + kQT - 1) / kQT;
+  PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)out, cu_seqlens, q_stride, k_stride,
+                  v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal};
+  dim3 grid(nseq * max_tiles, Hq);
+  if (D == 128)
+    prefill_attn_kernel<128><<<grid, 256, 0, s>>>(p);
+  else if (D == 64)
+    prefill_attn_kernel<64><<<grid, 256, 0, s>>>(p);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

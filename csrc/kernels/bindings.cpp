@@ -1,0 +1,300 @@
+// torch <-> HIP kernel bindings for llm_weighted_consensus_amd.ops._kernels.
+// Every op: validates device/dtype/shape on the host (a kernel must never see operands whose shape
+// disagrees with its grid), then launches on the caller's current HIP stream so it can be captured
+// into a hipGraph by torch.cuda.CUDAGraph.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int lwc_rmsnorm(const void*, void*, const void*, void*, int, int, float, hipStream_t);
+int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
+int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
+                      int, hipStream_t);
+int lwc_silu_mul(const void*, void*, int, int, hipStream_t);
+int lwc_bias_gelu(void*, const void*, int, int, hipStream_t);
+int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
+int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
+int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
+                     int, int, int, int, int, int, float, hipStream_t);
+int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, int, int, int, int, int, int, int,
+                          int, int, float, int, hipStream_t);
+int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
+               const float*, const float*, const float*, void*, const int*, const float*, const int*,
+               const unsigned int*, const int*, const unsigned long long*, const unsigned long long*, int, int*,
+               float*, int*, float*, hipStream_t);
+int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
+int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
+int lwc_vote_tally(const float*, const float*, int, int, int, float*, float*, float*, hipStream_t);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DTYPE(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has dtype ", (t).scalar_type(), ", expected ", dt)
+#define CHECK_BF16(t) \
+  CHECK_GPU(t);       \
+  CHECK_DTYPE(t, at::kBFloat16)
+#define CHECK_RC(rc, name) TORCH_CHECK((rc) == 0, name " launch failed with code ", (rc))
+
+template <typename T>
+const T* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<const T*>(t->data_ptr()) : nullptr;
+}
+
+void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& w, at::Tensor& out,
+             double eps) {
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_CONTIG(x); CHECK_CONTIG(out);
+  const int d = (int)x.size(-1);
+  const int rows = (int)(x.numel() / std::max<int64_t>(d, 1));
+  TORCH_CHECK(w.numel() == d && out.numel() == x.numel(), "rmsnorm: shape mismatch");
+  void* r = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16(*residual); CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "rmsnorm: residual shape mismatch");
+    r = residual->data_ptr();
+  }
+  CHECK_RC(lwc_rmsnorm(x.data_ptr(), r, w.data_ptr(), out.data_ptr(), rows, d, (float)eps, cur_stream()), "rmsnorm");
+}
+
+void layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& g,
+               const at::Tensor& b, at::Tensor& out, double eps) {
+  CHECK_BF16(x); CHECK_BF16(g); CHECK_BF16(b); CHECK_BF16(out);
+  CHECK_CONTIG(x); CHECK_CONTIG(out);
+  const int d = (int)x.size(-1);
+  const int rows = (int)(x.numel() / std::max<int64_t>(d, 1));
+  TORCH_CHECK(g.numel() == d && b.numel() == d && out.numel() == x.numel(), "layernorm: shape mismatch");
+  const void* r = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16(*residual); CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "layernorm: residual shape mismatch");
+    r = residual->data_ptr();
+  }
+  CHECK_RC(lwc_layernorm(x.data_ptr(), r, g.data_ptr(), b.data_ptr(), out.data_ptr(), rows, d, (float)eps,
+                         cur_stream()),
+           "layernorm");
+}
+
+void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const c10::optional<at::Tensor>& slots,
+                   const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& k_cache, at::Tensor& v_cache,
+                   int64_t Hq, int64_t Hkv, int64_t D) {
+  CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  CHECK_GPU(positions); CHECK_DTYPE(positions, at::kInt);
+  CHECK_DTYPE(cos_t, at::kFloat); CHECK_DTYPE(sin_t, at::kFloat);
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  const int T = (int)qkv.size(0);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_kv_write: qkv row is not (Hq+2Hkv)*D");
+  TORCH_CHECK(positions.numel() == T, "rope_kv_write: positions length");
+  TORCH_CHECK(cos_t.size(1) == D / 2 && sin_t.size(1) == D / 2, "rope_kv_write: cos/sin table width");
+  // k_cache [NB, Hkv, BS, D]; v_cache [NB, Hkv, D, BS]
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "rope_kv_write: k_cache shape");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == Hkv && v_cache.size(2) == D, "rope_kv_write: v_cache shape");
+  const int BS = (int)k_cache.size(2);
+  const int* sp = nullptr;
+  if (slots.has_value() && slots->defined()) {
+    CHECK_DTYPE(*slots, at::kInt);
+    TORCH_CHECK(slots->numel() == T, "rope_kv_write: slots length");
+    sp = slots->data_ptr<int>();
+  }
+  CHECK_RC(lwc_rope_kv_write(qkv.data_ptr(), positions.data_ptr<int>(), sp, cos_t.data_ptr<float>(),
+                             sin_t.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), T, (int)Hq, (int)Hkv,
+                             (int)D, BS, cur_stream()),
+           "rope_kv_write");
+}
+
+void silu_mul(const at::Tensor& in, at::Tensor& out) {
+  CHECK_BF16(in); CHECK_BF16(out); CHECK_CONTIG(in); CHECK_CONTIG(out);
+  const int F = (int)out.size(-1);
+  const int T = (int)(out.numel() / std::max(F, 1));
+  TORCH_CHECK(in.size(-1) == 2 * F && in.numel() == 2 * out.numel(), "silu_mul: shape mismatch");
+  CHECK_RC(lwc_silu_mul(in.data_ptr(), out.data_ptr(), T, F, cur_stream()), "silu_mul");
+}
+
+void bias_gelu(at::Tensor& x, const c10::optional<at::Tensor>& bias) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  const int F = (int)x.size(-1);
+  const int T = (int)(x.numel() / std::max(F, 1));
+  const void* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == F, "bias_gelu: bias length");
+    b = bias->data_ptr();
+  }
+  CHECK_RC(lwc_bias_gelu(x.data_ptr(), b, T, F, cur_stream()), "bias_gelu");
+}
+
+void embedding(const at::Tensor& table, const at::Tensor& ids, at::Tensor& out) {
+  CHECK_BF16(table); CHECK_BF16(out); CHECK_CONTIG(table); CHECK_CONTIG(out);
+  CHECK_GPU(ids); CHECK_DTYPE(ids, at::kInt);
+  const int T = (int)ids.numel(), d = (int)table.size(1);
+  TORCH_CHECK(out.numel() == (int64_t)T * d, "embedding: out shape");
+  CHECK_RC(lwc_embedding_gather(table.data_ptr(), ids.data_ptr<int>(), out.data_ptr(), T, d, (int)table.size(0),
+                                cur_stream()),
+           "embedding");
+}
+
+void kv_block_copy(at::Tensor& cache, const at::Tensor& pairs) {
+  // cache: [L*2, NB, ...block...]
+  CHECK_BF16(cache); CHECK_CONTIG(cache);
+  CHECK_GPU(pairs); CHECK_DTYPE(pairs, at::kInt); CHECK_CONTIG(pairs);
+  TORCH_CHECK(pairs.dim() == 2 && pairs.size(1) == 2, "kv_block_copy: pairs must be [P, 2]");
+  const int LK = (int)cache.size(0), NB = (int)cache.size(1);
+  const long long be = cache.numel() / ((long long)LK * NB);
+  CHECK_RC(lwc_kv_block_copy(cache.data_ptr(), pairs.data_ptr<int>(), (int)pairs.size(0), LK, NB, be, cur_stream()),
+           "kv_block_copy");
+}
+
+void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                  const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out,
+                  const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_lse,
+                  int64_t num_splits, double scale) {
+  // q: [B, >= Hq*D] with row stride; out: [B, Hq, D]
+  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
+  CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt);
+  CHECK_CONTIG(block_tables); CHECK_CONTIG(ctx_lens); CHECK_CONTIG(out);
+  TORCH_CHECK(q.stride(-1) == 1, "paged_decode: q rows must be contiguous");
+  const int B = (int)out.size(0), Hq = (int)out.size(1), D = (int)out.size(2);
+  const int Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
+  TORCH_CHECK(q.size(0) == B && q.size(1) >= Hq * D, "paged_decode: q shape");
+  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "paged_decode: v_cache must be [NB, Hkv, D, BS]");
+  TORCH_CHECK(block_tables.size(0) == B && ctx_lens.numel() == B, "paged_decode: batch mismatch");
+  float* po = nullptr;
+  float* pl = nullptr;
+  if (num_splits > 1) {
+    TORCH_CHECK(part_o.has_value() && part_lse.has_value(), "paged_decode: split-K needs workspaces");
+    TORCH_CHECK(part_o->numel() >= (int64_t)B * Hq * num_splits * D && part_lse->numel() >= (int64_t)B * Hq * num_splits,
+                "paged_decode: workspace too small");
+    po = part_o->data_ptr<float>();
+    pl = part_lse->data_ptr<float>();
+  }
+  CHECK_RC(lwc_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                            block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), out.data_ptr(), po, pl, B, Hq, Hkv,
+                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, cur_stream()),
+           "paged_decode");
+}
+
+void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
+                       const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, int64_t D,
+                       double scale, bool causal) {
+  // q/k/v: [T, *] 2-D views with unit inner stride (slices of the fused qkv row); out: [T, Hq*D]
+  CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
+  CHECK_DTYPE(cu_seqlens, at::kInt);
+  TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.dim() == 2 && out.dim() == 2, "prefill_attention: 2-D views expected");
+  TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1 && out.stride(1) == 1,
+              "prefill_attention: unit inner stride");
+  TORCH_CHECK(q.size(1) == Hq * D && k.size(1) == Hkv * D && v.size(1) == Hkv * D && out.size(1) == Hq * D,
+              "prefill_attention: head shape mismatch");
+  const int nseq = (int)cu_seqlens.numel() - 1;
+  CHECK_RC(lwc_prefill_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), cu_seqlens.data_ptr<int>(),
+                                 nseq, (int)max_seqlen, (int)q.stride(0), (int)k.stride(0), (int)v.stride(0),
+                                 (int)out.stride(0), (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0,
+                                 cur_stream()),
+           "prefill_attention");
+}
+
+void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& top_p, const at::Tensor& top_k,
+            const at::Tensor& min_p, const at::Tensor& top_a, const c10::optional<at::Tensor>& freq_pen,
+            const c10::optional<at::Tensor>& pres_pen, const c10::optional<at::Tensor>& rep_pen,
+            const c10::optional<at::Tensor>& counts, const c10::optional<at::Tensor>& count_rows,
+            const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& bias_rows,
+            const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& mask_rows,
+            const at::Tensor& seeds, const at::Tensor& offsets, int64_t num_logprobs, at::Tensor& out_token,
+            at::Tensor& out_logprob, at::Tensor& out_topk_ids, at::Tensor& out_topk_lp) {
+  CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits must be [B, V] with unit inner stride");
+  const int B = (int)logits.size(0), V = (int)logits.size(1);
+  for (const at::Tensor* t : {&temperature, &top_p, &min_p, &top_a}) {
+    CHECK_DTYPE(*t, at::kFloat);
+    TORCH_CHECK(t->numel() >= B, "sample: per-row parameter too short");
+  }
+  CHECK_DTYPE(top_k, at::kInt);
+  CHECK_DTYPE(seeds, at::kLong); CHECK_DTYPE(offsets, at::kLong);
+  TORCH_CHECK(out_token.numel() >= B && out_logprob.numel() >= B, "sample: outputs too short");
+  if (num_logprobs > 0)
+    TORCH_CHECK(out_topk_ids.numel() >= B * num_logprobs && out_topk_lp.numel() >= B * num_logprobs,
+                "sample: top-k outputs too short");
+  if (counts.has_value() && counts->defined()) {
+    TORCH_CHECK(counts->scalar_type() == at::kShort && counts->size(-1) == V, "sample: counts must be int16 [*, V]");
+  }
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->size(-1) == V, "sample: bias rows must be [*, V]");
+  if (mask.has_value() && mask->defined()) TORCH_CHECK(mask->size(-1) == V / 32, "sample: mask rows must be [*, V/32]");
+  CHECK_RC(lwc_sample(logits.data_ptr(), (int)logits.stride(0), V, B, temperature.data_ptr<float>(),
+                      top_p.data_ptr<float>(), top_k.data_ptr<int>(), min_p.data_ptr<float>(), top_a.data_ptr<float>(),
+                      opt_ptr<float>(freq_pen), opt_ptr<float>(pres_pen), opt_ptr<float>(rep_pen),
+                      counts.has_value() && counts->defined() ? counts->data_ptr() : nullptr, opt_ptr<int>(count_rows),
+                      opt_ptr<float>(bias), opt_ptr<int>(bias_rows), opt_ptr<unsigned int>(mask),
+                      opt_ptr<int>(mask_rows), reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
+                      reinterpret_cast<const unsigned long long*>(offsets.data_ptr()), (int)num_logprobs,
+                      out_token.data_ptr<int>(), out_logprob.data_ptr<float>(),
+                      num_logprobs > 0 ? out_topk_ids.data_ptr<int>() : nullptr,
+                      num_logprobs > 0 ? out_topk_lp.data_ptr<float>() : nullptr, cur_stream()),
+           "sample");
+}
+
+void pool_l2norm(const at::Tensor& hidden, const at::Tensor& cu_seqlens, int64_t mode, at::Tensor& out_f32,
+                 const c10::optional<at::Tensor>& out_bf16) {
+  CHECK_BF16(hidden); CHECK_DTYPE(cu_seqlens, at::kInt); CHECK_DTYPE(out_f32, at::kFloat);
+  TORCH_CHECK(hidden.dim() == 2 && hidden.stride(1) == 1, "pool_l2norm: hidden must be [T, d]");
+  const int nseq = (int)cu_seqlens.numel() - 1, d = (int)hidden.size(1);
+  TORCH_CHECK(out_f32.numel() == (int64_t)nseq * d, "pool_l2norm: out shape");
+  void* ob = nullptr;
+  if (out_bf16.has_value() && out_bf16->defined()) {
+    CHECK_BF16(*out_bf16);
+    TORCH_CHECK(out_bf16->numel() == (int64_t)nseq * d, "pool_l2norm: bf16 out shape");
+    ob = out_bf16->data_ptr();
+  }
+  CHECK_RC(lwc_pool_l2norm(hidden.data_ptr(), (int)hidden.stride(0), cu_seqlens.data_ptr<int>(), nseq, d, (int)mode,
+                           out_f32.data_ptr<float>(), ob, cur_stream()),
+           "pool_l2norm");
+}
+
+void cosine_consensus(const at::Tensor& E, at::Tensor& S, double inv_tau, at::Tensor& centrality, at::Tensor& weights,
+                      at::Tensor& best) {
+  // E: [R, n, d] bf16; S: [R, n_pad, n_pad] f32
+  CHECK_BF16(E); CHECK_CONTIG(E);
+  TORCH_CHECK(E.dim() == 3, "cosine_consensus: E must be [R, n, d]");
+  const int R = (int)E.size(0), n = (int)E.size(1), d = (int)E.size(2);
+  const int n_pad = (n + 15) / 16 * 16;
+  TORCH_CHECK(S.scalar_type() == at::kFloat && S.numel() >= (int64_t)R * n_pad * n_pad, "cosine_consensus: S size");
+  TORCH_CHECK(centrality.numel() >= (int64_t)R * n && weights.numel() >= (int64_t)R * n && best.numel() >= R,
+              "cosine_consensus: outputs too small");
+  CHECK_RC(lwc_cosine_consensus(E.data_ptr(), R, n, d, S.data_ptr<float>(), (float)inv_tau,
+                                centrality.data_ptr<float>(), weights.data_ptr<float>(), best.data_ptr<int>(),
+                                cur_stream()),
+           "cosine_consensus");
+}
+
+void vote_tally(const at::Tensor& votes, const at::Tensor& w, at::Tensor& cw, at::Tensor& conf, at::Tensor& voter_conf) {
+  CHECK_DTYPE(votes, at::kFloat); CHECK_DTYPE(w, at::kFloat); CHECK_CONTIG(votes); CHECK_CONTIG(w);
+  TORCH_CHECK(votes.dim() == 3, "vote_tally: votes must be [R, L, C]");
+  const int R = (int)votes.size(0), L = (int)votes.size(1), C = (int)votes.size(2);
+  TORCH_CHECK(w.numel() == (int64_t)R * L && cw.numel() == (int64_t)R * C && conf.numel() == (int64_t)R * C &&
+                  voter_conf.numel() == (int64_t)R * L,
+              "vote_tally: shape mismatch");
+  CHECK_RC(lwc_vote_tally(votes.data_ptr<float>(), w.data_ptr<float>(), R, L, C, cw.data_ptr<float>(),
+                          conf.data_ptr<float>(), voter_conf.data_ptr<float>(), cur_stream()),
+           "vote_tally");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels of llm_weighted_consensus_amd";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("layernorm", &layernorm);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("silu_mul", &silu_mul);
+  m.def("bias_gelu", &bias_gelu);
+  m.def("embedding", &embedding);
+  m.def("kv_block_copy", &kv_block_copy);
+  m.def("paged_decode", &paged_decode);
+  m.def("prefill_attention", &prefill_attention);
+  m.def("sample", &sample);
+  m.def("pool_l2norm", &pool_l2norm);
+  m.def("cosine_consensus", &cosine_consensus);
+  m.def("vote_tally", &vote_tally);
+}

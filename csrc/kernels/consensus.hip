@@ -1,0 +1,162 @@
+// Scoring kernels (gfx950):
+//   K9d  pool_l2norm        : CLS / mean / last-token pooling of encoder states + L2 normalisation;
+//   K10a cosine_consensus    : S = E E^T on MFMA (16x16 tiles, one wave each) followed by a row-reduce
+//                              + softmax kernel -> per-candidate centrality and consensus weights;
+//   K10b vote_tally          : weighted vote tally, confidence and per-voter agreement, batched.
+//
+// K10b is the GPU form of the reference tally/confidence loops
+// (src/score/completions/client.rs:384-455):
+//   cw_i = sum_l w_l * vote_l[i];  conf_i = cw_i / sum_i cw_i  (0 if the sum is 0);
+//   voter confidence_l = sum_i conf_i * vote_l[i].
+#include "common.h"
+
+namespace lwc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// hidden: [T, d] (row stride ld); cu_seqlens: [nseq+1]; out_f32: [nseq, d]; out_bf16: [nseq, d] (optional)
+// mode: 0 = CLS (first token), 1 = mean, 2 = last token
+__global__ void __launch_bounds__(256) pool_l2norm_kernel(const bf16_t* __restrict__ hidden, int ld,
+                                                         const int* __restrict__ cu, int d, int mode,
+                                                         float* __restrict__ out_f32, bf16_t* __restrict__ out_bf16) {
+  __shared__ float scratch[16];
+  __shared__ float pooled[4096];
+  const int s = blockIdx.x;
+  const int t0 = cu[s], t1 = cu[s + 1];
+  const int len = t1 - t0;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    float acc = 0.f;
+    if (len > 0) {
+      if (mode == 0)
+        acc = bf2f(hidden[(size_t)t0 * ld + c]);
+      else if (mode == 2)
+        acc = bf2f(hidden[(size_t)(t1 - 1) * ld + c]);
+      else {
+        for (int t = t0; t < t1; ++t) acc += bf2f(hidden[(size_t)t * ld + c]);
+        acc /= (float)len;
+      }
+    }
+    pooled[c] = acc;
+    ss += acc * acc;
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = ss > 0.f ? rsqrtf(ss) : 0.f;
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    const float v = pooled[c] * inv;
+    out_f32[(size_t)s * d + c] = v;
+    if (out_bf16) out_bf16[(size_t)s * d + c] = f2bf(v);
+  }
+}
+
+// E: [R, n, d] bf16 (rows L2-normalised); S: [R, n_pad, n_pad] f32, n_pad = round_up(n, 16)
+__global__ void __launch_bounds__(64) cosine_tiles_kernel(const bf16_t* __restrict__ E, int n, int d,
+                                                          float* __restrict__ S, int n_pad) {
+  const int ti = blockIdx.x, tj = blockIdx.y, r = blockIdx.z;
+  const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+  const bf16_t* Er = E + (size_t)r * n * d;
+  const int ri = ti * 16 + r16, rj = tj * 16 + r16;
+  float4v acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < d; k0 += 32) {
+    short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, b = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ri < n) a = *reinterpret_cast<const short8*>(Er + (size_t)ri * d + k0 + 8 * g);
+    if (rj < n) b = *reinterpret_cast<const short8*>(Er + (size_t)rj * d + k0 + 8 * g);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                  0, 0, 0);
+  }
+  float* Sr = S + (size_t)r * n_pad * n_pad;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Sr[(size_t)(ti * 16 + 4 * g + q) * n_pad + tj * 16 + r16] = acc[q];
+}
+
+// per request: centrality_i = mean_{j != i} S_ij ; weights = softmax(centrality / tau); best = argmax
+__global__ void __launch_bounds__(256) consensus_reduce_kernel(const float* __restrict__ S, int n, int n_pad,
+                                                              float inv_tau, float* __restrict__ centrality,
+                                                              float* __restrict__ weights, int* __restrict__ best) {
+  __shared__ float scratch[16];
+  __shared__ float cen[1024];
+  const int r = blockIdx.x;
+  const float* Sr = S + (size_t)r * n_pad * n_pad;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < n; ++j) s += (j == i) ? 0.f : Sr[(size_t)i * n_pad + j];
+    const float c = n > 1 ? s / (float)(n - 1) : 1.f;
+    cen[i] = c;
+    centrality[(size_t)r * n + i] = c;
+    mx = fmaxf(mx, c * inv_tau);
+  }
+  mx = block_max(mx, scratch);
+  float se = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) se += __expf(cen[i] * inv_tau - mx);
+  se = block_sum(se, scratch);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) weights[(size_t)r * n + i] = __expf(cen[i] * inv_tau - mx) / se;
+  if (threadIdx.x == 0) {
+    int bi = 0;
+    for (int i = 1; i < n; ++i)
+      if (cen[i] > cen[bi]) bi = i;
+    best[r] = bi;
+  }
+}
+
+// votes: [R, L, C], w: [R, L] -> cw: [R, C], conf: [R, C], voter_conf: [R, L]
+__global__ void __launch_bounds__(256) vote_tally_kernel(const float* __restrict__ votes, const float* __restrict__ w,
+                                                        int L, int C, float* __restrict__ cw, float* __restrict__ conf,
+                                                        float* __restrict__ voter_conf) {
+  __shared__ float scratch[16];
+  __shared__ float sconf[2048];
+  const int r = blockIdx.x;
+  const float* V = votes + (size_t)r * L * C;
+  const float* W = w + (size_t)r * L;
+  float part = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int l = 0; l < L; ++l) s += V[(size_t)l * C + c] * W[l];
+    cw[(size_t)r * C + c] = s;
+    sconf[c] = s;
+    part += s;
+  }
+  const float tot = block_sum(part, scratch);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float cf = tot > 0.f ? sconf[c] / tot : 0.f;
+    sconf[c] = cf;
+    conf[(size_t)r * C + c] = cf;
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < L; l += blockDim.x) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += sconf[c] * V[(size_t)l * C + c];
+    voter_conf[(size_t)r * L + l] = s;
+  }
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_pool_l2norm(const void* hidden, int ld, const int* cu, int nseq, int d, int mode, float* out_f32,
+                               void* out_bf16, hipStream_t s) {
+  using namespace lwc;
+  if (d > 4096) return -1;
+  if (nseq == 0) return 0;
+  pool_l2norm_kernel<<<nseq, 256, 0, s>>>((const bf16_t*)hidden, ld, cu, d, mode, out_f32, (bf16_t*)out_bf16);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_cosine_consensus(const void* E, int R, int n, int d, float* S, float inv_tau, float* centrality,
+                                    float* weights, int* best, hipStream_t s) {
+  using namespace lwc;
+  if (d % 32 != 0 || n > 1024) return -1;
+  if (R == 0 || n == 0) return 0;
+  const int nt = (n + 15) / 16, n_pad = nt * 16;
+  cosine_tiles_kernel<<<dim3(nt, nt, R), 64, 0, s>>>((const bf16_t*)E, n, d, S, n_pad);
+  consensus_reduce_kernel<<<R, 256, 0, s>>>(S, n, n_pad, inv_tau, centrality, weights, best);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_vote_tally(const float* votes, const float* w, int R, int L, int C, float* cw, float* conf,
+                              float* voter_conf, hipStream_t s) {
+  using namespace lwc;
+  if (C > 2048) return -1;
+  if (R == 0) return 0;
+  vote_tally_kernel<<<R, 256, 0, s>>>(votes, w, L, C, cw, conf, voter_conf);
+  return (int)hipGetLastError();
+}

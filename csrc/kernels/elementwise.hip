@@ -1,0 +1,188 @@
+// Element-wise / data-movement kernels for gfx950:
+//   K2  rope_kv_write   : rotate-half RoPE on q and k (in place in the fused qkv buffer) and scatter
+//                          k, v into the paged KV cache in the same pass;
+//   K5  silu_mul        : SwiGLU  out = silu(gate) * up  over a fused [T, 2F] gate_up buffer;
+//   K7  embedding_gather: token ids -> hidden rows;
+//   K9b bias_gelu       : x = gelu_erf(x + bias) in place (BERT FFN1 epilogue);
+//   K12 kv_block_copy   : copy-on-write fork of whole KV blocks (all layers, K and V).
+// All of them move 16 B per lane (Guideline 13); trig comes from a host-built cos/sin table
+// (Appendix B "Element-wise": on-device sin/cos turns RoPE VALU-bound).
+#include "common.h"
+
+namespace lwc {
+
+// qkv: [T, (Hq + 2*Hkv) * D]; cos/sin: [max_pos, D/2] f32; cache: [NB, Hkv, BS, D] (K and V)
+__global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ positions,
+                                                           const int* __restrict__ slots, const float* __restrict__ cos_t,
+                                                           const float* __restrict__ sin_t, bf16_t* __restrict__ kc,
+                                                           bf16_t* __restrict__ vc, int Hq, int Hkv, int D, int BS) {
+  const int t = blockIdx.x;
+  const int half = D >> 1;
+  const int vec_per_head_rot = half >> 3;  // threads per head for rotation (8 dims each half)
+  const int n_rot = (Hq + Hkv) * vec_per_head_rot;
+  const int vec_per_head = D >> 3;
+  const int n_v = Hkv * vec_per_head;
+  const int row_len = (Hq + 2 * Hkv) * D;
+  bf16_t* row = qkv + (size_t)t * row_len;
+  const int pos = positions[t];
+  const int slot = slots ? slots[t] : -1;
+  const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
+  for (int i = threadIdx.x; i < n_rot + n_v; i += blockDim.x) {
+    if (i < n_rot) {
+      const int h = i / vec_per_head_rot;      // 0..Hq+Hkv-1 (q heads then k heads)
+      const int c = (i % vec_per_head_rot) * 8;  // first-half dim offset
+      bf16_t* hp = row + h * D;
+      uint4v* p1 = reinterpret_cast<uint4v*>(hp + c);
+      uint4v* p2 = reinterpret_cast<uint4v*>(hp + c + half);
+      float x1[8], x2[8], o1[8], o2[8];
+      unpack8(*p1, x1);
+      unpack8(*p2, x2);
+      const float4* cp = reinterpret_cast<const float4*>(cos_t + (size_t)pos * half + c);
+      const float4* sp = reinterpret_cast<const float4*>(sin_t + (size_t)pos * half + c);
+      float cs[8], sn[8];
+      *reinterpret_cast<float4*>(cs) = cp[0];
+      *reinterpret_cast<float4*>(cs + 4) = cp[1];
+      *reinterpret_cast<float4*>(sn) = sp[0];
+      *reinterpret_cast<float4*>(sn + 4) = sp[1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o1[j] = x1[j] * cs[j] - x2[j] * sn[j];
+        o2[j] = x2[j] * cs[j] + x1[j] * sn[j];
+      }
+      const uint4v n1 = pack8(o1), n2 = pack8(o2);
+      *p1 = n1;
+      *p2 = n2;
+      if (h >= Hq && slot >= 0) {
+        const int kh = h - Hq;
+        bf16_t* dst = kc + (((size_t)blk * Hkv + kh) * BS + off) * D;
+        *reinterpret_cast<uint4v*>(dst + c) = n1;
+        *reinterpret_cast<uint4v*>(dst + c + half) = n2;
+      }
+    } else if (slot >= 0) {
+      // V is cached TRANSPOSED per block ([NB, Hkv, D, BS]) so that the decode kernel's P.V MFMA
+      // reads its B operand (a column of V) as contiguous tokens (see attention_decode.hip).
+      const int j = i - n_rot;
+      const int vh = j / vec_per_head, c = (j % vec_per_head) * 8;
+      const bf16_t* src = row + (Hq + Hkv + vh) * D + c;
+      bf16_t* dst = vc + (((size_t)blk * Hkv + vh) * D + c) * BS + off;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dst[(size_t)e * BS] = src[e];
+    }
+  }
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// in: [T, 2F] = [gate | up]; out: [T, F]
+__global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int T, int F) {
+  const int fv = F >> 3;
+  const size_t total = (size_t)T * fv;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = i / fv;
+    const int c = (int)(i % fv) * 8;
+    const bf16_t* r = in + t * 2 * F;
+    float g[8], u[8], o[8];
+    unpack8(*reinterpret_cast<const uint4v*>(r + c), g);
+    unpack8(*reinterpret_cast<const uint4v*>(r + F + c), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
+    *reinterpret_cast<uint4v*>(out + t * F + c) = pack8(o);
+  }
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// x: [T, F] in place, bias: [F] (may be null)
+__global__ void bias_gelu_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ bias, int T, int F) {
+  const int fv = F >> 3;
+  const size_t total = (size_t)T * fv;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % fv) * 8;
+    uint4v* p = reinterpret_cast<uint4v*>(x) + i;
+    float v[8], b[8];
+    unpack8(*p, v);
+    if (bias) {
+      unpack8(*reinterpret_cast<const uint4v*>(bias + c), b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += b[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+    *p = pack8(v);
+  }
+}
+
+// table: [V, d]; ids: [T] (int32); out: [T, d]
+__global__ void embedding_gather_kernel(const bf16_t* __restrict__ table, const int* __restrict__ ids,
+                                        bf16_t* __restrict__ out, int d, int V) {
+  const int t = blockIdx.x;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const uint4v* src = reinterpret_cast<const uint4v*>(table + (size_t)id * d);
+  uint4v* dst = reinterpret_cast<uint4v*>(out + (size_t)t * d);
+  for (int i = threadIdx.x; i < (d >> 3); i += blockDim.x) dst[i] = src[i];
+}
+
+// cache: [L, 2, NB, block_elems]; pairs: [P, 2] (src, dst) int32
+__global__ void kv_block_copy_kernel(bf16_t* __restrict__ cache, const int* __restrict__ pairs, int NB,
+                                     int64_t block_elems) {
+  const int p = blockIdx.x, lk = blockIdx.y;
+  const int src = pairs[2 * p], dst = pairs[2 * p + 1];
+  bf16_t* base = cache + (size_t)lk * NB * block_elems;
+  const uint4v* s = reinterpret_cast<const uint4v*>(base + (size_t)src * block_elems);
+  uint4v* d = reinterpret_cast<uint4v*>(base + (size_t)dst * block_elems);
+  for (int64_t i = threadIdx.x; i < (block_elems >> 3); i += blockDim.x) d[i] = s[i];
+}
+
+static int ew_grid(size_t work, int threads) {
+  size_t g = (work + threads - 1) / threads;
+  if (g > 4096) g = 4096;  // grid-stride beyond ~16 waves/CU (Guideline 11)
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_rope_kv_write(void* qkv, const int* positions, const int* slots, const float* cos_t,
+                                 const float* sin_t, void* kc, void* vc, int T, int Hq, int Hkv, int D, int BS,
+                                 hipStream_t s) {
+  using namespace lwc;
+  if (D % 16 != 0 || T <= 0) return T == 0 ? 0 : -1;
+  rope_kv_write_kernel<<<T, 256, 0, s>>>((bf16_t*)qkv, positions, slots, cos_t, sin_t, (bf16_t*)kc, (bf16_t*)vc, Hq,
+                                         Hkv, D, BS);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_silu_mul(const void* in, void* out, int T, int F, hipStream_t s) {
+  using namespace lwc;
+  if (F % 8 != 0) return -1;
+  if (T == 0) return 0;
+  silu_mul_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((const bf16_t*)in, (bf16_t*)out, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_bias_gelu(void* x, const void* bias, int T, int F, hipStream_t s) {
+  using namespace lwc;
+  if (F % 8 != 0) return -1;
+  if (T == 0) return 0;
+  bias_gelu_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((bf16_t*)x, (const bf16_t*)bias, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_embedding_gather(const void* table, const int* ids, void* out, int T, int d, int V,
+                                    hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0) return -1;
+  if (T == 0) return 0;
+  embedding_gather_kernel<<<T, 128, 0, s>>>((const bf16_t*)table, ids, (bf16_t*)out, d, V);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_kv_block_copy(void* cache, const int* pairs, int P, int LK, int NB, long long block_elems,
+                                 hipStream_t s) {
+  using namespace lwc;
+  if (block_elems % 8 != 0) return -1;
+  if (P == 0) return 0;
+  kv_block_copy_kernel<<<dim3(P, LK), 256, 0, s>>>((bf16_t*)cache, pairs, NB, block_elems);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,158 @@
+// K1 rmsnorm_fused_residual and K9a layernorm(+residual) for gfx950.
+//
+// One workgroup per row; every thread owns up to kMaxVec 16-byte vectors (8 bf16) of the row in
+// registers, so the row is read from HBM exactly once and written once (residual stream update and
+// normalised output in the same pass).  Memory-bound: the only levers are 16 B/lane accesses
+// (Guideline 13) and a single pass.
+//
+// Reference behaviour served: decoder layers for `LlmBase.model` (reference
+// src/score/llm/mod.rs:10) and the embeddings encoder (`WeightTrainingTableEmbeddings.model`,
+// src/score/model/mod.rs:309-314).
+#include "common.h"
+
+namespace lwc {
+
+constexpr int kMaxVec = 4;  // rows up to 4 * 8 * 1024 = 32768 elements
+
+// y = rmsnorm(x [+ residual]) * w ; if residual != nullptr: residual <- x + residual (pre-norm sum)
+template <bool kResidual>
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
+                                                      const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                                                      int d, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = d >> 3;
+  const uint4v* xr = reinterpret_cast<const uint4v*>(x + (size_t)row * d);
+  uint4v* rr = reinterpret_cast<uint4v*>(residual + (size_t)row * d);
+  const uint4v* wr = reinterpret_cast<const uint4v*>(w);
+  uint4v* yr = reinterpret_cast<uint4v*>(y + (size_t)row * d);
+  float v[kMaxVec][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxVec; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < nvec) {
+      unpack8(xr[i], v[k]);
+      if (kResidual) {
+        float r[8];
+        unpack8(rr[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+        rr[i] = pack8(v[k]);
+        // the normalised value is computed from the bf16-rounded sum, as the residual stream holds it
+        unpack8(rr[i], v[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+  for (int k = 0; k < kMaxVec; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < nvec) {
+      float wf[8], o[8];
+      unpack8(wr[i], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * inv * wf[j];
+      yr[i] = pack8(o);
+    }
+  }
+}
+
+// LayerNorm with affine: y = (h - mean)/sqrt(var+eps) * g + b, h = x (+ residual);
+// residual (if given) is NOT updated: BERT post-norm writes y back as the new stream.
+template <bool kResidual>
+__global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual,
+                                                        const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
+                                                        bf16_t* __restrict__ y, int d, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = d >> 3;
+  const uint4v* xr = reinterpret_cast<const uint4v*>(x + (size_t)row * d);
+  const uint4v* rr = reinterpret_cast<const uint4v*>(residual + (size_t)row * d);
+  const uint4v* gr = reinterpret_cast<const uint4v*>(g);
+  const uint4v* br = reinterpret_cast<const uint4v*>(b);
+  uint4v* yr = reinterpret_cast<uint4v*>(y + (size_t)row * d);
+  float v[kMaxVec][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxVec; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < nvec) {
+      unpack8(xr[i], v[k]);
+      if (kResidual) {
+        float r[8];
+        unpack8(rr[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[k][j];
+    }
+  }
+  const float mean = block_sum(s, scratch) / (float)d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxVec; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = v[k][j] - mean;
+        s2 += c * c;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(s2, scratch) / (float)d + eps);
+#pragma unroll
+  for (int k = 0; k < kMaxVec; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < nvec) {
+      float gf[8], bf[8], o[8];
+      unpack8(gr[i], gf);
+      unpack8(br[i], bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * inv * gf[j] + bf[j];
+      yr[i] = pack8(o);
+    }
+  }
+}
+
+static int norm_threads(int d) {
+  // one 16-byte vector per thread when the row allows it (shortest latency per row)
+  int nvec = d / 8;
+  int t = ((nvec + 63) / 64) * 64;
+  if (t < 64) t = 64;
+  if (t > 1024) t = 1024;
+  return t;
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_rmsnorm(const void* x, void* residual, const void* w, void* y, int rows, int d, float eps,
+                           hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0 || d > kMaxVec * 8 * 1024) return -1;
+  const int t = norm_threads(d);
+  if (residual)
+    rmsnorm_kernel<true><<<rows, t, 0, s>>>((const bf16_t*)x, (bf16_t*)residual, (const bf16_t*)w, (bf16_t*)y, d, eps);
+  else
+    rmsnorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)w, (bf16_t*)y, d, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_layernorm(const void* x, const void* residual, const void* g, const void* b, void* y, int rows,
+                             int d, float eps, hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0 || d > kMaxVec * 8 * 1024) return -1;
+  const int t = norm_threads(d);
+  if (residual)
+    layernorm_kernel<true><<<rows, t, 0, s>>>((const bf16_t*)x, (const bf16_t*)residual, (const bf16_t*)g,
+                                              (const bf16_t*)b, (bf16_t*)y, d, eps);
+  else
+    layernorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)g, (const bf16_t*)b,
+                                               (bf16_t*)y, d, eps);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,471 @@
+// K8a+K8b+K8c+K8d fused: logits processing, raw log-softmax + top-k logprobs, and top-k / top-p /
+// min-p / top-a filtered multinomial sampling (or greedy argmax) in ONE pass over each logits row.
+//
+// One 1024-thread workgroup per row.  The row (bf16, V <= 8*1024*SLOTS) is loaded ONCE from HBM into
+// registers as packed bf16 (16 B per load, SLOTS loads per thread) and every later phase — raw max and
+// log-sum-exp, the top-K selection for `top_logprobs`, penalties/bias/grammar mask, the filter
+// thresholds and the inverse-CDF draw — works on those registers plus block reductions.
+// Element index of (thread t, slot j, lane-element e) = (j*1024 + t)*8 + e.
+//
+// Thresholds are found by exact binary search over the 16-bit order-preserving key of the bf16 value
+// (16 block-reduction rounds), so top-p / top-k are exact (ties at the threshold are kept, as in the
+// usual "keep >= threshold" convention).  Randomness: Philox4x32-10 keyed by the per-sequence seed,
+// counter = per-sequence step — reproducible per (seed, step) independent of batch composition.
+//
+// Reference fields served: temperature/top_p/min_p/top_a/top_k/frequency_penalty/presence_penalty/
+// repetition_penalty/logit_bias (src/score/llm/mod.rs:39-72, validation :376-406,:490-508),
+// top_logprobs <= 20 (:455-467) feeding the vote extractor (src/score/completions/client.rs:1721-1793),
+// and constrained output modes (json_schema / tool_call, src/score/llm/mod.rs:690-696).
+#include "common.h"
+
+namespace lwc {
+
+constexpr int kSampT = 1024;
+constexpr int kMaxTopK = 20;
+constexpr int kCollect = 64;
+
+struct SampleParams {
+  const bf16_t* logits;  // [B, ld]
+  int ld, V;
+  const float* temperature;  // [B]  (<= 0 -> greedy)
+  const float* top_p;        // [B]  (>= 1 -> off)
+  const int* top_k;          // [B]  (<= 0 -> off)
+  const float* min_p;        // [B]  (<= 0 -> off)
+  const float* top_a;        // [B]  (<= 0 -> off)
+  const float* freq_pen;     // [B] or null
+  const float* pres_pen;     // [B] or null
+  const float* rep_pen;      // [B] or null
+  uint16_t* counts;          // [B, V] generated-token counts (or null); updated with the sample
+  const int* count_rows;     // [B] row of `counts` for each batch row (or null = identity)
+  const float* bias;         // [NBT, V] dense logit bias rows (or null)
+  const int* bias_rows;      // [B] row of `bias` (-1 = none)
+  const uint32_t* mask;      // [NMT, V/32] allowed-token bitmasks (or null)
+  const int* mask_rows;      // [B] row of `mask` (-1 = none)
+  const unsigned long long* seeds;    // [B]
+  const unsigned long long* offsets;  // [B] (step counter)
+  int num_logprobs;          // K for top logprobs (0..20)
+  int* out_token;            // [B]
+  float* out_logprob;        // [B]  raw logprob of the sampled token
+  int* out_topk_ids;         // [B, K]
+  float* out_topk_lp;        // [B, K]
+};
+
+// ---- Philox4x32-10 ----
+LWC_DEVICE void philox4x32(uint32_t (&ctr)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * ctr[0], hi0 = __umulhi(0xD2511F53u, ctr[0]);
+    const uint32_t lo1 = 0xCD9E8D57u * ctr[2], hi1 = __umulhi(0xCD9E8D57u, ctr[2]);
+    const uint32_t n0 = hi1 ^ ctr[1] ^ k0, n2 = hi0 ^ ctr[3] ^ k1;
+    ctr[0] = n0;
+    ctr[1] = lo1;
+    ctr[2] = n2;
+    ctr[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+LWC_DEVICE uint32_t f2key(float f) {  // order-preserving 16-bit key of the bf16-rounded value
+  const uint32_t b = __float_as_uint(f) >> 16;
+  return (b & 0x8000u) ? (~b & 0xffffu) : (b | 0x8000u);
+}
+LWC_DEVICE float key2f(uint32_t k) {
+  const uint32_t b = (k & 0x8000u) ? (k & 0x7fffu) : (~k & 0xffffu);
+  return __uint_as_float(b << 16);
+}
+
+// Keep the packed row opaque at the top of every pass: otherwise LICM hoists the 8*SLOTS unpacked
+// floats (or their keys) out of the binary-search loops and the kernel spills (1024 threads leave
+// 128 VGPRs per lane; the packed row alone is 4*SLOTS of them).
+#define OPAQUE_ROW(row)                                   \
+  _Pragma("unroll") for (int _j = 0; _j < SLOTS; ++_j) { \
+    asm volatile("" : "+v"(row[_j]));                     \
+  }
+
+// value of element e (0..7) of the row vector held in slot j (compile-time j, e: stays in VGPRs)
+#define GET(row, j, e) \
+  (((e)&1) ? __uint_as_float((row)[j][(e) >> 1] & 0xffff0000u) : __uint_as_float((row)[j][(e) >> 1] << 16))
+
+LWC_DEVICE int block_sum_i(int v, int* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  int r = lane < (kSampT / 64) ? scratch[lane] : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+  return r;
+}
+
+template <int SLOTS>
+__global__ void __launch_bounds__(kSampT) sample_kernel(SampleParams p) {
+  __shared__ float sred[32];
+  __shared__ int sredi[32];
+  __shared__ float s_cval[kCollect];
+  __shared__ int s_cidx[kCollect];
+  __shared__ int s_ccount;
+  __shared__ float s_scan[kSampT / 64];
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const bf16_t* lrow = p.logits + (size_t)b * p.ld;
+  const int nvec = p.V >> 3;
+
+  // ---- load the raw row once ----
+  uint4v row[SLOTS];
+#pragma unroll
+  for (int j = 0; j < SLOTS; ++j) {
+    const int vi = j * kSampT + t;
+    row[j] = vi < nvec ? *reinterpret_cast<const uint4v*>(lrow + (size_t)vi * 8) : uint4v{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};
+  }
+  // ---- raw log-sum-exp ----
+  float mx = -INFINITY;
+OPAQUE_ROW(row);
+#pragma unroll
+  for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx = fmaxf(mx, GET(row, j, e));
+  const float raw_max = block_max(mx, sred);
+  float se = 0.f;
+OPAQUE_ROW(row);
+#pragma unroll
+  for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) se += __expf(GET(row, j, e) - raw_max);
+  const float raw_lse = raw_max + __logf(block_sum(se, sred));
+
+  // ---- raw top-K (for top_logprobs) ----
+  const int K = p.num_logprobs;
+  if (K > 0) {
+    uint32_t lo = 0, hi = 0xffffu;  // largest key with count(>= key) >= K
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      OPAQUE_ROW(row);
+      int c = 0;
+OPAQUE_ROW(row);
+#pragma unroll
+      for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c += f2key(GET(row, j, e)) >= mid;
+      if (block_sum_i(c, sredi) >= K)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    if (t == 0) s_ccount = 0;
+    __syncthreads();
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = GET(row, j, e);
+        const int idx = (j * kSampT + t) * 8 + e;
+        if (idx < p.V && f2key(v) >= lo) {
+          const int slot = atomicAdd(&s_ccount, 1);
+          if (slot < kCollect) {
+            s_cval[slot] = v;
+            s_cidx[slot] = idx;
+          }
+        }
+      }
+    __syncthreads();
+    if (t < 64) {  // one wave: rank-sort the collected candidates (value desc, index asc)
+      const int n = min(s_ccount, kCollect);
+      if (t < n) {
+        const float v = s_cval[t];
+        const int ix = s_cidx[t];
+        int rank = 0;
+        for (int u = 0; u < n; ++u) {
+          const float w = s_cval[u];
+          rank += (w > v) || (w == v && s_cidx[u] < ix);
+        }
+        if (rank < K) {
+          p.out_topk_ids[(size_t)b * K + rank] = ix;
+          p.out_topk_lp[(size_t)b * K + rank] = v - raw_lse;
+        }
+      }
+    }
+  }
+
+  // ---- processed values y = raw + bias - penalties (masked -> -inf), stored back as bf16 ----
+  const float* brow = (p.bias && p.bias_rows[b] >= 0) ? p.bias + (size_t)p.bias_rows[b] * p.V : nullptr;
+  const uint32_t* mrow = (p.mask && p.mask_rows[b] >= 0) ? p.mask + (size_t)p.mask_rows[b] * (p.V >> 5) : nullptr;
+  const int crow_i = p.counts ? (p.count_rows ? p.count_rows[b] : b) : -1;
+  const uint16_t* crow = crow_i >= 0 ? p.counts + (size_t)crow_i * p.V : nullptr;
+  const float fpen = p.freq_pen ? p.freq_pen[b] : 0.f, ppen = p.pres_pen ? p.pres_pen[b] : 0.f;
+  const float rpen = p.rep_pen ? p.rep_pen[b] : 1.f;
+  const bool use_pen = crow && (fpen != 0.f || ppen != 0.f || rpen != 1.f);
+  if (brow || mrow || use_pen) {
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+      const int vi = j * kSampT + t;
+      if (vi >= nvec) continue;
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = GET(row, j, e);
+      if (brow) {
+        const float4 b0 = reinterpret_cast<const float4*>(brow + (size_t)vi * 8)[0];
+        const float4 b1 = reinterpret_cast<const float4*>(brow + (size_t)vi * 8)[1];
+        y[0] += b0.x; y[1] += b0.y; y[2] += b0.z; y[3] += b0.w;
+        y[4] += b1.x; y[5] += b1.y; y[6] += b1.z; y[7] += b1.w;
+      }
+      if (use_pen) {
+        const uint4v c4 = *reinterpret_cast<const uint4v*>(crow + (size_t)vi * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t c = (c4[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+          if (c) {
+            y[e] = y[e] > 0.f ? y[e] / rpen : y[e] * rpen;
+            y[e] -= fpen * (float)c + ppen;
+          }
+        }
+      }
+      if (mrow) {
+        const uint32_t m = (mrow[vi >> 2] >> ((vi & 3) * 8)) & 0xffu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (!((m >> e) & 1u)) y[e] = -INFINITY;
+      }
+      row[j] = pack8(y);
+    }
+  }
+
+  const float T = p.temperature[b];
+  int token = 0;
+  if (T <= 0.f) {
+    // ---- greedy: argmax (lowest index on ties) ----
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = GET(row, j, e);
+        const int idx = (j * kSampT + t) * 8 + e;
+        if (idx < p.V && (v > bv || (v == bv && idx < bi))) {
+          bv = v;
+          bi = idx;
+        }
+      }
+    const float gm = block_max(bv, sred);
+    int cand = (bv == gm) ? bi : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    __syncthreads();
+    if ((t & 63) == 0) sredi[t >> 6] = cand;
+    __syncthreads();
+    cand = (t & 63) < (kSampT / 64) ? sredi[t & 63] : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    token = cand == 0x7fffffff ? 0 : cand;
+  } else {
+    const float invT = 1.f / T;
+    float ym = -INFINITY;
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
+    const float ymax = block_max(ym, sred);
+    // mass of the elements with key >= KEY (macro, not a lambda: a by-reference capture of `row`
+    // makes it addressable and sends it to scratch)
+#define PR(y) __expf(((y)-ymax) * invT)
+#define MASS_GE(KEY, OUT)                                              \
+  do {                                                                 \
+    OPAQUE_ROW(row);                                                   \
+    float _s = 0.f;                                                    \
+    _Pragma("unroll") for (int j = 0; j < SLOTS; ++j) {                \
+      _Pragma("unroll") for (int e = 0; e < 8; ++e) {                  \
+        const float y = GET(row, j, e);                                \
+        _s += (f2key(y) >= (KEY) && y > -INFINITY) ? PR(y) : 0.f;      \
+      }                                                                \
+      __builtin_amdgcn_sched_barrier(0);                               \
+    }                                                                  \
+    OUT = block_sum(_s, sred);                                         \
+  } while (0)
+    uint32_t tau = 0;  // keep elements with key >= tau
+    const int k = p.top_k[b];
+    if (k > 0) {
+      uint32_t lo = 0, hi = 0xffffu;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        OPAQUE_ROW(row);
+        int c = 0;
+OPAQUE_ROW(row);
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) c += f2key(GET(row, j, e)) >= mid;
+        if (block_sum_i(c, sredi) >= k)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      tau = lo;
+    }
+    float Z;
+    MASS_GE(0u, Z);
+    const float tp = p.top_p[b];
+    if (tp < 1.f) {
+      float mk;
+      MASS_GE(tau, mk);
+      const float target = tp * mk;
+      uint32_t lo = tau, hi = 0xffffu;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        float mm;
+        MASS_GE(mid, mm);
+        if (mm >= target)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      tau = lo;
+    }
+    const float mp = p.min_p[b];
+    if (mp > 0.f) {  // p_i >= min_p * p_max  <=>  y >= ymax + T ln(min_p)
+      const uint32_t kk = f2key(ymax + T * __logf(mp));
+      tau = max(tau, kk);
+    }
+    const float ta = p.top_a[b];
+    if (ta > 0.f) {  // p_i >= top_a * p_max^2, p_max = 1/Z
+      const uint32_t kk = f2key(ymax + T * __logf(ta / Z));
+      tau = max(tau, kk);
+    }
+    const uint32_t ymax_key = f2key(ymax);
+    if (tau > ymax_key) tau = ymax_key;  // never filter out the argmax
+    // ---- inverse-CDF draw over the kept set (order: thread-major, then slot, then element) ----
+    float local = 0.f;
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float y = GET(row, j, e);
+        local += (f2key(y) >= tau && y > -INFINITY) ? PR(y) : 0.f;
+      }
+    // exclusive scan of `local` over threads
+    const int lane = t & 63, wid = t >> 6;
+    float incl = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float n = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += n;
+    }
+    __syncthreads();
+    if (lane == 63) s_scan[wid] = incl;
+    __syncthreads();
+    float wave_off = 0.f, total = 0.f;
+    for (int w = 0; w < kSampT / 64; ++w) {
+      const float s = s_scan[w];
+      if (w < wid) wave_off += s;
+      total += s;
+    }
+    const float excl = wave_off + incl - local;
+    uint32_t ctr[4] = {(uint32_t)p.offsets[b], (uint32_t)(p.offsets[b] >> 32), 0u, 0u};
+    philox4x32(ctr, (uint32_t)p.seeds[b], (uint32_t)(p.seeds[b] >> 32));
+    const float u01 = ((ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float u = u01 * total;
+    int found = 0x7fffffff;
+    if (local > 0.f && u >= excl && u < excl + local) {
+      float acc = excl;
+      int last = -1;
+OPAQUE_ROW(row);
+#pragma unroll
+      for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = GET(row, j, e);
+          const int idx = (j * kSampT + t) * 8 + e;
+          if (f2key(y) >= tau && y > -INFINITY) {
+            last = idx;
+            acc += PR(y);
+            if (found == 0x7fffffff && u < acc) found = idx;
+          }
+        }
+      if (found == 0x7fffffff) found = last;  // rounding at the top edge
+    }
+    // the owning thread is unique except for float ties at a boundary: take the minimum
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
+    __syncthreads();
+    if (lane == 0) sredi[wid] = found;
+    __syncthreads();
+    found = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
+    if (found == 0x7fffffff) {
+      // u landed past the last kept element through rounding: fall back to argmax
+      found = 0;
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+OPAQUE_ROW(row);
+#pragma unroll
+      for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = GET(row, j, e);
+          const int idx = (j * kSampT + t) * 8 + e;
+          if (idx < p.V && (v > bv || (v == bv && idx < bi))) {
+            bv = v;
+            bi = idx;
+          }
+        }
+      const float gm = block_max(bv, sred);
+      int cand = (bv == gm) ? bi : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+      __syncthreads();
+      if (lane == 0) sredi[wid] = cand;
+      __syncthreads();
+      cand = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+      found = cand == 0x7fffffff ? 0 : cand;
+    }
+    token = found;
+  }
+  if (t == 0) {
+    p.out_token[b] = token;
+    p.out_logprob[b] = bf2f(lrow[token]) - raw_lse;
+    if (p.counts && crow_i >= 0) {
+      uint16_t* c = p.counts + (size_t)crow_i * p.V + token;
+      if (*c < 0xffffu) *c += 1;
+    }
+  }
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_sample(const void* logits, int ld, int V, int B, const float* temperature, const float* top_p,
+                          const int* top_k, const float* min_p, const float* top_a, const float* freq_pen,
+                          const float* pres_pen, const float* rep_pen, void* counts, const int* count_rows,
+                          const float* bias, const int* bias_rows, const unsigned int* mask, const int* mask_rows,
+                          const unsigned long long* seeds, const unsigned long long* offsets, int num_logprobs,
+                          int* out_token, float* out_logprob, int* out_topk_ids, float* out_topk_lp, hipStream_t s) {
+  using namespace lwc;
+  if (V % 32 != 0 || num_logprobs < 0 || num_logprobs > kMaxTopK) return -1;
+  if (B == 0) return 0;
+  SampleParams p{(const bf16_t*)logits, ld, V, temperature, top_p, top_k, min_p, top_a, freq_pen, pres_pen, rep_pen,
+                 (uint16_t*)counts, count_rows, bias, bias_rows, mask, mask_rows, seeds, offsets, num_logprobs,
+                 out_token, out_logprob, out_topk_ids, out_topk_lp};
+  const int nvec = V / 8;
+  const int slots = (nvec + kSampT - 1) / kSampT;
+  if (slots <= 4)
+    sample_kernel<4><<<B, kSampT, 0, s>>>(p);
+  else if (slots <= 8)
+    sample_kernel<8><<<B, kSampT, 0, s>>>(p);
+  else if (slots <= 16)
+    sample_kernel<16><<<B, kSampT, 0, s>>>(p);
+  else if (slots <= 20)
+    sample_kernel<20><<<B, kSampT, 0, s>>>(p);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,81 @@
+// pybind11 module `llm_weighted_consensus_amd._runtime`: host runtime of the engine and the
+// consensus core.  No GPU dependency (plain g++), so CPU tests load exactly this code.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "block_manager.h"
+#include "consensus_core.h"
+
+namespace py = pybind11;
+using lwc::BlockManager;
+
+namespace {
+
+// Append one token to every sequence and build the padded decode batch in one call:
+// returns (block_tables[B, width] int32, ctx_lens[B] int32, slots[B] int32, positions[B] int32).
+// `width` >= every table length (the engine passes its captured-graph width).
+py::tuple prepare_decode(BlockManager& bm, const std::vector<int64_t>& seqs, int width, int pad_to) {
+  const int B = (int)seqs.size();
+  const int Bp = std::max(B, pad_to);
+  py::array_t<int32_t> bt({Bp, width}), ctx(Bp), slots(Bp), pos(Bp);
+  auto btm = bt.mutable_unchecked<2>();
+  auto cm = ctx.mutable_unchecked<1>();
+  auto sm = slots.mutable_unchecked<1>();
+  auto pm = pos.mutable_unchecked<1>();
+  for (int i = 0; i < B; ++i) {
+    const int64_t slot = bm.append_token(seqs[i]);
+    const auto& tab = bm.block_table(seqs[i]);
+    if ((int)tab.size() > width) throw std::runtime_error("prepare_decode: block table wider than batch width");
+    for (int j = 0; j < width; ++j) btm(i, j) = j < (int)tab.size() ? tab[j] : 0;
+    const int64_t len = bm.length(seqs[i]);
+    cm(i) = (int32_t)len;
+    sm(i) = (int32_t)slot;
+    pm(i) = (int32_t)(len - 1);
+  }
+  for (int i = B; i < Bp; ++i) {  // padding rows: 1-token context on block 0, no cache write
+    for (int j = 0; j < width; ++j) btm(i, j) = 0;
+    cm(i) = 1;
+    sm(i) = -1;
+    pm(i) = 0;
+  }
+  return py::make_tuple(bt, ctx, slots, pos);
+}
+
+// Slots of positions [start, start+count) of a sequence (prefill scatter targets).
+py::array_t<int32_t> slots_range(const BlockManager& bm, int64_t seq, int64_t start, int64_t count) {
+  py::array_t<int32_t> out(count);
+  auto m = out.mutable_unchecked<1>();
+  for (int64_t i = 0; i < count; ++i) m(i) = (int32_t)bm.slot(seq, start + i);
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "llm_weighted_consensus_amd host runtime: paged-KV block manager and consensus core";
+
+  py::class_<BlockManager>(m, "BlockManager")
+      .def(py::init<int, int>(), py::arg("num_blocks"), py::arg("block_size"))
+      .def_property_readonly("num_blocks", &BlockManager::num_blocks)
+      .def_property_readonly("block_size", &BlockManager::block_size)
+      .def_property_readonly("num_free", &BlockManager::num_free)
+      .def_property_readonly("num_sequences", &BlockManager::num_sequences)
+      .def("has_sequence", &BlockManager::has_sequence)
+      .def("blocks_for", &BlockManager::blocks_for)
+      .def("can_allocate", &BlockManager::can_allocate)
+      .def("add_sequence", &BlockManager::add_sequence)
+      .def("fork", &BlockManager::fork)
+      .def("append_token", &BlockManager::append_token)
+      .def("append_cost", &BlockManager::append_cost)
+      .def("free_sequence", &BlockManager::free_sequence)
+      .def("length", &BlockManager::length)
+      .def("block_table", &BlockManager::block_table)
+      .def("slot", &BlockManager::slot)
+      .def("refcount", &BlockManager::refcount)
+      .def("take_copies", &BlockManager::take_copies);
+  m.def("prepare_decode", &prepare_decode, py::arg("bm"), py::arg("seqs"), py::arg("width"), py::arg("pad_to") = 0);
+  m.def("slots_range", &slots_range);
+
+  lwc::bind_consensus_core(m);
+}

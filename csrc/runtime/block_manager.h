@@ -1,0 +1,70 @@
+// Paged-KV block manager for the MI355X engine (host side, C++).
+//
+// The KV cache of every GPU is one flat pool of fixed-size blocks (BS tokens x all layers).  A
+// sequence owns an ordered block table; blocks are reference counted so a sequence can be FORKED
+// (the N candidates / voters of one request share their prompt's blocks) and the first write into a
+// shared block triggers copy-on-write: a fresh block is allocated and a (src, dst) copy is queued
+// for the GPU (kv_block_copy kernel, K12) before the step that writes it.
+//
+// Sized for 288 GB of HBM3E: block ids are int32 (2^31 blocks x 16 tokens), sequence ids int64.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace lwc {
+
+class BlockManager {
+ public:
+  BlockManager(int num_blocks, int block_size);
+
+  int num_blocks() const { return num_blocks_; }
+  int block_size() const { return block_size_; }
+  int num_free() const { return (int)free_.size(); }
+  int num_sequences() const { return (int)seqs_.size(); }
+  bool has_sequence(int64_t seq) const { return seqs_.count(seq) != 0; }
+
+  // Blocks needed to hold `num_tokens` tokens for a new sequence.
+  int blocks_for(int64_t num_tokens) const { return (int)((num_tokens + block_size_ - 1) / block_size_); }
+  bool can_allocate(int num_blocks) const { return (int)free_.size() >= num_blocks; }
+
+  // Allocate a new sequence able to hold `num_tokens` tokens (its length is set to num_tokens).
+  void add_sequence(int64_t seq, int64_t num_tokens);
+  // Child shares every block of the parent (refcount++), same length.
+  void fork(int64_t parent, int64_t child);
+  // Grow the sequence by one token; returns the cache slot (block*BS + offset) of that token.
+  // Allocates a new block at block boundaries and performs copy-on-write on a shared last block.
+  int64_t append_token(int64_t seq);
+  // Number of extra blocks `append_token` may need for this sequence (0 or 1).
+  int append_cost(int64_t seq) const;
+  void free_sequence(int64_t seq);
+
+  int64_t length(int64_t seq) const { return get(seq).len; }
+  const std::vector<int32_t>& block_table(int64_t seq) const { return get(seq).blocks; }
+  // Slot of token position `pos` of the sequence.
+  int64_t slot(int64_t seq, int64_t pos) const;
+  int refcount(int32_t block) const { return ref_[block]; }
+
+  // Copy-on-write copies queued since the last call (src, dst); cleared by this call.
+  std::vector<std::pair<int32_t, int32_t>> take_copies();
+
+ private:
+  struct Seq {
+    std::vector<int32_t> blocks;
+    int64_t len = 0;
+  };
+  const Seq& get(int64_t seq) const;
+  Seq& get(int64_t seq);
+  int32_t alloc_block();
+  void release(int32_t block);
+
+  int num_blocks_, block_size_;
+  std::vector<int32_t> free_;
+  std::vector<int32_t> ref_;
+  std::unordered_map<int64_t, Seq> seqs_;
+  std::vector<std::pair<int32_t, int32_t>> copies_;
+};
+
+}  // namespace lwc

@@ -1,0 +1,141 @@
+"""BERT/BGE-style encoder (bge-small/base/large shapes) for embeddings on the gfx950 kernel set.
+
+Serves the reference's embeddings capability (`CreateEmbeddingResponse`, src/embeddings/response.rs:1-30,
+carried in training-table weight data src/score/completions/weight.rs:15-18) and the embedding
+consensus scorer.  Sequences are packed (cu_seqlens) — no padding FLOPs:
+
+    x   = LN(word[ids] + (pos + type0)[pos])          K7 gathers + K9a LN (+residual)
+    per layer (post-norm):
+      qkv = x Wqkv^T + b                               hipBLASLt (fused q|k|v)
+      a   = varlen bidirectional flash attention       K9c (MFMA, LDS-tiled QK^T)
+      x   = LN(x + a Wo^T + bo)                         K9a fused residual
+      h   = gelu(x W1^T + b1)                          hipBLASLt + K9b fused bias+GELU
+      x   = LN(x + h W2^T + b2)
+    e   = L2norm(pool(x))                               K9d (CLS for bge)
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .config import EncoderConfig
+
+POOL_MODES = {"cls": ops.POOL_CLS, "mean": ops.POOL_MEAN, "last": ops.POOL_LAST}
+
+
+@dataclass
+class EncLayer:
+    wqkv: torch.Tensor
+    bqkv: torch.Tensor
+    wo: torch.Tensor
+    bo: torch.Tensor
+    ln1_g: torch.Tensor
+    ln1_b: torch.Tensor
+    w1: torch.Tensor
+    b1: torch.Tensor
+    w2: torch.Tensor
+    b2: torch.Tensor
+    ln2_g: torch.Tensor
+    ln2_b: torch.Tensor
+
+
+class BertEncoder:
+    def __init__(self, cfg: EncoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 weights_path: Optional[str] = None):
+        if cfg.head_dim not in (64, 128):
+            raise NotImplementedError(f"encoder head_dim {cfg.head_dim} (attention kernel supports 64/128)")
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        if weights_path:
+            self._load(weights_path)
+        else:
+            self._random_init(seed)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    def _random_init(self, seed: int) -> None:
+        c, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 7)
+
+        def rnd(*shape, s=0.02):
+            return (torch.randn(*shape, generator=g, device=dev) * s).to(dt)
+
+        zeros = lambda *s: torch.zeros(*s, device=dev, dtype=dt)
+        ones = lambda *s: torch.ones(*s, device=dev, dtype=dt)
+        d, f = c.hidden, c.ffn
+        self.word = rnd(c.vocab_size, d)
+        pos = rnd(c.max_position, d)
+        typ = rnd(c.type_vocab, d)
+        self.pos_type = (pos.float() + typ[0].float()).to(dt).contiguous()
+        self.emb_ln_g, self.emb_ln_b = ones(d), zeros(d)
+        self.layers = [EncLayer(rnd(3 * d, d), zeros(3 * d), rnd(d, d), zeros(d), ones(d), zeros(d), rnd(f, d),
+                                zeros(f), rnd(d, f), zeros(d), ones(d), zeros(d)) for _ in range(c.layers)]
+
+    def _load(self, path: str) -> None:  # HF BertModel safetensors layout
+        from safetensors.torch import load_file
+
+        sd = load_file(path, device="cpu")
+        dev, dt = self.device, self.dtype
+        pre = "bert." if any(k.startswith("bert.") for k in sd) else ""
+        t = lambda n: sd[pre + n].to(device=dev, dtype=dt).contiguous()
+        self.word = t("embeddings.word_embeddings.weight")
+        self.pos_type = (t("embeddings.position_embeddings.weight").float()
+                         + t("embeddings.token_type_embeddings.weight")[0].float()).to(dt).contiguous()
+        self.emb_ln_g, self.emb_ln_b = t("embeddings.LayerNorm.weight"), t("embeddings.LayerNorm.bias")
+        self.layers = []
+        for i in range(self.cfg.layers):
+            p = f"encoder.layer.{i}."
+            qkv_w = torch.cat([t(p + f"attention.self.{n}.weight") for n in ("query", "key", "value")])
+            qkv_b = torch.cat([t(p + f"attention.self.{n}.bias") for n in ("query", "key", "value")])
+            self.layers.append(EncLayer(
+                qkv_w.contiguous(), qkv_b.contiguous(), t(p + "attention.output.dense.weight"),
+                t(p + "attention.output.dense.bias"), t(p + "attention.output.LayerNorm.weight"),
+                t(p + "attention.output.LayerNorm.bias"), t(p + "intermediate.dense.weight"),
+                t(p + "intermediate.dense.bias"), t(p + "output.dense.weight"), t(p + "output.dense.bias"),
+                t(p + "output.LayerNorm.weight"), t(p + "output.LayerNorm.bias")))
+
+    def forward_packed(self, ids: torch.Tensor, positions: torch.Tensor, cu: torch.Tensor, max_len: int) -> torch.Tensor:
+        """ids/positions [T] int32, cu [n+1] int32 -> hidden [T, d] bf16."""
+        c = self.cfg
+        H, Dh, d = c.heads, c.head_dim, c.hidden
+        T = ids.shape[0]
+        x = ops.layernorm(ops.embedding(self.word, ids), self.emb_ln_g, self.emb_ln_b, c.ln_eps,
+                          residual=ops.embedding(self.pos_type, positions))
+        for L in self.layers:
+            qkv = F.linear(x, L.wqkv, L.bqkv)
+            a = ops.prefill_attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], cu, max_len, H, H, Dh, self.scale,
+                                      causal=False)
+            o = F.linear(a, L.wo, L.bo)
+            x = ops.layernorm(o, L.ln1_g, L.ln1_b, c.ln_eps, residual=x)
+            h = ops.bias_gelu_(F.linear(x, L.w1), L.b1)
+            y = F.linear(h, L.w2, L.b2)
+            x = ops.layernorm(y, L.ln2_g, L.ln2_b, c.ln_eps, residual=x)
+        return x
+
+    def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        cap = min(max_tokens or self.cfg.max_position, self.cfg.max_position)
+        V = self.cfg.vocab_size
+        ids, pos, cu = [], [], [0]
+        for tl in token_lists:
+            tl = [int(t) % V for t in list(tl)[:cap]] or [0]
+            ids.extend(tl)
+            pos.extend(range(len(tl)))
+            cu.append(cu[-1] + len(tl))
+        dev = self.device
+        max_len = max(cu[i + 1] - cu[i] for i in range(len(cu) - 1))
+        return (torch.tensor(ids, dtype=torch.int32, device=dev), torch.tensor(pos, dtype=torch.int32, device=dev),
+                torch.tensor(cu, dtype=torch.int32, device=dev), max_len)
+
+    def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        """Embed sequences (token ids in this encoder's vocab; ids are folded into range) ->
+        (unit f32 [n, d], unit bf16 [n, d])."""
+        ids, pos, cu, max_len = self.pack(token_lists, max_tokens)
+        return self.embed_packed(ids, pos, cu, max_len)
+
+    def embed_packed(self, ids, pos, cu, max_len):
+        h = self.forward_packed(ids, pos, cu, max_len)
+        return ops.pool_l2norm(h, cu, POOL_MODES[self.cfg.pooling])

@@ -1,0 +1,211 @@
+"""Llama-family decoder (Llama-3 / Mistral shapes) on the gfx950 kernel set.
+
+This is the local generation backend that replaces the reference's upstream providers
+(reference: every voter is an OpenAI-compatible chat call, src/chat/completions/client.rs:308-332).
+
+Per layer (decode, B sequences):
+    rmsnorm(+residual)            K1 (fused residual add)
+    qkv  = x @ Wqkv^T             hipBLASLt GEMM (fused q|k|v weight)
+    rope + paged KV write         K2 (in place, one pass)
+    attn = paged GQA decode       K3 (MFMA, split-K)
+    o    = attn @ Wo^T            hipBLASLt
+    rmsnorm(+residual)            K1
+    gu   = x @ Wgu^T              hipBLASLt (fused gate|up weight)
+    act  = silu(g) * u            K5
+    down = act @ Wd^T             hipBLASLt
+Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over the fresh
+k/v of the qkv buffer; the k/v are scattered into the paged cache in the same RoPE pass.
+
+Plain library GEMMs go to hipBLASLt through torch (allowed by the design rules); everything else
+is a hand-written HIP kernel from ``llm_weighted_consensus_amd.ops``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .config import DecoderConfig
+
+
+def rope_tables(cfg: DecoderConfig, device, max_pos: Optional[int] = None):
+    """Host-built cos/sin tables [max_pos, D/2] f32 (Appendix B: no on-device trig), with the
+    Llama-3 frequency scaling when configured."""
+    D = cfg.head_dim
+    max_pos = max_pos or cfg.max_position
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, D, 2, dtype=torch.float64) / D))
+    if cfg.rope_scaling is not None:
+        factor, lo_f, hi_f, orig = cfg.rope_scaling
+        lo_wl, hi_wl = orig / lo_f, orig / hi_f
+        wl = 2 * math.pi / inv
+        smooth = (orig / wl - lo_f) / (hi_f - lo_f)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        inv = scaled
+    t = torch.arange(max_pos, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return ang.cos().float().to(device).contiguous(), ang.sin().float().to(device).contiguous()
+
+
+@dataclass
+class LayerWeights:
+    attn_norm: torch.Tensor
+    wqkv: torch.Tensor      # [(Hq+2Hkv)*D, d]
+    wo: torch.Tensor        # [d, Hq*D]
+    mlp_norm: torch.Tensor
+    w_gate_up: torch.Tensor  # [2F, d]  rows: gate then up
+    w_down: torch.Tensor    # [d, F]
+
+
+class KVCache:
+    """One flat bf16 pool for all layers: [L, 2, num_blocks, Hkv*BS*D]; per-layer K view
+    [NB, Hkv, BS, D] and transposed V view [NB, Hkv, D, BS]."""
+
+    def __init__(self, cfg: DecoderConfig, num_blocks: int, block_size: int, device, dtype=torch.bfloat16):
+        self.cfg, self.num_blocks, self.block_size = cfg, num_blocks, block_size
+        self.block_elems = cfg.kv_heads * block_size * cfg.head_dim
+        self.pool = torch.zeros(cfg.layers, 2, num_blocks, self.block_elems, dtype=dtype, device=device)
+        Hkv, D = cfg.kv_heads, cfg.head_dim
+        self.k = [self.pool[l, 0].view(num_blocks, Hkv, block_size, D) for l in range(cfg.layers)]
+        self.v = [self.pool[l, 1].view(num_blocks, Hkv, D, block_size) for l in range(cfg.layers)]
+
+    @staticmethod
+    def bytes_per_block(cfg: DecoderConfig, block_size: int) -> int:
+        return cfg.layers * 2 * cfg.kv_heads * block_size * cfg.head_dim * 2
+
+    def copy_blocks(self, pairs: torch.Tensor) -> None:
+        """Copy-on-write block copies (K12) for every layer, K and V."""
+        if pairs.numel():
+            ops.kv_block_copy(self.pool.view(self.cfg.layers * 2, self.num_blocks, self.block_elems), pairs)
+
+
+class LlamaModel:
+    def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 weights_path: Optional[str] = None, max_position: Optional[int] = None):
+        if cfg.num_experts:
+            raise NotImplementedError("MoE decoders use models.mixtral.MixtralModel")
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        self.cos, self.sin = rope_tables(cfg, self.device, max_position)
+        if weights_path:
+            self._load(weights_path)
+        else:
+            self._random_init(seed)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # ------------------------------------------------------------------ weights
+    def _random_init(self, seed: int) -> None:
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        std = 0.02
+
+        def rnd(*shape, s=std):
+            return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * s).to(dt)
+
+        d, qkv, F_ = cfg.hidden, cfg.qkv_dim, cfg.ffn
+        self.embed = rnd(cfg.vocab_size, d)
+        self.layers = []
+        out_std = std / math.sqrt(2 * cfg.layers)
+        for _ in range(cfg.layers):
+            self.layers.append(LayerWeights(
+                attn_norm=torch.ones(d, device=dev, dtype=dt),
+                wqkv=rnd(qkv, d),
+                wo=rnd(d, cfg.heads * cfg.head_dim, s=out_std),
+                mlp_norm=torch.ones(d, device=dev, dtype=dt),
+                w_gate_up=rnd(2 * F_, d),
+                w_down=rnd(d, F_, s=out_std),
+            ))
+        self.final_norm = torch.ones(d, device=dev, dtype=dt)
+        self.lm_head = self.embed if cfg.tie_embeddings else rnd(cfg.vocab_size, d)
+
+    def _load(self, path: str) -> None:
+        """Load HF-layout safetensors (model.layers.N.self_attn.q_proj.weight ...) and fuse q|k|v and
+        gate|up into the engine's layout."""
+        from safetensors.torch import load_file
+
+        files = sorted(Path(path).glob("*.safetensors")) if Path(path).is_dir() else [Path(path)]
+        sd = {}
+        for f in files:
+            sd.update(load_file(str(f), device="cpu"))
+        dev, dt = self.device, self.dtype
+
+        def t(name):
+            return sd[name].to(device=dev, dtype=dt).contiguous()
+
+        self.embed = t("model.embed_tokens.weight")
+        self.layers = []
+        for i in range(self.cfg.layers):
+            p = f"model.layers.{i}."
+            self.layers.append(LayerWeights(
+                attn_norm=t(p + "input_layernorm.weight"),
+                wqkv=torch.cat([t(p + "self_attn.q_proj.weight"), t(p + "self_attn.k_proj.weight"),
+                                t(p + "self_attn.v_proj.weight")]).contiguous(),
+                wo=t(p + "self_attn.o_proj.weight"),
+                mlp_norm=t(p + "post_attention_layernorm.weight"),
+                w_gate_up=torch.cat([t(p + "mlp.gate_proj.weight"), t(p + "mlp.up_proj.weight")]).contiguous(),
+                w_down=t(p + "mlp.down_proj.weight"),
+            ))
+        self.final_norm = t("model.norm.weight")
+        self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
+
+    # ------------------------------------------------------------------ forward
+    def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn) -> torch.Tensor:
+        """Runs every layer; x_res is the residual stream (updated in place); returns the final
+        normalised hidden state."""
+        cfg = self.cfg
+        T = x_res.shape[0]
+        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
+        for li, L in enumerate(self.layers):
+            qkv = F.linear(h, L.wqkv)
+            ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
+            attn = attn_fn(qkv, li)
+            o = F.linear(attn.view(T, Hq * D), L.wo)
+            h = ops.rmsnorm(o, L.mlp_norm, cfg.rms_eps, residual=x_res)
+            gu = F.linear(h, L.w_gate_up)
+            act = ops.silu_mul(gu)
+            down = F.linear(act, L.w_down)
+            nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
+            h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
+        return h
+
+    def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
+               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1) -> torch.Tensor:
+        """One decode step for B sequences -> logits [B, V] bf16.  All inputs are device tensors
+        (int32), so the whole call can be captured in a hipGraph."""
+        cfg = self.cfg
+        x = ops.embedding(self.embed, tokens)
+        B = tokens.shape[0]
+        part_o = part_lse = None
+        if num_splits > 1:
+            part_o = torch.empty(B * cfg.heads * num_splits * cfg.head_dim, dtype=torch.float32, device=x.device)
+            part_lse = torch.empty(B * cfg.heads * num_splits, dtype=torch.float32, device=x.device)
+
+        def attn_fn(qkv, li):
+            return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
+                                    num_splits=num_splits, part_o=part_o, part_lse=part_lse)
+
+        h = self._layers(x, cache, positions, slots, attn_fn)
+        return F.linear(h, self.lm_head)
+
+    def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cu_seqlens: torch.Tensor,
+                max_seqlen: int, last_idx: torch.Tensor, cache: KVCache) -> torch.Tensor:
+        """Prefill packed prompts (cu_seqlens) -> logits of each sequence's last token [nseq, V]."""
+        cfg = self.cfg
+        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        x = ops.embedding(self.embed, tokens)
+
+        def attn_fn(qkv, li):
+            q = qkv[:, : Hq * D]
+            k = qkv[:, Hq * D:(Hq + Hkv) * D]
+            v = qkv[:, (Hq + Hkv) * D:]
+            return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
+
+        h = self._layers(x, cache, positions, slots, attn_fn)
+        return F.linear(h.index_select(0, last_idx), self.lm_head)

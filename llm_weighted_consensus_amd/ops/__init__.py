@@ -1,0 +1,200 @@
+"""Python face of the hand-written gfx950 HIP kernels (``csrc/kernels``).
+
+Every function here allocates its outputs (unless ``out=`` is given) and calls straight into
+``_kernels.so``; there is no eager-PyTorch fallback.  If the extension is missing the first call
+raises: on a GPU box a silent fallback would hide that the native path is not the one running.
+
+Layout conventions shared with the engine:
+  * fused qkv rows  : [T, (Hq + 2*Hkv) * D]
+  * K cache (layer) : [num_blocks, Hkv, block_size, D]
+  * V cache (layer) : [num_blocks, Hkv, D, block_size]   (transposed, see attention_decode.hip)
+"""
+from __future__ import annotations
+
+import importlib
+from typing import Optional
+
+import torch
+
+_K = None
+_ERR: Optional[BaseException] = None
+
+
+def kernels():
+    """Return the loaded ``_kernels`` extension, raising loudly if it is unavailable."""
+    global _K, _ERR
+    if _K is None:
+        try:
+            _K = importlib.import_module("llm_weighted_consensus_amd.ops._kernels")
+        except BaseException as e:  # pragma: no cover - depends on the build
+            _ERR = e
+            raise RuntimeError(
+                "llm_weighted_consensus_amd HIP kernels are not built: run "
+                "`python -m llm_weighted_consensus_amd._build` (hipcc --offload-arch=gfx950)"
+            ) from e
+    return _K
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except RuntimeError:
+        return False
+
+
+# ---------------------------------------------------------------------------------------------
+# normalisation / element-wise
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = rmsnorm(x [+ residual]) * w.  With ``residual`` given, ``residual`` is updated in place to
+    ``x + residual`` (the pre-norm residual stream) — the fused K1 kernel."""
+    if out is None:
+        out = torch.empty_like(x)
+    kernels().rmsnorm(x, residual, w, out, float(eps))
+    return out
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
+              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = layernorm(x [+ residual]) * g + b (K9a)."""
+    if out is None:
+        out = torch.empty_like(x)
+    kernels().layernorm(x, residual, g, b, out, float(eps))
+    return out
+
+
+def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """SwiGLU over a fused [T, 2F] = [gate | up] buffer (K5)."""
+    F = gate_up.shape[-1] // 2
+    if out is None:
+        out = torch.empty(*gate_up.shape[:-1], F, dtype=gate_up.dtype, device=gate_up.device)
+    kernels().silu_mul(gate_up, out)
+    return out
+
+
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In place x = gelu_erf(x + bias) (K9b)."""
+    kernels().bias_gelu(x, bias)
+    return x
+
+
+def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row gather table[ids] (K7); ids int32."""
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    kernels().embedding(table, ids, out)
+    return out
+
+
+def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, Hq: int, Hkv: int, D: int,
+                  slots: Optional[torch.Tensor] = None) -> None:
+    """In-place rotate-half RoPE on q and k inside ``qkv`` and scatter k, v into the paged cache at
+    ``slots`` (K2).  ``slots=None`` only rotates (no cache write)."""
+    kernels().rope_kv_write(qkv, positions, slots, cos, sin, k_cache, v_cache, int(Hq), int(Hkv), int(D))
+
+
+def kv_block_copy(cache: torch.Tensor, pairs: torch.Tensor) -> None:
+    """Copy whole KV blocks src->dst for every layer, K and V (K12, copy-on-write fork).
+    ``cache`` is viewed as [L*2, num_blocks, ...]."""
+    kernels().kv_block_copy(cache, pairs)
+
+
+# ---------------------------------------------------------------------------------------------
+# attention
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                 ctx_lens: torch.Tensor, Hq: int, scale: float, num_splits: int = 1,
+                 out: Optional[torch.Tensor] = None, part_o: Optional[torch.Tensor] = None,
+                 part_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One-token paged GQA decode attention (K3).  q: [B, >=Hq*D] (row stride allowed)."""
+    B = q.shape[0]
+    D = k_cache.shape[-1]
+    if out is None:
+        out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    if num_splits > 1 and (part_o is None or part_lse is None):
+        part_o = torch.empty(B * Hq * num_splits * D, dtype=torch.float32, device=q.device)
+        part_lse = torch.empty(B * Hq * num_splits, dtype=torch.float32, device=q.device)
+    kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, part_o, part_lse, int(num_splits),
+                           float(scale))
+    return out
+
+
+def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int,
+                      Hq: int, Hkv: int, D: int, scale: float, causal: bool,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Varlen flash attention forward (K4 causal / K9c bidirectional); q,k,v are [T, H*D] views."""
+    if out is None:
+        out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    kernels().prefill_attention(q, k, v, out, cu_seqlens, int(max_seqlen), int(Hq), int(Hkv), int(D), float(scale),
+                                bool(causal))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# sampling / scoring
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+           min_p: torch.Tensor, top_a: torch.Tensor, seeds: torch.Tensor, offsets: torch.Tensor,
+           num_logprobs: int = 0, freq_pen=None, pres_pen=None, rep_pen=None, counts=None, count_rows=None,
+           bias=None, bias_rows=None, mask=None, mask_rows=None, out_token=None, out_logprob=None,
+           out_topk_ids=None, out_topk_lp=None):
+    """Fused sampler (K8a-d).  Returns (tokens[B] int32, token_logprob[B] f32, topk_ids[B,K], topk_lp[B,K])."""
+    B = logits.shape[0]
+    dev = logits.device
+    K = int(num_logprobs)
+    if out_token is None:
+        out_token = torch.empty(B, dtype=torch.int32, device=dev)
+    if out_logprob is None:
+        out_logprob = torch.empty(B, dtype=torch.float32, device=dev)
+    if out_topk_ids is None:
+        out_topk_ids = torch.empty(B, max(K, 1), dtype=torch.int32, device=dev)
+    if out_topk_lp is None:
+        out_topk_lp = torch.empty(B, max(K, 1), dtype=torch.float32, device=dev)
+    kernels().sample(logits, temperature, top_p, top_k, min_p, top_a, freq_pen, pres_pen, rep_pen, counts, count_rows,
+                     bias, bias_rows, mask, mask_rows, seeds, offsets, K, out_token, out_logprob, out_topk_ids,
+                     out_topk_lp)
+    return out_token, out_logprob, out_topk_ids[:, :K], out_topk_lp[:, :K]
+
+
+POOL_CLS, POOL_MEAN, POOL_LAST = 0, 1, 2
+
+
+def pool_l2norm(hidden: torch.Tensor, cu_seqlens: torch.Tensor, mode: int, out_bf16: bool = True):
+    """Pool packed encoder states per sequence and L2-normalise (K9d).  Returns (f32, bf16|None)."""
+    n = cu_seqlens.numel() - 1
+    d = hidden.shape[1]
+    of = torch.empty(n, d, dtype=torch.float32, device=hidden.device)
+    ob = torch.empty(n, d, dtype=torch.bfloat16, device=hidden.device) if out_bf16 else None
+    kernels().pool_l2norm(hidden, cu_seqlens, int(mode), of, ob)
+    return of, ob
+
+
+def cosine_consensus(E: torch.Tensor, tau: float = 0.05):
+    """Embedding consensus over R requests x n candidates (K10a): S = E E^T on MFMA, then
+    centrality_i = mean_{j!=i} S_ij and weights = softmax(centrality / tau).
+    E: [R, n, d] bf16 unit rows.  Returns (S [R,n,n], centrality [R,n], weights [R,n], best [R])."""
+    R, n, d = E.shape
+    n_pad = (n + 15) // 16 * 16
+    S = torch.empty(R, n_pad, n_pad, dtype=torch.float32, device=E.device)
+    cen = torch.empty(R, n, dtype=torch.float32, device=E.device)
+    w = torch.empty(R, n, dtype=torch.float32, device=E.device)
+    best = torch.empty(R, dtype=torch.int32, device=E.device)
+    kernels().cosine_consensus(E.contiguous(), S, 1.0 / float(tau), cen, w, best)
+    return S[:, :n, :n], cen, w, best
+
+
+def vote_tally(votes: torch.Tensor, weights: torch.Tensor):
+    """Batched weighted tally (K10b): votes [R, L, C], weights [R, L] ->
+    (choice_weight [R, C], confidence [R, C], voter_confidence [R, L])."""
+    R, L, C = votes.shape
+    cw = torch.empty(R, C, dtype=torch.float32, device=votes.device)
+    conf = torch.empty(R, C, dtype=torch.float32, device=votes.device)
+    vc = torch.empty(R, L, dtype=torch.float32, device=votes.device)
+    kernels().vote_tally(votes.contiguous(), weights.contiguous(), cw, conf, vc)
+    return cw, conf, vc

@@ -1,0 +1,111 @@
+"""Process-group bring-up and the collectives the framework uses (RCCL over xGMI on MI355X).
+
+One process per GPU; `torch.distributed` backend "nccl" IS RCCL on ROCm.  On CPU (tests) the same
+code runs over gloo.  Collectives used by the serving/bench paths:
+
+  C1 all_gather of candidate embeddings  [n_local, d] -> [world, n_local, d]
+  C2 gather of votes / tallies           (tiny, latency-bound)
+  C3 TP all-reduce                       (tensor-parallel decoders)
+  C5 broadcast / barrier                 (control)
+
+xGMI on MI355X is point-to-point (7 links per GPU): the payloads here are small (an all-gather of
+64 x 1024 bf16 = 128 KiB per rank), i.e. latency-bound, so we issue ONE collective per phase on a
+flat buffer instead of many small ones.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: Optional[str] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+
+_INFO = DistInfo()
+
+
+def init_from_env(device_type: Optional[str] = None, timeout_s: float = 600.0) -> DistInfo:
+    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/
+    MASTER_ADDR/MASTER_PORT).  Single-process when WORLD_SIZE is unset or 1."""
+    global _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(**kw)
+        _INFO = DistInfo(rank, world, local, backend)
+    else:
+        _INFO = DistInfo(rank, world, local, dist.get_backend() if dist.is_initialized() else None)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def barrier() -> None:
+    if _INFO.enabled:
+        if _INFO.backend == "nccl":
+            dist.barrier(device_ids=[_INFO.local_rank])
+        else:
+            dist.barrier()
+
+
+def all_gather(t: torch.Tensor) -> torch.Tensor:
+    """[*] per rank -> [world, *] (C1).  One collective on a contiguous buffer."""
+    if not _INFO.enabled:
+        return t.unsqueeze(0)
+    t = t.contiguous()
+    out = torch.empty((_INFO.world, *t.shape), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    return out
+
+
+def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    if _INFO.enabled:
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+    return t
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    if not _INFO.enabled:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    all_reduce_(t, "max")
+    return float(t.item())
+
+
+def broadcast_object(obj, src: int = 0):
+    if not _INFO.enabled:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

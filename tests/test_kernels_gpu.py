@@ -1,0 +1,283 @@
+"""Numerics of every hand-written gfx950 kernel against a plain PyTorch fp32 reference."""
+import math
+
+import pytest
+import torch
+
+from tests import torch_ref as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, dev, scale=1.0, g=None):
+    return (torch.randn(*shape, device=dev, generator=g) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    assert torch.isfinite(a).all(), "non-finite output"
+    assert (err <= lim).all(), f"max err {err.max().item():.4g} (atol {atol}, rtol {rtol})"
+
+
+@pytest.mark.parametrize("d", [384, 1024, 4096])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(gpu, d, with_res):
+    from llm_weighted_consensus_amd import ops
+
+    x = _bf(37, d, dev=gpu)
+    w = _bf(d, dev=gpu, scale=0.5) + 1
+    if with_res:
+        r = _bf(37, d, dev=gpu)
+        r0 = r.clone()
+        y = ops.rmsnorm(x, w, 1e-5, residual=r)
+        h = (x.float() + r0.float()).to(torch.bfloat16)
+        _close(r, h, 1e-2, 1e-2)
+        _close(y, ref.rmsnorm(h, w, 1e-5), 3e-2, 2e-2)
+    else:
+        y = ops.rmsnorm(x, w, 1e-5)
+        _close(y, ref.rmsnorm(x, w, 1e-5), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("d", [256, 768, 1024])
+def test_layernorm(gpu, d):
+    from llm_weighted_consensus_amd import ops
+
+    x, r = _bf(53, d, dev=gpu), _bf(53, d, dev=gpu)
+    g, b = _bf(d, dev=gpu, scale=0.2) + 1, _bf(d, dev=gpu, scale=0.2)
+    y = ops.layernorm(x, g, b, 1e-12, residual=r)
+    _close(y, ref.layernorm(x.float() + r.float(), g, b, 1e-12), 4e-2, 2e-2)
+    y2 = ops.layernorm(x, g, b, 1e-12)
+    _close(y2, ref.layernorm(x, g, b, 1e-12), 4e-2, 2e-2)
+
+
+def test_silu_mul_gelu_embedding(gpu):
+    from llm_weighted_consensus_amd import ops
+
+    gu = _bf(19, 2 * 1024, dev=gpu)
+    y = ops.silu_mul(gu)
+    g, u = gu.float().chunk(2, -1)
+    _close(y, torch.nn.functional.silu(g) * u, 2e-2, 2e-2)
+    x = _bf(11, 4096, dev=gpu)
+    b = _bf(4096, dev=gpu)
+    x0 = x.clone()
+    ops.bias_gelu_(x, b)
+    _close(x, torch.nn.functional.gelu(x0.float() + b.float()), 2e-2, 2e-2)
+    table = _bf(1000, 384, dev=gpu)
+    ids = torch.randint(0, 1000, (77,), device=gpu, dtype=torch.int32)
+    _close(ops.embedding(table, ids), table[ids.long()], 0)
+
+
+def test_rope_kv_write(gpu):
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import rope_tables
+
+    cfg = decoder_config("llama-tiny")
+    Hq, Hkv, D, BS, NB = cfg.heads, cfg.kv_heads, cfg.head_dim, 16, 12
+    cos, sin = rope_tables(cfg, gpu, 256)
+    T = 21
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu)
+    q0 = qkv.clone()
+    pos = torch.randint(0, 200, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:T].to(torch.int32)
+    kc = torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=gpu)
+    vc = torch.zeros(NB, Hkv, D, BS, dtype=torch.bfloat16, device=gpu)
+    ops.rope_kv_write(qkv, pos, cos, sin, kc, vc, Hq, Hkv, D, slots=slots)
+    q_ref = ref.rope(q0[:, : Hq * D].view(T, Hq, D), pos, cos, sin)
+    k_ref = ref.rope(q0[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D), pos, cos, sin)
+    v_ref = q0[:, (Hq + Hkv) * D:].view(T, Hkv, D)
+    _close(qkv[:, : Hq * D].view(T, Hq, D), q_ref, 2e-2, 1e-2)
+    _close(qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D), k_ref, 2e-2, 1e-2)
+    blk, off = (slots // BS).long(), (slots % BS).long()
+    _close(kc[blk, :, off, :], k_ref, 2e-2, 1e-2)
+    _close(vc[blk, :, :, off], v_ref, 0)
+
+
+@pytest.mark.parametrize("G,splits", [(4, 1), (4, 3), (1, 1), (8, 2)])
+def test_paged_decode(gpu, G, splits):
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(0)
+    Hkv, D, BS, NB = 2, 128, 16, 64
+    Hq = Hkv * G
+    B = 5
+    ctx = torch.tensor([1, 15, 16, 77, 200], dtype=torch.int32, device=gpu)
+    width = 16
+    kc = _bf(NB, Hkv, BS, D, dev=gpu)
+    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    # poison the cache beyond context with NaNs to check masking
+    perm = torch.randperm(NB, device=gpu)
+    bt = torch.zeros(B, width, dtype=torch.int32, device=gpu)
+    k = 0
+    for b in range(B):
+        nb = (int(ctx[b]) + BS - 1) // BS
+        bt[b, :nb] = perm[k:k + nb].to(torch.int32)
+        k += nb
+    for b in range(B):
+        L = int(ctx[b])
+        last = int(bt[b, (L - 1) // BS])
+        o = L % BS
+        if o:
+            kc[last, :, o:, :] = float("nan")
+            vc[last, :, :, o:] = float("nan")
+    q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
+    out = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits)
+    for b in range(B):
+        L = int(ctx[b])
+        toks = torch.arange(L, device=gpu)
+        blk = bt[b, toks // BS].long()
+        kk = kc[blk, :, toks % BS, :]  # [L, Hkv, D]
+        vv = vc[blk, :, :, toks % BS]  # [L, Hkv, D]
+        q = q_full[b, : Hq * D].view(1, Hq, D)
+        o = ref.attention(q, kk, vv, False, 1 / math.sqrt(D))[0]
+        _close(out[b], o, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,causal", [(128, 8, 2, True), (64, 4, 4, False), (128, 4, 4, False),
+                                             (64, 8, 2, True)])
+def test_prefill_attention(gpu, D, Hq, Hkv, causal):
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(1)
+    lens = [1, 17, 64, 100, 130]
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=gpu)
+    row = (Hq + 2 * Hkv) * D
+    qkv = _bf(T, row, dev=gpu)
+    q, k, v = qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    out = ops.prefill_attention(q, k, v, cu, max(lens), Hq, Hkv, D, 1 / math.sqrt(D), causal)
+    for i, L in enumerate(lens):
+        s0 = int(cu[i])
+        o = ref.attention(q[s0:s0 + L].reshape(L, Hq, D), k[s0:s0 + L].reshape(L, Hkv, D),
+                          v[s0:s0 + L].reshape(L, Hkv, D), causal, 1 / math.sqrt(D))
+        _close(out[s0:s0 + L].view(L, Hq, D), o, 2e-2, 2e-2)
+
+
+def _sample(logits, dev, n=None, **kw):
+    from llm_weighted_consensus_amd import ops
+
+    B = logits.shape[0]
+    f = lambda v: torch.full((B,), float(v), device=dev)
+    args = dict(temperature=f(kw.pop("temperature", 1.0)), top_p=f(kw.pop("top_p", 1.0)),
+                top_k=torch.full((B,), int(kw.pop("top_k", 0)), dtype=torch.int32, device=dev),
+                min_p=f(kw.pop("min_p", 0.0)), top_a=f(kw.pop("top_a", 0.0)),
+                seeds=kw.pop("seeds", torch.arange(B, device=dev, dtype=torch.int64) * 7919 + 1),
+                offsets=kw.pop("offsets", torch.zeros(B, device=dev, dtype=torch.int64)))
+    args.update(kw)
+    return ops.sample(logits, **args)
+
+
+def test_sample_greedy_and_logprobs(gpu):
+    torch.manual_seed(2)
+    V = 128256
+    logits = _bf(6, V, dev=gpu, scale=3.0)
+    tok, lp, ids, tlp = _sample(logits, gpu, temperature=0.0, num_logprobs=20)
+    lsm = torch.log_softmax(logits.float(), -1)
+    assert torch.equal(tok.long(), logits.float().argmax(-1))
+    _close(lp, lsm.gather(1, tok.long()[:, None])[:, 0], 2e-3, 1e-3)
+    ref_lp, ref_ids = lsm.topk(20, dim=-1)
+    _close(tlp, ref_lp, 2e-3, 1e-3)
+    # ids equal up to ties
+    _close(lsm.gather(1, ids.long()), ref_lp, 2e-3, 1e-3)
+
+
+def test_sample_distribution_top_p_top_k(gpu):
+    V = 4096
+    B = 4096  # many rows of the same logits, different seeds -> empirical distribution
+    base = torch.full((V,), -20.0, device=gpu)
+    base[:6] = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5], device=gpu)
+    logits = base.to(torch.bfloat16).expand(B, V)
+    p = torch.softmax(base.to(torch.bfloat16).float(), -1)
+    for kw, keep in [({}, 6), ({"top_p": 0.8}, None), ({"top_k": 3}, 3), ({"min_p": 0.3}, None)]:
+        tok, *_ = _sample(logits, gpu, **kw)
+        cnt = torch.bincount(tok.long(), minlength=V).float() / B
+        if "top_p" in kw:
+            cum = p[:6].cumsum(0)
+            keep = int((cum < kw["top_p"]).sum().item()) + 1
+        if "min_p" in kw:
+            keep = int((p[:6] >= kw["min_p"] * p[0]).sum().item())
+        q = p[:keep] / p[:keep].sum()
+        assert cnt[keep:].sum().item() == 0.0, kw
+        assert (cnt[:keep] - q).abs().max().item() < 0.04, (kw, cnt[:keep], q)
+
+
+def test_sample_bias_mask_penalty(gpu):
+    V = 4096
+    B = 3
+    logits = torch.zeros(B, V, device=gpu, dtype=torch.bfloat16)
+    bias = torch.zeros(2, V, device=gpu)
+    bias[0, 123] = 100.0
+    bias[1, 7] = 100.0
+    tok, *_ = _sample(logits, gpu, bias=bias, bias_rows=torch.tensor([0, 1, -1], dtype=torch.int32, device=gpu))
+    assert tok[0].item() == 123 and tok[1].item() == 7
+    mask = torch.zeros(1, V // 32, dtype=torch.int32, device=gpu)
+    mask[0, 3] = 1 << 5  # only token 3*32+5 = 101 allowed
+    tok, *_ = _sample(logits, gpu, mask=mask, mask_rows=torch.tensor([0, 0, -1], dtype=torch.int32, device=gpu))
+    assert tok[0].item() == 101 and tok[1].item() == 101
+    # repetition penalty pushes a dominant, already-generated token down
+    lg = torch.zeros(1, V, device=gpu, dtype=torch.bfloat16)
+    lg[0, 42] = 5.0
+    counts = torch.zeros(1, V, dtype=torch.int16, device=gpu)
+    counts[0, 42] = 3
+    one = lambda v: torch.tensor([v], device=gpu, dtype=torch.float32)
+    tok, *_ = _sample(lg, gpu, temperature=0.0, counts=counts, count_rows=torch.zeros(1, dtype=torch.int32, device=gpu),
+                      freq_pen=one(2.0), pres_pen=one(0.0), rep_pen=one(1.0))
+    assert tok[0].item() != 42
+    assert counts[0, tok[0].long()].item() == 1  # the sampled token was counted
+
+
+def test_sample_reproducible(gpu):
+    logits = _bf(8, 32000, dev=gpu, scale=2.0)
+    a, *_ = _sample(logits, gpu, top_p=0.9)
+    b, *_ = _sample(logits, gpu, top_p=0.9)
+    assert torch.equal(a, b)
+    c, *_ = _sample(logits, gpu, top_p=0.9, offsets=torch.ones(8, dtype=torch.int64, device=gpu))
+    assert not torch.equal(a, c)
+
+
+def test_pool_cosine_tally(gpu):
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(3)
+    lens = [3, 9, 1, 30]
+    T, d = sum(lens), 1024
+    h = _bf(T, d, dev=gpu)
+    cu = torch.tensor([0, 3, 12, 13, 43], dtype=torch.int32, device=gpu)
+    for mode in (ops.POOL_CLS, ops.POOL_MEAN, ops.POOL_LAST):
+        of, ob = ops.pool_l2norm(h, cu, mode)
+        for i in range(4):
+            seg = h[int(cu[i]):int(cu[i + 1])].float()
+            v = seg[0] if mode == 0 else (seg.mean(0) if mode == 1 else seg[-1])
+            _close(of[i], v / v.norm(), 2e-3, 1e-2)
+    R, n = 3, 37
+    E = torch.nn.functional.normalize(torch.randn(R, n, d, device=gpu), dim=-1).to(torch.bfloat16)
+    S, cen, w, best = ops.cosine_consensus(E, tau=0.1)
+    Sr = E.float() @ E.float().transpose(1, 2)
+    _close(S, Sr, 2e-3, 1e-2)
+    cr = (Sr.sum(-1) - Sr.diagonal(dim1=1, dim2=2)) / (n - 1)
+    _close(cen, cr, 2e-3, 1e-2)
+    _close(w, torch.softmax(cr / 0.1, -1), 2e-3, 2e-2)
+    assert torch.equal(best.long(), cr.argmax(-1))
+    votes = torch.rand(4, 9, 5, device=gpu)
+    votes = votes / votes.sum(-1, keepdim=True)
+    wts = torch.rand(4, 9, device=gpu)
+    cw, conf, vc = ops.vote_tally(votes, wts)
+    cw_r = torch.einsum("rlc,rl->rc", votes, wts)
+    conf_r = cw_r / cw_r.sum(-1, keepdim=True)
+    _close(cw, cw_r, 1e-5, 1e-5)
+    _close(conf, conf_r, 1e-5, 1e-5)
+    _close(vc, torch.einsum("rlc,rc->rl", votes, conf_r), 1e-5, 1e-5)
+
+
+def test_kv_block_copy(gpu):
+    from llm_weighted_consensus_amd import ops
+
+    cache = _bf(6, 10, 2 * 16 * 128, dev=gpu)
+    ref_c = cache.clone()
+    pairs = torch.tensor([[1, 4], [7, 2]], dtype=torch.int32, device=gpu)
+    ops.kv_block_copy(cache, pairs)
+    ref_c[:, 4] = ref_c[:, 1]
+    ref_c[:, 2] = ref_c[:, 7]
+    assert torch.equal(cache, ref_c)

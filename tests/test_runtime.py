@@ -1,0 +1,121 @@
+"""Host C++ runtime (CPU): paged-KV block manager and the consensus core key tree / votes / tally."""
+import math
+import random
+import re
+
+import pytest
+
+from llm_weighted_consensus_amd import _runtime as R
+
+
+def test_block_manager_fork_cow_and_free():
+    bm = R.BlockManager(8, 4)
+    bm.add_sequence(1, 6)  # 2 blocks, last partial
+    assert bm.num_free == 6 and bm.length(1) == 6
+    bm.fork(1, 2)
+    bm.fork(1, 3)
+    t1 = bm.block_table(1)
+    assert bm.block_table(2) == t1 and bm.refcount(t1[1]) == 3
+    s = bm.append_token(2)  # shared partial block -> copy-on-write
+    copies = bm.take_copies()
+    assert len(copies) == 1 and copies[0][0] == t1[1]
+    assert bm.block_table(2)[0] == t1[0] and bm.block_table(2)[1] == copies[0][1]
+    assert s == copies[0][1] * 4 + 2
+    assert bm.take_copies() == []
+    bm.append_token(2)
+    assert bm.append_cost(2) == 1  # block full -> needs a new block
+    bm.append_token(2)
+    assert len(bm.block_table(2)) == 3
+    for q in (1, 2, 3):
+        bm.free_sequence(q)
+    assert bm.num_free == 8
+
+
+def test_block_manager_exhaustion():
+    bm = R.BlockManager(2, 4)
+    bm.add_sequence(1, 8)
+    with pytest.raises(RuntimeError):
+        bm.add_sequence(2, 1)
+    with pytest.raises(RuntimeError):
+        bm.append_token(1)
+
+
+def test_prepare_decode_padding():
+    bm = R.BlockManager(16, 4)
+    bm.add_sequence(5, 3)
+    bt, ctx, slots, pos = R.prepare_decode(bm, [5], 4, 2)
+    assert bt.shape == (2, 4) and list(ctx) == [4, 1] and list(pos) == [3, 0] and slots[1] == -1
+    assert slots[0] == bm.slot(5, 3)
+
+
+def _ref_tree_keys(n, m):
+    """Python oracle of the reference SelectPfxTree shape (client.rs:1469-1517): multiset of key depths."""
+    def rec(length, force):
+        if not force and length <= m:
+            return [1] * length
+        k = (length + m - 1) // m
+        k = min(k, m)
+        base, extra = divmod(length, k)
+        fs = base + (1 if extra else 0) > m
+        out = []
+        for i in range(k):
+            out += [d + 1 for d in rec(base + (1 if i < extra else 0), fs)]
+        return out
+    return sorted(rec(n, False))
+
+
+@pytest.mark.parametrize("n,m", [(2, 20), (5, 20), (20, 20), (21, 20), (45, 5), (400, 20), (9, 2), (130, 3)])
+def test_key_tree_shape_matches_reference(n, m):
+    t = R.KeyTree(n, m, 7)
+    keys = t.keys
+    assert sorted(i for _, i in keys) == list(range(n))
+    assert len({k for k, _ in keys}) == n
+    for k, _ in keys:
+        assert re.fullmatch(r"(`[A-T]`)+", k)
+    assert sorted(k.count("`") // 2 for k, _ in keys) == _ref_tree_keys(n, m)
+
+
+def test_key_tree_vote_one_hot_and_last_match():
+    t = R.KeyTree(4, 20, 3)
+    (k0, i0), (k1, i1) = t.keys[0], t.keys[1]
+    v = t.vote(f"first {k0} then finally {k1}")
+    assert v[i1] == 1.0 and sum(v) == 1.0
+    bare = k0.strip("`")
+    v2 = t.vote(f"I choose {bare}.")
+    assert v2[i0] == 1.0
+    assert t.vote("no key here at all 123") is None
+
+
+def test_key_tree_vote_logprobs():
+    t = R.KeyTree(3, 3, 11)
+    (k0, i0), (k1, i1), (k2, i2) = t.keys
+    l0, l1, l2 = k0[1], k1[1], k2[1]
+    content = f"{k0}"
+    # tokens: "`", letter, "`" with top alternatives at the letter position
+    lp = [("`", [("`", 0.0)]),
+          (l0, [(l0, math.log(0.6)), (l1, math.log(0.3)), ("x", math.log(0.05)), (l2, float("nan"))]),
+          ("`", [("`", 0.0)])]
+    v = t.vote(content, lp)
+    assert abs(v[i0] - 0.6 / 0.9) < 1e-12 and abs(v[i1] - 0.3 / 0.9) < 1e-12 and v[i2] == 0.0
+    # multi-char token carrying the letter at byte offset 1
+    lp2 = [(f"`{l0}", [(f"`{l0}", math.log(0.5)), (f"`{l2}", math.log(0.5))]), ("`", [("`", 0.0)])]
+    v2 = t.vote(content, lp2)
+    assert abs(v2[i0] - 0.5) < 1e-12 and abs(v2[i2] - 0.5) < 1e-12
+    # no sibling letter among the alternatives -> one-hot fallback (reference: unreachable!())
+    lp3 = [("`", []), (l0, [("zz", 0.0)]), ("`", [])]
+    v3 = t.vote(content, lp3)
+    assert v3[i0] == 1.0
+
+
+def test_tally_and_error_codes():
+    r = R.tally([[0.5, 0.5, 0.0], [], [0.0, 1.0, 0.0]], [2.0, 5.0, 1.0], 3)
+    assert r.choice_weight == [1.0, 2.0, 0.0]
+    assert r.confidence == pytest.approx([1 / 3, 2 / 3, 0.0])
+    assert math.isnan(r.voter_confidence[1])
+    assert r.voter_confidence[2] == pytest.approx(2 / 3)
+    z = R.tally([[], []], [1.0, 1.0], 2)
+    assert z.confidence == [0.0, 0.0]
+    assert R.unify_error_codes([]) is None
+    assert R.unify_error_codes([429, 429]) == 429
+    assert R.unify_error_codes([429, 404]) == 400
+    assert R.unify_error_codes([404, 500]) == 500
