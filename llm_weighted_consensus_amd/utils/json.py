@@ -1,0 +1,148 @@
+"""serde_json-compatible JSON text.
+
+The reference serialises with serde_json (`preserve_order`, compact by default, `to_string_pretty` for
+the choice map shown to voters: src/score/completions/client.rs:1580-1603) and formats f64 with ryu
+(rust_decimal `serde-float` goes through f64 too, Cargo.toml:28).  Python's json differs only in float
+text (``1e-07`` vs ``1e-7``, ``1e+16`` vs ``1e16``, ``1e-05`` vs ``0.00001``) — which matters because
+model ids are hashes of the JSON text (src/score/llm/mod.rs:513-522).  String escaping of
+``json.dumps(ensure_ascii=False)`` already equals serde_json's (``\\"``, ``\\\\``, ``\\b\\f\\n\\r\\t``,
+other C0 controls as lowercase ``\\u00xx``).
+"""
+from __future__ import annotations
+
+import json as _json
+import math
+from typing import Any
+
+_enc_str = _json.encoder.py_encode_basestring  # ensure_ascii=False escaping (== serde_json)
+try:  # the C accelerator has identical output
+    from _json import encode_basestring as _enc_str  # type: ignore  # noqa: F811
+except Exception:  # pragma: no cover
+    pass
+
+
+def ryu_f64(x: float) -> str:
+    """Format an f64 exactly like serde_json/ryu (shortest round-trip digits, ryu layout)."""
+    if math.isnan(x) or math.isinf(x):
+        return "null"  # serde_json writes non-finite floats as null
+    if x == 0.0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    r = repr(x)
+    sign = ""
+    if r[0] == "-":
+        sign, r = "-", r[1:]
+    if "e" in r:
+        mant, e = r.split("e")
+        e = int(e)
+    else:
+        mant, e = r, 0
+    if "." in mant:
+        ip, fp = mant.split(".")
+    else:
+        ip, fp = mant, ""
+    if fp == "0":
+        fp = ""
+    digits = (ip + fp).lstrip("0")
+    k = e - len(fp)  # value = int(ip+fp) * 10^k
+    # strip trailing zeros into the exponent (shortest digits)
+    stripped = digits.rstrip("0")
+    k += len(digits) - len(stripped)
+    d = stripped or "0"
+    length = len(d)
+    kk = length + k
+    if 0 <= k and kk <= 16:
+        s = d + "0" * k + ".0"
+    elif 0 < kk <= 16:
+        s = d[:kk] + "." + d[kk:]
+    elif -5 < kk <= 0:
+        s = "0." + "0" * (-kk) + d
+    elif length == 1:
+        s = d + "e" + str(kk - 1)
+    else:
+        s = d[0] + "." + d[1:] + "e" + str(kk - 1)
+    return sign + s
+
+
+def _enc(v: Any, out: list) -> None:
+    if v is None:
+        out.append("null")
+    elif v is True:
+        out.append("true")
+    elif v is False:
+        out.append("false")
+    elif isinstance(v, str):
+        out.append(_enc_str(v))
+    elif isinstance(v, int):
+        out.append(str(v))
+    elif isinstance(v, float):
+        out.append(ryu_f64(v))
+    elif isinstance(v, dict):
+        out.append("{")
+        first = True
+        for k, x in v.items():
+            if not first:
+                out.append(",")
+            first = False
+            out.append(_enc_str(str(k)))
+            out.append(":")
+            _enc(x, out)
+        out.append("}")
+    elif isinstance(v, (list, tuple)):
+        out.append("[")
+        for i, x in enumerate(v):
+            if i:
+                out.append(",")
+            _enc(x, out)
+        out.append("]")
+    elif hasattr(v, "to_obj"):
+        _enc(v.to_obj(), out)
+    else:
+        raise TypeError(f"not JSON serialisable: {type(v)!r}")
+
+
+def dumps(v: Any) -> str:
+    """Compact serde_json text (serde_json::to_string)."""
+    out: list = []
+    _enc(v, out)
+    return "".join(out)
+
+
+def _enc_pretty(v: Any, out: list, ind: int) -> None:
+    if isinstance(v, dict):
+        if not v:
+            out.append("{}")
+            return
+        out.append("{\n")
+        items = list(v.items())
+        for i, (k, x) in enumerate(items):
+            out.append("  " * (ind + 1))
+            out.append(_enc_str(str(k)))
+            out.append(": ")
+            _enc_pretty(x, out, ind + 1)
+            out.append(",\n" if i + 1 < len(items) else "\n")
+        out.append("  " * ind + "}")
+    elif isinstance(v, (list, tuple)):
+        if not v:
+            out.append("[]")
+            return
+        out.append("[\n")
+        for i, x in enumerate(v):
+            out.append("  " * (ind + 1))
+            _enc_pretty(x, out, ind + 1)
+            out.append(",\n" if i + 1 < len(v) else "\n")
+        out.append("  " * ind + "]")
+    elif hasattr(v, "to_obj"):
+        _enc_pretty(v.to_obj(), out, ind)
+    else:
+        _enc(v, out)
+
+
+def dumps_pretty(v: Any) -> str:
+    """serde_json::to_string_pretty (two-space indent, ": " separators)."""
+    out: list = []
+    _enc_pretty(v, out, 0)
+    return "".join(out)
+
+
+def loads(s: str) -> Any:
+    return _json.loads(s)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a short bench run (no PMC counters here; those go in their own run).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/prof
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1"}
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python3 bench.py $ARGS > gpurun_out/prof_bench.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; tail -5 gpurun_out/prof_bench.log
+find gpurun_out/prof -name "*stats*" | head
+exit $rc
