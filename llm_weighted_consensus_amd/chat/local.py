@@ -1,0 +1,203 @@
+"""LocalChatClient: OpenAI-compatible chat completions served by the in-process MI355X engine.
+
+Replaces the reference's upstream HTTP round trip (src/chat/completions/client.rs:193-434) with
+`EngineService.submit`: the request's messages (archive references already resolved) are rendered
+with the model's chat template, sampled by the engine (paged KV, fused sampler), and streamed back as
+`ChatCompletionChunk`s.  Supported per request: n choices (prefix-shared), temperature/top_p/top_k/
+min_p/top_a, frequency/presence/repetition penalties, logit_bias, stop, seed, logprobs/top_logprobs,
+max_tokens/max_completion_tokens, `response_format: json_schema` and forced function `tool_choice`
+(constrained decoding), `stream_options.include_usage`.  Fallback over `models` follows the
+reference's attempt order (primary model, then each fallback) among the locally served models.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+import uuid
+from typing import Any, AsyncIterator, Dict, List, Optional
+
+from ..engine.constraints import constraint_for_schema
+from ..engine.sampling import SamplingParams
+from ..engine.service import EngineFailure, EngineService
+from ..errors import ChatError
+from ..schema import chat as C
+from ..utils import json as sjson
+from .base import ChatClient
+
+
+def render_chat_prompt(messages: List[Any], tools: Optional[List[C.Tool]] = None) -> str:
+    """Llama-3 style chat template over the resolved request messages."""
+    out = ["<|begin_of_text|>"]
+    if tools:
+        spec = sjson.dumps([t.to_obj() for t in tools])
+        out.append(f"<|start_header_id|>system<|end_header_id|>\n\nAvailable tools: {spec}<|eot_id|>")
+    for m in messages:
+        role = m.role
+        if isinstance(m, (C.SystemMessage, C.DeveloperMessage)):
+            body = C.simple_content_text(m.content)
+        elif isinstance(m, (C.UserMessage, C.ToolMessage)):
+            body = C.rich_content_text(m.content)
+        elif isinstance(m, C.AssistantMessage):
+            body = C.rich_content_text(m.content) if m.content is not None else ""
+            if m.refusal:
+                body += m.refusal
+            if m.tool_calls:
+                body += "".join(tc.template() for tc in m.tool_calls)
+        else:  # unresolved completion references never reach the engine
+            continue
+        out.append(f"<|start_header_id|>{role}<|end_header_id|>\n\n{body}<|eot_id|>")
+    out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    return "".join(out)
+
+
+class LocalChatClient(ChatClient):
+    def __init__(self, services: Dict[str, EngineService], default_max_tokens: int = 512,
+                 fallback: Optional[ChatClient] = None, archive=None):
+        self.services = services
+        self.default_max_tokens = default_max_tokens
+        self.fallback = fallback
+        self.archive = archive
+
+    def serves(self, model: str) -> bool:
+        return model in self.services
+
+    def _pick(self, req: C.ChatCompletionCreateParams) -> Optional[str]:
+        for m in [req.model] + list(req.models or []):
+            if m in self.services:
+                return m
+        return None
+
+    def sampling_params(self, req: C.ChatCompletionCreateParams, svc: EngineService, prompt_len: int):
+        tok = svc.engine.tokenizer
+        V = svc.engine.cfg.vocab_size
+        max_new = req.max_completion_tokens or req.max_tokens or self.default_max_tokens
+        max_new = max(1, min(max_new, svc.engine.max_model_len - prompt_len))
+        stop = [req.stop] if isinstance(req.stop, str) else list(req.stop or [])
+        bias = None
+        if req.logit_bias:
+            bias = {}
+            for k, v in req.logit_bias.items():
+                if not k.isdigit() or int(k) >= V:
+                    raise ChatError.invalid_request(f"logit_bias token out of range: {k}")
+                bias[int(k)] = float(v)
+        constraint, tool_name = None, None
+        rf = req.response_format
+        if isinstance(rf, C.ResponseFormatJsonSchema) and rf.json_schema.schema_ is not None:
+            constraint = constraint_for_schema(rf.json_schema.schema_, tok.eos_token_id)
+        tc = req.tool_choice
+        if isinstance(tc, C.ToolChoiceFunction) and req.tools:
+            tool = next((t for t in req.tools if t.function.name == tc.function.name), None)
+            if tool is None:
+                raise ChatError.invalid_request(f"tool_choice names an unknown function: {tc.function.name}")
+            tool_name = tool.function.name
+            if tool.function.parameters is not None:
+                constraint = constraint_for_schema(tool.function.parameters, tok.eos_token_id)
+        top_lp = int(req.top_logprobs or 0) if req.logprobs else 0
+        return SamplingParams(
+            temperature=1.0 if req.temperature is None else float(req.temperature),
+            top_p=1.0 if req.top_p is None else float(req.top_p),
+            top_k=int(req.top_k or 0), min_p=float(req.min_p or 0.0), top_a=float(req.top_a or 0.0),
+            frequency_penalty=float(req.frequency_penalty or 0.0), presence_penalty=float(req.presence_penalty or 0.0),
+            repetition_penalty=1.0 if req.repetition_penalty is None else float(req.repetition_penalty),
+            max_tokens=max_new, stop=stop, logprobs=bool(req.logprobs), top_logprobs=top_lp, seed=req.seed,
+            logit_bias=bias, constraint=constraint), tool_name
+
+    async def create_streaming(self, ctx: Any, request: C.ChatCompletionCreateParams) -> AsyncIterator[C.ChatCompletionChunk]:
+        if self.archive is not None:
+            from ..archive.resolve import fetch_completions_from_messages, replace_completion_messages
+
+            comps = await fetch_completions_from_messages(self.archive, ctx, request.messages)
+            request = request.model_copy()
+            request.messages = list(request.messages)
+            replace_completion_messages(comps, request.messages)
+        name = self._pick(request)
+        if name is None:
+            if self.fallback is not None:
+                return await self.fallback.create_streaming(ctx, request)
+            raise ChatError.model_not_found(request.model)
+        svc = self.services[name]
+        tok = svc.engine.tokenizer
+        prompt = render_chat_prompt(request.messages, request.tools)
+        ids = tok.encode(prompt, add_bos=True)
+        if len(ids) >= svc.engine.max_model_len:
+            raise ChatError.invalid_request(f"prompt of {len(ids)} tokens exceeds the model context "
+                                            f"({svc.engine.max_model_len})")
+        try:
+            sp, tool_name = self.sampling_params(request, svc, len(ids))
+        except ValueError as e:
+            raise ChatError.invalid_request(str(e))
+        n = int(request.n or 1)
+        if n < 1 or n > 128:
+            raise ChatError.invalid_request(f"n must be between 1 and 128: {n}")
+        include_usage = bool(request.stream_options and request.stream_options.include_usage) or not request.stream
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        try:
+            group = svc.submit(ids, sp, n, loop, q)
+        except ValueError as e:
+            raise ChatError.invalid_request(str(e))
+        cid = f"chatcmpl-{uuid.uuid4().hex}"
+        created = int(time.time())
+        return self._stream(svc, group, q, cid, created, name, len(ids), n, sp, tool_name, include_usage, tok)
+
+    async def _stream(self, svc, group, q, cid, created, model, prompt_len, n, sp, tool_name, include_usage, tok):
+        started = [False] * n
+        remaining = n
+        completion_tokens = 0
+        try:
+            while remaining > 0:
+                evs = [await q.get()]
+                while not q.empty():
+                    evs.append(q.get_nowait())
+                choices: Dict[int, C.StreamChoice] = {}
+                for ev in evs:
+                    if isinstance(ev, EngineFailure):
+                        raise ChatError.engine(ev.message)
+                    i = ev.seq.index
+                    completion_tokens += 1
+                    ch = choices.get(i)
+                    if ch is None:
+                        ch = C.StreamChoice(delta=C.Delta(), index=i)
+                        choices[i] = ch
+                    d = ch.delta
+                    if not started[i]:
+                        d.role = "assistant"
+                    if tool_name is not None:
+                        fn = C.StreamToolCallFunction(arguments=ev.text)
+                        if not started[i]:
+                            fn.name = tool_name
+                        tc = C.StreamToolCall(index=0, function=fn)
+                        if not started[i]:
+                            tc.id, tc.type = f"call_{uuid.uuid4().hex[:24]}", "function"
+                        if d.tool_calls is None:
+                            d.tool_calls = [tc]
+                        else:
+                            d.tool_calls[0].push(tc)
+                    else:
+                        d.content = (d.content or "") + ev.text
+                    started[i] = True
+                    if sp.logprobs:
+                        lp = C.Logprob(token=tok.token_str(ev.token_id), bytes=list(tok.token_bytes(ev.token_id)),
+                                       logprob=ev.logprob,
+                                       top_logprobs=[C.TopLogprob(token=tok.token_str(t), bytes=list(tok.token_bytes(t)),
+                                                                  logprob=l) for t, l in ev.top_logprobs])
+                        if ch.logprobs is None:
+                            ch.logprobs = C.Logprobs(content=[lp])
+                        else:
+                            ch.logprobs.content.append(lp)
+                    if ev.finished:
+                        remaining -= 1
+                        reason = ev.finish_reason
+                        if reason == "abort":
+                            reason = "error"
+                        ch.finish_reason = "tool_calls" if (tool_name is not None and reason == "stop") else reason
+                chunk = C.ChatCompletionChunk(id=cid, choices=[choices[k] for k in sorted(choices)], created=created,
+                                              model=model, provider="local")
+                if remaining == 0 and include_usage:
+                    chunk.usage = C.Usage(completion_tokens=completion_tokens, prompt_tokens=prompt_len,
+                                          total_tokens=prompt_len + completion_tokens, cost=0.0)
+                    chunk.with_total_cost()
+                yield chunk
+        finally:
+            if remaining > 0:
+                svc.abort(group)

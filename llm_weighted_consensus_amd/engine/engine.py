@@ -414,3 +414,36 @@ class LLMEngine:
             if g.bias_row >= 0:
                 self.free_bias_rows.append(g.bias_row)
                 g.bias_row = -1
+
+    # ------------------------------------------------------------------ cancellation / failure
+    def abort(self, g: SequenceGroup) -> None:
+        """Drop a group (client went away): frees its blocks and reservation, no more events."""
+        with self.lock:
+            if g in self.waiting:
+                self.waiting.remove(g)
+                for s in g.seqs:
+                    s.finished, s.finish_reason = True, "abort"
+                return
+        for s in g.seqs:
+            if not s.finished:
+                self._finish(s, "abort")
+        self.running = [s for s in self.running if not s.finished]
+
+    def fail_all(self, msg: str) -> List[SequenceGroup]:
+        """After an engine exception: finish every in-flight group and return them."""
+        groups = {}
+        with self.lock:
+            for g in self.waiting:
+                groups[g.id] = g
+            self.waiting.clear()
+        for s in self.running:
+            groups[s.group.id] = s.group
+        for g in groups.values():
+            for s in g.seqs:
+                if not s.finished:
+                    try:
+                        self._finish(s, "error")
+                    except Exception:  # pragma: no cover - best effort cleanup
+                        s.finished = True
+        self.running = []
+        return list(groups.values())

@@ -1,0 +1,110 @@
+"""Server configuration from the environment (+ optional `.env`).
+
+Every variable of the reference (src/main.rs:3-37) keeps its name and default; the remote provider
+bases are OPTIONAL here (they become the fallback tier behind the local MI355X engine).  New
+variables configure the local engine:
+
+  LWC_MODELS        JSON {name: {"arch": "llama-3-8b", "weights": "random:<seed>" | <path>,
+                          "max_model_len": 4096, "max_batch": 512}}   (default: none)
+  LWC_EMBED_MODELS  JSON {name: {"arch": "bge-large-en-v1.5", "weights": "random:<seed>" | <path>}}
+  LWC_GPU           device index for this process's engine (one process per GPU)
+  LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)
+  LWC_ARCHIVE_PATH  append-only JSONL log of completions (checkpoint/resume of the archive)
+  LWC_REGISTRY_PATH JSON file persisting registered score models
+  LWC_FAULT         fault injection for tests: worker_crash | slow_decode | bad_logprobs
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+
+def _load_dotenv(path: str = ".env") -> None:
+    if not os.path.exists(path):
+        return
+    with open(path, "r", encoding="utf-8") as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#") or "=" not in line:
+                continue
+            k, v = line.split("=", 1)
+            os.environ.setdefault(k.strip(), v.strip().strip('"').strip("'"))
+
+
+@dataclass
+class Config:
+    backoff_current_interval_millis: int = 100
+    backoff_initial_interval_millis: int = 100
+    backoff_randomization_factor: float = 0.5
+    backoff_multiplier: float = 1.5
+    backoff_max_interval_millis: int = 1000
+    backoff_max_elapsed_time_millis: int = 40000
+    first_chunk_timeout_millis: int = 10000
+    other_chunk_timeout_millis: int = 60000
+    openai_api_base: Optional[str] = None
+    openai_api_key: Optional[str] = None
+    openai_apis: Optional[str] = None
+    openai_user_agent: Optional[str] = None
+    openai_x_title: Optional[str] = None
+    openai_referer: Optional[str] = None
+    address: str = "0.0.0.0"
+    port: int = 5000
+    # local engine
+    models: Dict[str, dict] = field(default_factory=dict)
+    embed_models: Dict[str, dict] = field(default_factory=dict)
+    gpu: int = 0
+    kv_fraction: float = 0.85
+    archive_path: Optional[str] = None
+    registry_path: Optional[str] = None
+    fault: Optional[str] = None
+
+    @classmethod
+    def from_env(cls, dotenv: bool = True) -> "Config":
+        if dotenv:
+            _load_dotenv()
+        e = os.environ
+        c = cls()
+        ints = ["backoff_current_interval_millis", "backoff_initial_interval_millis", "backoff_max_interval_millis",
+                "backoff_max_elapsed_time_millis", "first_chunk_timeout_millis", "other_chunk_timeout_millis", "port"]
+        floats = ["backoff_randomization_factor", "backoff_multiplier"]
+        strs = ["openai_api_base", "openai_api_key", "openai_apis", "openai_user_agent", "openai_x_title",
+                "openai_referer", "address"]
+        for k in ints:
+            if k.upper() in e:
+                setattr(c, k, int(e[k.upper()]))
+        for k in floats:
+            if k.upper() in e:
+                setattr(c, k, float(e[k.upper()]))
+        for k in strs:
+            if k.upper() in e:
+                setattr(c, k, e[k.upper()])
+        if "LWC_MODELS" in e:
+            c.models = json.loads(e["LWC_MODELS"])
+        if "LWC_EMBED_MODELS" in e:
+            c.embed_models = json.loads(e["LWC_EMBED_MODELS"])
+        c.gpu = int(e.get("LWC_GPU", e.get("LOCAL_RANK", "0")))
+        c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))
+        c.archive_path = e.get("LWC_ARCHIVE_PATH")
+        c.registry_path = e.get("LWC_REGISTRY_PATH")
+        c.fault = e.get("LWC_FAULT")
+        return c
+
+    def api_bases(self):
+        """Remote tier (reference main.rs:76-96); empty instead of a panic when unset."""
+        from ..chat.remote import ApiBase
+
+        if self.openai_apis:
+            return [ApiBase(**x) for x in json.loads(self.openai_apis)]
+        if self.openai_api_base and self.openai_api_key:
+            return [ApiBase(self.openai_api_base, self.openai_api_key)]
+        return []
+
+    def backoff(self):
+        from ..chat.remote import Backoff
+
+        return Backoff(initial_interval=self.backoff_initial_interval_millis / 1000.0,
+                       randomization_factor=self.backoff_randomization_factor, multiplier=self.backoff_multiplier,
+                       max_interval=self.backoff_max_interval_millis / 1000.0,
+                       max_elapsed=self.backoff_max_elapsed_time_millis / 1000.0)

@@ -1,0 +1,92 @@
+"""Boot: config -> engines (one per configured model on this process's GPU) -> clients -> ASGI app.
+
+Mirrors the reference bring-up (src/main.rs:51-140): env config, archive, chat client, score client
+(model fetcher = registry, weight fetchers = static + training table), router, bind ADDRESS:PORT.
+Run one process per GPU (`LWC_GPU` / `LOCAL_RANK`) behind any HTTP load balancer.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ..archive.store import CompletionsArchive
+from ..chat.remote import RemoteChatClient, RoutingChatClient
+from ..score.multichat import ConsensusClient, MultichatClient
+from ..score.orchestrator import ScoreClient
+from ..score.registry import ModelRegistry
+from ..score.weights import TrainingTableWeights, WeightFetchers
+from .app import AppState, create_app
+from .config import Config
+
+
+def _weights_spec(spec: dict):
+    w = spec.get("weights", "random:0")
+    if isinstance(w, str) and w.startswith("random:"):
+        return None, int(w.split(":", 1)[1])
+    return w, 0
+
+
+def build_state(cfg: Config, chat_client=None) -> AppState:
+    archive = CompletionsArchive(path=cfg.archive_path)
+    registry = ModelRegistry(cfg.registry_path)
+    services, embedders = {}, {}
+    if cfg.models or cfg.embed_models:
+        import torch
+
+        from ..engine.engine import LLMEngine
+        from ..engine.service import EngineService
+        from ..engine.tokenizer import ByteTokenizer
+        from ..embeddings.service import EmbeddingService
+        from ..models.bert import BertEncoder
+        from ..models.config import decoder_config, encoder_config
+        from ..models.llama import LlamaModel
+
+        dev = torch.device("cuda", cfg.gpu)
+        torch.cuda.set_device(dev)
+        for name, spec in cfg.embed_models.items():
+            path, seed = _weights_spec(spec)
+            enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path)
+            embedders[name] = EmbeddingService(enc, name)
+        for name, spec in cfg.models.items():
+            path, seed = _weights_spec(spec)
+            dcfg = decoder_config(spec["arch"])
+            mlen = int(spec.get("max_model_len", 4096))
+            model = LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
+            tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
+            eng = LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
+                            kv_memory_fraction=cfg.kv_fraction / max(1, len(cfg.models)))
+            services[name] = EngineService(eng, name)
+    remote = None
+    bases = cfg.api_bases()
+    if bases:
+        remote = RemoteChatClient(bases, backoff=cfg.backoff(), user_agent=cfg.openai_user_agent,
+                                  x_title=cfg.openai_x_title, referer=cfg.openai_referer,
+                                  first_chunk_timeout=cfg.first_chunk_timeout_millis / 1000.0,
+                                  other_chunk_timeout=cfg.other_chunk_timeout_millis / 1000.0, archive=archive)
+    if chat_client is None:
+        local = None
+        if services:
+            from ..chat.local import LocalChatClient
+
+            local = LocalChatClient(services, archive=archive)
+        chat_client = RoutingChatClient(local, remote)
+    tt_embed = None
+    if embedders:
+        first = next(iter(embedders.values()))
+        tt_embed = lambda texts, max_tokens: first.embed_texts(texts, max_tokens)  # noqa: E731
+    score = ScoreClient(chat_client, registry, WeightFetchers(training_table=TrainingTableWeights(tt_embed)),
+                        archive=archive)
+    return AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
+                                                                                          archive),
+                    embedders=embedders, services=services, archive=archive, registry=registry)
+
+
+def main(argv: Optional[list] = None) -> None:
+    import uvicorn
+
+    cfg = Config.from_env()
+    state = build_state(cfg)
+    uvicorn.run(create_app(state), host=cfg.address, port=cfg.port, log_level="info")
+
+
+if __name__ == "__main__":
+    main()
