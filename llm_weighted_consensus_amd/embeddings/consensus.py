@@ -27,6 +27,26 @@ class ConsensusResult:
     similarity: torch.Tensor        # [R, N, N]
 
 
+def consensus_reference(E: torch.Tensor, tau: float) -> ConsensusResult:
+    """fp32 torch form of K10a (CPU plumbing path and the numerics oracle)."""
+    Ef = E.float()
+    S = Ef @ Ef.transpose(1, 2)
+    n = E.shape[1]
+    cen = (S.sum(-1) - S.diagonal(dim1=1, dim2=2)) / max(1, n - 1)
+    w = torch.softmax(cen / tau, -1)
+    return ConsensusResult(cen.argmax(-1).tolist(), w, cen, S)
+
+
+def gather_candidates(E_local: torch.Tensor) -> torch.Tensor:
+    """Candidate-parallel all-gather (C1): [R, n_local, d] per rank -> [R, world*n_local, d] with rank r's
+    shard at candidates [r*n_local, (r+1)*n_local)."""
+    if not pdist.info().enabled:
+        return E_local
+    R, n_local, d = E_local.shape
+    G = pdist.all_gather(E_local)  # [W, R, n_local, d]
+    return G.permute(1, 0, 2, 3).reshape(R, -1, d).contiguous()
+
+
 class EmbeddingConsensus:
     def __init__(self, encoder, tau: float = 0.05, max_tokens: Optional[int] = None):
         self.encoder = encoder
@@ -37,9 +57,11 @@ class EmbeddingConsensus:
         return self.encoder.embed(candidates, self.max_tokens)
 
     def score_local(self, E: torch.Tensor) -> ConsensusResult:
-        """E: [R, N, d] bf16 unit rows."""
-        S, cen, w, best = ops.cosine_consensus(E, self.tau)
-        return ConsensusResult(best.tolist(), w, cen, S)
+        """E: [R, N, d] unit rows (bf16 on the GPU: the MFMA kernel; any dtype on CPU: torch math)."""
+        if E.is_cuda:
+            S, cen, w, best = ops.cosine_consensus(E, self.tau)
+            return ConsensusResult(best.tolist(), w, cen, S)
+        return consensus_reference(E, self.tau)
 
     def score(self, requests: Sequence[Sequence[Sequence[int]]], gather: bool = False) -> ConsensusResult:
         """requests[r][i] = token ids of candidate i of request r (this rank's shard when gather=True;
@@ -49,7 +71,6 @@ class EmbeddingConsensus:
         flat = [c for req in requests for c in req]
         _, eb = self.embed(flat)
         E = eb.view(R, n_local, -1)
-        if gather and pdist.info().enabled:
-            G = pdist.all_gather(E)                         # [W, R, n_local, d]
-            E = G.permute(1, 0, 2, 3).reshape(R, -1, E.shape[-1])
+        if gather:
+            E = gather_candidates(E)
         return self.score_local(E.contiguous())

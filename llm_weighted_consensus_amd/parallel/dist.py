@@ -79,9 +79,10 @@ def all_gather(t: torch.Tensor) -> torch.Tensor:
     if not _INFO.enabled:
         return t.unsqueeze(0)
     t = t.contiguous()
-    out = torch.empty((_INFO.world, *t.shape), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t)
-    return out
+    flat = t.view(-1)
+    out = torch.empty(_INFO.world * flat.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, flat)  # flat 1-D form works for RCCL and gloo alike
+    return out.view(_INFO.world, *t.shape)
 
 
 def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:

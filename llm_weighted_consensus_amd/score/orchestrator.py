@@ -91,8 +91,8 @@ class ScoreClient:
                  weight_fetchers: Optional[WeightFetchers] = None, archive=None, rng_seed: Optional[int] = None,
                  register_inline_models: bool = True):
         self.chat = chat_client
-        self.models = model_registry or ModelRegistry()
-        self.weights = weight_fetchers or WeightFetchers()
+        self.models = model_registry if model_registry is not None else ModelRegistry()
+        self.weights = weight_fetchers if weight_fetchers is not None else WeightFetchers()
         self.archive = archive
         self.rng = random.Random(rng_seed)
         self.register_inline = register_inline_models

@@ -211,7 +211,7 @@ def create_app(state: AppState) -> Starlette:
         return _json(m.to_obj())
 
     async def get_model(request: Request):
-        m = state.registry.get(request.path_params["mid"]) if state.registry else None
+        m = state.registry.get(request.path_params["mid"]) if state.registry is not None else None
         if m is None:
             return _json({"kind": "score", "error": {"kind": "model_not_found", "error": "not found"}}, 404)
         return _json(m.to_obj())

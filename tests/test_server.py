@@ -1,0 +1,127 @@
+"""HTTP contract (CPU, in-process ASGI): SSE framing, [DONE], unary JSON, error statuses/bodies,
+model registry and metrics routes (reference src/main.rs:142-239)."""
+import asyncio
+import json
+
+import httpx
+import pytest
+
+from llm_weighted_consensus_amd.chat.fake import Failure, FakeChatClient, Scripted, select_keys
+from llm_weighted_consensus_amd.errors import ChatError
+from llm_weighted_consensus_amd.server.app import create_app
+from llm_weighted_consensus_amd.server.config import Config
+from llm_weighted_consensus_amd.server.main import build_state
+
+
+def policy(req):
+    if req.model == "down":
+        return Failure(ChatError.bad_status(503, "upstream down"))
+    keys = select_keys(req)
+    if keys:
+        return [Scripted(next(k for k, v in keys if "Paris" in v))]
+    return [Scripted("hello there", usage=(5, 2)), Scripted("second", usage=(5, 1))]
+
+
+@pytest.fixture()
+def client():
+    state = build_state(Config(), chat_client=FakeChatClient(policy))
+    app = create_app(state)
+    return httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t")
+
+
+def run(c):
+    return asyncio.run(c)
+
+
+def sse_events(text):
+    assert text.endswith("data: [DONE]\n\n")
+    return [e[len("data: "):] for e in text.split("\n\n") if e]
+
+
+SCORE = {"messages": [{"role": "user", "content": "Capital of France?"}],
+         "model": {"llms": [{"model": "v1"}, {"model": "v2", "weight": {"type": "static", "weight": 2}}]},
+         "choices": ["Paris", "Madrid"]}
+
+
+def test_score_unary_and_stream(client):
+    async def go():
+        r = await client.post("/score/completions", json=SCORE)
+        assert r.status_code == 200
+        body = r.json()
+        assert body["object"] == "chat.completion" and body["weight_data"] == {"type": "static"}
+        assert body["choices"][0]["confidence"] == pytest.approx(1.0)
+        r2 = await client.post("/score/completions", json=dict(SCORE, stream=True))
+        assert r2.status_code == 200 and r2.headers["content-type"].startswith("text/event-stream")
+        ev = sse_events(r2.text)
+        assert ev[-1] == "[DONE]"
+        chunks = [json.loads(e) for e in ev[:-1]]
+        assert all(c["object"] == "chat.completion.chunk" for c in chunks)
+        assert chunks[-1]["choices"][0]["confidence"] == pytest.approx(1.0)
+        # the model id is content-addressed and now registered
+        mid = body["model"]
+        r3 = await client.get(f"/score/models/{mid}")
+        assert r3.status_code == 200 and r3.json()["id"] == mid
+        r4 = await client.post("/score/completions", json=dict(SCORE, model=mid))
+        assert r4.status_code == 200 and r4.json()["model"] == mid
+    run(go())
+
+
+def test_score_errors(client):
+    async def go():
+        r = await client.post("/score/completions", json=dict(SCORE, choices=["one"]))
+        assert r.status_code == 400
+        assert r.json() == {"kind": "score", "error": {"kind": "expected_two_or_more_choices",
+                                                      "error": "expected 2 or more provided choices but got 1"}}
+        r = await client.post("/score/completions", json=dict(SCORE, model={"llms": [{"model": "down"}]}))
+        assert r.status_code == 503  # all votes failed with one code -> that code
+        assert r.json()["error"]["kind"] == "all_votes_failed"
+        r = await client.post("/score/completions", json=dict(SCORE, model={"llms": [{"model": "down"}]}, stream=True))
+        assert r.status_code == 200
+        ev = sse_events(r.text)
+        err = json.loads(ev[-2])
+        assert err == {"code": 503, "message": {"kind": "score", "error": {
+            "kind": "all_votes_failed", "error": "all votes failed, see choices for further details"}}}
+        r = await client.post("/score/completions", content=b"{not json")
+        assert r.status_code == 400
+        r = await client.post("/score/completions", json={"messages": []})
+        assert r.status_code == 422
+    run(go())
+
+
+def test_chat_routes(client):
+    async def go():
+        req = {"model": "m", "messages": [{"role": "user", "content": "hi"}], "n": 2}
+        r = await client.post("/chat/completions", json=req)
+        assert r.status_code == 200
+        b = r.json()
+        assert [c["message"]["content"] for c in b["choices"]] == ["hello there", "second"]
+        assert b["usage"]["prompt_tokens"] == 10
+        r = await client.post("/chat/completions", json=dict(req, stream=True))
+        ev = sse_events(r.text)
+        text = "".join(json.loads(e)["choices"][0]["delta"].get("content", "") for e in ev[:-1]
+                       if json.loads(e)["choices"] and json.loads(e)["choices"][0]["index"] == 0)
+        assert text == "hello there"
+        r = await client.post("/chat/completions", json=dict(req, model="down"))
+        assert r.status_code == 503 and r.json() == {"kind": "chat", "error": {"kind": "bad_status",
+                                                                              "error": "upstream down"}}
+        # archived chat completion can be referenced as a message
+        r2 = await client.post("/chat/completions", json={"model": "m", "messages": [
+            {"role": "chat_completion", "id": b["id"], "choice_index": 1}, {"role": "user", "content": "and?"}]})
+        assert r2.status_code == 200
+    run(go())
+
+
+def test_health_metrics_and_registry(client):
+    async def go():
+        r = await client.get("/health")
+        assert r.json()["status"] == "ok"
+        r = await client.post("/score/models", json={"llms": [{"model": "a"}]})
+        assert r.status_code == 200 and len(r.json()["id"]) == 22
+        r = await client.post("/score/models", json={"llms": []})
+        assert r.status_code == 400
+        await client.post("/score/completions", json=SCORE)
+        m = await client.get("/metrics")
+        assert "lwc_score_requests_total" in m.text
+        r = await client.post("/embeddings", json={"input": "x"})
+        assert r.status_code == 404
+    run(go())
