@@ -16,7 +16,9 @@ int lwc_bias_gelu(void*, const void*, int, int, hipStream_t);
 int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
 int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
-                     int, int, int, int, int, int, float, hipStream_t);
+                     int, int, int, int, int, int, float, const int*, const float*, const float*, hipStream_t);
+int lwc_paged_decode_prefix(const void*, int, const void*, const void*, const int*, const int*, const int*, int,
+                            float*, float*, int, int, int, int, int, int, float, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
@@ -151,7 +153,8 @@ void kv_block_copy(at::Tensor& cache, const at::Tensor& pairs) {
 void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out,
                   const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_lse,
-                  int64_t num_splits, double scale) {
+                  int64_t num_splits, double scale, const c10::optional<at::Tensor>& start_blk,
+                  const c10::optional<at::Tensor>& pre_o, const c10::optional<at::Tensor>& pre_lse) {
   // q: [B, >= Hq*D] with row stride; out: [B, Hq, D]
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt);
@@ -171,10 +174,43 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     po = part_o->data_ptr<float>();
     pl = part_lse->data_ptr<float>();
   }
+  const int* sb = nullptr;
+  const float* pro = nullptr;
+  const float* prl = nullptr;
+  if (start_blk.has_value() && start_blk->defined()) {
+    CHECK_DTYPE(*start_blk, at::kInt);
+    TORCH_CHECK(start_blk->numel() >= B, "paged_decode: start_blk too short");
+    TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "paged_decode: prefix merge needs pre_o/pre_lse");
+    TORCH_CHECK(pre_o->numel() >= (int64_t)B * Hq * D && pre_lse->numel() >= (int64_t)B * Hq,
+                "paged_decode: prefix partial buffers too small");
+    sb = start_blk->data_ptr<int>();
+    pro = pre_o->data_ptr<float>();
+    prl = pre_lse->data_ptr<float>();
+  }
   CHECK_RC(lwc_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), out.data_ptr(), po, pl, B, Hq, Hkv,
-                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, cur_stream()),
+                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, sb, pro, prl,
+                            cur_stream()),
            "paged_decode");
+}
+
+void paged_decode_prefix(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                         const at::Tensor& block_tables, const at::Tensor& tiles, at::Tensor& pre_o,
+                         at::Tensor& pre_lse, int64_t Hq, double scale) {
+  // tiles: [max_tiles, 3] int32 (row_start, nseq, prefix_blocks); unused tiles are all-zero rows.
+  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(tiles, at::kInt); CHECK_CONTIG(tiles);
+  CHECK_DTYPE(pre_o, at::kFloat); CHECK_DTYPE(pre_lse, at::kFloat);
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 3, "paged_decode_prefix: tiles must be [T, 3]");
+  const int B = (int)q.size(0), D = (int)k_cache.size(3), Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
+  TORCH_CHECK(block_tables.size(0) >= B, "paged_decode_prefix: block table rows");
+  TORCH_CHECK(pre_o.numel() >= (int64_t)B * Hq * D && pre_lse.numel() >= (int64_t)B * Hq,
+              "paged_decode_prefix: prefix partial buffers too small");
+  CHECK_RC(lwc_paged_decode_prefix(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                   block_tables.data_ptr<int>(), tiles.data_ptr<int>(), nullptr, (int)tiles.size(0),
+                                   pre_o.data_ptr<float>(), pre_lse.data_ptr<float>(), B, (int)Hq, Hkv, D, BS,
+                                   (int)block_tables.size(1), (float)scale, cur_stream()),
+           "paged_decode_prefix");
 }
 
 void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
@@ -292,6 +328,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding", &embedding);
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);
+  m.def("paged_decode_prefix", &paged_decode_prefix);
   m.def("prefill_attention", &prefill_attention);
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);

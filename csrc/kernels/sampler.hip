@@ -87,6 +87,11 @@ LWC_DEVICE float key2f(uint32_t k) {
 #define GET(row, j, e) \
   (((e)&1) ? __uint_as_float((row)[j][(e) >> 1] & 0xffff0000u) : __uint_as_float((row)[j][(e) >> 1] << 16))
 
+// fp16 helpers for the probability form of the row (u in [0,1] as packed fp16)
+LWC_DEVICE uint16_t h2bits(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+#define KEYU(row, j, e) ((((e)&1) ? ((row)[j][(e) >> 1] >> 16) : ((row)[j][(e) >> 1] & 0xffffu)))
+#define GETU(row, j, e) ((float)__builtin_bit_cast(_Float16, (uint16_t)KEYU(row, j, e)))
+
 LWC_DEVICE int block_sum_i(int v, int* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -273,35 +278,45 @@ OPAQUE_ROW(row);
 #pragma unroll
       for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
     const float ymax = block_max(ym, sred);
+    // ---- one exp per element: the row becomes u_i = exp((y_i - ymax)/T) in [0, 1] as packed fp16.
+    // Non-negative fp16 bit patterns are order-preserving, so every later threshold search compares
+    // raw 16-bit keys and sums fp16 values: no transcendental inside the 16-round searches.
+OPAQUE_ROW(row);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float y0 = GET(row, j, 2 * c), y1 = GET(row, j, 2 * c + 1);
+        const float u0 = y0 > -INFINITY ? __expf((y0 - ymax) * invT) : 0.f;
+        const float u1 = y1 > -INFINITY ? __expf((y1 - ymax) * invT) : 0.f;
+        row[j][c] = (uint32_t)h2bits(u0) | ((uint32_t)h2bits(u1) << 16);
+      }
+    }
     // mass of the elements with key >= KEY (macro, not a lambda: a by-reference capture of `row`
     // makes it addressable and sends it to scratch)
-#define PR(y) __expf(((y)-ymax) * invT)
 #define MASS_GE(KEY, OUT)                                              \
   do {                                                                 \
     OPAQUE_ROW(row);                                                   \
     float _s = 0.f;                                                    \
     _Pragma("unroll") for (int j = 0; j < SLOTS; ++j) {                \
       _Pragma("unroll") for (int e = 0; e < 8; ++e) {                  \
-        const float y = GET(row, j, e);                                \
-        _s += (f2key(y) >= (KEY) && y > -INFINITY) ? PR(y) : 0.f;      \
+        _s += (KEYU(row, j, e) >= (KEY)) ? GETU(row, j, e) : 0.f;      \
       }                                                                \
-      __builtin_amdgcn_sched_barrier(0);                               \
     }                                                                  \
     OUT = block_sum(_s, sred);                                         \
   } while (0)
     uint32_t tau = 0;  // keep elements with key >= tau
     const int k = p.top_k[b];
     if (k > 0) {
-      uint32_t lo = 0, hi = 0xffffu;
+      uint32_t lo = 0, hi = 0x3C00u;  // keys of [0, 1.0]
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
-        OPAQUE_ROW(row);
         int c = 0;
 OPAQUE_ROW(row);
 #pragma unroll
         for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) c += f2key(GET(row, j, e)) >= mid;
+          for (int e = 0; e < 8; ++e) c += KEYU(row, j, e) >= mid;
         if (block_sum_i(c, sredi) >= k)
           lo = mid;
         else
@@ -316,7 +331,7 @@ OPAQUE_ROW(row);
       float mk;
       MASS_GE(tau, mk);
       const float target = tp * mk;
-      uint32_t lo = tau, hi = 0xffffu;
+      uint32_t lo = tau, hi = 0x3C00u;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         float mm;
@@ -329,27 +344,18 @@ OPAQUE_ROW(row);
       tau = lo;
     }
     const float mp = p.min_p[b];
-    if (mp > 0.f) {  // p_i >= min_p * p_max  <=>  y >= ymax + T ln(min_p)
-      const uint32_t kk = f2key(ymax + T * __logf(mp));
-      tau = max(tau, kk);
-    }
+    if (mp > 0.f) tau = max(tau, (uint32_t)h2bits(mp));        // u_i >= min_p  (u_max = 1)
     const float ta = p.top_a[b];
-    if (ta > 0.f) {  // p_i >= top_a * p_max^2, p_max = 1/Z
-      const uint32_t kk = f2key(ymax + T * __logf(ta / Z));
-      tau = max(tau, kk);
-    }
-    const uint32_t ymax_key = f2key(ymax);
-    if (tau > ymax_key) tau = ymax_key;  // never filter out the argmax
+    if (ta > 0.f) tau = max(tau, (uint32_t)h2bits(ta / Z));    // p_i >= top_a p_max^2 <=> u_i >= top_a / Z
+    if (tau > 0x3C00u) tau = 0x3C00u;                           // never filter out the argmax (u = 1)
+    if (tau == 0u) tau = 1u;                                    // zero-mass elements are never kept
     // ---- inverse-CDF draw over the kept set (order: thread-major, then slot, then element) ----
     float local = 0.f;
 OPAQUE_ROW(row);
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float y = GET(row, j, e);
-        local += (f2key(y) >= tau && y > -INFINITY) ? PR(y) : 0.f;
-      }
+      for (int e = 0; e < 8; ++e) local += (KEYU(row, j, e) >= tau) ? GETU(row, j, e) : 0.f;
     // exclusive scan of `local` over threads
     const int lane = t & 63, wid = t >> 6;
     float incl = local;
@@ -381,11 +387,10 @@ OPAQUE_ROW(row);
       for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float y = GET(row, j, e);
           const int idx = (j * kSampT + t) * 8 + e;
-          if (f2key(y) >= tau && y > -INFINITY) {
+          if (KEYU(row, j, e) >= tau) {
             last = idx;
-            acc += PR(y);
+            acc += GETU(row, j, e);
             if (found == 0x7fffffff && u < acc) found = idx;
           }
         }
@@ -410,7 +415,7 @@ OPAQUE_ROW(row);
       for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float v = GET(row, j, e);
+          const float v = GETU(row, j, e);
           const int idx = (j * kSampT + t) * 8 + e;
           if (idx < p.V && (v > bv || (v == bv && idx < bi))) {
             bv = v;

@@ -89,17 +89,18 @@ class SequenceGroup:
 
 
 class _GraphBucket:
-    def __init__(self, B: int, width: int, splits: int):
-        self.B, self.width, self.splits = B, width, splits
+    def __init__(self, B: int, width: int, splits: int, max_tiles: int):
+        self.B, self.width, self.splits, self.max_tiles = B, width, splits, max_tiles
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.tokens = self.positions = self.slots = self.block_tables = self.ctx_lens = None
+        self.tiles = self.start_blk = None
         self.logits: Optional[torch.Tensor] = None
 
 
 class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
-                 use_graphs: bool = True, prefill_token_budget: int = 16384):
+                 use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -117,6 +118,7 @@ class LLMEngine:
         self.bm = BlockManager(num_blocks, block_size)
         self.free_blocks_unreserved = num_blocks
         self.use_graphs = use_graphs
+        self.prefix_sharing = prefix_sharing
         self.buckets: Dict[int, _GraphBucket] = {}
         self.waiting: Deque[SequenceGroup] = deque()
         self.running: List[Sequence] = []
@@ -257,11 +259,36 @@ class LLMEngine:
             # split-K so that a launch has >= ~1024 (batch, kv-head, split) workgroups
             splits = max(1, min(16, -(-1024 // (Bb * self.cfg.kv_heads))))
             splits = min(splits, max(1, self.width // 4))
-            bk = _GraphBucket(Bb, self.width, splits)
+            per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
+            bk = _GraphBucket(Bb, self.width, splits, -(-Bb // per))
             self.buckets[Bb] = bk
         return bk
 
-    def _run_decode(self, bk: _GraphBucket, bt, ctx, slots, pos, tokens) -> torch.Tensor:
+    def _prefix_plan(self, seqs: List[Sequence], bk: _GraphBucket):
+        """Tiles for the prefix-shared attention pass: runs of consecutive sequences of one group
+        (forked from one prompt) share the prompt's full blocks; each tile packs <= 16/G of them."""
+        tiles = np.zeros((bk.max_tiles, 3), dtype=np.int32)
+        start = np.zeros(bk.B, dtype=np.int32)
+        per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
+        nt, i, B = 0, 0, len(seqs)
+        while i < B:
+            g = seqs[i].group
+            j = i
+            while j < B and seqs[j].group is g:
+                j += 1
+            pblk = len(g.prompt_ids) // self.block_size
+            if j - i >= 2 and pblk > 0:
+                for r0 in range(i, j, per):
+                    n = min(per, j - r0)
+                    if nt >= bk.max_tiles:
+                        raise RuntimeError("prefix plan: tile overflow")
+                    tiles[nt] = (r0, n, pblk)
+                    nt += 1
+                start[i:j] = pblk
+            i = j
+        return tiles, start
+
+    def _run_decode(self, bk: _GraphBucket, bt, ctx, slots, pos, tokens, prefix=None) -> torch.Tensor:
         dev = self.device
         if bk.tokens is None:
             bk.tokens = torch.zeros(bk.B, dtype=torch.int32, device=dev)
@@ -269,15 +296,22 @@ class LLMEngine:
             bk.slots = torch.full((bk.B,), -1, dtype=torch.int32, device=dev)
             bk.block_tables = torch.zeros(bk.B, bk.width, dtype=torch.int32, device=dev)
             bk.ctx_lens = torch.ones(bk.B, dtype=torch.int32, device=dev)
+            if self.prefix_sharing:
+                bk.tiles = torch.zeros(bk.max_tiles, 3, dtype=torch.int32, device=dev)
+                bk.start_blk = torch.zeros(bk.B, dtype=torch.int32, device=dev)
         bk.tokens.copy_(tokens, non_blocking=True)
         bk.positions.copy_(pos, non_blocking=True)
         bk.slots.copy_(slots, non_blocking=True)
         bk.block_tables.copy_(bt, non_blocking=True)
         bk.ctx_lens.copy_(ctx, non_blocking=True)
+        if self.prefix_sharing:
+            bk.tiles.copy_(prefix[0], non_blocking=True)
+            bk.start_blk.copy_(prefix[1], non_blocking=True)
 
         def fwd():
             return self.model.decode(bk.tokens, bk.positions, bk.slots, bk.block_tables, bk.ctx_lens, self.cache,
-                                     num_splits=bk.splits)
+                                     num_splits=bk.splits,
+                                     prefix=(bk.tiles, bk.start_blk) if self.prefix_sharing else None)
 
         if not self.use_graphs:
             return fwd()
@@ -305,7 +339,11 @@ class LLMEngine:
         last = np.zeros(bk.B, dtype=np.int32)
         last[:B] = [s.tokens[-1] for s in seqs]
         pin = lambda a: torch.from_numpy(a).pin_memory()
-        logits = self._run_decode(bk, pin(bt), pin(ctx), pin(slots), pin(pos), pin(last))
+        prefix = None
+        if self.prefix_sharing:
+            tiles, start = self._prefix_plan(seqs, bk)
+            prefix = (pin(tiles), pin(start))
+        logits = self._run_decode(bk, pin(bt), pin(ctx), pin(slots), pin(pos), pin(last), prefix)
         self.stats["decode_tokens"] += B
         self.stats["steps"] += 1
         events = self._sample_and_advance(logits[:B], seqs)

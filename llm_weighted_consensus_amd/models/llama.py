@@ -176,9 +176,10 @@ class LlamaModel:
         return h
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
-               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1) -> torch.Tensor:
+               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None) -> torch.Tensor:
         """One decode step for B sequences -> logits [B, V] bf16.  All inputs are device tensors
-        (int32), so the whole call can be captured in a hipGraph."""
+        (int32), so the whole call can be captured in a hipGraph.  ``prefix`` = (tiles, start_blk)
+        enables the prefix-shared attention pass for sequences forked from one prompt."""
         cfg = self.cfg
         x = ops.embedding(self.embed, tokens)
         B = tokens.shape[0]
@@ -186,10 +187,19 @@ class LlamaModel:
         if num_splits > 1:
             part_o = torch.empty(B * cfg.heads * num_splits * cfg.head_dim, dtype=torch.float32, device=x.device)
             part_lse = torch.empty(B * cfg.heads * num_splits, dtype=torch.float32, device=x.device)
+        tiles = start_blk = pre_o = pre_lse = None
+        if prefix is not None:
+            tiles, start_blk = prefix
+            pre_o = torch.empty(B * cfg.heads * cfg.head_dim, dtype=torch.float32, device=x.device)
+            pre_lse = torch.empty(B * cfg.heads, dtype=torch.float32, device=x.device)
 
         def attn_fn(qkv, li):
+            if tiles is not None:
+                ops.paged_decode_prefix(qkv, cache.k[li], cache.v[li], block_tables, tiles, pre_o, pre_lse, cfg.heads,
+                                        self.scale)
             return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
-                                    num_splits=num_splits, part_o=part_o, part_lse=part_lse)
+                                    num_splits=num_splits, part_o=part_o, part_lse=part_lse, start_blk=start_blk,
+                                    pre_o=pre_o, pre_lse=pre_lse)
 
         h = self._layers(x, cache, positions, slots, attn_fn)
         return F.linear(h, self.lm_head)

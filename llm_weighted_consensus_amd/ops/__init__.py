@@ -110,8 +110,11 @@ def kv_block_copy(cache: torch.Tensor, pairs: torch.Tensor) -> None:
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  ctx_lens: torch.Tensor, Hq: int, scale: float, num_splits: int = 1,
                  out: Optional[torch.Tensor] = None, part_o: Optional[torch.Tensor] = None,
-                 part_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """One-token paged GQA decode attention (K3).  q: [B, >=Hq*D] (row stride allowed)."""
+                 part_lse: Optional[torch.Tensor] = None, start_blk: Optional[torch.Tensor] = None,
+                 pre_o: Optional[torch.Tensor] = None, pre_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One-token paged GQA decode attention (K3).  q: [B, >=Hq*D] (row stride allowed).
+    With ``start_blk`` (per-row first block of the suffix pass) the prefix partials ``pre_o`` /
+    ``pre_lse`` written by :func:`paged_decode_prefix` are merged into the result."""
     B = q.shape[0]
     D = k_cache.shape[-1]
     if out is None:
@@ -120,8 +123,17 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         part_o = torch.empty(B * Hq * num_splits * D, dtype=torch.float32, device=q.device)
         part_lse = torch.empty(B * Hq * num_splits, dtype=torch.float32, device=q.device)
     kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, part_o, part_lse, int(num_splits),
-                           float(scale))
+                           float(scale), start_blk, pre_o, pre_lse)
     return out
+
+
+def paged_decode_prefix(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                        tiles: torch.Tensor, pre_o: torch.Tensor, pre_lse: torch.Tensor, Hq: int,
+                        scale: float) -> None:
+    """Prefix-shared (cascade) pass of decode attention: for each tile (row_start, nseq, prefix_blocks)
+    the tile's sequences attend to their SHARED first `prefix_blocks` blocks in one MFMA pass
+    (16 query rows = nseq x G heads); writes normalised partials + log2-sum-exp per (row, head)."""
+    kernels().paged_decode_prefix(q, k_cache, v_cache, block_tables, tiles, pre_o, pre_lse, int(Hq), float(scale))
 
 
 def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int,

@@ -135,6 +135,67 @@ def test_paged_decode(gpu, G, splits):
         _close(out[b], o, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("G,splits", [(4, 1), (4, 2), (2, 1)])
+def test_paged_decode_prefix_shared(gpu, G, splits):
+    """Cascade path (shared-prefix MFMA pass + per-sequence suffix pass + merge) == plain decode."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(5)
+    Hkv, D, BS, NB = 2, 128, 16, 96
+    Hq = Hkv * G
+    P = 5                      # shared prefix blocks
+    B = 11                     # rows: group A = rows 0..6 (7 seqs), singleton row 7, group B = rows 8..10
+    ctx = torch.tensor([P * BS + k for k in (1, 3, 16, 17, 30, 2, 9)] + [40] + [3 * BS + 1, 3 * BS + 5, 3 * BS + 20],
+                       dtype=torch.int32, device=gpu)
+    width = 8
+    kc = _bf(NB, Hkv, BS, D, dev=gpu)
+    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    bt = torch.zeros(B, width, dtype=torch.int32, device=gpu)
+    nxt = 0
+
+    def take(n):
+        nonlocal nxt
+        r = torch.arange(nxt, nxt + n, dtype=torch.int32, device=gpu)
+        nxt += n
+        return r
+
+    shared_a, shared_b = take(P), take(3)
+    for b in range(B):
+        nb = (int(ctx[b]) + BS - 1) // BS
+        if b <= 6:
+            bt[b, :P] = shared_a
+            bt[b, P:nb] = take(nb - P)
+        elif b == 7:
+            bt[b, :nb] = take(nb)
+        else:
+            bt[b, :3] = shared_b
+            bt[b, 3:nb] = take(nb - 3)
+    per = 16 // G
+    tiles_l = []
+    for (s0, s1, p) in ((0, 7, P), (8, 11, 3)):
+        for r0 in range(s0, s1, per):
+            tiles_l.append((r0, min(per, s1 - r0), p))
+    max_tiles = -(-B // per)
+    tiles = torch.zeros(max_tiles, 3, dtype=torch.int32, device=gpu)
+    tiles[:len(tiles_l)] = torch.tensor(tiles_l, dtype=torch.int32, device=gpu)
+    start = torch.tensor([P] * 7 + [0] + [3] * 3, dtype=torch.int32, device=gpu)
+    q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
+    pre_o = torch.empty(B * Hq * D, device=gpu)
+    pre_lse = torch.empty(B * Hq, device=gpu)
+    ops.paged_decode_prefix(q_full, kc, vc, bt, tiles, pre_o, pre_lse, Hq, 1 / math.sqrt(D))
+    out = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits, start_blk=start,
+                           pre_o=pre_o, pre_lse=pre_lse)
+    plain = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits)
+    _close(out, plain, 1e-2, 1e-2)
+    for b in range(B):
+        L = int(ctx[b])
+        toks = torch.arange(L, device=gpu)
+        blk = bt[b, toks // BS].long()
+        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], vc[blk, :, :, toks % BS],
+                          False, 1 / math.sqrt(D))[0]
+        _close(out[b], o, 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize("D,Hq,Hkv,causal", [(128, 8, 2, True), (64, 4, 4, False), (128, 4, 4, False),
                                              (64, 8, 2, True)])
 def test_prefill_attention(gpu, D, Hq, Hkv, causal):

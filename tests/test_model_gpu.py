@@ -67,6 +67,24 @@ def test_engine_greedy_graph_equivalence_and_fork(tiny, gpu):
     assert outs[0][0][0][0] == first
 
 
+def test_engine_prefix_sharing_equivalence(tiny, gpu):
+    """The cascade (prefix-shared) attention path gives the same greedy continuations."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+
+    tok = ByteTokenizer(tiny.cfg.vocab_size)
+    prompts = [tok.encode("x" * 70 + " a shared prompt longer than a few KV blocks"), tok.encode("y" * 33)]
+    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    outs = []
+    for share in (False, True):
+        eng = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512, prefix_sharing=share)
+        outs.append(eng.generate(prompts, sp, n=5))
+    same = sum(a == b for ga, gb in zip(*outs) for ca, cb in zip(ga, gb) for a, b in zip(ca, cb))
+    total = sum(len(c) for g in outs[0] for c in g)
+    assert same >= 0.95 * total, (same, total)
+
+
 def test_engine_sampling_seeded(tiny, gpu):
     from llm_weighted_consensus_amd.engine.engine import LLMEngine
     from llm_weighted_consensus_amd.engine.sampling import SamplingParams
