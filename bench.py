@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--decoder", default="llama-3-8b")
     ap.add_argument("--encoder", default="bge-large-en-v1.5")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-prefix-sharing", action="store_true", help="disable the cascade prefix attention pass")
     ap.add_argument("--profile-steps", action="store_true", help="print a per-phase breakdown")
     return ap.parse_args()
 
@@ -70,7 +71,7 @@ def main():
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     max_len = a.prompt_len + a.gen_len + 16
     engine = LLMEngine(model, tok, max_batch=G * n_local, max_model_len=max_len, use_graphs=not a.no_graphs,
-                       kv_memory_fraction=0.5)
+                       kv_memory_fraction=0.5, prefix_sharing=not a.no_prefix_sharing)
     scorer = EmbeddingConsensus(encoder, tau=0.05, max_tokens=512)
     gen = torch.Generator().manual_seed(99)
 

@@ -42,6 +42,44 @@ py::tuple prepare_decode(BlockManager& bm, const std::vector<int64_t>& seqs, int
   return py::make_tuple(bt, ctx, slots, pos);
 }
 
+int32_t* writable_i32(py::array& a, int64_t need, const char* name) {
+  if (a.dtype().kind() != 'i' || a.itemsize() != 4 || !(a.flags() & py::array::c_style) || !a.writeable())
+    throw std::runtime_error(std::string("prepare_decode_into: ") + name + " must be a writable C-contiguous int32 array");
+  if (a.size() < need) throw std::runtime_error(std::string("prepare_decode_into: ") + name + " too short");
+  return static_cast<int32_t*>(a.mutable_data());
+}
+
+// Same as prepare_decode but writes straight into caller-owned arrays (views of one pinned staging
+// buffer), so a decode step costs a single host->device copy.  Only the first `used_width` columns
+// of each block-table row are rewritten (columns beyond a row's table are never read by the
+// attention kernels, which stop at ctx_len).
+void prepare_decode_into(BlockManager& bm, const std::vector<int64_t>& seqs, int width, int pad_to, py::array bt,
+                         py::array ctx, py::array slots, py::array pos) {
+  const int B = (int)seqs.size();
+  const int Bp = std::max(B, pad_to);
+  int32_t* btp = writable_i32(bt, (int64_t)Bp * width, "block_tables");
+  int32_t* cp = writable_i32(ctx, Bp, "ctx_lens");
+  int32_t* sp = writable_i32(slots, Bp, "slots");
+  int32_t* pp = writable_i32(pos, Bp, "positions");
+  for (int i = 0; i < B; ++i) {
+    const int64_t slot = bm.append_token(seqs[i]);
+    const auto& tab = bm.block_table(seqs[i]);
+    if ((int)tab.size() > width) throw std::runtime_error("prepare_decode_into: block table wider than batch width");
+    int32_t* row = btp + (size_t)i * width;
+    for (size_t j = 0; j < tab.size(); ++j) row[j] = (int32_t)tab[j];
+    const int64_t len = bm.length(seqs[i]);
+    cp[i] = (int32_t)len;
+    sp[i] = (int32_t)slot;
+    pp[i] = (int32_t)(len - 1);
+  }
+  for (int i = B; i < Bp; ++i) {  // padding rows: 1-token context on block 0, no cache write
+    btp[(size_t)i * width] = 0;
+    cp[i] = 1;
+    sp[i] = -1;
+    pp[i] = 0;
+  }
+}
+
 // Slots of positions [start, start+count) of a sequence (prefill scatter targets).
 py::array_t<int32_t> slots_range(const BlockManager& bm, int64_t seq, int64_t start, int64_t count) {
   py::array_t<int32_t> out(count);
@@ -75,6 +113,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("refcount", &BlockManager::refcount)
       .def("take_copies", &BlockManager::take_copies);
   m.def("prepare_decode", &prepare_decode, py::arg("bm"), py::arg("seqs"), py::arg("width"), py::arg("pad_to") = 0);
+  m.def("prepare_decode_into", &prepare_decode_into, py::arg("bm"), py::arg("seqs"), py::arg("width"),
+        py::arg("pad_to"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("slots"), py::arg("positions"));
   m.def("slots_range", &slots_range);
 
   lwc::bind_consensus_core(m);

@@ -7,7 +7,7 @@ src/score/completions/client.rs:343-356 mapped onto one GPU), and every `step()`
 sequences by one token with a single batched decode launch.
 
 Host runtime pieces are native C++ (`_runtime.BlockManager`: ref-counted paged-KV blocks with
-copy-on-write fork, `prepare_decode`: per-step batch tables).  The decode forward is captured once per
+copy-on-write fork, `prepare_decode_into`: per-step batch tables written straight into pinned staging).  The decode forward is captured once per
 batch bucket into a hipGraph (torch.cuda.CUDAGraph on ROCm) so a step is one graph replay plus the
 fused sampler launch.
 
@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from .._runtime import BlockManager, prepare_decode, slots_range
+from .._runtime import BlockManager, prepare_decode_into, slots_range
 from ..models.llama import KVCache
 from .sampling import SamplingParams
 from .tokenizer import IncrementalDecoder
@@ -54,6 +54,7 @@ class Sequence:
         self.group = group
         self.index = index
         self.seed = seed
+        self.n_launched = 0  # tokens sampled or in flight (the Philox offset of the next sample)
         self.tokens: List[int] = []
         self.text = ""
         self.finished = False
@@ -88,13 +89,76 @@ class SequenceGroup:
         return all(s.finished for s in self.seqs)
 
 
+_F32_PARAMS = ("temperature", "top_p", "min_p", "top_a", "freq_pen", "pres_pen", "rep_pen")
+_I32_PARAMS = ("top_k", "count_rows", "bias_rows")
+
+
 class _GraphBucket:
-    def __init__(self, B: int, width: int, splits: int, max_tiles: int):
+    """Per batch-size bucket: the captured decode graph plus ONE int32 staging layout holding every
+    per-step input (block tables, ctx lens, slots, positions, tokens, prefix tiles, sampler
+    parameters, Philox seeds/offsets).  The host side is two pinned buffers (alternating steps), the
+    device side one buffer whose views are the graph's inputs, so a step is one H2D copy."""
+
+    def __init__(self, B: int, width: int, splits: int, max_tiles: int, device):
         self.B, self.width, self.splits, self.max_tiles = B, width, splits, max_tiles
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.tokens = self.positions = self.slots = self.block_tables = self.ctx_lens = None
-        self.tiles = self.start_blk = None
         self.logits: Optional[torch.Tensor] = None
+        segs: List[Tuple[str, int]] = [("block_tables", B * width), ("ctx_lens", B), ("slots", B), ("positions", B),
+                                       ("tokens", B), ("tiles", max_tiles * 3), ("start_blk", B)]
+        segs += [(n, B) for n in _F32_PARAMS + _I32_PARAMS]
+        segs += [("seeds", 2 * B), ("offsets", 2 * B)]
+        self.off: Dict[str, Tuple[int, int]] = {}
+        o = 0
+        for name, n in segs:
+            o += o & 1  # keep every segment 8-byte aligned (int64 views)
+            self.off[name] = (o, o + n)
+            o += n
+        self.size = o + (o & 1)
+        self.dev = torch.zeros(self.size, dtype=torch.int32, device=device)
+        self.host = [torch.zeros(self.size, dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.host_static_key: List[object] = [None, None]
+        self.d = self._views(self.dev, torch)
+        self.h = [self._views(h.numpy(), np) for h in self.host]
+        self.out_dev: List[Optional[torch.Tensor]] = [None, None]
+        self.out_host: List[Optional[torch.Tensor]] = [None, None]
+
+    def _views(self, buf, lib):
+        f32 = torch.float32 if lib is torch else np.float32
+        i64 = torch.int64 if lib is torch else np.int64
+        v = {}
+        for name, (a, b) in self.off.items():
+            x = buf[a:b]
+            if name in _F32_PARAMS:
+                x = x.view(f32)
+            elif name in ("seeds", "offsets"):
+                x = x.view(i64)
+            v[name] = x
+        v["block_tables"] = v["block_tables"].reshape(self.B, self.width)
+        v["tiles"] = v["tiles"].reshape(self.max_tiles, 3)
+        return v
+
+    def outputs(self, parity: int, K: int):
+        """Sampler outputs for one step as views of one device buffer (tok | lp | topk ids | topk lp),
+        and the matching pinned host buffer (one D2H copy per step)."""
+        B, Kb = self.B, max(K, 1)
+        need = B * (2 + 2 * Kb)
+        if self.out_dev[parity] is None or self.out_dev[parity].numel() < need:
+            self.out_dev[parity] = torch.empty(need, dtype=torch.int32, device=self.dev.device)
+            self.out_host[parity] = torch.empty(need, dtype=torch.int32).pin_memory()
+        o = self.out_dev[parity]
+        tok = o[:B]
+        lp = o[B:2 * B].view(torch.float32)
+        ids = o[2 * B:2 * B + B * Kb].view(B, Kb)
+        lps = o[2 * B + B * Kb:need].view(torch.float32).view(B, Kb)
+        return (tok, lp, ids, lps), o[:need], self.out_host[parity][:need]
+
+
+class _Step:
+    """A launched (not yet processed) decode step."""
+
+    def __init__(self, seqs, key, bk, parity, K, tok_dev, out_host, event):
+        self.seqs, self.key, self.bk, self.parity, self.K = seqs, key, bk, parity, K
+        self.tok_dev, self.out_host, self.event = tok_dev, out_host, event
 
 
 class LLMEngine:
@@ -120,6 +184,9 @@ class LLMEngine:
         self.use_graphs = use_graphs
         self.prefix_sharing = prefix_sharing
         self.buckets: Dict[int, _GraphBucket] = {}
+        self.inflight: Optional[_Step] = None
+        self._step_no = 0
+        self._comp_cache: Tuple[object, Optional[dict]] = (None, None)
         self.waiting: Deque[SequenceGroup] = deque()
         self.running: List[Sequence] = []
         self.lock = threading.Lock()
@@ -145,17 +212,27 @@ class LLMEngine:
         return g
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or bool(self.running)
+        return bool(self.waiting) or bool(self.running) or self.inflight is not None
 
     def step(self) -> List[TokenEvent]:
-        """Run one engine iteration: admit+prefill waiting groups if any fit, else one decode step."""
+        """Run one engine iteration: admit+prefill waiting groups if any fit, else one decode step.
+
+        Decode steps are pipelined one deep: step t+1 is launched (its inputs need only the block
+        manager, and its input tokens are step t's sampler output, still on the device) BEFORE the
+        host syncs on and post-processes step t, so detokenisation, stop checks and callbacks overlap
+        the GPU.  A sequence that finishes at step t has one discarded row in step t+1."""
+        events: List[TokenEvent] = []
         with self.lock:
-            admitted = self._admit()
-        if admitted:
-            return self._prefill(admitted)
-        if self.running:
-            return self._decode()
-        return []
+            fits = self._first_waiting_fits()
+        if fits:
+            events += self._drain()
+            with self.lock:
+                admitted = self._admit()
+            if admitted:
+                return events + self._prefill(admitted)
+        if self.running or self.inflight is not None:
+            events += self._decode()
+        return events
 
     def generate(self, prompts: List[List[int]], params: SamplingParams, n: int = 1) -> List[List[List[int]]]:
         """Offline helper: run prompts to completion, return tokens[prompt][choice]."""
@@ -170,6 +247,14 @@ class LLMEngine:
         prompt_blocks = (len(g.prompt_ids) + bs - 1) // bs
         per_child = (len(g.prompt_ids) + g.params.max_tokens + bs - 1) // bs - len(g.prompt_ids) // bs
         return prompt_blocks + g.n * (per_child + 1)
+
+    def _first_waiting_fits(self) -> bool:
+        if not self.waiting:
+            return False
+        g = self.waiting[0]
+        live = sum(1 for s in self.running if not s.finished)
+        return live + g.n <= self.max_batch and (self._group_reservation(g) <= self.free_blocks_unreserved
+                                                 or (not self.running and self.inflight is None))
 
     def _admit(self) -> List[SequenceGroup]:
         out, tokens = [], 0
@@ -260,15 +345,16 @@ class LLMEngine:
             splits = max(1, min(16, -(-1024 // (Bb * self.cfg.kv_heads))))
             splits = min(splits, max(1, self.width // 4))
             per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
-            bk = _GraphBucket(Bb, self.width, splits, -(-Bb // per))
+            bk = _GraphBucket(Bb, self.width, splits, -(-Bb // per), self.device)
             self.buckets[Bb] = bk
         return bk
 
-    def _prefix_plan(self, seqs: List[Sequence], bk: _GraphBucket):
+    def _prefix_plan(self, seqs: List[Sequence], tiles: np.ndarray, start: np.ndarray) -> None:
         """Tiles for the prefix-shared attention pass: runs of consecutive sequences of one group
-        (forked from one prompt) share the prompt's full blocks; each tile packs <= 16/G of them."""
-        tiles = np.zeros((bk.max_tiles, 3), dtype=np.int32)
-        start = np.zeros(bk.B, dtype=np.int32)
+        (forked from one prompt) share the prompt's full blocks; each tile packs <= 16/G of them.
+        Unused tiles have nseq = 0."""
+        tiles[:] = 0
+        start[:] = 0
         per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
         nt, i, B = 0, 0, len(seqs)
         while i < B:
@@ -280,42 +366,61 @@ class LLMEngine:
             if j - i >= 2 and pblk > 0:
                 for r0 in range(i, j, per):
                     n = min(per, j - r0)
-                    if nt >= bk.max_tiles:
+                    if nt >= tiles.shape[0]:
                         raise RuntimeError("prefix plan: tile overflow")
                     tiles[nt] = (r0, n, pblk)
                     nt += 1
                 start[i:j] = pblk
             i = j
-        return tiles, start
 
-    def _run_decode(self, bk: _GraphBucket, bt, ctx, slots, pos, tokens, prefix=None) -> torch.Tensor:
-        dev = self.device
-        if bk.tokens is None:
-            bk.tokens = torch.zeros(bk.B, dtype=torch.int32, device=dev)
-            bk.positions = torch.zeros(bk.B, dtype=torch.int32, device=dev)
-            bk.slots = torch.full((bk.B,), -1, dtype=torch.int32, device=dev)
-            bk.block_tables = torch.zeros(bk.B, bk.width, dtype=torch.int32, device=dev)
-            bk.ctx_lens = torch.ones(bk.B, dtype=torch.int32, device=dev)
-            if self.prefix_sharing:
-                bk.tiles = torch.zeros(bk.max_tiles, 3, dtype=torch.int32, device=dev)
-                bk.start_blk = torch.zeros(bk.B, dtype=torch.int32, device=dev)
-        bk.tokens.copy_(tokens, non_blocking=True)
-        bk.positions.copy_(pos, non_blocking=True)
-        bk.slots.copy_(slots, non_blocking=True)
-        bk.block_tables.copy_(bt, non_blocking=True)
-        bk.ctx_lens.copy_(ctx, non_blocking=True)
+    def _static_inputs(self, seqs: List[Sequence], key, bk: _GraphBucket) -> dict:
+        """Per-composition inputs (prefix tiles, sampler parameters), rebuilt only when the batch
+        composition changes — in steady-state decoding only positions/slots/offsets move."""
+        ck, cached = self._comp_cache
+        if ck == key and cached is not None:
+            return cached
+        B = bk.B
+        ps = [s.params for s in seqs]
+        n = len(seqs)
+        st = {"tiles": np.zeros((bk.max_tiles, 3), np.int32), "start_blk": np.zeros(B, np.int32)}
         if self.prefix_sharing:
-            bk.tiles.copy_(prefix[0], non_blocking=True)
-            bk.start_blk.copy_(prefix[1], non_blocking=True)
+            self._prefix_plan(seqs, st["tiles"], st["start_blk"])
+
+        def col(vals, dt, fill=0):
+            a = np.full(B, fill, dtype=dt)
+            a[:n] = vals
+            return a
+
+        st["temperature"] = col([p.temperature for p in ps], np.float32, 1.0)
+        st["top_p"] = col([p.top_p for p in ps], np.float32, 1.0)
+        st["top_k"] = col([p.top_k for p in ps], np.int32)
+        st["min_p"] = col([p.min_p for p in ps], np.float32)
+        st["top_a"] = col([p.top_a for p in ps], np.float32)
+        st["freq_pen"] = col([p.frequency_penalty for p in ps], np.float32)
+        st["pres_pen"] = col([p.presence_penalty for p in ps], np.float32)
+        st["rep_pen"] = col([p.repetition_penalty for p in ps], np.float32, 1.0)
+        st["count_rows"] = col([s.count_row for s in seqs], np.int32, -1)
+        st["bias_rows"] = col([s.group.bias_row for s in seqs], np.int32, -1)
+        st["seeds"] = col([s.seed for s in seqs], np.int64)
+        st["K"] = max((p.top_logprobs for p in ps), default=0)
+        st["any_pen"] = any(p.uses_penalties for p in ps)
+        st["any_bias"] = any(s.group.bias_row >= 0 for s in seqs)
+        self._comp_cache = (key, st)
+        return st
+
+    def _ensure_graph(self, bk: _GraphBucket) -> None:
+        d = bk.d
 
         def fwd():
-            return self.model.decode(bk.tokens, bk.positions, bk.slots, bk.block_tables, bk.ctx_lens, self.cache,
-                                     num_splits=bk.splits,
-                                     prefix=(bk.tiles, bk.start_blk) if self.prefix_sharing else None)
+            return self.model.decode(d["tokens"], d["positions"], d["slots"], d["block_tables"], d["ctx_lens"],
+                                     self.cache, num_splits=bk.splits,
+                                     prefix=(d["tiles"], d["start_blk"]) if self.prefix_sharing else None)
 
         if not self.use_graphs:
-            return fwd()
+            bk.logits = fwd()
+            return
         if bk.graph is None:
+            dev = self.device
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
@@ -326,32 +431,132 @@ class LLMEngine:
                 bk.logits = fwd()
             bk.graph = g
         bk.graph.replay()
-        return bk.logits
 
-    def _decode(self) -> List[TokenEvent]:
-        seqs = self.running
+    def _launch(self, seqs: List[Sequence]) -> _Step:
+        """Stage inputs, replay the decode graph and launch the sampler for `seqs`; results are
+        copied to pinned host memory asynchronously (processed later by :meth:`_process`)."""
         B = len(seqs)
         bk = self._bucket(B)
-        bt, ctx, slots, pos = prepare_decode(self.bm, [s.id for s in seqs], bk.width, bk.B)
+        key = (bk.B, tuple(s.id for s in seqs))
+        parity = self._step_no & 1
+        self._step_no += 1
+        h = bk.h[parity]
+        prepare_decode_into(self.bm, [s.id for s in seqs], bk.width, bk.B, h["block_tables"], h["ctx_lens"],
+                            h["slots"], h["positions"])
+        st = self._static_inputs(seqs, key, bk)
+        if bk.host_static_key[parity] != key:
+            for name in ("tiles", "start_blk", "seeds") + _F32_PARAMS + _I32_PARAMS:
+                h[name][...] = st[name]
+            bk.host_static_key[parity] = key
+        prev = self.inflight
+        prev_rows = {}
+        if prev is not None and prev.key != key:
+            prev_rows = {s.id: i for i, s in enumerate(prev.seqs)}
+        offs = h["offsets"]
+        tok_h = h["tokens"]
+        from_prev_dst, from_prev_src = [], []
+        same = prev is not None and prev.key == key
+        for i, s in enumerate(seqs):
+            offs[i] = s.n_launched
+            if not same:
+                if len(s.tokens) == s.n_launched:
+                    tok_h[i] = s.tokens[-1]
+                else:  # last token still in flight: take it from the previous step's device output
+                    from_prev_dst.append(i)
+                    from_prev_src.append(prev_rows[s.id])
+            s.n_launched += 1
+        dev = self.device
         copies = self.bm.take_copies()
+        bk.dev.copy_(bk.host[parity], non_blocking=True)
+        d = bk.d
+        if same:
+            d["tokens"][:B].copy_(prev.tok_dev[:B])
+        elif from_prev_dst:
+            dst = torch.tensor(from_prev_dst, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+            src = torch.tensor(from_prev_src, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+            d["tokens"].index_copy_(0, dst, prev.tok_dev.index_select(0, src))
         if copies:
-            self.cache.copy_blocks(torch.tensor(copies, dtype=torch.int32, device=self.device))
-        last = np.zeros(bk.B, dtype=np.int32)
-        last[:B] = [s.tokens[-1] for s in seqs]
-        pin = lambda a: torch.from_numpy(a).pin_memory()
-        prefix = None
-        if self.prefix_sharing:
-            tiles, start = self._prefix_plan(seqs, bk)
-            prefix = (pin(tiles), pin(start))
-        logits = self._run_decode(bk, pin(bt), pin(ctx), pin(slots), pin(pos), pin(last), prefix)
+            self.cache.copy_blocks(torch.tensor(copies, dtype=torch.int32, device=dev))
+        self._ensure_graph(bk)
+        K = st["K"]
+        mask = mask_rows = None
+        cons = [i for i, s in enumerate(seqs) if s.constraint_state is not None]
+        if cons:
+            mask, mask_rows = self._constraint_masks(seqs, cons)
+        outs, out_dev, out_host = bk.outputs(parity, K)
+        ops.sample(bk.logits[:B], temperature=d["temperature"], top_p=d["top_p"], top_k=d["top_k"],
+                   min_p=d["min_p"], top_a=d["top_a"], seeds=d["seeds"], offsets=d["offsets"], num_logprobs=K,
+                   freq_pen=d["freq_pen"] if st["any_pen"] else None,
+                   pres_pen=d["pres_pen"] if st["any_pen"] else None,
+                   rep_pen=d["rep_pen"] if st["any_pen"] else None,
+                   counts=self.counts if st["any_pen"] else None,
+                   count_rows=d["count_rows"] if st["any_pen"] else None,
+                   bias=self.bias if st["any_bias"] else None,
+                   bias_rows=d["bias_rows"] if st["any_bias"] else None,
+                   mask=mask, mask_rows=mask_rows,
+                   out_token=outs[0], out_logprob=outs[1], out_topk_ids=outs[2], out_topk_lp=outs[3])
+        out_host.copy_(out_dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
         self.stats["decode_tokens"] += B
         self.stats["steps"] += 1
-        events = self._sample_and_advance(logits[:B], seqs)
-        self.running = [s for s in seqs if not s.finished]
+        return _Step(seqs, key, bk, parity, K, outs[0], out_host, ev)
+
+    def _constraint_masks(self, seqs: List[Sequence], cons: List[int]):
+        words = self.cfg.vocab_size // 32
+        m = np.zeros((len(cons), words), dtype=np.uint32)
+        rows = np.full(len(seqs), -1, dtype=np.int32)
+        for j, i in enumerate(cons):
+            s = seqs[i]
+            m[j] = s.params.constraint.mask(s.constraint_state, self.cfg.vocab_size)
+            rows[i] = j
+        return (torch.from_numpy(m.view(np.int32)).to(self.device),
+                torch.from_numpy(rows).to(self.device))
+
+    def _process(self, st: _Step) -> List[TokenEvent]:
+        st.event.synchronize()
+        B, K = len(st.seqs), st.K
+        Kb = max(K, 1)
+        Bp = st.bk.B
+        a = st.out_host.numpy()
+        tok_h = a[:B].tolist()
+        lp_h = a[Bp:Bp + B].view(np.float32).tolist()
+        if K:
+            ids_h = a[2 * Bp:2 * Bp + Bp * Kb].reshape(Bp, Kb)[:B, :K].tolist()
+            lps_h = a[2 * Bp + Bp * Kb:2 * Bp + 2 * Bp * Kb].view(np.float32).reshape(Bp, Kb)[:B, :K].tolist()
+        else:
+            ids_h = lps_h = None
+        return self._advance(st.seqs, tok_h, lp_h, ids_h, lps_h)
+
+    def _drain(self) -> List[TokenEvent]:
+        st, self.inflight = self.inflight, None
+        if st is None:
+            return []
+        events = self._process(st)
+        self.running = [s for s in self.running if not s.finished]
+        return events
+
+    def _decode(self) -> List[TokenEvent]:
+        events: List[TokenEvent] = []
+        # grammar masks depend on the previous token: constrained batches run unpipelined
+        sync = any(s.constraint_state is not None for s in self.running)
+        if sync and self.inflight is not None:
+            events += self._drain()
+        seqs = [s for s in self.running if not s.finished and s.n_launched < s.params.max_tokens]
+        if not seqs:
+            return events + self._drain()
+        cur = self._launch(seqs)
+        prev, self.inflight = self.inflight, cur
+        if prev is not None:
+            events += self._process(prev)
+        if sync:
+            events += self._drain()
+        self.running = [s for s in self.running if not s.finished]
         return events
 
     # ------------------------------------------------------------------ sampling + bookkeeping
     def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[TokenEvent]:
+        """Synchronous sampling (first token after prefill)."""
         B = len(seqs)
         dev = self.device
         ps = [s.params for s in seqs]
@@ -361,19 +566,10 @@ class LLMEngine:
         K = max((p.top_logprobs for p in ps), default=0)
         any_pen = any(p.uses_penalties for p in ps)
         any_bias = any(s.group.bias_row >= 0 for s in seqs)
-        cons = [s for s in seqs if s.constraint_state is not None]
+        cons = [i for i, s in enumerate(seqs) if s.constraint_state is not None]
         mask = mask_rows = None
         if cons:
-            words = self.cfg.vocab_size // 32
-            m = np.zeros((len(cons), words), dtype=np.uint32)
-            rows = np.full(B, -1, dtype=np.int32)
-            for j, s in enumerate(cons):
-                m[j] = s.params.constraint.mask(s.constraint_state, self.cfg.vocab_size)
-            for i, s in enumerate(seqs):
-                if s.constraint_state is not None:
-                    rows[i] = cons.index(s)
-            mask = torch.from_numpy(m.view(np.int32)).to(dev)
-            mask_rows = torch.from_numpy(rows).to(dev)
+            mask, mask_rows = self._constraint_masks(seqs, cons)
         tok, lp, tk_ids, tk_lp = ops.sample(
             logits,
             temperature=f32([p.temperature for p in ps]),
@@ -382,7 +578,7 @@ class LLMEngine:
             min_p=f32([p.min_p for p in ps]),
             top_a=f32([p.top_a for p in ps]),
             seeds=i64([s.seed for s in seqs]),
-            offsets=i64([len(s.tokens) for s in seqs]),
+            offsets=i64([s.n_launched for s in seqs]),
             num_logprobs=K,
             freq_pen=f32([p.frequency_penalty for p in ps]) if any_pen else None,
             pres_pen=f32([p.presence_penalty for p in ps]) if any_pen else None,
@@ -393,13 +589,19 @@ class LLMEngine:
             bias_rows=i32([s.group.bias_row for s in seqs]) if any_bias else None,
             mask=mask, mask_rows=mask_rows,
         )
-        tok_h = tok.cpu().tolist()
-        lp_h = lp.cpu().tolist()
-        tk_ids_h = tk_ids.cpu().tolist() if K else [[] for _ in range(B)]
-        tk_lp_h = tk_lp.cpu().tolist() if K else [[] for _ in range(B)]
+        for s in seqs:
+            s.n_launched += 1
+        return self._advance(seqs, tok.cpu().tolist(), lp.cpu().tolist(),
+                             tk_ids.cpu().tolist() if K else None, tk_lp.cpu().tolist() if K else None)
+
+    def _advance(self, seqs: List[Sequence], tok_h, lp_h, ids_h, lps_h) -> List[TokenEvent]:
+        """Host bookkeeping of one sampled token per sequence: append, grammar advance, detokenise,
+        stop / length checks, callbacks."""
         events = []
         eos = self.tokenizer.eos_token_id
         for i, s in enumerate(seqs):
+            if s.finished:  # finished (or aborted) while this step was in flight: discard the row
+                continue
             t = int(tok_h[i])
             p = s.params
             s.tokens.append(t)
@@ -428,7 +630,7 @@ class LLMEngine:
             if reason is None and len(s.tokens) >= p.max_tokens:
                 reason = "length"
             k = p.top_logprobs
-            top = list(zip(tk_ids_h[i][:k], tk_lp_h[i][:k])) if k else []
+            top = list(zip(ids_h[i][:k], lps_h[i][:k])) if k else []
             ev = TokenEvent(s, t, text, float(lp_h[i]), top)
             if reason is not None:
                 self._finish(s, reason)
@@ -484,4 +686,6 @@ class LLMEngine:
                     except Exception:  # pragma: no cover - best effort cleanup
                         s.finished = True
         self.running = []
+        self.inflight = None
+        self._comp_cache = (None, None)
         return list(groups.values())

@@ -15,4 +15,9 @@ rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
 [ "$STAGE" = "tests" ] && exit 0
 timeout -k 10 900 python bench.py --steps 3 --warmup 1 --profile-steps > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -20 gpurun_out/bench.log
+[ $rc -eq 0 ] || exit $rc
+if [ -n "$BENCH_EXTRA" ]; then  # optional A/B variant, e.g. BENCH_EXTRA=--no-prefix-sharing
+  timeout -k 10 900 python bench.py --steps 3 --warmup 1 --profile-steps $BENCH_EXTRA > gpurun_out/bench_b.log 2>&1
+  rc=$?; echo "bench($BENCH_EXTRA) rc=$rc"; tail -20 gpurun_out/bench_b.log
+fi
 exit $rc

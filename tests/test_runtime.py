@@ -48,6 +48,28 @@ def test_prepare_decode_padding():
     assert slots[0] == bm.slot(5, 3)
 
 
+def test_prepare_decode_into_matches_prepare_decode():
+    """The staging-buffer variant writes the same tables as prepare_decode (used columns)."""
+    import numpy as np
+
+    a, b = R.BlockManager(64, 4), R.BlockManager(64, 4)
+    for bm in (a, b):
+        bm.add_sequence(1, 9)
+        bm.add_sequence(2, 3)
+        bm.fork(1, 3)
+    bt, ctx, slots, pos = R.prepare_decode(a, [1, 3, 2], 6, 4)
+    buf = np.full(4 * 6 + 12, 77, dtype=np.int32)
+    bt2 = buf[:24].reshape(4, 6)
+    R.prepare_decode_into(b, [1, 3, 2], 6, 4, bt2, buf[24:28], buf[28:32], buf[32:36])
+    assert list(buf[24:28]) == list(ctx) and list(buf[28:32]) == list(slots) and list(buf[32:36]) == list(pos)
+    for i in range(3):
+        n = len(b.block_table([1, 3, 2][i]))
+        assert list(bt2[i, :n]) == list(bt[i, :n])
+    assert b.take_copies() == a.take_copies()
+    with pytest.raises(RuntimeError):
+        R.prepare_decode_into(b, [1], 6, 4, bt2, buf[24:28], buf[28:32], buf[32:36].astype(np.int64))
+
+
 def _ref_tree_keys(n, m):
     """Python oracle of the reference SelectPfxTree shape (client.rs:1469-1517): multiset of key depths."""
     def rec(length, force):
