@@ -41,6 +41,32 @@ def gemms(dev, Ms, tuned):
                   f"{fl:7.1f} TF/s {gb:7.0f} GB/s", flush=True)
 
 
+def gemm_layouts(dev, Ms):
+    """Same products through different operand layouts: hipBLASLt picks different kernels."""
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    for M in Ms:
+        for name, (N, K) in shapes.items():
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            wt = w.t().contiguous()
+            xt = x.t().contiguous()
+            cases = {
+                "NT  x@w^T": lambda: F.linear(x, w),
+                "NN  x@wt": lambda: torch.mm(x, wt),
+                "sw  w@x^T": lambda: torch.mm(w, xt),
+                "sw2 w@xT(view)": lambda: torch.mm(w, x.t()),
+            }
+            for cname, fn in cases.items():
+                us = timeit(fn, iters=20)
+                fl = 2 * M * N * K / (us * 1e-6) / 1e12
+                print(f"layout M={M:4d} {name:8s} {cname:16s}: {us:8.1f} us {fl:7.1f} TF/s", flush=True)
+    for n in (4096, 8192):
+        a = torch.randn(n, n, device=dev).to(torch.bfloat16)
+        b = torch.randn(n, n, device=dev).to(torch.bfloat16)
+        us = timeit(lambda: torch.mm(a, b), iters=10)
+        print(f"square {n}: {us:8.1f} us {2 * n ** 3 / (us * 1e-6) / 1e12:7.1f} TF/s", flush=True)
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -97,6 +123,8 @@ def main():
     dev = torch.device("cuda:0")
     if "gemm" in a.what:
         gemms(dev, [256, 512], tuned=os.environ.get("PYTORCH_TUNABLEOP_ENABLED") == "1")
+    if "layout" in a.what:
+        gemm_layouts(dev, [512, 1024])
     if "attn" in a.what:
         attention(dev)
     if "sample" in a.what:
