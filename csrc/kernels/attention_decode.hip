@@ -57,7 +57,187 @@ struct DecodeParams {
   float scale;
 };
 
-// PREFIX=true : blockIdx.x = tile;  PREFIX=false: blockIdx.x = sequence
+// K and V registers of one PAIR of 16-token blocks for one wave (K: 8 x 16 B, V: 16 x 8 B per lane).
+struct PairRegs {
+  short8 ka[4], kb[4];
+  short4v va[8], vb[8];
+};
+
+LWC_DEVICE void load_pair_k(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
+                            int g) {
+  const size_t kv_head_stride = (size_t)kBS * kD;  // elements per (block, head)
+  const int physA = bt[blkA];
+  const int physB = hasB ? bt[blkA + 1] : physA;
+  const bf16_t* kA = p.kc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
+  const bf16_t* kB = p.kc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    r.ka[s] = *reinterpret_cast<const short8*>(kA + r16 * kD + 32 * s + 8 * g);
+    r.kb[s] = *reinterpret_cast<const short8*>(kB + r16 * kD + 32 * s + 8 * g);
+  }
+}
+
+LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
+                            int g) {
+  const size_t kv_head_stride = (size_t)kBS * kD;
+  const int physA = bt[blkA];
+  const int physB = hasB ? bt[blkA + 1] : physA;
+  const bf16_t* vA = p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
+  const bf16_t* vB = p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    r.va[n] = *reinterpret_cast<const short4v*>(vA + (16 * n + r16) * kBS + 4 * g);
+    r.vb[n] = *reinterpret_cast<const short4v*>(vB + (16 * n + r16) * kBS + 4 * g);
+  }
+}
+
+LWC_DEVICE void load_pair(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
+                          int g) {
+  load_pair_k(r, p, bt, kvh, blkA, hasB, r16, g);
+  load_pair_v(r, p, bt, kvh, blkA, hasB, r16, g);
+}
+
+// S^T for the pair's two blocks (C layout: lane reg i = S^T[tok 4g+i][row r16]).
+LWC_DEVICE void pair_scores(const PairRegs& r, const short8 (&qf)[4], float4v& sa, float4v& sb) {
+  sa = float4v{0.f, 0.f, 0.f, 0.f};
+  sb = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    sa = mfma16(r.ka[s], qf[s], sa);
+    sb = mfma16(r.kb[s], qf[s], sb);
+  }
+}
+
+// Online-softmax update (log2 domain) for the pair; rescales O and returns the P operand.
+// Reductions over the 4 lanes {l, l^16, l^32, l^48} holding one query row's tokens: two VALU
+// half-swaps (v_permlane32_swap / v_permlane16_swap, gfx950) instead of LDS ds_bpermute round trips.
+LWC_DEVICE float row_max4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+LWC_DEVICE float row_sum4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+// Lazy rescaling threshold (log2 units): the running max is only raised — and O rescaled — when
+// some row's new scores exceed it by more than this, so P <= 2^8 and most pairs skip the rescale.
+constexpr float kLazyRescale = 8.f;
+
+// Online-softmax update (log2 domain) for the pair; rescales O when needed and returns the P operand.
+// `row_on` = false leaves this lane's query row untouched (p = 0): used when one wave carries rows
+// of several sequences and a pass covers only one of them.
+LWC_DEVICE void pair_softmax(const float4v& sa, const float4v& sb, int blkA, bool hasB, int ctx, bool row_on,
+                             float sl2, int g, float4v (&o)[8], float& m, float& l, short8& pf) {
+  const int blkB = blkA + 1;
+  float pa[4], pb[4];
+  float mx = -1e30f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ta = blkA * kBS + 4 * g + i, tb = blkB * kBS + 4 * g + i;
+    pa[i] = (row_on && ta < ctx) ? sa[i] * sl2 : -INFINITY;
+    pb[i] = (row_on && hasB && tb < ctx) ? sb[i] * sl2 : -INFINITY;
+    mx = fmaxf(mx, fmaxf(pa[i], pb[i]));
+  }
+  mx = row_max4(mx);
+  if (__any(mx > m + kLazyRescale)) {  // wave-uniform
+    const float m_new = fmaxf(m, mx);
+    const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+    l *= alpha;
+    m = m_new;
+    // O row (4g + i) belongs to query row 4g+i, whose alpha lives in lane 4g+i
+    float al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) al[i] = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= al[i];
+  }
+  float rs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pa[i] = __builtin_amdgcn_exp2f(pa[i] - m);
+    pb[i] = __builtin_amdgcn_exp2f(pb[i] - m);
+    rs += pa[i] + pb[i];
+  }
+  l += row_sum4(rs);
+  // P operand (A): k order {A: 4g+0..3, B: 4g+0..3}
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pf[i] = (short)f2bf(pa[i]);
+    pf[4 + i] = (short)f2bf(pb[i]);
+  }
+}
+
+// O += P V for the pair.  Cache slots past the context may hold stale/uninitialised bits (possibly
+// NaN): P = 0 there, but 0 * NaN = NaN, so in a pair that reaches past the context those V
+// elements are zeroed by select, not arithmetic.  Pairs fully inside take the select-free path.
+LWC_DEVICE void pair_values(const PairRegs& r, const short8& pf, int blkA, bool hasB, int ctx, int g,
+                            float4v (&o)[8]) {
+  const int blkB = blkA + 1;
+  if (hasB && (blkB + 1) * kBS <= ctx) {  // wave-uniform
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      short8 vf;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vf[i] = r.va[n][i];
+        vf[4 + i] = r.vb[n][i];
+      }
+      o[n] = mfma16(pf, vf, o[n]);
+    }
+    return;
+  }
+  bool okA[4], okB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    okA[i] = blkA * kBS + 4 * g + i < ctx;
+    okB[i] = hasB && (blkB * kBS + 4 * g + i < ctx);
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    short8 vf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      vf[i] = okA[i] ? r.va[n][i] : (short)0;
+      vf[4 + i] = okB[i] ? r.vb[n][i] : (short)0;
+    }
+    o[n] = mfma16(pf, vf, o[n]);
+  }
+}
+
+// One whole pair: scores, softmax, values.
+LWC_DEVICE void attend_pair(const PairRegs& r, int blkA, bool hasB, int ctx, const short8 (&qf)[4], float sl2, int g,
+                            float4v (&o)[8], float& m, float& l) {
+  float4v sa, sb;
+  pair_scores(r, qf, sa, sb);
+  short8 pf;
+  pair_softmax(sa, sb, blkA, hasB, ctx, true, sl2, g, o, m, l, pf);
+  pair_values(r, pf, blkA, hasB, ctx, g, o);
+}
+
+// Q^T operand (B) for the 4 k-steps of one wave; rows >= nrows are zero.
+template <bool PREFIX>
+LWC_DEVICE void load_q(short8 (&qf)[4], const DecodeParams& p, int row_seq0, int nrows, int kvh, int r16, int g) {
+  const bool valid = r16 < nrows;
+  const int rr = valid ? r16 : 0;
+  const int seq = PREFIX ? row_seq0 + rr / p.G : row_seq0;
+  const int hq = kvh * p.G + (PREFIX ? rr % p.G : rr);
+  const bf16_t* qh = p.q + (size_t)seq * p.q_stride + (size_t)hq * kD;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    short8 v = *reinterpret_cast<const short8*>(qh + 32 * s + 8 * g);
+    qf[s] = valid ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+// PREFIX=true : blockIdx.x = tile;  PREFIX=false: blockIdx.x = sequence.  4 waves split the item's
+// block pairs and combine through LDS: the long-context / small-batch path.
 template <bool PREFIX>
 __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   const int item = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
@@ -88,18 +268,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   auto row_head = [&](int row) { return kvh * p.G + (PREFIX ? row % p.G : row); };
   const int* bt = p.block_tables + (size_t)row_seq0 * p.max_blocks;  // prefix blocks are shared by the tile
 
-  // Q^T operand (B) for the 4 k-steps; rows >= nrows are zero.
   short8 qf[4];
-  {
-    const bool valid = r16 < nrows;
-    const int rr = valid ? r16 : 0;
-    const bf16_t* qh = p.q + (size_t)row_seq(rr) * p.q_stride + (size_t)row_head(rr) * kD;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      short8 v = *reinterpret_cast<const short8*>(qh + 32 * s + 8 * g);
-      qf[s] = valid ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  }
+  load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
   const float sl2 = p.scale * kLog2e;
 
   float4v o[8];
@@ -107,93 +277,11 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   for (int n = 0; n < 8; ++n) o[n] = float4v{0.f, 0.f, 0.f, 0.f};
   float m = -1e30f, l = 0.f;  // running max / sum (log2 domain) for row r16
 
-  const size_t kv_head_stride = (size_t)kBS * kD;  // elements per (block, head)
   for (int pair = blk_begin + 2 * wid; pair < blk_end; pair += 2 * kWaves) {
-    const int blkA = pair, blkB = pair + 1;
-    const bool hasB = blkB < blk_end;
-    const int physA = bt[blkA];
-    const int physB = hasB ? bt[blkB] : physA;
-    const bf16_t* kA = p.kc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
-    const bf16_t* kB = p.kc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
-    const bf16_t* vA = p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
-    const bf16_t* vB = p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
-    // issue all loads of the pair up front (K: 8 x 16 B, V: 16 x 8 B per lane)
-    short8 ka[4], kb[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      ka[s] = *reinterpret_cast<const short8*>(kA + r16 * kD + 32 * s + 8 * g);
-      kb[s] = *reinterpret_cast<const short8*>(kB + r16 * kD + 32 * s + 8 * g);
-    }
-    short4v va[8], vb[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      va[n] = *reinterpret_cast<const short4v*>(vA + (16 * n + r16) * kBS + 4 * g);
-      vb[n] = *reinterpret_cast<const short4v*>(vB + (16 * n + r16) * kBS + 4 * g);
-    }
-    float4v sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sa = mfma16(ka[s], qf[s], sa);
-      sb = mfma16(kb[s], qf[s], sb);
-    }
-    // scale into the log2 domain + mask tokens past the context
-    float pa[4], pb[4];
-    float mx = -1e30f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ta = blkA * kBS + 4 * g + r, tb = blkB * kBS + 4 * g + r;
-      pa[r] = ta < ctx ? sa[r] * sl2 : -INFINITY;
-      pb[r] = (hasB && tb < ctx) ? sb[r] * sl2 : -INFINITY;
-      mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float alpha = exp2f(m - m_new);
-    float rs = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      pa[r] = exp2f(pa[r] - m_new);
-      pb[r] = exp2f(pb[r] - m_new);
-      rs += pa[r] + pb[r];
-    }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = m_new;
-    // rescale O: O row (4g + r) belongs to row 4g+r, whose alpha lives in lane 4g+r
-    float al[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) al[r] = __shfl(alpha, 4 * g + r, 64);
-#pragma unroll
-    for (int n = 0; n < 8; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[n][r] *= al[r];
-    // P operand (A): k order {A: 4g+0..3, B: 4g+0..3}
-    short8 pf;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      pf[r] = (short)f2bf(pa[r]);
-      pf[4 + r] = (short)f2bf(pb[r]);
-    }
-    // cache slots past the context may hold stale/uninitialised bits (possibly NaN): P = 0 there,
-    // but 0 * NaN = NaN, so those V elements are zeroed by select, not by arithmetic.
-    bool okA[4], okB[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      okA[r] = blkA * kBS + 4 * g + r < ctx;
-      okB[r] = hasB && (blkB * kBS + 4 * g + r < ctx);
-    }
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      short8 vf;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        vf[r] = okA[r] ? va[n][r] : (short)0;
-        vf[4 + r] = okB[r] ? vb[n][r] : (short)0;
-      }
-      o[n] = mfma16(pf, vf, o[n]);
-    }
+    PairRegs r;
+    const bool hasB = pair + 1 < blk_end;
+    load_pair(r, p, bt, kvh, pair, hasB, r16, g);
+    attend_pair(r, pair, hasB, ctx, qf, sl2, g, o, m, l);
   }
 
   // ---- combine the 4 waves through LDS ----
@@ -254,6 +342,314 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   }
 }
 
+// One WAVE per item, kWaves independent items per workgroup, no LDS and no barriers: the
+// large-batch path (B * Hkv * splits >= kWaveKernelMinItems).  Item = tile (PREFIX) or
+// (sequence, split).  The block-pair loop is software-pipelined two deep in registers (the loads of
+// pair i+1 are in flight while pair i is on the MFMAs), and the epilogue merges the prefix partial
+// and writes straight from the accumulator layout.
+template <bool PREFIX>
+__global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, int num_items) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int item = blockIdx.x * kWaves + wid, kvh = blockIdx.y;
+  if (item >= num_items) return;  // the whole wave leaves; nothing below synchronises
+  const int r16 = lane & 15, g = lane >> 4;
+
+  int row_seq0, nrows, blk_begin, blk_end, ctx, split = 0;
+  if (PREFIX) {
+    const int* t = p.tiles + 3 * item;
+    row_seq0 = t[0];
+    nrows = t[1] * p.G;
+    blk_begin = 0;
+    blk_end = t[2];
+    ctx = blk_end * kBS;
+    if (nrows == 0) return;
+  } else {
+    row_seq0 = item / p.num_splits;
+    split = item - row_seq0 * p.num_splits;
+    nrows = p.G;
+    ctx = p.ctx_lens[row_seq0];
+    const int nblk_total = (ctx + kBS - 1) / kBS;
+    const int b0 = p.start_blk ? p.start_blk[row_seq0] : 0;
+    const int per_split = (nblk_total - b0 + p.num_splits - 1) / p.num_splits;
+    blk_begin = b0 + split * per_split;
+    blk_end = min(nblk_total, blk_begin + per_split);
+  }
+  const int* bt = p.block_tables + (size_t)row_seq0 * p.max_blocks;
+
+  short8 qf[4];
+  load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
+  const float sl2 = p.scale * kLog2e;
+
+  float4v o[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = float4v{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+
+  // Rolling one-set pipeline: the K registers are refilled with pair i+1 as soon as the S MFMAs
+  // of pair i have consumed them, the V registers right after the PV MFMAs — a pair's loads are in
+  // flight under the previous pair's softmax / PV work at ~1/2 the registers of a double buffer.
+  PairRegs r;
+  int pair = blk_begin;
+  if (pair < blk_end) {
+    load_pair_k(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g);
+    load_pair_v(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g);
+  }
+  while (pair < blk_end) {
+    const bool hasB = pair + 1 < blk_end;
+    const int nxt = pair + 2;
+    float4v sa, sb;
+    pair_scores(r, qf, sa, sb);
+    if (nxt < blk_end) load_pair_k(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g);
+    short8 pf;
+    pair_softmax(sa, sb, pair, hasB, ctx, true, sl2, g, o, m, l, pf);
+    pair_values(r, pf, pair, hasB, ctx, g, o);
+    if (nxt < blk_end) load_pair_v(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g);
+    pair = nxt;
+  }
+
+  // epilogue: lane (g, r16) owns rows 4g+i, dims 16n+r16; row stats live in lane (row)
+  const bool merge_prefix = !PREFIX && p.num_splits == 1 && p.start_blk && p.start_blk[row_seq0] > 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int R = 4 * g + i;
+    const float li = __shfl(l, R, 64), mi = __shfl(m, R, 64);
+    if (R >= nrows) continue;
+    const int seq = PREFIX ? row_seq0 + R / p.G : row_seq0;
+    const int hq = kvh * p.G + (PREFIX ? R % p.G : R);
+    const size_t bh = (size_t)seq * p.Hq + hq;
+    if (PREFIX || p.num_splits > 1) {
+      const float inv = li > 0.f ? 1.f / li : 0.f;
+      float* dst = PREFIX ? p.pre_o + bh * kD : p.part_o + (bh * p.num_splits + split) * kD;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) dst[16 * n + r16] = o[n][i] * inv;
+      if (r16 == 0) {
+        const float lse = li > 0.f ? mi + log2f(li) : -INFINITY;
+        if (PREFIX)
+          p.pre_lse[bh] = lse;
+        else
+          p.part_lse[bh * p.num_splits + split] = lse;
+      }
+    } else {
+      float fo = 1.f, fp = 0.f, L = li;
+      const float* pre = nullptr;
+      if (merge_prefix) {
+        const float plse = p.pre_lse[bh];
+        const float M = fmaxf(mi, plse);
+        fo = exp2f(mi - M);
+        fp = exp2f(plse - M);
+        L = li * fo + fp;
+        pre = p.pre_o + bh * kD;
+      }
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      bf16_t* dst = p.out + bh * kD;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        float v = o[n][i] * fo;
+        if (pre) v += fp * pre[16 * n + r16];
+        dst[16 * n + r16] = f2bf(v * inv);
+      }
+    }
+  }
+}
+
+// B * Hkv * splits at/above which the wave-per-item kernel runs (tests lower it to cover both paths)
+static int g_wave_min_items = 2048;
+
+// ---------------------------------------------------------------------------------------------
+// CASCADE kernel: the shared-prompt pass and every sequence's own suffix in ONE launch, no partials.
+//
+// Workgroup = kCWaves waves = one SUPER-TILE (row_start, nseq, prefix_blocks) x one KV head; wave w
+// owns sequences row_start + w*per .. (+per), per = 16/G, as its 16 MFMA query rows (seq, head).
+//  phase 1 (prefix): the super-tile's sequences share their first `prefix_blocks` blocks.  The WG
+//    stages kCPairs block pairs at a time into LDS (K rows XOR-swizzled by 16 B chunk, V^T linear),
+//    and every wave runs the pair loop for its 16 rows out of LDS: the prompt's KV is read from HBM
+//    once per (super-tile, head) — 32 sequences for Llama-3's G=4 — instead of once per sequence.
+//  phase 2 (suffix): each wave walks its sequences' own blocks from global memory (rolling register
+//    pipeline that crosses sequence boundaries), masking the rows of the other sequences
+//    (row_on), so the prefix and suffix softmax states merge in registers.
+//  epilogue: bf16 output straight from the accumulator layout.
+// Super-tiles with prefix_blocks = 0 are plain decode for up to kCWaves*per unrelated sequences.
+constexpr int kCWaves = 8;
+constexpr int kCPairs = 8;                         // pairs staged per LDS chunk (128 KiB)
+constexpr int kCRounds = 1024 / (kCWaves * 64);     // 16 B loads per thread per pair
+constexpr int kPairBytes = 4 * kBS * kD * 2;        // K_A, K_B, V_A^T, V_B^T = 16 KiB
+constexpr int kSegBytes = kBS * kD * 2;             // 4 KiB
+
+struct CascadeParams {
+  const bf16_t* q;
+  const bf16_t* kc;
+  const bf16_t* vc;
+  const int* block_tables;
+  const int* ctx_lens;
+  const int* tiles;  // [max_tiles, 3]
+  bf16_t* out;       // [B, Hq, D]
+  int q_stride, Hq, Hkv, G, max_blocks;
+  float scale;
+};
+
+__global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(CascadeParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // heads are the fast grid dimension: the real tiles (a prefix of the table) are dispatched first,
+  // the graph-capture slack (nseq = 0 entries) last
+  const int tile = blockIdx.y, kvh = blockIdx.x;
+  const int* t = p.tiles + 3 * tile;
+  const int row_start = t[0], nseq = t[1], pblk = t[2];
+  if (nseq <= 0) return;  // uniform for the whole workgroup, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int per = 16 / p.G;
+  const int s0 = row_start + wid * per;
+  const int nseq_w = max(0, min(per, nseq - wid * per));
+  const int nrows = nseq_w * p.G;
+  const float sl2 = p.scale * kLog2e;
+  const size_t kv_head_stride = (size_t)kBS * kD;
+
+  short8 qf[4];
+  DecodeParams qp{};
+  qp.q = p.q;
+  qp.q_stride = p.q_stride;
+  qp.G = p.G;
+  load_q<true>(qf, qp, s0, nrows, kvh, r16, g);
+
+  float4v o[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) o[n] = float4v{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+
+  // ---- phase 1: shared prefix through LDS ----
+  auto phase1 = [&]() {
+  const int* bt0 = p.block_tables + (size_t)row_start * p.max_blocks;
+  const int pctx = pblk * kBS;
+  for (int c0 = 0; c0 < pblk; c0 += 2 * kCPairs) {
+    const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
+    __syncthreads();  // previous chunk fully consumed
+    // LDS-DMA (global_load_lds_dwordx4): wave-instruction (pair, round) writes 1 KiB contiguously,
+    // lane-linear; the K image's XOR swizzle is applied to the SOURCE address instead.
+#pragma unroll
+    for (int pi = 0; pi < kCPairs; ++pi) {
+#pragma unroll
+      for (int rd = 0; rd < kCRounds; ++rd) {
+        const int u = rd * (kCWaves * 64) + tid;  // 16 B unit of the pair's 16 KiB image
+        const int seg = u >> 8, pos = u & 255;
+        const int blk = c0 + 2 * pi + (seg & 1);
+        if (pi < npairs && blk < pblk) {  // wave-uniform: a wave's 64 units lie in one segment
+          const int phys = bt0[blk];
+          const unsigned char* src =
+              reinterpret_cast<const unsigned char*>(((seg < 2) ? p.kc : p.vc) +
+                                                     ((size_t)phys * p.Hkv + kvh) * kv_head_stride);
+          if (seg < 2) {  // K [16 tok][256 B]: 16 B chunk XOR row
+            const int row = pos >> 4, pch = pos & 15;
+            src += row * 256 + ((pch ^ row) << 4);
+          } else {  // V^T [128 dim][32 B]: 16 B halves XOR row bit 3 (ds_read_b64 lane groups of 32)
+            const int row = pos >> 1, h = pos & 1;
+            src += row * 32 + ((h ^ ((row >> 3) & 1)) << 4);
+          }
+          unsigned char* dst = smem + pi * kPairBytes + (rd * (kCWaves * 64) + wid * 64) * 16;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (nrows > 0) {
+      for (int pi = 0; pi < npairs; ++pi) {
+        const int blkA = c0 + 2 * pi;
+        const bool hasB = blkA + 1 < pblk;
+        const unsigned char* pb = smem + pi * kPairBytes;
+        PairRegs r;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ch = ((4 * s + g) ^ r16) << 4;
+          r.ka[s] = *reinterpret_cast<const short8*>(pb + r16 * 256 + ch);
+          r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          const int off = (16 * n + r16) * (kBS * 2) + ((((g >> 1) ^ (r16 >> 3)) & 1) << 4) + ((g & 1) << 3);
+          r.va[n] = *reinterpret_cast<const short4v*>(pb + 2 * kSegBytes + off);
+          r.vb[n] = *reinterpret_cast<const short4v*>(pb + 3 * kSegBytes + off);
+        }
+        attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
+      }
+    }
+  }
+
+  };
+
+  // ---- phase 2: each sequence's own blocks, rolling pipeline across the wave's sequences ----
+  auto phase2 = [&]() {
+  if (nrows > 0) {
+    auto seq_end = [&](int j) { return (p.ctx_lens[s0 + j] + kBS - 1) / kBS; };
+    // current position (j, pair); skip sequences with an empty suffix
+    int j = 0, pair = pblk, end = seq_end(0);
+    while (j < nseq_w && pair >= end) {
+      ++j;
+      if (j < nseq_w) end = seq_end(j);
+    }
+    if (j < nseq_w) {
+      DecodeParams lp{};
+      lp.kc = p.kc;
+      lp.vc = p.vc;
+      lp.Hkv = p.Hkv;
+      PairRegs r;
+      const int* bt = p.block_tables + (size_t)(s0 + j) * p.max_blocks;
+      load_pair_k(r, lp, bt, kvh, pair, pair + 1 < end, r16, g);
+      load_pair_v(r, lp, bt, kvh, pair, pair + 1 < end, r16, g);
+      while (j < nseq_w) {
+        const int ctx = p.ctx_lens[s0 + j];
+        const bool hasB = pair + 1 < end;
+        const bool row_on = r16 < nrows && r16 / p.G == j;
+        // next position
+        int j2 = j, pair2 = pair + 2, end2 = end;
+        while (j2 < nseq_w && pair2 >= end2) {
+          ++j2;
+          if (j2 < nseq_w) {
+            end2 = seq_end(j2);
+            pair2 = pblk;
+          }
+        }
+        const int* bt2 = p.block_tables + (size_t)(s0 + min(j2, nseq_w - 1)) * p.max_blocks;
+        float4v sa, sb;
+        pair_scores(r, qf, sa, sb);
+        if (j2 < nseq_w) load_pair_k(r, lp, bt2, kvh, pair2, pair2 + 1 < end2, r16, g);
+        short8 pf;
+        pair_softmax(sa, sb, pair, hasB, ctx, row_on, sl2, g, o, m, l, pf);
+        pair_values(r, pf, pair, hasB, ctx, g, o);
+        if (j2 < nseq_w) load_pair_v(r, lp, bt2, kvh, pair2, pair2 + 1 < end2, r16, g);
+        j = j2;
+        pair = pair2;
+        end = end2;
+      }
+    }
+  }
+
+  };
+
+  // Softmax merging is order-free: odd workgroups stream their suffixes first, so a CU's two
+  // resident workgroups overlap one's LDS-bound prefix phase with the other's HBM-bound suffix.
+  if (tile & 1) {
+    phase2();
+    phase1();
+  } else {
+    phase1();
+    phase2();
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int R = 4 * g + i;
+    const float li = __shfl(l, R, 64);
+    if (R >= nrows) continue;
+    const int seq = s0 + R / p.G;
+    const int hq = kvh * p.G + R % p.G;
+    const float inv = li > 0.f ? 1.f / li : 0.f;
+    bf16_t* dst = p.out + ((size_t)seq * p.Hq + hq) * kD;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) dst[16 * n + r16] = f2bf(o[n][i] * inv);
+  }
+}
+
 // Combine split-K partials (+ the prefix partial): out[b, hq, :] = sum_s 2^(lse_s - LSE) o_s
 __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(const float* __restrict__ part_o,
                                                                   const float* __restrict__ part_lse,
@@ -285,6 +681,12 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(const float* _
 
 }  // namespace lwc
 
+extern "C" int lwc_set_decode_wave_min_items(int n) {
+  const int old = lwc::g_wave_min_items;
+  lwc::g_wave_min_items = n;
+  return old;
+}
+
 // Plain / suffix decode.  start_blk, pre_o, pre_lse may be null (no prefix sharing).
 extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                                 const int* ctx_lens, void* out, float* part_o, float* part_lse, int B, int Hq,
@@ -298,7 +700,12 @@ extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, con
   DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, (bf16_t*)out,
                  part_o, part_lse, nullptr, start_blk, (float*)pre_o, (float*)pre_lse, q_stride, Hq, Hkv, Hq / Hkv,
                  max_blocks, num_splits, 0, scale};
-  paged_decode_kernel<false><<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p);
+  if ((long)B * Hkv * num_splits >= g_wave_min_items) {
+    const int items = B * num_splits;
+    paged_decode_wave_kernel<false><<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items);
+  } else {
+    paged_decode_kernel<false><<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p);
+  }
   if (num_splits > 1)
     paged_decode_reduce_kernel<<<B * Hq, kD, 0, s>>>(part_o, part_lse, start_blk, pre_o, pre_lse, (bf16_t*)out,
                                                      num_splits, Hq);
@@ -317,6 +724,30 @@ extern "C" int lwc_paged_decode_prefix(const void* q, int q_stride, const void* 
   if (max_tiles == 0) return 0;
   DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, nullptr, nullptr, nullptr,
                  nullptr, tiles, nullptr, pre_o, pre_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, 1, max_tiles, scale};
-  paged_decode_kernel<true><<<dim3(max_tiles, Hkv, 1), 256, 0, s>>>(p);
+  paged_decode_wave_kernel<true><<<dim3((max_tiles + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, max_tiles);
   return (int)hipGetLastError();
 }
+
+// Cascade decode (shared prefix + suffix in one launch); tiles = [max_tiles, 3] super-tiles
+// (row_start, nseq <= kCWaves*16/G, prefix_blocks), unused entries nseq = 0.
+extern "C" int lwc_paged_decode_cascade(const void* q, int q_stride, const void* kc, const void* vc,
+                                        const int* block_tables, const int* ctx_lens, const int* tiles, int max_tiles,
+                                        void* out, int Hq, int Hkv, int D, int BS, int max_blocks, float scale,
+                                        hipStream_t s) {
+  using namespace lwc;
+  if (D != kD || BS != kBS || Hq % Hkv != 0 || 16 % (Hq / Hkv) != 0) return -1;
+  if (max_tiles == 0) return 0;
+  CascadeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, tiles,
+                  (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale};
+  const size_t lds = (size_t)kCPairs * kPairBytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)paged_decode_cascade_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr_set = true;
+  }
+  paged_decode_cascade_kernel<<<dim3(Hkv, max_tiles), kCWaves * 64, lds, s>>>(p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_cascade_rows_per_tile(int G) { return lwc::kCWaves * (16 / G); }

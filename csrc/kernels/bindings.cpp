@@ -17,8 +17,12 @@ int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStrea
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
 int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
                      int, int, int, int, int, int, float, const int*, const float*, const float*, hipStream_t);
+int lwc_set_decode_wave_min_items(int);
 int lwc_paged_decode_prefix(const void*, int, const void*, const void*, const int*, const int*, const int*, int,
                             float*, float*, int, int, int, int, int, int, float, hipStream_t);
+int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const int*, const int*, const int*, int, void*,
+                             int, int, int, int, int, float, hipStream_t);
+int lwc_cascade_rows_per_tile(int);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
@@ -213,6 +217,26 @@ void paged_decode_prefix(const at::Tensor& q, const at::Tensor& k_cache, const a
            "paged_decode_prefix");
 }
 
+void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                          const at::Tensor& block_tables, const at::Tensor& ctx_lens, const at::Tensor& tiles,
+                          at::Tensor& out, int64_t Hq, double scale) {
+  // tiles: [max_tiles, 3] int32 super-tiles (row_start, nseq, prefix_blocks), nseq <= cascade_rows_per_tile(G);
+  // the engine builds them on the host (rows must stay < B: the kernel trusts the table).
+  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out); CHECK_CONTIG(out);
+  CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt); CHECK_DTYPE(tiles, at::kInt);
+  CHECK_CONTIG(tiles); CHECK_CONTIG(block_tables); CHECK_CONTIG(ctx_lens);
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 3, "paged_decode_cascade: tiles must be [T, 3]");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode_cascade: q must be [B, >=Hq*D] rows");
+  const int B = (int)q.size(0), D = (int)k_cache.size(3), Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
+  TORCH_CHECK(block_tables.size(0) >= B && ctx_lens.numel() >= B, "paged_decode_cascade: batch tables too short");
+  TORCH_CHECK(out.numel() >= (int64_t)B * Hq * D, "paged_decode_cascade: out too small");
+  CHECK_RC(lwc_paged_decode_cascade(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                    block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), tiles.data_ptr<int>(),
+                                    (int)tiles.size(0), out.data_ptr(), (int)Hq, Hkv, D, BS,
+                                    (int)block_tables.size(1), (float)scale, cur_stream()),
+           "paged_decode_cascade");
+}
+
 void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                        const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, int64_t D,
                        double scale, bool causal) {
@@ -328,6 +352,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding", &embedding);
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);
+  m.def("paged_decode_cascade", &paged_decode_cascade);
+  m.def("cascade_rows_per_tile", &lwc_cascade_rows_per_tile, "sequences per cascade super-tile for a GQA ratio G");
+  m.def("set_decode_wave_min_items", &lwc_set_decode_wave_min_items,
+        "B*Hkv*splits threshold of the wave-per-item decode kernel; returns the previous value");
   m.def("paged_decode_prefix", &paged_decode_prefix);
   m.def("prefill_attention", &prefill_attention);
   m.def("sample", &sample);

@@ -104,7 +104,7 @@ class _GraphBucket:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.logits: Optional[torch.Tensor] = None
         segs: List[Tuple[str, int]] = [("block_tables", B * width), ("ctx_lens", B), ("slots", B), ("positions", B),
-                                       ("tokens", B), ("tiles", max_tiles * 3), ("start_blk", B)]
+                                       ("tokens", B), ("tiles", max(1, max_tiles) * 3)]
         segs += [(n, B) for n in _F32_PARAMS + _I32_PARAMS]
         segs += [("seeds", 2 * B), ("offsets", 2 * B)]
         self.off: Dict[str, Tuple[int, int]] = {}
@@ -134,7 +134,7 @@ class _GraphBucket:
                 x = x.view(i64)
             v[name] = x
         v["block_tables"] = v["block_tables"].reshape(self.B, self.width)
-        v["tiles"] = v["tiles"].reshape(self.max_tiles, 3)
+        v["tiles"] = v["tiles"].reshape(max(1, self.max_tiles), 3)
         return v
 
     def outputs(self, parity: int, K: int):
@@ -153,6 +153,61 @@ class _GraphBucket:
         return (tok, lp, ids, lps), o[:need], self.out_host[parity][:need]
 
 
+def cascade_table_size(B: int, per_tile: int) -> int:
+    """Rows of a bucket's cascade tile table: one tile per `per_tile` sequences plus slack for group
+    boundaries (ragged groups beyond the slack degrade to plain rows, see :func:`cascade_tiles`).
+    Slack entries are launched workgroups that exit at once, so it is kept small."""
+    return -(-B // per_tile) + min(B // 8, 32)
+
+
+def cascade_tiles(runs: List[Tuple[int, int, int]], per_tile: int, tiles: np.ndarray) -> int:
+    """Fill `tiles` [T, 3] with cascade super-tiles (row_start, nseq, prefix_blocks).
+
+    `runs` are the batch's consecutive (start, count, prompt_blocks) sequence runs, one per group.
+    Runs of >= 2 sequences with a non-empty prompt block prefix get their own tiles (<= per_tile
+    sequences each); everything else is packed into plain tiles (prefix_blocks = 0).  If the table
+    would overflow, the remaining groups degrade to plain rows.  Returns the number of tiles."""
+    T = tiles.shape[0]
+    tiles[:] = 0
+    nt = 0
+    plain: List[int] = []  # [start, end) of the pending plain stretch
+
+    def emit(r0: int, n: int, pblk: int):
+        nonlocal nt
+        for a in range(r0, r0 + n, per_tile):
+            if nt >= T:
+                raise RuntimeError("cascade plan: tile table overflow")
+            tiles[nt] = (a, min(per_tile, r0 + n - a), pblk)
+            nt += 1
+
+    def flush():
+        if plain:
+            emit(plain[0], plain[1] - plain[0], 0)
+            plain.clear()
+
+    total = sum(n for _, n, _ in runs)
+    for idx, (start, n, pblk) in enumerate(runs):
+        shared = n >= 2 and pblk > 0
+        if shared:
+            # tiles this run needs + a worst-case plain tail must still fit
+            rest = total - (start + n)
+            pending = -(-(plain[1] - plain[0]) // per_tile) if plain else 0
+            need = pending + -(-n // per_tile) + -(-rest // per_tile)
+            if nt + need > T:
+                shared = False
+        if shared:
+            flush()
+            emit(start, n, pblk)
+        else:
+            if plain and plain[1] == start:
+                plain[1] = start + n
+            else:
+                flush()
+                plain.extend([start, start + n])
+    flush()
+    return nt
+
+
 class _Step:
     """A launched (not yet processed) decode step."""
 
@@ -164,7 +219,8 @@ class _Step:
 class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
-                 use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True):
+                 use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
+                 cascade_min_batch: int = 128):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -183,6 +239,9 @@ class LLMEngine:
         self.free_blocks_unreserved = num_blocks
         self.use_graphs = use_graphs
         self.prefix_sharing = prefix_sharing
+        # decode batches >= this bucket use the cascade (shared-prompt) attention kernel; smaller ones
+        # the split-K kernel, which spreads a few long contexts over more workgroups
+        self.cascade_min_batch = cascade_min_batch
         self.buckets: Dict[int, _GraphBucket] = {}
         self.inflight: Optional[_Step] = None
         self._step_no = 0
@@ -344,34 +403,27 @@ class LLMEngine:
             # split-K so that a launch has >= ~1024 (batch, kv-head, split) workgroups
             splits = max(1, min(16, -(-1024 // (Bb * self.cfg.kv_heads))))
             splits = min(splits, max(1, self.width // 4))
-            per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
-            bk = _GraphBucket(Bb, self.width, splits, -(-Bb // per), self.device)
+            max_tiles = 0
+            if self.prefix_sharing and Bb >= self.cascade_min_batch:
+                per = ops.cascade_rows_per_tile(self.cfg.heads // self.cfg.kv_heads)
+                max_tiles = cascade_table_size(Bb, per)
+            bk = _GraphBucket(Bb, self.width, splits, max_tiles, self.device)
             self.buckets[Bb] = bk
         return bk
 
-    def _prefix_plan(self, seqs: List[Sequence], tiles: np.ndarray, start: np.ndarray) -> None:
-        """Tiles for the prefix-shared attention pass: runs of consecutive sequences of one group
-        (forked from one prompt) share the prompt's full blocks; each tile packs <= 16/G of them.
-        Unused tiles have nseq = 0."""
-        tiles[:] = 0
-        start[:] = 0
-        per = max(1, 16 // (self.cfg.heads // self.cfg.kv_heads))
-        nt, i, B = 0, 0, len(seqs)
+    def _cascade_plan(self, seqs: List[Sequence], tiles: np.ndarray) -> None:
+        """Super-tiles of the cascade decode kernel (see :func:`cascade_tiles`): runs of consecutive
+        sequences forked from one prompt share the prompt's full blocks."""
+        runs, i, B = [], 0, len(seqs)
         while i < B:
             g = seqs[i].group
             j = i
             while j < B and seqs[j].group is g:
                 j += 1
-            pblk = len(g.prompt_ids) // self.block_size
-            if j - i >= 2 and pblk > 0:
-                for r0 in range(i, j, per):
-                    n = min(per, j - r0)
-                    if nt >= tiles.shape[0]:
-                        raise RuntimeError("prefix plan: tile overflow")
-                    tiles[nt] = (r0, n, pblk)
-                    nt += 1
-                start[i:j] = pblk
+            runs.append((i, j - i, len(g.prompt_ids) // self.block_size))
             i = j
+        per = ops.cascade_rows_per_tile(self.cfg.heads // self.cfg.kv_heads)
+        cascade_tiles(runs, per, tiles)
 
     def _static_inputs(self, seqs: List[Sequence], key, bk: _GraphBucket) -> dict:
         """Per-composition inputs (prefix tiles, sampler parameters), rebuilt only when the batch
@@ -382,9 +434,9 @@ class LLMEngine:
         B = bk.B
         ps = [s.params for s in seqs]
         n = len(seqs)
-        st = {"tiles": np.zeros((bk.max_tiles, 3), np.int32), "start_blk": np.zeros(B, np.int32)}
-        if self.prefix_sharing:
-            self._prefix_plan(seqs, st["tiles"], st["start_blk"])
+        st = {"tiles": np.zeros((max(1, bk.max_tiles), 3), np.int32)}
+        if bk.max_tiles:
+            self._cascade_plan(seqs, st["tiles"])
 
         def col(vals, dt, fill=0):
             a = np.full(B, fill, dtype=dt)
@@ -414,7 +466,7 @@ class LLMEngine:
         def fwd():
             return self.model.decode(d["tokens"], d["positions"], d["slots"], d["block_tables"], d["ctx_lens"],
                                      self.cache, num_splits=bk.splits,
-                                     prefix=(d["tiles"], d["start_blk"]) if self.prefix_sharing else None)
+                                     cascade_tiles=d["tiles"] if bk.max_tiles else None)
 
         if not self.use_graphs:
             bk.logits = fwd()
@@ -445,7 +497,7 @@ class LLMEngine:
                             h["slots"], h["positions"])
         st = self._static_inputs(seqs, key, bk)
         if bk.host_static_key[parity] != key:
-            for name in ("tiles", "start_blk", "seeds") + _F32_PARAMS + _I32_PARAMS:
+            for name in ("tiles", "seeds") + _F32_PARAMS + _I32_PARAMS:
                 h[name][...] = st[name]
             bk.host_static_key[parity] = key
         prev = self.inflight

@@ -176,10 +176,13 @@ class LlamaModel:
         return h
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
-               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None) -> torch.Tensor:
+               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None,
+               cascade_tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One decode step for B sequences -> logits [B, V] bf16.  All inputs are device tensors
-        (int32), so the whole call can be captured in a hipGraph.  ``prefix`` = (tiles, start_blk)
-        enables the prefix-shared attention pass for sequences forked from one prompt."""
+        (int32), so the whole call can be captured in a hipGraph.  Attention variants:
+        ``cascade_tiles`` [T, 3] — one-launch cascade kernel (shared prompt blocks read once per
+        super-tile; the engine's large-batch path); ``prefix`` = (tiles, start_blk) — two-pass prefix +
+        suffix kernels; neither — split-K paged decode."""
         cfg = self.cfg
         x = ops.embedding(self.embed, tokens)
         B = tokens.shape[0]
@@ -192,6 +195,14 @@ class LlamaModel:
             tiles, start_blk = prefix
             pre_o = torch.empty(B * cfg.heads * cfg.head_dim, dtype=torch.float32, device=x.device)
             pre_lse = torch.empty(B * cfg.heads, dtype=torch.float32, device=x.device)
+
+        if cascade_tiles is not None:
+            def attn_fn(qkv, li):
+                return ops.paged_decode_cascade(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cascade_tiles,
+                                                cfg.heads, self.scale)
+
+            h = self._layers(x, cache, positions, slots, attn_fn)
+            return F.linear(h, self.lm_head)
 
         def attn_fn(qkv, li):
             if tiles is not None:

@@ -127,6 +127,12 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
     return out
 
 
+def set_decode_wave_min_items(n: int) -> int:
+    """Batch threshold (B * Hkv * splits) above which decode uses the wave-per-item kernel instead of
+    the 4-waves-per-sequence kernel; returns the previous value (tests force both paths)."""
+    return int(kernels().set_decode_wave_min_items(int(n)))
+
+
 def paged_decode_prefix(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                         tiles: torch.Tensor, pre_o: torch.Tensor, pre_lse: torch.Tensor, Hq: int,
                         scale: float) -> None:
@@ -134,6 +140,26 @@ def paged_decode_prefix(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.T
     the tile's sequences attend to their SHARED first `prefix_blocks` blocks in one MFMA pass
     (16 query rows = nseq x G heads); writes normalised partials + log2-sum-exp per (row, head)."""
     kernels().paged_decode_prefix(q, k_cache, v_cache, block_tables, tiles, pre_o, pre_lse, int(Hq), float(scale))
+
+
+def cascade_rows_per_tile(G: int) -> int:
+    """Sequences per cascade super-tile (8 waves x 16/G sequences)."""
+    return int(kernels().cascade_rows_per_tile(int(G)))
+
+
+def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                         ctx_lens: torch.Tensor, tiles: torch.Tensor, Hq: int, scale: float,
+                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Cascade decode attention in ONE launch (K3c): per super-tile (row_start, nseq, prefix_blocks) the
+    tile's sequences read their shared first `prefix_blocks` blocks once through LDS, then each
+    sequence's own blocks; softmax states merge in registers.  Every row < B must be covered by
+    exactly one tile (prefix_blocks = 0 for sequences that share nothing)."""
+    B = q.shape[0]
+    D = k_cache.shape[-1]
+    if out is None:
+        out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    kernels().paged_decode_cascade(q, k_cache, v_cache, block_tables, ctx_lens, tiles, out, int(Hq), float(scale))
+    return out
 
 
 def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int,

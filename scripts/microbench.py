@@ -85,6 +85,75 @@ def attention(dev):
             print(f"paged_decode B={B:4d} ctx={ctx_len:5d} splits={splits}: {us:8.1f} us {gb:7.0f} GB/s", flush=True)
 
 
+def attention_prefix(dev):
+    """The bench's decode attention: R groups of N candidates sharing a 256-token prompt, suffix of
+    `gen` tokens each — prefix (cascade) pass + suffix pass vs plain, both kernel paths."""
+    from llm_weighted_consensus_amd import ops
+
+    Hq, Hkv, D, BS = 32, 8, 128, 16
+    for (R, N, P, gen) in [(16, 64, 16, 64), (8, 64, 16, 64), (16, 64, 16, 120)]:
+        B = R * N
+        sblk = (gen + 1 + BS - 1) // BS
+        NB = R * P + B * sblk + 8
+        kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
+        vc = torch.randn(NB, Hkv, D, BS, device=dev).to(torch.bfloat16)
+        width = P + sblk
+        bt = torch.zeros(B, width, dtype=torch.int32)
+        for r in range(R):
+            bt[r * N:(r + 1) * N, :P] = torch.arange(r * P, (r + 1) * P, dtype=torch.int32)
+        bt[:, P:] = (R * P + torch.arange(B * sblk, dtype=torch.int32)).view(B, sblk)
+        bt = bt.to(dev)
+        ctx = torch.full((B,), P * BS + gen + 1, device=dev, dtype=torch.int32)
+        q = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+        per = 16 // (Hq // Hkv)
+        tl = [(r * N + j, min(per, N - j), P) for r in range(R) for j in range(0, N, per)]
+        tiles = torch.tensor(tl, dtype=torch.int32, device=dev)
+        start = torch.full((B,), P, dtype=torch.int32, device=dev)
+        pre_o = torch.empty(B * Hq * D, device=dev)
+        pre_lse = torch.empty(B * Hq, device=dev)
+        sc = 1 / math.sqrt(D)
+        for path, thr in (("wg4", 1 << 30), ("wave", 0)):
+            old = ops.set_decode_wave_min_items(thr)
+            t_pre = timeit(lambda: ops.paged_decode_prefix(q, kc, vc, bt, tiles, pre_o, pre_lse, Hq, sc))
+            t_suf = timeit(lambda: ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc, start_blk=start, pre_o=pre_o,
+                                                    pre_lse=pre_lse))
+            t_plain = timeit(lambda: ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc))
+            ops.set_decode_wave_min_items(old)
+            suf_gb = B * (gen + 1) * Hkv * D * 4 / (t_suf * 1e-6) / 1e9
+            print(f"prefix-decode R={R} N={N} P={P * BS} gen={gen} [{path}]: prefix {t_pre:7.1f} us  "
+                  f"suffix {t_suf:7.1f} us ({suf_gb:5.0f} GB/s)  plain {t_plain:7.1f} us", flush=True)
+        from llm_weighted_consensus_amd.engine.engine import cascade_table_size, cascade_tiles
+        import numpy as np
+
+        per_t = ops.cascade_rows_per_tile(Hq // Hkv)
+        ct = np.zeros((cascade_table_size(B, per_t), 3), dtype=np.int32)
+        nt = cascade_tiles([(r * N, N, P) for r in range(R)], per_t, ct)
+        ct_exact = torch.from_numpy(ct[:nt].copy()).to(dev)
+        ct = torch.from_numpy(ct).to(dev)
+        t_exact = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct_exact, Hq, sc))
+        print(f"  cascade exact grid ({nt} tiles): {t_exact:7.1f} us", flush=True)
+        t_c = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct, Hq, sc))
+        ref_o = ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc)
+        got = ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct, Hq, sc)
+        err = (got.float() - ref_o.float()).abs().max().item()
+        print(f"cascade-decode R={R} N={N} P={P * BS} gen={gen}: {t_c:7.1f} us  (max|diff| vs plain {err:.3g})",
+              flush=True)
+        # decomposition: prefix only (ctx = prompt), suffix only (own blocks moved to the front, no prefix)
+        ctx_p = torch.full((B,), P * BS, device=dev, dtype=torch.int32)
+        t_p = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx_p, ct, Hq, sc))
+        bt_s = torch.zeros_like(bt)
+        bt_s[:, :sblk] = bt[:, P:]
+        ctx_s = torch.full((B,), gen + 1, device=dev, dtype=torch.int32)
+        ct_s = np.zeros((cascade_table_size(B, per_t), 3), dtype=np.int32)
+        cascade_tiles([(0, B, 0)], per_t, ct_s)
+        ct_s = torch.from_numpy(ct_s).to(dev)
+        t_s = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt_s, ctx_s, ct_s, Hq, sc))
+        ctx_f = torch.full((B,), P * BS + gen + 1, device=dev, dtype=torch.int32)
+        t_f = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx_f, ct_s, Hq, sc))
+        print(f"  cascade parts: prefix-only {t_p:7.1f} us  suffix-only {t_s:7.1f} us  "
+              f"no-sharing full ctx {t_f:7.1f} us", flush=True)
+
+
 def sampler(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -127,6 +196,8 @@ def main():
         gemm_layouts(dev, [512, 1024])
     if "attn" in a.what:
         attention(dev)
+    if "prefix" in a.what:
+        attention_prefix(dev)
     if "sample" in a.what:
         sampler(dev)
     if "small" in a.what:

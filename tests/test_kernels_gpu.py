@@ -2,6 +2,7 @@
 import math
 
 import pytest
+import numpy as np
 import torch
 
 from tests import torch_ref as ref
@@ -95,8 +96,18 @@ def test_rope_kv_write(gpu):
     _close(vc[blk, :, :, off], v_ref, 0)
 
 
+@pytest.fixture(params=["wg4", "wave"])
+def decode_path(request, gpu):
+    """Run a decode test through the 4-waves-per-sequence kernel and the wave-per-item kernel."""
+    from llm_weighted_consensus_amd import ops
+
+    old = ops.set_decode_wave_min_items(1 << 30 if request.param == "wg4" else 0)
+    yield request.param
+    ops.set_decode_wave_min_items(old)
+
+
 @pytest.mark.parametrize("G,splits", [(4, 1), (4, 3), (1, 1), (8, 2)])
-def test_paged_decode(gpu, G, splits):
+def test_paged_decode(gpu, G, splits, decode_path):
     from llm_weighted_consensus_amd import ops
 
     torch.manual_seed(0)
@@ -135,8 +146,66 @@ def test_paged_decode(gpu, G, splits):
         _close(out[b], o, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("G", [4, 2, 1, 8])
+def test_paged_decode_cascade(gpu, G):
+    """One-launch cascade kernel (LDS-staged shared prompt + per-sequence suffix) == reference, over
+    groups spanning several super-tiles, odd prefix block counts, plain rows and NaN-poisoned slots."""
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.engine.engine import cascade_tiles
+
+    torch.manual_seed(11)
+    Hkv, D, BS = 2, 128, 16
+    Hq = Hkv * G
+    per = ops.cascade_rows_per_tile(G)
+    # (count, prefix blocks): a group larger than one super-tile, an odd prefix, a singleton, a
+    # group with an empty prefix (plain), and a short group
+    groups = [(per + 9, 2), (7, 5), (1, 4), (3, 0), (3, 3)]
+    B = sum(c for c, _ in groups)
+    width = 12
+    NB = 4 + sum(p + c * (width - p) for c, p in groups)
+    kc = _bf(NB, Hkv, BS, D, dev=gpu)
+    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    bt = torch.zeros(B, width, dtype=torch.int32)
+    ctx = torch.zeros(B, dtype=torch.int32)
+    nxt, row, runs = 0, 0, []
+    g = torch.Generator().manual_seed(3)
+    for c, pblk in groups:
+        shared = torch.arange(nxt, nxt + pblk, dtype=torch.int32)
+        nxt += pblk
+        for _ in range(c):
+            L = pblk * BS + int(torch.randint(1, (width - pblk) * BS, (1,), generator=g))
+            nb = -(-L // BS)
+            bt[row, :pblk] = shared
+            bt[row, pblk:nb] = torch.arange(nxt, nxt + nb - pblk, dtype=torch.int32)
+            nxt += nb - pblk
+            ctx[row] = L
+            row += 1
+        runs.append((row - c, c, pblk))
+    for b in range(B):  # poison slots past the context
+        L = int(ctx[b])
+        if L % BS:
+            last = int(bt[b, (L - 1) // BS])
+            kc[last, :, L % BS:, :] = float("nan")
+            vc[last, :, :, L % BS:] = float("nan")
+    tiles_np = np.zeros((-(-B // per) + len(groups) + 2, 3), dtype=np.int32)
+    nt = cascade_tiles(runs, per, tiles_np)
+    assert nt >= len(groups)
+    bt, ctx = bt.to(gpu), ctx.to(gpu)
+    tiles = torch.from_numpy(tiles_np).to(gpu)
+    q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
+    out = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D))
+    assert torch.isfinite(out.float()).all()
+    for b in range(B):
+        L = int(ctx[b])
+        toks = torch.arange(L, device=gpu)
+        blk = bt[b, toks // BS].long()
+        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], vc[blk, :, :, toks % BS],
+                          False, 1 / math.sqrt(D))[0]
+        _close(out[b], o, 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize("G,splits", [(4, 1), (4, 2), (2, 1)])
-def test_paged_decode_prefix_shared(gpu, G, splits):
+def test_paged_decode_prefix_shared(gpu, G, splits, decode_path):
     """Cascade path (shared-prefix MFMA pass + per-sequence suffix pass + merge) == plain decode."""
     from llm_weighted_consensus_amd import ops
 
