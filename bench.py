@@ -8,8 +8,9 @@ row-reduce) and pick the answer.  A bench *step* serves R requests per GPU end-t
 
 Multi-GPU (torchrun, one rank per GPU, RCCL): candidate-parallel — the global batch is R*W requests and
 rank r samples candidates [r*N/W, (r+1)*N/W) of EVERY request (per-GPU decode batch stays R*N: weak
-scaling); one all-gather of the candidate embeddings (C1) gives every rank all N candidates of every
-request, then the consensus kernel runs.  Timed region: K steps bracketed by barrier + synchronize on
+scaling).  Each rank prefills only its own R prompts; their KV blocks and last-token logits are
+all-gathered (C4) so no prompt is computed twice; one all-gather of the candidate embeddings (C1)
+gives every rank all N candidates of every request, then the consensus kernel runs.  Timed region: K steps bracketed by barrier + synchronize on
 both sides; the reported time is the max over ranks.
 
     python bench.py --gpus N --steps K --warmup W
@@ -53,6 +54,7 @@ def main():
     from llm_weighted_consensus_amd.models.config import decoder_config, encoder_config
     from llm_weighted_consensus_amd.models.llama import LlamaModel
     from llm_weighted_consensus_amd.parallel import dist as pdist
+    from llm_weighted_consensus_amd.parallel.prefill_share import all_gather_prefills
 
     info = pdist.init_from_env("cuda")
     W, rank = info.world, info.rank
@@ -80,10 +82,15 @@ def main():
         prompts = [torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=gen).tolist() for _ in range(G)]
         t0 = time.perf_counter()
         groups = []
+        shared = None
+        if W > 1:
+            # C4: prefill only this rank's R prompts, all-gather their KV blocks + last logits (RCCL)
+            kv, lg, nbl = engine.export_prefill(prompts[rank * R:(rank + 1) * R])
+            shared = all_gather_prefills(kv, lg, nbl)
         for gi, p in enumerate(prompts):
             sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True,
                                 seed=(step_idx * 1000003 + gi) * 131 + rank)
-            groups.append(engine.add_request(p, sp, n=n_local))
+            groups.append(engine.add_request(p, sp, n=n_local, prefilled=shared[gi] if shared else None))
         while engine.has_work():
             engine.step()
         t1 = time.perf_counter()
@@ -139,7 +146,8 @@ def main():
                 "prompt_len": a.prompt_len,
                 "gen_len": a.gen_len,
                 "sampling": "temperature 0.8, top_p 0.95",
-                "parallelism": f"candidate-parallel cp{W} (RCCL all-gather of embeddings)" if W > 1 else "single GPU",
+                "parallelism": (f"candidate-parallel cp{W} (RCCL all-gather of prompt KV + embeddings)" if W > 1
+                                else "single GPU"),
             },
         }
         print(json.dumps(out), flush=True)

@@ -83,6 +83,7 @@ class SequenceGroup:
         self.seqs = [Sequence(self, i, (base * 1000003 + i) & ((1 << 63) - 1)) for i in range(n)]
         self.bias_row = -1
         self.reserved_blocks = 0
+        self.prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     @property
     def finished(self) -> bool:
@@ -258,7 +259,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: Seq[int], params: SamplingParams, n: int = 1,
-                    callback: Optional[Callable[[TokenEvent], None]] = None) -> SequenceGroup:
+                    callback: Optional[Callable[[TokenEvent], None]] = None,
+                    prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SequenceGroup:
+        """Queue a request of `n` sequences.  ``prefilled`` = (kv [L, 2, nblocks, block_elems],
+        logits [V]) starts it from a prompt prefilled elsewhere (see :meth:`export_prefill`)."""
         params.validate(self.cfg.vocab_size)
         if len(prompt_ids) == 0:
             raise ValueError("empty prompt")
@@ -266,6 +270,7 @@ class LLMEngine:
             raise ValueError(f"prompt ({len(prompt_ids)}) + max_tokens ({params.max_tokens}) exceeds "
                              f"max_model_len ({self.max_model_len})")
         g = SequenceGroup(self, list(prompt_ids), params, n, callback)
+        g.prefilled = prefilled
         with self.lock:
             self.waiting.append(g)
         return g
@@ -327,26 +332,28 @@ class LLMEngine:
                     self.waiting.popleft()
                     raise RuntimeError("request needs more KV blocks than the cache holds")
                 break
-            if out and tokens + len(g.prompt_ids) > self.prefill_token_budget:
+            cost = len(g.prompt_ids) if g.prefilled is None else 0  # imported prompts cost no compute
+            if out and tokens + cost > self.prefill_token_budget:
                 break
             self.waiting.popleft()
             g.reserved_blocks = need
             self.free_blocks_unreserved -= need
-            tokens += len(g.prompt_ids)
+            tokens += cost
             out.append(g)
         return out
 
     # ------------------------------------------------------------------ prefill
-    def _prefill(self, groups: List[SequenceGroup]) -> List[TokenEvent]:
+    def _run_prefill(self, prompts: List[List[int]], parents: List[int]) -> torch.Tensor:
+        """Prefill packed prompts into freshly added transient sequences `parents`; returns the
+        last-token logits [len(prompts), V]."""
         dev = self.device
         toks, pos, slots, cu, last = [], [], [], [0], []
-        for g in groups:
-            L = len(g.prompt_ids)
-            parent = -g.id  # negative ids: transient prompt sequences
-            self.bm.add_sequence(parent, L)
-            toks.extend(g.prompt_ids)
+        for pid, p in zip(parents, prompts):
+            L = len(p)
+            self.bm.add_sequence(pid, L)
+            toks.extend(p)
             pos.extend(range(L))
-            slots.append(slots_range(self.bm, parent, 0, L))
+            slots.append(slots_range(self.bm, pid, 0, L))
             cu.append(cu[-1] + L)
             last.append(cu[-1] - 1)
         t_tok = torch.tensor(toks, dtype=torch.int32, device=dev)
@@ -354,21 +361,68 @@ class LLMEngine:
         t_slots = torch.from_numpy(np.concatenate(slots)).to(dev)
         t_cu = torch.tensor(cu, dtype=torch.int32, device=dev)
         t_last = torch.tensor(last, dtype=torch.int64, device=dev)
-        max_len = max(len(g.prompt_ids) for g in groups)
+        max_len = max(len(p) for p in prompts)
         logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache)
         self.stats["prefill_tokens"] += len(toks)
+        return logits
+
+    def export_prefill(self, prompts: List[List[int]]) -> Tuple[torch.Tensor, torch.Tensor, List[int]]:
+        """Prefill prompts WITHOUT starting any sequences and return what another engine needs to
+        start them without recomputing: (kv [L, 2, sum(nblocks), block_elems], logits [n, V], nblocks).
+
+        This is the multi-GPU candidate-parallel path: each rank prefills its own share of the
+        requests, the prompt KV blocks and last-token logits are all-gathered over RCCL, and every
+        rank then samples its candidates of every request from the imported prompts
+        (:meth:`add_request` with ``prefilled=``).  Must be called between steps."""
+        if self.inflight is not None:
+            raise RuntimeError("export_prefill while a decode step is in flight")
+        parents = [-(1 << 40) - i for i in range(len(prompts))]
+        need = sum((len(p) + self.block_size - 1) // self.block_size for p in prompts)
+        if need > self.free_blocks_unreserved:
+            raise RuntimeError("export_prefill: not enough free KV blocks")
+        logits = self._run_prefill(prompts, parents)
+        blocks: List[int] = []
+        nblocks: List[int] = []
+        for pid in parents:
+            tab = list(self.bm.block_table(pid))
+            blocks.extend(tab)
+            nblocks.append(len(tab))
+        idx = torch.tensor(blocks, dtype=torch.int64, device=self.device)
+        kv = self.cache.pool.index_select(2, idx)
+        for pid in parents:
+            self.bm.free_sequence(pid)
+        return kv, logits, nblocks
+
+    def _prefill(self, groups: List[SequenceGroup]) -> List[TokenEvent]:
+        dev = self.device
+        compute = [g for g in groups if g.prefilled is None]
+        imported = [g for g in groups if g.prefilled is not None]
+        logits_of: Dict[int, torch.Tensor] = {}
+        if compute:
+            lg = self._run_prefill([g.prompt_ids for g in compute], [-g.id for g in compute])
+            for i, g in enumerate(compute):
+                logits_of[g.id] = lg[i]
+        for g in imported:
+            kv, row = g.prefilled
+            parent = -g.id
+            self.bm.add_sequence(parent, len(g.prompt_ids))
+            tab = torch.tensor(list(self.bm.block_table(parent)), dtype=torch.int64, device=dev)
+            if kv.shape[2] != tab.numel():
+                raise ValueError(f"imported KV has {kv.shape[2]} blocks, prompt needs {tab.numel()}")
+            self.cache.pool.index_copy_(2, tab, kv)
+            logits_of[g.id] = row
+            g.prefilled = None  # drop the reference: the cache owns the data now
         # fork every group into its n sequences (shared prompt blocks), then sample first tokens
         rows, seqs = [], []
-        for gi, g in enumerate(groups):
+        for g in groups:
             parent = -g.id
             for s in g.seqs:
                 self.bm.fork(parent, s.id)
                 self._attach_rows(s)
-                rows.append(gi)
+                rows.append(logits_of[g.id])
                 seqs.append(s)
             self.bm.free_sequence(parent)
-        idx = torch.tensor(rows, dtype=torch.int64, device=dev)
-        events = self._sample_and_advance(logits.index_select(0, idx), seqs)
+        events = self._sample_and_advance(torch.stack(rows), seqs)
         for s in seqs:
             if not s.finished:
                 self.running.append(s)

@@ -40,18 +40,25 @@ _INFO = DistInfo()
 
 def init_from_env(device_type: Optional[str] = None, timeout_s: float = 600.0) -> DistInfo:
     """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/
-    MASTER_ADDR/MASTER_PORT).  Single-process when WORLD_SIZE is unset or 1."""
+    MASTER_ADDR/MASTER_PORT).  Single-process when WORLD_SIZE is unset or 1.
+
+    ``LWC_SHARE_ONE_GPU=1`` is a rehearsal mode for one-GPU boxes: every rank uses GPU 0 and the
+    collectives run over gloo (staged through host memory), so the multi-rank code paths can be
+    exercised end to end where RCCL cannot put two ranks on one device."""
     global _INFO
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    share = os.environ.get("LWC_SHARE_ONE_GPU") == "1"
+    if share:
+        local = 0
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
         torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        backend = "nccl" if device_type == "cuda" and not share else "gloo"
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
@@ -74,20 +81,37 @@ def barrier() -> None:
             dist.barrier()
 
 
+def all_gather_flat(t: torch.Tensor) -> torch.Tensor:
+    """[*] per rank -> [world, *]: one all_gather_into_tensor on the flattened buffer (the 1-D form
+    works for RCCL and gloo alike; GPU tensors under gloo are staged through host memory)."""
+    W = _INFO.world
+    flat = t.contiguous().view(-1)
+    if _INFO.backend == "gloo" and flat.is_cuda:
+        host = flat.cpu()
+        out = torch.empty(W * host.numel(), dtype=host.dtype)
+        dist.all_gather_into_tensor(out, host)
+        return out.to(t.device).view(W, *t.shape)
+    out = torch.empty(W * flat.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, flat)
+    return out.view(W, *t.shape)
+
+
 def all_gather(t: torch.Tensor) -> torch.Tensor:
     """[*] per rank -> [world, *] (C1).  One collective on a contiguous buffer."""
     if not _INFO.enabled:
         return t.unsqueeze(0)
-    t = t.contiguous()
-    flat = t.view(-1)
-    out = torch.empty(_INFO.world * flat.numel(), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, flat)  # flat 1-D form works for RCCL and gloo alike
-    return out.view(_INFO.world, *t.shape)
+    return all_gather_flat(t)
 
 
 def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     if _INFO.enabled:
-        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        if _INFO.backend == "gloo" and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=rop)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=rop)
     return t
 
 

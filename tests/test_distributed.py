@@ -53,3 +53,48 @@ def test_candidate_parallel_gather_gloo():
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res)
     assert all(m == 1.0 for _, _, m in res)
+
+
+def _prefill_share_worker(rank, world, port, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+    from llm_weighted_consensus_amd.parallel.prefill_share import all_gather_prefills
+
+    pdist.init_from_env("cpu")
+    L, E, V = 3, 5, 7
+    # rank r owns r+1 prompts with r+2 ... blocks each: uneven counts exercise the padding path
+    nblocks = [rank + 2 + i for i in range(rank + 1)]
+    kv = torch.stack([torch.full((L, 2, E), 100.0 * rank + b) for b in range(sum(nblocks))], dim=2)
+    logits = torch.stack([torch.full((V,), 10.0 * rank + i) for i in range(len(nblocks))])
+    got = all_gather_prefills(kv, logits, nblocks)
+    ok = True
+    idx = 0
+    for r in range(world):
+        nbs = [r + 2 + i for i in range(r + 1)]
+        off = 0
+        for i, nb in enumerate(nbs):
+            k, lg = got[idx]
+            ok &= k.shape == (L, 2, nb, E)
+            ok &= bool((k[0, 0, :, 0] == torch.arange(off, off + nb) + 100.0 * r).all())
+            ok &= bool((lg == 10.0 * r + i).all())
+            off += nb
+            idx += 1
+    ok &= idx == len(got)
+    out_q.put((rank, ok))
+    pdist.shutdown()
+
+
+def test_prefill_share_all_gather_gloo():
+    """C4: uneven per-rank prompt/block counts are padded, gathered once and split back per prompt."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prefill_share_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)

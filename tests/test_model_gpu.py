@@ -98,3 +98,28 @@ def test_engine_sampling_seeded(tiny, gpu):
     b = eng.generate([tok.encode("abc")], sp, n=4)
     assert a == b
     assert len({tuple(x) for x in a[0]}) > 1  # different children sample differently
+
+
+def test_engine_export_import_prefill_equivalence(tiny, gpu):
+    """Candidate-parallel path: a prompt prefilled by export_prefill and started via add_request(prefilled=)
+    samples exactly what the engine's own prefill path samples (same seeds)."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.parallel.prefill_share import all_gather_prefills
+
+    tok = ByteTokenizer(tiny.cfg.vocab_size)
+    prompts = [tok.encode("z" * 40 + " exported prompt"), tok.encode("q" * 16)]  # partial + exact block
+    sp = SamplingParams(temperature=0.9, top_p=0.9, max_tokens=10, ignore_eos=True, seed=77)
+    a = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512)
+    want = a.generate(prompts, sp, n=3)
+    b = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512)
+    kv, lg, nbl = b.export_prefill(prompts)
+    assert b.bm.num_free == 256 and kv.shape[2] == sum(nbl) and len(nbl) == 2
+    shared = all_gather_prefills(kv, lg, nbl)  # single process: plain split
+    groups = [b.add_request(p, sp, n=3, prefilled=shared[i]) for i, p in enumerate(prompts)]
+    while b.has_work():
+        b.step()
+    got = [[list(s.tokens) for s in g.seqs] for g in groups]
+    assert got == want
+    assert b.bm.num_free == 256
