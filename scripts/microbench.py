@@ -67,6 +67,30 @@ def gemm_layouts(dev, Ms):
         print(f"square {n}: {us:8.1f} us {2 * n ** 3 / (us * 1e-6) / 1e12:7.1f} TF/s", flush=True)
 
 
+def gemm_backends(dev, Ms):
+    """The decode GEMM shapes through each BLAS backend torch can dispatch to on ROCm."""
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    for lib in ("cublaslt", "cublas", "ck"):
+        try:
+            torch.backends.cuda.preferred_blas_library(lib)
+        except Exception as e:  # noqa: BLE001
+            print(f"backend {lib}: unavailable ({e})", flush=True)
+            continue
+        for M in Ms:
+            for name, (N, K) in shapes.items():
+                x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+                try:
+                    us = timeit(lambda: F.linear(x, w), iters=20)
+                except Exception as e:  # noqa: BLE001
+                    print(f"backend {lib} M={M} {name}: failed ({type(e).__name__})", flush=True)
+                    continue
+                fl = 2 * M * N * K / (us * 1e-6) / 1e12
+                print(f"backend {lib:8s} M={M:4d} {name:8s}: {us:8.1f} us {fl:7.1f} TF/s", flush=True)
+    torch.backends.cuda.preferred_blas_library("cublaslt")
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -191,7 +215,9 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if "gemm" in a.what:
-        gemms(dev, [256, 512], tuned=os.environ.get("PYTORCH_TUNABLEOP_ENABLED") == "1")
+        gemms(dev, [int(m) for m in os.environ.get("MICRO_M", "256,512").split(",")], tuned=os.environ.get("PYTORCH_TUNABLEOP_ENABLED") == "1")
+    if "backends" in a.what:
+        gemm_backends(dev, [1024, 1536])
     if "layout" in a.what:
         gemm_layouts(dev, [512, 1024])
     if "attn" in a.what:
