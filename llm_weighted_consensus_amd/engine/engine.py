@@ -32,7 +32,7 @@ from ..models.llama import KVCache
 from .sampling import SamplingParams
 from .tokenizer import IncrementalDecoder
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 384, 512, 768, 1024, 1536, 2048)
+BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096)
 
 
 @dataclass
