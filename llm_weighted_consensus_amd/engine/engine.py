@@ -16,6 +16,7 @@ never run out of blocks and no preemption path is needed; 288 GB of HBM3E makes 
 """
 from __future__ import annotations
 
+import gc
 import itertools
 import random
 import threading
@@ -56,7 +57,7 @@ class Sequence:
         self.seed = seed
         self.n_launched = 0  # tokens sampled or in flight (the Philox offset of the next sample)
         self.tokens: List[int] = []
-        self.text = ""
+        self._text: Optional[str] = None  # streamed text (callback / stop strings), else decoded on demand
         self.finished = False
         self.finish_reason: Optional[str] = None
         self.count_row = -1
@@ -66,6 +67,21 @@ class Sequence:
     @property
     def params(self) -> SamplingParams:
         return self.group.params
+
+    @property
+    def text(self) -> str:
+        """Generated text.  Streamed incrementally when a callback or stop strings need it during
+        generation; otherwise decoded from the tokens on first access (no per-token host work)."""
+        if self._text is not None:
+            return self._text
+        tok = self.group.engine.tokenizer
+        eos = tok.eos_token_id
+        ids = [t for t in self.tokens if t != eos and t not in self.params.stop_token_ids]
+        return tok.decode(ids)
+
+    @text.setter
+    def text(self, v: str) -> None:
+        self._text = v
 
 
 class SequenceGroup:
@@ -221,7 +237,7 @@ class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
                  use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
-                 cascade_min_batch: int = 128):
+                 cascade_min_batch: int = 128, tune_gc: bool = True):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -256,6 +272,12 @@ class LLMEngine:
         self.bias: Optional[torch.Tensor] = None    # [max_batch, V] f32, lazily
         self.free_bias_rows = list(range(max_batch))
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0}
+        # step() returns TokenEvents only when asked (callbacks always get theirs)
+        self.collect_events = False
+        if tune_gc:
+            # thousands of live sequences make full collections (triggered by the per-token
+            # allocation churn) cost ~100 ms pauses that stall the GPU; raise the gen-0 threshold
+            gc.set_threshold(max(gc.get_threshold()[0], 200_000), 50, 100)
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: Seq[int], params: SamplingParams, n: int = 1,
@@ -701,10 +723,12 @@ class LLMEngine:
                              tk_ids.cpu().tolist() if K else None, tk_lp.cpu().tolist() if K else None)
 
     def _advance(self, seqs: List[Sequence], tok_h, lp_h, ids_h, lps_h) -> List[TokenEvent]:
-        """Host bookkeeping of one sampled token per sequence: append, grammar advance, detokenise,
-        stop / length checks, callbacks."""
+        """Host bookkeeping of one sampled token per sequence: append, grammar advance, stop / length
+        checks, and — only where someone consumes it — incremental detokenisation and a TokenEvent
+        (a callback, or ``collect_events``).  The common batch path is an append and two compares."""
         events = []
         eos = self.tokenizer.eos_token_id
+        collect = self.collect_events
         for i, s in enumerate(seqs):
             if s.finished:  # finished (or aborted) while this step was in flight: discard the row
                 continue
@@ -713,37 +737,45 @@ class LLMEngine:
             s.tokens.append(t)
             if s.constraint_state is not None:
                 s.constraint_state = p.constraint.advance(s.constraint_state, t)
+            cb = s.group.callback
             reason = None
             text = ""
             if t == eos and not p.ignore_eos:
                 reason = "stop"
-            elif t in p.stop_token_ids:
+            elif p.stop_token_ids and t in p.stop_token_ids:
                 reason = "stop"
-            else:
+            elif cb is not None or p.stop:
+                if s._text is None:
+                    s._text = ""
                 text = s.detok.push(t)
-                s.text += text
+                s._text += text
                 if p.stop:
                     for st in p.stop:
-                        k = s.text.find(st)
+                        k = s._text.find(st)
                         if k >= 0:
-                            cut = len(s.text) - k
+                            cut = len(s._text) - k
                             text = text[: max(0, len(text) - cut)]
-                            s.text = s.text[:k]
+                            s._text = s._text[:k]
                             reason = "stop"
                             break
             if reason is None and s.constraint_state is not None and p.constraint.is_done(s.constraint_state):
                 reason = "stop"
             if reason is None and len(s.tokens) >= p.max_tokens:
                 reason = "length"
+            if cb is None and not collect:
+                if reason is not None:
+                    self._finish(s, reason)
+                continue
             k = p.top_logprobs
             top = list(zip(ids_h[i][:k], lps_h[i][:k])) if k else []
             ev = TokenEvent(s, t, text, float(lp_h[i]), top)
             if reason is not None:
                 self._finish(s, reason)
                 ev.finished, ev.finish_reason = True, reason
-            events.append(ev)
-            if s.group.callback is not None:
-                s.group.callback(ev)
+            if collect:
+                events.append(ev)
+            if cb is not None:
+                cb(ev)
         return events
 
     def _finish(self, s: Sequence, reason: str) -> None:
