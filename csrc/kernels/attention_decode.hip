@@ -109,21 +109,6 @@ LWC_DEVICE void pair_scores(const PairRegs& r, const short8 (&qf)[4], float4v& s
 }
 
 // Online-softmax update (log2 domain) for the pair; rescales O and returns the P operand.
-// Reductions over the 4 lanes {l, l^16, l^32, l^48} holding one query row's tokens: two VALU
-// half-swaps (v_permlane32_swap / v_permlane16_swap, gfx950) instead of LDS ds_bpermute round trips.
-LWC_DEVICE float row_max4(float v) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
-}
-LWC_DEVICE float row_sum4(float v) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
-}
-
 // Lazy rescaling threshold (log2 units): the running max is only raised — and O rescaled — when
 // some row's new scores exceed it by more than this, so P <= 2^8 and most pairs skip the rescale.
 constexpr float kLazyRescale = 8.f;

@@ -1,5 +1,6 @@
 // K4 prefill_attn_varlen (causal, GQA) and K9c encoder_attn (bidirectional) — one flash-attention
-// forward for packed variable-length sequences (cu_seqlens), head_dim 64 or 128, bf16 in/out.
+// forward for packed variable-length sequences (cu_seqlens), head_dim 32 (bge-small), 64 or 128,
+// bf16 in/out.
 //
 // Workgroup = 4 waves = 64 query rows of one (sequence, query head); each wave owns 16 rows and
 // walks 32-key tiles that all 4 waves share through a double-buffered, XOR-swizzled LDS image
@@ -48,7 +49,8 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   constexpr int KS = D / 32;                // k-steps for S
   constexpr int NS = D / 16;                // n-subtiles for O
   constexpr int TILE_BYTES = kKT * D * 2;   // one K or V tile
-  constexpr int CH_PER_THREAD = kKT * CPR / 256;
+  constexpr int CHUNKS = kKT * CPR;            // 16 B chunks per K (or V) tile
+  constexpr int CH_PER_THREAD = (CHUNKS + 255) / 256;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];  // [buf][K|V]
 
   const int seq = blockIdx.x / p.max_tiles, qtile = blockIdx.x % p.max_tiles;
@@ -81,7 +83,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       const int c = threadIdx.x + 256 * i;
       const int row = c / CPR, ch = c % CPR;
       const int key = tile * kKT + row;
-      if (key < len) {
+      if (c < CHUNKS && key < len) {
         stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(s0 + key) * p.k_stride + kvh * D + ch * 8);
         stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(s0 + key) * p.v_stride + kvh * D + ch * 8);
       } else {
@@ -96,6 +98,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
 #pragma unroll
     for (int i = 0; i < CH_PER_THREAD; ++i) {
       const int c = threadIdx.x + 256 * i;
+      if (c >= CHUNKS) break;
       const int row = c / CPR, ch = c % CPR;
       const int off = (row * CPR + (ch ^ (row & (CPR - 1)))) * 16;
       *reinterpret_cast<uint4v*>(kb + off) = stk[i];
@@ -139,8 +142,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       pb[r] = vbk ? sb[r] * sl2 : -INFINITY;
       mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = row_max4(mx);
     const float m_new = fmaxf(m, mx);
     const float alpha = exp2f(m - m_new);
     float rs = 0.f;
@@ -150,9 +152,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       pb[r] = exp2f(pb[r] - m_new);
       rs += pa[r] + pb[r];
     }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
+    l = l * alpha + row_sum4(rs);
     m = m_new;
     float al[4];
 #pragma unroll
@@ -231,6 +231,8 @@ extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v
     prefill_attn_kernel<128><<<grid, 256, 0, s>>>(p);
   else if (D == 64)
     prefill_attn_kernel<64><<<grid, 256, 0, s>>>(p);
+  else if (D == 32)
+    prefill_attn_kernel<32><<<grid, 256, 0, s>>>(p);
   else
     return -1;
   return (int)hipGetLastError();

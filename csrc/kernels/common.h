@@ -83,6 +83,22 @@ LWC_DEVICE float block_max(float v, float* scratch) {
   return wave_max(r);
 }
 
+// Reductions over the 4 lanes {l, l^16, l^32, l^48} holding one query row's tokens: two VALU
+// half-swaps (v_permlane32_swap / v_permlane16_swap, gfx950) instead of LDS ds_bpermute round trips.
+LWC_DEVICE float row_max4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+LWC_DEVICE float row_sum4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): consecutive remapped ids land on the same XCD so neighbouring tiles share L2.
 LWC_DEVICE int xcd_remap(int orig, int nwg) {

@@ -12,6 +12,11 @@ consensus scorer.  Sequences are packed (cu_seqlens) — no padding FLOPs:
       h   = gelu(x W1^T + b1)                          hipBLASLt + K9b fused bias+GELU
       x   = LN(x + h W2^T + b2)
     e   = L2norm(pool(x))                               K9d (CLS for bge)
+
+On a CPU device the same weights run through :meth:`BertEncoder.forward_reference` (plain fp32
+PyTorch): that is BASELINE config 1 ("bge-small embeddings + cosine score on CPU, plumbing, no GPU")
+and the numerics oracle of the GPU tests — it is selected by the device, never as a fallback for a
+GPU whose kernels failed to load.
 """
 from __future__ import annotations
 
@@ -47,8 +52,8 @@ class EncLayer:
 class BertEncoder:
     def __init__(self, cfg: EncoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  weights_path: Optional[str] = None):
-        if cfg.head_dim not in (64, 128):
-            raise NotImplementedError(f"encoder head_dim {cfg.head_dim} (attention kernel supports 64/128)")
+        if cfg.head_dim not in (32, 64, 128):
+            raise NotImplementedError(f"encoder head_dim {cfg.head_dim} (attention kernel supports 32/64/128)")
         self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
         if weights_path:
             self._load(weights_path)
@@ -63,6 +68,8 @@ class BertEncoder:
 
         def rnd(*shape, s=0.02):
             return (torch.randn(*shape, generator=g, device=dev) * s).to(dt)
+        # NOTE: the same seed gives different weights on CPU and GPU generators; tests that compare
+        # the two paths build one model and move it with :meth:`to`.
 
         zeros = lambda *s: torch.zeros(*s, device=dev, dtype=dt)
         ones = lambda *s: torch.ones(*s, device=dev, dtype=dt)
@@ -98,8 +105,43 @@ class BertEncoder:
                 t(p + "intermediate.dense.bias"), t(p + "output.dense.weight"), t(p + "output.dense.bias"),
                 t(p + "output.LayerNorm.weight"), t(p + "output.LayerNorm.bias")))
 
+    def forward_reference(self, ids: torch.Tensor, positions: torch.Tensor, cu: torch.Tensor) -> torch.Tensor:
+        """Plain fp32 PyTorch forward of the same packed batch -> hidden [T, d] f32 (CPU path / oracle)."""
+        c = self.cfg
+        H, Dh, d = c.heads, c.head_dim, c.hidden
+        f32 = lambda t: t.float()
+        x = F.layer_norm(f32(self.word)[ids.long()] + f32(self.pos_type)[positions.long()], (d,),
+                         f32(self.emb_ln_g), f32(self.emb_ln_b), c.ln_eps)
+        bounds = cu.tolist()
+        for L in self.layers:
+            qkv = x @ f32(L.wqkv).t() + f32(L.bqkv)
+            a = torch.empty(x.shape[0], d, dtype=torch.float32, device=x.device)
+            for i in range(len(bounds) - 1):
+                s0, s1 = bounds[i], bounds[i + 1]
+                q = qkv[s0:s1, :d].view(-1, H, Dh)
+                k = qkv[s0:s1, d:2 * d].view(-1, H, Dh)
+                v = qkv[s0:s1, 2 * d:].view(-1, H, Dh)
+                p = (torch.einsum("qhd,khd->hqk", q, k) * self.scale).softmax(-1)
+                a[s0:s1] = torch.einsum("hqk,khd->qhd", p, v).reshape(-1, d)
+            x = F.layer_norm(x + a @ f32(L.wo).t() + f32(L.bo), (d,), f32(L.ln1_g), f32(L.ln1_b), c.ln_eps)
+            h = F.gelu(x @ f32(L.w1).t() + f32(L.b1))
+            x = F.layer_norm(x + h @ f32(L.w2).t() + f32(L.b2), (d,), f32(L.ln2_g), f32(L.ln2_b), c.ln_eps)
+        return x
+
+    @staticmethod
+    def pool_reference(h: torch.Tensor, cu: torch.Tensor, mode: str) -> torch.Tensor:
+        b = cu.tolist()
+        rows = []
+        for i in range(len(b) - 1):
+            seg = h[b[i]:b[i + 1]].float()
+            rows.append(seg[0] if mode == "cls" else seg[-1] if mode == "last" else seg.mean(0))
+        return F.normalize(torch.stack(rows), dim=-1)
+
     def forward_packed(self, ids: torch.Tensor, positions: torch.Tensor, cu: torch.Tensor, max_len: int) -> torch.Tensor:
-        """ids/positions [T] int32, cu [n+1] int32 -> hidden [T, d] bf16."""
+        """ids/positions [T] int32, cu [n+1] int32 -> hidden [T, d] bf16 (HIP kernels; CPU device:
+        the fp32 reference)."""
+        if self.device.type == "cpu":
+            return self.forward_reference(ids, positions, cu)
         c = self.cfg
         H, Dh, d = c.heads, c.head_dim, c.hidden
         T = ids.shape[0]
@@ -115,6 +157,17 @@ class BertEncoder:
             y = F.linear(h, L.w2, L.b2)
             x = ops.layernorm(y, L.ln2_g, L.ln2_b, c.ln_eps, residual=x)
         return x
+
+    def to(self, device, dtype=None) -> "BertEncoder":
+        """Copy of this encoder on another device (e.g. a GPU model's weights on CPU for the oracle)."""
+        out = BertEncoder.__new__(BertEncoder)
+        out.cfg, out.device, out.scale = self.cfg, torch.device(device), self.scale
+        out.dtype = dtype or self.dtype
+        mv = lambda t: t.to(device=device, dtype=out.dtype)
+        out.word, out.pos_type, out.emb_ln_g, out.emb_ln_b = (mv(self.word), mv(self.pos_type), mv(self.emb_ln_g),
+                                                             mv(self.emb_ln_b))
+        out.layers = [EncLayer(*[mv(getattr(L, f)) for f in EncLayer.__dataclass_fields__]) for L in self.layers]
+        return out
 
     def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
         cap = min(max_tokens or self.cfg.max_position, self.cfg.max_position)
@@ -138,4 +191,7 @@ class BertEncoder:
 
     def embed_packed(self, ids, pos, cu, max_len):
         h = self.forward_packed(ids, pos, cu, max_len)
+        if self.device.type == "cpu":
+            e = self.pool_reference(h, cu, self.cfg.pooling)
+            return e, e.to(torch.bfloat16)
         return ops.pool_l2norm(h, cu, POOL_MODES[self.cfg.pooling])

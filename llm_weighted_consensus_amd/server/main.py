@@ -40,11 +40,17 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         from ..models.config import decoder_config, encoder_config
         from ..models.llama import LlamaModel
 
-        dev = torch.device("cuda", cfg.gpu)
-        torch.cuda.set_device(dev)
+        if cfg.device == "cpu":
+            if cfg.models:
+                raise ValueError("LWC_DEVICE=cpu serves embedding models only (decoders need an MI355X)")
+            dev = torch.device("cpu")
+        else:
+            dev = torch.device("cuda", cfg.gpu)
+            torch.cuda.set_device(dev)
         for name, spec in cfg.embed_models.items():
             path, seed = _weights_spec(spec)
-            enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path)
+            enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
+                              dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
             embedders[name] = EmbeddingService(enc, name)
         for name, spec in cfg.models.items():
             path, seed = _weights_spec(spec)

@@ -266,7 +266,7 @@ def test_paged_decode_prefix_shared(gpu, G, splits, decode_path):
 
 
 @pytest.mark.parametrize("D,Hq,Hkv,causal", [(128, 8, 2, True), (64, 4, 4, False), (128, 4, 4, False),
-                                             (64, 8, 2, True)])
+                                             (64, 8, 2, True), (32, 12, 12, False), (32, 4, 2, True)])
 def test_prefill_attention(gpu, D, Hq, Hkv, causal):
     from llm_weighted_consensus_amd import ops
 

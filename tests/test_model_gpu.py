@@ -123,3 +123,23 @@ def test_engine_export_import_prefill_equivalence(tiny, gpu):
     got = [[list(s.tokens) for s in g.seqs] for g in groups]
     assert got == want
     assert b.bm.num_free == 256
+
+
+@pytest.mark.parametrize("arch", ["bge-small-en-v1.5", "bert-tiny"])
+def test_bert_encoder_matches_reference(gpu, arch):
+    """HIP encoder (LN, varlen bidirectional attention incl. head_dim 32, bias+GELU, pooling) vs the
+    fp32 PyTorch reference forward of the same weights."""
+    from llm_weighted_consensus_amd.models.bert import BertEncoder
+    from llm_weighted_consensus_amd.models.config import encoder_config
+
+    m = BertEncoder(encoder_config(arch), device=gpu, seed=5)
+    lists = [[101] + list(range(1000, 1000 + n)) + [102] for n in (3, 40, 77, 130)]
+    ids, pos, cu, max_len = m.pack(lists)
+    h = m.forward_packed(ids, pos, cu, max_len)
+    ref = m.forward_reference(ids, pos, cu)
+    for i in range(len(lists)):
+        s0, s1 = int(cu[i]), int(cu[i + 1])
+        assert _cos(h[s0:s1], ref[s0:s1]) > 0.995, (arch, i)
+    e, _ = m.embed_packed(ids, pos, cu, max_len)
+    er = BertEncoder.pool_reference(ref, cu, m.cfg.pooling)
+    assert (e - er).abs().max().item() < 2e-2

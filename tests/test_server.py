@@ -125,3 +125,29 @@ def test_health_metrics_and_registry(client):
         r = await client.post("/embeddings", json={"input": "x"})
         assert r.status_code == 404
     run(go())
+
+
+def test_config1_cpu_canned_completions_embedding_consensus():
+    """BASELINE config 1: 4 canned completions, bge-small embeddings + cosine consensus, all on CPU
+    (LWC_DEVICE=cpu path: fp32 reference encoder, no GPU)."""
+    canned = ["Paris is the capital of France.", "The capital of France is Paris.",
+              "Paris.", "I think it is Lyon, but I am not sure at all about that."]
+    cfg = Config(device="cpu", embed_models={"bge-small": {"arch": "bge-small-en-v1.5", "weights": "random:3"}})
+    state = build_state(cfg, chat_client=FakeChatClient(lambda req: [Scripted(t) for t in canned]))
+    app = create_app(state)
+    c = httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t")
+
+    async def go():
+        r = await c.post("/consensus/completions", json={
+            "messages": [{"role": "user", "content": "Capital of France?"}], "model": "local", "n": 4,
+            "embedding_model": "bge-small"})
+        assert r.status_code == 200, r.text
+        body = r.json()
+        ch = body["choices"]
+        assert len(ch) == 4 and [x["message"]["content"] for x in ch] == canned
+        assert sum(x["confidence"] for x in ch) == pytest.approx(1.0)
+        emb = body["weight_data"]["embeddings_response"]["data"]
+        assert len(emb) == 4 and len(emb[0]["embedding"]) == 384
+        r = await c.post("/embeddings", json={"input": ["a", "bb"], "model": "bge-small"})
+        assert r.status_code == 200 and len(r.json()["data"]) == 2
+    run(go())
