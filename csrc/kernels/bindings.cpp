@@ -23,6 +23,11 @@ int lwc_paged_decode_prefix(const void*, int, const void*, const void*, const in
 int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const int*, const int*, const int*, int, void*,
                              int, int, int, int, int, float, hipStream_t);
 int lwc_cascade_rows_per_tile(int);
+int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
+                     int, int, int, int, int, int, long long, int, hipStream_t);
+int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
+int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
+int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
@@ -237,6 +242,86 @@ void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const 
            "paged_decode_cascade");
 }
 
+void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& row_off, int64_t max_slots,
+                  const c10::optional<at::Tensor>& a_scale, const c10::optional<at::Tensor>& w_scale,
+                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& a_rows) {
+  // A [rows, K] (bf16 | fp8 e4m3fn, unit inner stride), W [G, N, K] contiguous, C [rows, N] bf16,
+  // row_off [G+1] int32 on the device (group boundaries; the kernel trusts them to be <= rows).
+  CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_DTYPE(row_off, at::kInt); CHECK_CONTIG(row_off);
+  CHECK_CONTIG(W);
+  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(fp8 ? W.scalar_type() == at::kFloat8_e4m3fn : (A.scalar_type() == at::kBFloat16 &&
+              W.scalar_type() == at::kBFloat16), "grouped_gemm: A/W must both be bf16 or both fp8 e4m3fn");
+  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1, "grouped_gemm: 2-D row-major A/C");
+  TORCH_CHECK(W.dim() == 3, "grouped_gemm: W must be [G, N, K]");
+  const int G = (int)W.size(0), N = (int)W.size(1), K = (int)W.size(2);
+  TORCH_CHECK(A.size(1) == K && C.size(1) == N, "grouped_gemm: shape mismatch");
+  const int* ar = nullptr;
+  if (a_rows.has_value() && a_rows->defined()) {
+    CHECK_DTYPE(*a_rows, at::kInt); CHECK_CONTIG(*a_rows);
+    TORCH_CHECK(a_rows->numel() >= C.size(0), "grouped_gemm: a_rows shorter than the output rows");
+    ar = a_rows->data_ptr<int>();
+  } else {
+    TORCH_CHECK(C.size(0) >= A.size(0), "grouped_gemm: C rows < A rows");
+  }
+  TORCH_CHECK(row_off.numel() == G + 1, "grouped_gemm: row_off must have G+1 entries");
+  const float* as = nullptr;
+  const float* ws = nullptr;
+  if (fp8) {
+    TORCH_CHECK(a_scale.has_value() && w_scale.has_value(), "grouped_gemm: fp8 needs a_scale and w_scale");
+    CHECK_DTYPE(*a_scale, at::kFloat); CHECK_DTYPE(*w_scale, at::kFloat);
+    TORCH_CHECK(a_scale->numel() >= A.size(0) && w_scale->numel() == (int64_t)G * N, "grouped_gemm: scale shapes");
+    as = a_scale->data_ptr<float>();
+    ws = w_scale->data_ptr<float>();
+  }
+  const void* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == (int64_t)G * N, "grouped_gemm: bias must be [G, N]");
+    b = bias->data_ptr();
+  }
+  CHECK_RC(lwc_grouped_gemm(A.data_ptr(), W.data_ptr(), C.data_ptr(), row_off.data_ptr<int>(), as, ws, b, ar, G,
+                            (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0), (long long)N * K, fp8 ? 1 : 0,
+                            cur_stream()),
+           "grouped_gemm");
+}
+
+void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Tensor& topk_w, at::Tensor& row_off,
+               at::Tensor& src_row, at::Tensor& inv) {
+  CHECK_BF16(logits); CHECK_CONTIG(logits);
+  TORCH_CHECK(logits.dim() == 2, "moe_route: logits must be [T, E]");
+  const int T = (int)logits.size(0), E = (int)logits.size(1);
+  for (const at::Tensor* t : {&topk_ids, &row_off, &src_row, &inv}) {
+    CHECK_GPU(*t); CHECK_DTYPE(*t, at::kInt); CHECK_CONTIG(*t);
+  }
+  CHECK_DTYPE(topk_w, at::kFloat); CHECK_CONTIG(topk_w);
+  TORCH_CHECK(topk_ids.numel() >= (int64_t)T * k && topk_w.numel() >= (int64_t)T * k && src_row.numel() >= (int64_t)T * k &&
+              inv.numel() >= (int64_t)T * k && row_off.numel() == E + 1, "moe_route: output sizes");
+  CHECK_RC(lwc_moe_route(logits.data_ptr(), T, E, (int)k, topk_ids.data_ptr<int>(), topk_w.data_ptr<float>(),
+                         row_off.data_ptr<int>(), src_row.data_ptr<int>(), inv.data_ptr<int>(), cur_stream()),
+           "moe_route");
+}
+
+void moe_combine(const at::Tensor& Y, const at::Tensor& inv, const at::Tensor& w, int64_t k, at::Tensor& out) {
+  CHECK_BF16(Y); CHECK_BF16(out); CHECK_CONTIG(Y); CHECK_CONTIG(out);
+  CHECK_DTYPE(inv, at::kInt); CHECK_DTYPE(w, at::kFloat);
+  const int T = (int)out.size(0), d = (int)out.size(1);
+  TORCH_CHECK(Y.size(1) == d && inv.numel() >= (int64_t)T * k && w.numel() >= (int64_t)T * k, "moe_combine: shapes");
+  CHECK_RC(lwc_moe_combine(Y.data_ptr(), inv.data_ptr<int>(), w.data_ptr<float>(), T, (int)k, d, out.data_ptr(),
+                           cur_stream()),
+           "moe_combine");
+}
+
+void quant_fp8_rows(const at::Tensor& x, at::Tensor& q, at::Tensor& scale) {
+  CHECK_BF16(x); CHECK_CONTIG(x); CHECK_CONTIG(q);
+  TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn && q.numel() == x.numel(), "quant_fp8_rows: q must be e4m3fn like x");
+  CHECK_DTYPE(scale, at::kFloat);
+  const int d = (int)x.size(-1), rows = (int)(x.numel() / d);
+  TORCH_CHECK(scale.numel() >= rows, "quant_fp8_rows: scale too short");
+  CHECK_RC(lwc_quant_fp8_rows(x.data_ptr(), rows, d, q.data_ptr(), scale.data_ptr<float>(), cur_stream()),
+           "quant_fp8_rows");
+}
+
 void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                        const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, int64_t D,
                        double scale, bool causal) {
@@ -352,6 +437,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding", &embedding);
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);
+  m.def("grouped_gemm", &grouped_gemm);
+  m.def("moe_route", &moe_route);
+  m.def("moe_combine", &moe_combine);
+  m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("paged_decode_cascade", &paged_decode_cascade);
   m.def("cascade_rows_per_tile", &lwc_cascade_rows_per_tile, "sequences per cascade super-tile for a GQA ratio G");
   m.def("set_decode_wave_min_items", &lwc_set_decode_wave_min_items,

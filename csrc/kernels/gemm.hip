@@ -1,0 +1,188 @@
+// K6g grouped GEMM on MFMA: C[rows, N] = A[rows, K] . W_g[N, K]^T for row groups g (MoE experts),
+// with the group table on the DEVICE so a launch needs no host sync (graph-capturable), plus the
+// fp8 (OCP e4m3) variant with per-row activation and per-channel weight scales (config 5).
+//
+//   groups : row_off[G+1] (device, int32): group g owns rows [row_off[g], row_off[g+1]) of A and C and
+//            multiplies them by W + g * w_group_stride.  A plain GEMM is G = 1, row_off = {0, M}.
+//            Optional a_rows[r] gathers A's row per output row (MoE dispatch without a permute copy).
+//   grid   : x = m-tile SLOT (>= sum_g ceil(M_g / BM); surplus slots exit), y = n-tile.
+//   tile   : BM x BN = 128 x 128, BK = 64; 4 waves as 2 x 2, each 64 x 64 = 4 x 4 MFMA 16x16 tiles.
+//   K loop : register-staged double-buffered LDS (next K-tile's global loads in flight under the
+//            current tile's MFMAs, written to the other LDS buffer after them: one barrier per step),
+//            16-byte chunks XOR-swizzled by row (conflict-free ds_read_b128 fragment reads).
+//   MFMA   : bf16: mfma_f32_16x16x32_bf16 (lane: row r16, k-chunk g); fp8: mfma_f32_16x16x32_fp8_fp8
+//            (8 fp8 per lane per k=32 step, so one 16 B LDS chunk holds two k-steps).
+// Both operands are K-contiguous (torch.nn.functional.linear layout), so A and W tiles share one
+// staging / fragment code path.
+#include "common.h"
+
+namespace lwc {
+
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kGM = 128, kGN = 128;
+constexpr int kGKBytes = 128;          // bytes of K per tile row (64 bf16 or 128 fp8)
+constexpr int kGChunks = kGKBytes / 16;  // 16 B chunks per tile row
+constexpr int kGTileBytes = kGM * kGKBytes;  // 16 KiB per operand tile
+
+struct GemmParams {
+  const uint8_t* A;     // [rows, K] (bf16 or fp8), row stride lda elements
+  const uint8_t* W;     // [G][N, K]
+  bf16_t* C;            // [rows, N], row stride ldc
+  const int* row_off;   // [G + 1]
+  const float* a_scale; // fp8: [rows] per-row activation scales
+  const float* w_scale; // fp8: [G][N] per-channel weight scales
+  const bf16_t* bias;   // optional [G][N]
+  const int* a_rows;    // optional [rows]: A row of output row r is a_rows[r] (MoE dispatch gather)
+  int G, N, K, lda, ldc;
+  long long w_group_stride;  // elements
+};
+
+LWC_DEVICE float4v mfma_bf16(const short8& a, const short8& b, const float4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(gbf16x8, a), __builtin_bit_cast(gbf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+template <bool FP8>
+__global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
+  constexpr int ES = FP8 ? 1 : 2;  // element size
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2][2][kGTileBytes];  // [buf][A|W]
+
+  // ---- locate (group, m-tile) of this slot ----
+  int slot = blockIdx.x, g = 0, m_begin = 0, m_end = 0;
+  for (; g < p.G; ++g) {
+    const int r0 = p.row_off[g], r1 = p.row_off[g + 1];
+    const int nt = (r1 - r0 + kGM - 1) / kGM;
+    if (slot < nt) {
+      m_begin = r0 + slot * kGM;
+      m_end = r1;
+      break;
+    }
+    slot -= nt;
+  }
+  if (g >= p.G) return;  // surplus slot (uniform for the workgroup)
+  const int n0 = blockIdx.y * kGN;
+  const uint8_t* W = p.W + (size_t)g * p.w_group_stride * ES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int KT = p.K * ES / kGKBytes;  // K tiles (K * ES is a multiple of 128 B)
+  // staging: 1024 chunks per operand tile, 4 per thread
+  uint4v sa[4], sw[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      const int ar = m_begin + row;
+      const size_t kb = (size_t)kt * kGKBytes + ch * 16;
+      if (ar < m_end) {
+        const int src = p.a_rows ? p.a_rows[ar] : ar;
+        sa[i] = *reinterpret_cast<const uint4v*>(p.A + (size_t)src * p.lda * ES + kb);
+      } else {
+        sa[i] = uint4v{0, 0, 0, 0};
+      }
+      const int wr = n0 + row;
+      sw[i] = wr < p.N ? *reinterpret_cast<const uint4v*>(W + (size_t)wr * p.K * ES + kb) : uint4v{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      const int off = row * kGKBytes + ((ch ^ (row & 7)) << 4);
+      *reinterpret_cast<uint4v*>(&smem[buf][0][off]) = sa[i];
+      *reinterpret_cast<uint4v*>(&smem[buf][1][off]) = sw[i];
+    }
+  };
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) gload(kt + 1);
+    const uint8_t* As = smem[buf][0];
+    const uint8_t* Ws = smem[buf][1];
+    // two 16 B-chunk halves of the 128 B k-slice: bf16 -> 2 k-steps of 32; fp8 -> 4 k-steps of 32
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = 4 * s + q;
+      uint4v af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wm * 64 + i * 16 + r16;
+        af[i] = *reinterpret_cast<const uint4v*>(As + ra * kGKBytes + ((ch ^ (ra & 7)) << 4));
+        const int rb = wn * 64 + i * 16 + r16;
+        bfr[i] = *reinterpret_cast<const uint4v*>(Ws + rb * kGKBytes + ((ch ^ (rb & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (FP8) {
+            // lane q holds k [16*ch, 16*ch + 16) of its row as 16 fp8; mfma fp8 16x16x32 takes 8 fp8 per
+            // lane, so the chunk feeds two MFMAs (bytes 0-7, then 8-15).  A and W use the same
+            // k -> (mfma, lane, slot) permutation, so the dot product is unchanged.
+            const long a0 = (long)af[i].x | ((long)af[i].y << 32), a1 = (long)af[i].z | ((long)af[i].w << 32);
+            const long b0 = (long)bfr[j].x | ((long)bfr[j].y << 32), b1 = (long)bfr[j].z | ((long)bfr[j].w << 32);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0, b0, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1, b1, acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = mfma_bf16(__builtin_bit_cast(short8, af[i]), __builtin_bit_cast(short8, bfr[j]), acc[i][j]);
+          }
+        }
+    }
+    if (kt + 1 < KT) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: scales, bias, bf16 store (lane reg r = C[row 4q + r][col r16] of each 16x16) ----
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + r16;
+    if (col >= p.N) continue;
+    const float ws = FP8 ? p.w_scale[(size_t)g * p.N + col] : 1.f;
+    const float bv = p.bias ? bf2f(p.bias[(size_t)g * p.N + col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m_begin + wm * 64 + i * 16 + 4 * q + r;
+        if (row < m_end) {
+          const float as = FP8 ? p.a_scale[p.a_rows ? p.a_rows[row] : row] : 1.f;
+          p.C[(size_t)row * p.ldc + col] = f2bf(acc[i][j][r] * as * ws + bv);
+        }
+      }
+  }
+}
+
+}  // namespace lwc
+
+// max_slots: grid x; must be >= sum_g ceil(M_g / 128) (sum_g <= ceil(M_total / 128) + G works for any split).
+extern "C" int lwc_grouped_gemm(const void* A, const void* W, void* C, const int* row_off, const float* a_scale,
+                                const float* w_scale, const void* bias, const int* a_rows, int G, int max_slots, int N,
+                                int K, int lda, int ldc, long long w_group_stride, int fp8, hipStream_t s) {
+  using namespace lwc;
+  const int es = fp8 ? 1 : 2;
+  if ((K * es) % kGKBytes != 0 || N % 16 != 0 || G < 1) return -1;
+  if (fp8 && (!a_scale || !w_scale)) return -2;
+  if (max_slots == 0) return 0;
+  GemmParams p{(const uint8_t*)A, (const uint8_t*)W, (bf16_t*)C, row_off, a_scale, w_scale, (const bf16_t*)bias,
+               a_rows, G, N, K, lda, ldc, w_group_stride};
+  dim3 grid(max_slots, (N + kGN - 1) / kGN);
+  if (fp8)
+    grouped_gemm_kernel<true><<<grid, 256, 0, s>>>(p);
+  else
+    grouped_gemm_kernel<false><<<grid, 256, 0, s>>>(p);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,178 @@
+// K11 Mixture-of-experts plumbing (Mixtral-8x7B, BASELINE config 5) + fp8 activation quantisation.
+//
+//   moe_route   : router logits [T, E] -> top-k experts per token, their softmax weights
+//                 (Mixtral: softmax over all E, keep top-k, renormalise == softmax over the top-k
+//                 logits), per-expert segments row_off[E+1] and the dispatch permutation
+//                   src_row[pos] = token of expert-sorted row pos,   inv[t*k + j] = pos of (t, j).
+//                 One workgroup: counts in LDS, prefix in LDS, slots by LDS atomics.  Row order inside
+//                 an expert segment is arbitrary (atomics) but every row is computed independently,
+//                 so results are deterministic.  Everything stays on the device (graph-capturable).
+//   moe_combine : out[t] = sum_j w[t, j] * Y[inv[t*k + j]]   (expert outputs back to token order)
+//   quant_fp8_rows : per-row dynamic e4m3 (OCP) quantisation: scale = amax / 448.
+// The expert GEMMs themselves are the grouped MFMA GEMM (gemm.hip) reading A through src_row.
+#include "common.h"
+
+namespace lwc {
+
+constexpr int kMaxExperts = 64;
+constexpr int kMaxTopK = 8;
+
+template <int EM, int KM>
+__global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restrict__ logits, int T, int E, int k,
+                                                         int* __restrict__ topk_ids, float* __restrict__ topk_w,
+                                                         int* __restrict__ row_off, int* __restrict__ src_row,
+                                                         int* __restrict__ inv) {
+  __shared__ int s_count[kMaxExperts];
+  __shared__ int s_cursor[kMaxExperts];
+  const int tid = threadIdx.x;
+  if (tid < E) s_count[tid] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += blockDim.x) {
+    // fully unrolled over the compile-time bounds so the per-token arrays stay in registers
+    float lv[EM];
+    bool taken[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      lv[e] = e < E ? bf2f(logits[(size_t)t * E + e]) : -INFINITY;
+      taken[e] = e >= E;
+    }
+    int ids[KM];
+    float vals[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {  // repeated arg-max (ties -> lower expert id)
+      if (j >= k) break;
+      int best = 0;
+      float bv = -INFINITY;
+      bool found = false;
+#pragma unroll
+      for (int e = 0; e < EM; ++e) {
+        if (!taken[e] && (!found || lv[e] > bv)) {
+          best = e;
+          bv = lv[e];
+          found = true;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EM; ++e) taken[e] |= e == best;
+      ids[j] = best;
+      vals[j] = bv;
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      if (j >= k) break;
+      vals[j] = __expf(vals[j] - vals[0]);
+      sum += vals[j];
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      if (j >= k) break;
+      topk_ids[t * k + j] = ids[j];
+      topk_w[t * k + j] = vals[j] / sum;
+      atomicAdd(&s_count[ids[j]], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      row_off[e] = acc;
+      s_cursor[e] = acc;
+      acc += s_count[e];
+    }
+    row_off[E] = acc;
+  }
+  __syncthreads();
+  for (int i = tid; i < T * k; i += blockDim.x) {
+    const int e = topk_ids[i];
+    const int pos = atomicAdd(&s_cursor[e], 1);
+    src_row[pos] = i / k;
+    inv[i] = pos;
+  }
+}
+
+// one workgroup per token; d % 8 == 0
+__global__ void __launch_bounds__(256) moe_combine_kernel(const bf16_t* __restrict__ Y, const int* __restrict__ inv,
+                                                          const float* __restrict__ w, int k, int d,
+                                                          bf16_t* __restrict__ out) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x * 8; c < d; c += blockDim.x * 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = w[t * k + j];
+      float y[8];
+      unpack8(*reinterpret_cast<const uint4v*>(Y + (size_t)inv[t * k + j] * d + c), y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += wj * y[e];
+    }
+    *reinterpret_cast<uint4v*>(out + (size_t)t * d + c) = pack8(acc);
+  }
+}
+
+// one workgroup per row; d % 8 == 0.  q = x / scale as e4m3 (OCP fn), scale = amax / 448.
+__global__ void __launch_bounds__(256) quant_fp8_rows_kernel(const bf16_t* __restrict__ x, int d,
+                                                             uint8_t* __restrict__ q, float* __restrict__ scale) {
+  __shared__ float red[8];
+  const int r = blockIdx.x;
+  const bf16_t* row = x + (size_t)r * d;
+  float amax = 0.f;
+  for (int c = threadIdx.x * 8; c < d; c += blockDim.x * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4v*>(row + c), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  }
+  amax = block_max(amax, red);
+  const float s = fmaxf(amax, 1e-12f) / 448.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[r] = s;
+  for (int c = threadIdx.x * 8; c < d; c += blockDim.x * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4v*>(row + c), v);
+    uint32_t lo = 0, hi = 0;
+    // v_cvt_pk_fp8_f32: two f32 -> two e4m3 bytes in the low / high word half
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+    *reinterpret_cast<uint2*>(q + (size_t)r * d + c) = make_uint2(lo, hi);
+  }
+}
+
+}  // namespace lwc
+
+extern "C" int lwc_moe_route(const void* logits, int T, int E, int k, int* topk_ids, float* topk_w, int* row_off,
+                             int* src_row, int* inv, hipStream_t s) {
+  using namespace lwc;
+  if (E > kMaxExperts || k > kMaxTopK || k > E || k < 1) return -1;
+  if (T == 0) {
+    (void)hipMemsetAsync(row_off, 0, sizeof(int) * (E + 1), s);
+    return (int)hipGetLastError();
+  }
+  if (E <= 8 && k <= 2)
+    moe_route_kernel<8, 2><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w, row_off, src_row, inv);
+  else if (E <= 16)
+    moe_route_kernel<16, kMaxTopK><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w, row_off,
+                                                       src_row, inv);
+  else
+    moe_route_kernel<kMaxExperts, kMaxTopK><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w,
+                                                               row_off, src_row, inv);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_moe_combine(const void* Y, const int* inv, const float* w, int T, int k, int d, void* out,
+                               hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0) return -1;
+  if (T == 0) return 0;
+  moe_combine_kernel<<<T, 256, 0, s>>>((const bf16_t*)Y, inv, w, k, d, (bf16_t*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_quant_fp8_rows(const void* x, int rows, int d, void* q, float* scale, hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  quant_fp8_rows_kernel<<<rows, 256, 0, s>>>((const bf16_t*)x, d, (uint8_t*)q, scale);
+  return (int)hipGetLastError();
+}

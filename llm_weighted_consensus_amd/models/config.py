@@ -70,6 +70,9 @@ DECODERS = {
                                 max_position=32768),
     "mixtral-8x7b": DecoderConfig("mixtral-8x7b", 32000, 4096, 32, 32, 8, 128, 14336, rope_theta=1e6, rms_eps=1e-5,
                                   max_position=32768, num_experts=8, experts_per_token=2),
+    # e5-mistral-7b-instruct: Mistral-7B decoder used as an embedder (last-token pooling, 4096-d)
+    "e5-mistral-7b": DecoderConfig("e5-mistral-7b", 32000, 4096, 32, 32, 8, 128, 14336, rope_theta=10000.0,
+                                   rms_eps=1e-5, max_position=32768),
     # tests / smoke: same code paths, tiny sizes
     "llama-tiny": DecoderConfig("llama-tiny", 4096, 512, 2, 8, 2, 128, 1024, rope_theta=500000.0, max_position=2048,
                                 bos_token_id=1, eos_token_id=2),

@@ -1,0 +1,47 @@
+"""Decoder-as-embedder (e5-mistral-7b style, BASELINE config 5's embedder): the last token's final hidden
+state of a causal decoder, L2-normalised (4096-d for Mistral-7B shapes).
+
+Runs the same gfx950 kernel set as generation (`LlamaModel.encode`: cache-less prefill path, varlen
+causal flash attention, fused RMSNorm/RoPE/SwiGLU) and pools with the K9d pool_l2norm kernel in LAST
+mode.  It exposes the `embed(token_lists, max_tokens)` interface of `BertEncoder`, so the embeddings
+service, the consensus scorer and the training-table weights use either encoder family.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from .. import ops
+from .config import DecoderConfig
+
+
+class DecoderEmbedder:
+    def __init__(self, model, max_tokens: int = 4096):
+        self.model = model
+        self.device = model.device
+        self.max_tokens = max_tokens
+        cfg: DecoderConfig = model.cfg
+        # the embeddings service reads these like an EncoderConfig
+        self.cfg = type("EmbedCfg", (), {"vocab_size": cfg.vocab_size, "max_position": max_tokens,
+                                         "hidden": cfg.hidden, "pooling": "last", "name": cfg.name})()
+
+    def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        cap = min(max_tokens or self.max_tokens, self.max_tokens)
+        V = self.cfg.vocab_size
+        ids, pos, cu = [], [], [0]
+        for tl in token_lists:
+            tl = [int(t) % V for t in list(tl)[-cap:]] or [0]  # keep the END: the last token is pooled
+            ids.extend(tl)
+            pos.extend(range(len(tl)))
+            cu.append(cu[-1] + len(tl))
+        dev = self.device
+        max_len = max(cu[i + 1] - cu[i] for i in range(len(cu) - 1))
+        return (torch.tensor(ids, dtype=torch.int32, device=dev), torch.tensor(pos, dtype=torch.int32, device=dev),
+                torch.tensor(cu, dtype=torch.int32, device=dev), max_len)
+
+    def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        """-> (unit f32 [n, d], unit bf16 [n, d])"""
+        ids, pos, cu, max_len = self.pack(token_lists, max_tokens)
+        h = self.model.encode(ids, pos, cu, max_len)
+        return ops.pool_l2norm(h, cu, ops.POOL_LAST)

@@ -85,10 +85,19 @@ class KVCache:
             ops.kv_block_copy(self.pool.view(self.cfg.layers * 2, self.num_blocks, self.block_elems), pairs)
 
 
+class _NullCache:
+    """Shape-only stand-in for KVCache when no KV is written (encode): one shared 1-block buffer."""
+
+    def __init__(self, cfg: DecoderConfig, device):
+        buf = torch.zeros(2, 1, cfg.kv_heads, 16, cfg.head_dim, dtype=torch.bfloat16, device=device)
+        self.k = [buf[0]] * cfg.layers
+        self.v = [buf[1].view(1, cfg.kv_heads, cfg.head_dim, 16)] * cfg.layers
+
+
 class LlamaModel:
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  weights_path: Optional[str] = None, max_position: Optional[int] = None):
-        if cfg.num_experts:
+        if cfg.num_experts and type(self) is LlamaModel:
             raise NotImplementedError("MoE decoders use models.mixtral.MixtralModel")
         self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
         self.cos, self.sin = rope_tables(cfg, self.device, max_position)
@@ -166,14 +175,20 @@ class LlamaModel:
             qkv = F.linear(h, L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
             attn = attn_fn(qkv, li)
-            o = F.linear(attn.view(T, Hq * D), L.wo)
+            o = self._attn_out(attn.view(T, Hq * D), L)
             h = ops.rmsnorm(o, L.mlp_norm, cfg.rms_eps, residual=x_res)
-            gu = F.linear(h, L.w_gate_up)
-            act = ops.silu_mul(gu)
-            down = F.linear(act, L.w_down)
+            down = self._mlp(h, L)
             nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
             h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
         return h
+
+    def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
+        """Output projection (row-parallel + all-reduce in tensor-parallel subclasses)."""
+        return F.linear(attn, L.wo)
+
+    def _mlp(self, h: torch.Tensor, L) -> torch.Tensor:
+        """Dense SwiGLU MLP: fused gate|up GEMM, K5 silu_mul, down GEMM."""
+        return F.linear(ops.silu_mul(F.linear(h, L.w_gate_up)), L.w_down)
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None,
@@ -214,6 +229,22 @@ class LlamaModel:
 
         h = self._layers(x, cache, positions, slots, attn_fn)
         return F.linear(h, self.lm_head)
+
+    def encode(self, tokens: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor,
+               max_seqlen: int) -> torch.Tensor:
+        """Cache-less causal forward of packed sequences -> final-normed hidden states [T, d] (decoder used
+        as an embedder, e.g. e5-mistral: the caller pools the last token).  RoPE runs without a cache
+        write (slots=None), attention is the varlen prefill kernel over the fresh k/v."""
+        cfg = self.cfg
+        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        null = _NullCache(cfg, self.device)
+        x = ops.embedding(self.embed, tokens)
+
+        def attn_fn(qkv, li):
+            return ops.prefill_attention(qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:],
+                                         cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
+
+        return self._layers(x, null, positions, None, attn_fn)
 
     def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cu_seqlens: torch.Tensor,
                 max_seqlen: int, last_idx: torch.Tensor, cache: KVCache) -> torch.Tensor:

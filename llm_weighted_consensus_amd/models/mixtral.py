@@ -1,0 +1,164 @@
+"""Mixtral-style sparse mixture-of-experts decoder (BASELINE config 5: Mixtral-8x7B sampler, fp8 MFMA,
+tensor-parallel degree 2).
+
+Attention, KV cache, prefill/decode/cascade paths are the Llama ones (`LlamaModel`); only the MLP
+changes.  Per layer, for the T tokens of a step:
+
+    logits = h Wr^T                      [T, E]        hipBLASLt (tiny)
+    route  = top-k softmax, segments     K11a moe_route (one workgroup, all on the device)
+    gu     = grouped GEMM over experts   K6g, A rows gathered through src_row (no permute copy)
+    act    = silu(g) * u                 K5
+    y      = grouped GEMM over experts   K6g
+    out    = sum_j w[t,j] y[inv[t,j]]    K11d moe_combine
+With ``fp8=True`` the expert weights are OCP e4m3 with per-output-channel scales (quantised at load)
+and activations are quantised per row on the fly (K11e), feeding the fp8 MFMA path of the grouped
+GEMM: half the weight bytes — what bounds a MoE decode step, which touches every expert's weights.
+
+Tensor parallelism (``tp_group``): attention heads and every expert's FFN columns are split across
+the ranks (Megatron layout: q/k/v and gate|up column-parallel, o and down row-parallel); the two
+row-parallel outputs are summed with one all-reduce each (C3) before the residual norm.  The shard is
+taken from the full random-init / loaded weights so any TP degree computes the same function.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .config import DecoderConfig
+from .llama import LlamaModel, rope_tables
+
+
+@dataclass
+class MoELayerWeights:
+    attn_norm: torch.Tensor
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    mlp_norm: torch.Tensor
+    router: torch.Tensor          # [E, d]
+    w13: torch.Tensor             # [E, 2F_local, d]  (bf16 or e4m3fn)
+    w2: torch.Tensor              # [E, d, F_local]
+    s13: Optional[torch.Tensor]   # fp8 per-channel scales [E, 2F_local]
+    s2: Optional[torch.Tensor]    # [E, d]
+
+
+class MixtralModel(LlamaModel):
+    def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8: bool = False,
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+        if not cfg.num_experts:
+            raise ValueError(f"{cfg.name} is dense; use LlamaModel")
+        if cfg.heads % tp_size or cfg.kv_heads % tp_size or cfg.ffn % tp_size:
+            raise ValueError(f"tp_size {tp_size} must divide heads, kv_heads and ffn")
+        self.fp8, self.tp_rank, self.tp_size, self.tp_group = fp8, tp_rank, tp_size, tp_group
+        self.full_cfg = cfg
+        super().__init__(cfg, device=device, dtype=dtype, seed=seed, weights_path=weights_path,
+                         max_position=max_position)
+        # the attention kernels see the per-rank head counts
+        if tp_size > 1:
+            from dataclasses import replace
+
+            self.cfg = replace(cfg, heads=cfg.heads // tp_size, kv_heads=cfg.kv_heads // tp_size)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # ------------------------------------------------------------------ weights
+    def _shard_layer(self, attn_norm, wq, wk, wv, wo, mlp_norm, router, w1, w3, w2) -> MoELayerWeights:
+        """Full per-layer tensors -> this rank's shard (+ fp8 quantisation of the experts)."""
+        r, n = self.tp_rank, self.tp_size
+        cfg = self.full_cfg
+        D, F_ = cfg.head_dim, cfg.ffn
+        hq, hk, fl = cfg.heads // n, cfg.kv_heads // n, F_ // n
+        q = wq[r * hq * D:(r + 1) * hq * D]
+        k = wk[r * hk * D:(r + 1) * hk * D]
+        v = wv[r * hk * D:(r + 1) * hk * D]
+        wqkv = torch.cat([q, k, v]).contiguous()
+        wo_s = wo[:, r * hq * D:(r + 1) * hq * D].contiguous()
+        w13 = torch.cat([w1[:, r * fl:(r + 1) * fl], w3[:, r * fl:(r + 1) * fl]], dim=1).contiguous()  # [E,2fl,d]
+        w2_s = w2[:, :, r * fl:(r + 1) * fl].contiguous()                                             # [E,d,fl]
+        s13 = s2 = None
+        if self.fp8:
+            w13, s13 = ops.quant_fp8_weight(w13)
+            w2_s, s2 = ops.quant_fp8_weight(w2_s)
+        return MoELayerWeights(attn_norm, wqkv, wo_s, mlp_norm, router.contiguous(), w13, w2_s, s13, s2)
+
+    def _random_init(self, seed: int) -> None:
+        cfg, dev, dt = self.full_cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        std = 0.02
+
+        def rnd(*shape, s=std):
+            return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * s).to(dt)
+
+        d, F_, E, D = cfg.hidden, cfg.ffn, cfg.num_experts, cfg.head_dim
+        self.embed = rnd(cfg.vocab_size, d)
+        out_std = std / math.sqrt(2 * cfg.layers)
+        self.layers = []
+        for _ in range(cfg.layers):
+            wq, wk, wv = rnd(cfg.heads * D, d), rnd(cfg.kv_heads * D, d), rnd(cfg.kv_heads * D, d)
+            wo = rnd(d, cfg.heads * D, s=out_std)
+            router = rnd(E, d, s=0.1)
+            w1, w3 = rnd(E, F_, d), rnd(E, F_, d)
+            w2 = rnd(E, d, F_, s=out_std)
+            ones = torch.ones(d, device=dev, dtype=dt)
+            self.layers.append(self._shard_layer(ones, wq, wk, wv, wo, ones.clone(), router, w1, w3, w2))
+            del w1, w3, w2
+        self.final_norm = torch.ones(d, device=dev, dtype=dt)
+        self.lm_head = self.embed if cfg.tie_embeddings else rnd(cfg.vocab_size, d)
+
+    def _load(self, path: str) -> None:
+        """HF Mixtral safetensors (model.layers.N.block_sparse_moe.{gate,experts.e.w1/w2/w3})."""
+        from pathlib import Path
+
+        from safetensors.torch import load_file
+
+        files = sorted(Path(path).glob("*.safetensors")) if Path(path).is_dir() else [Path(path)]
+        sd = {}
+        for f in files:
+            sd.update(load_file(str(f), device="cpu"))
+        dev, dt = self.device, self.dtype
+        t = lambda n: sd[n].to(device=dev, dtype=dt).contiguous()  # noqa: E731
+        cfg = self.full_cfg
+        self.embed = t("model.embed_tokens.weight")
+        self.layers = []
+        for i in range(cfg.layers):
+            p = f"model.layers.{i}."
+            m = p + "block_sparse_moe."
+            ex = lambda w: torch.stack([t(f"{m}experts.{e}.{w}.weight") for e in range(cfg.num_experts)])  # noqa
+            self.layers.append(self._shard_layer(
+                t(p + "input_layernorm.weight"), t(p + "self_attn.q_proj.weight"), t(p + "self_attn.k_proj.weight"),
+                t(p + "self_attn.v_proj.weight"), t(p + "self_attn.o_proj.weight"),
+                t(p + "post_attention_layernorm.weight"), t(m + "gate.weight"), ex("w1"), ex("w3"), ex("w2")))
+        self.final_norm = t("model.norm.weight")
+        self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
+
+    # ------------------------------------------------------------------ forward pieces
+    def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            from ..parallel import dist as pdist
+
+            pdist.all_reduce_(x, group=self.tp_group)
+        return x
+
+    def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
+        return self._all_reduce(F.linear(attn, L.wo))
+
+    def _mlp(self, h: torch.Tensor, L: MoELayerWeights) -> torch.Tensor:
+        k = self.full_cfg.experts_per_token
+        logits = F.linear(h, L.router)
+        _ids, w, row_off, src, inv = ops.moe_route(logits, k)
+        rows = h.shape[0] * k
+        if self.fp8:
+            hq, hs = ops.quant_fp8_rows(h)
+            gu = ops.grouped_gemm(hq, L.w13, row_off, a_rows=src, rows=rows, a_scale=hs, w_scale=L.s13)
+            act = ops.silu_mul(gu)
+            aq, as_ = ops.quant_fp8_rows(act)
+            y = ops.grouped_gemm(aq, L.w2, row_off, a_scale=as_, w_scale=L.s2)
+        else:
+            gu = ops.grouped_gemm(h, L.w13, row_off, a_rows=src, rows=rows)
+            y = ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)
+        return self._all_reduce(ops.moe_combine(y, inv, w, k))

@@ -174,6 +174,71 @@ def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seql
 
 
 # ---------------------------------------------------------------------------------------------
+# GEMM
+
+
+def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_slots: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None, a_scale: Optional[torch.Tensor] = None,
+                 w_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+                 a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None) -> torch.Tensor:
+    """Grouped GEMM on MFMA (K6g): rows [row_off[g], row_off[g+1]) of A times W[g]^T -> C [rows, N] bf16.
+    ``a_rows`` [rows] gathers A's row for each output row (MoE dispatch; then ``rows`` = len(a_rows)).
+    ``row_off`` lives on the device (MoE expert segments: no host sync, graph-capturable).  fp8 e4m3fn
+    A/W take per-row ``a_scale`` and per-channel ``w_scale`` (config 5).  ``max_slots`` bounds the m-tiles
+    (default: ceil(rows/128) + G, enough for any split of the rows into G groups)."""
+    if rows is None:
+        rows = a_rows.numel() if a_rows is not None else A.shape[0]
+    G, N = W.shape[0], W.shape[1]
+    if max_slots is None:
+        max_slots = -(-rows // 128) + G
+    if out is None:
+        out = torch.empty(rows, N, dtype=torch.bfloat16, device=A.device)
+    kernels().grouped_gemm(A, W, out, row_off, int(max_slots), a_scale, w_scale, bias, a_rows)
+    return out
+
+
+def moe_route(logits: torch.Tensor, k: int):
+    """Router top-k + softmax over the selected logits, expert segments and dispatch permutation (K11a).
+    logits [T, E] bf16 -> (topk_ids [T,k] i32, topk_w [T,k] f32, row_off [E+1] i32, src_row [T*k] i32,
+    inv [T*k] i32): expert-sorted row p reads token src_row[p]; (t, j) landed at row inv[t*k+j]."""
+    T, E = logits.shape
+    dev = logits.device
+    ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+    w = torch.empty(T, k, dtype=torch.float32, device=dev)
+    row_off = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    src = torch.empty(T * k, dtype=torch.int32, device=dev)
+    inv = torch.empty(T * k, dtype=torch.int32, device=dev)
+    kernels().moe_route(logits.contiguous(), int(k), ids, w, row_off, src, inv)
+    return ids, w, row_off, src, inv
+
+
+def moe_combine(Y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, k: int,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[t] = sum_j w[t, j] * Y[inv[t*k + j]] (K11d): expert outputs back to token order."""
+    T = w.shape[0]
+    if out is None:
+        out = torch.empty(T, Y.shape[1], dtype=Y.dtype, device=Y.device)
+    kernels().moe_combine(Y, inv, w, int(k), out)
+    return out
+
+
+def quant_fp8_rows(x: torch.Tensor):
+    """Per-row dynamic OCP e4m3 quantisation: (q [.., d] float8_e4m3fn, scale [rows] f32), x ~= q * scale."""
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    scale = torch.empty(x.numel() // x.shape[-1], dtype=torch.float32, device=x.device)
+    kernels().quant_fp8_rows(x.contiguous(), q, scale)
+    return q, scale
+
+
+def quant_fp8_weight(w: torch.Tensor):
+    """Per-output-channel OCP e4m3 weight quantisation (host-side torch, load time): w [..., N, K] ->
+    (q e4m3fn, scale [..., N] f32)."""
+    s = (w.float().abs().amax(-1).clamp(min=1e-12) / 448.0)
+    q = (w.float() / s.unsqueeze(-1)).to(torch.float8_e4m3fn)
+    return q.contiguous(), s.contiguous()
+
+
+# ---------------------------------------------------------------------------------------------
 # sampling / scoring
 
 

@@ -103,15 +103,16 @@ def all_gather(t: torch.Tensor) -> torch.Tensor:
     return all_gather_flat(t)
 
 
-def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+def all_reduce_(t: torch.Tensor, op: str = "sum", group=None) -> torch.Tensor:
+    """In-place all-reduce (C3 for tensor parallelism, or control reductions)."""
     if _INFO.enabled:
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         if _INFO.backend == "gloo" and t.is_cuda:
             h = t.cpu()
-            dist.all_reduce(h, op=rop)
+            dist.all_reduce(h, op=rop, group=group)
             t.copy_(h)
         else:
-            dist.all_reduce(t, op=rop)
+            dist.all_reduce(t, op=rop, group=group)
     return t
 
 

@@ -91,6 +91,40 @@ def gemm_backends(dev, Ms):
     torch.backends.cuda.preferred_blas_library("cublaslt")
 
 
+def grouped(dev):
+    """Hand-written grouped MFMA GEMM (K6g) vs hipBLASLt on plain shapes, and the MoE decode shape."""
+    from llm_weighted_consensus_amd import ops
+
+    shapes = {"qkv": (6144, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    for M in (512, 3072):
+        for name, (N, K) in shapes.items():
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            off = torch.tensor([0, M], dtype=torch.int32, device=dev)
+            t_h = timeit(lambda: F.linear(x, w), iters=20)
+            t_g = timeit(lambda: ops.grouped_gemm(x, w.unsqueeze(0), off), iters=20)
+            xq = x.to(torch.float8_e4m3fn)
+            wq = w.unsqueeze(0).to(torch.float8_e4m3fn)
+            sa = torch.ones(M, device=dev)
+            sw = torch.ones(1, N, device=dev)
+            t_8 = timeit(lambda: ops.grouped_gemm(xq, wq, off, a_scale=sa, w_scale=sw), iters=20)
+            fl = 2 * M * N * K / 1e12
+            print(f"ggemm M={M:4d} {name:8s}: hipblaslt {t_h:7.1f} us ({fl / t_h * 1e6:6.0f} TF/s)  "
+                  f"mfma-bf16 {t_g:7.1f} us ({fl / t_g * 1e6:6.0f})  mfma-fp8 {t_8:7.1f} us ({fl / t_8 * 1e6:6.0f})",
+                  flush=True)
+    # Mixtral decode MoE: T tokens x top-2 over 8 experts, d=4096, ffn=14336 (gate_up fused 28672)
+    E, d, f = 8, 4096, 14336
+    w13 = (torch.randn(E, 2 * f, d, device=dev) * 0.02).to(torch.bfloat16)
+    for T in (256, 1024):
+        rows = 2 * T
+        sizes = torch.full((E,), rows // E, dtype=torch.int64)
+        off = torch.cat([torch.zeros(1, dtype=torch.int64), sizes.cumsum(0)]).to(torch.int32).to(dev)
+        x = torch.randn(rows, d, device=dev).to(torch.bfloat16)
+        t = timeit(lambda: ops.grouped_gemm(x, w13, off), iters=10)
+        fl = 2 * rows * 2 * f * d / 1e12
+        print(f"ggemm moe gate_up T={T}: {t:7.1f} us ({fl / t * 1e6:6.0f} TF/s)", flush=True)
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -218,6 +252,8 @@ def main():
         gemms(dev, [int(m) for m in os.environ.get("MICRO_M", "256,512").split(",")], tuned=os.environ.get("PYTORCH_TUNABLEOP_ENABLED") == "1")
     if "backends" in a.what:
         gemm_backends(dev, [1024, 1536])
+    if "grouped" in a.what:
+        grouped(dev)
     if "layout" in a.what:
         gemm_layouts(dev, [512, 1024])
     if "attn" in a.what:

@@ -411,3 +411,38 @@ def test_kv_block_copy(gpu):
     ref_c[:, 4] = ref_c[:, 1]
     ref_c[:, 2] = ref_c[:, 7]
     assert torch.equal(cache, ref_c)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_grouped_gemm(gpu, fp8):
+    """Grouped MFMA GEMM (MoE expert segments on the device, incl. an empty and a ragged group) vs
+    per-group fp32 matmuls; fp8 e4m3fn operands with per-row / per-channel scales."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(3)
+    G, N, K = 4, 384, 256
+    sizes = [130, 0, 7, 300]
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    A = torch.randn(rows, K, device=gpu)
+    W = torch.randn(G, N, K, device=gpu) * 0.05
+    bias = (torch.randn(G, N, device=gpu) * 0.1).to(torch.bfloat16)
+    if fp8:
+        a_s = A.abs().amax(1).clamp(min=1e-6) / 448.0
+        w_s = W.abs().amax(2).clamp(min=1e-6) / 448.0
+        Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
+        Wq = (W / w_s[:, :, None]).to(torch.float8_e4m3fn)
+        out = ops.grouped_gemm(Aq, Wq, off, a_scale=a_s.float().contiguous(), w_scale=w_s.float().contiguous(),
+                               bias=bias)
+        Ar = Aq.float() * a_s[:, None]
+        Wr = Wq.float() * w_s[:, :, None]
+    else:
+        Ab, Wb = A.to(torch.bfloat16), W.to(torch.bfloat16)
+        out = ops.grouped_gemm(Ab, Wb, off, bias=bias)
+        Ar, Wr = Ab.float(), Wb.float()
+    o = off.tolist()
+    for g in range(G):
+        if o[g + 1] == o[g]:
+            continue
+        ref_g = Ar[o[g]:o[g + 1]] @ Wr[g].t() + bias[g].float()
+        _close(out[o[g]:o[g + 1]], ref_g, 2e-2, 2e-2)

@@ -143,3 +143,53 @@ def test_bert_encoder_matches_reference(gpu, arch):
     e, _ = m.embed_packed(ids, pos, cu, max_len)
     er = BertEncoder.pool_reference(ref, cu, m.cfg.pooling)
     assert (e - er).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_mixtral_moe_matches_reference_and_engine(gpu, fp8):
+    """Mixtral MoE decoder (router top-2, grouped MFMA expert GEMMs, combine; fp8 experts) vs the fp32
+    reference, then greedy generation through the engine (cascade + graphs) with prefill/decode agreeing."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import KVCache
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=2, max_position=1024, fp8=fp8)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    toks = torch.randint(0, m.cfg.vocab_size, (37,), generator=g).to(gpu)
+    ref_logits = ref.llama_forward(m, toks)
+    cache = KVCache(m.cfg, 16, 16, gpu)
+    P = 37
+    lg = m.prefill(toks.int(), torch.arange(P, dtype=torch.int32, device=gpu), torch.arange(P, dtype=torch.int32,
+                   device=gpu), torch.tensor([0, P], dtype=torch.int32, device=gpu), P,
+                   torch.tensor([P - 1], device=gpu), cache)
+    # bf16 activations can flip near-tie router choices vs fp32, so the bound is looser than dense
+    assert _cos(lg[0], ref_logits[P - 1]) > (0.985 if fp8 else 0.99)
+    tok = ByteTokenizer(m.cfg.vocab_size)
+    eng = LLMEngine(m, tok, num_blocks=1024, max_batch=160, max_model_len=512, cascade_min_batch=1)
+    sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+    outs = eng.generate([tok.encode("mixture of experts " * 3)], sp, n=130)
+    assert all(o == outs[0][0] for o in outs[0])  # greedy children agree (cascade tiles > 1 per group)
+    assert eng.bm.num_free == 1024
+
+
+def test_decoder_embedder_last_token(tiny, gpu):
+    """e5-mistral-style embedder: cache-less encode == the fp32 reference forward's final normed state of the
+    last token (pooled, unit norm), independent of batch packing."""
+    from llm_weighted_consensus_amd.models.embedder import DecoderEmbedder
+
+    emb = DecoderEmbedder(tiny)
+    lists = [[5, 6, 7, 8, 9] * 7, [11, 12, 13], list(range(100, 190))]
+    e, _ = emb.embed(lists)
+    assert torch.allclose(e.norm(dim=-1), torch.ones(3, device=gpu), atol=1e-3)
+    for i, tl in enumerate(lists):
+        t = torch.tensor(tl, device=gpu)
+        cfg = tiny.cfg
+        # reference: hidden state before lm_head = rmsnorm(x) at the last position
+        x = ref.llama_hidden(tiny, t)[-1]
+        r = torch.nn.functional.normalize(x, dim=0)
+        assert _cos(e[i], r) > 0.995
+        solo, _ = emb.embed([tl])
+        assert _cos(solo[0], e[i]) > 0.999

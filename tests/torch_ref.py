@@ -40,7 +40,7 @@ def attention(q, k, v, causal, scale):
     return torch.einsum("hqk,khd->qhd", p, v.float())
 
 
-def llama_forward(model, tokens):
+def llama_forward(model, tokens, hidden_only=False):
     """Full-sequence fp32 forward of a models.llama.LlamaModel (single sequence) -> logits [T, V]."""
     cfg = model.cfg
     T = tokens.shape[0]
@@ -58,8 +58,35 @@ def llama_forward(model, tokens):
         a = attention(q, k, v, True, 1.0 / math.sqrt(D)).reshape(T, Hq * D)
         x = x + a @ L.wo.float().t()
         h = rmsnorm(x, L.mlp_norm, cfg.rms_eps)
-        gu = h @ L.w_gate_up.float().t()
-        g, u = gu.chunk(2, dim=-1)
-        x = x + (F.silu(g) * u) @ L.w_down.float().t()
+        if hasattr(L, "router"):
+            x = x + moe_mlp(model, L, h)
+        else:
+            gu = h @ L.w_gate_up.float().t()
+            g, u = gu.chunk(2, dim=-1)
+            x = x + (F.silu(g) * u) @ L.w_down.float().t()
     h = rmsnorm(x, model.final_norm, cfg.rms_eps)
+    if hidden_only:
+        return h
     return h @ model.lm_head.float().t()
+
+
+def llama_hidden(model, tokens):
+    """Final RMS-normed hidden states [T, d] (fp32) of the reference forward."""
+    return llama_forward(model, tokens, hidden_only=True)
+
+
+def moe_mlp(model, L, h):
+    """fp32 Mixtral MoE MLP (TP=1 weights; fp8 experts dequantised with their per-channel scales)."""
+    k = model.full_cfg.experts_per_token
+    logits = h @ L.router.float().t()
+    top, ids = logits.topk(k, dim=-1)
+    w = top.softmax(-1)
+    w13 = L.w13.float() * (L.s13.unsqueeze(-1) if L.s13 is not None else 1.0)
+    w2 = L.w2.float() * (L.s2.unsqueeze(-1) if L.s2 is not None else 1.0)
+    out = torch.zeros_like(h)
+    for t in range(h.shape[0]):
+        for j in range(k):
+            e = int(ids[t, j])
+            g, u = (h[t] @ w13[e].t()).chunk(2)
+            out[t] += w[t, j] * ((F.silu(g) * u) @ w2[e].t())
+    return out
