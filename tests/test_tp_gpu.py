@@ -1,0 +1,77 @@
+"""Tensor parallelism (C3) on the GPU: a TP=2 Mixtral (heads and expert FFN columns split, row-parallel
+outputs all-reduced) computes the same logits as TP=1.  Two ranks share the one GPU of the test box
+(LWC_SHARE_ONE_GPU=1: gloo collectives staged through host memory); on an 8-GPU node the same code
+runs over RCCL."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, fp8, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.llama import KVCache
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
+                         tp_rank=rank, tp_size=world)
+        g = torch.Generator().manual_seed(9)
+        P = 29
+        toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(dev)
+        cache = KVCache(m.cfg, 8, 16, dev)
+        ar = torch.arange(P, dtype=torch.int32, device=dev)
+        lg = m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=dev), P,
+                       torch.tensor([P - 1], device=dev), cache)
+        q.put((rank, lg[0].float().cpu()))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_mixtral_tp2_matches_tp1(gpu, fp8):
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import KVCache
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, fp8, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    assert all(isinstance(v, torch.Tensor) for v in res.values()), res
+    # TP=1 reference in this process
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512, fp8=fp8)
+    g = torch.Generator().manual_seed(9)
+    P = 29
+    toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(gpu)
+    cache = KVCache(m.cfg, 8, 16, gpu)
+    ar = torch.arange(P, dtype=torch.int32, device=gpu)
+    lg = m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=gpu), P,
+                   torch.tensor([P - 1], device=gpu), cache)[0].float().cpu()
+    for r in range(2):
+        c = torch.nn.functional.cosine_similarity(res[r], lg, dim=0).item()
+        assert c > 0.99, (r, c)
+    assert torch.equal(res[0], res[1])  # ranks agree exactly (replicated after the all-reduce)
