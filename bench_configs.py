@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Benchmarks for the other BASELINE.json configs (the headline config is bench.py):
+
+  encoder  config 2: bge-base-en-v1.5 bf16 on 1 MI355X, 64-candidate batches -> embeddings/s (+ the
+           cosine-consensus GEMM per batch)
+  moe      config 5: Mixtral-8x7B sampler (fp8 experts by default) + e5-mistral-7b embedder, N candidates
+           per request, embedding consensus -> answers/s.  Run under torchrun with --tp 2 for the TP=2
+           layout (heads and expert FFN split, RCCL all-reduce per row-parallel projection)
+
+(config 1 is the CPU plumbing test tests/test_server.py::test_config1_cpu_...; config 3 is
+`bench.py --candidates 32`; config 4 is `bench.py` under torchrun.)  Synthetic token ids and
+random-init weights; timing brackets the steps with synchronize (+ barrier under torchrun); one JSON
+line per run on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def _sync(dev, dist_on):
+    torch.cuda.synchronize(dev)
+    if dist_on:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+
+        pdist.barrier()
+        torch.cuda.synchronize(dev)
+
+
+def bench_encoder(a):
+    from llm_weighted_consensus_amd.embeddings.consensus import EmbeddingConsensus
+    from llm_weighted_consensus_amd.models.bert import BertEncoder
+    from llm_weighted_consensus_amd.models.config import encoder_config
+
+    dev = torch.device("cuda", 0)
+    enc = BertEncoder(encoder_config(a.encoder), device=dev, seed=1)
+    scorer = EmbeddingConsensus(enc, tau=0.05, max_tokens=512)
+    g = torch.Generator().manual_seed(0)
+    R, N, L = a.requests, a.candidates, a.seq_len
+    reqs = [[torch.randint(1000, 30000, (L,), generator=g).tolist() for _ in range(N)] for _ in range(R)]
+    for _ in range(a.warmup):
+        scorer.score(reqs)
+    _sync(dev, False)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = scorer.score(reqs)
+    _sync(dev, False)
+    dt = (time.perf_counter() - t0) / a.steps
+    return {"metric": "embeddings/sec (config 2: bge-base bf16, 64-candidate cosine consensus)",
+            "value": round(R * N / dt, 1), "unit": "embeddings/s", "n_gpus": 1, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+            "data": "synthetic token ids, random-init weights", "best_of_first_request": int(res.best[0]),
+            "config": {"model": a.encoder, "global_batch": R, "candidates_per_request": N, "seq_len": L}}
+
+
+def bench_moe(a):
+    from llm_weighted_consensus_amd.embeddings.consensus import EmbeddingConsensus
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.embedder import DecoderEmbedder
+    from llm_weighted_consensus_amd.models.llama import LlamaModel
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+
+    info = pdist.init_from_env("cuda")
+    tp = info.world if a.tp > 1 else 1
+    if a.tp > 1 and info.world != a.tp:
+        raise SystemExit(f"--tp {a.tp} needs torchrun with {a.tp} ranks (WORLD_SIZE={info.world})")
+    dev = torch.device("cuda", info.local_rank)
+    dcfg = decoder_config(a.decoder)
+    model = MixtralModel(dcfg, device=dev, seed=11, max_position=a.prompt_len + a.gen_len + 64, fp8=not a.bf16,
+                         tp_rank=info.rank if tp > 1 else 0, tp_size=tp)
+    emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64)
+    scorer = EmbeddingConsensus(DecoderEmbedder(emb_model, max_tokens=a.gen_len + 16), tau=0.05)
+    tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
+    R, N = a.requests, a.candidates
+    engine = LLMEngine(model, tok, max_batch=R * N, max_model_len=a.prompt_len + a.gen_len + 16,
+                       kv_memory_fraction=0.4, use_graphs=tp == 1)
+    g = torch.Generator().manual_seed(5)
+
+    def step(i):
+        groups = []
+        for r in range(R):
+            p = torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=g).tolist()
+            sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True, seed=i * 977 + r)
+            groups.append(engine.add_request(p, sp, n=N))
+        while engine.has_work():
+            engine.step()
+        return scorer.score([[s.tokens for s in gr.seqs] for gr in groups])
+
+    for i in range(a.warmup):
+        step(i)
+    _sync(dev, info.enabled)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    _sync(dev, info.enabled)
+    dt = pdist.max_over_ranks((time.perf_counter() - t0) / a.steps, dev)
+    return {"metric": "consensus answers/sec (config 5: Mixtral-8x7B sampler + e5-mistral-7b embedder)",
+            "value": round(R / dt, 4), "unit": "answers/s", "n_gpus": tp, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "bf16 activations, fp8 e4m3 expert weights" if not a.bf16 else "bf16",
+            "data": "synthetic prompts (random token ids), random-init weights",
+            "generated_tokens_per_s": round(R * N * a.gen_len / dt, 1),
+            "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": R, "candidates_per_request": N,
+                       "seq_len": a.prompt_len + a.gen_len, "parallelism": f"tp{tp}"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["encoder", "moe"])
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--requests", type=int, default=None)
+    ap.add_argument("--candidates", type=int, default=64)
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--prompt-len", type=int, default=256)
+    ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--encoder", default="bge-base-en-v1.5")
+    ap.add_argument("--decoder", default="mixtral-8x7b")
+    ap.add_argument("--embedder", default="e5-mistral-7b")
+    ap.add_argument("--bf16", action="store_true", help="bf16 experts instead of fp8")
+    ap.add_argument("--tp", type=int, default=1)
+    a = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if a.which == "encoder":
+        a.requests = a.requests or 64
+        out = bench_encoder(a)
+    else:
+        a.requests = a.requests or 8
+        out = bench_moe(a)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

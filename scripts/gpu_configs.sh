@@ -1,0 +1,18 @@
+#!/bin/bash
+# BASELINE configs 2, 3 and 5 (TP=1) on one MI355X; results -> gpurun_out/configs.log
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+: > gpurun_out/configs.log
+if [ "${ONLY:-}" != "moe" ]; then
+timeout -k 10 240 python bench_configs.py encoder >> gpurun_out/configs.log 2> gpurun_out/configs_err.log
+rc=$?; echo "config2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --candidates 32 --steps 2 --warmup 1 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
+rc=$?; echo "config3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
+[ "${ONLY:-}" = "small" ] && { cat gpurun_out/configs.log; exit 0; }
+timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-8} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
+rc=$?; echo "config5 rc=$rc"
+cat gpurun_out/configs.log
+exit $rc
