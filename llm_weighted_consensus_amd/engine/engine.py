@@ -20,6 +20,7 @@ import gc
 import itertools
 import random
 import threading
+import time
 from collections import deque
 from dataclasses import dataclass, field
 from typing import Callable, Deque, Dict, List, Optional, Sequence as Seq, Tuple
@@ -28,6 +29,8 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.faults import FaultInjector
+from ..utils.tracing import RequestTimer, span
 from .._runtime import BlockManager, prepare_decode_into, slots_range
 from ..models.llama import KVCache
 from .sampling import SamplingParams
@@ -99,6 +102,7 @@ class SequenceGroup:
         self.seqs = [Sequence(self, i, (base * 1000003 + i) & ((1 << 63) - 1)) for i in range(n)]
         self.bias_row = -1
         self.reserved_blocks = 0
+        self.timer = RequestTimer()
         self.prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     @property
@@ -272,6 +276,7 @@ class LLMEngine:
         self.bias: Optional[torch.Tensor] = None    # [max_batch, V] f32, lazily
         self.free_bias_rows = list(range(max_batch))
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0}
+        self.faults = FaultInjector.from_env()
         # step() returns TokenEvents only when asked (callbacks always get theirs)
         self.collect_events = False
         if tune_gc:
@@ -307,15 +312,17 @@ class LLMEngine:
         manager, and its input tokens are step t's sampler output, still on the device) BEFORE the
         host syncs on and post-processes step t, so detokenisation, stop checks and callbacks overlap
         the GPU.  A sequence that finishes at step t has one discarded row in step t+1."""
+        self.faults.on_step()
         events: List[TokenEvent] = []
         with self.lock:
             fits = self._first_waiting_fits()
         if fits:
             events += self._drain()
-            with self.lock:
+            with span("schedule"), self.lock:
                 admitted = self._admit()
             if admitted:
-                return events + self._prefill(admitted)
+                with span("prefill"):
+                    return events + self._prefill(admitted)
         if self.running or self.inflight is not None:
             events += self._decode()
         return events
@@ -357,8 +364,10 @@ class LLMEngine:
             cost = len(g.prompt_ids) if g.prefilled is None else 0  # imported prompts cost no compute
             if out and tokens + cost > self.prefill_token_budget:
                 break
+            self.faults.on_admit()
             self.waiting.popleft()
             g.reserved_blocks = need
+            g.timer.started()
             self.free_blocks_unreserved -= need
             tokens += cost
             out.append(g)
@@ -445,6 +454,8 @@ class LLMEngine:
                 seqs.append(s)
             self.bm.free_sequence(parent)
         events = self._sample_and_advance(torch.stack(rows), seqs)
+        for g in groups:
+            g.timer.token()
         for s in seqs:
             if not s.finished:
                 self.running.append(s)
@@ -673,10 +684,12 @@ class LLMEngine:
         seqs = [s for s in self.running if not s.finished and s.n_launched < s.params.max_tokens]
         if not seqs:
             return events + self._drain()
-        cur = self._launch(seqs)
+        with span("decode.launch"):
+            cur = self._launch(seqs)
         prev, self.inflight = self.inflight, cur
         if prev is not None:
-            events += self._process(prev)
+            with span("decode.process"):
+                events += self._process(prev)
         if sync:
             events += self._drain()
         self.running = [s for s in self.running if not s.finished]
@@ -768,7 +781,10 @@ class LLMEngine:
                 continue
             k = p.top_logprobs
             top = list(zip(ids_h[i][:k], lps_h[i][:k])) if k else []
-            ev = TokenEvent(s, t, text, float(lp_h[i]), top)
+            lp = float(lp_h[i])
+            if self.faults.bad_logprobs:
+                lp, top = float("nan"), [(a, float("nan")) for a, _ in top]
+            ev = TokenEvent(s, t, text, lp, top)
             if reason is not None:
                 self._finish(s, reason)
                 ev.finished, ev.finish_reason = True, reason
@@ -787,6 +803,9 @@ class LLMEngine:
             s.count_row = -1
         g = s.group
         if g.finished:
+            g.timer.tokens = max(len(x.tokens) for x in g.seqs)
+            g.timer.t_last = time.perf_counter()
+            g.timer.finished()
             self.free_blocks_unreserved += g.reserved_blocks
             g.reserved_blocks = 0
             if g.bias_row >= 0:

@@ -24,6 +24,15 @@ from ..schema import score as S
 from ..utils import json as sjson
 
 
+def torch_cuda_ok() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
 class Metrics:
     def __init__(self):
         self.counters: Dict[str, float] = {}
@@ -46,7 +55,16 @@ class Metrics:
                 lines.append(f'lwc_engine_{k}_total{{model="{name}"}} {v}')
             lines.append(f'lwc_engine_failures_total{{model="{name}"}} {svc.failures}')
         lines.append(f"lwc_uptime_seconds {time.time() - self.t0:.1f}")
-        return "\n".join(lines) + "\n"
+        if torch_cuda_ok():
+            import torch
+
+            for i in range(torch.cuda.device_count()):
+                free, total = torch.cuda.mem_get_info(i)
+                lines.append(f'lwc_gpu_hbm_used_bytes{{gpu="{i}"}} {total - free}')
+                lines.append(f'lwc_gpu_hbm_total_bytes{{gpu="{i}"}} {total}')
+        from ..utils.tracing import STATS
+
+        return "\n".join(lines) + "\n" + STATS.prometheus()
 
 
 class AppState:

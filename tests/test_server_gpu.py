@@ -1,0 +1,97 @@
+"""End-to-end on the GPU (the minimum slice): the ASGI server with a local
+random-init Llama voter model and a local BGE encoder.  /score/completions with N voters that all map
+to the local engine (json_schema output mode: constrained decoding guarantees a parseable key; votes
+from real top-k logprobs), /chat/completions streaming, /multichat, /consensus, /embeddings — and
+the fault path: an injected engine crash turns every voter into an error choice and the request into
+the reference's AllVotesFailed status."""
+import asyncio
+import json
+
+import httpx
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MODELS = {"tiny": {"arch": "llama-tiny", "weights": "random:1", "max_model_len": 2048, "max_batch": 64}}
+EMBED = {"bge-small": {"arch": "bge-small-en-v1.5", "weights": "random:2"}}
+
+
+def _client(monkeypatch, fault=None):
+    from llm_weighted_consensus_amd.server.app import create_app
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+
+    if fault:
+        monkeypatch.setenv("LWC_FAULT", fault)
+    else:
+        monkeypatch.delenv("LWC_FAULT", raising=False)
+    state = build_state(Config(models=MODELS, embed_models=EMBED, kv_fraction=0.05))
+    return state, httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t",
+                                    timeout=120)
+
+
+def _close(state):
+    for svc in state.services.values():
+        svc.close()
+
+
+SCORE = {"messages": [{"role": "user", "content": "Which city is the capital of France?"}],
+         "model": {"llms": [{"model": "tiny", "output_mode": "json_schema", "top_logprobs": 5},
+                            {"model": "tiny", "output_mode": "json_schema", "top_logprobs": 5, "temperature": 0.5},
+                            {"model": "tiny", "output_mode": "instruction", "top_logprobs": 5,
+                             "weight": {"type": "static", "weight": 2}}]},
+         "choices": ["Paris", "Madrid", "Rome"]}
+
+
+def test_score_chat_multichat_consensus_embeddings_local(gpu, monkeypatch):
+    state, c = _client(monkeypatch)
+
+    async def go():
+        r = await c.post("/score/completions", json=SCORE)
+        assert r.status_code == 200, r.text
+        body = r.json()
+        provided = [ch for ch in body["choices"] if ch["index"] < 3]
+        assert len(provided) == 3
+        # json_schema voters always produce a valid key -> their votes exist and sum to 1
+        voters = [ch for ch in body["choices"] if ch["index"] >= 3]
+        assert len(voters) == 3
+        ok = [v for v in voters if v.get("error") is None]
+        assert len(ok) >= 2
+        conf = sum(ch["confidence"] or 0 for ch in provided)
+        assert conf == pytest.approx(1.0, abs=1e-6)
+        # streaming chat from the local engine
+        r = await c.post("/chat/completions", json={"model": "tiny", "stream": True, "max_tokens": 8,
+                                                    "messages": [{"role": "user", "content": "hi"}], "n": 2})
+        assert r.status_code == 200 and r.text.endswith("data: [DONE]\n\n")
+        chunks = [json.loads(e[6:]) for e in r.text.split("\n\n") if e.startswith("data: {")]
+        assert chunks and all(ch["object"] == "chat.completion.chunk" for ch in chunks)
+        r = await c.post("/consensus/completions", json={"model": "tiny", "n": 4, "max_tokens": 12,
+                                                         "messages": [{"role": "user", "content": "say hi"}],
+                                                         "embedding_model": "bge-small"})
+        assert r.status_code == 200, r.text
+        assert sum(ch["confidence"] for ch in r.json()["choices"]) == pytest.approx(1.0, abs=1e-5)
+        r = await c.post("/embeddings", json={"model": "bge-small", "input": ["alpha", "beta"]})
+        assert r.status_code == 200 and len(r.json()["data"][0]["embedding"]) == 384
+        r = await c.get("/metrics")
+        assert "lwc_latency_seconds_count" in r.text and "lwc_engine_running" in r.text
+
+    try:
+        asyncio.run(go())
+    finally:
+        _close(state)
+
+
+def test_injected_engine_crash_gives_all_votes_failed(gpu, monkeypatch):
+    state, c = _client(monkeypatch, fault="worker_crash:1+")
+
+    async def go():
+        r = await c.post("/score/completions", json=SCORE)
+        # every voter failed with the engine's 500 -> AllVotesFailed(500)
+        assert r.status_code == 500, r.text
+        assert r.json()["kind"] == "score"
+
+    try:
+        asyncio.run(go())
+    finally:
+        _close(state)
+    assert all(svc.failures >= 1 for svc in state.services.values())
