@@ -99,7 +99,8 @@ class SequenceGroup:
         self.n = n
         self.callback = callback
         base = params.seed if params.seed is not None else random.getrandbits(63)
-        self.seqs = [Sequence(self, i, (base * 1000003 + i) & ((1 << 63) - 1)) for i in range(n)]
+        off = params.seed_offset
+        self.seqs = [Sequence(self, i, (base * 1000003 + off + i) & ((1 << 63) - 1)) for i in range(n)]
         self.bias_row = -1
         self.reserved_blocks = 0
         self.timer = RequestTimer()

@@ -1,0 +1,320 @@
+"""EngineGroup: one engine WORKER PROCESS per GPU behind one front end (SURVEY.md §7.1 "EngineGroup (1
+worker/GPU), candidate router"; §5 "worker heartbeat; on GPU/worker failure, drain and reschedule its
+sequences to surviving GPUs").
+
+* Each worker is a spawned process that owns one GPU and one `LLMEngine` (built from a JSON-able model
+  spec by ``worker_factory``), reads requests from its own queue and sends token events back on a
+  shared queue, batched per engine step.  It stamps a shared heartbeat every loop.
+* The front end exposes the `EngineService` API (`submit / abort / close / load`, plus an
+  ``engine`` facade with tokenizer / cfg / max_model_len), so `LocalChatClient` serves a whole node
+  through it unchanged.
+* Candidate routing: a request's n candidates are split across the live workers, least-loaded first
+  (candidate-parallel — the multichat / voter fan-out of the reference,
+  src/score/completions/client.rs:343-356, spread over GPUs); each worker's local choice indices are
+  offset into the request's global 0..n-1.  Candidate i gets seed base*1000003+i exactly as on one
+  engine, so results do not depend on the split.
+* Failure handling: a worker that exits or stops heart-beating is marked dead; each of its request
+  portions that has not emitted a token yet is resubmitted to a surviving worker, the others fail
+  with `EngineFailure` (the client turns that into an error choice / AllVotesFailed).
+"""
+from __future__ import annotations
+
+import importlib
+import itertools
+import multiprocessing as mp
+import queue as pyqueue
+import random
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field, replace
+from typing import Any, Dict, List, Optional
+
+from .sampling import SamplingParams
+from .service import EngineFailure
+
+
+@dataclass
+class GroupTokenEvent:
+    """Token event re-created in the front end (same fields the LocalChatClient reads)."""
+    index: int
+    token_id: int
+    text: str
+    logprob: float
+    top_logprobs: list
+    finished: bool
+    finish_reason: Optional[str]
+
+    @property
+    def seq(self):
+        return self
+
+
+@dataclass
+class _Portion:
+    worker: int
+    offset: int
+    n: int
+    params: SamplingParams
+    emitted: int = 0
+    finished: int = 0
+
+
+@dataclass
+class GroupRequest:
+    rid: int
+    prompt_ids: list
+    loop: Any
+    queue: Any
+    portions: List[_Portion] = field(default_factory=list)
+    failed: bool = False
+
+
+def _resolve(path: str):
+    mod, _, fn = path.partition(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop) -> None:
+    """Worker process: build the engine, serve requests until told to stop."""
+    try:
+        engine = _resolve(factory)(spec, wid)
+    except BaseException as e:  # report and die: the front end marks the worker dead
+        ev_q.put(("fatal", wid, f"{type(e).__name__}: {e}"))
+        return
+    ev_q.put(("ready", wid, None))
+    groups: Dict[int, Any] = {}
+    batch: List[tuple] = []
+    while not stop.is_set():
+        hb.value = time.time()
+        try:
+            block = not engine.has_work()
+            msg = req_q.get(timeout=0.2) if block else req_q.get_nowait()
+        except pyqueue.Empty:
+            msg = None
+        while msg is not None:
+            kind = msg[0]
+            if kind == "submit":
+                _, rid, prompt, params, n, offset = msg
+
+                def cb(ev, rid=rid, offset=offset):
+                    batch.append((rid, ev.seq.index + offset, ev.token_id, ev.text, ev.logprob,
+                                  list(ev.top_logprobs), ev.finished, ev.finish_reason))
+
+                try:
+                    groups[rid] = engine.add_request(prompt, params, n=n, callback=cb)
+                except ValueError as e:
+                    ev_q.put(("error", wid, (rid, str(e))))
+            elif kind == "abort":
+                g = groups.pop(msg[1], None)
+                if g is not None:
+                    engine.abort(g)
+            try:
+                msg = req_q.get_nowait()
+            except pyqueue.Empty:
+                msg = None
+        if engine.has_work():
+            try:
+                engine.step()
+            except Exception as e:  # engine failure: fail in-flight groups, keep the worker alive
+                traceback.print_exc()
+                for g in engine.fail_all(f"{type(e).__name__}: {e}"):
+                    rid = next((r for r, gg in groups.items() if gg is g), None)
+                    if rid is not None:
+                        ev_q.put(("error", wid, (rid, f"{type(e).__name__}: {e}")))
+        if batch:
+            ev_q.put(("tokens", wid, batch))
+            batch = []
+        for rid in [r for r, g in groups.items() if g.finished]:
+            groups.pop(rid)
+
+
+class _EngineFacade:
+    def __init__(self, tokenizer, cfg, max_model_len):
+        self.tokenizer, self.cfg, self.max_model_len = tokenizer, cfg, max_model_len
+        self.running, self.waiting = [], []
+
+
+class EngineGroup:
+    def __init__(self, spec: dict, devices: List[int], factory: str = "llm_weighted_consensus_amd.engine.group:build_engine",
+                 tokenizer=None, cfg=None, max_model_len: int = 4096, heartbeat_timeout: float = 30.0,
+                 start_timeout: float = 600.0):
+        self.spec, self.devices, self.factory = spec, list(devices), factory
+        self.heartbeat_timeout = heartbeat_timeout
+        ctx = mp.get_context("spawn")
+        self.ev_q = ctx.Queue()
+        self.stop = ctx.Event()
+        self.req_qs, self.hbs, self.procs = [], [], []
+        for wid, dev in enumerate(self.devices):
+            q = ctx.Queue()
+            hb = ctx.Value("d", time.time())
+            p = ctx.Process(target=worker_main, args=(wid, dict(spec, device=dev), factory, q, self.ev_q, hb, self.stop),
+                            daemon=True, name=f"lwc-worker-{wid}")
+            p.start()
+            self.req_qs.append(q)
+            self.hbs.append(hb)
+            self.procs.append(p)
+        self.alive = [True] * len(self.procs)
+        self.ready = [False] * len(self.procs)
+        self.load_of = [0] * len(self.procs)
+        self.requests: Dict[int, GroupRequest] = {}
+        self._rid = itertools.count(1)
+        self._lock = threading.Lock()
+        self.failures = 0
+        self.engine = _EngineFacade(tokenizer, cfg, max_model_len)
+        self._reader = threading.Thread(target=self._read, name="lwc-group-reader", daemon=True)
+        self._reader.start()
+        deadline = time.time() + start_timeout
+        while not all(r or not a for r, a in zip(self.ready, self.alive)):
+            if time.time() > deadline:
+                raise RuntimeError("EngineGroup: workers did not start")
+            self._check_health()
+            time.sleep(0.05)
+        if not any(self.alive):
+            raise RuntimeError("EngineGroup: every worker failed to start")
+
+    # ------------------------------------------------------------------ EngineService API
+    @property
+    def load(self) -> int:
+        return sum(self.load_of)
+
+    def live_workers(self) -> List[int]:
+        return [i for i, a in enumerate(self.alive) if a and self.ready[i]]
+
+    def submit(self, prompt_ids, params: SamplingParams, n: int, loop, queue) -> GroupRequest:
+        self._check_health()
+        live = self.live_workers()
+        if not live:
+            raise ValueError("no live engine workers")
+        rid = next(self._rid)
+        req = GroupRequest(rid, list(prompt_ids), loop, queue)
+        # candidate i of the request keeps seed base*1000003+i however the n candidates are split
+        base = params.seed if params.seed is not None else random.getrandbits(63)
+        order = sorted(live, key=lambda w: self.load_of[w])
+        share = [n // len(order) + (1 if k < n % len(order) else 0) for k in range(len(order))]
+        offset = 0
+        with self._lock:
+            self.requests[rid] = req
+            for w, m in zip(order, share):
+                if m == 0:
+                    continue
+                p = _Portion(w, offset, m, replace(params, seed=base, seed_offset=offset))
+                req.portions.append(p)
+                self.load_of[w] += m
+                self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset))
+                offset += m
+        return req
+
+    def abort(self, req: GroupRequest) -> None:
+        with self._lock:
+            self.requests.pop(req.rid, None)
+            for p in req.portions:
+                if self.alive[p.worker]:
+                    self.req_qs[p.worker].put(("abort", req.rid))
+                self.load_of[p.worker] -= p.n - p.finished
+
+    def close(self) -> None:
+        self.stop.set()
+        for p in self.procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+
+    # ------------------------------------------------------------------ reader / health
+    def _deliver(self, req: GroupRequest, item) -> None:
+        req.loop.call_soon_threadsafe(req.queue.put_nowait, item)
+
+    def _read(self) -> None:
+        while not self.stop.is_set():
+            try:
+                kind, wid, payload = self.ev_q.get(timeout=0.5)
+            except pyqueue.Empty:
+                self._check_health()
+                continue
+            except (EOFError, OSError):
+                return
+            if kind == "ready":
+                self.ready[wid] = True
+            elif kind == "fatal":
+                self.alive[wid] = False
+                self.failures += 1
+            elif kind == "error":
+                rid, msg = payload
+                with self._lock:
+                    req = self.requests.pop(rid, None)
+                if req is not None:
+                    self.failures += 1
+                    self._deliver(req, EngineFailure(msg))
+            elif kind == "tokens":
+                with self._lock:
+                    for (rid, idx, tid, text, lp, top, fin, reason) in payload:
+                        req = self.requests.get(rid)
+                        if req is None:
+                            continue
+                        p = next((p for p in req.portions if p.worker == wid and p.offset <= idx < p.offset + p.n),
+                                 None)
+                        if p is not None:
+                            p.emitted += 1
+                            if fin:
+                                p.finished += 1
+                                self.load_of[wid] -= 1
+                        self._deliver(req, GroupTokenEvent(idx, tid, text, lp, top, fin, reason))
+                        if all(pp.finished == pp.n for pp in req.portions):
+                            self.requests.pop(rid, None)
+            self._check_health()
+
+    def _check_health(self) -> None:
+        now = time.time()
+        for w, p in enumerate(self.procs):
+            if not self.alive[w]:
+                continue
+            stale = self.ready[w] and now - self.hbs[w].value > self.heartbeat_timeout
+            if not p.is_alive() or stale:
+                self._worker_died(w, "exited" if not p.is_alive() else "heartbeat timeout")
+
+    def _worker_died(self, w: int, why: str) -> None:
+        self.alive[w] = False
+        self.failures += 1
+        self.load_of[w] = 0
+        live = self.live_workers()
+        with self._lock:
+            for rid, req in list(self.requests.items()):
+                for p in [p for p in req.portions if p.worker == w and p.finished < p.n]:
+                    if p.emitted == 0 and live:
+                        # nothing streamed yet: reschedule the portion on the least-loaded survivor
+                        t = min(live, key=lambda x: self.load_of[x])
+                        p.worker = t
+                        self.load_of[t] += p.n
+                        self.req_qs[t].put(("submit", rid, req.prompt_ids, p.params, p.n, p.offset))
+                    else:
+                        self.requests.pop(rid, None)
+                        self._deliver(req, EngineFailure(f"engine worker {w} {why}"))
+                        break
+
+
+def build_engine(spec: dict, wid: int):
+    """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
+    ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8"})."""
+    import torch
+
+    from ..models.config import decoder_config
+    from ..models.llama import LlamaModel
+    from .engine import LLMEngine
+    from .tokenizer import ByteTokenizer
+
+    dev = torch.device("cuda", int(spec.get("device", 0)))
+    torch.cuda.set_device(dev)
+    cfg = decoder_config(spec["arch"])
+    w = spec.get("weights", "random:0")
+    path, seed = (None, int(w.split(":", 1)[1])) if w.startswith("random:") else (w, 0)
+    mlen = int(spec.get("max_model_len", 4096))
+    if cfg.num_experts:
+        from ..models.mixtral import MixtralModel
+
+        model = MixtralModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
+                             fp8=bool(spec.get("fp8", False)))
+    else:
+        model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
+    tok = ByteTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
+    return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
+                     kv_memory_fraction=float(spec.get("kv_fraction", 0.85)))

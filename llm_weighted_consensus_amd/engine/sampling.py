@@ -28,6 +28,9 @@ class SamplingParams:
     logprobs: bool = False
     top_logprobs: int = 0
     seed: Optional[int] = None
+    # index of this request's first candidate when its n candidates are split across engines
+    # (EngineGroup): candidate i draws with seed*1000003 + seed_offset + i on whichever GPU runs it
+    seed_offset: int = 0
     logit_bias: Optional[Dict[int, float]] = None
     # constrained decoding: an object with .mask(state) / .advance(state, token) / .start()
     constraint: Optional[object] = None

@@ -49,10 +49,15 @@ class Metrics:
             e = svc.engine
             lines.append(f'lwc_engine_running{{model="{name}"}} {len(e.running)}')
             lines.append(f'lwc_engine_waiting{{model="{name}"}} {len(e.waiting)}')
-            lines.append(f'lwc_engine_kv_free_blocks{{model="{name}"}} {e.bm.num_free}')
-            lines.append(f'lwc_engine_kv_total_blocks{{model="{name}"}} {e.bm.num_blocks}')
-            for k, v in e.stats.items():
+            lines.append(f'lwc_engine_load{{model="{name}"}} {svc.load}')
+            bm = getattr(e, "bm", None)
+            if bm is not None:
+                lines.append(f'lwc_engine_kv_free_blocks{{model="{name}"}} {bm.num_free}')
+                lines.append(f'lwc_engine_kv_total_blocks{{model="{name}"}} {bm.num_blocks}')
+            for k, v in getattr(e, "stats", {}).items():
                 lines.append(f'lwc_engine_{k}_total{{model="{name}"}} {v}')
+            if hasattr(svc, "alive"):
+                lines.append(f'lwc_engine_workers_alive{{model="{name}"}} {sum(svc.alive)}')
             lines.append(f'lwc_engine_failures_total{{model="{name}"}} {svc.failures}')
         lines.append(f"lwc_uptime_seconds {time.time() - self.t0:.1f}")
         if torch_cuda_ok():

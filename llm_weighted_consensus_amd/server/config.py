@@ -8,6 +8,8 @@ variables configure the local engine:
                           "max_model_len": 4096, "max_batch": 512}}   (default: none)
   LWC_EMBED_MODELS  JSON {name: {"arch": "bge-large-en-v1.5", "weights": "random:<seed>" | <path>}}
   LWC_GPU           device index for this process's engine (one process per GPU)
+  LWC_GPUS          comma list of devices: >1 entries serve each model through an EngineGroup (one
+                    worker process per GPU, candidates of a request split across them, failover)
   LWC_DEVICE        "cuda" (default) or "cpu": CPU runs embedding models only, on the fp32 reference
                     path (BASELINE config 1: canned completions + bge-small cosine consensus, no GPU)
   LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)
@@ -57,6 +59,7 @@ class Config:
     models: Dict[str, dict] = field(default_factory=dict)
     embed_models: Dict[str, dict] = field(default_factory=dict)
     gpu: int = 0
+    gpus: List[int] = field(default_factory=list)
     device: str = "cuda"
     kv_fraction: float = 0.85
     archive_path: Optional[str] = None
@@ -89,6 +92,8 @@ class Config:
             c.embed_models = json.loads(e["LWC_EMBED_MODELS"])
         c.gpu = int(e.get("LWC_GPU", e.get("LOCAL_RANK", "0")))
         c.device = e.get("LWC_DEVICE", "cuda").lower()
+        if e.get("LWC_GPUS"):
+            c.gpus = [int(x) for x in e["LWC_GPUS"].split(",") if x.strip()]
         c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))
         c.archive_path = e.get("LWC_ARCHIVE_PATH")
         c.registry_path = e.get("LWC_REGISTRY_PATH")

@@ -53,9 +53,17 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                               dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
             embedders[name] = EmbeddingService(enc, name)
         for name, spec in cfg.models.items():
-            path, seed = _weights_spec(spec)
             dcfg = decoder_config(spec["arch"])
             mlen = int(spec.get("max_model_len", 4096))
+            if len(cfg.gpus) > 1:  # one worker process per GPU behind one front end
+                from ..engine.group import EngineGroup
+
+                wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)))
+                services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
+                                             tokenizer=ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id,
+                                                                     dcfg.eos_token_id))
+                continue
+            path, seed = _weights_spec(spec)
             model = LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
             tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
             eng = LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,

@@ -1,0 +1,74 @@
+"""EngineGroup (CPU, fake engines in spawned worker processes): candidate routing across workers with
+global choice indices and split-independent seeds; a killed worker's not-yet-started portions are
+rescheduled on a survivor, started ones fail with EngineFailure; abort and close."""
+import asyncio
+import os
+import signal
+import time
+
+import pytest
+
+from llm_weighted_consensus_amd.engine.group import EngineGroup
+from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+from llm_weighted_consensus_amd.engine.service import EngineFailure
+
+FACTORY = "tests.fake_engine:make"
+
+
+def _collect(group, n, params, timeout=30):
+    async def go():
+        loop = asyncio.get_running_loop()
+        q = asyncio.Queue()
+        group.submit([1, 2, 3], params, n, loop, q)
+        toks = {i: [] for i in range(n)}
+        done = 0
+        while done < n:
+            ev = await asyncio.wait_for(q.get(), timeout)
+            if isinstance(ev, EngineFailure):
+                return toks, ev
+            toks[ev.seq.index].append(ev.token_id)
+            done += ev.finished
+        return toks, None
+
+    return asyncio.run(go())
+
+
+def test_group_splits_candidates_and_keeps_seeds():
+    g = EngineGroup({"delay": 0.0}, devices=[0, 0, 0], factory=FACTORY)
+    try:
+        sp = SamplingParams(max_tokens=4, seed=42)
+        toks, err = _collect(g, 7, sp)
+        assert err is None and sorted(toks) == list(range(7))
+        for i, t in toks.items():  # candidate i used seed 42*1000003 + i regardless of its worker
+            s = 42 * 1000003 + i
+            assert t == [(s + k) % 1000 for k in range(4)]
+        assert g.load == 0
+    finally:
+        g.close()
+
+
+def test_group_worker_death_reschedules_or_fails():
+    g = EngineGroup({"delay": 0.05}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=5)
+    try:
+        sp = SamplingParams(max_tokens=50, seed=1)
+        victim = g.procs[0]
+
+        async def go():
+            loop = asyncio.get_running_loop()
+            q = asyncio.Queue()
+            g.submit([1], sp, 4, loop, q)
+            ev = await asyncio.wait_for(q.get(), 30)  # tokens are flowing on both workers
+            os.kill(victim.pid, signal.SIGKILL)
+            while True:
+                ev = await asyncio.wait_for(q.get(), 30)
+                if isinstance(ev, EngineFailure):
+                    return ev
+
+        ev = asyncio.run(go())
+        assert "engine worker 0" in ev.message
+        assert g.alive == [False, True]
+        # new requests go to the survivor only
+        toks, err = _collect(g, 3, SamplingParams(max_tokens=3, seed=5))
+        assert err is None and len(toks) == 3
+    finally:
+        g.close()

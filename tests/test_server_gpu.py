@@ -95,3 +95,32 @@ def test_injected_engine_crash_gives_all_votes_failed(gpu, monkeypatch):
     finally:
         _close(state)
     assert all(svc.failures >= 1 for svc in state.services.values())
+
+
+def test_engine_group_two_workers_serve_chat(gpu, monkeypatch):
+    """LWC_GPUS with two entries: an EngineGroup of two worker processes (both on the box's one GPU here)
+    serves a chat request whose n candidates are split across them."""
+    from llm_weighted_consensus_amd.server.app import create_app
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+
+    monkeypatch.delenv("LWC_FAULT", raising=False)
+    monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    state = build_state(Config(models=MODELS, gpus=[0, 0], kv_fraction=0.04))
+    c = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t", timeout=300)
+    svc = state.services["tiny"]
+
+    async def go():
+        r = await c.post("/chat/completions", json={"model": "tiny", "max_tokens": 6, "n": 6, "seed": 3,
+                                                    "messages": [{"role": "user", "content": "hello"}]})
+        assert r.status_code == 200, r.text
+        ch = r.json()["choices"]
+        assert sorted(x["index"] for x in ch) == list(range(6))
+        r = await c.get("/metrics")
+        assert 'lwc_engine_workers_alive{model="tiny"} 2' in r.text
+
+    try:
+        assert len(svc.live_workers()) == 2
+        asyncio.run(go())
+    finally:
+        svc.close()
