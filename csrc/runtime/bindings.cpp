@@ -10,6 +10,35 @@
 namespace py = pybind11;
 using lwc::BlockManager;
 
+namespace lwc {
+// Python face of the consensus core (kept out of consensus_core.cpp so the core also builds without
+// Python, e.g. the sanitizer self-test csrc/tests/runtime_selftest.cpp).
+void bind_consensus_core(py::module_& m) {
+  py::class_<KeyTree>(m, "KeyTree")
+      .def(py::init<int, int, uint64_t>(), py::arg("source_len"), py::arg("max_branch_len"), py::arg("seed"))
+      .def_property_readonly("keys", &KeyTree::keys)
+      .def_property_readonly("depth", &KeyTree::depth)
+      .def_property_readonly("source_len", &KeyTree::source_len)
+      .def("regex_patterns", &KeyTree::regex_patterns)
+      .def("find_key", &KeyTree::find_key)
+      .def(
+          "vote",
+          [](const KeyTree& t, const std::string& content,
+             std::optional<std::vector<std::pair<std::string, std::vector<std::pair<std::string, double>>>>> lp) {
+            return t.vote(content, lp ? &*lp : nullptr);
+          },
+          py::arg("content"), py::arg("logprobs") = py::none());
+  py::class_<TallyResult>(m, "TallyResult")
+      .def_readonly("choice_weight", &TallyResult::choice_weight)
+      .def_readonly("confidence", &TallyResult::confidence)
+      .def_readonly("voter_confidence", &TallyResult::voter_confidence);
+  m.def("tally", &tally, py::arg("votes"), py::arg("weights"), py::arg("num_choices"));
+  m.def("unify_error_codes", &unify_error_codes);
+}
+
+}  // namespace lwc
+
+
 namespace {
 
 // Append one token to every sequence and build the padded decode batch in one call:

@@ -1,14 +1,9 @@
 #include "consensus_core.h"
 
-#include <pybind11/pybind11.h>
-#include <pybind11/stl.h>
-
 #include <algorithm>
 #include <cmath>
 #include <numeric>
 #include <stdexcept>
-
-namespace py = pybind11;
 
 namespace lwc {
 
@@ -257,29 +252,6 @@ std::optional<int> unify_error_codes(const std::vector<int>& codes) {
     if (e != code) code = (e >= 400 && e < 500 && code >= 400 && code < 500) ? 400 : 500;
   }
   return code;
-}
-
-void bind_consensus_core(py::module_& m) {
-  py::class_<KeyTree>(m, "KeyTree")
-      .def(py::init<int, int, uint64_t>(), py::arg("source_len"), py::arg("max_branch_len"), py::arg("seed"))
-      .def_property_readonly("keys", &KeyTree::keys)
-      .def_property_readonly("depth", &KeyTree::depth)
-      .def_property_readonly("source_len", &KeyTree::source_len)
-      .def("regex_patterns", &KeyTree::regex_patterns)
-      .def("find_key", &KeyTree::find_key)
-      .def(
-          "vote",
-          [](const KeyTree& t, const std::string& content,
-             std::optional<std::vector<std::pair<std::string, std::vector<std::pair<std::string, double>>>>> lp) {
-            return t.vote(content, lp ? &*lp : nullptr);
-          },
-          py::arg("content"), py::arg("logprobs") = py::none());
-  py::class_<TallyResult>(m, "TallyResult")
-      .def_readonly("choice_weight", &TallyResult::choice_weight)
-      .def_readonly("confidence", &TallyResult::confidence)
-      .def_readonly("voter_confidence", &TallyResult::voter_confidence);
-  m.def("tally", &tally, py::arg("votes"), py::arg("weights"), py::arg("num_choices"));
-  m.def("unify_error_codes", &unify_error_codes);
 }
 
 }  // namespace lwc

@@ -18,10 +18,6 @@
 #include <utility>
 #include <vector>
 
-namespace pybind11 {
-class module_;
-}
-
 namespace lwc {
 
 constexpr int kNumLetters = 20;  // 'A'..'T'
@@ -78,7 +74,5 @@ TallyResult tally(const std::vector<std::vector<double>>& votes, const std::vect
 // Error-code unification when every voter failed (reference client.rs:385-409): same code, else
 // 400 if all codes are 4xx, else 500.  `codes` empty => no error.
 std::optional<int> unify_error_codes(const std::vector<int>& codes);
-
-void bind_consensus_core(pybind11::module_& m);
 
 }  // namespace lwc
