@@ -25,6 +25,7 @@ int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const i
 int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
                      int, int, int, int, int, int, long long, int, hipStream_t);
+int lwc_gemm256(const void*, const void*, void*, const void*, int, int, int, int, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -286,6 +287,23 @@ void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const
            "grouped_gemm");
 }
 
+void gemm256(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R) {
+  // C[M, N] = A[M, K] . W[N, K]^T (+ R), bf16, row-major with unit inner stride.
+  CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(C); CHECK_CONTIG(W);
+  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1, "gemm256: 2-D row-major A/C");
+  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
+  TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm256: shape mismatch");
+  const void* r = nullptr;
+  if (R.has_value() && R->defined()) {
+    CHECK_BF16(*R);
+    TORCH_CHECK(R->sizes() == C.sizes() && R->strides() == C.strides(), "gemm256: residual must match C");
+    r = R->data_ptr();
+  }
+  CHECK_RC(lwc_gemm256(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
+                       cur_stream()),
+           "gemm256");
+}
+
 void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Tensor& topk_w, at::Tensor& row_off,
                at::Tensor& src_row, at::Tensor& inv) {
   CHECK_BF16(logits); CHECK_CONTIG(logits);
@@ -438,6 +456,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);
   m.def("grouped_gemm", &grouped_gemm);
+  m.def("gemm256", &gemm256);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);
   m.def("quant_fp8_rows", &quant_fp8_rows);

@@ -197,6 +197,16 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
     return out
 
 
+def gemm(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
+         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Hand-written 256x256-tile MFMA GEMM (K6): A [M, K] . W[N, K]^T (+ residual) -> [M, N] bf16
+    (same contract as F.linear without bias)."""
+    if out is None:
+        out = torch.empty(A.shape[0], W.shape[0], dtype=torch.bfloat16, device=A.device)
+    kernels().gemm256(A, W, out, residual)
+    return out
+
+
 def moe_route(logits: torch.Tensor, k: int):
     """Router top-k + softmax over the selected logits, expert segments and dispatch permutation (K11a).
     logits [T, E] bf16 -> (topk_ids [T,k] i32, topk_w [T,k] f32, row_off [E+1] i32, src_row [T*k] i32,

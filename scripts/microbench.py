@@ -95,8 +95,9 @@ def grouped(dev):
     """Hand-written grouped MFMA GEMM (K6g) vs hipBLASLt on plain shapes, and the MoE decode shape."""
     from llm_weighted_consensus_amd import ops
 
-    shapes = {"qkv": (6144, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
-    for M in (512, 3072):
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    for M in (1024, 3072):
         for name, (N, K) in shapes.items():
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)
             w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
@@ -108,9 +109,12 @@ def grouped(dev):
             sa = torch.ones(M, device=dev)
             sw = torch.ones(1, N, device=dev)
             t_8 = timeit(lambda: ops.grouped_gemm(xq, wq, off, a_scale=sa, w_scale=sw), iters=20)
+            t_2 = timeit(lambda: ops.gemm(x, w), iters=20)
+            err = (ops.gemm(x, w).float() - F.linear(x, w).float()).abs().max().item()
             fl = 2 * M * N * K / 1e12
             print(f"ggemm M={M:4d} {name:8s}: hipblaslt {t_h:7.1f} us ({fl / t_h * 1e6:6.0f} TF/s)  "
-                  f"mfma-bf16 {t_g:7.1f} us ({fl / t_g * 1e6:6.0f})  mfma-fp8 {t_8:7.1f} us ({fl / t_8 * 1e6:6.0f})",
+                  f"gemm256 {t_2:7.1f} us ({fl / t_2 * 1e6:6.0f}, err {err:.3g})  "
+                  f"grouped-bf16 {t_g:7.1f} us ({fl / t_g * 1e6:6.0f})  grouped-fp8 {t_8:7.1f} us ({fl / t_8 * 1e6:6.0f})",
                   flush=True)
     # Mixtral decode MoE: T tokens x top-2 over 8 experts, d=4096, ffn=14336 (gate_up fused 28672)
     E, d, f = 8, 4096, 14336

@@ -446,3 +446,17 @@ def test_grouped_gemm(gpu, fp8):
             continue
         ref_g = Ar[o[g]:o[g + 1]] @ Wr[g].t() + bias[g].float()
         _close(out[o[g]:o[g + 1]], ref_g, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,res", [(512, 768, 256, False), (300, 1024, 512, True), (1024, 4096, 4096, False)])
+def test_gemm256(gpu, M, N, K, res):
+    """256x256-tile LDS-DMA MFMA GEMM (+ fused residual add) vs an fp32 matmul, incl. a ragged M tail."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) * 0.05).to(torch.bfloat16)
+    R = torch.randn(M, N, device=gpu).to(torch.bfloat16) if res else None
+    out = ops.gemm(A, W, residual=R)
+    ref_o = A.float() @ W.float().t() + (R.float() if res else 0)
+    _close(out, ref_o, 3e-2, 1e-2)
