@@ -561,53 +561,64 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
 
   };
 
-  // ---- phase 2: each sequence's own blocks, rolling pipeline across the wave's sequences ----
+  // ---- phase 2: each sequence's own blocks, two pairs in flight per wave ----
+  // Positions walk (sequence j of the wave, block pair) across the wave's sequences.  Two register
+  // sets alternate (unrolled by two, so no register copies of in-flight loads): while one pair is on
+  // the MFMAs the next pair's K and V are already loading — two pairs (32 KiB) in flight per wave.
   auto phase2 = [&]() {
-  if (nrows > 0) {
-    auto seq_end = [&](int j) { return (p.ctx_lens[s0 + j] + kBS - 1) / kBS; };
-    // current position (j, pair); skip sequences with an empty suffix
-    int j = 0, pair = pblk, end = seq_end(0);
-    while (j < nseq_w && pair >= end) {
-      ++j;
-      if (j < nseq_w) end = seq_end(j);
-    }
-    if (j < nseq_w) {
-      DecodeParams lp{};
-      lp.kc = p.kc;
-      lp.vc = p.vc;
-      lp.Hkv = p.Hkv;
-      PairRegs r;
-      const int* bt = p.block_tables + (size_t)(s0 + j) * p.max_blocks;
-      load_pair_k(r, lp, bt, kvh, pair, pair + 1 < end, r16, g);
-      load_pair_v(r, lp, bt, kvh, pair, pair + 1 < end, r16, g);
-      while (j < nseq_w) {
-        const int ctx = p.ctx_lens[s0 + j];
-        const bool hasB = pair + 1 < end;
-        const bool row_on = r16 < nrows && r16 / p.G == j;
-        // next position
-        int j2 = j, pair2 = pair + 2, end2 = end;
-        while (j2 < nseq_w && pair2 >= end2) {
-          ++j2;
-          if (j2 < nseq_w) {
-            end2 = seq_end(j2);
-            pair2 = pblk;
-          }
-        }
-        const int* bt2 = p.block_tables + (size_t)(s0 + min(j2, nseq_w - 1)) * p.max_blocks;
-        float4v sa, sb;
-        pair_scores(r, qf, sa, sb);
-        if (j2 < nseq_w) load_pair_k(r, lp, bt2, kvh, pair2, pair2 + 1 < end2, r16, g);
-        short8 pf;
-        pair_softmax(sa, sb, pair, hasB, ctx, row_on, sl2, g, o, m, l, pf);
-        pair_values(r, pf, pair, hasB, ctx, g, o);
-        if (j2 < nseq_w) load_pair_v(r, lp, bt2, kvh, pair2, pair2 + 1 < end2, r16, g);
-        j = j2;
-        pair = pair2;
-        end = end2;
+    if (nrows <= 0) return;
+    DecodeParams lp{};
+    lp.kc = p.kc;
+    lp.vc = p.vc;
+    lp.Hkv = p.Hkv;
+    struct Pos {
+      int j, pair, end, ctx;
+    };
+    auto seq_pos = [&](int j) {  // first suffix pair of sequence j (or beyond), skipping empty suffixes
+      Pos q{j, pblk, 0, 0};
+      while (q.j < nseq_w) {
+        q.ctx = p.ctx_lens[s0 + q.j];
+        q.end = (q.ctx + kBS - 1) / kBS;
+        if (q.pair < q.end) break;
+        ++q.j;
       }
+      return q;
+    };
+    auto next = [&](Pos q) {
+      q.pair += 2;
+      return q.pair < q.end ? q : seq_pos(q.j + 1);
+    };
+    auto load = [&](PairRegs& r, const Pos& q) {
+      const int* bt = p.block_tables + (size_t)(s0 + q.j) * p.max_blocks;
+      load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
+      load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
+    };
+    auto attend = [&](const PairRegs& r, const Pos& q) {
+      const bool row_on = r16 < nrows && r16 / p.G == q.j;
+      float4v sa, sb;
+      pair_scores(r, qf, sa, sb);
+      short8 pf;
+      pair_softmax(sa, sb, q.pair, q.pair + 1 < q.end, q.ctx, row_on, sl2, g, o, m, l, pf);
+      pair_values(r, pf, q.pair, q.pair + 1 < q.end, q.ctx, g, o);
+    };
+    PairRegs ra, rb;
+    Pos p0 = seq_pos(0);
+    if (p0.j >= nseq_w) return;
+    Pos p1 = next(p0);
+    load(ra, p0);
+    if (p1.j < nseq_w) load(rb, p1);
+    while (true) {
+      attend(ra, p0);
+      if (p1.j >= nseq_w) break;
+      const Pos p2 = next(p1);
+      if (p2.j < nseq_w) load(ra, p2);
+      attend(rb, p1);
+      if (p2.j >= nseq_w) break;
+      const Pos p3 = next(p2);
+      if (p3.j < nseq_w) load(rb, p3);
+      p0 = p2;
+      p1 = p3;
     }
-  }
-
   };
 
   // Softmax merging is order-free: odd workgroups stream their suffixes first, so a CU's two

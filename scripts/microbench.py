@@ -153,7 +153,10 @@ def attention_prefix(dev):
     from llm_weighted_consensus_amd import ops
 
     Hq, Hkv, D, BS = 32, 8, 128, 16
-    for (R, N, P, gen) in [(16, 64, 16, 64), (8, 64, 16, 64), (16, 64, 16, 120)]:
+    cases = [(16, 64, 16, 64), (48, 64, 16, 64), (48, 64, 16, 120)]
+    if os.environ.get("MICRO_PREFIX_QUICK"):
+        cases = [(16, 64, 16, 64), (48, 64, 16, 64)]
+    for (R, N, P, gen) in cases:
         B = R * N
         sblk = (gen + 1 + BS - 1) // BS
         NB = R * P + B * sblk + 8
@@ -174,7 +177,7 @@ def attention_prefix(dev):
         pre_o = torch.empty(B * Hq * D, device=dev)
         pre_lse = torch.empty(B * Hq, device=dev)
         sc = 1 / math.sqrt(D)
-        for path, thr in (("wg4", 1 << 30), ("wave", 0)):
+        for path, thr in (() if os.environ.get("MICRO_PREFIX_QUICK") else (("wg4", 1 << 30), ("wave", 0))):
             old = ops.set_decode_wave_min_items(thr)
             t_pre = timeit(lambda: ops.paged_decode_prefix(q, kc, vc, bt, tiles, pre_o, pre_lse, Hq, sc))
             t_suf = timeit(lambda: ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc, start_blk=start, pre_o=pre_o,
