@@ -7,10 +7,13 @@ One consensus answer = one request fully served: prefill its prompt, sample N ca
 row-reduce) and pick the answer.  A bench *step* serves R requests per GPU end-to-end.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL): candidate-parallel — the global batch is R*W requests and
-rank r samples candidates [r*N/W, (r+1)*N/W) of EVERY request (per-GPU decode batch stays R*N: weak
-scaling).  Each rank prefills only its own R prompts; their KV blocks and last-token logits are
-all-gathered (C4) so no prompt is computed twice; one all-gather of the candidate embeddings (C1)
-gives every rank all N candidates of every request, then the consensus kernel runs.  Timed region: K steps bracketed by barrier + synchronize on
+the ranks form W/cp candidate-parallel groups of cp GPUs (cp = min(W, N/32) by default, so each GPU
+keeps >= 32 candidates of a request and the cascade attention still shares each prompt across >= 32
+sequences).  Group d serves R*cp requests; each of its ranks samples N/cp candidates of every one of
+them (per-GPU decode batch stays R*N: weak scaling).  Each rank prefills only R of the group's prompts;
+their KV blocks and last-token logits are all-gathered inside the group (C4) so no prompt is computed
+twice; one all-gather of the candidate embeddings (C1) gives the group all N candidates of its
+requests, then the consensus kernel runs.  Timed region: K steps bracketed by barrier + synchronize on
 both sides; the reported time is the max over ranks.
 
     python bench.py --gpus N --steps K --warmup W
@@ -39,6 +42,9 @@ def parse():
     ap.add_argument("--encoder", default="bge-large-en-v1.5")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-sharing", action="store_true", help="disable the cascade prefix attention pass")
+    ap.add_argument("--cp", type=int, default=0,
+                    help="candidate-parallel degree (ranks sharing one request's candidates); 0 = auto: "
+                         "min(world, candidates // 32) so every GPU keeps >= 32 candidates per request")
     ap.add_argument("--profile-steps", action="store_true", help="print a per-phase breakdown")
     return ap.parse_args()
 
@@ -62,9 +68,15 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {W}", file=sys.stderr)
     dev = torch.device("cuda", info.local_rank)
     N, R = a.candidates, a.requests
-    assert N % W == 0, "candidates must divide across ranks"
-    n_local = N // W
-    G = R * W  # global requests per step
+    cp = a.cp or max(1, min(W, N // 32))
+    while W % cp or N % cp:
+        cp -= 1
+    n_local = N // cp
+    G = R * W  # global requests per step (weak scaling: R per GPU)
+    # ranks form W/cp candidate groups; group d serves requests [d*R*cp, (d+1)*R*cp), each of its cp ranks
+    # samples n_local candidates of every one of them (per-GPU decode batch = R*N at any W)
+    cgroup, gidx, crank = pdist.candidate_groups(cp)
+    Rg = R * cp
 
     dcfg = decoder_config(a.decoder)
     ecfg = encoder_config(a.encoder)
@@ -72,30 +84,32 @@ def main():
     encoder = BertEncoder(ecfg, device=dev, seed=4321)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     max_len = a.prompt_len + a.gen_len + 16
-    engine = LLMEngine(model, tok, max_batch=G * n_local, max_model_len=max_len, use_graphs=not a.no_graphs,
+    engine = LLMEngine(model, tok, max_batch=Rg * n_local, max_model_len=max_len, use_graphs=not a.no_graphs,
                        kv_memory_fraction=0.5, prefix_sharing=not a.no_prefix_sharing)
     scorer = EmbeddingConsensus(encoder, tau=0.05, max_tokens=512)
     gen = torch.Generator().manual_seed(99)
 
     def one_step(step_idx: int):
         # identical synthetic prompts on every rank (same generator)
-        prompts = [torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=gen).tolist() for _ in range(G)]
+        all_prompts = [torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=gen).tolist() for _ in range(G)]
+        prompts = all_prompts[gidx * Rg:(gidx + 1) * Rg]  # this candidate group's requests
         t0 = time.perf_counter()
         groups = []
         shared = None
-        if W > 1:
-            # C4: prefill only this rank's R prompts, all-gather their KV blocks + last logits (RCCL)
-            kv, lg, nbl = engine.export_prefill(prompts[rank * R:(rank + 1) * R])
-            shared = all_gather_prefills(kv, lg, nbl)
+        if cp > 1:
+            # C4: prefill only this rank's R of the group's prompts, all-gather their KV blocks + last
+            # logits inside the candidate group (RCCL)
+            kv, lg, nbl = engine.export_prefill(prompts[crank * R:(crank + 1) * R])
+            shared = all_gather_prefills(kv, lg, nbl, group=cgroup)
         for gi, p in enumerate(prompts):
             sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True,
-                                seed=(step_idx * 1000003 + gi) * 131 + rank)
+                                seed=(step_idx * 1000003 + gidx * Rg + gi) * 131 + crank)
             groups.append(engine.add_request(p, sp, n=n_local, prefilled=shared[gi] if shared else None))
         while engine.has_work():
             engine.step()
         t1 = time.perf_counter()
         cands = [[s.tokens for s in g.seqs] for g in groups]
-        res = scorer.score(cands, gather=W > 1)
+        res = scorer.score(cands, gather=cp > 1, group=cgroup)
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         return res, t1 - t0, t2 - t1
@@ -146,8 +160,9 @@ def main():
                 "prompt_len": a.prompt_len,
                 "gen_len": a.gen_len,
                 "sampling": "temperature 0.8, top_p 0.95",
-                "parallelism": (f"candidate-parallel cp{W} (RCCL all-gather of prompt KV + embeddings)" if W > 1
-                                else "single GPU"),
+                "parallelism": (f"cp{cp} x dp{W // cp}: candidate-parallel groups of {cp} GPUs (RCCL all-gather of "
+                                f"prompt KV + embeddings inside a group), request-parallel across groups"
+                                if W > 1 else "single GPU"),
             },
         }
         print(json.dumps(out), flush=True)

@@ -37,13 +37,13 @@ def consensus_reference(E: torch.Tensor, tau: float) -> ConsensusResult:
     return ConsensusResult(cen.argmax(-1).tolist(), w, cen, S)
 
 
-def gather_candidates(E_local: torch.Tensor) -> torch.Tensor:
-    """Candidate-parallel all-gather (C1): [R, n_local, d] per rank -> [R, world*n_local, d] with rank r's
-    shard at candidates [r*n_local, (r+1)*n_local)."""
+def gather_candidates(E_local: torch.Tensor, group=None) -> torch.Tensor:
+    """Candidate-parallel all-gather (C1): [R, n_local, d] per rank -> [R, cp*n_local, d] with group rank
+    r's shard at candidates [r*n_local, (r+1)*n_local) (``group`` = the candidate-parallel ranks)."""
     if not pdist.info().enabled:
         return E_local
     R, n_local, d = E_local.shape
-    G = pdist.all_gather(E_local)  # [W, R, n_local, d]
+    G = pdist.all_gather(E_local, group)  # [cp, R, n_local, d]
     return G.permute(1, 0, 2, 3).reshape(R, -1, d).contiguous()
 
 
@@ -63,7 +63,8 @@ class EmbeddingConsensus:
             return ConsensusResult(best.tolist(), w, cen, S)
         return consensus_reference(E, self.tau)
 
-    def score(self, requests: Sequence[Sequence[Sequence[int]]], gather: bool = False) -> ConsensusResult:
+    def score(self, requests: Sequence[Sequence[Sequence[int]]], gather: bool = False,
+              group=None) -> ConsensusResult:
         """requests[r][i] = token ids of candidate i of request r (this rank's shard when gather=True;
         every rank must hold the same R and the same shard size)."""
         R = len(requests)
@@ -72,5 +73,5 @@ class EmbeddingConsensus:
         _, eb = self.embed(flat)
         E = eb.view(R, n_local, -1)
         if gather:
-            E = gather_candidates(E)
+            E = gather_candidates(E, group)
         return self.score_local(E.contiguous())

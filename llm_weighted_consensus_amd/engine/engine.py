@@ -177,9 +177,10 @@ class _GraphBucket:
 
 def cascade_table_size(B: int, per_tile: int) -> int:
     """Rows of a bucket's cascade tile table: one tile per `per_tile` sequences plus slack for group
-    boundaries (ragged groups beyond the slack degrade to plain rows, see :func:`cascade_tiles`).
-    Slack entries are launched workgroups that exit at once, so it is kept small."""
-    return -(-B // per_tile) + min(B // 8, 32)
+    boundaries — enough for every group to own a tile down to groups of 8 sequences (e.g. 64 candidates
+    split over 8 GPUs); smaller groups beyond the slack degrade to plain rows (:func:`cascade_tiles`).
+    Unused entries are workgroups that exit at once (measured: no cost vs an exact grid)."""
+    return -(-B // per_tile) + B // 8 + 1
 
 
 def cascade_tiles(runs: List[Tuple[int, int, int]], per_tile: int, tiles: np.ndarray) -> int:

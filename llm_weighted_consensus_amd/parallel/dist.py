@@ -81,26 +81,47 @@ def barrier() -> None:
             dist.barrier()
 
 
-def all_gather_flat(t: torch.Tensor) -> torch.Tensor:
-    """[*] per rank -> [world, *]: one all_gather_into_tensor on the flattened buffer (the 1-D form
+def group_size(group=None) -> int:
+    return dist.get_world_size(group) if _INFO.enabled else 1
+
+
+def all_gather_flat(t: torch.Tensor, group=None) -> torch.Tensor:
+    """[*] per rank -> [group size, *]: one all_gather_into_tensor on the flattened buffer (the 1-D form
     works for RCCL and gloo alike; GPU tensors under gloo are staged through host memory)."""
-    W = _INFO.world
+    W = group_size(group)
     flat = t.contiguous().view(-1)
     if _INFO.backend == "gloo" and flat.is_cuda:
         host = flat.cpu()
         out = torch.empty(W * host.numel(), dtype=host.dtype)
-        dist.all_gather_into_tensor(out, host)
+        dist.all_gather_into_tensor(out, host, group=group)
         return out.to(t.device).view(W, *t.shape)
     out = torch.empty(W * flat.numel(), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, flat)
+    dist.all_gather_into_tensor(out, flat, group=group)
     return out.view(W, *t.shape)
 
 
-def all_gather(t: torch.Tensor) -> torch.Tensor:
-    """[*] per rank -> [world, *] (C1).  One collective on a contiguous buffer."""
+def all_gather(t: torch.Tensor, group=None) -> torch.Tensor:
+    """[*] per rank -> [group size, *] (C1).  One collective on a contiguous buffer."""
     if not _INFO.enabled:
         return t.unsqueeze(0)
-    return all_gather_flat(t)
+    return all_gather_flat(t, group)
+
+
+def candidate_groups(cp: int):
+    """Split the world into world/cp consecutive groups of cp ranks (candidate-parallel inside a group,
+    request-parallel across groups).  Every rank creates every group (collective), returns
+    (this rank's group handle or None when cp == 1 / single process, group index, rank in group)."""
+    if not _INFO.enabled:
+        return None, 0, 0
+    W, r = _INFO.world, _INFO.rank
+    if cp < 1 or W % cp:
+        raise ValueError(f"candidate-parallel degree {cp} must divide the world size {W}")
+    mine = None
+    for d in range(W // cp):
+        g = dist.new_group(ranks=list(range(d * cp, (d + 1) * cp)))
+        if d == r // cp:
+            mine = g
+    return (mine if cp > 1 else None), r // cp, r % cp
 
 
 def all_reduce_(t: torch.Tensor, op: str = "sum", group=None) -> torch.Tensor:

@@ -21,35 +21,35 @@ import torch
 from . import dist as pdist
 
 
-def _gather_flat(t: torch.Tensor, world: int) -> torch.Tensor:
-    return pdist.all_gather_flat(t)
+def _gather_flat(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    return pdist.all_gather_flat(t, group)
 
 
-def all_gather_prefills(kv: torch.Tensor, logits: torch.Tensor,
-                        nblocks: List[int]) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+def all_gather_prefills(kv: torch.Tensor, logits: torch.Tensor, nblocks: List[int],
+                        group=None) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     """kv [L, 2, sum(nblocks), E] + logits [n, V] of this rank's prompts -> per prompt of ALL ranks
     (rank-major order) a (kv [L, 2, nb, E] view, logits [V] view) pair.
 
     Ranks may hold different numbers of prompts and blocks: the per-rank counts travel first (one tiny
     all-gather), then the KV and logits are padded to the largest rank and gathered once each."""
     info = pdist.info()
-    if not info.enabled:
+    if not info.enabled or group is None and info.world == 1:
         out, off = [], 0
         for i, nb in enumerate(nblocks):
             out.append((kv[:, :, off:off + nb], logits[i]))
             off += nb
         return out
-    W = info.world
+    W = pdist.group_size(group)
     dev = kv.device
     n = len(nblocks)
     counts = torch.tensor([n, int(sum(nblocks))], dtype=torch.int64, device=dev)
-    counts = _gather_flat(counts, W).cpu().tolist()
+    counts = _gather_flat(counts, W, group).cpu().tolist()
     max_n = max(c[0] for c in counts)
     max_nb = max(c[1] for c in counts)
     nbl = torch.zeros(max(max_n, 1), dtype=torch.int64, device=dev)
     if n:
         nbl[:n] = torch.tensor(nblocks, dtype=torch.int64, device=dev)
-    nbl_all = _gather_flat(nbl, W).cpu().tolist()
+    nbl_all = _gather_flat(nbl, W, group).cpu().tolist()
     L, two, nb_here, E = kv.shape
     kv_pad = kv
     if nb_here < max_nb:
@@ -60,8 +60,8 @@ def all_gather_prefills(kv: torch.Tensor, logits: torch.Tensor,
     if n < max(max_n, 1):
         lg_pad = torch.zeros(max(max_n, 1), V, dtype=logits.dtype, device=dev)
         lg_pad[:n] = logits
-    kv_all = _gather_flat(kv_pad, W)       # [W, L, 2, max_nb, E]
-    lg_all = _gather_flat(lg_pad, W)       # [W, max_n, V]
+    kv_all = _gather_flat(kv_pad, W, group)       # [W, L, 2, max_nb, E]
+    lg_all = _gather_flat(lg_pad, W, group)       # [W, max_n, V]
     out = []
     for r in range(W):
         off = 0

@@ -6,8 +6,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-LWC_SHARE_ONE_GPU=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 \
-  --requests ${REH_R:-4} --profile-steps > gpurun_out/rehearsal.log 2>&1
+NP=${REH_W:-2}
+LWC_SHARE_ONE_GPU=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP \
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus $NP --steps 1 --warmup 1 \
+  --requests ${REH_R:-4} --profile-steps ${REH_ARGS:-} > gpurun_out/rehearsal.log 2>&1
 rc=$?; echo "rehearsal rc=$rc"; grep -v amdgpu.ids gpurun_out/rehearsal.log | tail -8
 exit $rc

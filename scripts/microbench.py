@@ -262,7 +262,7 @@ def main():
     if "grouped" in a.what:
         grouped(dev)
     if "layout" in a.what:
-        gemm_layouts(dev, [512, 1024])
+        gemm_layouts(dev, [int(m) for m in os.environ.get("MICRO_M", "512,1024").split(",")])
     if "attn" in a.what:
         attention(dev)
     if "prefix" in a.what:

@@ -98,3 +98,33 @@ def test_prefill_share_all_gather_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+def _groups_worker(rank, world, port, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from llm_weighted_consensus_amd.embeddings.consensus import gather_candidates
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+
+    pdist.init_from_env("cpu")
+    g, gidx, crank = pdist.candidate_groups(2)
+    E = torch.full((3, 2, 4), float(rank))
+    got = gather_candidates(E, g)          # only the 2 ranks of this candidate group
+    ok = got.shape == (3, 4, 4) and got[0, :2].eq(gidx * 2).all() and got[0, 2:].eq(gidx * 2 + 1).all()
+    out_q.put((rank, bool(ok), gidx, crank))
+    pdist.shutdown()
+
+
+def test_candidate_groups_gloo():
+    """cp=2 x dp=2 over 4 ranks: gathers stay inside each candidate group."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_groups_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1:] for r in res] == [(True, 0, 0), (True, 0, 1), (True, 1, 0), (True, 1, 1)]
