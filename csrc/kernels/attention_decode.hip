@@ -5,7 +5,9 @@
 // Layout (all bf16):
 //   q        : [B, q_stride] — head hq at q + b*q_stride + hq*D (q lives inside the fused qkv row)
 //   k_cache  : [NB, Hkv, BS, D]          (token-major rows of D)
-//   v_cache  : [NB, Hkv, D, BS]          (TRANSPOSED: a column of V = BS contiguous tokens)
+//   v_cache  : [NB, Hkv, BS/4, D, 4]     (4-token INTERLEAVED: 4 consecutive tokens of one dim are
+//                                         8 contiguous bytes = one lane's PV B-operand slice; a token's
+//                                         row is written with 8 B stride, 4 dims per 32 B sector)
 //   block_tables [B, max_blocks] int32, ctx_lens [B] int32
 //
 // MFMA design (mfma_f32_16x16x32_bf16, one wave = 64 lanes, lane l: r16 = l & 15, g = l >> 4):
@@ -15,7 +17,7 @@
 //     C      : lane reg r = S^T[tok 4g + r][row r16]
 //   O = P V per 32 tokens (a PAIR of blocks A,B), k permuted as {A: 4g+0..3, B: 4g+0..3}:
 //     A (P)  : exactly the softmaxed S^T_A, S^T_B accumulator registers (no data movement)
-//     B (V)  : lane holds V[those 8 tokens][dim 16n + r16] -> two 8 B loads from the transposed cache
+//     B (V)  : lane holds V[those 8 tokens][dim 16n + r16] -> two 8 B loads from the interleaved cache
 //     C      : lane reg r = O[row 4g + r][dim 16n + r16]
 // The 16 MFMA rows are "query rows".  Plain decode: row = a query head of ONE sequence (only G of 16
 // rows are real — the op is HBM-bound so idle rows cost nothing).  Prefix mode: the n sequences that
@@ -85,9 +87,9 @@ LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, i
   const bf16_t* vA = p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
   const bf16_t* vB = p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    r.va[n] = *reinterpret_cast<const short4v*>(vA + (16 * n + r16) * kBS + 4 * g);
-    r.vb[n] = *reinterpret_cast<const short4v*>(vB + (16 * n + r16) * kBS + 4 * g);
+  for (int n = 0; n < 8; ++n) {  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
+    r.va[n] = *reinterpret_cast<const short4v*>(vA + (g * kD + 16 * n + r16) * 4);
+    r.vb[n] = *reinterpret_cast<const short4v*>(vB + (g * kD + 16 * n + r16) * 4);
   }
 }
 
@@ -525,9 +527,9 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
           if (seg < 2) {  // K [16 tok][256 B]: 16 B chunk XOR row
             const int row = pos >> 4, pch = pos & 15;
             src += row * 256 + ((pch ^ row) << 4);
-          } else {  // V^T [128 dim][32 B]: 16 B halves XOR row bit 3 (ds_read_b64 lane groups of 32)
-            const int row = pos >> 1, h = pos & 1;
-            src += row * 32 + ((h ^ ((row >> 3) & 1)) << 4);
+          } else {  // V [4 token groups][128 dim][8 B]: odd groups XOR byte bit 7 (ds_read_b64 halves)
+            const int b = pos << 4;
+            src += b ^ (((b >> 10) & 1) << 7);
           }
           unsigned char* dst = smem + pi * kPairBytes + (rd * (kCWaves * 64) + wid * 64) * 16;
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -550,7 +552,7 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
         }
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
-          const int off = (16 * n + r16) * (kBS * 2) + ((((g >> 1) ^ (r16 >> 3)) & 1) << 4) + ((g & 1) << 3);
+          const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
           r.va[n] = *reinterpret_cast<const short4v*>(pb + 2 * kSegBytes + off);
           r.vb[n] = *reinterpret_cast<const short4v*>(pb + 3 * kSegBytes + off);
         }

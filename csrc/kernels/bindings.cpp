@@ -44,6 +44,13 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// V cache of one layer: [NB, Hkv, BS/4, D, 4] bf16, the 4-token interleaved layout of the decode kernels.
+void check_v_cache(const at::Tensor& v, const at::Tensor& k, const char* who) {
+  TORCH_CHECK(v.dim() == 5 && v.size(0) == k.size(0) && v.size(1) == k.size(1) && v.size(2) * 4 == k.size(2) &&
+                  v.size(3) == k.size(3) && v.size(4) == 4 && v.is_contiguous(),
+              who, ": v_cache must be [NB, Hkv, BS/4, D, 4] matching k_cache [NB, Hkv, BS, D]");
+}
+
 #define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_DTYPE(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has dtype ", (t).scalar_type(), ", expected ", dt)
@@ -102,9 +109,9 @@ void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const c10::opti
   TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_kv_write: qkv row is not (Hq+2Hkv)*D");
   TORCH_CHECK(positions.numel() == T, "rope_kv_write: positions length");
   TORCH_CHECK(cos_t.size(1) == D / 2 && sin_t.size(1) == D / 2, "rope_kv_write: cos/sin table width");
-  // k_cache [NB, Hkv, BS, D]; v_cache [NB, Hkv, D, BS]
+  // k_cache [NB, Hkv, BS, D]; v_cache [NB, Hkv, BS/4, D, 4] (4-token interleaved)
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "rope_kv_write: k_cache shape");
-  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == Hkv && v_cache.size(2) == D, "rope_kv_write: v_cache shape");
+  check_v_cache(v_cache, k_cache, "rope_kv_write");
   const int BS = (int)k_cache.size(2);
   const int* sp = nullptr;
   if (slots.has_value() && slots->defined()) {
@@ -173,7 +180,7 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
   const int B = (int)out.size(0), Hq = (int)out.size(1), D = (int)out.size(2);
   const int Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
   TORCH_CHECK(q.size(0) == B && q.size(1) >= Hq * D, "paged_decode: q shape");
-  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "paged_decode: v_cache must be [NB, Hkv, D, BS]");
+  check_v_cache(v_cache, k_cache, "paged_decode");
   TORCH_CHECK(block_tables.size(0) == B && ctx_lens.numel() == B, "paged_decode: batch mismatch");
   float* po = nullptr;
   float* pl = nullptr;
@@ -209,6 +216,7 @@ void paged_decode_prefix(const at::Tensor& q, const at::Tensor& k_cache, const a
                          at::Tensor& pre_lse, int64_t Hq, double scale) {
   // tiles: [max_tiles, 3] int32 (row_start, nseq, prefix_blocks); unused tiles are all-zero rows.
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  check_v_cache(v_cache, k_cache, "paged_decode_prefix");
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(tiles, at::kInt); CHECK_CONTIG(tiles);
   CHECK_DTYPE(pre_o, at::kFloat); CHECK_DTYPE(pre_lse, at::kFloat);
   TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 3, "paged_decode_prefix: tiles must be [T, 3]");
@@ -229,6 +237,7 @@ void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const 
   // tiles: [max_tiles, 3] int32 super-tiles (row_start, nseq, prefix_blocks), nseq <= cascade_rows_per_tile(G);
   // the engine builds them on the host (rows must stay < B: the kernel trusts the table).
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out); CHECK_CONTIG(out);
+  check_v_cache(v_cache, k_cache, "paged_decode_cascade");
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt); CHECK_DTYPE(tiles, at::kInt);
   CHECK_CONTIG(tiles); CHECK_CONTIG(block_tables); CHECK_CONTIG(ctx_lens);
   TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 3, "paged_decode_cascade: tiles must be [T, 3]");

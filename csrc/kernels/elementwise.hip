@@ -11,7 +11,8 @@
 
 namespace lwc {
 
-// qkv: [T, (Hq + 2*Hkv) * D]; cos/sin: [max_pos, D/2] f32; cache: [NB, Hkv, BS, D] (K and V)
+// qkv: [T, (Hq + 2*Hkv) * D]; cos/sin: [max_pos, D/2] f32; K cache [NB, Hkv, BS, D];
+// V cache [NB, Hkv, BS/4, D, 4] (4-token interleaved)
 __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ positions,
                                                            const int* __restrict__ slots, const float* __restrict__ cos_t,
                                                            const float* __restrict__ sin_t, bf16_t* __restrict__ kc,
@@ -20,53 +21,50 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
   const int half = D >> 1;
   const int vec_per_head_rot = half >> 3;  // threads per head for rotation (8 dims each half)
   const int n_rot = (Hq + Hkv) * vec_per_head_rot;
-  const int vec_per_head = D >> 3;
-  const int n_v = Hkv * vec_per_head;
   const int row_len = (Hq + 2 * Hkv) * D;
   bf16_t* row = qkv + (size_t)t * row_len;
   const int pos = positions[t];
   const int slot = slots ? slots[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
-  for (int i = threadIdx.x; i < n_rot + n_v; i += blockDim.x) {
-    if (i < n_rot) {
-      const int h = i / vec_per_head_rot;      // 0..Hq+Hkv-1 (q heads then k heads)
-      const int c = (i % vec_per_head_rot) * 8;  // first-half dim offset
-      bf16_t* hp = row + h * D;
-      uint4v* p1 = reinterpret_cast<uint4v*>(hp + c);
-      uint4v* p2 = reinterpret_cast<uint4v*>(hp + c + half);
-      float x1[8], x2[8], o1[8], o2[8];
-      unpack8(*p1, x1);
-      unpack8(*p2, x2);
-      const float4* cp = reinterpret_cast<const float4*>(cos_t + (size_t)pos * half + c);
-      const float4* sp = reinterpret_cast<const float4*>(sin_t + (size_t)pos * half + c);
-      float cs[8], sn[8];
-      *reinterpret_cast<float4*>(cs) = cp[0];
-      *reinterpret_cast<float4*>(cs + 4) = cp[1];
-      *reinterpret_cast<float4*>(sn) = sp[0];
-      *reinterpret_cast<float4*>(sn + 4) = sp[1];
+  for (int i = threadIdx.x; i < n_rot; i += blockDim.x) {
+    const int h = i / vec_per_head_rot;      // 0..Hq+Hkv-1 (q heads then k heads)
+    const int c = (i % vec_per_head_rot) * 8;  // first-half dim offset
+    bf16_t* hp = row + h * D;
+    uint4v* p1 = reinterpret_cast<uint4v*>(hp + c);
+    uint4v* p2 = reinterpret_cast<uint4v*>(hp + c + half);
+    float x1[8], x2[8], o1[8], o2[8];
+    unpack8(*p1, x1);
+    unpack8(*p2, x2);
+    const float4* cp = reinterpret_cast<const float4*>(cos_t + (size_t)pos * half + c);
+    const float4* sp = reinterpret_cast<const float4*>(sin_t + (size_t)pos * half + c);
+    float cs[8], sn[8];
+    *reinterpret_cast<float4*>(cs) = cp[0];
+    *reinterpret_cast<float4*>(cs + 4) = cp[1];
+    *reinterpret_cast<float4*>(sn) = sp[0];
+    *reinterpret_cast<float4*>(sn + 4) = sp[1];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o1[j] = x1[j] * cs[j] - x2[j] * sn[j];
-        o2[j] = x2[j] * cs[j] + x1[j] * sn[j];
-      }
-      const uint4v n1 = pack8(o1), n2 = pack8(o2);
-      *p1 = n1;
-      *p2 = n2;
-      if (h >= Hq && slot >= 0) {
-        const int kh = h - Hq;
-        bf16_t* dst = kc + (((size_t)blk * Hkv + kh) * BS + off) * D;
-        *reinterpret_cast<uint4v*>(dst + c) = n1;
-        *reinterpret_cast<uint4v*>(dst + c + half) = n2;
-      }
-    } else if (slot >= 0) {
-      // V is cached TRANSPOSED per block ([NB, Hkv, D, BS]) so that the decode kernel's P.V MFMA
-      // reads its B operand (a column of V) as contiguous tokens (see attention_decode.hip).
-      const int j = i - n_rot;
-      const int vh = j / vec_per_head, c = (j % vec_per_head) * 8;
-      const bf16_t* src = row + (Hq + Hkv + vh) * D + c;
-      bf16_t* dst = vc + (((size_t)blk * Hkv + vh) * D + c) * BS + off;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dst[(size_t)e * BS] = src[e];
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = x1[j] * cs[j] - x2[j] * sn[j];
+      o2[j] = x2[j] * cs[j] + x1[j] * sn[j];
+    }
+    const uint4v n1 = pack8(o1), n2 = pack8(o2);
+    *p1 = n1;
+    *p2 = n2;
+    if (h >= Hq && slot >= 0) {
+      const int kh = h - Hq;
+      bf16_t* dst = kc + (((size_t)blk * Hkv + kh) * BS + off) * D;
+      *reinterpret_cast<uint4v*>(dst + c) = n1;
+      *reinterpret_cast<uint4v*>(dst + c + half) = n2;
+    }
+  }
+  // V is cached 4-token interleaved per block ([NB, Hkv, BS/4, D, 4]) so the decode kernels' P.V MFMA
+  // reads 4 consecutive tokens of a dim as one 8 B load (see attention_decode.hip).  One element per
+  // thread, consecutive threads = consecutive dims: a wave's 64 stores cover 16 32-byte sectors.
+  if (slot >= 0) {
+    const bf16_t* vsrc = row + (Hq + Hkv) * D;
+    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) {
+      const int vh = i / D, d = i - vh * D;
+      vc[((size_t)blk * Hkv + vh) * D * BS + ((off >> 2) * D + d) * 4 + (off & 3)] = vsrc[i];
     }
   }
 }

@@ -65,7 +65,7 @@ class LayerWeights:
 
 class KVCache:
     """One flat bf16 pool for all layers: [L, 2, num_blocks, Hkv*BS*D]; per-layer K view
-    [NB, Hkv, BS, D] and transposed V view [NB, Hkv, D, BS]."""
+    [NB, Hkv, BS, D] and 4-token-interleaved V view [NB, Hkv, BS/4, D, 4] (see attention_decode.hip)."""
 
     def __init__(self, cfg: DecoderConfig, num_blocks: int, block_size: int, device, dtype=torch.bfloat16):
         self.cfg, self.num_blocks, self.block_size = cfg, num_blocks, block_size
@@ -73,7 +73,7 @@ class KVCache:
         self.pool = torch.zeros(cfg.layers, 2, num_blocks, self.block_elems, dtype=dtype, device=device)
         Hkv, D = cfg.kv_heads, cfg.head_dim
         self.k = [self.pool[l, 0].view(num_blocks, Hkv, block_size, D) for l in range(cfg.layers)]
-        self.v = [self.pool[l, 1].view(num_blocks, Hkv, D, block_size) for l in range(cfg.layers)]
+        self.v = [self.pool[l, 1].view(num_blocks, Hkv, block_size // 4, D, 4) for l in range(cfg.layers)]
 
     @staticmethod
     def bytes_per_block(cfg: DecoderConfig, block_size: int) -> int:
@@ -91,7 +91,7 @@ class _NullCache:
     def __init__(self, cfg: DecoderConfig, device):
         buf = torch.zeros(2, 1, cfg.kv_heads, 16, cfg.head_dim, dtype=torch.bfloat16, device=device)
         self.k = [buf[0]] * cfg.layers
-        self.v = [buf[1].view(1, cfg.kv_heads, cfg.head_dim, 16)] * cfg.layers
+        self.v = [buf[1].view(1, cfg.kv_heads, 4, cfg.head_dim, 4)] * cfg.layers
 
 
 class LlamaModel:

@@ -7,7 +7,7 @@ raises: on a GPU box a silent fallback would hide that the native path is not th
 Layout conventions shared with the engine:
   * fused qkv rows  : [T, (Hq + 2*Hkv) * D]
   * K cache (layer) : [num_blocks, Hkv, block_size, D]
-  * V cache (layer) : [num_blocks, Hkv, D, block_size]   (transposed, see attention_decode.hip)
+  * V cache (layer) : [num_blocks, Hkv, block_size/4, D, 4]   (4-token interleaved, see attention_decode.hip)
 """
 from __future__ import annotations
 
@@ -95,6 +95,16 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor,
     """In-place rotate-half RoPE on q and k inside ``qkv`` and scatter k, v into the paged cache at
     ``slots`` (K2).  ``slots=None`` only rotates (no cache write)."""
     kernels().rope_kv_write(qkv, positions, slots, cos, sin, k_cache, v_cache, int(Hq), int(Hkv), int(D))
+
+
+def v_token(v_cache: torch.Tensor, block: int, t: int) -> torch.Tensor:
+    """[Hkv, D] view of token `t` of block `block` in a 4-token-interleaved V cache."""
+    return v_cache[block, :, t // 4, :, t % 4]
+
+
+def v_gather(v_cache: torch.Tensor, blocks: torch.Tensor, toks: torch.Tensor) -> torch.Tensor:
+    """V rows [L, Hkv, D] of (block, token-in-block) pairs from a 4-token-interleaved V cache."""
+    return v_cache[blocks.long(), :, toks.long() // 4, :, toks.long() % 4]
 
 
 def kv_block_copy(cache: torch.Tensor, pairs: torch.Tensor) -> None:

@@ -137,7 +137,7 @@ def attention(dev):
         nb = (ctx_len + BS - 1) // BS
         NB = B * nb + 8
         kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
-        vc = torch.randn(NB, Hkv, D, BS, device=dev).to(torch.bfloat16)
+        vc = torch.randn(NB, Hkv, BS // 4, D, 4, device=dev).to(torch.bfloat16)
         bt = torch.arange(B * nb, device=dev, dtype=torch.int32).view(B, nb)
         ctx = torch.full((B,), ctx_len, device=dev, dtype=torch.int32)
         q = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
@@ -161,7 +161,7 @@ def attention_prefix(dev):
         sblk = (gen + 1 + BS - 1) // BS
         NB = R * P + B * sblk + 8
         kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
-        vc = torch.randn(NB, Hkv, D, BS, device=dev).to(torch.bfloat16)
+        vc = torch.randn(NB, Hkv, BS // 4, D, 4, device=dev).to(torch.bfloat16)
         width = P + sblk
         bt = torch.zeros(B, width, dtype=torch.int32)
         for r in range(R):
@@ -239,7 +239,19 @@ def sampler(dev):
 def small(dev):
     from llm_weighted_consensus_amd import ops
 
-    for T in (256, 512):
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import KVCache, rope_tables
+
+    cfg = decoder_config("llama-3-8b")
+    cos, sin = rope_tables(cfg, dev, 4096)
+    for T in (512, 3072):
+        cache = KVCache(cfg, T + 64, 16, dev)
+        qkv = torch.randn(T, cfg.qkv_dim, device=dev).to(torch.bfloat16)
+        pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
+        slots = (torch.randperm(T, device=dev).to(torch.int32) * 16 + 5)
+        us = timeit(lambda: ops.rope_kv_write(qkv, pos, cos, sin, cache.k[0], cache.v[0], 32, 8, 128, slots=slots))
+        print(f"rope_kv_write T={T}: {us:6.1f} us", flush=True)
+    for T in (512, 3072):
         x = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
         r = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
         w = torch.ones(4096, device=dev, dtype=torch.bfloat16)

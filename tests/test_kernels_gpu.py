@@ -84,7 +84,7 @@ def test_rope_kv_write(gpu):
     pos = torch.randint(0, 200, (T,), device=gpu, dtype=torch.int32)
     slots = torch.randperm(NB * BS, device=gpu)[:T].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=gpu)
-    vc = torch.zeros(NB, Hkv, D, BS, dtype=torch.bfloat16, device=gpu)
+    vc = torch.zeros(NB, Hkv, BS // 4, D, 4, dtype=torch.bfloat16, device=gpu)
     ops.rope_kv_write(qkv, pos, cos, sin, kc, vc, Hq, Hkv, D, slots=slots)
     q_ref = ref.rope(q0[:, : Hq * D].view(T, Hq, D), pos, cos, sin)
     k_ref = ref.rope(q0[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D), pos, cos, sin)
@@ -93,7 +93,7 @@ def test_rope_kv_write(gpu):
     _close(qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D), k_ref, 2e-2, 1e-2)
     blk, off = (slots // BS).long(), (slots % BS).long()
     _close(kc[blk, :, off, :], k_ref, 2e-2, 1e-2)
-    _close(vc[blk, :, :, off], v_ref, 0)
+    _close(ops.v_token(vc, blk, off), v_ref, 0)
 
 
 @pytest.fixture(params=["wg4", "wave"])
@@ -117,7 +117,7 @@ def test_paged_decode(gpu, G, splits, decode_path):
     ctx = torch.tensor([1, 15, 16, 77, 200], dtype=torch.int32, device=gpu)
     width = 16
     kc = _bf(NB, Hkv, BS, D, dev=gpu)
-    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    vc = _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
     # poison the cache beyond context with NaNs to check masking
     perm = torch.randperm(NB, device=gpu)
     bt = torch.zeros(B, width, dtype=torch.int32, device=gpu)
@@ -132,7 +132,8 @@ def test_paged_decode(gpu, G, splits, decode_path):
         o = L % BS
         if o:
             kc[last, :, o:, :] = float("nan")
-            vc[last, :, :, o:] = float("nan")
+            for tt in range(o, BS):
+                ops.v_token(vc, last, tt).fill_(float("nan"))
     q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
     out = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits)
     for b in range(B):
@@ -140,7 +141,7 @@ def test_paged_decode(gpu, G, splits, decode_path):
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()
         kk = kc[blk, :, toks % BS, :]  # [L, Hkv, D]
-        vv = vc[blk, :, :, toks % BS]  # [L, Hkv, D]
+        vv = ops.v_gather(vc, blk, toks % BS)  # [L, Hkv, D]
         q = q_full[b, : Hq * D].view(1, Hq, D)
         o = ref.attention(q, kk, vv, False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
@@ -164,7 +165,7 @@ def test_paged_decode_cascade(gpu, G):
     width = 12
     NB = 4 + sum(p + c * (width - p) for c, p in groups)
     kc = _bf(NB, Hkv, BS, D, dev=gpu)
-    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    vc = _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
     bt = torch.zeros(B, width, dtype=torch.int32)
     ctx = torch.zeros(B, dtype=torch.int32)
     nxt, row, runs = 0, 0, []
@@ -186,7 +187,8 @@ def test_paged_decode_cascade(gpu, G):
         if L % BS:
             last = int(bt[b, (L - 1) // BS])
             kc[last, :, L % BS:, :] = float("nan")
-            vc[last, :, :, L % BS:] = float("nan")
+            for tt in range(L % BS, BS):
+                ops.v_token(vc, last, tt).fill_(float("nan"))
     tiles_np = np.zeros((-(-B // per) + len(groups) + 2, 3), dtype=np.int32)
     nt = cascade_tiles(runs, per, tiles_np)
     assert nt >= len(groups)
@@ -199,7 +201,7 @@ def test_paged_decode_cascade(gpu, G):
         L = int(ctx[b])
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()
-        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], vc[blk, :, :, toks % BS],
+        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
                           False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
 
@@ -218,7 +220,7 @@ def test_paged_decode_prefix_shared(gpu, G, splits, decode_path):
                        dtype=torch.int32, device=gpu)
     width = 8
     kc = _bf(NB, Hkv, BS, D, dev=gpu)
-    vc = _bf(NB, Hkv, D, BS, dev=gpu)
+    vc = _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
     bt = torch.zeros(B, width, dtype=torch.int32, device=gpu)
     nxt = 0
 
@@ -260,7 +262,7 @@ def test_paged_decode_prefix_shared(gpu, G, splits, decode_path):
         L = int(ctx[b])
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()
-        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], vc[blk, :, :, toks % BS],
+        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
                           False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
 
