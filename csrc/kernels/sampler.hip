@@ -44,6 +44,8 @@ struct SampleParams {
   const unsigned long long* seeds;    // [B]
   const unsigned long long* offsets;  // [B] (step counter)
   int num_logprobs;          // K for top logprobs (0..20)
+  int mask_logprobs;         // 1: rows with a grammar mask report logprobs over the MASKED distribution
+                             //    (the restricted softmax over the allowed tokens — the vote fast path)
   int* out_token;            // [B]
   float* out_logprob;        // [B]  raw logprob of the sampled token
   int* out_topk_ids;         // [B, K]
@@ -121,10 +123,21 @@ __global__ void __launch_bounds__(kSampT) sample_kernel(SampleParams p) {
 
   // ---- load the raw row once ----
   uint4v row[SLOTS];
+  const uint32_t* lmask =
+      (p.mask_logprobs && p.mask && p.mask_rows[b] >= 0) ? p.mask + (size_t)p.mask_rows[b] * (p.V >> 5) : nullptr;
 #pragma unroll
   for (int j = 0; j < SLOTS; ++j) {
     const int vi = j * kSampT + t;
     row[j] = vi < nvec ? *reinterpret_cast<const uint4v*>(lrow + (size_t)vi * 8) : uint4v{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};
+    if (lmask && vi < nvec) {  // constrained logprobs: disallowed tokens are -inf from the start
+      const uint32_t bits = (lmask[vi >> 2] >> ((vi & 3) * 8)) & 0xffu;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t lo = (bits >> (2 * c)) & 1u ? (row[j][c] & 0xffffu) : 0xff80u;
+        const uint32_t hi = (bits >> (2 * c + 1)) & 1u ? (row[j][c] >> 16) : 0xff80u;
+        row[j][c] = lo | (hi << 16);
+      }
+    }
   }
   // ---- raw log-sum-exp ----
   float mx = -INFINITY;
@@ -145,7 +158,9 @@ OPAQUE_ROW(row);
   // ---- raw top-K (for top_logprobs) ----
   const int K = p.num_logprobs;
   if (K > 0) {
-    uint32_t lo = 0, hi = 0xffffu;  // largest key with count(>= key) >= K
+    // largest key with count(>= key) >= K, never below the key just above -inf (0x7f): masked-out
+    // (-inf) entries are not candidates, so a row with < K finite values returns fewer (rest: id -1)
+    uint32_t lo = 0x80u, hi = 0xffffu;
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
       OPAQUE_ROW(row);
@@ -180,6 +195,10 @@ OPAQUE_ROW(row);
     __syncthreads();
     if (t < 64) {  // one wave: rank-sort the collected candidates (value desc, index asc)
       const int n = min(s_ccount, kCollect);
+      for (int r = n + t; r < K; r += 64) {  // fewer finite values than K: empty slots
+        p.out_topk_ids[(size_t)b * K + r] = -1;
+        p.out_topk_lp[(size_t)b * K + r] = -INFINITY;
+      }
       if (t < n) {
         const float v = s_cval[t];
         const int ix = s_cidx[t];
@@ -453,13 +472,14 @@ extern "C" int lwc_sample(const void* logits, int ld, int V, int B, const float*
                           const float* pres_pen, const float* rep_pen, void* counts, const int* count_rows,
                           const float* bias, const int* bias_rows, const unsigned int* mask, const int* mask_rows,
                           const unsigned long long* seeds, const unsigned long long* offsets, int num_logprobs,
-                          int* out_token, float* out_logprob, int* out_topk_ids, float* out_topk_lp, hipStream_t s) {
+                          int mask_logprobs, int* out_token, float* out_logprob, int* out_topk_ids,
+                          float* out_topk_lp, hipStream_t s) {
   using namespace lwc;
   if (V % 32 != 0 || num_logprobs < 0 || num_logprobs > kMaxTopK) return -1;
   if (B == 0) return 0;
   SampleParams p{(const bf16_t*)logits, ld, V, temperature, top_p, top_k, min_p, top_a, freq_pen, pres_pen, rep_pen,
                  (uint16_t*)counts, count_rows, bias, bias_rows, mask, mask_rows, seeds, offsets, num_logprobs,
-                 out_token, out_logprob, out_topk_ids, out_topk_lp};
+                 mask_logprobs, out_token, out_logprob, out_topk_ids, out_topk_lp};
   const int nvec = V / 8;
   const int slots = (nvec + kSampT - 1) / kSampT;
   if (slots <= 4)

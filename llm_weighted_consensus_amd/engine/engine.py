@@ -243,7 +243,7 @@ class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
                  use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
-                 cascade_min_batch: int = 128, tune_gc: bool = True):
+                 cascade_min_batch: int = 128, tune_gc: bool = True, constrained_logprobs: bool = False):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -265,6 +265,9 @@ class LLMEngine:
         # decode batches >= this bucket use the cascade (shared-prompt) attention kernel; smaller ones
         # the split-K kernel, which spreads a few long contexts over more workgroups
         self.cascade_min_batch = cascade_min_batch
+        # report logprobs of grammar-constrained steps over the allowed tokens only (vote fast path:
+        # at a constrained key letter that is the restricted softmax over the sibling letters)
+        self.constrained_logprobs = constrained_logprobs
         self.buckets: Dict[int, _GraphBucket] = {}
         self.inflight: Optional[_Step] = None
         self._step_no = 0
@@ -634,7 +637,7 @@ class LLMEngine:
                    count_rows=d["count_rows"] if st["any_pen"] else None,
                    bias=self.bias if st["any_bias"] else None,
                    bias_rows=d["bias_rows"] if st["any_bias"] else None,
-                   mask=mask, mask_rows=mask_rows,
+                   mask=mask, mask_rows=mask_rows, mask_logprobs=self.constrained_logprobs,
                    out_token=outs[0], out_logprob=outs[1], out_topk_ids=outs[2], out_topk_lp=outs[3])
         out_host.copy_(out_dev, non_blocking=True)
         ev = torch.cuda.Event()
@@ -730,7 +733,7 @@ class LLMEngine:
             count_rows=i32([s.count_row for s in seqs]) if any_pen else None,
             bias=self.bias if any_bias else None,
             bias_rows=i32([s.group.bias_row for s in seqs]) if any_bias else None,
-            mask=mask, mask_rows=mask_rows,
+            mask=mask, mask_rows=mask_rows, mask_logprobs=self.constrained_logprobs,
         )
         for s in seqs:
             s.n_launched += 1
@@ -782,7 +785,7 @@ class LLMEngine:
                     self._finish(s, reason)
                 continue
             k = p.top_logprobs
-            top = list(zip(ids_h[i][:k], lps_h[i][:k])) if k else []
+            top = [(a, v) for a, v in zip(ids_h[i][:k], lps_h[i][:k]) if a >= 0] if k else []
             lp = float(lp_h[i])
             if self.faults.bad_logprobs:
                 lp, top = float("nan"), [(a, float("nan")) for a, _ in top]

@@ -15,7 +15,10 @@ variables configure the local engine:
   LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)
   LWC_ARCHIVE_PATH  append-only JSONL log of completions (checkpoint/resume of the archive)
   LWC_REGISTRY_PATH JSON file persisting registered score models
-  LWC_FAULT         fault injection for tests: worker_crash | slow_decode | bad_logprobs
+  LWC_FAULT         fault injection for tests: worker_crash | slow_decode | bad_logprobs | oom
+  LWC_CONSTRAINED_LOGPROBS  1: constrained (json_schema / tool-call) voters get logprobs over the allowed
+                    tokens, so a key letter's vote is the exact restricted softmax over its siblings
+                    instead of whatever of them made the raw top-k (default 0 = reference semantics)
 """
 from __future__ import annotations
 
@@ -61,6 +64,7 @@ class Config:
     gpu: int = 0
     gpus: List[int] = field(default_factory=list)
     device: str = "cuda"
+    constrained_logprobs: bool = False
     kv_fraction: float = 0.85
     archive_path: Optional[str] = None
     registry_path: Optional[str] = None
@@ -92,6 +96,7 @@ class Config:
             c.embed_models = json.loads(e["LWC_EMBED_MODELS"])
         c.gpu = int(e.get("LWC_GPU", e.get("LOCAL_RANK", "0")))
         c.device = e.get("LWC_DEVICE", "cuda").lower()
+        c.constrained_logprobs = e.get("LWC_CONSTRAINED_LOGPROBS", "0") == "1"
         if e.get("LWC_GPUS"):
             c.gpus = [int(x) for x in e["LWC_GPUS"].split(",") if x.strip()]
         c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))

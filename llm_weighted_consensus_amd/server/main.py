@@ -67,7 +67,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             model = LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
             tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
             eng = LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
-                            kv_memory_fraction=cfg.kv_fraction / max(1, len(cfg.models)))
+                            kv_memory_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
+                            constrained_logprobs=cfg.constrained_logprobs)
             services[name] = EngineService(eng, name)
     remote = None
     bases = cfg.api_bases()

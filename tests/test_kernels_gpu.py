@@ -462,3 +462,32 @@ def test_gemm256(gpu, M, N, K, res):
     out = ops.gemm(A, W, residual=R)
     ref_o = A.float() @ W.float().t() + (R.float() if res else 0)
     _close(out, ref_o, 3e-2, 1e-2)
+
+
+def test_sample_constrained_logprobs(gpu):
+    """mask_logprobs: a masked row's top-k logprobs are the restricted log-softmax over the allowed
+    tokens (sum of their probabilities = 1), in the raw order of the allowed logits; unmasked rows and
+    the default keep raw-distribution logprobs."""
+    from llm_weighted_consensus_amd import ops
+
+    V = 4096
+    torch.manual_seed(2)
+    logits = (torch.randn(2, V, device=gpu) * 3).to(torch.bfloat16)
+    allowed = [65, 66, 67, 70, 84]  # 'A' 'B' 'C' 'F' 'T'
+    mask = torch.zeros(1, V // 32, dtype=torch.int32, device=gpu)
+    for a in allowed:
+        mask[0, a // 32] |= 1 << (a % 32)
+    rows = torch.tensor([0, -1], dtype=torch.int32, device=gpu)
+    f = lambda v: torch.full((2,), float(v), device=gpu)
+    args = (logits, f(1.0), f(1.0), torch.zeros(2, dtype=torch.int32, device=gpu), f(0), f(0),
+            torch.arange(2, device=gpu, dtype=torch.int64), torch.zeros(2, device=gpu, dtype=torch.int64))
+    tok, lp, ids, lps = ops.sample(*args, num_logprobs=8, mask=mask, mask_rows=rows, mask_logprobs=True)
+    got = {int(i): float(v) for i, v in zip(ids[0].tolist(), lps[0].tolist()) if v > -1e30}
+    assert set(got) == set(allowed)
+    ref_lp = torch.log_softmax(logits[0, allowed].float(), 0)
+    for a, r in zip(allowed, ref_lp.tolist()):
+        assert abs(got[a] - r) < 2e-2
+    raw = torch.log_softmax(logits[1].float(), 0)
+    assert abs(lps[1, 0].item() - raw.max().item()) < 2e-2  # unmasked row: raw distribution
+    _, _, ids2, lps2 = ops.sample(*args, num_logprobs=8, mask=mask, mask_rows=rows)
+    assert abs(lps2[0, 0].item() - torch.log_softmax(logits[0].float(), 0).max().item()) < 2e-2
