@@ -24,6 +24,7 @@ import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -170,18 +171,22 @@ class BertEncoder:
         return out
 
     def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        """Varlen packing (ids folded into the vocab, truncated at max_tokens, empty -> [0]) with numpy:
+        thousands of candidates per consensus batch must not cost per-token Python work."""
         cap = min(max_tokens or self.cfg.max_position, self.cfg.max_position)
         V = self.cfg.vocab_size
-        ids, pos, cu = [], [], [0]
-        for tl in token_lists:
-            tl = [int(t) % V for t in list(tl)[:cap]] or [0]
-            ids.extend(tl)
-            pos.extend(range(len(tl)))
-            cu.append(cu[-1] + len(tl))
+        lens = np.fromiter((max(1, min(len(tl), cap)) for tl in token_lists), dtype=np.int64, count=len(token_lists))
+        cu = np.zeros(len(lens) + 1, dtype=np.int64)
+        np.cumsum(lens, out=cu[1:])
+        if len(lens) and (lens == lens[0]).all() and all(len(tl) >= lens[0] for tl in token_lists):
+            ids = np.asarray([tl[: lens[0]] for tl in token_lists], dtype=np.int64).reshape(-1)
+        else:
+            ids = np.concatenate([np.asarray(list(tl)[:cap] or [0], dtype=np.int64) for tl in token_lists])
+        ids %= V
+        pos = np.arange(int(cu[-1]), dtype=np.int64) - np.repeat(cu[:-1], lens)
         dev = self.device
-        max_len = max(cu[i + 1] - cu[i] for i in range(len(cu) - 1))
-        return (torch.tensor(ids, dtype=torch.int32, device=dev), torch.tensor(pos, dtype=torch.int32, device=dev),
-                torch.tensor(cu, dtype=torch.int32, device=dev), max_len)
+        return (torch.from_numpy(ids.astype(np.int32)).to(dev), torch.from_numpy(pos.astype(np.int32)).to(dev),
+                torch.from_numpy(cu.astype(np.int32)).to(dev), int(lens.max()))
 
     def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
         """Embed sequences (token ids in this encoder's vocab; ids are folded into range) ->
