@@ -136,6 +136,10 @@ def main():
     if a.profile_steps and rank == 0:
         print(f"# generate {gen_t / a.steps * 1e3:.1f} ms/step, score {score_t / a.steps * 1e3:.1f} ms/step, "
               f"decode steps {engine.stats['steps']}", file=sys.stderr)
+        from llm_weighted_consensus_amd.ops import gemm_plan
+        for k, v in gemm_plan.table().items():
+            print(f"# gemm {k}: " + " ".join(f"{b}={t:.1f}us" if isinstance(t, float) else f"{b}={t}"
+                                             for b, t in v.items()), file=sys.stderr)
     if rank == 0:
         out = {
             "metric": "consensus answers/sec (whole node) + embeddings/sec, N=64 Llama-3-8B@bge-large",

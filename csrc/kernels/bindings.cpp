@@ -11,7 +11,7 @@ int lwc_rmsnorm(const void*, void*, const void*, void*, int, int, float, hipStre
 int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
 int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
                       int, hipStream_t);
-int lwc_silu_mul(const void*, void*, int, int, hipStream_t);
+int lwc_silu_mul(const void*, void*, int, int, int, hipStream_t);
 int lwc_bias_gelu(void*, const void*, int, int, hipStream_t);
 int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
@@ -26,6 +26,8 @@ int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
                      int, int, int, int, int, int, long long, int, hipStream_t);
 int lwc_gemm256(const void*, const void*, void*, const void*, int, int, int, int, int, hipStream_t);
+int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
+int lwc_gemm8p_slots();
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -125,12 +127,13 @@ void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const c10::opti
            "rope_kv_write");
 }
 
-void silu_mul(const at::Tensor& in, at::Tensor& out) {
+void silu_mul(const at::Tensor& in, at::Tensor& out, int64_t block) {
   CHECK_BF16(in); CHECK_BF16(out); CHECK_CONTIG(in); CHECK_CONTIG(out);
   const int F = (int)out.size(-1);
   const int T = (int)(out.numel() / std::max(F, 1));
   TORCH_CHECK(in.size(-1) == 2 * F && in.numel() == 2 * out.numel(), "silu_mul: shape mismatch");
-  CHECK_RC(lwc_silu_mul(in.data_ptr(), out.data_ptr(), T, F, cur_stream()), "silu_mul");
+  TORCH_CHECK(block == 0 || (block % 8 == 0 && F % block == 0), "silu_mul: block must divide F, multiple of 8");
+  CHECK_RC(lwc_silu_mul(in.data_ptr(), out.data_ptr(), T, F, (int)block, cur_stream()), "silu_mul");
 }
 
 void bias_gelu(at::Tensor& x, const c10::optional<at::Tensor>& bias) {
@@ -313,6 +316,35 @@ void gemm256(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10:
            "gemm256");
 }
 
+void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
+            at::Tensor& ws, at::Tensor& flags) {
+  // epi 0: C[M, N] = A . W^T; 1: + R; 2: C[M, N/2] = silu(gate) * up over a 32-row gate/up interleaved W.
+  CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(C); CHECK_CONTIG(W);
+  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1, "gemm8p: 2-D row-major A/C");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi must be 0, 1 or 2");
+  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
+  const int NC = epi == 2 ? N / 2 : N;
+  TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == NC, "gemm8p: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && N % (epi == 2 ? 64 : 8) == 0 && A.stride(0) % 8 == 0 && C.stride(0) % 8 == 0,
+              "gemm8p: needs K % 64 == 0, N % 8 == 0 (SwiGLU: N % 64 == 0) and 16-byte aligned rows");
+  const void* r = nullptr;
+  if (epi == 1) {
+    TORCH_CHECK(R.has_value() && R->defined(), "gemm8p: epi 1 needs a residual");
+    CHECK_BF16(*R);
+    TORCH_CHECK(R->sizes() == C.sizes() && R->strides() == C.strides(), "gemm8p: residual must match C");
+    r = R->data_ptr();
+  }
+  // stream-K workspace: one fp32 256x256 partial tile and one flag per workgroup (flags zero between calls)
+  const int slots = lwc_gemm8p_slots();
+  CHECK_GPU(ws); CHECK_DTYPE(ws, at::kFloat); CHECK_CONTIG(ws);
+  CHECK_GPU(flags); CHECK_DTYPE(flags, at::kInt); CHECK_CONTIG(flags);
+  TORCH_CHECK(ws.numel() >= (int64_t)slots * 65536 && flags.numel() >= slots, "gemm8p: workspace too small (",
+              slots, " slots)");
+  CHECK_RC(lwc_gemm8p(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, ws.data_ptr<float>(), flags.data_ptr<int>(), M, N,
+                      K, (int)A.stride(0), (int)C.stride(0), (int)epi, cur_stream()),
+           "gemm8p");
+}
+
 void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Tensor& topk_w, at::Tensor& row_off,
                at::Tensor& src_row, at::Tensor& inv) {
   CHECK_BF16(logits); CHECK_CONTIG(logits);
@@ -466,6 +498,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("paged_decode", &paged_decode);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("gemm256", &gemm256);
+  m.def("gemm8p", &gemm8p);
+  m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);
   m.def("quant_fp8_rows", &quant_fp8_rows);

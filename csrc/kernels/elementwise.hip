@@ -72,16 +72,18 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
 // in: [T, 2F] = [gate | up]; out: [T, F]
-__global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int T, int F) {
+// gate of output column c at input column (c / blk) * 2 * blk + c % blk, up at + blk (blk = F: [gate | up]
+// halves; blk = 32: the gate/up interleaved weight layout of gemm8p's SwiGLU epilogue)
+__global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int T, int F, int blk) {
   const int fv = F >> 3;
   const size_t total = (size_t)T * fv;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const size_t t = i / fv;
     const int c = (int)(i % fv) * 8;
-    const bf16_t* r = in + t * 2 * F;
+    const bf16_t* r = in + t * 2 * F + (c / blk) * 2 * blk + c % blk;
     float g[8], u[8], o[8];
-    unpack8(*reinterpret_cast<const uint4v*>(r + c), g);
-    unpack8(*reinterpret_cast<const uint4v*>(r + F + c), u);
+    unpack8(*reinterpret_cast<const uint4v*>(r), g);
+    unpack8(*reinterpret_cast<const uint4v*>(r + blk), u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
     *reinterpret_cast<uint4v*>(out + t * F + c) = pack8(o);
@@ -151,11 +153,12 @@ extern "C" int lwc_rope_kv_write(void* qkv, const int* positions, const int* slo
   return (int)hipGetLastError();
 }
 
-extern "C" int lwc_silu_mul(const void* in, void* out, int T, int F, hipStream_t s) {
+extern "C" int lwc_silu_mul(const void* in, void* out, int T, int F, int blk, hipStream_t s) {
   using namespace lwc;
-  if (F % 8 != 0) return -1;
+  if (blk <= 0) blk = F;
+  if (F % 8 != 0 || blk % 8 != 0 || F % blk != 0) return -1;
   if (T == 0) return 0;
-  silu_mul_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((const bf16_t*)in, (bf16_t*)out, T, F);
+  silu_mul_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((const bf16_t*)in, (bf16_t*)out, T, F, blk);
   return (int)hipGetLastError();
 }
 

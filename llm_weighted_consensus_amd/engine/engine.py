@@ -501,6 +501,11 @@ class LLMEngine:
                 max_tiles = cascade_table_size(Bb, per)
             bk = _GraphBucket(Bb, self.width, splits, max_tiles, self.device)
             self.buckets[Bb] = bk
+            if hasattr(self.model, "tune_gemms"):
+                # per-shape GEMM backend (ops/gemm_plan.py), measured once per bucket, before any graph
+                # of it is captured (graph and eager decode then run the same kernels)
+                with span("tune_gemms"):
+                    self.model.tune_gemms(Bb)
         return bk
 
     def _cascade_plan(self, seqs: List[Sequence], tiles: np.ndarray) -> None:

@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import gemm_plan
 from .config import DecoderConfig
 
 
@@ -59,8 +60,9 @@ class LayerWeights:
     wqkv: torch.Tensor      # [(Hq+2Hkv)*D, d]
     wo: torch.Tensor        # [d, Hq*D]
     mlp_norm: torch.Tensor
-    w_gate_up: torch.Tensor  # [2F, d]  rows: gate then up
+    w_gate_up: torch.Tensor  # [2F, d]  rows: gate then up (gu_block 0) or interleaved in blocks of gu_block
     w_down: torch.Tensor    # [d, F]
+    gu_block: int = 0
 
 
 class KVCache:
@@ -106,6 +108,15 @@ class LlamaModel:
         else:
             self._random_init(seed)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.g8_ws = None
+        if self.device.type == "cuda":
+            # gemm8p (ops/gemm_plan.py): the gate|up rows interleaved in blocks of 32 so its epilogue can
+            # apply SwiGLU; a stream-K workspace owned by the model (never allocated inside a capture)
+            for L in self.layers:
+                if isinstance(L, LayerWeights) and L.gu_block == 0 and L.w_gate_up.shape[0] % 64 == 0:
+                    L.w_gate_up = ops.swiglu_interleave(L.w_gate_up)
+                    L.gu_block = 32
+            self.g8_ws = ops.new_gemm8p_workspace(self.device)
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int) -> None:
@@ -172,7 +183,7 @@ class LlamaModel:
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
         h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
         for li, L in enumerate(self.layers):
-            qkv = F.linear(h, L.wqkv)
+            qkv = self._proj(h, L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
             attn = attn_fn(qkv, li)
             o = self._attn_out(attn.view(T, Hq * D), L)
@@ -182,13 +193,39 @@ class LlamaModel:
             h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
         return h
 
+    def _proj(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        """Dense projection on the per-shape backend (hipBLASLt or gemm8p, ops/gemm_plan.py)."""
+        if self.g8_ws is None:
+            return F.linear(x, w)
+        return gemm_plan.linear(x, w, ws=self.g8_ws)
+
     def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
         """Output projection (row-parallel + all-reduce in tensor-parallel subclasses)."""
-        return F.linear(attn, L.wo)
+        return self._proj(attn, L.wo)
 
     def _mlp(self, h: torch.Tensor, L) -> torch.Tensor:
-        """Dense SwiGLU MLP: fused gate|up GEMM, K5 silu_mul, down GEMM."""
-        return F.linear(ops.silu_mul(F.linear(h, L.w_gate_up)), L.w_down)
+        """Dense SwiGLU MLP: gate|up GEMM with SwiGLU (fused in gemm8p's epilogue, or hipBLASLt + K5
+        silu_mul), down GEMM."""
+        if self.g8_ws is None:
+            act = ops.silu_mul(F.linear(h, L.w_gate_up), block=L.gu_block)
+        else:
+            act = gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
+        return self._proj(act, L.w_down)
+
+    def tune_gemms(self, M: int) -> None:
+        """Pick the GEMM backend of every decode projection at batch M by timing both (before the
+        bucket's hipGraph is captured; see ops/gemm_plan.py)."""
+        if self.g8_ws is None or not isinstance(self.layers[0], LayerWeights):
+            return
+        cfg, L = self.cfg, self.layers[0]
+        x = torch.randn(M, cfg.hidden, device=self.device).to(self.dtype)
+        xa = torch.randn(M, cfg.heads * cfg.head_dim, device=self.device).to(self.dtype)
+        xf = torch.randn(M, cfg.ffn, device=self.device).to(self.dtype)
+        gemm_plan.tune(x, L.wqkv, ws=self.g8_ws)
+        gemm_plan.tune(xa, L.wo, ws=self.g8_ws)
+        gemm_plan.tune(x, L.w_gate_up, "swiglu", L.gu_block, ws=self.g8_ws)
+        gemm_plan.tune(xf, L.w_down, ws=self.g8_ws)
+        gemm_plan.tune(x, self.lm_head, ws=self.g8_ws)
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None,
@@ -217,7 +254,7 @@ class LlamaModel:
                                                 cfg.heads, self.scale)
 
             h = self._layers(x, cache, positions, slots, attn_fn)
-            return F.linear(h, self.lm_head)
+            return self._proj(h, self.lm_head)
 
         def attn_fn(qkv, li):
             if tiles is not None:
@@ -228,7 +265,7 @@ class LlamaModel:
                                     pre_o=pre_o, pre_lse=pre_lse)
 
         h = self._layers(x, cache, positions, slots, attn_fn)
-        return F.linear(h, self.lm_head)
+        return self._proj(h, self.lm_head)
 
     def encode(self, tokens: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor,
                max_seqlen: int) -> torch.Tensor:

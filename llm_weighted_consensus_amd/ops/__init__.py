@@ -66,12 +66,13 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
     return out
 
 
-def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """SwiGLU over a fused [T, 2F] = [gate | up] buffer (K5)."""
+def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None, block: int = 0) -> torch.Tensor:
+    """SwiGLU over a fused [T, 2F] = [gate | up] buffer (K5); ``block`` > 0: columns interleaved
+    gate/up in blocks of ``block`` (the :func:`swiglu_interleave` weight layout)."""
     F = gate_up.shape[-1] // 2
     if out is None:
         out = torch.empty(*gate_up.shape[:-1], F, dtype=gate_up.dtype, device=gate_up.device)
-    kernels().silu_mul(gate_up, out)
+    kernels().silu_mul(gate_up, out, int(block))
     return out
 
 
@@ -215,6 +216,56 @@ def gemm(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = No
         out = torch.empty(A.shape[0], W.shape[0], dtype=torch.bfloat16, device=A.device)
     kernels().gemm256(A, W, out, residual)
     return out
+
+
+def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, swiglu: bool = False, ws=None) -> torch.Tensor:
+    """8-phase 256x256-tile MFMA GEMM (K6, csrc/kernels/gemm8p.hip): A [M, K] . W[N, K]^T (+ residual)
+    -> [M, N] bf16.  ``swiglu=True`` takes a gate/up weight laid out by :func:`swiglu_interleave` and
+    returns silu(A Wg^T) * (A Wu^T) [M, N/2] from the GEMM epilogue (no [M, N] intermediate).
+    ``ws`` = (partials, flags) stream-K workspace (:func:`gemm8p_workspace`); a model passes its own so
+    a captured graph owns no allocation; default: one per (device, stream), created outside capture."""
+    N = W.shape[0] // 2 if swiglu else W.shape[0]
+    if out is None:
+        out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
+    epi = 2 if swiglu else (1 if residual is not None else 0)
+    part, flags = ws if ws is not None else gemm8p_workspace(A.device)
+    kernels().gemm8p(A, W, out, residual, epi, part, flags)
+    return out
+
+
+_G8_WS: dict = {}
+
+
+def new_gemm8p_workspace(device: torch.device):
+    """(fp32 partials [slots * 65536], int32 flags [slots]) for gemm8p's stream-K tail.  GEMMs that may
+    run concurrently (different streams) need different workspaces; the kernel leaves the flags zero."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("gemm8p workspace must be allocated outside hipGraph capture")
+    slots = kernels().gemm8p_slots()
+    return (torch.empty(slots * 65536, dtype=torch.float32, device=device),
+            torch.zeros(slots, dtype=torch.int32, device=device))
+
+
+def gemm8p_workspace(device: torch.device):
+    """Default gemm8p workspace of the current (device, stream)."""
+    device = torch.device(device)
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _G8_WS.get(key)
+    if ws is None:
+        ws = _G8_WS[key] = new_gemm8p_workspace(device)
+    return ws
+
+
+def swiglu_interleave(w_gate_up: torch.Tensor, block: int = 32) -> torch.Tensor:
+    """[gate (F rows); up (F rows)] -> rows interleaved in blocks of ``block``: gate[0:32], up[0:32],
+    gate[32:64], ... — the layout gemm8p's SwiGLU epilogue expects (each 64-row group of a tile holds a
+    gate block and the matching up block)."""
+    F2, K = w_gate_up.shape
+    F = F2 // 2
+    assert F % block == 0, "ffn size must be a multiple of the interleave block"
+    g, u = w_gate_up[:F].view(F // block, block, K), w_gate_up[F:].view(F // block, block, K)
+    return torch.stack([g, u], dim=1).reshape(F2, K).contiguous()
 
 
 def moe_route(logits: torch.Tensor, k: int):

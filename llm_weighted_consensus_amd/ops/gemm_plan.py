@@ -1,0 +1,99 @@
+"""Per-shape GEMM backend choice for the decoder projections (K6).
+
+Two backends compute ``A . W^T`` for the dense projections:
+
+* ``blas`` — hipBLASLt through ``torch.nn.functional.linear`` (its own stream-K kernels);
+* ``g8``   — the hand-written 8-phase MFMA GEMM with a stream-K tail (``csrc/kernels/gemm8p.hip``),
+  which also fuses the SwiGLU of the gate|up projection into its epilogue.
+
+Neither wins everywhere (``profiles/gemm8p.md``: g8 is ahead on the fused gate_up+SwiGLU and the qkv
+projection at decode batch 3072, hipBLASLt on most shapes at batch 1024), so the choice is made per
+(M, N, K, epilogue) by timing both on the device, once, before a decode bucket's hipGraph is captured
+(:meth:`LlamaModel.tune_gemms`).  Untuned shapes (prefill, encode) use hipBLASLt.
+``LWC_GEMM=blas|g8`` forces one backend (``auto`` = measured, the default).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import gemm8p, silu_mul
+
+MODE = os.environ.get("LWC_GEMM", "auto")
+_CHOICE: Dict[Tuple[int, int, int, str], str] = {}
+TIMINGS: Dict[Tuple[int, int, int, str], Dict[str, float]] = {}
+
+
+def choice(M: int, N: int, K: int, epi: str) -> str:
+    if MODE in ("blas", "g8"):
+        return MODE
+    return _CHOICE.get((M, N, K, epi), "blas")
+
+
+def _g8_ok(N: int, K: int, epi: str) -> bool:
+    return K % 64 == 0 and N % (64 if epi == "swiglu" else 8) == 0
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, ws=None) -> torch.Tensor:
+    """x [M, K] . w[N, K]^T -> [M, N] bf16 on the chosen backend."""
+    M, K = x.shape
+    N = w.shape[0]
+    if choice(M, N, K, "plain") == "g8" and _g8_ok(N, K, "plain") and x.stride(1) == 1:
+        return gemm8p(x, w, ws=ws)
+    return F.linear(x, w)
+
+
+def swiglu(x: torch.Tensor, w_gu: torch.Tensor, block: int, ws=None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) [M, F] for a fused gate|up weight [2F, K] whose rows are [gate; up]
+    (block 0) or interleaved in blocks of ``block`` (ops.swiglu_interleave; required by g8)."""
+    M, K = x.shape
+    N = w_gu.shape[0]
+    if block == 32 and choice(M, N, K, "swiglu") == "g8" and _g8_ok(N, K, "swiglu") and x.stride(1) == 1:
+        return gemm8p(x, w_gu, swiglu=True, ws=ws)
+    return silu_mul(F.linear(x, w_gu), block=block)
+
+
+def _time(fn, iters: int = 5, rounds: int = 3) -> float:
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) / iters * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, ws=None) -> Optional[str]:
+    """Time both backends for this (M, N, K, epi) and record the faster (no-op under graph capture, off
+    the GPU, for an already tuned shape, or when a backend is forced)."""
+    M, K = x.shape
+    N = w.shape[0]
+    key = (M, N, K, epi)
+    if MODE != "auto" or key in _CHOICE or not x.is_cuda or torch.cuda.is_current_stream_capturing():
+        return _CHOICE.get(key)
+    if not _g8_ok(N, K, epi) or (epi == "swiglu" and block != 32):
+        _CHOICE[key] = "blas"
+        return "blas"
+    if epi == "swiglu":
+        t_blas = _time(lambda: silu_mul(F.linear(x, w), block=block))
+        t_g8 = _time(lambda: gemm8p(x, w, swiglu=True, ws=ws))
+    else:
+        t_blas = _time(lambda: F.linear(x, w))
+        t_g8 = _time(lambda: gemm8p(x, w, ws=ws))
+    TIMINGS[key] = {"blas": t_blas, "g8": t_g8}
+    _CHOICE[key] = "g8" if t_g8 < t_blas else "blas"
+    return _CHOICE[key]
+
+
+def table() -> Dict[str, Dict[str, float]]:
+    """Measured shapes -> {backend: us, 'choice': ...} (for logs and /metrics)."""
+    return {f"{M}x{N}x{K}:{e}": dict(TIMINGS.get((M, N, K, e), {}), choice=c)
+            for (M, N, K, e), c in _CHOICE.items()}

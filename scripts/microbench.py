@@ -129,6 +129,53 @@ def grouped(dev):
         print(f"ggemm moe gate_up T={T}: {t:7.1f} us ({fl / t * 1e6:6.0f} TF/s)", flush=True)
 
 
+def gemm8p_study(dev, Ms):
+    """8-phase 256x256 GEMM (csrc/kernels/gemm8p.hip) vs hipBLASLt vs the 2-phase gemm256, interleaved
+    rounds in one process (median of 3), random operands; plus the fused SwiGLU epilogue against
+    hipBLASLt gate_up + silu_mul."""
+    from llm_weighted_consensus_amd import ops
+
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    cases = [(M, name, N, K) for M in Ms for name, (N, K) in shapes.items()]
+    cases += [(4096, "sq4096", 4096, 4096), (8192, "sq8192", 8192, 8192)]
+    for M, name, N, K in cases:
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        fns = {"hipblaslt": lambda: torch.matmul(x, w.t(), out=o), "gemm8p": lambda: ops.gemm8p(x, w, out=o),
+               "gemm256": lambda: ops.gemm(x, w, out=o)}
+        ref = F.linear(x, w).float()
+        err = (ops.gemm8p(x, w).float() - ref).abs().max().item()
+        res = {k: [] for k in fns}
+        for _ in range(3):
+            for k, fn in fns.items():
+                res[k].append(timeit(fn, iters=10 if M * N * K > 1e11 else 30))
+        fl = 2 * M * N * K / 1e12
+        line = "  ".join(f"{k} {sorted(v)[1]:8.1f} us ({fl / sorted(v)[1] * 1e6:5.0f})" for k, v in res.items())
+        print(f"g8 M={M:5d} {name:8s}: {line}  err {err:.3g}", flush=True)
+    for M in Ms:
+        N, K = 28672, 4096
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        wi = ops.swiglu_interleave(w)
+        gu = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+
+        def unfused():
+            torch.matmul(x, w.t(), out=gu)
+            ops.silu_mul(gu, out=h)
+
+        ref = F.silu(F.linear(x, w).float()[:, :N // 2]) * F.linear(x, w).float()[:, N // 2:]
+        err = (ops.gemm8p(x, wi, swiglu=True).float() - ref).abs().max().item()
+        ta, tb = [], []
+        for _ in range(3):
+            ta.append(timeit(unfused, iters=10))
+            tb.append(timeit(lambda: ops.gemm8p(x, wi, out=h, swiglu=True), iters=10))
+        print(f"g8 swiglu M={M:5d}: hipblaslt+silu_mul {sorted(ta)[1]:8.1f} us  gemm8p-fused {sorted(tb)[1]:8.1f} us"
+              f"  err {err:.3g}", flush=True)
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -273,6 +320,8 @@ def main():
         gemm_backends(dev, [1024, 1536])
     if "grouped" in a.what:
         grouped(dev)
+    if "g8" in a.what:
+        gemm8p_study(dev, [int(m) for m in os.environ.get("MICRO_M", "3072,1024").split(",")])
     if "layout" in a.what:
         gemm_layouts(dev, [int(m) for m in os.environ.get("MICRO_M", "512,1024").split(",")])
     if "attn" in a.what:

@@ -464,6 +464,37 @@ def test_gemm256(gpu, M, N, K, res):
     _close(out, ref_o, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [
+    (512, 768, 256, "plain"), (300, 1024, 512, "res"), (4096, 4096, 4096, "plain"),  # data-parallel only
+    (200, 8, 64, "plain"),                      # one partial tile, one K tile
+    (3072, 6144, 4096, "plain"),                # 288 tiles: all stream-K, 1-2 workgroups per tile
+    (1000, 4096, 14336, "res"),                 # 64 tiles: 4 workgroups per tile, 3 partials each
+    (777, 2048, 1024, "swiglu"),                # shrunken grid, half-tile ranges
+    (5000, 1280, 128, "plain"),                 # 2-iteration ranges, stream-K + 3 data-parallel rounds
+    (3072, 28672, 4096, "swiglu")])             # gate_up: 320 stream-K tiles + 4 data-parallel rounds
+def test_gemm8p(gpu, M, N, K, epi):
+    """8-phase 256x256 MFMA GEMM with the stream-K tail (plain / residual / SwiGLU epilogue) vs an fp32
+    matmul: ragged M and N tails, single-K-tile problems, tiles split over 1-4 workgroups.  Each case runs
+    twice (the second launch depends on the first leaving the partial flags zero)."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    for _ in range(2):
+        if epi == "swiglu":
+            F = N // 2
+            out = ops.gemm8p(A, ops.swiglu_interleave(W), swiglu=True)
+            _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
+            continue
+        R = torch.randn(M, N, device=gpu).to(torch.bfloat16) if epi == "res" else None
+        out = ops.gemm8p(A, W, residual=R)
+        _close(out, ref + (R.float() if R is not None else 0), 3e-2, 1e-2)
+    torch.cuda.synchronize()
+    assert int(ops.gemm8p_workspace(A.device)[1].abs().sum()) == 0, "stream-K flags left set"
+
+
 def test_sample_constrained_logprobs(gpu):
     """mask_logprobs: a masked row's top-k logprobs are the restricted log-softmax over the allowed
     tokens (sum of their probabilities = 1), in the raw order of the allowed logits; unmasked rows and

@@ -62,7 +62,11 @@ def llama_forward(model, tokens, hidden_only=False):
             x = x + moe_mlp(model, L, h)
         else:
             gu = h @ L.w_gate_up.float().t()
-            g, u = gu.chunk(2, dim=-1)
+            if getattr(L, "gu_block", 0):  # gate/up rows interleaved in blocks (ops.swiglu_interleave)
+                gu = gu.view(gu.shape[0], -1, 2, L.gu_block)
+                g, u = gu[:, :, 0].reshape(gu.shape[0], -1), gu[:, :, 1].reshape(gu.shape[0], -1)
+            else:
+                g, u = gu.chunk(2, dim=-1)
             x = x + (F.silu(g) * u) @ L.w_down.float().t()
     h = rmsnorm(x, model.final_norm, cfg.rms_eps)
     if hidden_only:
