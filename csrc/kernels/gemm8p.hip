@@ -47,6 +47,7 @@
 //   the next launch (flags start zeroed), barrier, plain loads.
 //   epilogue  : accumulators -> bf16 (SwiGLU / residual applied in registers) -> LDS -> 16 B row stores.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -71,7 +72,8 @@ struct Params {
   float* ws;    // [8 * wpx, kPartialF] partial tiles
   int* flags;   // [8 * wpx] partial-ready flags (zero between launches)
   int M, N, K, lda, ldc;  // N = rows of W
-  int tiles_m, KT;
+  int tiles_m, tiles_n, KT;
+  int gm;  // tile order: groups of gm m-tiles, n fastest across a group (32 consecutive tiles ~ 4 x 8)
   int wpx, sk_tiles, dp_rounds;
 };
 
@@ -88,6 +90,18 @@ LWC_DEVICE void sk_range(const Params& p, int x, int j, int& a, int& e) {
   const int ix = (t1 - t0) * p.KT;
   a = t0 * p.KT + (int)((long long)ix * j / p.wpx);
   e = t0 * p.KT + (int)((long long)ix * (j + 1) / p.wpx);
+}
+
+// Tile t -> (m, n): grouped order, gm m-tiles per group, m fastest inside the group, so the wpx
+// consecutive tiles an XCD runs in one round form a ~gm x (wpx / gm) block whose A and W panels its
+// L2 shares (a plain m-fastest order spans every m-tile of the matrix: 1.5x the L2 misses at 4096^3).
+LWC_DEVICE void tile_mn(const Params& p, int t, int& m, int& n) {
+  const int group = p.gm * p.tiles_n;
+  const int first_m = (t / group) * p.gm;
+  const int gsz = min(p.tiles_m - first_m, p.gm);
+  const int in = t % group;
+  m = first_m + in % gsz;
+  n = in / gsz;
 }
 
 template <int EPI>
@@ -117,7 +131,9 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
     } else {
       break;
     }
-    const int m0 = (tile % p.tiles_m) * 256, n0 = (tile / p.tiles_m) * 256;
+    int tm, tn;
+    tile_mn(p, tile, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
     // Lane geometry is re-derived per item from an opaque copy of threadIdx.x: hoisted out of the
     // item loop, the ~100 epilogue / fragment addresses it feeds would stay live and spill.
     int tid = threadIdx.x;
@@ -162,6 +178,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
       f1 = *reinterpret_cast<const uint4v*>(u + row0 * 128 + off1);
     };
 
+    // acc[i][jj] = 16 x 16 tile (i, jj) of the wave's 128 x 64 (lane: rows 4q..4q+3 of column r16).
+    // (The 32x32x16 MFMA with the same units and phases measured ~10 % slower on every shape.)
     float4v acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -195,54 +213,44 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
   __builtin_amdgcn_s_setprio(0);                     \
   G8_BAR()
 
-    // prologue: K tile klo -> buffer 0; A0 and B0 landed, A1 and B1 may still be in flight
-    stage(0, smem, klo);
-    stage(2, smem, klo);
-    stage(3, smem, klo);
-    stage(1, smem, klo);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    const int nt = khi - klo;  // K tiles of this item; tile r lives in LDS buffer r & 1
+#define G8_STAGE(U, R) stage(U, smem + ((R) & 1) * kBufB, klo + (R))
+#define G8_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+#define G8_TILE(R, ST1, ST2, ST3, ST4, W1, W2, W4) \
+  {                                                \
+    uint8_t* cb = smem + ((R) & 1) * kBufB;        \
+    rdB(cb, kUB0, b0);                             \
+    __builtin_amdgcn_sched_barrier(0);             \
+    rdA(cb, kUA0);                                 \
+    ST1;                                           \
+    W1;                                            \
+    G8_MFMA(0, 0, b0);                             \
+    rdB(cb, kUB1, b1);                             \
+    ST2;                                           \
+    W2;                                            \
+    G8_MFMA(0, 2, b1);                             \
+    rdA(cb, kUA1);                                 \
+    ST3;                                           \
+    G8_MFMA(4, 2, b1);                             \
+    ST4;                                           \
+    W4;                                            \
+    G8_MFMA(4, 0, b0);                             \
+  }
+    // unit issue runs 4 units ahead of consumption: tile r stages tile r+1 (A0 B0 B1 A1 in P1..P4), 2 units
+    // in flight at each wait.  (A 6-unit lead — B1, A1 of r+1 and A0, B0 of r+2, vmcnt(8) — measured the
+    // same at 4096^3 and on the decode shapes: the DMA latency is covered, the cost is in the barriers.)
+    G8_STAGE(0, 0); G8_STAGE(2, 0); G8_STAGE(3, 0); G8_STAGE(1, 0);
+    G8_VM(4);
     G8_BAR();
     if (wr == 1) G8_BAR();  // stagger the two wave rows by one barrier
-
-    for (int kt = klo; kt < khi - 1; ++kt) {
-      const int cur = (kt - klo) & 1;
-      uint8_t* cb = smem + cur * kBufB;
-      uint8_t* nb = smem + (cur ^ 1) * kBufB;
-      // P1
-      rdB(cb, kUB0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      rdA(cb, kUA0);
-      stage(0, nb, kt + 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      G8_MFMA(0, 0, b0);
-      // P2
-      rdB(cb, kUB1, b1);
-      stage(2, nb, kt + 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      G8_MFMA(0, 2, b1);
-      // P3
-      rdA(cb, kUA1);
-      stage(3, nb, kt + 1);
-      G8_MFMA(4, 2, b1);
-      // P4
-      stage(1, nb, kt + 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      G8_MFMA(4, 0, b0);
-    }
-    {  // last K tile of the item: nothing to stage, drain
-      uint8_t* cb = smem + ((khi - 1 - klo) & 1) * kBufB;
-      rdB(cb, kUB0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      rdA(cb, kUA0);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      G8_MFMA(0, 0, b0);
-      rdB(cb, kUB1, b1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      G8_MFMA(0, 2, b1);
-      rdA(cb, kUA1);
-      G8_MFMA(4, 2, b1);
-      G8_MFMA(4, 0, b0);
-    }
+    int r = 0;
+    for (; r < nt - 1; ++r)
+      G8_TILE(r, G8_STAGE(0, r + 1), G8_STAGE(2, r + 1), G8_STAGE(3, r + 1), G8_STAGE(1, r + 1), G8_VM(4), G8_VM(4),
+              G8_VM(4))
+    G8_TILE(r, , , , , G8_VM(2), G8_VM(0), )
+#undef G8_TILE
+#undef G8_VM
+#undef G8_STAGE
     if (wr == 0) G8_BAR();  // re-align the wave rows
 #undef G8_MFMA
 #undef G8_BAR
@@ -352,6 +360,13 @@ int launch(const Params& p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Experiment knob (A/B in one process, scripts/microbench.py g8ab): LWC_G8_GM, the tile group height
+// (default 8; 1 = plain m-fastest order).
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 int device_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -391,7 +406,7 @@ extern "C" int lwc_gemm8p(const void* A, const void* W, void* C, const void* R, 
     sk = tiles - dp * G;
   }
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, ws, flags,
-           M, N, K, lda, ldc, tiles_m, KT, wpx, sk, dp};
+           M, N, K, lda, ldc, tiles_m, tiles_n, KT, std::max(1, env_int("LWC_G8_GM", 8)), wpx, sk, dp};
   switch (epi) {
     case EPI_PLAIN: return launch<EPI_PLAIN>(p, s);
     case EPI_RESIDUAL: return launch<EPI_RESIDUAL>(p, s);

@@ -176,6 +176,34 @@ def gemm8p_study(dev, Ms):
               f"  err {err:.3g}", flush=True)
 
 
+def gemm8p_ab(dev):
+    """A/B of gemm8p knobs (env LWC_G8_*, read at launch) in interleaved rounds, median of 5."""
+    from llm_weighted_consensus_amd import ops
+
+    variants = [v.split(":") for v in os.environ.get("G8_VARIANTS", "GM=1:STAGGER=1,GM=4:STAGGER=1,GM=8:STAGGER=1,"
+                                                     "GM=4:STAGGER=0").split(",")]
+    shapes = [(4096, 4096, 4096, False), (3072, 28672, 4096, True), (3072, 6144, 4096, False),
+              (3072, 4096, 14336, False), (3072, 4096, 4096, False), (3072, 128256, 4096, False),
+              (8192, 8192, 8192, False)]
+    for M, N, K, sw in shapes:
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        if sw:
+            w = ops.swiglu_interleave(w)
+        res = {",".join(v): [] for v in variants}
+        for _ in range(5):
+            for v in variants:
+                for kv in v:
+                    k, val = kv.split("=")
+                    os.environ["LWC_G8_" + k] = val
+                res[",".join(v)].append(timeit(lambda: ops.gemm8p(x, w, swiglu=sw), iters=10))
+        fl = 2 * M * N * K / 1e12
+        line = "  ".join(f"[{k}] {sorted(t)[2]:7.1f} us ({fl / sorted(t)[2] * 1e6:5.0f})" for k, t in res.items())
+        print(f"g8ab {M}x{N}x{K}{' swiglu' if sw else ''}: {line}", flush=True)
+    for k in ("LWC_G8_GM", "LWC_G8_STAGGER"):
+        os.environ.pop(k, None)
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -320,6 +348,8 @@ def main():
         gemm_backends(dev, [1024, 1536])
     if "grouped" in a.what:
         grouped(dev)
+    if "g8ab" in a.what:
+        gemm8p_ab(dev)
     if "g8" in a.what:
         gemm8p_study(dev, [int(m) for m in os.environ.get("MICRO_M", "3072,1024").split(",")])
     if "layout" in a.what:
