@@ -25,6 +25,8 @@
 // are read ONCE per tile instead of once per sequence: for N candidates of one prompt this removes
 // (N-1)/N of the prompt's KV traffic and finally uses the MFMA rows.  The suffix pass (each
 // sequence's own blocks) merges the prefix partial (o, lse) in its epilogue.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace lwc {
@@ -226,9 +228,13 @@ LWC_DEVICE void load_q(short8 (&qf)[4], const DecodeParams& p, int row_seq0, int
 // PREFIX=true : blockIdx.x = tile;  PREFIX=false: blockIdx.x = sequence.  4 waves split the item's
 // block pairs and combine through LDS: the long-context / small-batch path.
 template <bool PREFIX>
-__global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
+__global__ void __launch_bounds__(256)
+    paged_decode_kernel(DecodeParams p, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens) {
   const int item = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: the compiler then knows everything derived from it (sequence, block
+  // indices) is wave-uniform and loads block tables / ctx lens with SCALAR loads — as vector loads each
+  // one needed an s_waitcnt vmcnt(0) that drained the K/V loads in flight (the pipeline collapsed)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, g = lane >> 4;
 
   int row_seq0, nrows, blk_begin, blk_end, ctx;
@@ -243,7 +249,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   } else {
     row_seq0 = item;
     nrows = p.G;
-    ctx = p.ctx_lens[item];
+    ctx = ctx_lens[item];
     const int nblk_total = (ctx + kBS - 1) / kBS;
     const int b0 = p.start_blk ? p.start_blk[item] : 0;
     const int per_split = (nblk_total - b0 + p.num_splits - 1) / p.num_splits;
@@ -253,7 +259,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
   // row -> (sequence, query head)
   auto row_seq = [&](int row) { return PREFIX ? row_seq0 + row / p.G : row_seq0; };
   auto row_head = [&](int row) { return kvh * p.G + (PREFIX ? row % p.G : row); };
-  const int* bt = p.block_tables + (size_t)row_seq0 * p.max_blocks;  // prefix blocks are shared by the tile
+  const int* bt = block_tables + (size_t)row_seq0 * p.max_blocks;  // prefix blocks are shared by the tile
 
   short8 qf[4];
   load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
@@ -335,8 +341,13 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(DecodeParams p) {
 // pair i+1 are in flight while pair i is on the MFMAs), and the epilogue merges the prefix partial
 // and writes straight from the accumulator layout.
 template <bool PREFIX>
-__global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, int num_items) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+__global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, int num_items,
+                                                                const int* __restrict__ block_tables,
+                                                                const int* __restrict__ ctx_lens) {
+  // wid through readfirstlane: the compiler then knows everything derived from it (sequence, block
+  // indices) is wave-uniform and loads block tables / ctx lens with SCALAR loads — as vector loads each
+  // one needed an s_waitcnt vmcnt(0) that drained the K/V loads in flight (the pipeline collapsed)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int item = blockIdx.x * kWaves + wid, kvh = blockIdx.y;
   if (item >= num_items) return;  // the whole wave leaves; nothing below synchronises
   const int r16 = lane & 15, g = lane >> 4;
@@ -354,14 +365,14 @@ __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, 
     row_seq0 = item / p.num_splits;
     split = item - row_seq0 * p.num_splits;
     nrows = p.G;
-    ctx = p.ctx_lens[row_seq0];
+    ctx = ctx_lens[row_seq0];
     const int nblk_total = (ctx + kBS - 1) / kBS;
     const int b0 = p.start_blk ? p.start_blk[row_seq0] : 0;
     const int per_split = (nblk_total - b0 + p.num_splits - 1) / p.num_splits;
     blk_begin = b0 + split * per_split;
     blk_end = min(nblk_total, blk_begin + per_split);
   }
-  const int* bt = p.block_tables + (size_t)row_seq0 * p.max_blocks;
+  const int* bt = block_tables + (size_t)row_seq0 * p.max_blocks;
 
   short8 qf[4];
   load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
@@ -457,7 +468,7 @@ static int g_wave_min_items = 2048;
 //  epilogue: bf16 output straight from the accumulator layout.
 // Super-tiles with prefix_blocks = 0 are plain decode for up to kCWaves*per unrelated sequences.
 constexpr int kCWaves = 8;
-constexpr int kCPairs = 8;                         // pairs staged per LDS chunk (128 KiB)
+constexpr int kCPairsMax = 8;                      // pairs staged per LDS chunk (<= 128 KiB)
 constexpr int kCRounds = 1024 / (kCWaves * 64);     // 16 B loads per thread per pair
 constexpr int kPairBytes = 4 * kBS * kD * 2;        // K_A, K_B, V_A^T, V_B^T = 16 KiB
 constexpr int kSegBytes = kBS * kD * 2;             // 4 KiB
@@ -474,15 +485,22 @@ struct CascadeParams {
   float scale;
 };
 
-__global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(CascadeParams p) {
+// The index tables come in as const __restrict__ kernel arguments (not through the params struct): with
+// uniform addresses the compiler may then use SCALAR loads for them (no possible clobber by the output
+// stores).  As vector loads every block-table / ctx-len read needed an s_waitcnt vmcnt(0), which drained
+// the K/V loads in flight and serialised both phases.
+template <int kCPairs>
+__global__ void __launch_bounds__(kCWaves * 64)
+    paged_decode_cascade_kernel(CascadeParams p, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens,
+                                const int* __restrict__ tiles) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // heads are the fast grid dimension: the real tiles (a prefix of the table) are dispatched first,
   // the graph-capture slack (nseq = 0 entries) last
   const int tile = blockIdx.y, kvh = blockIdx.x;
-  const int* t = p.tiles + 3 * tile;
+  const int* t = tiles + 3 * tile;
   const int row_start = t[0], nseq = t[1], pblk = t[2];
   if (nseq <= 0) return;  // uniform for the whole workgroup, before any barrier
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // see above
   const int r16 = lane & 15, g = lane >> 4;
   const int per = 16 / p.G;
   const int s0 = row_start + wid * per;
@@ -505,7 +523,7 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
 
   // ---- phase 1: shared prefix through LDS ----
   auto phase1 = [&]() {
-  const int* bt0 = p.block_tables + (size_t)row_start * p.max_blocks;
+  const int* bt0 = block_tables + (size_t)row_start * p.max_blocks;
   const int pctx = pblk * kBS;
   for (int c0 = 0; c0 < pblk; c0 += 2 * kCPairs) {
     const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
@@ -516,8 +534,9 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
     for (int pi = 0; pi < kCPairs; ++pi) {
 #pragma unroll
       for (int rd = 0; rd < kCRounds; ++rd) {
-        const int u = rd * (kCWaves * 64) + tid;  // 16 B unit of the pair's 16 KiB image
-        const int seg = u >> 8, pos = u & 255;
+        // 16 B unit u = rd*512 + tid of the pair's 16 KiB image: segment (K_A, K_B, V_A, V_B) u >> 8 is
+        // wave-uniform (rd*2 + wid/4), the position inside it is (wid%4)*64 + lane
+        const int seg = rd * 2 + (wid >> 2), pos = ((wid & 3) << 6) + lane;
         const int blk = c0 + 2 * pi + (seg & 1);
         if (pi < npairs && blk < pblk) {  // wave-uniform: a wave's 64 units lie in one segment
           const int phys = bt0[blk];
@@ -579,7 +598,7 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
     auto seq_pos = [&](int j) {  // first suffix pair of sequence j (or beyond), skipping empty suffixes
       Pos q{j, pblk, 0, 0};
       while (q.j < nseq_w) {
-        q.ctx = p.ctx_lens[s0 + q.j];
+        q.ctx = ctx_lens[s0 + q.j];
         q.end = (q.ctx + kBS - 1) / kBS;
         if (q.pair < q.end) break;
         ++q.j;
@@ -591,7 +610,7 @@ __global__ void __launch_bounds__(kCWaves * 64) paged_decode_cascade_kernel(Casc
       return q.pair < q.end ? q : seq_pos(q.j + 1);
     };
     auto load = [&](PairRegs& r, const Pos& q) {
-      const int* bt = p.block_tables + (size_t)(s0 + q.j) * p.max_blocks;
+      const int* bt = block_tables + (size_t)(s0 + q.j) * p.max_blocks;
       load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
       load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
     };
@@ -700,9 +719,10 @@ extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, con
                  max_blocks, num_splits, 0, scale};
   if ((long)B * Hkv * num_splits >= g_wave_min_items) {
     const int items = B * num_splits;
-    paged_decode_wave_kernel<false><<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items);
+    paged_decode_wave_kernel<false><<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items, block_tables,
+                                                                                             ctx_lens);
   } else {
-    paged_decode_kernel<false><<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p);
+    paged_decode_kernel<false><<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p, block_tables, ctx_lens);
   }
   if (num_splits > 1)
     paged_decode_reduce_kernel<<<B * Hq, kD, 0, s>>>(part_o, part_lse, start_blk, pre_o, pre_lse, (bf16_t*)out,
@@ -722,7 +742,8 @@ extern "C" int lwc_paged_decode_prefix(const void* q, int q_stride, const void* 
   if (max_tiles == 0) return 0;
   DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, nullptr, nullptr, nullptr,
                  nullptr, tiles, nullptr, pre_o, pre_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, 1, max_tiles, scale};
-  paged_decode_wave_kernel<true><<<dim3((max_tiles + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, max_tiles);
+  paged_decode_wave_kernel<true><<<dim3((max_tiles + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, max_tiles,
+                                                                                            block_tables, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -737,14 +758,27 @@ extern "C" int lwc_paged_decode_cascade(const void* q, int q_stride, const void*
   if (max_tiles == 0) return 0;
   CascadeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, tiles,
                   (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale};
-  const size_t lds = (size_t)kCPairs * kPairBytes;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)paged_decode_cascade_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
-    attr_set = true;
+  static int pairs = 0;
+  if (pairs == 0) {
+    const char* e = getenv("LWC_CASCADE_PAIRS");
+    pairs = e ? atoi(e) : 8;
+    for (int k : {2, 4, 8})
+      (void)hipFuncSetAttribute(k == 2 ? (const void*)paged_decode_cascade_kernel<2>
+                                       : k == 4 ? (const void*)paged_decode_cascade_kernel<4>
+                                                : (const void*)paged_decode_cascade_kernel<8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, k * kPairBytes);
   }
-  paged_decode_cascade_kernel<<<dim3(Hkv, max_tiles), kCWaves * 64, lds, s>>>(p);
+  {
+    const char* e = getenv("LWC_CASCADE_PAIRS");  // experiment knob, re-read per launch
+    if (e) pairs = atoi(e);
+  }
+  const dim3 grid(Hkv, max_tiles);
+  if (pairs == 2)
+    paged_decode_cascade_kernel<2><<<grid, kCWaves * 64, 2 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
+  else if (pairs == 4)
+    paged_decode_cascade_kernel<4><<<grid, kCWaves * 64, 4 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
+  else
+    paged_decode_cascade_kernel<8><<<grid, kCWaves * 64, 8 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
   return (int)hipGetLastError();
 }
 

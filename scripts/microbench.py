@@ -273,6 +273,12 @@ def attention_prefix(dev):
         t_exact = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct_exact, Hq, sc))
         print(f"  cascade exact grid ({nt} tiles): {t_exact:7.1f} us", flush=True)
         t_c = timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct, Hq, sc))
+        for pairs in os.environ.get("CASCADE_PAIRS", "").split(","):
+            if pairs:
+                os.environ["LWC_CASCADE_PAIRS"] = pairs
+                tp_ = [timeit(lambda: ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct, Hq, sc)) for _ in range(3)]
+                print(f"  cascade LDS pairs={pairs}: {sorted(tp_)[1]:7.1f} us", flush=True)
+        os.environ.pop("LWC_CASCADE_PAIRS", None)
         ref_o = ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc)
         got = ops.paged_decode_cascade(q, kc, vc, bt, ctx, ct, Hq, sc)
         err = (got.float() - ref_o.float()).abs().max().item()
