@@ -9,5 +9,9 @@ ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1"}
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py $ARGS > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -5 gpurun_out/prof_bench.log
-find gpurun_out/prof -name "*stats*" | head
+STATS=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
+[ -n "$STATS" ] && python3 scripts/summarize_profile.py "$STATS" "bench.py $ARGS (rocprofv3 --kernel-trace --stats)" \
+    gpurun_out/prof_summary.md > /dev/null
+# keep the stats, drop the multi-MB per-dispatch trace (gpurun copies back <= 64 MiB)
+find gpurun_out/prof -name "*kernel_trace.csv" -delete
 exit $rc
