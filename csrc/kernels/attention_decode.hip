@@ -67,38 +67,49 @@ struct PairRegs {
   short4v va[8], vb[8];
 };
 
+// Token rows at or past `ctx` (the tail of a sequence's last block, or a pair without a B block) are
+// not fetched: the lanes that own them skip the load (exec-masked, no HBM/L2 traffic) and hold zeros.
+// Their scores are masked to -inf and their V elements selected away (pair_softmax / pair_values), so
+// the values never matter; zeros only keep the registers defined.  At the bench's decode shape the
+// suffix's last block is on average half empty: ~10 % of the suffix bytes.
 LWC_DEVICE void load_pair_k(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
-                            int g) {
+                            int g, int ctx = 0x7fffffff) {
   const size_t kv_head_stride = (size_t)kBS * kD;  // elements per (block, head)
   const int physA = bt[blkA];
   const int physB = hasB ? bt[blkA + 1] : physA;
   const bf16_t* kA = p.kc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
   const bf16_t* kB = p.kc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+  const bool okA = blkA * kBS + r16 < ctx;
+  const bool okB = hasB && (blkA + 1) * kBS + r16 < ctx;
+  const short8 z{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    r.ka[s] = *reinterpret_cast<const short8*>(kA + r16 * kD + 32 * s + 8 * g);
-    r.kb[s] = *reinterpret_cast<const short8*>(kB + r16 * kD + 32 * s + 8 * g);
+    r.ka[s] = okA ? *reinterpret_cast<const short8*>(kA + r16 * kD + 32 * s + 8 * g) : z;
+    r.kb[s] = okB ? *reinterpret_cast<const short8*>(kB + r16 * kD + 32 * s + 8 * g) : z;
   }
 }
 
 LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
-                            int g) {
+                            int g, int ctx = 0x7fffffff) {
   const size_t kv_head_stride = (size_t)kBS * kD;
   const int physA = bt[blkA];
   const int physB = hasB ? bt[blkA + 1] : physA;
   const bf16_t* vA = p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
   const bf16_t* vB = p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+  const bool okA = blkA * kBS + 4 * g < ctx;  // lane group g holds tokens 4g..4g+3
+  const bool okB = hasB && (blkA + 1) * kBS + 4 * g < ctx;
+  const short4v z{0, 0, 0, 0};
 #pragma unroll
   for (int n = 0; n < 8; ++n) {  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
-    r.va[n] = *reinterpret_cast<const short4v*>(vA + (g * kD + 16 * n + r16) * 4);
-    r.vb[n] = *reinterpret_cast<const short4v*>(vB + (g * kD + 16 * n + r16) * 4);
+    r.va[n] = okA ? *reinterpret_cast<const short4v*>(vA + (g * kD + 16 * n + r16) * 4) : z;
+    r.vb[n] = okB ? *reinterpret_cast<const short4v*>(vB + (g * kD + 16 * n + r16) * 4) : z;
   }
 }
 
 LWC_DEVICE void load_pair(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
-                          int g) {
-  load_pair_k(r, p, bt, kvh, blkA, hasB, r16, g);
-  load_pair_v(r, p, bt, kvh, blkA, hasB, r16, g);
+                          int g, int ctx = 0x7fffffff) {
+  load_pair_k(r, p, bt, kvh, blkA, hasB, r16, g, ctx);
+  load_pair_v(r, p, bt, kvh, blkA, hasB, r16, g, ctx);
 }
 
 // S^T for the pair's two blocks (C layout: lane reg i = S^T[tok 4g+i][row r16]).
@@ -273,7 +284,7 @@ __global__ void __launch_bounds__(256)
   for (int pair = blk_begin + 2 * wid; pair < blk_end; pair += 2 * kWaves) {
     PairRegs r;
     const bool hasB = pair + 1 < blk_end;
-    load_pair(r, p, bt, kvh, pair, hasB, r16, g);
+    load_pair(r, p, bt, kvh, pair, hasB, r16, g, ctx);
     attend_pair(r, pair, hasB, ctx, qf, sl2, g, o, m, l);
   }
 
@@ -389,19 +400,19 @@ __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, 
   PairRegs r;
   int pair = blk_begin;
   if (pair < blk_end) {
-    load_pair_k(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g);
-    load_pair_v(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g);
+    load_pair_k(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g, ctx);
+    load_pair_v(r, p, bt, kvh, pair, pair + 1 < blk_end, r16, g, ctx);
   }
   while (pair < blk_end) {
     const bool hasB = pair + 1 < blk_end;
     const int nxt = pair + 2;
     float4v sa, sb;
     pair_scores(r, qf, sa, sb);
-    if (nxt < blk_end) load_pair_k(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g);
+    if (nxt < blk_end) load_pair_k(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g, ctx);
     short8 pf;
     pair_softmax(sa, sb, pair, hasB, ctx, true, sl2, g, o, m, l, pf);
     pair_values(r, pf, pair, hasB, ctx, g, o);
-    if (nxt < blk_end) load_pair_v(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g);
+    if (nxt < blk_end) load_pair_v(r, p, bt, kvh, nxt, nxt + 1 < blk_end, r16, g, ctx);
     pair = nxt;
   }
 
@@ -611,8 +622,8 @@ __global__ void __launch_bounds__(kCWaves * 64)
     };
     auto load = [&](PairRegs& r, const Pos& q) {
       const int* bt = block_tables + (size_t)(s0 + q.j) * p.max_blocks;
-      load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
-      load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g);
+      load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
+      load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
     };
     auto attend = [&](const PairRegs& r, const Pos& q) {
       const bool row_on = r16 < nrows && r16 / p.G == q.j;

@@ -304,7 +304,7 @@ def sampler(dev):
     from llm_weighted_consensus_amd import ops
 
     V = 128256
-    for B in (256, 512):
+    for B in (512, 3072):
         logits = (torch.randn(B, V, device=dev) * 2).to(torch.bfloat16)
         f = lambda v: torch.full((B,), float(v), device=dev)
         seeds = torch.arange(B, device=dev, dtype=torch.int64)
