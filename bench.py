@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--requests", type=int, default=48, help="requests per GPU per step (R)")
+    ap.add_argument("--requests", type=int, default=64, help="requests per GPU per step (R)")
     ap.add_argument("--candidates", type=int, default=64, help="candidates per request (N)")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=128)

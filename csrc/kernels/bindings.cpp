@@ -36,7 +36,7 @@ int lwc_prefill_attention(const void*, const void*, const void*, void*, const in
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
                const float*, const float*, const float*, void*, const int*, const float*, const int*,
                const unsigned int*, const int*, const unsigned long long*, const unsigned long long*, int, int,
-               int*, float*, int*, float*, hipStream_t);
+               int, int*, float*, int*, float*, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
 int lwc_vote_tally(const float*, const float*, int, int, int, float*, float*, float*, hipStream_t);
@@ -407,7 +407,8 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
             const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& bias_rows,
             const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& mask_rows,
             const at::Tensor& seeds, const at::Tensor& offsets, int64_t num_logprobs, at::Tensor& out_token,
-            at::Tensor& out_logprob, at::Tensor& out_topk_ids, at::Tensor& out_topk_lp, bool mask_logprobs) {
+            at::Tensor& out_logprob, at::Tensor& out_topk_ids, at::Tensor& out_topk_lp, bool mask_logprobs,
+            bool need_logprob) {
   CHECK_BF16(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits must be [B, V] with unit inner stride");
   const int B = (int)logits.size(0), V = (int)logits.size(1);
@@ -433,7 +434,7 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
                       opt_ptr<float>(bias), opt_ptr<int>(bias_rows), opt_ptr<unsigned int>(mask),
                       opt_ptr<int>(mask_rows), reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
                       reinterpret_cast<const unsigned long long*>(offsets.data_ptr()), (int)num_logprobs,
-                      mask_logprobs ? 1 : 0, out_token.data_ptr<int>(), out_logprob.data_ptr<float>(),
+                      mask_logprobs ? 1 : 0, need_logprob ? 1 : 0, out_token.data_ptr<int>(), out_logprob.data_ptr<float>(),
                       num_logprobs > 0 ? out_topk_ids.data_ptr<int>() : nullptr,
                       num_logprobs > 0 ? out_topk_lp.data_ptr<float>() : nullptr, cur_stream()),
            "sample");

@@ -46,6 +46,8 @@ struct SampleParams {
   int num_logprobs;          // K for top logprobs (0..20)
   int mask_logprobs;         // 1: rows with a grammar mask report logprobs over the MASKED distribution
                              //    (the restricted softmax over the allowed tokens — the vote fast path)
+  int need_logprob;          // 0: no caller reads out_logprob (and K == 0): the raw log-sum-exp is not
+                             //    computed and out_logprob is NaN
   int* out_token;            // [B]
   float* out_logprob;        // [B]  raw logprob of the sampled token
   int* out_topk_ids;         // [B, K]
@@ -115,6 +117,8 @@ __global__ void __launch_bounds__(kSampT) sample_kernel(SampleParams p) {
   __shared__ int s_cidx[kCollect];
   __shared__ int s_ccount;
   __shared__ float s_scan[kSampT / 64];
+  __shared__ uint32_t s_tkey[kSampT];
+  __shared__ uint32_t s_lb, s_fkey;
 
   const int b = blockIdx.x;
   const int t = threadIdx.x;
@@ -139,79 +143,90 @@ __global__ void __launch_bounds__(kSampT) sample_kernel(SampleParams p) {
       }
     }
   }
-  // ---- raw log-sum-exp ----
+  // ---- raw max (+ each thread's own max key: the top-K search bound) and log-sum-exp ----
   float mx = -INFINITY;
 OPAQUE_ROW(row);
 #pragma unroll
   for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) mx = fmaxf(mx, GET(row, j, e));
+  const uint32_t my_maxkey = f2key(mx);
   const float raw_max = block_max(mx, sred);
+  const int lane = t & 63, wid = t >> 6;
+  const int K = p.num_logprobs;
+  // The raw log-sum-exp (the denominator of every reported logprob) is only computed when some output
+  // needs it, and its exp sum rides along in a pass that runs anyway: the processed-row pass, or the
+  // sampling pass's exp when the row is unprocessed (then its max IS the raw max).  Only a greedy
+  // unprocessed row pays a pass of its own.
+  const bool need_lse = p.need_logprob || K > 0;
   float se = 0.f;
+
+  // ---- raw top-K (for top_logprobs): candidates collected here, ranked and written once the
+  // log-sum-exp is known ----
+  if (K > 0) {
+    // Bound first: the K largest per-thread maxima are K distinct elements, so the K-th largest element
+    // of the row is >= the K-th largest thread max (lb).  One wave finds lb over the 1024 thread maxima
+    // (no block barriers inside the search); the elements >= lb — rarely more than a few dozen — are
+    // then collected in one pass.  Only if they overflow the collection buffer does the exact 16-round
+    // search over the whole row run (starting from lb).  Masked (-inf, key 0x7f) entries are never
+    // candidates: a row with < K finite values returns fewer (rest: id -1).
+    if (t == 0) s_ccount = 0;
+    s_tkey[t] = my_maxkey;
+    __syncthreads();
+    if (t < 64) {
+      uint32_t lo = 0x80u, hi = 0xffffu;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        float c = 0.f;
+#pragma unroll
+        for (int i = 0; i < kSampT / 64; ++i) c += s_tkey[i * 64 + t] >= mid ? 1.f : 0.f;
+        if (wave_sum(c) >= (float)K)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      if (t == 0) s_lb = lo;
+    }
+    __syncthreads();
+    uint32_t lo = s_lb;
+#pragma unroll 1
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      if (attempt == 1) {  // overflow: exact search for the K-th largest key, then collect again
+        uint32_t hi = 0xffffu;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          int c = 0;
 OPAQUE_ROW(row);
 #pragma unroll
-  for (int j = 0; j < SLOTS; ++j)
+          for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) se += __expf(GET(row, j, e) - raw_max);
-  const float raw_lse = raw_max + __logf(block_sum(se, sred));
-
-  // ---- raw top-K (for top_logprobs) ----
-  const int K = p.num_logprobs;
-  if (K > 0) {
-    // largest key with count(>= key) >= K, never below the key just above -inf (0x7f): masked-out
-    // (-inf) entries are not candidates, so a row with < K finite values returns fewer (rest: id -1)
-    uint32_t lo = 0x80u, hi = 0xffffu;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      OPAQUE_ROW(row);
-      int c = 0;
+            for (int e = 0; e < 8; ++e) c += f2key(GET(row, j, e)) >= mid;
+          if (block_sum_i(c, sredi) >= K)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        __syncthreads();
+        if (t == 0) s_ccount = 0;
+        __syncthreads();
+      }
 OPAQUE_ROW(row);
 #pragma unroll
       for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) c += f2key(GET(row, j, e)) >= mid;
-      if (block_sum_i(c, sredi) >= K)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    if (t == 0) s_ccount = 0;
-    __syncthreads();
-OPAQUE_ROW(row);
-#pragma unroll
-    for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = GET(row, j, e);
-        const int idx = (j * kSampT + t) * 8 + e;
-        if (idx < p.V && f2key(v) >= lo) {
-          const int slot = atomicAdd(&s_ccount, 1);
-          if (slot < kCollect) {
-            s_cval[slot] = v;
-            s_cidx[slot] = idx;
+        for (int e = 0; e < 8; ++e) {
+          const float v = GET(row, j, e);
+          const int idx = (j * kSampT + t) * 8 + e;
+          if (f2key(v) >= lo) {  // padding past V holds -inf (key 0x7f < lo): never collected
+            const int slot = atomicAdd(&s_ccount, 1);
+            if (slot < kCollect) {
+              s_cval[slot] = v;
+              s_cidx[slot] = idx;
+            }
           }
         }
-      }
-    __syncthreads();
-    if (t < 64) {  // one wave: rank-sort the collected candidates (value desc, index asc)
-      const int n = min(s_ccount, kCollect);
-      for (int r = n + t; r < K; r += 64) {  // fewer finite values than K: empty slots
-        p.out_topk_ids[(size_t)b * K + r] = -1;
-        p.out_topk_lp[(size_t)b * K + r] = -INFINITY;
-      }
-      if (t < n) {
-        const float v = s_cval[t];
-        const int ix = s_cidx[t];
-        int rank = 0;
-        for (int u = 0; u < n; ++u) {
-          const float w = s_cval[u];
-          rank += (w > v) || (w == v && s_cidx[u] < ix);
-        }
-        if (rank < K) {
-          p.out_topk_ids[(size_t)b * K + rank] = ix;
-          p.out_topk_lp[(size_t)b * K + rank] = v - raw_lse;
-        }
-      }
+      __syncthreads();
+      if (s_ccount <= kCollect) break;  // block-uniform
     }
   }
 
@@ -223,7 +238,8 @@ OPAQUE_ROW(row);
   const float fpen = p.freq_pen ? p.freq_pen[b] : 0.f, ppen = p.pres_pen ? p.pres_pen[b] : 0.f;
   const float rpen = p.rep_pen ? p.rep_pen[b] : 1.f;
   const bool use_pen = crow && (fpen != 0.f || ppen != 0.f || rpen != 1.f);
-  if (brow || mrow || use_pen) {
+  const bool processed = brow || mrow || use_pen;
+  if (processed) {
 OPAQUE_ROW(row);
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
@@ -232,6 +248,10 @@ OPAQUE_ROW(row);
       float y[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = GET(row, j, e);
+      if (need_lse) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) se += __expf(y[e] - raw_max);
+      }
       if (brow) {
         const float4 b0 = reinterpret_cast<const float4*>(brow + (size_t)vi * 8)[0];
         const float4 b1 = reinterpret_cast<const float4*>(brow + (size_t)vi * 8)[1];
@@ -261,7 +281,18 @@ OPAQUE_ROW(row);
 
   const float T = p.temperature[b];
   int token = 0;
+  float raw_lse = __builtin_nanf("");
   if (T <= 0.f) {
+    if (need_lse) {
+      if (!processed) {
+OPAQUE_ROW(row);
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) se += __expf(GET(row, j, e) - raw_max);
+      }
+      raw_lse = raw_max + __logf(block_sum(se, sred));
+    }
     // ---- greedy: argmax (lowest index on ties) ----
     float bv = -INFINITY;
     int bi = 0x7fffffff;
@@ -290,16 +321,30 @@ OPAQUE_ROW(row);
     token = cand == 0x7fffffff ? 0 : cand;
   } else {
     const float invT = 1.f / T;
-    float ym = -INFINITY;
+    float ymax = raw_max;  // unprocessed row: the processed max IS the raw max (no extra pass)
+    if (processed) {
+      float ym = -INFINITY;
 OPAQUE_ROW(row);
 #pragma unroll
-    for (int j = 0; j < SLOTS; ++j)
+      for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
-    const float ymax = block_max(ym, sred);
+        for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
+      ymax = block_max(ym, sred);
+    }
     // ---- one exp per element: the row becomes u_i = exp((y_i - ymax)/T) in [0, 1] as packed fp16.
     // Non-negative fp16 bit patterns are order-preserving, so every later threshold search compares
-    // raw 16-bit keys and sums fp16 values: no transcendental inside the 16-round searches.
+    // raw 16-bit keys and sums fp16 values: no transcendental inside the searches.  The same pass
+    // sums this thread's share of Z (over the ROUNDED values, as every later mass is).
+    float zloc = 0.f;
+    // unprocessed row + logprobs wanted: the raw exp sum needs its own pass over the raw values (fusing
+    // it into the pass below doubles that pass's live values and the SLOTS=16 instance spills)
+    if (need_lse && !processed) {
+OPAQUE_ROW(row);
+#pragma unroll
+      for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) se += __expf(GET(row, j, e) - raw_max);
+    }
 OPAQUE_ROW(row);
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
@@ -308,8 +353,24 @@ OPAQUE_ROW(row);
         const float y0 = GET(row, j, 2 * c), y1 = GET(row, j, 2 * c + 1);
         const float u0 = y0 > -INFINITY ? __expf((y0 - ymax) * invT) : 0.f;
         const float u1 = y1 > -INFINITY ? __expf((y1 - ymax) * invT) : 0.f;
-        row[j][c] = (uint32_t)h2bits(u0) | ((uint32_t)h2bits(u1) << 16);
+        const uint16_t h0 = h2bits(u0), h1 = h2bits(u1);
+        zloc += (float)__builtin_bit_cast(_Float16, h0) + (float)__builtin_bit_cast(_Float16, h1);
+        row[j][c] = (uint32_t)h0 | ((uint32_t)h1 << 16);
       }
+    }
+    float Z;
+    if (need_lse) {  // both sums in one block reduction
+      const float zw = wave_sum(zloc), sw = wave_sum(se);
+      __syncthreads();
+      if (lane == 0) {
+        sred[wid] = zw;
+        sred[16 + wid] = sw;
+      }
+      __syncthreads();
+      Z = wave_sum(lane < kSampT / 64 ? sred[lane] : 0.f);
+      raw_lse = raw_max + __logf(wave_sum(lane < kSampT / 64 ? sred[16 + lane] : 0.f));
+    } else {
+      Z = block_sum(zloc, sred);
     }
     // mass of the elements with key >= KEY (macro, not a lambda: a by-reference capture of `row`
     // makes it addressable and sends it to scratch)
@@ -324,7 +385,7 @@ OPAQUE_ROW(row);
     }                                                                  \
     OUT = block_sum(_s, sred);                                         \
   } while (0)
-    uint32_t tau = 0;  // keep elements with key >= tau
+    uint32_t tau_k = 0;  // top-k: keep elements with key >= tau_k
     const int k = p.top_k[b];
     if (k > 0) {
       uint32_t lo = 0, hi = 0x3C00u;  // keys of [0, 1.0]
@@ -341,16 +402,146 @@ OPAQUE_ROW(row);
         else
           hi = mid - 1;
       }
-      tau = lo;
+      tau_k = lo;
     }
-    float Z;
-    MASS_GE(0u, Z);
+    // the filters other than top-p are plain lower bounds on the key
+    uint32_t L0 = tau_k;
+    const float mp = p.min_p[b];
+    if (mp > 0.f) L0 = max(L0, (uint32_t)h2bits(mp));        // u_i >= min_p  (u_max = 1)
+    const float ta = p.top_a[b];
+    if (ta > 0.f) L0 = max(L0, (uint32_t)h2bits(fminf(ta / Z, 1.f)));  // p_i >= top_a p_max^2 <=> u_i >= top_a / Z
+    if (L0 > 0x3C00u) L0 = 0x3C00u;                            // never filter out the argmax (u = 1)
+    if (L0 == 0u) L0 = 1u;                                     // zero-mass elements are never kept
+    // ---- top-p by rejection first (exact): draw s from the distribution over {key >= L0}; s is in the
+    // nucleus {key >= tau_p} iff the mass strictly above it is < top_p * mass(top-k set).  Accepted
+    // (probability >= top_p), s is exactly a draw from the nucleus-and-filters distribution.  Rejected,
+    // tau_p > key_s is known: the exact search for tau_p starts there and a fresh uniform is drawn
+    // over {key >= max(tau_p, L0)} — the result is again exactly distributed (the fallback does not
+    // depend on the rejected draw).  Saves the ~14 block-wide passes of a threshold search per row in
+    // the common case.
     const float tp = p.top_p[b];
+    float target = 0.f;
     if (tp < 1.f) {
-      float mk;
-      MASS_GE(tau, mk);
-      const float target = tp * mk;
-      uint32_t lo = tau, hi = 0x3C00u;
+      float mk = Z;
+      if (tau_k > 0u) MASS_GE(tau_k, mk);
+      target = tp * mk;
+    }
+    uint32_t ctr[4] = {(uint32_t)p.offsets[b], (uint32_t)(p.offsets[b] >> 32), 0u, 0u};
+    philox4x32(ctr, (uint32_t)p.seeds[b], (uint32_t)(p.seeds[b] >> 32));
+    uint32_t tau = L0;
+    bool check = tp < 1.f;
+    int found = 0;
+#pragma unroll 1
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      // ---- inverse-CDF draw over {key >= tau} (order: thread-major, then slot, then element) ----
+      float local = 0.f;
+      if (tau <= 1u) {
+        local = zloc;  // every positive element is kept: the thread's share of Z
+      } else {
+OPAQUE_ROW(row);
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) local += (KEYU(row, j, e) >= tau) ? GETU(row, j, e) : 0.f;
+      }
+      // exclusive scan of `local` over threads
+      float incl = local;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float n = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += n;
+      }
+      __syncthreads();
+      if (lane == 63) s_scan[wid] = incl;
+      __syncthreads();
+      float wave_off = 0.f, total = 0.f;
+      for (int w = 0; w < kSampT / 64; ++w) {
+        const float sw = s_scan[w];
+        if (w < wid) wave_off += sw;
+        total += sw;
+      }
+      const float excl = wave_off + incl - local;
+      const float u01 = (((attempt == 0 ? ctr[0] : ctr[1]) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float u = u01 * total;
+      int mine = 0x7fffffff;
+      uint32_t mine_key = 0x3C00u;
+      if (local > 0.f && u >= excl && u < excl + local) {
+        float acc = excl;
+        int last = -1;
+        uint32_t last_key = 0u;
+OPAQUE_ROW(row);
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int idx = (j * kSampT + t) * 8 + e;
+            const uint32_t kk = KEYU(row, j, e);
+            if (kk >= tau && kk > 0u) {
+              last = idx;
+              last_key = kk;
+              acc += GETU(row, j, e);
+              if (mine == 0x7fffffff && u < acc) {
+                mine = idx;
+                mine_key = kk;
+              }
+            }
+          }
+        if (mine == 0x7fffffff && last >= 0) {  // rounding at the top edge
+          mine = last;
+          mine_key = last_key;
+        }
+      }
+      // the owning thread is unique except for float ties at a boundary: take the minimum
+      found = mine;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
+      __syncthreads();
+      if (lane == 0) sredi[wid] = found;
+      __syncthreads();
+      found = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
+      if (found == 0x7fffffff) {
+        // u landed past the last kept element through rounding: fall back to argmax (key 0x3C00: always
+        // inside the nucleus)
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+OPAQUE_ROW(row);
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = GETU(row, j, e);
+            const int idx = (j * kSampT + t) * 8 + e;
+            if (v > bv || (v == bv && idx < bi)) {  // padding past V has u = 0 < u_max = 1
+              bv = v;
+              bi = idx;
+            }
+          }
+        const float gm = block_max(bv, sred);
+        int cand = (bv == gm) ? bi : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+        __syncthreads();
+        if (lane == 0) sredi[wid] = cand;
+        __syncthreads();
+        cand = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+        found = cand == 0x7fffffff ? 0 : cand;
+        break;
+      }
+      if (!check) break;
+      // ---- nucleus test of the draw ----
+      __syncthreads();
+      if (mine == found) s_fkey = mine_key;
+      __syncthreads();
+      const uint32_t ks = s_fkey;
+      float above;
+      MASS_GE(ks + 1u, above);
+      if (above < target) break;  // accepted (block-uniform)
+      // rejected: tau_p > ks.  Exact search for the largest key with mass(>= key) >= target.
+      uint32_t lo = ks + 1u, hi = 0x3C00u;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         float mm;
@@ -360,100 +551,31 @@ OPAQUE_ROW(row);
         else
           hi = mid - 1;
       }
-      tau = lo;
+      tau = max(lo, L0);
+      check = false;
     }
-    const float mp = p.min_p[b];
-    if (mp > 0.f) tau = max(tau, (uint32_t)h2bits(mp));        // u_i >= min_p  (u_max = 1)
-    const float ta = p.top_a[b];
-    if (ta > 0.f) tau = max(tau, (uint32_t)h2bits(ta / Z));    // p_i >= top_a p_max^2 <=> u_i >= top_a / Z
-    if (tau > 0x3C00u) tau = 0x3C00u;                           // never filter out the argmax (u = 1)
-    if (tau == 0u) tau = 1u;                                    // zero-mass elements are never kept
-    // ---- inverse-CDF draw over the kept set (order: thread-major, then slot, then element) ----
-    float local = 0.f;
-OPAQUE_ROW(row);
-#pragma unroll
-    for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) local += (KEYU(row, j, e) >= tau) ? GETU(row, j, e) : 0.f;
-    // exclusive scan of `local` over threads
-    const int lane = t & 63, wid = t >> 6;
-    float incl = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float n = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += n;
-    }
-    __syncthreads();
-    if (lane == 63) s_scan[wid] = incl;
-    __syncthreads();
-    float wave_off = 0.f, total = 0.f;
-    for (int w = 0; w < kSampT / 64; ++w) {
-      const float s = s_scan[w];
-      if (w < wid) wave_off += s;
-      total += s;
-    }
-    const float excl = wave_off + incl - local;
-    uint32_t ctr[4] = {(uint32_t)p.offsets[b], (uint32_t)(p.offsets[b] >> 32), 0u, 0u};
-    philox4x32(ctr, (uint32_t)p.seeds[b], (uint32_t)(p.seeds[b] >> 32));
-    const float u01 = ((ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-    const float u = u01 * total;
-    int found = 0x7fffffff;
-    if (local > 0.f && u >= excl && u < excl + local) {
-      float acc = excl;
-      int last = -1;
-OPAQUE_ROW(row);
-#pragma unroll
-      for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int idx = (j * kSampT + t) * 8 + e;
-          if (KEYU(row, j, e) >= tau) {
-            last = idx;
-            acc += GETU(row, j, e);
-            if (found == 0x7fffffff && u < acc) found = idx;
-          }
-        }
-      if (found == 0x7fffffff) found = last;  // rounding at the top edge
-    }
-    // the owning thread is unique except for float ties at a boundary: take the minimum
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
-    __syncthreads();
-    if (lane == 0) sredi[wid] = found;
-    __syncthreads();
-    found = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
-    if (found == 0x7fffffff) {
-      // u landed past the last kept element through rounding: fall back to argmax
-      found = 0;
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-OPAQUE_ROW(row);
-#pragma unroll
-      for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = GETU(row, j, e);
-          const int idx = (j * kSampT + t) * 8 + e;
-          if (idx < p.V && (v > bv || (v == bv && idx < bi))) {
-            bv = v;
-            bi = idx;
-          }
-        }
-      const float gm = block_max(bv, sred);
-      int cand = (bv == gm) ? bi : 0x7fffffff;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
-      __syncthreads();
-      if (lane == 0) sredi[wid] = cand;
-      __syncthreads();
-      cand = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
-      found = cand == 0x7fffffff ? 0 : cand;
-    }
+#undef MASS_GE
     token = found;
+  }
+  if (K > 0 && t < 64) {  // one wave: rank-sort the collected top-K candidates (value desc, index asc)
+    const int n = min(s_ccount, kCollect);
+    for (int r = n + t; r < K; r += 64) {  // fewer finite values than K: empty slots
+      p.out_topk_ids[(size_t)b * K + r] = -1;
+      p.out_topk_lp[(size_t)b * K + r] = -INFINITY;
+    }
+    if (t < n) {
+      const float v = s_cval[t];
+      const int ix = s_cidx[t];
+      int rank = 0;
+      for (int u = 0; u < n; ++u) {
+        const float w = s_cval[u];
+        rank += (w > v) || (w == v && s_cidx[u] < ix);
+      }
+      if (rank < K) {
+        p.out_topk_ids[(size_t)b * K + rank] = ix;
+        p.out_topk_lp[(size_t)b * K + rank] = v - raw_lse;
+      }
+    }
   }
   if (t == 0) {
     p.out_token[b] = token;
@@ -472,14 +594,14 @@ extern "C" int lwc_sample(const void* logits, int ld, int V, int B, const float*
                           const float* pres_pen, const float* rep_pen, void* counts, const int* count_rows,
                           const float* bias, const int* bias_rows, const unsigned int* mask, const int* mask_rows,
                           const unsigned long long* seeds, const unsigned long long* offsets, int num_logprobs,
-                          int mask_logprobs, int* out_token, float* out_logprob, int* out_topk_ids,
+                          int mask_logprobs, int need_logprob, int* out_token, float* out_logprob, int* out_topk_ids,
                           float* out_topk_lp, hipStream_t s) {
   using namespace lwc;
   if (V % 32 != 0 || num_logprobs < 0 || num_logprobs > kMaxTopK) return -1;
   if (B == 0) return 0;
   SampleParams p{(const bf16_t*)logits, ld, V, temperature, top_p, top_k, min_p, top_a, freq_pen, pres_pen, rep_pen,
                  (uint16_t*)counts, count_rows, bias, bias_rows, mask, mask_rows, seeds, offsets, num_logprobs,
-                 mask_logprobs, out_token, out_logprob, out_topk_ids, out_topk_lp};
+                 mask_logprobs, need_logprob, out_token, out_logprob, out_topk_ids, out_topk_lp};
   const int nvec = V / 8;
   const int slots = (nvec + kSampT - 1) / kSampT;
   if (slots <= 4)

@@ -36,7 +36,7 @@ from ..models.llama import KVCache
 from .sampling import SamplingParams
 from .tokenizer import IncrementalDecoder
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096)
+BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096, 5120, 6144, 8192)
 
 
 @dataclass
@@ -552,6 +552,7 @@ class LLMEngine:
         st["bias_rows"] = col([s.group.bias_row for s in seqs], np.int32, -1)
         st["seeds"] = col([s.seed for s in seqs], np.int64)
         st["K"] = max((p.top_logprobs for p in ps), default=0)
+        st["need_lp"] = any(p.logprobs for p in ps)
         st["any_pen"] = any(p.uses_penalties for p in ps)
         st["any_bias"] = any(s.group.bias_row >= 0 for s in seqs)
         self._comp_cache = (key, st)
@@ -643,7 +644,7 @@ class LLMEngine:
                    bias=self.bias if st["any_bias"] else None,
                    bias_rows=d["bias_rows"] if st["any_bias"] else None,
                    mask=mask, mask_rows=mask_rows, mask_logprobs=self.constrained_logprobs,
-                   out_token=outs[0], out_logprob=outs[1], out_topk_ids=outs[2], out_topk_lp=outs[3])
+                   need_logprob=st["need_lp"], out_token=outs[0], out_logprob=outs[1], out_topk_ids=outs[2], out_topk_lp=outs[3])
         out_host.copy_(out_dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -739,6 +740,7 @@ class LLMEngine:
             bias=self.bias if any_bias else None,
             bias_rows=i32([s.group.bias_row for s in seqs]) if any_bias else None,
             mask=mask, mask_rows=mask_rows, mask_logprobs=self.constrained_logprobs,
+            need_logprob=any(p.logprobs for p in ps),
         )
         for s in seqs:
             s.n_launched += 1

@@ -317,11 +317,13 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
            min_p: torch.Tensor, top_a: torch.Tensor, seeds: torch.Tensor, offsets: torch.Tensor,
            num_logprobs: int = 0, freq_pen=None, pres_pen=None, rep_pen=None, counts=None, count_rows=None,
            bias=None, bias_rows=None, mask=None, mask_rows=None, out_token=None, out_logprob=None,
-           out_topk_ids=None, out_topk_lp=None, mask_logprobs: bool = False):
+           out_topk_ids=None, out_topk_lp=None, mask_logprobs: bool = False, need_logprob: bool = True):
     """Fused sampler (K8a-d).  Returns (tokens[B] int32, token_logprob[B] f32, topk_ids[B,K], topk_lp[B,K]).
     Logprobs are over the raw model distribution (OpenAI semantics); with ``mask_logprobs`` rows that
     carry a grammar mask report them over the MASKED distribution instead — at a constrained key-letter
-    step that is the exact restricted softmax over the sibling letters (the local vote fast path)."""
+    step that is the exact restricted softmax over the sibling letters (the local vote fast path).
+    ``need_logprob=False`` (and ``num_logprobs=0``): nobody reads the sampled token's logprob, so the raw
+    log-sum-exp is skipped (one exp pass fewer per row) and ``token_logprob`` is NaN."""
     B = logits.shape[0]
     dev = logits.device
     K = int(num_logprobs)
@@ -335,7 +337,7 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
         out_topk_lp = torch.empty(B, max(K, 1), dtype=torch.float32, device=dev)
     kernels().sample(logits, temperature, top_p, top_k, min_p, top_a, freq_pen, pres_pen, rep_pen, counts, count_rows,
                      bias, bias_rows, mask, mask_rows, seeds, offsets, K, out_token, out_logprob, out_topk_ids,
-                     out_topk_lp, bool(mask_logprobs))
+                     out_topk_lp, bool(mask_logprobs), bool(need_logprob))
     return out_token, out_logprob, out_topk_ids[:, :K], out_topk_lp[:, :K]
 
 

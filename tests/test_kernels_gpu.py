@@ -369,6 +369,26 @@ def test_sample_reproducible(gpu):
     assert not torch.equal(a, c)
 
 
+def test_sample_skip_logprob(gpu):
+    """need_logprob=False skips the raw log-sum-exp: same tokens as the full path for every sampling mode,
+    NaN token logprob; the full path's logprob matches the fp32 log-softmax (fused into the sampling
+    pass for unprocessed rows, into the bias pass for processed ones)."""
+    torch.manual_seed(5)
+    B, V = 16, 128256
+    logits = _bf(B, V, dev=gpu, scale=2.0)
+    lsm = torch.log_softmax(logits.float(), -1)
+    bias = torch.zeros(1, V, device=gpu)
+    bias[0, :64] = 3.0
+    rows = torch.tensor([0, -1] * (B // 2), dtype=torch.int32, device=gpu)
+    for kw in ({"temperature": 0.0}, {"top_p": 0.9, "temperature": 0.8}, {"top_k": 50}, {"bias": bias, "bias_rows": rows},
+               {"temperature": 0.0, "bias": bias, "bias_rows": rows}):
+        t1, lp1, *_ = _sample(logits, gpu, **kw)
+        t0, lp0, *_ = _sample(logits, gpu, need_logprob=False, **kw)
+        assert torch.equal(t0, t1), kw
+        assert torch.isnan(lp0).all(), kw
+        _close(lp1, lsm.gather(1, t1.long()[:, None])[:, 0], 2e-3, 1e-3)
+
+
 def test_pool_cosine_tally(gpu):
     from llm_weighted_consensus_amd import ops
 
