@@ -181,17 +181,33 @@ class LlamaModel:
         cfg = self.cfg
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        # Dense single-rank layers add the o / down projections into the residual stream inside the GEMM
+        # (gemm_plan.linear_add_), so the norms that follow only read x_res and write h.  Subclasses that
+        # reduce the projections across ranks or route them through experts use the separate
+        # residual-add + norm kernel.
+        fused = self._dense_residual and self.g8_ws is not None
         h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
         for li, L in enumerate(self.layers):
             qkv = self._proj(h, L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
             attn = attn_fn(qkv, li)
-            o = self._attn_out(attn.view(T, Hq * D), L)
-            h = ops.rmsnorm(o, L.mlp_norm, cfg.rms_eps, residual=x_res)
-            down = self._mlp(h, L)
             nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
-            h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
+            if fused:
+                gemm_plan.linear_add_(attn.view(T, Hq * D), L.wo, x_res, ws=self.g8_ws)
+                h = ops.rmsnorm(x_res, L.mlp_norm, cfg.rms_eps)
+                gemm_plan.linear_add_(self._act(h, L), L.w_down, x_res, ws=self.g8_ws)
+                h = ops.rmsnorm(x_res, nxt, cfg.rms_eps)
+            else:
+                o = self._attn_out(attn.view(T, Hq * D), L)
+                h = ops.rmsnorm(o, L.mlp_norm, cfg.rms_eps, residual=x_res)
+                down = self._mlp(h, L)
+                h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
         return h
+
+    @property
+    def _dense_residual(self) -> bool:
+        cls = type(self)
+        return cls._attn_out is LlamaModel._attn_out and cls._mlp is LlamaModel._mlp
 
     def _proj(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         """Dense projection on the per-shape backend (hipBLASLt or gemm8p, ops/gemm_plan.py)."""
@@ -206,11 +222,13 @@ class LlamaModel:
     def _mlp(self, h: torch.Tensor, L) -> torch.Tensor:
         """Dense SwiGLU MLP: gate|up GEMM with SwiGLU (fused in gemm8p's epilogue, or hipBLASLt + K5
         silu_mul), down GEMM."""
+        return self._proj(self._act(h, L), L.w_down)
+
+    def _act(self, h: torch.Tensor, L) -> torch.Tensor:
+        """silu(h Wg^T) * (h Wu^T): the gate|up GEMM with its SwiGLU."""
         if self.g8_ws is None:
-            act = ops.silu_mul(F.linear(h, L.w_gate_up), block=L.gu_block)
-        else:
-            act = gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
-        return self._proj(act, L.w_down)
+            return ops.silu_mul(F.linear(h, L.w_gate_up), block=L.gu_block)
+        return gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
 
     def tune_gemms(self, M: int) -> None:
         """Pick the GEMM backend of every decode projection at batch M by timing both (before the
@@ -222,9 +240,10 @@ class LlamaModel:
         xa = torch.randn(M, cfg.heads * cfg.head_dim, device=self.device).to(self.dtype)
         xf = torch.randn(M, cfg.ffn, device=self.device).to(self.dtype)
         gemm_plan.tune(x, L.wqkv, ws=self.g8_ws)
-        gemm_plan.tune(xa, L.wo, ws=self.g8_ws)
+        epi = "residual" if self._dense_residual else "plain"
+        gemm_plan.tune(xa, L.wo, epi, ws=self.g8_ws)
         gemm_plan.tune(x, L.w_gate_up, "swiglu", L.gu_block, ws=self.g8_ws)
-        gemm_plan.tune(xf, L.w_down, ws=self.g8_ws)
+        gemm_plan.tune(xf, L.w_down, epi, ws=self.g8_ws)
         gemm_plan.tune(x, self.lm_head, ws=self.g8_ws)
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,

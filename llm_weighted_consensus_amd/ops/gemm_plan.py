@@ -4,7 +4,8 @@ Two backends compute ``A . W^T`` for the dense projections:
 
 * ``blas`` — hipBLASLt through ``torch.nn.functional.linear`` (its own stream-K kernels);
 * ``g8``   — the hand-written 8-phase MFMA GEMM with a stream-K tail (``csrc/kernels/gemm8p.hip``),
-  which also fuses the SwiGLU of the gate|up projection into its epilogue.
+  which also fuses the SwiGLU of the gate|up projection, or the residual add of the o / down
+  projections (:func:`linear_add_`), into its epilogue.
 
 Neither wins everywhere (``profiles/gemm8p.md``: g8 is ahead on the fused gate_up+SwiGLU and the qkv
 projection at decode batch 3072, hipBLASLt on most shapes at batch 1024), so the choice is made per
@@ -46,6 +47,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, ws=None) -> torch.Tensor:
     return F.linear(x, w)
 
 
+def linear_add_(x: torch.Tensor, w: torch.Tensor, acc: torch.Tensor, ws=None) -> torch.Tensor:
+    """acc += x [M, K] . w[N, K]^T in place (the residual-stream update of the o / down projections):
+    hipBLASLt with beta = 1 (C = D = acc, one fp32 sum and one rounding), or gemm8p's residual
+    epilogue writing over its residual operand (every output element is read and written by the same
+    lane).  Saves the separate residual add's read and write of the [M, N] projection output."""
+    M, K = x.shape
+    N = w.shape[0]
+    if (choice(M, N, K, "residual") == "g8" and _g8_ok(N, K, "residual") and x.stride(1) == 1
+            and acc.is_contiguous()):
+        return gemm8p(x, w, residual=acc, out=acc, ws=ws)
+    return acc.addmm_(x, w.t())
+
+
 def swiglu(x: torch.Tensor, w_gu: torch.Tensor, block: int, ws=None) -> torch.Tensor:
     """silu(x Wg^T) * (x Wu^T) [M, F] for a fused gate|up weight [2F, K] whose rows are [gate; up]
     (block 0) or interleaved in blocks of ``block`` (ops.swiglu_interleave; required by g8)."""
@@ -85,6 +99,10 @@ def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, w
     if epi == "swiglu":
         t_blas = _time(lambda: silu_mul(F.linear(x, w), block=block))
         t_g8 = _time(lambda: gemm8p(x, w, swiglu=True, ws=ws))
+    elif epi == "residual":
+        acc = torch.zeros(M, N, dtype=x.dtype, device=x.device)
+        t_blas = _time(lambda: acc.addmm_(x, w.t()))
+        t_g8 = _time(lambda: gemm8p(x, w, residual=acc, out=acc, ws=ws))
     else:
         t_blas = _time(lambda: F.linear(x, w))
         t_g8 = _time(lambda: gemm8p(x, w, ws=ws))

@@ -515,6 +515,36 @@ def test_gemm8p(gpu, M, N, K, epi):
     assert int(ops.gemm8p_workspace(A.device)[1].abs().sum()) == 0, "stream-K flags left set"
 
 
+@pytest.mark.parametrize("backend", ["g8", "blas"])
+@pytest.mark.parametrize("M,N,K", [(520, 1024, 2048), (3072, 4096, 4096)])
+def test_linear_add_inplace(gpu, backend, M, N, K):
+    """gemm_plan.linear_add_: acc += A W^T in place (gemm8p's residual epilogue writing over its residual
+    operand / hipBLASLt beta = 1) vs an fp32 matmul + add, repeated so the second call accumulates onto
+    the first call's result."""
+    from llm_weighted_consensus_amd.ops import gemm_plan
+
+    torch.manual_seed(M + K)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    acc = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    ref = acc.float()
+    key = (M, N, K, "residual")
+    old = gemm_plan._CHOICE.get(key)
+    gemm_plan._CHOICE[key] = backend
+    try:
+        for _ in range(2):
+            ref = ref + A.float() @ W.float().t()
+            out = gemm_plan.linear_add_(A, W, acc)
+            assert out.data_ptr() == acc.data_ptr()
+            _close(acc, ref, 5e-2, 2e-2)
+            ref = acc.float()  # the next call accumulates onto the rounded stream, as the model does
+    finally:
+        if old is None:
+            gemm_plan._CHOICE.pop(key, None)
+        else:
+            gemm_plan._CHOICE[key] = old
+
+
 def test_sample_constrained_logprobs(gpu):
     """mask_logprobs: a masked row's top-k logprobs are the restricted log-softmax over the allowed
     tokens (sum of their probabilities = 1), in the raw order of the allowed logits; unmasked rows and
