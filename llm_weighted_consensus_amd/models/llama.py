@@ -30,7 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops import gemm_plan
+from ..ops import blas_tuning, gemm_plan
 from .config import DecoderConfig
 
 
@@ -117,6 +117,7 @@ class LlamaModel:
                     L.w_gate_up = ops.swiglu_interleave(L.w_gate_up)
                     L.gu_block = 32
             self.g8_ws = ops.new_gemm8p_workspace(self.device)
+            blas_tuning.enable()  # offline-tuned hipBLASLt / rocBLAS solutions for the library GEMMs
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int) -> None:
