@@ -228,9 +228,9 @@ def attention_prefix(dev):
     from llm_weighted_consensus_amd import ops
 
     Hq, Hkv, D, BS = 32, 8, 128, 16
-    cases = [(16, 64, 16, 64), (48, 64, 16, 64), (48, 64, 16, 120)]
+    cases = [(16, 64, 16, 64), (48, 64, 16, 64), (48, 64, 16, 120), (64, 64, 16, 64)]
     if os.environ.get("MICRO_PREFIX_QUICK"):
-        cases = [(16, 64, 16, 64), (48, 64, 16, 64)]
+        cases = [(48, 64, 16, 64), (64, 64, 16, 64)]
     for (R, N, P, gen) in cases:
         B = R * N
         sblk = (gen + 1 + BS - 1) // BS
@@ -304,7 +304,7 @@ def sampler(dev):
     from llm_weighted_consensus_amd import ops
 
     V = 128256
-    for B in (512, 3072):
+    for B in (512, 4096):
         logits = (torch.randn(B, V, device=dev) * 2).to(torch.bfloat16)
         f = lambda v: torch.full((B,), float(v), device=dev)
         seeds = torch.arange(B, device=dev, dtype=torch.int64)
