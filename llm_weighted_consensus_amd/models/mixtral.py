@@ -18,6 +18,15 @@ Tensor parallelism (``tp_group``): attention heads and every expert's FFN column
 the ranks (Megatron layout: q/k/v and gate|up column-parallel, o and down row-parallel); the two
 row-parallel outputs are summed with one all-reduce each (C3) before the residual norm.  The shard is
 taken from the full random-init / loaded weights so any TP degree computes the same function.
+
+Expert parallelism (``ep_group``, C4, `parallel/expert.py`): the alternative to TP for the MoE layers.
+Rank r of the EP group keeps experts [r*E/W, (r+1)*E/W) with their FULL FFN width (grouped-GEMM tiles
+stay 2x wider than under TP=2) and replicated attention; each rank decodes its own sequences and the
+(token, slot) rows travel to the expert owners and back with two all-to-alls per layer (fp8 mode
+dispatches the e4m3 rows + per-row scales: half the bytes).  Ranks must step in lockstep (every rank
+calls every layer, with zero tokens if idle); the padded exchange with a fixed ``ep_capacity`` (the
+most tokens any rank feeds a layer in one step, e.g. the largest decode bucket) keeps the decode step
+free of host synchronisation.
 """
 from __future__ import annotations
 
@@ -49,9 +58,22 @@ class MoELayerWeights:
 class MixtralModel(LlamaModel):
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8: bool = False,
-                 tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, ep_rank: int = 0, ep_size: int = 1,
+                 ep_group=None, ep_mode: str = "padded", ep_capacity: Optional[int] = None):
         if not cfg.num_experts:
             raise ValueError(f"{cfg.name} is dense; use LlamaModel")
+        if ep_size > 1 and tp_size > 1:
+            raise ValueError("choose TP or EP for the MoE decoder, not both")
+        if cfg.num_experts % ep_size:
+            raise ValueError(f"ep_size {ep_size} must divide num_experts {cfg.num_experts}")
+        self.ep_rank, self.ep_size, self.ep_capacity = ep_rank, ep_size, ep_capacity
+        self.ep = None
+        if ep_size > 1:
+            from ..parallel.expert import ExpertParallel
+
+            self.ep = ExpertParallel(cfg.num_experts, group=ep_group, mode=ep_mode)
+            if self.ep.W != ep_size:
+                raise ValueError(f"ep_group has {self.ep.W} ranks, ep_size is {ep_size}")
         if cfg.heads % tp_size or cfg.kv_heads % tp_size or cfg.ffn % tp_size:
             raise ValueError(f"tp_size {tp_size} must divide heads, kv_heads and ffn")
         self.fp8, self.tp_rank, self.tp_size, self.tp_group = fp8, tp_rank, tp_size, tp_group
@@ -77,6 +99,10 @@ class MixtralModel(LlamaModel):
         v = wv[r * hk * D:(r + 1) * hk * D]
         wqkv = torch.cat([q, k, v]).contiguous()
         wo_s = wo[:, r * hq * D:(r + 1) * hq * D].contiguous()
+        if self.ep_size > 1:  # this EP rank's experts, full FFN width
+            el = cfg.num_experts // self.ep_size
+            e0 = self.ep_rank * el
+            w1, w3, w2 = w1[e0:e0 + el], w3[e0:e0 + el], w2[e0:e0 + el]
         w13 = torch.cat([w1[:, r * fl:(r + 1) * fl], w3[:, r * fl:(r + 1) * fl]], dim=1).contiguous()  # [E,2fl,d]
         w2_s = w2[:, :, r * fl:(r + 1) * fl].contiguous()                                             # [E,d,fl]
         s13 = s2 = None
@@ -147,18 +173,42 @@ class MixtralModel(LlamaModel):
     def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
         return self._all_reduce(F.linear(attn, L.wo))
 
+    def _experts(self, x: torch.Tensor, row_off: torch.Tensor, L: MoELayerWeights,
+                 scale: Optional[torch.Tensor] = None, a_rows: Optional[torch.Tensor] = None,
+                 rows: Optional[int] = None) -> torch.Tensor:
+        """Grouped expert FFN over expert-major rows (optionally gathered through ``a_rows``)."""
+        if self.fp8:
+            gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows, a_scale=scale, w_scale=L.s13)
+            aq, as_ = ops.quant_fp8_rows(ops.silu_mul(gu))
+            return ops.grouped_gemm(aq, L.w2, row_off, a_scale=as_, w_scale=L.s2)
+        gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows)
+        return ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)
+
+    def _mlp_ep(self, h: torch.Tensor, L: MoELayerWeights) -> torch.Tensor:
+        """EP MoE layer: route locally, dispatch rows to the expert owners, combine locally."""
+        k = self.full_cfg.experts_per_token
+        _ids, w, row_off, src, inv = ops.moe_route(F.linear(h, L.router), k)
+        idx = src.long()
+        if self.fp8:
+            hq, hs = ops.quant_fp8_rows(h)
+            xs = hq.view(torch.uint8)[idx].view(torch.float8_e4m3fn)  # e4m3 rows gathered as bytes
+            ss = hs[idx]
+        else:
+            xs, ss = h[idx], None
+        cap = None if self.ep_capacity is None else self.ep_capacity * k
+        y = self.ep.run(xs, row_off, lambda xl, ro, sl: self._experts(xl, ro, L, sl), x_scale=ss, capacity=cap)
+        return ops.moe_combine(y.contiguous(), inv, w, k)
+
     def _mlp(self, h: torch.Tensor, L: MoELayerWeights) -> torch.Tensor:
+        if self.ep is not None:
+            return self._mlp_ep(h, L)
         k = self.full_cfg.experts_per_token
         logits = F.linear(h, L.router)
         _ids, w, row_off, src, inv = ops.moe_route(logits, k)
         rows = h.shape[0] * k
         if self.fp8:
             hq, hs = ops.quant_fp8_rows(h)
-            gu = ops.grouped_gemm(hq, L.w13, row_off, a_rows=src, rows=rows, a_scale=hs, w_scale=L.s13)
-            act = ops.silu_mul(gu)
-            aq, as_ = ops.quant_fp8_rows(act)
-            y = ops.grouped_gemm(aq, L.w2, row_off, a_scale=as_, w_scale=L.s2)
+            y = self._experts(hq, row_off, L, hs, a_rows=src, rows=rows)
         else:
-            gu = ops.grouped_gemm(h, L.w13, row_off, a_rows=src, rows=rows)
-            y = ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)
+            y = self._experts(h, row_off, L, a_rows=src, rows=rows)
         return self._all_reduce(ops.moe_combine(y, inv, w, k))

@@ -6,6 +6,7 @@ code runs over gloo.  Collectives used by the serving/bench paths (SURVEY.md §2
   C1 all_gather of candidate embeddings  [n_local, d] -> [world, n_local, d]
   C2 gather of votes / tallies           (tiny, latency-bound)
   C3 TP all-reduce                       (tensor-parallel decoders)
+  C4 all_to_all_single                   (expert-parallel MoE dispatch / combine, parallel/expert.py)
   C5 broadcast / barrier                 (control)
 
 xGMI on MI355X is point-to-point (7 links per GPU): the payloads here are small (an all-gather of
@@ -98,6 +99,36 @@ def all_gather_flat(t: torch.Tensor, group=None) -> torch.Tensor:
     out = torch.empty(W * flat.numel(), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, flat, group=group)
     return out.view(W, *t.shape)
+
+
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None,
+                      group=None) -> torch.Tensor:
+    """All-to-all along dim 0 (C4, expert-parallel dispatch/combine): equal splits when the split lists
+    are None.  GPU tensors under gloo are staged through host memory (one-GPU rehearsal mode)."""
+    if not _INFO.enabled:
+        out.copy_(inp)
+        return out
+    if _INFO.backend == "gloo":
+        # host staging; dtypes gloo does not reduce over (bf16, fp8) travel as raw bytes per row
+        h_in = inp.detach().cpu().contiguous()
+        h = torch.empty(out.shape, dtype=out.dtype)
+        if h_in.dtype not in (torch.float32, torch.float64, torch.int32, torch.int64, torch.uint8):
+            row = 1
+            for n in h_in.shape[1:]:
+                row *= n
+            bi = h_in.reshape(h_in.shape[0], row).view(torch.uint8)
+            bo = h.view(h.shape[0], row).view(torch.uint8)
+            dist.all_to_all_single(bo, bi, out_splits, in_splits, group=group)
+        else:
+            dist.all_to_all_single(h, h_in, out_splits, in_splits, group=group)
+        out.copy_(h)
+        return out
+    if inp.dtype == torch.float8_e4m3fn:  # e4m3 rows travel as bytes
+        dist.all_to_all_single(out.view(torch.uint8), inp.contiguous().view(torch.uint8), out_splits, in_splits,
+                               group=group)
+        return out
+    dist.all_to_all_single(out, inp.contiguous(), out_splits, in_splits, group=group)
+    return out
 
 
 def all_gather(t: torch.Tensor, group=None) -> torch.Tensor:

@@ -75,3 +75,57 @@ def test_mixtral_tp2_matches_tp1(gpu, fp8):
         c = torch.nn.functional.cosine_similarity(res[r], lg, dim=0).item()
         assert c > 0.99, (r, c)
     assert torch.equal(res[0], res[1])  # ranks agree exactly (replicated after the all-reduce)
+
+
+def _ep_worker(rank, world, port, fp8, mode, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.llama import KVCache
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
+                         ep_rank=rank, ep_size=world, ep_mode=mode, ep_capacity=64 if mode == "padded" else None)
+        q.put((rank, _prefill_logits(m, dev, P=23 + 9 * rank, seed=rank)))  # each rank its own prompt
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def _prefill_logits(m, dev, P, seed):
+    from llm_weighted_consensus_amd.models.llama import KVCache
+
+    g = torch.Generator().manual_seed(100 + seed)
+    toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(dev)
+    cache = KVCache(m.cfg, 8, 16, dev)
+    ar = torch.arange(P, dtype=torch.int32, device=dev)
+    return m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=dev), P,
+                     torch.tensor([P - 1], device=dev), cache)[0].float().cpu()
+
+
+@pytest.mark.parametrize("fp8,mode", [(False, "padded"), (True, "padded"), (False, "exact")])
+def test_mixtral_ep2_matches_ep1(gpu, fp8, mode):
+    """Expert parallelism (C4): two EP ranks (2 of mixtral-tiny's 4 experts each, full FFN width), each
+    prefilling a DIFFERENT prompt, give the logits a single-rank model computes for that prompt."""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ep_worker, args=(r, 2, port, fp8, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    assert all(isinstance(v, torch.Tensor) for v in res.values()), res
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512, fp8=fp8)
+    for r in range(2):
+        ref = _prefill_logits(m, gpu, P=23 + 9 * r, seed=r)
+        c = torch.nn.functional.cosine_similarity(res[r], ref, dim=0).item()
+        assert c > 0.999, (r, c)
