@@ -3,25 +3,41 @@
 Produces the reference's `CreateEmbeddingResponse` (src/embeddings/response.rs:4-30).  Texts are
 byte-tokenized into the encoder vocabulary (no tokenizer downloads here), packed varlen (no padding
 FLOPs) and run through the gfx950 encoder kernels on a dedicated HIP stream so embedding work can
-overlap the decode engine on the same GPU.
+overlap the decode engine on the same GPU.  Embeddings are kept in an HBM-resident, content-addressed
+archive (`archive/hbm.py`, ``LWC_EMBED_CACHE_MB``): a text the encoder has already seen on this GPU is
+gathered from the slab instead of re-encoded.
 """
 from __future__ import annotations
 
+import os
 import threading
-from typing import List, Sequence, Tuple, Union
+from typing import List, Optional, Sequence, Tuple, Union
 
 import torch
 
+from ..archive.hbm import ResidentEmbeddings
 from ..schema import chat as C
 from ..schema import score as S
 
 
 class EmbeddingService:
-    def __init__(self, encoder, name: str):
+    def __init__(self, encoder, name: str, cache_mb: Optional[float] = None):
         self.encoder = encoder
         self.name = name
         self.lock = threading.Lock()
         self.stream = torch.cuda.Stream(device=encoder.device) if encoder.device.type == "cuda" else None
+        if cache_mb is None:
+            cache_mb = float(os.environ.get("LWC_EMBED_CACHE_MB", "4096" if self.stream is not None else "64"))
+        self.cache = (ResidentEmbeddings(encoder.cfg.hidden, encoder.device, int(cache_mb * 2**20))
+                      if cache_mb > 0 else None)
+
+    def _encode(self, lists: Sequence[Sequence[int]], max_tokens: int) -> torch.Tensor:
+        if self.stream is not None:
+            with torch.cuda.stream(self.stream):
+                f32, _ = self.encoder.embed(lists, max_tokens)
+            self.stream.synchronize()
+            return f32
+        return self.encoder.embed(lists, max_tokens)[0]
 
     def tokenize(self, text: str) -> List[int]:
         V = self.encoder.cfg.vocab_size
@@ -29,12 +45,10 @@ class EmbeddingService:
 
     def embed_token_lists(self, lists: Sequence[Sequence[int]], max_tokens: int = 512) -> Tuple[torch.Tensor, int]:
         with self.lock:
-            if self.stream is not None:
-                with torch.cuda.stream(self.stream):
-                    f32, _ = self.encoder.embed(lists, max_tokens)
-                self.stream.synchronize()
+            if self.cache is not None:
+                f32, _ = self.cache.embed_through(lists, max_tokens, lambda miss: self._encode(miss, max_tokens))
             else:
-                f32, _ = self.encoder.embed(lists, max_tokens)
+                f32 = self._encode(lists, max_tokens)
         ntok = sum(min(len(l), max_tokens, self.encoder.cfg.max_position) for l in lists)
         return f32, ntok
 

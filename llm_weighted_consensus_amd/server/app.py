@@ -59,6 +59,11 @@ class Metrics:
             if hasattr(svc, "alive"):
                 lines.append(f'lwc_engine_workers_alive{{model="{name}"}} {sum(svc.alive)}')
             lines.append(f'lwc_engine_failures_total{{model="{name}"}} {svc.failures}')
+        for name, svc in (state.embedders or {}).items():
+            cache = getattr(svc, "cache", None)
+            if cache is not None:
+                for k, v in cache.stats().items():
+                    lines.append(f'lwc_embed_cache_{k}{{model="{name}"}} {v}')
         lines.append(f"lwc_uptime_seconds {time.time() - self.t0:.1f}")
         if torch_cuda_ok():
             import torch
