@@ -37,6 +37,8 @@ struct PrefillParams {
   const bf16_t* v;
   bf16_t* out;
   const int* cu_seqlens;
+  const int* cu_seqlens_k;  // null: keys = queries; else sequence s attends keys [cu_k[s], cu_k[s+1]) and its
+                            // queries are the LAST len_q of those positions (cached-prefix prefill)
   int q_stride, k_stride, v_stride, o_stride;  // elements per token row
   int Hq, Hkv, nseq, max_tiles;
   float scale;
@@ -58,6 +60,10 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   const int s0 = p.cu_seqlens[seq], len = p.cu_seqlens[seq + 1] - s0;
   const int q0 = qtile * kQT;
   if (q0 >= len) return;  // whole workgroup exits together (uniform)
+  // keys: the sequence's own rows, or (cached prefix) a longer key range whose last len rows are the queries
+  const int ks0 = p.cu_seqlens_k ? p.cu_seqlens_k[seq] : s0;
+  const int klen = p.cu_seqlens_k ? p.cu_seqlens_k[seq + 1] - ks0 : len;
+  const int qoff = klen - len;  // key position of query row 0
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int qrow = q0 + wid * 16 + r16;  // this lane's query (as B-operand column)
@@ -72,7 +78,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   const float sl2 = p.scale * 1.4426950408889634f;
 
   const int q_last = min(len, q0 + kQT) - 1;
-  const int kv_end = p.causal ? q_last + 1 : len;
+  const int kv_end = p.causal ? q_last + 1 + qoff : klen;
   const int ntiles = (kv_end + kKT - 1) / kKT;
 
   // staging registers
@@ -83,9 +89,9 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       const int c = threadIdx.x + 256 * i;
       const int row = c / CPR, ch = c % CPR;
       const int key = tile * kKT + row;
-      if (c < CHUNKS && key < len) {
-        stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(s0 + key) * p.k_stride + kvh * D + ch * 8);
-        stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(s0 + key) * p.v_stride + kvh * D + ch * 8);
+      if (c < CHUNKS && key < klen) {
+        stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(ks0 + key) * p.k_stride + kvh * D + ch * 8);
+        stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(ks0 + key) * p.v_stride + kvh * D + ch * 8);
       } else {
         stk[i] = uint4v{0, 0, 0, 0};
         stv[i] = uint4v{0, 0, 0, 0};
@@ -136,8 +142,8 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ka_ = t * kKT + 4 * g + r, kb_ = ka_ + 16;
-      const bool va = ka_ < len && (!p.causal || ka_ <= qrow);
-      const bool vbk = kb_ < len && (!p.causal || kb_ <= qrow);
+      const bool va = ka_ < klen && (!p.causal || ka_ <= qrow + qoff);
+      const bool vbk = kb_ < klen && (!p.causal || kb_ <= qrow + qoff);
       pa[r] = va ? sa[r] * sl2 : -INFINITY;
       pb[r] = vbk ? sb[r] * sl2 : -INFINITY;
       mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
@@ -218,13 +224,14 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
 }  // namespace lwc
 
 extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v, void* out, const int* cu_seqlens,
-                                     int nseq, int max_seqlen, int q_stride, int k_stride, int v_stride, int o_stride,
+                                     const int* cu_seqlens_k, int nseq, int max_seqlen, int q_stride, int k_stride, int v_stride, int o_stride,
                                      int Hq, int Hkv, int D, float scale, int causal, hipStream_t s) {
   using namespace lwc;
   if (Hq % Hkv != 0) return -1;
   if (nseq == 0 || max_seqlen == 0) return 0;
   const int max_tiles = (max_seqlen + kQT - 1) / kQT;
-  PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)out, cu_seqlens, q_stride, k_stride,
+  PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)out, cu_seqlens, cu_seqlens_k,
+                  q_stride, k_stride,
                   v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal};
   dim3 grid(nseq * max_tiles, Hq);
   if (D == 128)

@@ -31,7 +31,7 @@ int lwc_gemm8p_slots();
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
-int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, int, int, int, int, int, int, int,
+int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
                const float*, const float*, const float*, void*, const int*, const float*, const int*,
@@ -383,10 +383,19 @@ void quant_fp8_rows(const at::Tensor& x, at::Tensor& q, at::Tensor& scale) {
 
 void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                        const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, int64_t D,
-                       double scale, bool causal) {
-  // q/k/v: [T, *] 2-D views with unit inner stride (slices of the fused qkv row); out: [T, Hq*D]
+                       double scale, bool causal, const c10::optional<at::Tensor>& cu_seqlens_k) {
+  // q/k/v: [T, *] 2-D views with unit inner stride (slices of the fused qkv row); out: [T, Hq*D].
+  // cu_seqlens_k (optional): per-sequence key ranges in k/v, each at least as long as the sequence's query
+  // range (the caller checks the lengths on the host; queries are the last rows of the key range).
   CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
   CHECK_DTYPE(cu_seqlens, at::kInt);
+  const int* cuk = nullptr;
+  if (cu_seqlens_k.has_value()) {
+    CHECK_DTYPE((*cu_seqlens_k), at::kInt);
+    TORCH_CHECK(cu_seqlens_k->numel() == cu_seqlens.numel(), "prefill_attention: cu_seqlens_k size mismatch");
+    TORCH_CHECK(k.size(0) == v.size(0), "prefill_attention: k/v row mismatch");
+    cuk = cu_seqlens_k->data_ptr<int>();
+  }
   TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.dim() == 2 && out.dim() == 2, "prefill_attention: 2-D views expected");
   TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1 && out.stride(1) == 1,
               "prefill_attention: unit inner stride");
@@ -394,7 +403,7 @@ void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tenso
               "prefill_attention: head shape mismatch");
   const int nseq = (int)cu_seqlens.numel() - 1;
   CHECK_RC(lwc_prefill_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), cu_seqlens.data_ptr<int>(),
-                                 nseq, (int)max_seqlen, (int)q.stride(0), (int)k.stride(0), (int)v.stride(0),
+                                 cuk, nseq, (int)max_seqlen, (int)q.stride(0), (int)k.stride(0), (int)v.stride(0),
                                  (int)out.stride(0), (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0,
                                  cur_stream()),
            "prefill_attention");

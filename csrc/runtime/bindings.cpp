@@ -136,6 +136,13 @@ PYBIND11_MODULE(_runtime, m) {
       .def("append_token", &BlockManager::append_token)
       .def("append_cost", &BlockManager::append_cost)
       .def("free_sequence", &BlockManager::free_sequence)
+      .def("set_prefix_caching", &BlockManager::set_prefix_caching)
+      .def_property_readonly("prefix_caching", &BlockManager::prefix_caching)
+      .def("match_prefix", &BlockManager::match_prefix)
+      .def("add_sequence_cached", &BlockManager::add_sequence_cached)
+      .def("cache_prefix", &BlockManager::cache_prefix)
+      .def_property_readonly("num_cached_blocks", &BlockManager::num_cached_blocks)
+      .def_property_readonly("num_evictable", &BlockManager::num_evictable)
       .def("length", &BlockManager::length)
       .def("block_table", &BlockManager::block_table)
       .def("slot", &BlockManager::slot)

@@ -1,5 +1,6 @@
 #include "block_manager.h"
 
+#include <algorithm>
 #include <string>
 
 namespace lwc {
@@ -24,16 +25,142 @@ BlockManager::Seq& BlockManager::get(int64_t seq) {
 }
 
 int32_t BlockManager::alloc_block() {
-  if (free_.empty()) throw std::runtime_error("BlockManager: out of KV blocks");
-  const int32_t b = free_.back();
-  free_.pop_back();
+  int32_t b;
+  if (!free_.empty()) {
+    b = free_.back();
+    free_.pop_back();
+  } else if (!lru_.empty()) {  // reclaim the least recently used cached block
+    b = lru_.front();
+    lru_.pop_front();
+    unregister(b);
+  } else {
+    throw std::runtime_error("BlockManager: out of KV blocks");
+  }
   ref_[b] = 1;
   return b;
 }
 
 void BlockManager::release(int32_t block) {
   if (ref_[block] <= 0) throw std::logic_error("BlockManager: double free of block " + std::to_string(block));
-  if (--ref_[block] == 0) free_.push_back(block);
+  if (--ref_[block] == 0) {
+    if (registered_.size() && registered_[block])
+      lru_pos_[block] = lru_.insert(lru_.end(), block);  // stays resident until the pool needs it
+    else
+      free_.push_back(block);
+  }
+}
+
+void BlockManager::acquire_cached(int32_t block) {
+  if (ref_[block] == 0) lru_.erase(lru_pos_[block]);
+  ++ref_[block];
+}
+
+void BlockManager::unregister(int32_t block) {
+  if (!registered_[block]) return;
+  auto it = by_key_.find(key_[block]);
+  if (it != by_key_.end() && it->second == block) by_key_.erase(it);
+  registered_[block] = 0;
+}
+
+static inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ULL;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+static constexpr uint64_t kRootKey = 0x243f6a8885a308d3ULL;
+
+uint64_t BlockManager::chain_key(uint64_t parent, const int32_t* toks) const {
+  uint64_t h = mix64(parent ^ 0x6a09e667f3bcc909ULL);
+  for (int i = 0; i < block_size_; ++i) h = mix64(h ^ ((uint64_t)(uint32_t)toks[i] << 1 | 1ULL) ^ (uint64_t)i << 40);
+  return h;
+}
+
+void BlockManager::set_prefix_caching(bool on) {
+  if (on && registered_.empty()) {
+    key_.assign(num_blocks_, 0);
+    parent_key_.assign(num_blocks_, 0);
+    registered_.assign(num_blocks_, 0);
+    block_tokens_.assign((size_t)num_blocks_ * block_size_, 0);
+    lru_pos_.resize(num_blocks_);
+  }
+  if (!on) {  // drop the cache: unreferenced cached blocks go back to the free list
+    for (int32_t b : lru_) free_.push_back(b);
+    lru_.clear();
+    by_key_.clear();
+    std::fill(registered_.begin(), registered_.end(), 0);
+  }
+  prefix_caching_ = on;
+}
+
+std::vector<int32_t> BlockManager::match_blocks(const std::vector<int32_t>& tokens, int64_t max_blocks) const {
+  std::vector<int32_t> out;
+  if (!prefix_caching_) return out;
+  uint64_t parent = kRootKey;
+  for (int64_t i = 0; i < max_blocks; ++i) {
+    const int32_t* t = tokens.data() + i * block_size_;
+    const uint64_t k = chain_key(parent, t);
+    auto it = by_key_.find(k);
+    if (it == by_key_.end()) break;
+    const int32_t b = it->second;
+    if (parent_key_[b] != parent ||
+        !std::equal(t, t + block_size_, block_tokens_.begin() + (size_t)b * block_size_))
+      break;  // hash collision: treat as a miss
+    out.push_back(b);
+    parent = k;
+  }
+  return out;
+}
+
+int64_t BlockManager::match_prefix(const std::vector<int32_t>& tokens) const {
+  if (tokens.empty()) return 0;
+  return (int64_t)match_blocks(tokens, ((int64_t)tokens.size() - 1) / block_size_).size() * block_size_;
+}
+
+int64_t BlockManager::add_sequence_cached(int64_t seq, const std::vector<int32_t>& tokens) {
+  if (seqs_.count(seq)) throw std::invalid_argument("BlockManager: sequence exists " + std::to_string(seq));
+  const int64_t n = (int64_t)tokens.size();
+  const std::vector<int32_t> hit = match_blocks(tokens, n > 0 ? (n - 1) / block_size_ : 0);
+  const int need = blocks_for(n) - (int)hit.size();
+  // the matched blocks may sit in the LRU list: taking them must not count them as allocatable
+  int in_lru = 0;
+  for (int32_t b : hit) in_lru += ref_[b] == 0;
+  if (num_free() - in_lru < need) throw std::runtime_error("BlockManager: out of KV blocks");
+  Seq s;
+  s.blocks.reserve(blocks_for(n) + 8);
+  for (int32_t b : hit) {
+    acquire_cached(b);
+    s.blocks.push_back(b);
+  }
+  for (int i = 0; i < need; ++i) s.blocks.push_back(alloc_block());
+  s.len = n;
+  seqs_.emplace(seq, std::move(s));
+  return (int64_t)hit.size() * block_size_;
+}
+
+void BlockManager::cache_prefix(int64_t seq, const std::vector<int32_t>& tokens) {
+  if (!prefix_caching_) return;
+  const Seq& s = get(seq);
+  const int64_t full = std::min<int64_t>((int64_t)tokens.size(), s.len) / block_size_;
+  uint64_t parent = kRootKey;
+  for (int64_t i = 0; i < full && i < (int64_t)s.blocks.size(); ++i) {
+    const int32_t b = s.blocks[i];
+    const int32_t* t = tokens.data() + i * block_size_;
+    const uint64_t k = chain_key(parent, t);
+    if (!registered_[b]) {
+      auto it = by_key_.find(k);
+      if (it == by_key_.end()) {  // first copy of this prefix block: register it
+        registered_[b] = 1;
+        key_[b] = k;
+        parent_key_[b] = parent;
+        std::copy(t, t + block_size_, block_tokens_.begin() + (size_t)b * block_size_);
+        by_key_.emplace(k, b);
+      }
+    }
+    parent = k;
+  }
 }
 
 void BlockManager::add_sequence(int64_t seq, int64_t num_tokens) {

@@ -9,6 +9,7 @@
 // Sized for 288 GB of HBM3E: block ids are int32 (2^31 blocks x 16 tokens), sequence ids int64.
 #pragma once
 #include <cstdint>
+#include <list>
 #include <stdexcept>
 #include <unordered_map>
 #include <utility>
@@ -22,13 +23,14 @@ class BlockManager {
 
   int num_blocks() const { return num_blocks_; }
   int block_size() const { return block_size_; }
-  int num_free() const { return (int)free_.size(); }
+  // free blocks + unreferenced prefix-cache blocks (reclaimed on demand, least recently used first)
+  int num_free() const { return (int)(free_.size() + lru_.size()); }
   int num_sequences() const { return (int)seqs_.size(); }
   bool has_sequence(int64_t seq) const { return seqs_.count(seq) != 0; }
 
   // Blocks needed to hold `num_tokens` tokens for a new sequence.
   int blocks_for(int64_t num_tokens) const { return (int)((num_tokens + block_size_ - 1) / block_size_); }
-  bool can_allocate(int num_blocks) const { return (int)free_.size() >= num_blocks; }
+  bool can_allocate(int num_blocks) const { return num_free() >= num_blocks; }
 
   // Allocate a new sequence able to hold `num_tokens` tokens (its length is set to num_tokens).
   void add_sequence(int64_t seq, int64_t num_tokens);
@@ -50,6 +52,25 @@ class BlockManager {
   // Copy-on-write copies queued since the last call (src, dst); cleared by this call.
   std::vector<std::pair<int32_t, int32_t>> take_copies();
 
+  // ---- automatic prefix caching (cross-request KV reuse) ----
+  // A FULL prompt block can be registered under a chain key: key_i = H(key_{i-1}, the block's BS token
+  // ids), key_{-1} = a root constant, so a key names the whole token prefix up to that block.  A later
+  // sequence whose prompt starts with the same tokens takes those blocks by reference instead of
+  // recomputing them; every match also compares the block's stored tokens and parent key.  Registered
+  // blocks that no sequence references stay resident in an LRU list and are reclaimed only when the pool
+  // runs dry, so the cache costs no capacity.  Disabled by default.
+  void set_prefix_caching(bool on);
+  bool prefix_caching() const { return prefix_caching_; }
+  // Prompt tokens a new sequence would take from the cache: a multiple of BS, and at most
+  // tokens.size() - 1 (the last prompt token is always computed: its logits start decoding).
+  int64_t match_prefix(const std::vector<int32_t>& tokens) const;
+  // add_sequence(seq, tokens.size()) reusing the cached prefix blocks; returns the reused token count.
+  int64_t add_sequence_cached(int64_t seq, const std::vector<int32_t>& tokens);
+  // Register the sequence's blocks that `tokens` (its prompt) fills completely.
+  void cache_prefix(int64_t seq, const std::vector<int32_t>& tokens);
+  int num_cached_blocks() const { return (int)by_key_.size(); }
+  int num_evictable() const { return (int)lru_.size(); }
+
  private:
   struct Seq {
     std::vector<int32_t> blocks;
@@ -59,10 +80,23 @@ class BlockManager {
   Seq& get(int64_t seq);
   int32_t alloc_block();
   void release(int32_t block);
+  void acquire_cached(int32_t block);
+  void unregister(int32_t block);
+  uint64_t chain_key(uint64_t parent, const int32_t* toks) const;
+  // walk the cached chain of `tokens`; returns matched block ids (<= max_blocks of them)
+  std::vector<int32_t> match_blocks(const std::vector<int32_t>& tokens, int64_t max_blocks) const;
 
   int num_blocks_, block_size_;
   std::vector<int32_t> free_;
   std::vector<int32_t> ref_;
+  // prefix cache
+  bool prefix_caching_ = false;
+  std::unordered_map<uint64_t, int32_t> by_key_;
+  std::vector<uint64_t> key_, parent_key_;       // per block (valid when registered_[b])
+  std::vector<char> registered_;
+  std::vector<int32_t> block_tokens_;            // [num_blocks * BS] token ids of registered blocks
+  std::list<int32_t> lru_;                       // unreferenced registered blocks, oldest first
+  std::vector<std::list<int32_t>::iterator> lru_pos_;
   std::unordered_map<int64_t, Seq> seqs_;
   std::vector<std::pair<int32_t, int32_t>> copies_;
 };

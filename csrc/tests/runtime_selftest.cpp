@@ -3,6 +3,7 @@
 // block allocation / fork / copy-on-write / free churn, the key tree for many choice counts, vote
 // extraction with and without logprobs, tally and error unification.  Exit code 0 = pass; ASan/UBSan
 // abort on any memory or UB error.  Driven by tests/test_native_sanitizers.py.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -50,6 +51,49 @@ static void block_manager_churn() {
   for (int64_t s : live) bm.free_sequence(s);
   CHECK(bm.num_free() == 512);
   CHECK(bm.num_sequences() == 0);
+}
+
+// prefix cache: prompts drawn from a few shared stems so blocks are reused, resurrected from the LRU
+// list and evicted under pressure; every reused block must hold the same tokens as the new prompt
+static void prefix_cache_churn() {
+  lwc::BlockManager bm(256, 16);
+  bm.set_prefix_caching(true);
+  std::mt19937 rng(11);
+  std::vector<std::vector<int32_t>> stems(6);
+  for (auto& st : stems)
+    for (int i = 0; i < 80; ++i) st.push_back((int32_t)(rng() % 1000));
+  std::vector<std::pair<int64_t, std::vector<int32_t>>> live;
+  int64_t next = 1;
+  for (int it = 0; it < 5000; ++it) {
+    if (rng() % 3 != 0 || live.empty()) {
+      std::vector<int32_t> p = stems[rng() % stems.size()];
+      p.resize(1 + rng() % p.size());
+      for (int i = (int)(rng() % 20); i > 0; --i) p.push_back((int32_t)(rng() % 1000));
+      const int need = bm.blocks_for((int64_t)p.size());
+      if (!bm.can_allocate(need)) {
+        const size_t i = rng() % live.size();
+        bm.free_sequence(live[i].first);
+        live.erase(live.begin() + i);
+        continue;
+      }
+      const int64_t c = bm.add_sequence_cached(next, p);
+      CHECK(c % 16 == 0 && c < (int64_t)p.size());
+      const auto& tab = bm.block_table(next);
+      for (auto& lv : live)  // a shared block means a shared token prefix up to that block
+        for (int64_t b = 0; b < c / 16 && b < (int64_t)bm.block_table(lv.first).size(); ++b)
+          if (bm.block_table(lv.first)[b] == tab[b])
+            CHECK(std::equal(p.begin(), p.begin() + (b + 1) * 16, lv.second.begin()));
+      bm.cache_prefix(next, p);
+      live.emplace_back(next++, p);
+    } else {
+      const size_t i = rng() % live.size();
+      bm.free_sequence(live[i].first);
+      live.erase(live.begin() + i);
+    }
+  }
+  for (auto& lv : live) bm.free_sequence(lv.first);
+  CHECK(bm.num_free() == 256);
+  CHECK(bm.num_evictable() == bm.num_cached_blocks());
 }
 
 static void key_tree_and_votes() {
@@ -103,6 +147,7 @@ static void tally_and_codes() {
 
 int main() {
   block_manager_churn();
+  prefix_cache_churn();
   key_tree_and_votes();
   tally_and_codes();
   std::puts("runtime selftest ok");

@@ -243,7 +243,8 @@ class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
                  use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
-                 cascade_min_batch: int = 128, tune_gc: bool = True, constrained_logprobs: bool = False):
+                 cascade_min_batch: int = 128, tune_gc: bool = True, constrained_logprobs: bool = False,
+                 prefix_caching: bool = False):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -259,6 +260,11 @@ class LLMEngine:
             num_blocks = max(64, int(free * kv_memory_fraction) // per)
         self.cache = KVCache(self.cfg, num_blocks, block_size, self.device)
         self.bm = BlockManager(num_blocks, block_size)
+        # cross-request prefix cache (C++ block manager): prompts that start with an already computed
+        # token prefix (the shared messages of a score request's voters, a repeated conversation) reuse
+        # its full KV blocks and prefill only the tail
+        self.prefix_caching = prefix_caching
+        self.bm.set_prefix_caching(prefix_caching)
         self.free_blocks_unreserved = num_blocks
         self.use_graphs = use_graphs
         self.prefix_sharing = prefix_sharing
@@ -280,7 +286,7 @@ class LLMEngine:
         self.free_count_rows = list(range(max_batch))
         self.bias: Optional[torch.Tensor] = None    # [max_batch, V] f32, lazily
         self.free_bias_rows = list(range(max_batch))
-        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0}
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_cache_tokens": 0}
         self.faults = FaultInjector.from_env()
         # step() returns TokenEvents only when asked (callbacks always get theirs)
         self.collect_events = False
@@ -379,26 +385,42 @@ class LLMEngine:
         return out
 
     # ------------------------------------------------------------------ prefill
-    def _run_prefill(self, prompts: List[List[int]], parents: List[int]) -> torch.Tensor:
+    def _run_prefill(self, prompts: List[List[int]], parents: List[int], use_cache: bool = False) -> torch.Tensor:
         """Prefill packed prompts into freshly added transient sequences `parents`; returns the
-        last-token logits [len(prompts), V]."""
+        last-token logits [len(prompts), V].  With ``use_cache`` the prompts' cached prefix blocks are
+        taken from the prefix cache and only the tails are computed (attention still sees the whole
+        prompt), and the prompts' full blocks are registered for later requests."""
         dev = self.device
-        toks, pos, slots, cu, last = [], [], [], [0], []
+        toks, pos, slots, cu, last, cached = [], [], [], [0], [], []
         for pid, p in zip(parents, prompts):
             L = len(p)
-            self.bm.add_sequence(pid, L)
-            toks.extend(p)
-            pos.extend(range(L))
-            slots.append(slots_range(self.bm, pid, 0, L))
-            cu.append(cu[-1] + L)
+            c = int(self.bm.add_sequence_cached(pid, p)) if use_cache else 0
+            if not use_cache:
+                self.bm.add_sequence(pid, L)
+            cached.append(c)
+            toks.extend(p[c:])
+            pos.extend(range(c, L))
+            slots.append(slots_range(self.bm, pid, c, L - c))
+            cu.append(cu[-1] + L - c)
             last.append(cu[-1] - 1)
+        ctx = None
+        if any(cached):
+            k_lens = [len(p) for p in prompts]
+            ctx = {"k_slots": torch.from_numpy(np.concatenate([slots_range(self.bm, pid, 0, L)
+                                                               for pid, L in zip(parents, k_lens)]).astype(np.int64)).to(dev),
+                   "cu_k": torch.tensor(np.concatenate([[0], np.cumsum(k_lens)]), dtype=torch.int32, device=dev),
+                   "q_lens": [L - c for L, c in zip(k_lens, cached)], "k_lens": k_lens}
+            self.stats["prefix_cache_tokens"] += sum(cached)
         t_tok = torch.tensor(toks, dtype=torch.int32, device=dev)
         t_pos = torch.tensor(pos, dtype=torch.int32, device=dev)
         t_slots = torch.from_numpy(np.concatenate(slots)).to(dev)
         t_cu = torch.tensor(cu, dtype=torch.int32, device=dev)
         t_last = torch.tensor(last, dtype=torch.int64, device=dev)
-        max_len = max(len(p) for p in prompts)
-        logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache)
+        max_len = max(len(p) - c for p, c in zip(prompts, cached))
+        logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache, ctx=ctx)
+        if use_cache:
+            for pid, p in zip(parents, prompts):
+                self.bm.cache_prefix(pid, p)
         self.stats["prefill_tokens"] += len(toks)
         return logits
 
@@ -435,7 +457,8 @@ class LLMEngine:
         imported = [g for g in groups if g.prefilled is not None]
         logits_of: Dict[int, torch.Tensor] = {}
         if compute:
-            lg = self._run_prefill([g.prompt_ids for g in compute], [-g.id for g in compute])
+            lg = self._run_prefill([g.prompt_ids for g in compute], [-g.id for g in compute],
+                                   use_cache=self.prefix_caching)
             for i, g in enumerate(compute):
                 logits_of[g.id] = lg[i]
         for g in imported:

@@ -294,7 +294,8 @@ class EngineGroup:
 
 def build_engine(spec: dict, wid: int):
     """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
-    ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8"})."""
+    ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8",
+    "prefix_caching", "constrained_logprobs"}); MoE archs get the Mixtral model."""
     import torch
 
     from ..models.config import decoder_config
@@ -317,4 +318,6 @@ def build_engine(spec: dict, wid: int):
         model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
     tok = ByteTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
     return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
-                     kv_memory_fraction=float(spec.get("kv_fraction", 0.85)))
+                     kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),
+                     prefix_caching=bool(spec.get("prefix_caching", True)),
+                     constrained_logprobs=bool(spec.get("constrained_logprobs", False)))

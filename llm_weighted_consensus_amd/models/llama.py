@@ -304,14 +304,24 @@ class LlamaModel:
         return self._layers(x, null, positions, None, attn_fn)
 
     def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cu_seqlens: torch.Tensor,
-                max_seqlen: int, last_idx: torch.Tensor, cache: KVCache) -> torch.Tensor:
-        """Prefill packed prompts (cu_seqlens) -> logits of each sequence's last token [nseq, V]."""
+                max_seqlen: int, last_idx: torch.Tensor, cache: KVCache, ctx: Optional[dict] = None) -> torch.Tensor:
+        """Prefill packed prompts (cu_seqlens) -> logits of each sequence's last token [nseq, V].
+
+        ``ctx`` (cross-request prefix cache): the packed tokens are only each prompt's UNCACHED tail and
+        attention also needs the cached head.  ctx = {k_slots [sum klen] int64: cache slots of every
+        position of each prompt (cached + new), cu_k [nseq+1] int32, q_lens, k_lens (host lists)}; per
+        layer, after the new rows are written, the whole key range is gathered from the paged cache and
+        the varlen kernel runs with queries at the end of each key range."""
         cfg = self.cfg
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
         x = ops.embedding(self.embed, tokens)
 
         def attn_fn(qkv, li):
             q = qkv[:, : Hq * D]
+            if ctx is not None:
+                kf, vf = ops.kv_gather(cache.k[li], cache.v[li], ctx["k_slots"])
+                return ops.prefill_attention(q, kf, vf, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True,
+                                             cu_seqlens_k=ctx["cu_k"], lens=(ctx["q_lens"], ctx["k_lens"]))
             k = qkv[:, Hq * D:(Hq + Hkv) * D]
             v = qkv[:, (Hq + Hkv) * D:]
             return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)

@@ -12,7 +12,7 @@ Layout conventions shared with the engine:
 from __future__ import annotations
 
 import importlib
-from typing import Optional
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -175,13 +175,34 @@ def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.
 
 def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int,
                       Hq: int, Hkv: int, D: int, scale: float, causal: bool,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Varlen flash attention forward (K4 causal / K9c bidirectional); q,k,v are [T, H*D] views."""
+                      out: Optional[torch.Tensor] = None, cu_seqlens_k: Optional[torch.Tensor] = None,
+                      lens: Optional[Tuple[Sequence[int], Sequence[int]]] = None) -> torch.Tensor:
+    """Varlen flash attention forward (K4 causal / K9c bidirectional); q,k,v are [T, H*D] views.
+    ``cu_seqlens_k``: k/v hold their own per-sequence ranges (cached-prefix prefill: each sequence's
+    queries are the LAST rows of its key range, causal with that offset); ``lens`` = the host-side
+    (q lengths, k lengths), checked here before the launch."""
     if out is None:
         out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    if cu_seqlens_k is not None:
+        if lens is None:
+            raise ValueError("prefill_attention: cu_seqlens_k needs the host-side lengths")
+        ql, kl = lens
+        if len(ql) != len(kl) or any(a > b for a, b in zip(ql, kl)) or sum(kl) > k.shape[0] or sum(ql) > q.shape[0]:
+            raise ValueError("prefill_attention: key ranges must cover their queries and fit k/v")
     kernels().prefill_attention(q, k, v, out, cu_seqlens, int(max_seqlen), int(Hq), int(Hkv), int(D), float(scale),
-                                bool(causal))
+                                bool(causal), cu_seqlens_k)
     return out
+
+
+def kv_gather(k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor):
+    """Token rows of one layer's paged cache -> contiguous (k [n, Hkv*D], v [n, Hkv*D]) bf16, for the
+    cached-prefix prefill (the cached blocks' keys/values next to the freshly written ones).  ``slots``
+    [n] int64 = block * BS + offset; k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, BS/4, D, 4]."""
+    NB, Hkv, BS, D = k_cache.shape
+    blk, off = slots // BS, slots % BS
+    k = k_cache.permute(0, 2, 1, 3)[blk, off]                    # [n, Hkv, D]
+    v = v_cache.permute(0, 2, 4, 1, 3)[blk, off // 4, off % 4]   # [n, Hkv, D]
+    return k.reshape(-1, Hkv * D), v.reshape(-1, Hkv * D)
 
 
 # ---------------------------------------------------------------------------------------------

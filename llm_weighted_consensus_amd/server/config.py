@@ -65,6 +65,7 @@ class Config:
     gpus: List[int] = field(default_factory=list)
     device: str = "cuda"
     constrained_logprobs: bool = False
+    prefix_caching: bool = True
     kv_fraction: float = 0.85
     archive_path: Optional[str] = None
     registry_path: Optional[str] = None
@@ -97,6 +98,7 @@ class Config:
         c.gpu = int(e.get("LWC_GPU", e.get("LOCAL_RANK", "0")))
         c.device = e.get("LWC_DEVICE", "cuda").lower()
         c.constrained_logprobs = e.get("LWC_CONSTRAINED_LOGPROBS", "0") == "1"
+        c.prefix_caching = e.get("LWC_PREFIX_CACHE", "1") == "1"
         if e.get("LWC_GPUS"):
             c.gpus = [int(x) for x in e["LWC_GPUS"].split(",") if x.strip()]
         c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))

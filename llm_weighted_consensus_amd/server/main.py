@@ -32,13 +32,11 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if cfg.models or cfg.embed_models:
         import torch
 
-        from ..engine.engine import LLMEngine
         from ..engine.service import EngineService
         from ..engine.tokenizer import ByteTokenizer
         from ..embeddings.service import EmbeddingService
         from ..models.bert import BertEncoder
         from ..models.config import decoder_config, encoder_config
-        from ..models.llama import LlamaModel
 
         if cfg.device == "cpu":
             if cfg.models:
@@ -58,17 +56,17 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             if len(cfg.gpus) > 1:  # one worker process per GPU behind one front end
                 from ..engine.group import EngineGroup
 
-                wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)))
+                wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
+                             prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs)
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id,
                                                                      dcfg.eos_token_id))
                 continue
-            path, seed = _weights_spec(spec)
-            model = LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
-            tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
-            eng = LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
-                            kv_memory_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
-                            constrained_logprobs=cfg.constrained_logprobs)
+            from ..engine.group import build_engine
+
+            eng = build_engine(dict(spec, device=cfg.gpu, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
+                                    prefix_caching=cfg.prefix_caching,
+                                    constrained_logprobs=cfg.constrained_logprobs), 0)
             services[name] = EngineService(eng, name)
     remote = None
     bases = cfg.api_bases()

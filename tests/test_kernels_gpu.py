@@ -287,6 +287,29 @@ def test_prefill_attention(gpu, D, Hq, Hkv, causal):
         _close(out[s0:s0 + L].view(L, Hq, D), o, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 4, 4)])
+def test_prefill_attention_key_ranges(gpu, D, Hq, Hkv):
+    """Cached-prefix prefill: each sequence's queries are the LAST rows of a longer key range (causal
+    with that offset); k/v come from their own packed buffer."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(2)
+    ql, kl = [1, 17, 64, 70], [33, 17, 200, 118]
+    cu_q = torch.tensor([0] + list(torch.tensor(ql).cumsum(0)), dtype=torch.int32, device=gpu)
+    cu_k = torch.tensor([0] + list(torch.tensor(kl).cumsum(0)), dtype=torch.int32, device=gpu)
+    q = _bf(sum(ql), Hq * D, dev=gpu)
+    k, v = _bf(sum(kl), Hkv * D, dev=gpu), _bf(sum(kl), Hkv * D, dev=gpu)
+    sc = 1 / math.sqrt(D)
+    out = ops.prefill_attention(q, k, v, cu_q, max(ql), Hq, Hkv, D, sc, True, cu_seqlens_k=cu_k, lens=(ql, kl))
+    for i, (a, b) in enumerate(zip(ql, kl)):
+        q0, k0 = int(cu_q[i]), int(cu_k[i])
+        o = ref.attention(q[q0:q0 + a].reshape(a, Hq, D), k[k0:k0 + b].reshape(b, Hkv, D),
+                          v[k0:k0 + b].reshape(b, Hkv, D), True, sc)
+        _close(out[q0:q0 + a].view(a, Hq, D), o, 2e-2, 2e-2)
+    with pytest.raises(ValueError):  # a key range shorter than its queries is refused on the host
+        ops.prefill_attention(q, k, v, cu_q, max(ql), Hq, Hkv, D, sc, True, cu_seqlens_k=cu_k, lens=(ql, [1, 1, 1, 1]))
+
+
 def _sample(logits, dev, n=None, **kw):
     from llm_weighted_consensus_amd import ops
 

@@ -193,3 +193,54 @@ def test_decoder_embedder_last_token(tiny, gpu):
         assert _cos(e[i], r) > 0.995
         solo, _ = emb.embed([tl])
         assert _cos(solo[0], e[i]) > 0.999
+
+
+def test_prefill_with_cached_prefix_matches_full_prefill(tiny, gpu):
+    """Cross-request prefix cache at the model level: prefilling only a prompt's tail on top of its cached
+    head blocks (key ranges gathered from the paged cache) gives the full prefill's last-token logits."""
+    import numpy as np
+
+    from llm_weighted_consensus_amd.models.llama import KVCache
+
+    m = tiny
+    cache = KVCache(m.cfg, 64, 16, gpu)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    P, C = 53, 32  # 2 cached blocks, 21 new tokens
+    toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(gpu).int()
+    ar = torch.arange(P, dtype=torch.int32, device=gpu)
+    full = m.prefill(toks, ar, ar, torch.tensor([0, P], dtype=torch.int32, device=gpu), P,
+                     torch.tensor([P - 1], device=gpu), cache)
+    # second sequence: blocks 0,1 shared with the first, tail in blocks 8.. (slots 128..)
+    slots_tail = torch.arange(128, 128 + P - C, dtype=torch.int32, device=gpu)
+    k_slots = torch.cat([torch.arange(C, device=gpu), slots_tail.long()])
+    ctx = {"k_slots": k_slots, "cu_k": torch.tensor([0, P], dtype=torch.int32, device=gpu),
+           "q_lens": [P - C], "k_lens": [P]}
+    part = m.prefill(toks[C:], ar[C:], slots_tail, torch.tensor([0, P - C], dtype=torch.int32, device=gpu), P - C,
+                     torch.tensor([P - C - 1], device=gpu), cache, ctx=ctx)
+    assert _cos(part[0], full[0]) > 0.999
+
+
+def test_engine_prefix_cache_reuses_blocks_across_requests(tiny, gpu):
+    """Two requests sharing a long prompt head: with the prefix cache the second prefills only its tail,
+    yet greedy continuations equal the uncached engine's."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+
+    tok = ByteTokenizer(tiny.cfg.vocab_size)
+    head = "system: select the response among the choices below. " * 3
+    p1, p2 = tok.encode(head + "voter one keys A B"), tok.encode(head + "voter two keys Q R T")
+    sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    outs = []
+    for cache_on in (False, True):
+        eng = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512, prefix_caching=cache_on)
+        a = eng.generate([p1], sp, n=2)
+        b = eng.generate([p2], sp, n=2)
+        outs.append((a, b))
+        if cache_on:
+            assert eng.stats["prefix_cache_tokens"] >= (len(tok.encode(head)) // 16 - 1) * 16
+            assert eng.bm.num_free == 256  # cached blocks are evictable capacity
+            assert eng.bm.num_cached_blocks > 0
+        else:
+            assert eng.stats["prefix_cache_tokens"] == 0
+    assert outs[0] == outs[1]

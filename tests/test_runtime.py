@@ -141,3 +141,73 @@ def test_tally_and_error_codes():
     assert R.unify_error_codes([429, 429]) == 429
     assert R.unify_error_codes([429, 404]) == 400
     assert R.unify_error_codes([404, 500]) == 500
+
+
+def test_prefix_cache_reuse_and_cap():
+    bm = R.BlockManager(16, 4)
+    bm.set_prefix_caching(True)
+    p = list(range(100, 111))  # 11 tokens: 2 full blocks + a partial one
+    assert bm.add_sequence_cached(1, p) == 0
+    bm.cache_prefix(1, p)
+    assert bm.num_cached_blocks == 2  # only blocks the prompt fills completely
+    t1 = list(bm.block_table(1))
+    # same prompt + a longer tail: the two full blocks are shared, the rest is fresh
+    q = p[:8] + [7, 7, 7, 7, 7]
+    assert bm.match_prefix(q) == 8
+    assert bm.add_sequence_cached(2, q) == 8
+    t2 = bm.block_table(2)
+    assert t2[:2] == t1[:2] and t2[2] not in t1 and bm.refcount(t1[0]) == 2
+    # a prompt that IS exactly the cached blocks still computes its last token: only 1 block reused
+    assert bm.match_prefix(p[:8]) == 4
+    # different first block -> nothing reused, even though the second block's tokens match
+    assert bm.match_prefix([0, 0, 0, 0] + p[4:8] + [1]) == 0
+    bm.set_prefix_caching(False)
+    assert bm.match_prefix(q) == 0
+    bm.set_prefix_caching(True)
+
+
+def test_prefix_cache_lru_eviction_keeps_capacity():
+    bm = R.BlockManager(6, 4)
+    bm.set_prefix_caching(True)
+    a = list(range(9))        # 2 full blocks + 1
+    bm.add_sequence_cached(1, a)
+    bm.cache_prefix(1, a)
+    bm.free_sequence(1)
+    # cached-but-unreferenced blocks still count as free capacity
+    assert bm.num_free == 6 and bm.num_evictable == 2 and bm.num_cached_blocks == 2
+    assert bm.add_sequence_cached(2, a) == 8 and bm.num_evictable == 0  # resurrected from the LRU
+    bm.free_sequence(2)
+    # a request that needs every block evicts the cached ones (oldest first) instead of failing
+    bm.add_sequence(3, 24)
+    assert bm.num_free == 0 and bm.num_cached_blocks == 0
+    bm.free_sequence(3)
+    assert bm.match_prefix(a) == 0 and bm.num_free == 6
+    with pytest.raises(RuntimeError):
+        bm.add_sequence_cached(4, list(range(30)))
+
+
+def test_prefix_cache_chain_is_content_addressed():
+    bm = R.BlockManager(32, 4)
+    bm.set_prefix_caching(True)
+    rng = random.Random(0)
+    prompts = [[rng.randrange(50) for _ in range(rng.randrange(1, 30))] for _ in range(40)]
+    prompts += [p[: len(p) // 2] + [1, 2, 3] for p in prompts[:10]]
+    live = {}
+    for i, p in enumerate(prompts):
+        try:
+            c = bm.add_sequence_cached(i, p)
+        except RuntimeError:
+            for j in list(live):
+                bm.free_sequence(j)
+            live.clear()
+            c = bm.add_sequence_cached(i, p)
+        # every reused block must have been registered for exactly these tokens: re-derive from the
+        # prompts that registered them (content equality of the covered prefix)
+        tab = bm.block_table(i)
+        for b in range(c // 4):
+            owners = [q for j, q in live.items() if j != i and b < len(bm.block_table(j))
+                      and bm.block_table(j)[b] == tab[b]]
+            for q in owners:
+                assert q[: (b + 1) * 4] == p[: (b + 1) * 4]
+        bm.cache_prefix(i, p)
+        live[i] = p
