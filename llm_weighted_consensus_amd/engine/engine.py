@@ -456,10 +456,10 @@ class LLMEngine:
         compute = [g for g in groups if g.prefilled is None]
         imported = [g for g in groups if g.prefilled is not None]
         logits_of: Dict[int, torch.Tensor] = {}
-        if compute:
-            lg = self._run_prefill([g.prompt_ids for g in compute], [-g.id for g in compute],
+        for wave in self._prefill_waves(compute):
+            lg = self._run_prefill([g.prompt_ids for g in wave], [-g.id for g in wave],
                                    use_cache=self.prefix_caching)
-            for i, g in enumerate(compute):
+            for i, g in enumerate(wave):
                 logits_of[g.id] = lg[i]
         for g in imported:
             kv, row = g.prefilled
@@ -488,6 +488,35 @@ class LLMEngine:
             if not s.finished:
                 self.running.append(s)
         return events
+
+    def _prefill_waves(self, groups: List[SequenceGroup]) -> List[List[SequenceGroup]]:
+        """Split one admission batch so prompts that share a head INSIDE the batch (the voters of one
+        score request: same messages, different key tails) compute it once: the first prompt of each
+        shared head goes in wave 1, the prompts that would reuse more of it than the cache already holds
+        go in wave 2 and take the head from the prefix cache wave 1 just filled."""
+        if not self.prefix_caching or len(groups) < 2:
+            return [groups] if groups else []
+        bs = self.block_size
+        leaders: Dict[tuple, np.ndarray] = {}
+        first, second = [], []
+        for g in groups:
+            p = g.prompt_ids
+            if len(p) <= bs:
+                first.append(g)
+                continue
+            key = tuple(p[:bs])
+            lead = leaders.get(key)
+            if lead is None:
+                leaders[key] = np.asarray(p, dtype=np.int64)
+                first.append(g)
+                continue
+            a = np.asarray(p, dtype=np.int64)
+            n = min(len(a), len(lead))
+            diff = np.nonzero(a[:n] != lead[:n])[0]
+            common = int(diff[0]) if diff.size else n
+            shared = min(common, len(p) - 1) // bs * bs
+            (second if shared > self.bm.match_prefix(p) else first).append(g)
+        return [w for w in (first, second) if w]
 
     def _attach_rows(self, s: Sequence) -> None:
         p = s.params

@@ -15,7 +15,7 @@ from llm_weighted_consensus_amd.engine.service import EngineFailure
 FACTORY = "tests.fake_engine:make"
 
 
-def _collect(group, n, params, timeout=30):
+def _collect(group, n, params, timeout=120):
     async def go():
         loop = asyncio.get_running_loop()
         q = asyncio.Queue()
@@ -57,10 +57,10 @@ def test_group_worker_death_reschedules_or_fails():
             loop = asyncio.get_running_loop()
             q = asyncio.Queue()
             g.submit([1], sp, 4, loop, q)
-            ev = await asyncio.wait_for(q.get(), 30)  # tokens are flowing on both workers
+            ev = await asyncio.wait_for(q.get(), 120)  # tokens are flowing on both workers
             os.kill(victim.pid, signal.SIGKILL)
             while True:
-                ev = await asyncio.wait_for(q.get(), 30)
+                ev = await asyncio.wait_for(q.get(), 120)
                 if isinstance(ev, EngineFailure):
                     return ev
 

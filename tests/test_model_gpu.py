@@ -244,3 +244,24 @@ def test_engine_prefix_cache_reuses_blocks_across_requests(tiny, gpu):
         else:
             assert eng.stats["prefix_cache_tokens"] == 0
     assert outs[0] == outs[1]
+
+
+def test_engine_prefix_cache_shares_heads_within_one_batch(tiny, gpu):
+    """Voters of one score request arrive together: the shared head is computed once (wave 1) and the
+    other prompts take it from the cache (wave 2), with unchanged greedy output."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+
+    tok = ByteTokenizer(tiny.cfg.vocab_size)
+    head = "user: which answer is right? " * 4
+    prompts = [tok.encode(head + f"system: keys {k}") for k in ("A B", "C D E", "F G", "H")]
+    sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+    outs, stats = [], []
+    for cache_on in (False, True):
+        eng = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512, prefix_caching=cache_on)
+        outs.append(eng.generate(prompts, sp, n=1))
+        stats.append(dict(eng.stats))
+    assert outs[0] == outs[1]
+    saved = stats[0]["prefill_tokens"] - stats[1]["prefill_tokens"]
+    assert saved == stats[1]["prefix_cache_tokens"] >= 3 * 96
