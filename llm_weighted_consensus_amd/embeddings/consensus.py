@@ -73,5 +73,7 @@ class EmbeddingConsensus:
         _, eb = self.embed(flat)
         E = eb.view(R, n_local, -1)
         if gather:
-            E = gather_candidates(E, group)
+            # a dead / hung peer must not take this rank's answers down: on a failed all-gather the group
+            # is aborted and the consensus runs over the local shard of candidates
+            E = pdist.guarded(gather_candidates, E, group, fallback=lambda: E)
         return self.score_local(E.contiguous())

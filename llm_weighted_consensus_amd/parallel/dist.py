@@ -39,7 +39,7 @@ class DistInfo:
 _INFO = DistInfo()
 
 
-def init_from_env(device_type: Optional[str] = None, timeout_s: float = 600.0) -> DistInfo:
+def init_from_env(device_type: Optional[str] = None, timeout_s: Optional[float] = None) -> DistInfo:
     """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/
     MASTER_ADDR/MASTER_PORT).  Single-process when WORLD_SIZE is unset or 1.
 
@@ -47,6 +47,8 @@ def init_from_env(device_type: Optional[str] = None, timeout_s: float = 600.0) -
     collectives run over gloo (staged through host memory), so the multi-rank code paths can be
     exercised end to end where RCCL cannot put two ranks on one device."""
     global _INFO
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("LWC_COLLECTIVE_TIMEOUT_S", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -182,6 +184,44 @@ def broadcast_object(obj, src: int = 0):
     lst = [obj]
     dist.broadcast_object_list(lst, src=src)
     return lst[0]
+
+
+class CollectiveFailure(RuntimeError):
+    """A collective failed (peer died, timeout, transport error); the process group has been aborted and
+    this process continues single-rank (``info().enabled`` is now False)."""
+
+
+def abort() -> None:
+    """Tear the process group down after a failed collective WITHOUT waiting on peers (a dead peer would
+    hang a graceful destroy), and continue as a single rank.  RCCL communicators are aborted by the
+    backend's own abort; gloo just drops its sockets."""
+    global _INFO
+    if dist.is_initialized():
+        try:
+            pg = dist.distributed_c10d._get_default_group()
+            if hasattr(pg, "abort"):
+                pg.abort()
+        except Exception:  # noqa: BLE001 - best effort: the group is being discarded
+            pass
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+    _INFO = DistInfo(_INFO.rank, 1, _INFO.local_rank, None)
+
+
+def guarded(fn, *args, fallback=None, **kw):
+    """Run a collective; on failure abort the group (see :func:`abort`) and return ``fallback()`` (or
+    raise :class:`CollectiveFailure` when no fallback is given).  Failure detection is the process
+    group's own timeout (``init_from_env(timeout_s=...)``, ``LWC_COLLECTIVE_TIMEOUT_S``) plus the
+    transport noticing a dead peer — whichever comes first."""
+    try:
+        return fn(*args, **kw)
+    except Exception as e:  # noqa: BLE001 - any transport / timeout error
+        abort()
+        if fallback is None:
+            raise CollectiveFailure(f"collective {getattr(fn, '__name__', fn)} failed: {e}") from e
+        return fallback()
 
 
 def shutdown() -> None:

@@ -128,3 +128,51 @@ def test_candidate_groups_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert [r[1:] for r in res] == [(True, 0, 0), (True, 0, 1), (True, 1, 0), (True, 1, 1)]
+
+
+def _dead_peer_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_COLLECTIVE_TIMEOUT_S="5")
+    import time
+
+    from llm_weighted_consensus_amd.embeddings.consensus import gather_candidates
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+
+    pdist.init_from_env("cpu")
+    pdist.barrier()
+    if rank == 1:
+        os._exit(0)  # the peer dies without a word
+    E = torch.nn.functional.normalize(torch.randn(2, 3, 8), dim=-1)
+    t0 = time.time()
+    got = pdist.guarded(gather_candidates, E, None, fallback=lambda: E)
+    ok = torch.equal(got, E) and not pdist.info().enabled
+    # further collectives are single-rank no-ops now
+    ok = ok and pdist.all_gather(E).shape == (1, 2, 3, 8) and pdist.max_over_ranks(3.0) == 3.0
+    q.put((ok, time.time() - t0))
+
+
+def test_collective_failure_aborts_and_falls_back():
+    """Failure detection for collectives: a peer dies, the surviving rank's guarded all-gather fails
+    within the process-group timeout, the group is aborted and the rank continues single-rank with
+    its local shard."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok, dt = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok and dt < 60, dt
+
+
+def test_guarded_without_fallback_raises():
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+
+    def boom():
+        raise RuntimeError("transport closed")
+
+    with pytest.raises(pdist.CollectiveFailure):
+        pdist.guarded(boom)
+    assert pdist.guarded(lambda: 7) == 7
