@@ -1,6 +1,7 @@
 """Embeddings service: OpenAI-compatible `/embeddings` on the local BGE encoder.
 
 Produces the reference's `CreateEmbeddingResponse` (src/embeddings/response.rs:4-30).  Texts are
+tokenized with the model's own tokenizer.json when the spec names one (WordPiece [CLS] ... [SEP]), else
 byte-tokenized into the encoder vocabulary (no tokenizer downloads here), packed varlen (no padding
 FLOPs) and run through the gfx950 encoder kernels on a dedicated HIP stream so embedding work can
 overlap the decode engine on the same GPU.  Embeddings are kept in an HBM-resident, content-addressed
@@ -21,9 +22,10 @@ from ..schema import score as S
 
 
 class EmbeddingService:
-    def __init__(self, encoder, name: str, cache_mb: Optional[float] = None):
+    def __init__(self, encoder, name: str, cache_mb: Optional[float] = None, tokenizer=None):
         self.encoder = encoder
         self.name = name
+        self.tokenizer = tokenizer
         self.lock = threading.Lock()
         self.stream = torch.cuda.Stream(device=encoder.device) if encoder.device.type == "cuda" else None
         if cache_mb is None:
@@ -40,6 +42,8 @@ class EmbeddingService:
         return self.encoder.embed(lists, max_tokens)[0]
 
     def tokenize(self, text: str) -> List[int]:
+        if self.tokenizer is not None:
+            return self.tokenizer.encode_with_specials(text)
         V = self.encoder.cfg.vocab_size
         return [101] + [(b % (V - 1000)) + 1000 for b in text.encode("utf-8")] + [102]  # [CLS] ... [SEP]
 

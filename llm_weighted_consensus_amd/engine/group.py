@@ -295,13 +295,14 @@ class EngineGroup:
 def build_engine(spec: dict, wid: int):
     """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
     ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8",
-    "prefix_caching", "constrained_logprobs"}); MoE archs get the Mixtral model."""
+    "prefix_caching", "constrained_logprobs", "tokenizer": path to a tokenizer.json}); MoE archs get the
+    Mixtral model."""
     import torch
 
     from ..models.config import decoder_config
     from ..models.llama import LlamaModel
     from .engine import LLMEngine
-    from .tokenizer import ByteTokenizer
+    from .tokenizer import load_tokenizer
 
     dev = torch.device("cuda", int(spec.get("device", 0)))
     torch.cuda.set_device(dev)
@@ -316,7 +317,7 @@ def build_engine(spec: dict, wid: int):
                              fp8=bool(spec.get("fp8", False)))
     else:
         model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
-    tok = ByteTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
+    tok = load_tokenizer(spec, cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
     return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
                      kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),
                      prefix_caching=bool(spec.get("prefix_caching", True)),

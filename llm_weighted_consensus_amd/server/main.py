@@ -33,7 +33,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         import torch
 
         from ..engine.service import EngineService
-        from ..engine.tokenizer import ByteTokenizer
+        from ..engine.tokenizer import HFTokenizer, load_tokenizer
         from ..embeddings.service import EmbeddingService
         from ..models.bert import BertEncoder
         from ..models.config import decoder_config, encoder_config
@@ -49,7 +49,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             path, seed = _weights_spec(spec)
             enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
                               dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
-            embedders[name] = EmbeddingService(enc, name)
+            tok = HFTokenizer(spec["tokenizer"]) if spec.get("tokenizer") else None
+            embedders[name] = EmbeddingService(enc, name, tokenizer=tok)
         for name, spec in cfg.models.items():
             dcfg = decoder_config(spec["arch"])
             mlen = int(spec.get("max_model_len", 4096))
@@ -59,8 +60,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
                              prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs)
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
-                                             tokenizer=ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id,
-                                                                     dcfg.eos_token_id))
+                                             tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
+                                                                      dcfg.eos_token_id))
                 continue
             from ..engine.group import build_engine
 
