@@ -25,29 +25,68 @@ from ..utils import json as sjson
 from .base import ChatClient
 
 
-def render_chat_prompt(messages: List[Any], tools: Optional[List[C.Tool]] = None) -> str:
-    """Llama-3 style chat template over the resolved request messages."""
-    out = ["<|begin_of_text|>"]
+def _message_body(m: Any) -> Optional[str]:
+    if isinstance(m, (C.SystemMessage, C.DeveloperMessage)):
+        return C.simple_content_text(m.content)
+    if isinstance(m, (C.UserMessage, C.ToolMessage)):
+        return C.rich_content_text(m.content)
+    if isinstance(m, C.AssistantMessage):
+        body = C.rich_content_text(m.content) if m.content is not None else ""
+        if m.refusal:
+            body += m.refusal
+        if m.tool_calls:
+            body += "".join(tc.template() for tc in m.tool_calls)
+        return body
+    return None  # unresolved completion references never reach the engine
+
+
+CHAT_TEMPLATES = ("llama3", "mistral", "chatml")
+
+
+def template_for(arch: str) -> str:
+    """Default chat template of a decoder architecture (a model spec's "chat_template" overrides it)."""
+    a = arch.lower()
+    if "mistral" in a or "mixtral" in a:
+        return "mistral"
+    if "qwen" in a:
+        return "chatml"
+    return "llama3"
+
+
+def render_chat_prompt(messages: List[Any], tools: Optional[List[C.Tool]] = None, template: str = "llama3") -> str:
+    """Render the resolved request messages with the model's chat template.  The BOS token is NOT part of
+    the text: the engine adds it as an id (a real tokenizer would otherwise see it twice).
+
+    llama3  : <|start_header_id|>role<|end_header_id|>\n\nbody<|eot_id|> ... assistant header
+    mistral : [INST] system\n\nuser [/INST]assistant</s>[INST] ... [/INST]  (every non-assistant turn
+              between two answers is one instruction, joined by blank lines)
+    chatml  : <|im_start|>role\nbody<|im_end|>\n ... <|im_start|>assistant\n"""
+    turns = [(m.role, b) for m in messages if (b := _message_body(m)) is not None]
+    sep = "\n\n"
     if tools:
-        spec = sjson.dumps([t.to_obj() for t in tools])
-        out.append(f"<|start_header_id|>system<|end_header_id|>\n\nAvailable tools: {spec}<|eot_id|>")
-    for m in messages:
-        role = m.role
-        if isinstance(m, (C.SystemMessage, C.DeveloperMessage)):
-            body = C.simple_content_text(m.content)
-        elif isinstance(m, (C.UserMessage, C.ToolMessage)):
-            body = C.rich_content_text(m.content)
-        elif isinstance(m, C.AssistantMessage):
-            body = C.rich_content_text(m.content) if m.content is not None else ""
-            if m.refusal:
-                body += m.refusal
-            if m.tool_calls:
-                body += "".join(tc.template() for tc in m.tool_calls)
-        else:  # unresolved completion references never reach the engine
-            continue
-        out.append(f"<|start_header_id|>{role}<|end_header_id|>\n\n{body}<|eot_id|>")
-    out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
-    return "".join(out)
+        turns.insert(0, ("system", f"Available tools: {sjson.dumps([t.to_obj() for t in tools])}"))
+    if template == "llama3":
+        out = [f"<|start_header_id|>{r}<|end_header_id|>\n\n{b}<|eot_id|>" for r, b in turns]
+        out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
+        return "".join(out)
+    if template == "chatml":
+        out = [f"<|im_start|>{r}\n{b}<|im_end|>\n" for r, b in turns]
+        out.append("<|im_start|>assistant\n")
+        return "".join(out)
+    if template == "mistral":
+        out, cur = [], []
+        for r, b in turns:
+            if r == "assistant":
+                if cur:
+                    out.append(f"[INST] {sep.join(cur)} [/INST]")
+                    cur = []
+                out.append(f"{b}</s>")
+            else:  # system / developer / user / tool turns between two answers form one instruction
+                cur.append(b)
+        if cur:
+            out.append(f"[INST] {sep.join(cur)} [/INST]")
+        return "".join(out)
+    raise ValueError(f"unknown chat template {template!r} (one of {CHAT_TEMPLATES})")
 
 
 class LocalChatClient(ChatClient):
@@ -117,7 +156,8 @@ class LocalChatClient(ChatClient):
             raise ChatError.model_not_found(request.model)
         svc = self.services[name]
         tok = svc.engine.tokenizer
-        prompt = render_chat_prompt(request.messages, request.tools)
+        template = getattr(svc, "chat_template", None) or template_for(svc.engine.cfg.name)
+        prompt = render_chat_prompt(request.messages, request.tools, template)
         ids = tok.encode(prompt, add_bos=True)
         if len(ids) >= svc.engine.max_model_len:
             raise ChatError.invalid_request(f"prompt of {len(ids)} tokens exceeds the model context "

@@ -62,6 +62,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
                                                                       dcfg.eos_token_id))
+                services[name].chat_template = spec.get("chat_template")
                 continue
             from ..engine.group import build_engine
 
@@ -69,6 +70,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                                     prefix_caching=cfg.prefix_caching,
                                     constrained_logprobs=cfg.constrained_logprobs), 0)
             services[name] = EngineService(eng, name)
+            services[name].chat_template = spec.get("chat_template")
     remote = None
     bases = cfg.api_bases()
     if bases:
