@@ -42,6 +42,13 @@ class EmbeddingService:
         return self.encoder.embed(lists, max_tokens)[0]
 
     def tokenize(self, text: str) -> List[int]:
+        dec = getattr(self.encoder, "model", None)  # decoder-as-embedder: the pooled last token is EOS
+        if dec is not None:
+            bos, eos = dec.cfg.bos_token_id, dec.cfg.eos_token_id
+            V = dec.cfg.vocab_size
+            body = (self.tokenizer.encode_with_specials(text) if self.tokenizer is not None
+                    else ([bos if bos is not None else V - 2] + list(text.encode("utf-8"))))
+            return body + [eos if eos is not None else V - 1]
         if self.tokenizer is not None:
             return self.tokenizer.encode_with_specials(text)
         V = self.encoder.cfg.vocab_size

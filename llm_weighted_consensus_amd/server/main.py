@@ -36,7 +36,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         from ..engine.tokenizer import HFTokenizer, load_tokenizer
         from ..embeddings.service import EmbeddingService
         from ..models.bert import BertEncoder
-        from ..models.config import decoder_config, encoder_config
+        from ..models.config import DECODERS, decoder_config, encoder_config
 
         if cfg.device == "cpu":
             if cfg.models:
@@ -47,8 +47,19 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             torch.cuda.set_device(dev)
         for name, spec in cfg.embed_models.items():
             path, seed = _weights_spec(spec)
-            enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
-                              dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
+            if spec["arch"] in DECODERS:  # decoder-as-embedder (e5-mistral): last-token pooling
+                if dev.type == "cpu":
+                    raise ValueError(f"embedding model {name}: decoder embedders need an MI355X")
+                from ..models.embedder import DecoderEmbedder
+                from ..models.llama import LlamaModel
+
+                dcfg = decoder_config(spec["arch"])
+                mtok = int(spec.get("max_tokens", 4096))
+                enc = DecoderEmbedder(LlamaModel(dcfg, device=dev, seed=seed, weights_path=path,
+                                                 max_position=mtok + 64), max_tokens=mtok)
+            else:
+                enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
+                                  dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
             tok = HFTokenizer(spec["tokenizer"]) if spec.get("tokenizer") else None
             embedders[name] = EmbeddingService(enc, name, tokenizer=tok)
         for name, spec in cfg.models.items():

@@ -124,3 +124,24 @@ def test_engine_group_two_workers_serve_chat(gpu, monkeypatch):
         asyncio.run(go())
     finally:
         svc.close()
+
+
+def test_decoder_embedder_served_from_embed_models(gpu):
+    """An embed-model spec naming a DECODER arch serves /embeddings through the decoder-as-embedder
+    (e5-mistral style: last-token pooling of the final hidden state), unit-norm rows of the model's width."""
+    from llm_weighted_consensus_amd.server.app import create_app
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+
+    state = build_state(Config(embed_models={"e5": {"arch": "llama-tiny", "weights": "random:5", "max_tokens": 256}}))
+    c = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t", timeout=120)
+
+    async def go():
+        r = await c.post("/embeddings", json={"input": ["a cat", "a dog", "a cat"], "model": "e5"})
+        assert r.status_code == 200, r.text
+        data = r.json()["data"]
+        assert len(data) == 3 and len(data[0]["embedding"]) == 512
+        n = sum(x * x for x in data[0]["embedding"]) ** 0.5
+        assert abs(n - 1.0) < 1e-2
+        assert data[0]["embedding"] == data[2]["embedding"]  # same text -> same row (cache or not)
+    asyncio.run(go())
