@@ -24,7 +24,7 @@ int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const i
                              int, int, int, int, int, float, hipStream_t);
 int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
-                     int, int, int, int, int, int, long long, int, hipStream_t);
+                     int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
 int lwc_gemm256(const void*, const void*, void*, const void*, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
@@ -257,7 +257,7 @@ void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const 
 
 void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& row_off, int64_t max_slots,
                   const c10::optional<at::Tensor>& a_scale, const c10::optional<at::Tensor>& w_scale,
-                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& a_rows) {
+                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& a_rows, int64_t splits) {
   // A [rows, K] (bf16 | fp8 e4m3fn, unit inner stride), W [G, N, K] contiguous, C [rows, N] bf16,
   // row_off [G+1] int32 on the device (group boundaries; the kernel trusts them to be <= rows).
   CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_DTYPE(row_off, at::kInt); CHECK_CONTIG(row_off);
@@ -293,8 +293,12 @@ void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const
     TORCH_CHECK(bias->numel() == (int64_t)G * N, "grouped_gemm: bias must be [G, N]");
     b = bias->data_ptr();
   }
+  TORCH_CHECK(splits >= 1, "grouped_gemm: splits must be >= 1");
+  at::Tensor c32;  // split-K: fp32 accumulation buffer over all output rows
+  if (splits > 1) c32 = at::zeros({C.size(0), N}, C.options().dtype(at::kFloat));
   CHECK_RC(lwc_grouped_gemm(A.data_ptr(), W.data_ptr(), C.data_ptr(), row_off.data_ptr<int>(), as, ws, b, ar, G,
                             (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0), (long long)N * K, fp8 ? 1 : 0,
+                            splits > 1 ? c32.data_ptr<float>() : nullptr, (int)splits, (long long)C.size(0),
                             cur_stream()),
            "grouped_gemm");
 }

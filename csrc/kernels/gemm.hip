@@ -36,6 +36,8 @@ struct GemmParams {
   const int* a_rows;    // optional [rows]: A row of output row r is a_rows[r] (MoE dispatch gather)
   int G, N, K, lda, ldc;
   long long w_group_stride;  // elements
+  float* C32;           // split-K (splits > 1): fp32 [rows, N] accumulation buffer (zeroed), C unused
+  int splits;           // K split into `splits` ranges (grid z); partials added with fp32 atomics
 };
 
 LWC_DEVICE float4v mfma_bf16(const short8& a, const short8& b, const float4v& c) {
@@ -68,24 +70,32 @@ __global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
   const int r16 = lane & 15, q = lane >> 4;
   const int wm = wid >> 1, wn = wid & 1;
 
-  const int KT = p.K * ES / kGKBytes;  // K tiles (K * ES is a multiple of 128 B)
-  // staging: 1024 chunks per operand tile, 4 per thread
+  const int KT_all = p.K * ES / kGKBytes;  // K tiles (K * ES is a multiple of 128 B)
+  // split-K: this workgroup's K-tile range
+  const int kper = (KT_all + p.splits - 1) / p.splits;
+  const int kt0 = blockIdx.z * kper, KT = min(KT_all, kt0 + kper) - kt0;
+  if (KT <= 0) return;  // uniform
+  // staging: 1024 chunks per operand tile, 4 per thread.  The A row pointers (MoE gather through
+  // a_rows) are resolved ONCE: a per-iteration index load would put a dependent memory round trip in
+  // front of every K tile's A loads.
+  const uint8_t* arow[4];
+  const uint8_t* wrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, ch = c & 7;
+    const int ar = m_begin + row;
+    arow[i] = ar < m_end ? p.A + (size_t)(p.a_rows ? p.a_rows[ar] : ar) * p.lda * ES + ch * 16 : nullptr;
+    const int wr = n0 + row;
+    wrow[i] = wr < p.N ? W + (size_t)wr * p.K * ES + ch * 16 : nullptr;
+  }
   uint4v sa[4], sw[4];
   auto gload = [&](int kt) {
+    const size_t kb = (size_t)(kt0 + kt) * kGKBytes;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      const int ar = m_begin + row;
-      const size_t kb = (size_t)kt * kGKBytes + ch * 16;
-      if (ar < m_end) {
-        const int src = p.a_rows ? p.a_rows[ar] : ar;
-        sa[i] = *reinterpret_cast<const uint4v*>(p.A + (size_t)src * p.lda * ES + kb);
-      } else {
-        sa[i] = uint4v{0, 0, 0, 0};
-      }
-      const int wr = n0 + row;
-      sw[i] = wr < p.N ? *reinterpret_cast<const uint4v*>(W + (size_t)wr * p.K * ES + kb) : uint4v{0, 0, 0, 0};
+      sa[i] = arow[i] ? *reinterpret_cast<const uint4v*>(arow[i] + kb) : uint4v{0, 0, 0, 0};
+      sw[i] = wrow[i] ? *reinterpret_cast<const uint4v*>(wrow[i] + kb) : uint4v{0, 0, 0, 0};
     }
   };
   auto lstore = [&](int buf) {
@@ -152,7 +162,7 @@ __global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
     const int col = n0 + wn * 64 + j * 16 + r16;
     if (col >= p.N) continue;
     const float ws = FP8 ? p.w_scale[(size_t)g * p.N + col] : 1.f;
-    const float bv = p.bias ? bf2f(p.bias[(size_t)g * p.N + col]) : 0.f;
+    const float bv = p.bias && blockIdx.z == 0 ? bf2f(p.bias[(size_t)g * p.N + col]) : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -160,29 +170,55 @@ __global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
         const int row = m_begin + wm * 64 + i * 16 + 4 * q + r;
         if (row < m_end) {
           const float as = FP8 ? p.a_scale[p.a_rows ? p.a_rows[row] : row] : 1.f;
-          p.C[(size_t)row * p.ldc + col] = f2bf(acc[i][j][r] * as * ws + bv);
+          const float v = acc[i][j][r] * as * ws + bv;
+          if (p.splits > 1)
+            atomicAdd(p.C32 + (size_t)row * p.N + col, v);
+          else
+            p.C[(size_t)row * p.ldc + col] = f2bf(v);
         }
       }
   }
 }
 
+// split-K finalize: fp32 accumulation buffer -> bf16 C
+__global__ void __launch_bounds__(256) f32_to_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                          long long n, int N, int ldc) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i * 4 >= n) return;
+  const long long e = i * 4;  // N % 16 == 0: a 4-group never crosses a row
+  const float4 v = *reinterpret_cast<const float4*>(src + e);
+  bf16_t* o = dst + (e / N) * ldc + e % N;
+  o[0] = f2bf(v.x);
+  o[1] = f2bf(v.y);
+  o[2] = f2bf(v.z);
+  o[3] = f2bf(v.w);
+}
+
 }  // namespace lwc
 
 // max_slots: grid x; must be >= sum_g ceil(M_g / 128) (sum_g <= ceil(M_total / 128) + G works for any split).
+// splits > 1: split-K over grid z; `c32` = zeroed fp32 [rows, N] workspace (rows = max row index + 1),
+// finalised into C (bf16) by a second kernel.
 extern "C" int lwc_grouped_gemm(const void* A, const void* W, void* C, const int* row_off, const float* a_scale,
                                 const float* w_scale, const void* bias, const int* a_rows, int G, int max_slots, int N,
-                                int K, int lda, int ldc, long long w_group_stride, int fp8, hipStream_t s) {
+                                int K, int lda, int ldc, long long w_group_stride, int fp8, float* c32, int splits,
+                                long long rows, hipStream_t s) {
   using namespace lwc;
   const int es = fp8 ? 1 : 2;
-  if ((K * es) % kGKBytes != 0 || N % 16 != 0 || G < 1) return -1;
+  if ((K * es) % kGKBytes != 0 || N % 16 != 0 || G < 1 || splits < 1) return -1;
   if (fp8 && (!a_scale || !w_scale)) return -2;
+  if (splits > 1 && !c32) return -3;
   if (max_slots == 0) return 0;
   GemmParams p{(const uint8_t*)A, (const uint8_t*)W, (bf16_t*)C, row_off, a_scale, w_scale, (const bf16_t*)bias,
-               a_rows, G, N, K, lda, ldc, w_group_stride};
-  dim3 grid(max_slots, (N + kGN - 1) / kGN);
+               a_rows, G, N, K, lda, ldc, w_group_stride, c32, splits};
+  dim3 grid(max_slots, (N + kGN - 1) / kGN, splits);
   if (fp8)
     grouped_gemm_kernel<true><<<grid, 256, 0, s>>>(p);
   else
     grouped_gemm_kernel<false><<<grid, 256, 0, s>>>(p);
+  if (splits > 1 && rows > 0) {
+    const long long n = rows * N;
+    f32_to_bf16_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(c32, (bf16_t*)C, n, N, ldc);
+  }
   return (int)hipGetLastError();
 }

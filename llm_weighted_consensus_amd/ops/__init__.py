@@ -212,20 +212,28 @@ def kv_gather(k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor)
 def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_slots: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, a_scale: Optional[torch.Tensor] = None,
                  w_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
-                 a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None) -> torch.Tensor:
+                 a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None,
+                 splits: Optional[int] = None) -> torch.Tensor:
     """Grouped GEMM on MFMA (K6g): rows [row_off[g], row_off[g+1]) of A times W[g]^T -> C [rows, N] bf16.
     ``a_rows`` [rows] gathers A's row for each output row (MoE dispatch; then ``rows`` = len(a_rows)).
     ``row_off`` lives on the device (MoE expert segments: no host sync, graph-capturable).  fp8 e4m3fn
     A/W take per-row ``a_scale`` and per-channel ``w_scale`` (config 5).  ``max_slots`` bounds the m-tiles
-    (default: ceil(rows/128) + G, enough for any split of the rows into G groups)."""
+    (default: ceil(rows/128) + G, enough for any split of the rows into G groups).  ``splits`` > 1 splits
+    K over that many workgroups per tile (fp32 atomics into a workspace, then one bf16 pass); default:
+    chosen so a small-M launch (MoE decode down projection: 8 experts x 32 column tiles) still puts
+    ~4 workgroups on every CU."""
     if rows is None:
         rows = a_rows.numel() if a_rows is not None else A.shape[0]
-    G, N = W.shape[0], W.shape[1]
+    G, N, K = W.shape[0], W.shape[1], W.shape[2]
     if max_slots is None:
         max_slots = -(-rows // 128) + G
     if out is None:
         out = torch.empty(rows, N, dtype=torch.bfloat16, device=A.device)
-    kernels().grouped_gemm(A, W, out, row_off, int(max_slots), a_scale, w_scale, bias, a_rows)
+    if splits is None:
+        k_tiles = K * W.element_size() // 128
+        wgs = max(1, -(-rows // 128)) * -(-N // 128)  # lower bound on the live tiles
+        splits = max(1, min(k_tiles // 8, -(-1024 // wgs))) if wgs < 512 else 1
+    kernels().grouped_gemm(A, W, out, row_off, int(max_slots), a_scale, w_scale, bias, a_rows, int(splits))
     return out
 
 

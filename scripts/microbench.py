@@ -300,6 +300,37 @@ def attention_prefix(dev):
               f"no-sharing full ctx {t_f:7.1f} us", flush=True)
 
 
+def moe_decode(dev):
+    """Mixtral decode MoE at the config-5 batch: fp8 experts, T tokens x top-2 over 8 experts, balanced and
+    router-driven (uneven) segments; time and the expert-weight bytes streamed per second."""
+    from llm_weighted_consensus_amd import ops
+
+    E, d, f = 8, 4096, 14336
+    g = torch.Generator(device=dev).manual_seed(0)
+    w13 = (torch.randn(E, 2 * f, d, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    w2 = (torch.randn(E, d, f, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q13, s13 = ops.quant_fp8_weight(w13)
+    q2, s2 = ops.quant_fp8_weight(w2)
+    del w13, w2
+    router = (torch.randn(E, d, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    for T in [int(t) for t in os.environ.get("MICRO_MOE_T", "512,2048").split(",")]:
+        rows = 2 * T
+        h = torch.randn(T, d, device=dev, generator=g).to(torch.bfloat16)
+        _ids, _w, off_r, src, _inv = ops.moe_route(torch.nn.functional.linear(h, router), 2)
+        sizes = torch.full((E,), rows // E, dtype=torch.int64)
+        off_b = torch.cat([torch.zeros(1, dtype=torch.int64), sizes.cumsum(0)]).to(torch.int32).to(dev)
+        hq, hs = ops.quant_fp8_rows(h)
+        act = torch.randn(rows, f, device=dev, generator=g).to(torch.bfloat16)
+        aq, as_ = ops.quant_fp8_rows(act)
+        for label, off in (("balanced", off_b), ("routed", off_r)):
+            t13 = timeit(lambda: ops.grouped_gemm(hq, q13, off, a_rows=src, rows=rows, a_scale=hs, w_scale=s13), iters=20)
+            t2 = timeit(lambda: ops.grouped_gemm(aq, q2, off, a_scale=as_, w_scale=s2), iters=20)
+            mx = int((off[1:] - off[:-1]).max())
+            print(f"moe fp8 T={T:5d} {label:8s} (max rows/expert {mx:4d}): w13 {t13:7.1f} us "
+                  f"({q13.numel() / t13 / 1e3:5.0f} GB/s of weights)  w2 {t2:7.1f} us ({q2.numel() / t2 / 1e3:5.0f} GB/s)",
+                  flush=True)
+
+
 def sampler(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -366,6 +397,8 @@ def main():
         attention_prefix(dev)
     if "sample" in a.what:
         sampler(dev)
+    if "moe" in a.what:
+        moe_decode(dev)
     if "small" in a.what:
         small(dev)
 

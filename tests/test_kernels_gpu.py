@@ -459,7 +459,8 @@ def test_kv_block_copy(gpu):
 
 
 @pytest.mark.parametrize("fp8", [False, True])
-def test_grouped_gemm(gpu, fp8):
+@pytest.mark.parametrize("splits", [None, 3])
+def test_grouped_gemm(gpu, fp8, splits):
     """Grouped MFMA GEMM (MoE expert segments on the device, incl. an empty and a ragged group) vs
     per-group fp32 matmuls; fp8 e4m3fn operands with per-row / per-channel scales."""
     from llm_weighted_consensus_amd import ops
@@ -478,12 +479,12 @@ def test_grouped_gemm(gpu, fp8):
         Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
         Wq = (W / w_s[:, :, None]).to(torch.float8_e4m3fn)
         out = ops.grouped_gemm(Aq, Wq, off, a_scale=a_s.float().contiguous(), w_scale=w_s.float().contiguous(),
-                               bias=bias)
+                               bias=bias, splits=splits)
         Ar = Aq.float() * a_s[:, None]
         Wr = Wq.float() * w_s[:, :, None]
     else:
         Ab, Wb = A.to(torch.bfloat16), W.to(torch.bfloat16)
-        out = ops.grouped_gemm(Ab, Wb, off, bias=bias)
+        out = ops.grouped_gemm(Ab, Wb, off, bias=bias, splits=splits)
         Ar, Wr = Ab.float(), Wb.float()
     o = off.tolist()
     for g in range(G):
