@@ -134,7 +134,7 @@ def main():
         a.requests = a.requests or 64
         out = bench_encoder(a)
     else:
-        a.requests = a.requests or 8
+        a.requests = a.requests or 32  # 2048-sequence decode batch: amortises the expert-weight stream
         out = bench_moe(a)
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(out), flush=True)

@@ -12,7 +12,7 @@ timeout -k 10 400 python bench.py --candidates 32 --steps 2 --warmup 1 >> gpurun
 rc=$?; echo "config3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 [ "${ONLY:-}" = "small" ] && { cat gpurun_out/configs.log; exit 0; }
-timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-8} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
+timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-32} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
 rc=$?; echo "config5 rc=$rc"
 cat gpurun_out/configs.log
 exit $rc
