@@ -7,8 +7,8 @@
 //            Optional a_rows[r] gathers A's row per output row (MoE dispatch without a permute copy).
 //   grid   : x = m-tile SLOT (>= sum_g ceil(M_g / BM); surplus slots exit), y = n-tile.
 //   tile   : BM x BN = 128 x 128, BK = 64; 4 waves as 2 x 2, each 64 x 64 = 4 x 4 MFMA 16x16 tiles.
-//   K loop : register-staged double-buffered LDS (next K-tile's global loads in flight under the
-//            current tile's MFMAs, written to the other LDS buffer after them: one barrier per step),
+//   K loop : register-staged, one LDS stage (next K-tile's global loads in flight under the current
+//            tile's MFMAs, written to LDS after a barrier; 4 workgroups per CU hide each other's stalls),
 //            16-byte chunks XOR-swizzled by row (conflict-free ds_read_b128 fragment reads).
 //   MFMA   : bf16: mfma_f32_16x16x32_bf16 (lane: row r16, k-chunk g); fp8: mfma_f32_16x16x32_fp8_fp8
 //            (8 fp8 per lane per k=32 step, so one 16 B LDS chunk holds two k-steps).
@@ -46,9 +46,12 @@ LWC_DEVICE float4v mfma_bf16(const short8& a, const short8& b, const float4v& c)
 }
 
 template <bool FP8>
-__global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
+__global__ void __launch_bounds__(256, 3) grouped_gemm_kernel(GemmParams p) {
   constexpr int ES = FP8 ? 1 : 2;  // element size
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2][2][kGTileBytes];  // [buf][A|W]
+  // ONE LDS stage (32 KiB): the next K tile waits in registers.  Four workgroups fit a CU (LDS 4 x 32 KiB,
+  // 128 VGPRs = 4 waves per SIMD), so while one workgroup stalls on its loads the others compute — the
+  // small-M MoE decode launches are latency-bound, and occupancy buys more than a second LDS buffer.
+  __shared__ __attribute__((aligned(16))) uint8_t smem[1][2][kGTileBytes];  // [stage][A|W]
 
   // ---- locate (group, m-tile) of this slot ----
   int slot = blockIdx.x, g = 0, m_begin = 0, m_end = 0;
@@ -116,13 +119,13 @@ __global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
   gload(0);
-  lstore(0);
-  __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < KT) gload(kt + 1);
-    const uint8_t* As = smem[buf][0];
-    const uint8_t* Ws = smem[buf][1];
+    __syncthreads();  // everyone is done reading the previous tile
+    lstore(0);
+    __syncthreads();
+    if (kt + 1 < KT) gload(kt + 1);  // in flight under this tile's MFMAs
+    const uint8_t* As = smem[0][0];
+    const uint8_t* Ws = smem[0][1];
     // two 16 B-chunk halves of the 128 B k-slice: bf16 -> 2 k-steps of 32; fp8 -> 4 k-steps of 32
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -152,8 +155,6 @@ __global__ void __launch_bounds__(256) grouped_gemm_kernel(GemmParams p) {
           }
         }
     }
-    if (kt + 1 < KT) lstore(buf ^ 1);
-    __syncthreads();
   }
 
   // ---- epilogue: scales, bias, bf16 store (lane reg r = C[row 4q + r][col r16] of each 16x16) ----
