@@ -38,6 +38,9 @@ struct GemmParams {
   long long w_group_stride;  // elements
   float* C32;           // split-K (splits > 1): fp32 [rows, N] accumulation buffer (zeroed), C unused
   int splits;           // K split into `splits` ranges (grid z); partials added with fp32 atomics
+  int slots;            // m-tile slots per n-tile (grid mapping below)
+  int n_tiles;
+  int xcd_group;        // 1: 1-D grid, the m-slots of one n-tile on ONE XCD back to back (see below)
 };
 
 LWC_DEVICE float4v mfma_bf16(const short8& a, const short8& b, const float4v& c) {
@@ -53,8 +56,23 @@ __global__ void __launch_bounds__(256, 3) grouped_gemm_kernel(GemmParams p) {
   // small-M MoE decode launches are latency-bound, and occupancy buys more than a second LDS buffer.
   __shared__ __attribute__((aligned(16))) uint8_t smem[1][2][kGTileBytes];  // [stage][A|W]
 
+  // ---- grid mapping ----
+  // xcd_group = 0: x = m-slot, y = n-tile.  xcd_group = 1 (experts with several m-tiles, e.g. a large
+  // MoE decode batch): workgroup ids are dealt round-robin to the 8 XCDs, so id = local * 8 + xcd, and
+  // each XCD walks ITS n-tiles (j = xcd mod 8) with all m-slots of an n-tile consecutive: every m-tile
+  // of an expert reuses the same weight tile from that XCD's L2 instead of streaming it again from HBM.
+  int slot, ntile;
+  if (p.xcd_group) {
+    const int id = blockIdx.x, xcd = id & 7, local = id >> 3;
+    ntile = (local / p.slots) * 8 + xcd;
+    slot = local % p.slots;
+    if (ntile >= p.n_tiles) return;  // uniform
+  } else {
+    slot = blockIdx.x;
+    ntile = blockIdx.y;
+  }
   // ---- locate (group, m-tile) of this slot ----
-  int slot = blockIdx.x, g = 0, m_begin = 0, m_end = 0;
+  int g = 0, m_begin = 0, m_end = 0;
   for (; g < p.G; ++g) {
     const int r0 = p.row_off[g], r1 = p.row_off[g + 1];
     const int nt = (r1 - r0 + kGM - 1) / kGM;
@@ -66,7 +84,7 @@ __global__ void __launch_bounds__(256, 3) grouped_gemm_kernel(GemmParams p) {
     slot -= nt;
   }
   if (g >= p.G) return;  // surplus slot (uniform for the workgroup)
-  const int n0 = blockIdx.y * kGN;
+  const int n0 = ntile * kGN;
   const uint8_t* W = p.W + (size_t)g * p.w_group_stride * ES;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -210,9 +228,13 @@ extern "C" int lwc_grouped_gemm(const void* A, const void* W, void* C, const int
   if (fp8 && (!a_scale || !w_scale)) return -2;
   if (splits > 1 && !c32) return -3;
   if (max_slots == 0) return 0;
+  const int n_tiles = (N + kGN - 1) / kGN;
+  // several m-tiles per group on average (rows >= 2 * 128 * G): group each n-tile's m-slots on one XCD
+  const int xcd_group = rows >= 2LL * kGM * G ? 1 : 0;
   GemmParams p{(const uint8_t*)A, (const uint8_t*)W, (bf16_t*)C, row_off, a_scale, w_scale, (const bf16_t*)bias,
-               a_rows, G, N, K, lda, ldc, w_group_stride, c32, splits};
-  dim3 grid(max_slots, (N + kGN - 1) / kGN, splits);
+               a_rows, G, N, K, lda, ldc, w_group_stride, c32, splits, max_slots, n_tiles, xcd_group};
+  const dim3 grid = xcd_group ? dim3((unsigned)(((n_tiles + 7) / 8) * max_slots * 8), 1, splits)
+                              : dim3(max_slots, n_tiles, splits);
   if (fp8)
     grouped_gemm_kernel<true><<<grid, 256, 0, s>>>(p);
   else

@@ -596,3 +596,35 @@ def test_sample_constrained_logprobs(gpu):
     assert abs(lps[1, 0].item() - raw.max().item()) < 2e-2  # unmasked row: raw distribution
     _, _, ids2, lps2 = ops.sample(*args, num_logprobs=8, mask=mask, mask_rows=rows)
     assert abs(lps2[0, 0].item() - torch.log_softmax(logits[0].float(), 0).max().item()) < 2e-2
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_grouped_gemm_xcd_grouped_mapping(gpu, fp8):
+    """Groups with several m-tiles each (rows >= 2*128*G) take the XCD-grouped 1-D grid; n-tile count
+    not a multiple of 8, ragged groups, a gathered A (MoE dispatch) — vs fp32 matmuls."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(5)
+    G, N, K = 2, 3 * 128 + 16, 256
+    sizes = [300, 433]
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    A = torch.randn(rows + 11, K, device=gpu)
+    src = torch.randperm(rows + 11, device=gpu)[:rows].to(torch.int32)
+    W = torch.randn(G, N, K, device=gpu) * 0.05
+    if fp8:
+        a_s = A.abs().amax(1).clamp(min=1e-6) / 448.0
+        w_s = W.abs().amax(2).clamp(min=1e-6) / 448.0
+        Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
+        Wq = (W / w_s[:, :, None]).to(torch.float8_e4m3fn)
+        out = ops.grouped_gemm(Aq, Wq, off, a_scale=a_s.float().contiguous(), w_scale=w_s.float().contiguous(),
+                               a_rows=src, rows=rows)
+        Ar, Wr = Aq.float() * a_s[:, None], Wq.float() * w_s[:, :, None]
+    else:
+        Ab, Wb = A.to(torch.bfloat16), W.to(torch.bfloat16)
+        out = ops.grouped_gemm(Ab, Wb, off, a_rows=src, rows=rows)
+        Ar, Wr = Ab.float(), Wb.float()
+    o = off.tolist()
+    Ag = Ar[src.long()]
+    for g in range(G):
+        _close(out[o[g]:o[g + 1]], Ag[o[g]:o[g + 1]] @ Wr[g].t(), 2e-2, 2e-2)
