@@ -31,6 +31,7 @@ int lwc_gemm8p_slots();
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
+int lwc_silu_mul_quant_fp8(const void*, int, int, int, void*, float*, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
@@ -385,6 +386,18 @@ void quant_fp8_rows(const at::Tensor& x, at::Tensor& q, at::Tensor& scale) {
            "quant_fp8_rows");
 }
 
+void silu_mul_quant_fp8(const at::Tensor& gu, at::Tensor& q, at::Tensor& scale, int64_t block) {
+  // gu [rows, 2F] bf16 (gate | up, or interleaved in blocks) -> q [rows, F] e4m3fn, scale [rows] f32
+  CHECK_BF16(gu); CHECK_CONTIG(gu); CHECK_CONTIG(q); CHECK_DTYPE(scale, at::kFloat);
+  TORCH_CHECK(gu.dim() == 2 && q.dim() == 2 && q.scalar_type() == at::kFloat8_e4m3fn, "silu_mul_quant_fp8: 2-D");
+  const int rows = (int)gu.size(0), F = (int)q.size(1);
+  TORCH_CHECK(gu.size(1) == 2 * F && q.size(0) == rows && scale.numel() >= rows, "silu_mul_quant_fp8: shape mismatch");
+  TORCH_CHECK(block == 0 || (block % 8 == 0 && F % block == 0), "silu_mul_quant_fp8: bad block");
+  CHECK_RC(lwc_silu_mul_quant_fp8(gu.data_ptr(), rows, F, (int)block, q.data_ptr(), scale.data_ptr<float>(),
+                                  cur_stream()),
+           "silu_mul_quant_fp8");
+}
+
 void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                        const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, int64_t D,
                        double scale, bool causal, const c10::optional<at::Tensor>& cu_seqlens_k) {
@@ -523,6 +536,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "B*Hkv*splits threshold of the wave-per-item decode kernel; returns the previous value");
   m.def("paged_decode_prefix", &paged_decode_prefix);
   m.def("prefill_attention", &prefill_attention);
+  m.def("silu_mul_quant_fp8", &silu_mul_quant_fp8);
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);

@@ -139,7 +139,83 @@ __global__ void __launch_bounds__(256) quant_fp8_rows_kernel(const bf16_t* __res
   }
 }
 
+// SwiGLU + per-row e4m3 quantisation in one pass (the MoE expert FFN between its two fp8 GEMMs):
+// gu [rows, 2F] (gate | up, or interleaved in blocks of blk) -> q [rows, F] e4m3 + scale [rows].  One
+// workgroup per row keeps silu(g)*u in registers across the row-max reduction, so the bf16 activation is
+// never written or re-read (F <= 8 * 256 * kMaxC; larger rows take the recompute loop).
+constexpr int kSqMaxC = 8;
+LWC_DEVICE float silu_q(float x) { return x / (1.f + __expf(-x)); }
+__global__ void __launch_bounds__(256) silu_mul_quant_fp8_kernel(const bf16_t* __restrict__ gu, int F, int blk,
+                                                                 uint8_t* __restrict__ q, float* __restrict__ scale) {
+  __shared__ float red[8];
+  const int r = blockIdx.x;
+  const bf16_t* row = gu + (size_t)r * 2 * F;
+  const int nchunk = F >> 3;
+  const bool hold = nchunk <= 256 * kSqMaxC;
+  float act[kSqMaxC][8];
+  auto compute = [&](int c, float (&o)[8]) {
+    const bf16_t* src = row + (c / blk) * 2 * blk + c % blk;
+    float g[8], u[8];
+    unpack8(*reinterpret_cast<const uint4v*>(src), g);
+    unpack8(*reinterpret_cast<const uint4v*>(src + blk), u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(f2bf(silu_q(g[e]) * u[e]));  // the value the bf16 path would hold
+  };
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < kSqMaxC; ++i) {
+    const int ci = threadIdx.x + 256 * i;
+    if (hold && ci < nchunk) {
+      compute(ci * 8, act[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(act[i][e]));
+    }
+  }
+  if (!hold) {
+    for (int ci = threadIdx.x; ci < nchunk; ci += 256) {
+      float o[8];
+      compute(ci * 8, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(o[e]));
+    }
+  }
+  amax = block_max(amax, red);
+  const float sc = fmaxf(amax, 1e-12f) / 448.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) scale[r] = sc;
+  auto store = [&](int c, const float (&v)[8]) {
+    uint32_t lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+    *reinterpret_cast<uint2*>(q + (size_t)r * F + c) = make_uint2(lo, hi);
+  };
+  if (hold) {
+#pragma unroll
+    for (int i = 0; i < kSqMaxC; ++i) {
+      const int ci = threadIdx.x + 256 * i;
+      if (ci < nchunk) store(ci * 8, act[i]);
+    }
+  } else {
+    for (int ci = threadIdx.x; ci < nchunk; ci += 256) {
+      float o[8];
+      compute(ci * 8, o);
+      store(ci * 8, o);
+    }
+  }
+}
+
 }  // namespace lwc
+
+extern "C" int lwc_silu_mul_quant_fp8(const void* gu, int rows, int F, int blk, void* q, float* scale, hipStream_t s) {
+  using namespace lwc;
+  if (blk <= 0) blk = F;
+  if (F % 8 != 0 || blk % 8 != 0 || F % blk != 0) return -1;
+  if (rows == 0) return 0;
+  silu_mul_quant_fp8_kernel<<<rows, 256, 0, s>>>((const bf16_t*)gu, F, blk, (uint8_t*)q, scale);
+  return (int)hipGetLastError();
+}
 
 extern "C" int lwc_moe_route(const void* logits, int T, int E, int k, int* topk_ids, float* topk_w, int* row_off,
                              int* src_row, int* inv, hipStream_t s) {

@@ -179,7 +179,7 @@ class MixtralModel(LlamaModel):
         """Grouped expert FFN over expert-major rows (optionally gathered through ``a_rows``)."""
         if self.fp8:
             gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows, a_scale=scale, w_scale=L.s13)
-            aq, as_ = ops.quant_fp8_rows(ops.silu_mul(gu))
+            aq, as_ = ops.silu_mul_quant_fp8(gu)
             return ops.grouped_gemm(aq, L.w2, row_off, a_scale=as_, w_scale=L.s2)
         gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows)
         return ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)

@@ -628,3 +628,17 @@ def test_grouped_gemm_xcd_grouped_mapping(gpu, fp8):
     Ag = Ar[src.long()]
     for g in range(G):
         _close(out[o[g]:o[g + 1]], Ag[o[g]:o[g + 1]] @ Wr[g].t(), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("F,block", [(14336, 0), (512, 32), (40000, 0)])
+def test_silu_mul_quant_fp8_matches_unfused(gpu, F, block):
+    """Fused SwiGLU + e4m3 row quantisation == quant_fp8_rows(silu_mul(x)) (register-held rows and the
+    recompute path for rows wider than 16384)."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(9)
+    gu = (torch.randn(37, 2 * F, device=gpu) * 3).to(torch.bfloat16)
+    q, s = ops.silu_mul_quant_fp8(gu, block=block)
+    q_ref, s_ref = ops.quant_fp8_rows(ops.silu_mul(gu, block=block))
+    torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
