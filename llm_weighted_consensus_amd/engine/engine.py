@@ -287,6 +287,8 @@ class LLMEngine:
         self.bias: Optional[torch.Tensor] = None    # [max_batch, V] f32, lazily
         self.free_bias_rows = list(range(max_batch))
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_cache_tokens": 0}
+        self._mask_rows_of: Optional[Dict[tuple, int]] = None  # mask content -> device mask table row
+        self._mask_limit = 4096
         self.faults = FaultInjector.from_env()
         # step() returns TokenEvents only when asked (callbacks always get theirs)
         self.collect_events = False
@@ -705,15 +707,51 @@ class LLMEngine:
         return _Step(seqs, key, bk, parity, K, outs[0], out_host, ev)
 
     def _constraint_masks(self, seqs: List[Sequence], cons: List[int]):
-        words = self.cfg.vocab_size // 32
-        m = np.zeros((len(cons), words), dtype=np.uint32)
+        """(mask table [rows, V/32] int32 on the device, per-sequence row [B] int32).
+
+        Constrained spans only ever allow raw bytes (ids < 256) and EOS, so a mask is determined by its
+        256 allowed bytes + the EOS flag.  Masks are keyed by that content: every distinct mask is built
+        and uploaded ONCE into a device-resident table (the voters of a score request, each with its own
+        shuffled key enum, still share most states: '{', the property name, quotes, ...), and a step
+        uploads only the B row indices."""
+        if self._mask_rows_of is None:
+            self._mask_rows_of = {}
+            self._mask_table = torch.zeros(64, self.cfg.vocab_size // 32, dtype=torch.int32, device=self.device)
         rows = np.full(len(seqs), -1, dtype=np.int32)
-        for j, i in enumerate(cons):
+        new: List[Tuple[int, np.ndarray]] = []
+        words = self.cfg.vocab_size // 32
+        for i in cons:
             s = seqs[i]
-            m[j] = s.params.constraint.mask(s.constraint_state, self.cfg.vocab_size)
-            rows[i] = j
-        return (torch.from_numpy(m.view(np.int32)).to(self.device),
-                torch.from_numpy(rows).to(self.device))
+            c = s.params.constraint
+            allowed, eos = c.allowed_bytes(s.constraint_state)
+            if not allowed.any():
+                eos = True  # dead end: allow EOS so the sequence can stop
+            packed = np.packbits(allowed, bitorder="little")  # 32 bytes = words 0..7
+            key = (packed.tobytes(), bool(eos), c.eos_id)
+            r = self._mask_rows_of.get(key)
+            if r is None:
+                if len(self._mask_rows_of) >= self._mask_limit:  # bounded: start the table over
+                    self._mask_rows_of.clear()
+                    return self._constraint_masks(seqs, cons)
+                r = len(self._mask_rows_of)
+                self._mask_rows_of[key] = r
+                m = np.zeros(words, dtype=np.uint32)
+                m[:8] = packed.view(np.uint32)
+                if eos and 0 <= c.eos_id < self.cfg.vocab_size:
+                    m[c.eos_id >> 5] |= np.uint32(1 << (c.eos_id & 31))
+                new.append((r, m))
+            rows[i] = r
+        if new:
+            need = max(r for r, _ in new) + 1
+            if need > self._mask_table.shape[0]:
+                grown = torch.zeros(max(need, 2 * self._mask_table.shape[0]), self._mask_table.shape[1],
+                                    dtype=torch.int32, device=self.device)
+                grown[:self._mask_table.shape[0]] = self._mask_table
+                self._mask_table = grown
+            idx = torch.tensor([r for r, _ in new], dtype=torch.int64)
+            vals = torch.from_numpy(np.stack([m for _, m in new]).view(np.int32))
+            self._mask_table.index_copy_(0, idx.to(self.device), vals.to(self.device))
+        return self._mask_table, torch.from_numpy(rows).to(self.device)
 
     def _process(self, st: _Step) -> List[TokenEvent]:
         st.event.synchronize()

@@ -2,7 +2,7 @@
 
 The HTTP front end is a single asyncio event loop (no shared mutable state across threads except
 the engine's lock-protected waiting queue); the engine thread owns the GPU and runs `step()` in a
-loop.  Token events are handed back with `loop.call_soon_threadsafe`.  Abort (client disconnect)
+loop.  Token events are handed back with `loop.call_soon_threadsafe`, batched per engine step.  Abort (client disconnect)
 is queued and applied by the engine thread between steps.
 """
 from __future__ import annotations
@@ -30,6 +30,7 @@ class EngineService:
         self._cv = threading.Condition()
         self._aborts: List[SequenceGroup] = []
         self._stop = False
+        self._pending: dict = {}  # event loop -> [(queue, event)] produced by the current step
         self._thread = threading.Thread(target=self._run, name=f"engine-{name}", daemon=True)
         self._thread.start()
         self.failures = 0
@@ -38,8 +39,11 @@ class EngineService:
     # ------------------------------------------------------------------ async API
     def submit(self, prompt_ids, params: SamplingParams, n: int, loop: asyncio.AbstractEventLoop,
                queue: asyncio.Queue) -> SequenceGroup:
+        # events are buffered per event loop during an engine step and handed over with ONE thread-safe
+        # call per loop per step (a per-token call_soon_threadsafe is a self-pipe write each, and hundreds
+        # per step of them compete with the engine thread for the GIL)
         def cb(ev: TokenEvent):
-            loop.call_soon_threadsafe(queue.put_nowait, ev)
+            self._pending.setdefault(loop, []).append((queue, ev))
 
         g = self.engine.add_request(prompt_ids, params, n=n, callback=cb)
         g.loop, g.queue = loop, queue
@@ -75,6 +79,7 @@ class EngineService:
                 aborts, self._aborts = self._aborts, []
             for g in aborts:
                 eng.abort(g)
+            self._flush()  # events an abort produced
             if not eng.has_work():
                 continue
             t0 = time.perf_counter()
@@ -84,8 +89,23 @@ class EngineService:
                 self.failures += 1
                 msg = f"{type(e).__name__}: {e}"
                 traceback.print_exc()
+                self._flush()  # tokens of the failed step first, then the failures
                 for g in eng.fail_all(msg):
                     loop, q = getattr(g, "loop", None), getattr(g, "queue", None)
                     if loop is not None:
                         loop.call_soon_threadsafe(q.put_nowait, EngineFailure(msg))
+            self._flush()
             self.last_step_s = time.perf_counter() - t0
+
+    @staticmethod
+    def _deliver(batch) -> None:
+        for q, ev in batch:
+            q.put_nowait(ev)
+
+    def _flush(self) -> None:
+        pending, self._pending = self._pending, {}
+        for loop, batch in pending.items():
+            try:
+                loop.call_soon_threadsafe(self._deliver, batch)
+            except RuntimeError:  # the client's loop is gone
+                pass
