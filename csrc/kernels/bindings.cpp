@@ -15,6 +15,7 @@ int lwc_silu_mul(const void*, void*, int, int, int, hipStream_t);
 int lwc_bias_gelu(void*, const void*, int, int, hipStream_t);
 int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
+int lwc_kv_gather(const void*, const void*, const long long*, void*, void*, int, int, int, int, hipStream_t);
 int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
                      int, int, int, int, int, int, float, const int*, const float*, const float*, hipStream_t);
 int lwc_set_decode_wave_min_items(int);
@@ -158,6 +159,21 @@ void embedding(const at::Tensor& table, const at::Tensor& ids, at::Tensor& out) 
   CHECK_RC(lwc_embedding_gather(table.data_ptr(), ids.data_ptr<int>(), out.data_ptr(), T, d, (int)table.size(0),
                                 cur_stream()),
            "embedding");
+}
+
+void kv_gather(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& slots, at::Tensor& ko, at::Tensor& vo) {
+  // kc [NB, Hkv, BS, D], vc [NB, Hkv, BS/4, D, 4] (one layer), slots [n] int64 (< NB*BS, checked by the
+  // caller's block manager), ko/vo [n, Hkv*D] contiguous bf16
+  CHECK_BF16(kc); CHECK_BF16(vc); CHECK_BF16(ko); CHECK_BF16(vo); CHECK_CONTIG(kc); CHECK_CONTIG(vc);
+  CHECK_DTYPE(slots, at::kLong); CHECK_CONTIG(slots); CHECK_CONTIG(ko); CHECK_CONTIG(vo);
+  TORCH_CHECK(kc.dim() == 4 && vc.dim() == 5, "kv_gather: cache layouts");
+  const int Hkv = (int)kc.size(1), BS = (int)kc.size(2), D = (int)kc.size(3);
+  const int n = (int)slots.numel();
+  TORCH_CHECK(ko.size(0) == n && vo.size(0) == n && ko.size(1) == Hkv * D && vo.size(1) == Hkv * D,
+              "kv_gather: output shapes");
+  CHECK_RC(lwc_kv_gather(kc.data_ptr(), vc.data_ptr(), (const long long*)slots.data_ptr<int64_t>(), ko.data_ptr(),
+                         vo.data_ptr(), n, Hkv, D, BS, cur_stream()),
+           "kv_gather");
 }
 
 void kv_block_copy(at::Tensor& cache, const at::Tensor& pairs) {
@@ -537,6 +553,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("paged_decode_prefix", &paged_decode_prefix);
   m.def("prefill_attention", &prefill_attention);
   m.def("silu_mul_quant_fp8", &silu_mul_quant_fp8);
+  m.def("kv_gather", &kv_gather);
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);

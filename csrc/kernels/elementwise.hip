@@ -134,6 +134,33 @@ __global__ void kv_block_copy_kernel(bf16_t* __restrict__ cache, const int* __re
   for (int64_t i = threadIdx.x; i < (block_elems >> 3); i += blockDim.x) d[i] = s[i];
 }
 
+// Paged cache rows -> contiguous [n, Hkv*D] K and V (cached-prefix prefill).  One thread per (token, head,
+// 8 dims): K is one 16 B load; V (4-token interleaved, 8 B per dim-quad) is 8 x 8 B loads whose token lane
+// is extracted.  Neighbouring tokens of a quad share their 32 B sectors through the cache.
+__global__ void kv_gather_kernel(const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                 const int64_t* __restrict__ slots, bf16_t* __restrict__ ko, bf16_t* __restrict__ vo,
+                                 int n, int Hkv, int D, int BS) {
+  const int chunks = D >> 3;
+  const size_t total = (size_t)n * Hkv * chunks;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % chunks);
+    const int h = (int)((i / chunks) % Hkv);
+    const size_t t = i / ((size_t)chunks * Hkv);
+    const int64_t sl = slots[t];
+    const int64_t blk = sl / BS;
+    const int off = (int)(sl % BS);
+    const size_t head = ((size_t)blk * Hkv + h) * BS * D;  // element offset of (block, head)
+    const size_t orow = t * (size_t)Hkv * D + (size_t)h * D + c * 8;
+    *reinterpret_cast<uint4v*>(ko + orow) = *reinterpret_cast<const uint4v*>(kc + head + (size_t)off * D + c * 8);
+    const bf16_t* vq = vc + head + (size_t)(off >> 2) * D * 4 + (off & 3);  // dim d at vq[4 d]
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)vq[4 * (c * 8 + 2 * e)] | ((uint32_t)vq[4 * (c * 8 + 2 * e + 1)] << 16);
+    *reinterpret_cast<uint4v*>(vo + orow) = uint4v{w[0], w[1], w[2], w[3]};
+  }
+}
+
 static int ew_grid(size_t work, int threads) {
   size_t g = (work + threads - 1) / threads;
   if (g > 4096) g = 4096;  // grid-stride beyond ~16 waves/CU (Guideline 11)
@@ -176,6 +203,16 @@ extern "C" int lwc_embedding_gather(const void* table, const int* ids, void* out
   if (d % 8 != 0) return -1;
   if (T == 0) return 0;
   embedding_gather_kernel<<<T, 128, 0, s>>>((const bf16_t*)table, ids, (bf16_t*)out, d, V);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_kv_gather(const void* kc, const void* vc, const long long* slots, void* ko, void* vo, int n,
+                             int Hkv, int D, int BS, hipStream_t s) {
+  using namespace lwc;
+  if (D % 8 != 0 || BS % 4 != 0) return -1;
+  if (n == 0) return 0;
+  kv_gather_kernel<<<ew_grid((size_t)n * Hkv * (D / 8), 256), 256, 0, s>>>(
+      (const bf16_t*)kc, (const bf16_t*)vc, (const int64_t*)slots, (bf16_t*)ko, (bf16_t*)vo, n, Hkv, D, BS);
   return (int)hipGetLastError();
 }
 

@@ -408,8 +408,10 @@ class LLMEngine:
         ctx = None
         if any(cached):
             k_lens = [len(p) for p in prompts]
-            ctx = {"k_slots": torch.from_numpy(np.concatenate([slots_range(self.bm, pid, 0, L)
-                                                               for pid, L in zip(parents, k_lens)]).astype(np.int64)).to(dev),
+            ks = np.concatenate([slots_range(self.bm, pid, 0, L) for pid, L in zip(parents, k_lens)]).astype(np.int64)
+            if ks.size and (ks.min() < 0 or ks.max() >= self.bm.num_blocks * self.block_size):
+                raise RuntimeError("prefix-cache prefill: KV slot out of range")
+            ctx = {"k_slots": torch.from_numpy(ks).to(dev),
                    "cu_k": torch.tensor(np.concatenate([[0], np.cumsum(k_lens)]), dtype=torch.int32, device=dev),
                    "q_lens": [L - c for L, c in zip(k_lens, cached)], "k_lens": k_lens}
             self.stats["prefix_cache_tokens"] += sum(cached)

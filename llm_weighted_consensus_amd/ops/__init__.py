@@ -199,10 +199,11 @@ def kv_gather(k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor)
     cached-prefix prefill (the cached blocks' keys/values next to the freshly written ones).  ``slots``
     [n] int64 = block * BS + offset; k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, BS/4, D, 4]."""
     NB, Hkv, BS, D = k_cache.shape
-    blk, off = slots // BS, slots % BS
-    k = k_cache.permute(0, 2, 1, 3)[blk, off]                    # [n, Hkv, D]
-    v = v_cache.permute(0, 2, 4, 1, 3)[blk, off // 4, off % 4]   # [n, Hkv, D]
-    return k.reshape(-1, Hkv * D), v.reshape(-1, Hkv * D)
+    slots = slots.to(torch.int64).contiguous()  # < NB * BS: the caller checks on the host (no device sync here)
+    k = torch.empty(slots.numel(), Hkv * D, dtype=k_cache.dtype, device=k_cache.device)
+    v = torch.empty_like(k)
+    kernels().kv_gather(k_cache, v_cache, slots, k, v)
+    return k, v
 
 
 # ---------------------------------------------------------------------------------------------

@@ -642,3 +642,20 @@ def test_silu_mul_quant_fp8_matches_unfused(gpu, F, block):
     q_ref, s_ref = ops.quant_fp8_rows(ops.silu_mul(gu, block=block))
     torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
     assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+
+
+def test_kv_gather_matches_cache_layout(gpu):
+    """Paged K / 4-token-interleaved V rows -> contiguous [n, Hkv*D] (cached-prefix prefill) vs torch
+    indexing of the same cache."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(4)
+    NB, Hkv, BS, D = 9, 2, 16, 128
+    kc = torch.randn(NB, Hkv, BS, D, device=gpu).to(torch.bfloat16)
+    vc = torch.randn(NB, Hkv, BS // 4, D, 4, device=gpu).to(torch.bfloat16)
+    slots = torch.tensor([0, 1, 2, 3, 5, 17, 31, 32, 70, 143, 100, 99], dtype=torch.int64, device=gpu)
+    k, v = ops.kv_gather(kc, vc, slots)
+    blk, off = slots // BS, slots % BS
+    k_ref = kc.permute(0, 2, 1, 3)[blk, off].reshape(len(slots), -1)
+    v_ref = vc.permute(0, 2, 4, 1, 3)[blk, off // 4, off % 4].reshape(len(slots), -1)
+    assert torch.equal(k, k_ref) and torch.equal(v, v_ref)
