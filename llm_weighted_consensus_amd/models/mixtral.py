@@ -39,7 +39,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from .config import DecoderConfig
-from .llama import LlamaModel, rope_tables
+from .llama import LlamaModel
 
 
 @dataclass

@@ -11,7 +11,6 @@ from typing import Annotated, Any, Dict, List, Literal, Optional, Union
 
 from pydantic import Field
 
-from ..utils import json as sjson
 from .base import Wire, first_some, push_opt_list, push_opt_num, push_opt_str
 
 # ============================================================================ request side

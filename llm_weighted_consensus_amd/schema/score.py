@@ -15,7 +15,7 @@ from pydantic import Field
 
 from ..errors import ResponseError
 from .base import Wire, first_some
-from .chat import (ChatCompletionChunk, Delta, FinishReason, Logprobs, Message, ServiceTier, StreamOptions, Tool,
+from .chat import (Delta, FinishReason, Logprobs, Message, ServiceTier, StreamOptions, Tool,
                    UnaryChoice, UnaryMessage, UsageRequest, Usage, push_choices)
 
 # ============================================================================ request

@@ -1,7 +1,7 @@
 """Score-choice conversions (reference src/score/completions/client.rs:1165-1289)."""
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import Optional
 
 from ..schema import chat as C
 from ..schema import score as S

@@ -22,7 +22,7 @@ from typing import Any, List, Optional
 import torch
 
 from .. import ops
-from ..errors import ChatError, ResponseError, ScoreError, StatusError
+from ..errors import ResponseError, ScoreError, StatusError
 from ..schema import chat as C
 from ..schema import score as S
 from .orchestrator import ChoiceIndexer, ScoreClient
