@@ -10,8 +10,8 @@
 //   K loop : register-staged, one LDS stage (next K-tile's global loads in flight under the current
 //            tile's MFMAs, written to LDS after a barrier; 4 workgroups per CU hide each other's stalls),
 //            16-byte chunks XOR-swizzled by row (conflict-free ds_read_b128 fragment reads).
-//   MFMA   : bf16: mfma_f32_16x16x32_bf16 (lane: row r16, k-chunk g); fp8: mfma_f32_16x16x32_fp8_fp8
-//            (8 fp8 per lane per k=32 step, so one 16 B LDS chunk holds two k-steps).
+//   MFMA   : bf16: mfma_f32_16x16x32_bf16 (lane: row r16, k-chunk g); fp8: the block-scaled
+//            mfma_scale_f32_16x16x128_f8f6f4 with unit scales (32 e4m3 per lane, whole 128 B k-slice).
 // Both operands are K-contiguous (torch.nn.functional.linear layout), so A and W tiles share one
 // staging / fragment code path.
 #include "common.h"
@@ -19,6 +19,7 @@
 namespace lwc {
 
 typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+typedef int v8i32 __attribute__((ext_vector_type(8)));
 
 constexpr int kGM = 128, kGN = 128;
 constexpr int kGKBytes = 128;          // bytes of K per tile row (64 bf16 or 128 fp8)
@@ -144,34 +145,50 @@ __global__ void __launch_bounds__(256, 3) grouped_gemm_kernel(GemmParams p) {
     if (kt + 1 < KT) gload(kt + 1);  // in flight under this tile's MFMAs
     const uint8_t* As = smem[0][0];
     const uint8_t* Ws = smem[0][1];
-    // two 16 B-chunk halves of the 128 B k-slice: bf16 -> 2 k-steps of 32; fp8 -> 4 k-steps of 32
+    if constexpr (FP8) {
+      // one block-scaled MFMA 16x16x128 (e4m3 x e4m3, unit e8m0 scales: the per-row / per-channel
+      // scales stay in the epilogue) per 16x16 tile covers the whole 128-byte k-slice: twice the fp8
+      // rate of four 16x16x32 MFMAs.  Lane group q holds the row's 16 B chunks q and 4+q for A and W
+      // alike, so both operands see the same k permutation and the dot product is unchanged.
+      uint4v b0[4], b1[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = 4 * s + q;
-      uint4v af[4], bfr[4];
+      for (int j = 0; j < 4; ++j) {
+        const int rb = wn * 64 + j * 16 + r16;
+        b0[j] = *reinterpret_cast<const uint4v*>(Ws + rb * kGKBytes + ((q ^ (rb & 7)) << 4));
+        b1[j] = *reinterpret_cast<const uint4v*>(Ws + rb * kGKBytes + (((4 + q) ^ (rb & 7)) << 4));
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ra = wm * 64 + i * 16 + r16;
-        af[i] = *reinterpret_cast<const uint4v*>(As + ra * kGKBytes + ((ch ^ (ra & 7)) << 4));
-        const int rb = wn * 64 + i * 16 + r16;
-        bfr[i] = *reinterpret_cast<const uint4v*>(Ws + rb * kGKBytes + ((ch ^ (rb & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
+        const uint4v a0 = *reinterpret_cast<const uint4v*>(As + ra * kGKBytes + ((q ^ (ra & 7)) << 4));
+        const uint4v a1 = *reinterpret_cast<const uint4v*>(As + ra * kGKBytes + (((4 + q) ^ (ra & 7)) << 4));
+        const v8i32 av = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if constexpr (FP8) {
-            // lane q holds k [16*ch, 16*ch + 16) of its row as 16 fp8; mfma fp8 16x16x32 takes 8 fp8 per
-            // lane, so the chunk feeds two MFMAs (bytes 0-7, then 8-15).  A and W use the same
-            // k -> (mfma, lane, slot) permutation, so the dot product is unchanged.
-            const long a0 = (long)af[i].x | ((long)af[i].y << 32), a1 = (long)af[i].z | ((long)af[i].w << 32);
-            const long b0 = (long)bfr[j].x | ((long)bfr[j].y << 32), b1 = (long)bfr[j].z | ((long)bfr[j].w << 32);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0, b0, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1, b1, acc[i][j], 0, 0, 0);
-          } else {
-            acc[i][j] = mfma_bf16(__builtin_bit_cast(short8, af[i]), __builtin_bit_cast(short8, bfr[j]), acc[i][j]);
-          }
+          const v8i32 bv = {(int)b0[j].x, (int)b0[j].y, (int)b0[j].z, (int)b0[j].w,
+                            (int)b1[j].x, (int)b1[j].y, (int)b1[j].z, (int)b1[j].w};
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc[i][j], 0, 0, 0, 127, 0, 127);
         }
+      }
+    } else {
+      // two 16 B-chunk halves of the 128 B k-slice: 2 k-steps of 32 bf16 each
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ch = 4 * s + q;
+        uint4v af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ra = wm * 64 + i * 16 + r16;
+          af[i] = *reinterpret_cast<const uint4v*>(As + ra * kGKBytes + ((ch ^ (ra & 7)) << 4));
+          const int rb = wn * 64 + i * 16 + r16;
+          bfr[i] = *reinterpret_cast<const uint4v*>(Ws + rb * kGKBytes + ((ch ^ (rb & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = mfma_bf16(__builtin_bit_cast(short8, af[i]), __builtin_bit_cast(short8, bfr[j]), acc[i][j]);
+      }
     }
   }
 
