@@ -52,6 +52,12 @@ def parse():
 def main():
     a = parse()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from llm_weighted_consensus_amd.parallel import launch
+
+    # `python bench.py --gpus N` without torchrun: this process only launches N ranks (never touches the GPU)
+    rc = launch.maybe_self_launch(a.gpus, __file__)
+    if rc is not None:
+        sys.exit(rc)
     from llm_weighted_consensus_amd.embeddings.consensus import EmbeddingConsensus
     from llm_weighted_consensus_amd.engine.engine import LLMEngine
     from llm_weighted_consensus_amd.engine.sampling import SamplingParams
@@ -64,8 +70,7 @@ def main():
 
     info = pdist.init_from_env("cuda")
     W, rank = info.world, info.rank
-    if W != a.gpus:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {W}", file=sys.stderr)
+    launch.check_world(a.gpus, W)
     dev = torch.device("cuda", info.local_rank)
     N, R = a.candidates, a.requests
     cp = a.cp or max(1, min(W, N // 32))
@@ -133,6 +138,7 @@ def main():
     answers = G * a.steps
     value = answers / elapsed
     emb_per_s = G * N * a.steps / elapsed
+    seen = pdist.world_size_seen()  # collective: ranks that actually took part in an all-reduce
     if a.profile_steps and rank == 0:
         print(f"# generate {gen_t / a.steps * 1e3:.1f} ms/step, score {score_t / a.steps * 1e3:.1f} ms/step, "
               f"decode steps {engine.stats['steps']}", file=sys.stderr)
@@ -146,6 +152,8 @@ def main():
             "value": round(value, 4),
             "unit": "answers/s",
             "n_gpus": W,
+            "backend": info.backend or "none (single process)",
+            "world_size": seen,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),

@@ -4,8 +4,8 @@
   encoder  config 2: bge-base-en-v1.5 bf16 on 1 MI355X, 64-candidate batches -> embeddings/s (+ the
            cosine-consensus GEMM per batch)
   moe      config 5: Mixtral-8x7B sampler (fp8 experts by default) + e5-mistral-7b embedder, N candidates
-           per request, embedding consensus -> answers/s.  Run under torchrun with --tp 2 for the TP=2
-           layout (heads and expert FFN split, RCCL all-reduce per row-parallel projection)
+           per request, embedding consensus -> answers/s.  `--tp 2` self-launches 2 ranks (or run it under
+           torchrun) for the TP=2 layout (heads and expert FFN split, RCCL all-reduce per row-parallel projection)
 
 (config 1 is the CPU plumbing test tests/test_server.py::test_config1_cpu_...; config 3 is
 `bench.py --candidates 32`; config 4 is `bench.py` under torchrun.)  Synthetic token ids and
@@ -130,6 +130,13 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if a.which == "moe" and a.tp > 1:
+        from llm_weighted_consensus_amd.parallel import launch
+
+        # `bench_configs.py moe --tp 2` without torchrun: launch the TP ranks (this process never touches the GPU)
+        rc = launch.maybe_self_launch(a.tp, __file__)
+        if rc is not None:
+            sys.exit(rc)
     if a.which == "encoder":
         a.requests = a.requests or 64
         out = bench_encoder(a)

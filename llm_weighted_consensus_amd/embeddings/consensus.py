@@ -25,6 +25,11 @@ class ConsensusResult:
     weights: torch.Tensor           # [R, N] softmax(centrality / tau)
     centrality: torch.Tensor        # [R, N]
     similarity: torch.Tensor        # [R, N, N]
+    # True when a failed candidate all-gather left this rank with only its own shard: best / weights then
+    # cover candidates [candidate_offset, candidate_offset + n_local) of each request; ``best`` is already
+    # mapped to the request's global candidate numbering
+    partial: bool = False
+    candidate_offset: int = 0
 
 
 def consensus_reference(E: torch.Tensor, tau: float) -> ConsensusResult:
@@ -72,8 +77,18 @@ class EmbeddingConsensus:
         flat = [c for req in requests for c in req]
         _, eb = self.embed(flat)
         E = eb.view(R, n_local, -1)
-        if gather:
+        partial = False
+        offset = 0
+        if gather and pdist.info().enabled:
             # a dead / hung peer must not take this rank's answers down: on a failed all-gather the group
-            # is aborted and the consensus runs over the local shard of candidates
-            E = pdist.guarded(gather_candidates, E, group, fallback=lambda: E)
-        return self.score_local(E.contiguous())
+            # is aborted and the consensus runs over the local shard of candidates (flagged as partial)
+            crank = pdist.dist.get_rank(group) if group is not None else pdist.info().rank
+            lost = []
+            E = pdist.guarded(gather_candidates, E, group, fallback=lambda: lost.append(1) or E)
+            if lost:
+                partial, offset = True, crank * n_local
+        res = self.score_local(E.contiguous())
+        if partial:
+            res.partial, res.candidate_offset = True, offset
+            res.best = [b + offset for b in res.best]
+        return res

@@ -178,6 +178,18 @@ def max_over_ranks(x: float, device=None) -> float:
     return float(t.item())
 
 
+def world_size_seen() -> int:
+    """Number of ranks that take part in one all-reduce of ones on the default group (collective; on
+    RCCL the tensor lives on this rank's GPU).  Reported in the bench line so a whole-node number can be
+    checked against the world the backend actually formed."""
+    if not _INFO.enabled:
+        return 1
+    dev = torch.device("cuda", _INFO.local_rank) if _INFO.backend == "nccl" else torch.device("cpu")
+    t = torch.ones(1, dtype=torch.int32, device=dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
 def broadcast_object(obj, src: int = 0):
     if not _INFO.enabled:
         return obj
@@ -210,14 +222,35 @@ def abort() -> None:
     _INFO = DistInfo(_INFO.rank, 1, _INFO.local_rank, None)
 
 
+_TRANSPORT_MARKERS = ("gloo", "transport", "nccl", "rccl", "timed out", "timeout", "connection", "closed by peer", "socket",
+                      "abort", "broken pipe", "reset by peer", "watchdog")
+
+
+def is_transport_error(e: BaseException) -> bool:
+    """True for failures of the collective transport itself (dead or hung peer, socket / RCCL error,
+    process-group timeout).  Local bugs — OOM, shape / dtype mismatches, bad arguments — are NOT: they
+    propagate unchanged and the process group stays up."""
+    if isinstance(e, torch.OutOfMemoryError):
+        return False
+    if isinstance(e, (dist.DistError, TimeoutError, ConnectionError)):
+        return True
+    if type(e) is RuntimeError:
+        msg = str(e).lower()
+        return any(m in msg for m in _TRANSPORT_MARKERS)
+    return False
+
+
 def guarded(fn, *args, fallback=None, **kw):
-    """Run a collective; on failure abort the group (see :func:`abort`) and return ``fallback()`` (or
-    raise :class:`CollectiveFailure` when no fallback is given).  Failure detection is the process
-    group's own timeout (``init_from_env(timeout_s=...)``, ``LWC_COLLECTIVE_TIMEOUT_S``) plus the
-    transport noticing a dead peer — whichever comes first."""
+    """Run a collective; on a TRANSPORT failure (:func:`is_transport_error`) abort the group (see
+    :func:`abort`) and return ``fallback()`` (or raise :class:`CollectiveFailure` when no fallback is
+    given).  Any other exception is re-raised untouched.  Failure detection is the process group's own
+    timeout (``init_from_env(timeout_s=...)``, ``LWC_COLLECTIVE_TIMEOUT_S``) plus the transport noticing a
+    dead peer — whichever comes first."""
     try:
         return fn(*args, **kw)
-    except Exception as e:  # noqa: BLE001 - any transport / timeout error
+    except Exception as e:  # noqa: BLE001 - classified below
+        if not is_transport_error(e):
+            raise
         abort()
         if fallback is None:
             raise CollectiveFailure(f"collective {getattr(fn, '__name__', fn)} failed: {e}") from e

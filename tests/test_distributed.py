@@ -176,3 +176,117 @@ def test_guarded_without_fallback_raises():
     with pytest.raises(pdist.CollectiveFailure):
         pdist.guarded(boom)
     assert pdist.guarded(lambda: 7) == 7
+
+
+def _world8_worker(rank, world, port, out_q):
+    """The bench's exact multi-GPU layout at world 8: cp=2 candidate groups x dp=4 request groups."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from llm_weighted_consensus_amd.embeddings.consensus import consensus_reference, gather_candidates
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+    from llm_weighted_consensus_amd.parallel.prefill_share import all_gather_prefills
+
+    pdist.init_from_env("cpu")
+    cp = 2
+    cgroup, gidx, crank = pdist.candidate_groups(cp)
+    ok = (gidx, crank) == (rank // cp, rank % cp)
+    # C4 inside the candidate group: each rank prefilled R=2 prompts of its group's 4 (3 blocks each)
+    R, L, E, V, nb = 2, 2, 4, 5, 3
+    kv = torch.stack([torch.full((L, 2, E), 1000.0 * rank + b) for b in range(R * nb)], dim=2)
+    lg = torch.stack([torch.full((V,), 10.0 * rank + i) for i in range(R)])
+    shared = all_gather_prefills(kv, lg, [nb] * R, group=cgroup)
+    ok &= len(shared) == R * cp
+    for j, (k, l) in enumerate(shared):
+        src = gidx * cp + j // R          # global rank that prefilled group prompt j
+        ok &= bool((l == 10.0 * src + j % R).all()) and bool((k[0, 0, :, 0] == 1000.0 * src + (j % R) * nb
+                                                            + torch.arange(nb)).all())
+    # C1 inside the candidate group: rank shard = candidates [crank*n_local, (crank+1)*n_local)
+    N, d = 8, 16
+    g = torch.Generator().manual_seed(7 + gidx)   # one candidate set per request group
+    full = torch.nn.functional.normalize(torch.randn(R * cp, N, d, generator=g), dim=-1)
+    n_local = N // cp
+    got = gather_candidates(full[:, crank * n_local:(crank + 1) * n_local].contiguous(), cgroup)
+    ok &= torch.equal(got, full)
+    ok &= consensus_reference(got, 0.1).best == consensus_reference(full, 0.1).best
+    seen = pdist.world_size_seen()
+    ok &= pdist.max_over_ranks(float(rank)) == world - 1
+    out_q.put((rank, bool(ok), seen))
+    pdist.shutdown()
+
+
+def test_bench_layout_cp2_dp4_world8_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world8_worker, args=(r, 8, port, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[0] for r in res] == list(range(8))
+    assert all(ok for _, ok, _ in res), res
+    assert all(seen == 8 for _, _, seen in res)
+
+
+def test_guarded_reraises_local_errors_without_abort():
+    """Only transport failures abort the group; OOM / shape bugs propagate unchanged."""
+    from llm_weighted_consensus_amd.parallel import dist as pdist
+
+    def shape_bug():
+        raise RuntimeError("shape '[3, 4]' is invalid for input of size 7")
+
+    def oom():
+        raise torch.OutOfMemoryError("HIP out of memory")
+
+    with pytest.raises(RuntimeError, match="invalid for input"):
+        pdist.guarded(shape_bug, fallback=lambda: 0)
+    with pytest.raises(torch.OutOfMemoryError):
+        pdist.guarded(oom, fallback=lambda: 0)
+    with pytest.raises(ValueError):
+        pdist.guarded(lambda: (_ for _ in ()).throw(ValueError("bad")), fallback=lambda: 0)
+    assert pdist.is_transport_error(RuntimeError("[gloo/transport/tcp/pair.cc:547] Connection closed by peer"))
+    assert pdist.is_transport_error(torch.distributed.DistBackendError("NCCL error: unhandled system error"))
+
+
+_LAUNCH_CHILD = r'''
+import os, sys, torch
+sys.path.insert(0, sys.argv[1])
+from llm_weighted_consensus_amd.parallel import dist as pdist
+info = pdist.init_from_env("cpu")
+seen = pdist.world_size_seen()
+if info.rank == 0:
+    print("WORLD", info.world, seen, info.backend, flush=True)
+if len(sys.argv) > 2 and int(sys.argv[2]) == info.rank:
+    sys.exit(3)
+pdist.barrier()
+pdist.shutdown()
+'''
+
+
+def test_self_launch_spawns_ranks(tmp_path):
+    """`bench.py --gpus N` self-launch: the launcher starts N ranks with torchrun-style env over 127.0.0.1
+    and returns the worst exit status."""
+    import subprocess
+    import sys
+
+    from llm_weighted_consensus_amd.parallel import launch
+
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "child.py"
+    script.write_text(_LAUNCH_CHILD)
+    out = tmp_path / "out.txt"
+    code = ("import sys; sys.path.insert(0, %r); from llm_weighted_consensus_amd.parallel import launch; "
+            "sys.exit(launch.launch(3, [sys.executable, %r, %r]))" % (ROOT, str(script), ROOT))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "WORLD 3 3 gloo" in r.stdout
+    # a failing rank makes the launcher fail (the others are stopped, not left hanging in a collective)
+    code_fail = code.replace("%r]))" % ROOT, "%r, '1']))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code_fail], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    with pytest.raises(SystemExit):
+        launch.check_world(8, 1)
+    launch.check_world(2, 2)
