@@ -122,7 +122,7 @@ class LocalChatClient(ChatClient):
         constraint, tool_name = None, None
         rf = req.response_format
         if isinstance(rf, C.ResponseFormatJsonSchema) and rf.json_schema.schema_ is not None:
-            constraint = constraint_for_schema(rf.json_schema.schema_, tok.eos_token_id)
+            constraint = constraint_for_schema(rf.json_schema.schema_, tok, V)
         tc = req.tool_choice
         if isinstance(tc, C.ToolChoiceFunction) and req.tools:
             tool = next((t for t in req.tools if t.function.name == tc.function.name), None)
@@ -130,7 +130,7 @@ class LocalChatClient(ChatClient):
                 raise ChatError.invalid_request(f"tool_choice names an unknown function: {tc.function.name}")
             tool_name = tool.function.name
             if tool.function.parameters is not None:
-                constraint = constraint_for_schema(tool.function.parameters, tok.eos_token_id)
+                constraint = constraint_for_schema(tool.function.parameters, tok, V)
         top_lp = int(req.top_logprobs or 0) if req.logprobs else 0
         return SamplingParams(
             temperature=1.0 if req.temperature is None else float(req.temperature),

@@ -5,11 +5,21 @@ schema built in src/score/completions/client.rs:1299-1339, always `strict: true`
 object with an enum `response_key` and, with synthetic reasoning, a free-text `_think` first.  It is
 compiled to a sequence of segments — literal bytes, a JSON string body, or a choice among literal
 alternatives (a byte trie) — and the engine applies the mask produced for each step inside the fused
-sampler kernel (the `mask` operand).  Works on the byte-level tokenizer (token id == byte for
-0..255); multi-byte synthetic tokens are never allowed inside a constrained span.
+sampler kernel (the `mask` operand).
+
+The FSM runs over BYTES; the sampler masks TOKENS.  :class:`TokenConstraint` bridges the two for any
+tokenizer exposing exact per-token bytes (``token_bytes``: the byte tokenizer, byte-level BPE,
+SentencePiece with byte fallback): a token is allowed in a state iff the FSM accepts ALL of its bytes
+from that state, and the state advances by the token's bytes.  Allowed sets are computed against a
+sorted byte-string index of the vocabulary (a trie walked by bisection, guided by the FSM's allowed
+bytes) and, for free-string states, vectorised over the whole vocabulary (a token stays inside a JSON
+string iff every byte is string-safe; only tokens whose first unsafe byte can close the string are
+walked one by one).  Masks are cached per FSM state equivalence class.
 """
 from __future__ import annotations
 
+import bisect
+import hashlib
 import json
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
@@ -48,7 +58,6 @@ def _trie(options: Sequence[bytes]) -> Dict:
 
 # printable ASCII minus the quote and backslash: keeps constrained text valid UTF-8 and valid JSON
 _STR_ALLOWED = np.array([1 if (0x20 <= b < 0x7F and b not in (0x22, 0x5C)) else 0 for b in range(256)], dtype=bool)
-_POW2 = (np.uint64(1) << np.arange(32, dtype=np.uint64))
 
 
 class SegmentConstraint:
@@ -126,17 +135,6 @@ class SegmentConstraint:
             return self.advance(self._normalize((i + 1, 0)), token)
         return (len(self.segments), 0)
 
-    def mask(self, st, vocab_size: int) -> np.ndarray:
-        """uint32 bitmask [vocab_size/32] for the sampler kernel."""
-        allowed, eos = self.allowed_bytes(st)
-        bits = np.zeros(vocab_size, dtype=bool)
-        bits[:256] = allowed
-        if eos and 0 <= self.eos_id < vocab_size:
-            bits[self.eos_id] = True
-        if not bits.any():  # dead end: allow EOS so the sequence can stop
-            bits[self.eos_id] = True
-        return (bits.reshape(-1, 32).astype(np.uint64) @ _POW2).astype(np.uint32)
-
 
 def _lit(s: str) -> Lit:
     return Lit(s.encode("utf-8"))
@@ -162,7 +160,7 @@ def compile_json_schema(schema: Any) -> Optional[List[Segment]]:
         if "enum" in p and all(isinstance(e, str) for e in p["enum"]):
             segs.append(Alt([json.dumps(e, ensure_ascii=False).encode("utf-8") for e in p["enum"]]))
         elif p.get("type") == "string":
-            segs += [_lit('"'), Str(), _lit('"')]
+            segs += [_lit('"'), Str(int(p.get("maxLength", 2048))), _lit('"')]
         elif p.get("type") == "boolean":
             segs.append(Alt([b"true", b"false"]))
         else:
@@ -171,6 +169,166 @@ def compile_json_schema(schema: Any) -> Optional[List[Segment]]:
     return segs
 
 
-def constraint_for_schema(schema: Any, eos_id: int) -> Optional[SegmentConstraint]:
+class TokenVocab:
+    """Per-tokenizer index for token-level masks (built once per tokenizer and model vocab, cached on the
+    tokenizer object): exact token bytes, a lexicographically sorted byte-string index (the vocabulary
+    trie: a node is a contiguous range), per token the position and value of its first JSON-string-unsafe
+    byte.  Ids with no bytes (specials, padding ids beyond the tokenizer) are never allowed."""
+
+    def __init__(self, tok, vocab_size: int):
+        self.vocab_size = vocab_size
+        n_tok = min(vocab_size, getattr(tok, "vocab_size", vocab_size))
+        self.tb: List[bytes] = [tok.token_bytes(i) for i in range(n_tok)] + [b""] * (vocab_size - n_tok)
+        ids = [i for i, b in enumerate(self.tb) if b]
+        ids.sort(key=lambda i: self.tb[i])
+        self.keys = [self.tb[i] for i in ids]
+        self.ids = ids
+        self.max_len = max((len(b) for b in self.keys), default=1)
+        self.lens = np.array([len(b) for b in self.tb], dtype=np.int64)
+        fu = np.zeros(vocab_size, dtype=np.int64)   # index of the first string-unsafe byte (= len if none)
+        fub = np.zeros(vocab_size, dtype=np.int64)  # that byte (0 if none)
+        for i, b in enumerate(self.tb):
+            if not b:
+                continue
+            arr = np.frombuffer(b, dtype=np.uint8)
+            bad = np.nonzero(~_STR_ALLOWED[arr])[0]
+            fu[i] = bad[0] if len(bad) else len(b)
+            fub[i] = arr[bad[0]] if len(bad) else 0
+        self.first_unsafe, self.first_unsafe_byte = fu, fub
+        self.nonempty = self.lens > 0
+
+    @staticmethod
+    def of(tok, vocab_size: int) -> "TokenVocab":
+        cache = tok.__dict__.setdefault("_lwc_token_vocab", {})
+        tv = cache.get(vocab_size)
+        if tv is None:
+            tv = cache[vocab_size] = TokenVocab(tok, vocab_size)
+        return tv
+
+    def child_range(self, lo: int, hi: int, depth: int, b: int) -> Tuple[int, int]:
+        """Sub-range of [lo, hi) (all sharing a prefix of length ``depth``) whose byte ``depth`` is ``b``."""
+        keys = self.keys
+        pre = keys[lo][:depth] if lo < hi else b""
+        a = bisect.bisect_left(keys, pre + bytes([b]), lo, hi)
+        z = bisect.bisect_left(keys, pre + bytes([b + 1]), a, hi) if b < 255 else hi
+        return a, z
+
+
+class TokenConstraint:
+    """Token-level view of a byte FSM (:class:`SegmentConstraint`) for one tokenizer.  The engine calls
+    ``start`` / ``advance(state, token_id)`` / ``is_done`` and ``mask_entry(state) -> (digest, uint32
+    [V/32] bitmask)``; masks are cached per state equivalence class."""
+
+    def __init__(self, fsm: SegmentConstraint, vocab: TokenVocab):
+        self.fsm = fsm
+        self.vocab = vocab
+        self.eos_id = fsm.eos_id
+        self._masks: Dict[Any, Tuple[bytes, np.ndarray]] = {}
+
+    def start(self):
+        return self.fsm.start()
+
+    def is_done(self, st) -> bool:
+        return self.fsm.is_done(st)
+
+    def advance_bytes(self, st, data: bytes):
+        """State after consuming ``data``, or None if the FSM rejects a byte."""
+        fsm = self.fsm
+        for b in data:
+            allowed, _ = fsm.allowed_bytes(st)
+            if not allowed[b]:
+                return None
+            st = fsm.advance(st, b)
+        return st
+
+    def advance(self, st, token: int):
+        if token == self.eos_id or not (0 <= token < self.vocab.vocab_size):
+            return (len(self.fsm.segments), 0)
+        nxt = self.advance_bytes(st, self.vocab.tb[token])
+        return (len(self.fsm.segments), 0) if nxt is None else nxt
+
+    # ---- masks
+    def _key(self, st):
+        i, local = st
+        segs = self.fsm.segments
+        if i >= len(segs):
+            return ("done",)
+        seg = segs[i]
+        if isinstance(seg, Str):  # only the remaining length matters, and only up to the longest token
+            return (i, "str", min(seg.max_len - local, self.vocab.max_len + 1))
+        if isinstance(seg, Alt):
+            return (i, "alt", id(local))
+        return (i, "lit", local)
+
+    def allowed_tokens(self, st) -> Tuple[np.ndarray, bool]:
+        """(bool [V] allowed tokens, eos allowed) in FSM state ``st``."""
+        fsm, tv = self.fsm, self.vocab
+        V = tv.vocab_size
+        ok = np.zeros(V, dtype=bool)
+        if fsm.is_done(st):
+            return ok, True
+        i, local = st
+        seg = fsm.segments[i]
+        if isinstance(seg, Str):
+            room = seg.max_len - local
+            # tokens that stay inside the string: every byte string-safe and the length fits
+            ok |= tv.nonempty & (tv.first_unsafe == tv.lens) & (tv.lens <= room)
+            # tokens that close the string: a safe prefix, then a byte the FSM accepts to end it
+            allowed, _ = fsm.allowed_bytes(st)
+            cand = np.nonzero(tv.nonempty & (tv.first_unsafe < tv.lens) & (tv.first_unsafe <= room)
+                              & allowed[tv.first_unsafe_byte])[0]
+            for t in cand.tolist():
+                k = int(tv.first_unsafe[t])
+                if self.advance_bytes((i, local + k), tv.tb[t][k:]) is not None:
+                    ok[t] = True
+            return ok, False
+        # literal / alternative states: walk the vocabulary trie guided by the FSM's allowed bytes
+        stack = [(st, 0, len(tv.keys), 0)]
+        ids, keys = tv.ids, tv.keys
+        while stack:
+            cur, lo, hi, depth = stack.pop()
+            while lo < hi and len(keys[lo]) == depth:  # tokens ending exactly here were fully accepted
+                if depth:
+                    ok[ids[lo]] = True
+                lo += 1
+            if lo >= hi or fsm.is_done(cur):
+                continue
+            ci, clocal = cur
+            if isinstance(fsm.segments[ci], Str):
+                # entered a free string mid-token: finish the (few) tokens of this subtree one by one
+                for k in range(lo, hi):
+                    if self.advance_bytes(cur, keys[k][depth:]) is not None:
+                        ok[ids[k]] = True
+                continue
+            allowed, _ = fsm.allowed_bytes(cur)
+            for b in np.nonzero(allowed)[0].tolist():
+                a, z = tv.child_range(lo, hi, depth, b)
+                if a < z:
+                    stack.append((fsm.advance(cur, b), a, z, depth + 1))
+        return ok, False
+
+    def mask_entry(self, st) -> Tuple[bytes, np.ndarray]:
+        """(content digest, uint32 bitmask [V/32]) for the sampler's mask table."""
+        key = self._key(st)
+        hit = self._masks.get(key)
+        if hit is not None:
+            return hit
+        ok, eos = self.allowed_tokens(st)
+        if (eos or not ok.any()) and 0 <= self.eos_id < ok.shape[0]:
+            ok[self.eos_id] = True  # done, or a dead end: EOS lets the sequence stop
+        words = np.packbits(ok, bitorder="little").view(np.uint32)
+        hit = (hashlib.blake2b(words.tobytes(), digest_size=16).digest(), words)
+        self._masks[key] = hit
+        return hit
+
+
+def constraint_for_schema(schema: Any, tok, vocab_size: Optional[int] = None) -> Optional[TokenConstraint]:
+    """Schema -> token-level constraint for ``tok`` (``vocab_size`` = the model's logits width, which may
+    exceed the tokenizer's vocabulary; defaults to the tokenizer's)."""
     segs = compile_json_schema(schema)
-    return SegmentConstraint(segs, eos_id) if segs is not None else None
+    if segs is None:
+        return None
+    V = vocab_size or tok.vocab_size
+    if V % 32:
+        raise ValueError(f"vocab size {V} is not a multiple of 32 (mask words)")
+    return TokenConstraint(SegmentConstraint(segs, tok.eos_token_id), TokenVocab.of(tok, V))

@@ -711,9 +711,9 @@ class LLMEngine:
     def _constraint_masks(self, seqs: List[Sequence], cons: List[int]):
         """(mask table [rows, V/32] int32 on the device, per-sequence row [B] int32).
 
-        Constrained spans only ever allow raw bytes (ids < 256) and EOS, so a mask is determined by its
-        256 allowed bytes + the EOS flag.  Masks are keyed by that content: every distinct mask is built
-        and uploaded ONCE into a device-resident table (the voters of a score request, each with its own
+        Each constraint maps its FSM state to a cached full-vocabulary token mask + content digest
+        (:meth:`TokenConstraint.mask_entry`).  Masks are keyed by that digest: every distinct mask is
+        uploaded ONCE into a device-resident table (the voters of a score request, each with its own
         shuffled key enum, still share most states: '{', the property name, quotes, ...), and a step
         uploads only the B row indices."""
         if self._mask_rows_of is None:
@@ -721,15 +721,9 @@ class LLMEngine:
             self._mask_table = torch.zeros(64, self.cfg.vocab_size // 32, dtype=torch.int32, device=self.device)
         rows = np.full(len(seqs), -1, dtype=np.int32)
         new: List[Tuple[int, np.ndarray]] = []
-        words = self.cfg.vocab_size // 32
         for i in cons:
             s = seqs[i]
-            c = s.params.constraint
-            allowed, eos = c.allowed_bytes(s.constraint_state)
-            if not allowed.any():
-                eos = True  # dead end: allow EOS so the sequence can stop
-            packed = np.packbits(allowed, bitorder="little")  # 32 bytes = words 0..7
-            key = (packed.tobytes(), bool(eos), c.eos_id)
+            key, m = s.params.constraint.mask_entry(s.constraint_state)
             r = self._mask_rows_of.get(key)
             if r is None:
                 if len(self._mask_rows_of) >= self._mask_limit:  # bounded: start the table over
@@ -737,10 +731,6 @@ class LLMEngine:
                     return self._constraint_masks(seqs, cons)
                 r = len(self._mask_rows_of)
                 self._mask_rows_of[key] = r
-                m = np.zeros(words, dtype=np.uint32)
-                m[:8] = packed.view(np.uint32)
-                if eos and 0 <= c.eos_id < self.cfg.vocab_size:
-                    m[c.eos_id >> 5] |= np.uint32(1 << (c.eos_id & 31))
                 new.append((r, m))
             rows[i] = r
         if new:

@@ -32,7 +32,8 @@ class SamplingParams:
     # (EngineGroup): candidate i draws with seed*1000003 + seed_offset + i on whichever GPU runs it
     seed_offset: int = 0
     logit_bias: Optional[Dict[int, float]] = None
-    # constrained decoding: an object with .mask(state) / .advance(state, token) / .start()
+    # constrained decoding (engine/constraints.py TokenConstraint): .start() / .advance(state, token) /
+    # .is_done(state) / .mask_entry(state)
     constraint: Optional[object] = None
 
     @property

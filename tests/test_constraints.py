@@ -1,0 +1,135 @@
+"""Token-level constrained decoding (K8d host side) over REAL tokenizers: byte-level BPE (Llama-3 family)
+and SentencePiece with byte fallback (Llama-2 / Mistral family), both built offline by `tokenizers`, plus
+the byte tokenizer.  The score voters' json_schema / tool_call schemas (reference
+src/score/completions/client.rs:1299-1339) must only ever produce parseable JSON with a valid
+response key, whatever the tokenizer's id layout is.
+
+Soundness and completeness are checked by brute force against the byte FSM: a token is allowed in a
+state iff the FSM accepts all its bytes from that state."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+from llm_weighted_consensus_amd.engine.constraints import TokenVocab, compile_json_schema, constraint_for_schema
+from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer, HFTokenizer
+from llm_weighted_consensus_amd.score.orchestrator import response_key_format
+
+pytest.importorskip("tokenizers")
+from tests.test_tokenizers import _bytelevel, _sentencepiece  # noqa: E402
+
+KEYS = ["`A`", "`B`", "`C`", "`T`"]
+
+
+def _schema(think: bool, max_len=None):
+    s = response_key_format(KEYS, think).json_schema.schema_
+    if think and max_len:
+        s = json.loads(json.dumps(s))
+        s["properties"]["_think"]["maxLength"] = max_len
+    return s
+
+
+def _tokenizers(tmp_path):
+    bl = HFTokenizer(_bytelevel(tmp_path), bos_token_id=0, eos_token_id=1)
+    sp = HFTokenizer(_sentencepiece(tmp_path), bos_token_id=1, eos_token_id=2)
+    return {"bytelevel": (bl, 416), "sentencepiece": (sp, 608), "byte": (ByteTokenizer(512), 512)}
+
+
+def _walk(c, rng, max_steps=400, close_bias=0.25):
+    """Random walk over the allowed tokens; returns the emitted token ids (EOS excluded)."""
+    st = c.start()
+    out = []
+    for _ in range(max_steps):
+        ok, eos = c.allowed_tokens(st)
+        if c.is_done(st):
+            assert eos
+            return out
+        ids = np.nonzero(ok)[0].tolist()
+        assert ids, "dead end before the schema completed"
+        closing = [t for t in ids if b'"' in c.vocab.tb[t]]
+        t = rng.choice(closing if closing and rng.random() < close_bias else ids)
+        st = c.advance(st, t)
+        out.append(t)
+    raise AssertionError("schema did not complete")
+
+
+@pytest.mark.parametrize("kind", ["bytelevel", "sentencepiece", "byte"])
+@pytest.mark.parametrize("think", [False, True])
+def test_constrained_walk_is_valid_json(tmp_path, kind, think):
+    tok, V = _tokenizers(tmp_path)[kind]
+    c = constraint_for_schema(_schema(think, max_len=24), tok, V)
+    rng = random.Random(1)
+    for _ in range(30):
+        ids = _walk(c, rng)
+        text = b"".join(c.vocab.tb[t] for t in ids).decode("utf-8")
+        obj = json.loads(text)
+        assert obj["response_key"] in KEYS
+        assert list(obj) == (["_think", "response_key"] if think else ["response_key"])
+        # the tokenizer's own detokenisation agrees (ids are real ids of this vocabulary)
+        if kind != "byte":
+            assert tok.decode(ids) == text
+
+
+@pytest.mark.parametrize("kind", ["bytelevel", "sentencepiece"])
+def test_token_masks_sound_and_complete(tmp_path, kind):
+    """Every state reached on a walk: allowed == {t : FSM accepts bytes(t)} by brute force."""
+    tok, V = _tokenizers(tmp_path)[kind]
+    c = constraint_for_schema(_schema(True, max_len=12), tok, V)
+    rng = random.Random(3)
+    st = c.start()
+    seen = 0
+    while not c.is_done(st):
+        ok, _ = c.allowed_tokens(st)
+        brute = np.array([bool(c.vocab.tb[t]) and c.advance_bytes(st, c.vocab.tb[t]) is not None
+                          for t in range(V)])
+        assert np.array_equal(ok, brute), np.nonzero(ok != brute)[0][:10]
+        ids = np.nonzero(ok)[0].tolist()
+        st = c.advance(st, rng.choice(ids))
+        seen += 1
+    assert seen > 3
+
+
+def test_ids_0_255_are_not_bytes_for_real_tokenizers(tmp_path):
+    """The round-1 bug: masks over ids 0..255 as raw bytes.  With byte-level BPE, id 123 is not '{'."""
+    tok, V = _tokenizers(tmp_path)["bytelevel"]
+    c = constraint_for_schema(_schema(False), tok, V)
+    ok, _ = c.allowed_tokens(c.start())
+    allowed = [c.vocab.tb[t] for t in np.nonzero(ok)[0]]
+    assert allowed and all(b.startswith(b"{") for b in allowed)
+    brace_ids = tok.ids_for_text("{")
+    assert ok[brace_ids[0]] and brace_ids[0] != ord("{") or ok[ord("{")]
+    # the mask entry packs the same set, plus nothing else
+    _, words = c.mask_entry(c.start())
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little").astype(bool)
+    assert np.array_equal(bits[:V], ok)
+
+
+def test_multi_segment_tokens_allowed(tmp_path):
+    """Merged tokens that span segment boundaries (e.g. '{"' or '"response_key') are allowed, not just single bytes."""
+    tok, V = _tokenizers(tmp_path)["bytelevel"]
+    c = constraint_for_schema(_schema(False), tok, V)
+    ok, _ = c.allowed_tokens(c.start())
+    lens = [len(c.vocab.tb[t]) for t in np.nonzero(ok)[0]]
+    assert max(lens) > 1, [c.vocab.tb[t] for t in np.nonzero(ok)[0]]
+
+
+def test_string_room_and_mask_cache(tmp_path):
+    tok, V = _tokenizers(tmp_path)["byte"]
+    c = constraint_for_schema(_schema(True, max_len=6), tok, V)
+    st = c.advance_bytes(c.start(), b'{"_think":"abcdef')
+    ok, _ = c.allowed_tokens(st)
+    assert {c.vocab.tb[t] for t in np.nonzero(ok)[0]} == {b'"'}  # no room left: only the closing quote
+    st2 = c.advance_bytes(c.start(), b'{"_think":"a')
+    st3 = c.advance_bytes(c.start(), b'{"_think":"b')
+    assert c.mask_entry(st2)[0] == c.mask_entry(st3)[0]
+    assert c._key(st2) == c._key(st3)
+    assert c.advance(st, tok.eos_token_id)[0] == len(c.fsm.segments)
+
+
+def test_token_vocab_cached_per_tokenizer(tmp_path):
+    tok, V = _tokenizers(tmp_path)["sentencepiece"]
+    assert TokenVocab.of(tok, V) is TokenVocab.of(tok, V)
+    assert compile_json_schema({"type": "array"}) is None
+    with pytest.raises(ValueError):
+        constraint_for_schema(_schema(False), tok, 607)

@@ -57,7 +57,12 @@ def test_group_worker_death_reschedules_or_fails():
             loop = asyncio.get_running_loop()
             q = asyncio.Queue()
             g.submit([1], sp, 4, loop, q)
-            ev = await asyncio.wait_for(q.get(), 120)  # tokens are flowing on both workers
+            # kill worker 0 only once ITS portion (choices 0-1 of 4) has started streaming: an unstarted
+            # portion would be rescheduled instead of failing (a loaded host can start worker 1 first)
+            while True:
+                ev = await asyncio.wait_for(q.get(), 120)
+                if not isinstance(ev, EngineFailure) and ev.seq.index < 2:
+                    break
             os.kill(victim.pid, signal.SIGKILL)
             while True:
                 ev = await asyncio.wait_for(q.get(), 120)

@@ -145,3 +145,43 @@ def test_decoder_embedder_served_from_embed_models(gpu):
         assert abs(n - 1.0) < 1e-2
         assert data[0]["embedding"] == data[2]["embedding"]  # same text -> same row (cache or not)
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("kind", ["bytelevel", "sentencepiece"])
+def test_constrained_voters_with_real_tokenizer(gpu, tmp_path, kind):
+    """json_schema and tool_call voters on a model served with a REAL tokenizer.json (built offline):
+    token-level masks from the tokenizer's bytes, so every voter emits parseable JSON with a valid key
+    and a vote (round-1 masks assumed id == byte and produced garbage here)."""
+    from llm_weighted_consensus_amd.server.app import create_app
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+    from tests.test_tokenizers import _bytelevel, _sentencepiece
+
+    path = (_bytelevel if kind == "bytelevel" else _sentencepiece)(tmp_path)
+    models = {"tiny": dict(MODELS["tiny"], tokenizer=path)}
+    state = build_state(Config(models=models, kv_fraction=0.05))
+    c = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t", timeout=120)
+    req = {"messages": [{"role": "user", "content": "Which city is the capital of France?"}],
+           "model": {"llms": [{"model": "tiny", "output_mode": "json_schema", "top_logprobs": 5},
+                              {"model": "tiny", "output_mode": "json_schema", "top_logprobs": 5, "temperature": 1.5},
+                              {"model": "tiny", "output_mode": "tool_call", "top_logprobs": 5}]},
+           "choices": ["Paris", "Madrid", "Rome"]}
+
+    async def go():
+        r = await c.post("/score/completions", json=req)
+        assert r.status_code == 200, r.text
+        body = r.json()
+        voters = [ch for ch in body["choices"] if ch["index"] >= 3]
+        assert len(voters) == 3
+        for v in voters:
+            assert v.get("error") is None, v
+            msg = v["message"]
+            text = msg["content"] if msg.get("content") else msg["tool_calls"][0]["function"]["arguments"]
+            obj = json.loads(text)
+            assert obj["response_key"] in ("`A`", "`B`", "`C`"), text
+            assert v["vote"] is not None and sum(v["vote"]) == pytest.approx(1.0, abs=1e-6)
+
+    try:
+        asyncio.run(go())
+    finally:
+        _close(state)
