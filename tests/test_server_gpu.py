@@ -179,7 +179,7 @@ def test_constrained_voters_with_real_tokenizer(gpu, tmp_path, kind):
             text = msg["content"] if msg.get("content") else msg["tool_calls"][0]["function"]["arguments"]
             obj = json.loads(text)
             assert obj["response_key"] in ("`A`", "`B`", "`C`"), text
-            assert v["vote"] is not None and sum(v["vote"]) == pytest.approx(1.0, abs=1e-6)
+            assert msg["vote"] is not None and sum(msg["vote"]) == pytest.approx(1.0, abs=1e-6)
 
     try:
         asyncio.run(go())
