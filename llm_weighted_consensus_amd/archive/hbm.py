@@ -72,7 +72,9 @@ class ResidentEmbeddings:
 
     def put(self, keys: Sequence[bytes], emb: torch.Tensor) -> None:
         """Insert rows (evicting least-recently-used rows when the slab is full).  Keys already present are
-        refreshed, not duplicated.  Rows beyond the capacity are simply not stored."""
+        refreshed, not duplicated.  At most ``capacity`` NEW keys are stored per call (the excess is skipped):
+        otherwise a key inserted earlier in the same call could be evicted and its slot handed to a later
+        key, leaving two rows of one index_copy_ aimed at one slot."""
         if self.capacity == 0 or not keys:
             return
         rows, slots = [], []
@@ -80,6 +82,8 @@ class ResidentEmbeddings:
             for i, k in enumerate(keys):
                 if k in self._slots:
                     self._slots.move_to_end(k)
+                    continue
+                if len(rows) >= self.capacity:
                     continue
                 if not self._free:
                     if not self._slots:

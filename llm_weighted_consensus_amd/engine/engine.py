@@ -392,6 +392,17 @@ class LLMEngine:
         last-token logits [len(prompts), V].  With ``use_cache`` the prompts' cached prefix blocks are
         taken from the prefix cache and only the tails are computed (attention still sees the whole
         prompt), and the prompts' full blocks are registered for later requests."""
+        added: List[int] = []
+        try:
+            return self._run_prefill_inner(prompts, parents, use_cache, added)
+        except BaseException:
+            # a later prompt of the wave ran out of KV blocks (or the prefill failed): release the transient
+            # parents already created and the cached blocks they acquired, then re-raise
+            for pid in added:
+                self.bm.free_sequence(pid)
+            raise
+
+    def _run_prefill_inner(self, prompts, parents, use_cache, added) -> torch.Tensor:
         dev = self.device
         toks, pos, slots, cu, last, cached = [], [], [], [0], [], []
         for pid, p in zip(parents, prompts):
@@ -399,6 +410,7 @@ class LLMEngine:
             c = int(self.bm.add_sequence_cached(pid, p)) if use_cache else 0
             if not use_cache:
                 self.bm.add_sequence(pid, L)
+            added.append(pid)
             cached.append(c)
             toks.extend(p[c:])
             pos.extend(range(c, L))

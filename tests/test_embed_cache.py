@@ -67,3 +67,23 @@ def test_service_cache_matches_uncached_encoder():
     assert torch.allclose(again, ref[[3, 0]], atol=1e-6)
     st = cached.cache.stats()
     assert st["entries"] == 3 and st["hits"] == 2 and st["misses"] == 4  # an in-call repeat counts as a miss
+
+
+def test_put_more_misses_than_capacity_keeps_rows_consistent():
+    """More new keys in one put() than the slab holds: no slot is written twice, every stored key maps to
+    its own row."""
+    import torch
+
+    from llm_weighted_consensus_amd.archive.hbm import ResidentEmbeddings
+
+    r = ResidentEmbeddings(4, "cpu", budget_bytes=3 * 4 * 4)
+    assert r.capacity == 3
+    r.put([b"old"], torch.full((1, 4), -1.0))
+    keys = [bytes([i]) * 16 for i in range(5)]
+    emb = torch.arange(5, dtype=torch.float32)[:, None].repeat(1, 4)
+    r.put(keys, emb)
+    slots = r.lookup(keys)
+    stored = [(i, s) for i, s in enumerate(slots) if s is not None]
+    assert len(stored) == 3 and len({s for _, s in stored}) == 3
+    for i, s in stored:
+        assert torch.equal(r.gather([s])[0], emb[i])

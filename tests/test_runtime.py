@@ -211,3 +211,22 @@ def test_prefix_cache_chain_is_content_addressed():
                 assert q[: (b + 1) * 4] == p[: (b + 1) * 4]
         bm.cache_prefix(i, p)
         live[i] = p
+
+
+def test_run_prefill_frees_parents_when_a_later_prompt_does_not_fit():
+    """A wave whose later prompt runs out of KV blocks must release the transient parents (and the cached
+    blocks they acquired) created before the failure (engine._run_prefill)."""
+    import types
+
+    from llm_weighted_consensus_amd import _runtime as R
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+
+    for use_cache in (False, True):
+        bm = R.BlockManager(6, 4)
+        bm.set_prefix_caching(use_cache)
+        fake = types.SimpleNamespace(bm=bm, device="cpu")
+        fake._run_prefill_inner = lambda *a: LLMEngine._run_prefill_inner(fake, *a)
+        prompts = [list(range(8)), list(range(100, 120))]  # 2 blocks, then 5 blocks: the second does not fit
+        with pytest.raises(RuntimeError, match="out of KV blocks"):
+            LLMEngine._run_prefill(fake, prompts, [-1, -2], use_cache=use_cache)
+        assert bm.num_sequences == 0 and bm.num_free == 6 and not bm.has_sequence(-1)
