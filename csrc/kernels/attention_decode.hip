@@ -20,11 +20,11 @@
 //     B (V)  : lane holds V[those 8 tokens][dim 16n + r16] -> two 8 B loads from the interleaved cache
 //     C      : lane reg r = O[row 4g + r][dim 16n + r16]
 // The 16 MFMA rows are "query rows".  Plain decode: row = a query head of ONE sequence (only G of 16
-// rows are real — the op is HBM-bound so idle rows cost nothing).  Prefix mode: the n sequences that
-// share a prompt are packed 16/G per wave-tile, row = (sequence, head), and the shared prompt blocks
-// are read ONCE per tile instead of once per sequence: for N candidates of one prompt this removes
-// (N-1)/N of the prompt's KV traffic and finally uses the MFMA rows.  The suffix pass (each
-// sequence's own blocks) merges the prefix partial (o, lse) in its epilogue.
+// rows are real — the op is HBM-bound so idle rows cost nothing).  Cascade kernel: the n sequences
+// that share a prompt are packed 16/G per wave-tile, row = (sequence, head), and the shared prompt
+// blocks are read ONCE per tile instead of once per sequence: for N candidates of one prompt this
+// removes (N-1)/N of the prompt's KV traffic and finally uses the MFMA rows; each sequence's own
+// blocks follow in the same launch, softmax states merged in registers.
 #include <cstdlib>
 
 #include "common.h"
@@ -52,12 +52,7 @@ struct DecodeParams {
   bf16_t* out;          // [B, Hq, D]   (suffix/plain with num_splits == 1)
   float* part_o;        // [B, Hq, S, D] (num_splits > 1)
   float* part_lse;      // [B, Hq, S]
-  // prefix sharing
-  const int* tiles;     // [max_tiles, 3] (row_start, nseq, prefix_blocks); prefix pass only
-  const int* start_blk; // [B] first block of the suffix pass (0 = no prefix partial to merge)
-  float* pre_o;         // [B, Hq, D] normalised prefix partial
-  float* pre_lse;       // [B, Hq]    its log2-sum-exp
-  int q_stride, Hq, Hkv, G, max_blocks, num_splits, num_tiles;
+  int q_stride, Hq, Hkv, G, max_blocks, num_splits;
   float scale;
 };
 
@@ -236,9 +231,8 @@ LWC_DEVICE void load_q(short8 (&qf)[4], const DecodeParams& p, int row_seq0, int
   }
 }
 
-// PREFIX=true : blockIdx.x = tile;  PREFIX=false: blockIdx.x = sequence.  4 waves split the item's
-// block pairs and combine through LDS: the long-context / small-batch path.
-template <bool PREFIX>
+// blockIdx.x = sequence.  4 waves split the sequence's block pairs and combine through LDS: the
+// long-context / small-batch path.
 __global__ void __launch_bounds__(256)
     paged_decode_kernel(DecodeParams p, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens) {
   const int item = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
@@ -248,32 +242,16 @@ __global__ void __launch_bounds__(256)
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, g = lane >> 4;
 
-  int row_seq0, nrows, blk_begin, blk_end, ctx;
-  if (PREFIX) {
-    if (item >= p.num_tiles) return;
-    const int* t = p.tiles + 3 * item;
-    row_seq0 = t[0];
-    nrows = t[1] * p.G;
-    blk_begin = 0;
-    blk_end = t[2];
-    ctx = blk_end * kBS;
-  } else {
-    row_seq0 = item;
-    nrows = p.G;
-    ctx = ctx_lens[item];
-    const int nblk_total = (ctx + kBS - 1) / kBS;
-    const int b0 = p.start_blk ? p.start_blk[item] : 0;
-    const int per_split = (nblk_total - b0 + p.num_splits - 1) / p.num_splits;
-    blk_begin = b0 + split * per_split;
-    blk_end = min(nblk_total, blk_begin + per_split);
-  }
-  // row -> (sequence, query head)
-  auto row_seq = [&](int row) { return PREFIX ? row_seq0 + row / p.G : row_seq0; };
-  auto row_head = [&](int row) { return kvh * p.G + (PREFIX ? row % p.G : row); };
-  const int* bt = block_tables + (size_t)row_seq0 * p.max_blocks;  // prefix blocks are shared by the tile
+  const int nrows = p.G;
+  const int ctx = ctx_lens[item];
+  const int nblk_total = (ctx + kBS - 1) / kBS;
+  const int per_split = (nblk_total + p.num_splits - 1) / p.num_splits;
+  const int blk_begin = split * per_split;
+  const int blk_end = min(nblk_total, blk_begin + per_split);
+  const int* bt = block_tables + (size_t)item * p.max_blocks;
 
   short8 qf[4];
-  load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
+  load_q<false>(qf, p, item, nrows, kvh, r16, g);
   const float sl2 = p.scale * kLog2e;
 
   float4v o[8];
@@ -289,8 +267,8 @@ __global__ void __launch_bounds__(256)
   }
 
   // ---- combine the 4 waves through LDS ----
-  __shared__ float s_m[kWaves + 1][16], s_l[kWaves + 1][16];
-  __shared__ float s_o[kWaves + 1][16][kD + 4];
+  __shared__ float s_m[kWaves][16], s_l[kWaves][16];
+  __shared__ float s_o[kWaves][16][kD + 4];
   if (g == 0) {
     s_m[wid][r16] = m;
     s_l[wid][r16] = l;
@@ -304,54 +282,36 @@ __global__ void __launch_bounds__(256)
   const int t = threadIdx.x;
   const int h = t >> 4, dc = (t & 15) * 8;
   if (h < nrows) {
-    const int seq = row_seq(h), hq = row_head(h);
-    int nparts = kWaves;
-    // suffix/plain pass with one split: the prefix partial joins as a 5th "wave" (m = lse, l = 1)
-    const bool merge_prefix = !PREFIX && p.num_splits == 1 && p.start_blk && p.start_blk[seq] > 0;
-    if (merge_prefix) {
-      s_m[kWaves][h] = p.pre_lse[(size_t)seq * p.Hq + hq];
-      s_l[kWaves][h] = 1.f;
-      const float* po = p.pre_o + ((size_t)seq * p.Hq + hq) * kD + dc;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_o[kWaves][h][dc + j] = po[j];
-      nparts = kWaves + 1;
-    }
+    const int hq = kvh * p.G + h;
     float M = -1e30f;
-    for (int w = 0; w < nparts; ++w) M = fmaxf(M, s_m[w][h]);
+    for (int w = 0; w < kWaves; ++w) M = fmaxf(M, s_m[w][h]);
     float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int w = 0; w < nparts; ++w) {
+    for (int w = 0; w < kWaves; ++w) {
       const float f = exp2f(s_m[w][h] - M);
       L += f * s_l[w][h];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += f * s_o[w][h][dc + j];
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    if (PREFIX) {
-      float* po = p.pre_o + ((size_t)seq * p.Hq + hq) * kD + dc;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) po[j] = acc[j] * inv;
-      if ((t & 15) == 0) p.pre_lse[(size_t)seq * p.Hq + hq] = L > 0.f ? M + log2f(L) : -INFINITY;
-    } else if (p.num_splits == 1) {
+    if (p.num_splits == 1) {
       float outv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) outv[j] = acc[j] * inv;
-      *reinterpret_cast<uint4v*>(p.out + ((size_t)seq * p.Hq + hq) * kD + dc) = pack8(outv);
+      *reinterpret_cast<uint4v*>(p.out + ((size_t)item * p.Hq + hq) * kD + dc) = pack8(outv);
     } else {
-      float* po = p.part_o + (((size_t)seq * p.Hq + hq) * p.num_splits + split) * kD + dc;
+      float* po = p.part_o + (((size_t)item * p.Hq + hq) * p.num_splits + split) * kD + dc;
 #pragma unroll
       for (int j = 0; j < 8; ++j) po[j] = acc[j] * inv;
       if ((t & 15) == 0)
-        p.part_lse[((size_t)seq * p.Hq + hq) * p.num_splits + split] = L > 0.f ? M + log2f(L) : -INFINITY;
+        p.part_lse[((size_t)item * p.Hq + hq) * p.num_splits + split] = L > 0.f ? M + log2f(L) : -INFINITY;
     }
   }
 }
 
 // One WAVE per item, kWaves independent items per workgroup, no LDS and no barriers: the
-// large-batch path (B * Hkv * splits >= kWaveKernelMinItems).  Item = tile (PREFIX) or
-// (sequence, split).  The block-pair loop is software-pipelined two deep in registers (the loads of
-// pair i+1 are in flight while pair i is on the MFMAs), and the epilogue merges the prefix partial
-// and writes straight from the accumulator layout.
-template <bool PREFIX>
+// large-batch path (B * Hkv * splits >= kWaveKernelMinItems).  Item = (sequence, split).  The block-pair
+// loop is software-pipelined in registers (the loads of pair i+1 are in flight while pair i is on the
+// MFMAs), and the epilogue writes straight from the accumulator layout.
 __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, int num_items,
                                                                 const int* __restrict__ block_tables,
                                                                 const int* __restrict__ ctx_lens) {
@@ -363,30 +323,18 @@ __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, 
   if (item >= num_items) return;  // the whole wave leaves; nothing below synchronises
   const int r16 = lane & 15, g = lane >> 4;
 
-  int row_seq0, nrows, blk_begin, blk_end, ctx, split = 0;
-  if (PREFIX) {
-    const int* t = p.tiles + 3 * item;
-    row_seq0 = t[0];
-    nrows = t[1] * p.G;
-    blk_begin = 0;
-    blk_end = t[2];
-    ctx = blk_end * kBS;
-    if (nrows == 0) return;
-  } else {
-    row_seq0 = item / p.num_splits;
-    split = item - row_seq0 * p.num_splits;
-    nrows = p.G;
-    ctx = ctx_lens[row_seq0];
-    const int nblk_total = (ctx + kBS - 1) / kBS;
-    const int b0 = p.start_blk ? p.start_blk[row_seq0] : 0;
-    const int per_split = (nblk_total - b0 + p.num_splits - 1) / p.num_splits;
-    blk_begin = b0 + split * per_split;
-    blk_end = min(nblk_total, blk_begin + per_split);
-  }
-  const int* bt = block_tables + (size_t)row_seq0 * p.max_blocks;
+  const int seq = item / p.num_splits;
+  const int split = item - seq * p.num_splits;
+  const int nrows = p.G;
+  const int ctx = ctx_lens[seq];
+  const int nblk_total = (ctx + kBS - 1) / kBS;
+  const int per_split = (nblk_total + p.num_splits - 1) / p.num_splits;
+  const int blk_begin = split * per_split;
+  const int blk_end = min(nblk_total, blk_begin + per_split);
+  const int* bt = block_tables + (size_t)seq * p.max_blocks;
 
   short8 qf[4];
-  load_q<PREFIX>(qf, p, row_seq0, nrows, kvh, r16, g);
+  load_q<false>(qf, p, seq, nrows, kvh, r16, g);
   const float sl2 = p.scale * kLog2e;
 
   float4v o[8];
@@ -417,46 +365,22 @@ __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, 
   }
 
   // epilogue: lane (g, r16) owns rows 4g+i, dims 16n+r16; row stats live in lane (row)
-  const bool merge_prefix = !PREFIX && p.num_splits == 1 && p.start_blk && p.start_blk[row_seq0] > 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int R = 4 * g + i;
     const float li = __shfl(l, R, 64), mi = __shfl(m, R, 64);
     if (R >= nrows) continue;
-    const int seq = PREFIX ? row_seq0 + R / p.G : row_seq0;
-    const int hq = kvh * p.G + (PREFIX ? R % p.G : R);
-    const size_t bh = (size_t)seq * p.Hq + hq;
-    if (PREFIX || p.num_splits > 1) {
-      const float inv = li > 0.f ? 1.f / li : 0.f;
-      float* dst = PREFIX ? p.pre_o + bh * kD : p.part_o + (bh * p.num_splits + split) * kD;
+    const size_t bh = (size_t)seq * p.Hq + kvh * p.G + R;
+    const float inv = li > 0.f ? 1.f / li : 0.f;
+    if (p.num_splits > 1) {
+      float* dst = p.part_o + (bh * p.num_splits + split) * kD;
 #pragma unroll
       for (int n = 0; n < 8; ++n) dst[16 * n + r16] = o[n][i] * inv;
-      if (r16 == 0) {
-        const float lse = li > 0.f ? mi + log2f(li) : -INFINITY;
-        if (PREFIX)
-          p.pre_lse[bh] = lse;
-        else
-          p.part_lse[bh * p.num_splits + split] = lse;
-      }
+      if (r16 == 0) p.part_lse[bh * p.num_splits + split] = li > 0.f ? mi + log2f(li) : -INFINITY;
     } else {
-      float fo = 1.f, fp = 0.f, L = li;
-      const float* pre = nullptr;
-      if (merge_prefix) {
-        const float plse = p.pre_lse[bh];
-        const float M = fmaxf(mi, plse);
-        fo = exp2f(mi - M);
-        fp = exp2f(plse - M);
-        L = li * fo + fp;
-        pre = p.pre_o + bh * kD;
-      }
-      const float inv = L > 0.f ? 1.f / L : 0.f;
       bf16_t* dst = p.out + bh * kD;
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        float v = o[n][i] * fo;
-        if (pre) v += fp * pre[16 * n + r16];
-        dst[16 * n + r16] = f2bf(v * inv);
-      }
+      for (int n = 0; n < 8; ++n) dst[16 * n + r16] = f2bf(o[n][i] * inv);
     }
   }
 }
@@ -678,18 +602,14 @@ __global__ void __launch_bounds__(kCWaves * 64)
   }
 }
 
-// Combine split-K partials (+ the prefix partial): out[b, hq, :] = sum_s 2^(lse_s - LSE) o_s
+// Combine split-K partials: out[b, hq, :] = sum_s 2^(lse_s - LSE) o_s / sum_s 2^(lse_s - LSE)
 __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(const float* __restrict__ part_o,
                                                                   const float* __restrict__ part_lse,
-                                                                  const int* __restrict__ start_blk,
-                                                                  const float* __restrict__ pre_o,
-                                                                  const float* __restrict__ pre_lse,
-                                                                  bf16_t* __restrict__ out, int S, int Hq) {
+                                                                  bf16_t* __restrict__ out, int S) {
   const int bh = blockIdx.x;  // b * Hq + hq
   const int d = threadIdx.x;  // 0..127
-  const bool pre = start_blk && start_blk[bh / Hq] > 0;
   const float* lse = part_lse + (size_t)bh * S;
-  float M = pre ? pre_lse[bh] : -INFINITY;
+  float M = -INFINITY;
   for (int s = 0; s < S; ++s) M = fmaxf(M, lse[s]);
   float L = 0.f, acc = 0.f;
   if (M != -INFINITY) {
@@ -697,11 +617,6 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(const float* _
       const float f = exp2f(lse[s] - M);
       L += f;
       acc += f * part_o[((size_t)bh * S + s) * kD + d];
-    }
-    if (pre) {
-      const float f = exp2f(pre_lse[bh] - M);
-      L += f;
-      acc += f * pre_o[(size_t)bh * kD + d];
     }
   }
   out[(size_t)bh * kD + d] = f2bf(L > 0.f ? acc / L : 0.f);
@@ -715,46 +630,25 @@ extern "C" int lwc_set_decode_wave_min_items(int n) {
   return old;
 }
 
-// Plain / suffix decode.  start_blk, pre_o, pre_lse may be null (no prefix sharing).
+// Plain split-K paged decode (the small-batch / no-shared-prompt path; the engine's large batches with
+// forked prompts use the cascade kernel below).
 extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                                 const int* ctx_lens, void* out, float* part_o, float* part_lse, int B, int Hq,
-                                int Hkv, int D, int BS, int max_blocks, int num_splits, float scale,
-                                const int* start_blk, const float* pre_o, const float* pre_lse, hipStream_t s) {
+                                int Hkv, int D, int BS, int max_blocks, int num_splits, float scale, hipStream_t s) {
   using namespace lwc;
   if (D != kD || BS != kBS || Hq % Hkv != 0 || Hq / Hkv > 16 || num_splits < 1) return -1;
   if (num_splits > 1 && (!part_o || !part_lse)) return -2;
-  if (start_blk && (!pre_o || !pre_lse)) return -3;
   if (B == 0) return 0;
   DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, (bf16_t*)out,
-                 part_o, part_lse, nullptr, start_blk, (float*)pre_o, (float*)pre_lse, q_stride, Hq, Hkv, Hq / Hkv,
-                 max_blocks, num_splits, 0, scale};
+                 part_o, part_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, num_splits, scale};
   if ((long)B * Hkv * num_splits >= g_wave_min_items) {
     const int items = B * num_splits;
-    paged_decode_wave_kernel<false><<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items, block_tables,
-                                                                                             ctx_lens);
+    paged_decode_wave_kernel<<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items, block_tables,
+                                                                                      ctx_lens);
   } else {
-    paged_decode_kernel<false><<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p, block_tables, ctx_lens);
+    paged_decode_kernel<<<dim3(B, Hkv, num_splits), 256, 0, s>>>(p, block_tables, ctx_lens);
   }
-  if (num_splits > 1)
-    paged_decode_reduce_kernel<<<B * Hq, kD, 0, s>>>(part_o, part_lse, start_blk, pre_o, pre_lse, (bf16_t*)out,
-                                                     num_splits, Hq);
-  return (int)hipGetLastError();
-}
-
-// Prefix pass: one workgroup per (tile, kv head); tiles = [max_tiles, 3] (row_start, nseq, prefix_blocks),
-// the first `num_tiles` valid; nseq * G <= 16.  Writes pre_o / pre_lse for the tiles' rows.
-extern "C" int lwc_paged_decode_prefix(const void* q, int q_stride, const void* kc, const void* vc,
-                                       const int* block_tables, const int* tiles, const int* num_tiles_dev,
-                                       int max_tiles, float* pre_o, float* pre_lse, int B, int Hq, int Hkv, int D,
-                                       int BS, int max_blocks, float scale, hipStream_t s) {
-  using namespace lwc;
-  (void)num_tiles_dev;
-  if (D != kD || BS != kBS || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
-  if (max_tiles == 0) return 0;
-  DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, nullptr, nullptr, nullptr,
-                 nullptr, tiles, nullptr, pre_o, pre_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, 1, max_tiles, scale};
-  paged_decode_wave_kernel<true><<<dim3((max_tiles + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, max_tiles,
-                                                                                            block_tables, nullptr);
+  if (num_splits > 1) paged_decode_reduce_kernel<<<B * Hq, kD, 0, s>>>(part_o, part_lse, (bf16_t*)out, num_splits);
   return (int)hipGetLastError();
 }
 

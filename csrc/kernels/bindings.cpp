@@ -17,16 +17,13 @@ int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStrea
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
 int lwc_kv_gather(const void*, const void*, const long long*, void*, void*, int, int, int, int, hipStream_t);
 int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
-                     int, int, int, int, int, int, float, const int*, const float*, const float*, hipStream_t);
+                     int, int, int, int, int, int, float, hipStream_t);
 int lwc_set_decode_wave_min_items(int);
-int lwc_paged_decode_prefix(const void*, int, const void*, const void*, const int*, const int*, const int*, int,
-                            float*, float*, int, int, int, int, int, int, float, hipStream_t);
 int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const int*, const int*, const int*, int, void*,
                              int, int, int, int, int, float, hipStream_t);
 int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
-int lwc_gemm256(const void*, const void*, void*, const void*, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
@@ -41,7 +38,6 @@ int lwc_sample(const void*, int, int, int, const float*, const float*, const int
                int, int*, float*, int*, float*, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
-int lwc_vote_tally(const float*, const float*, int, int, int, float*, float*, float*, hipStream_t);
 }
 
 namespace {
@@ -190,8 +186,7 @@ void kv_block_copy(at::Tensor& cache, const at::Tensor& pairs) {
 void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out,
                   const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_lse,
-                  int64_t num_splits, double scale, const c10::optional<at::Tensor>& start_blk,
-                  const c10::optional<at::Tensor>& pre_o, const c10::optional<at::Tensor>& pre_lse) {
+                  int64_t num_splits, double scale) {
   // q: [B, >= Hq*D] with row stride; out: [B, Hq, D]
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt);
@@ -211,44 +206,10 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     po = part_o->data_ptr<float>();
     pl = part_lse->data_ptr<float>();
   }
-  const int* sb = nullptr;
-  const float* pro = nullptr;
-  const float* prl = nullptr;
-  if (start_blk.has_value() && start_blk->defined()) {
-    CHECK_DTYPE(*start_blk, at::kInt);
-    TORCH_CHECK(start_blk->numel() >= B, "paged_decode: start_blk too short");
-    TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "paged_decode: prefix merge needs pre_o/pre_lse");
-    TORCH_CHECK(pre_o->numel() >= (int64_t)B * Hq * D && pre_lse->numel() >= (int64_t)B * Hq,
-                "paged_decode: prefix partial buffers too small");
-    sb = start_blk->data_ptr<int>();
-    pro = pre_o->data_ptr<float>();
-    prl = pre_lse->data_ptr<float>();
-  }
   CHECK_RC(lwc_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), out.data_ptr(), po, pl, B, Hq, Hkv,
-                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, sb, pro, prl,
-                            cur_stream()),
+                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, cur_stream()),
            "paged_decode");
-}
-
-void paged_decode_prefix(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
-                         const at::Tensor& block_tables, const at::Tensor& tiles, at::Tensor& pre_o,
-                         at::Tensor& pre_lse, int64_t Hq, double scale) {
-  // tiles: [max_tiles, 3] int32 (row_start, nseq, prefix_blocks); unused tiles are all-zero rows.
-  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
-  check_v_cache(v_cache, k_cache, "paged_decode_prefix");
-  CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(tiles, at::kInt); CHECK_CONTIG(tiles);
-  CHECK_DTYPE(pre_o, at::kFloat); CHECK_DTYPE(pre_lse, at::kFloat);
-  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 3, "paged_decode_prefix: tiles must be [T, 3]");
-  const int B = (int)q.size(0), D = (int)k_cache.size(3), Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
-  TORCH_CHECK(block_tables.size(0) >= B, "paged_decode_prefix: block table rows");
-  TORCH_CHECK(pre_o.numel() >= (int64_t)B * Hq * D && pre_lse.numel() >= (int64_t)B * Hq,
-              "paged_decode_prefix: prefix partial buffers too small");
-  CHECK_RC(lwc_paged_decode_prefix(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
-                                   block_tables.data_ptr<int>(), tiles.data_ptr<int>(), nullptr, (int)tiles.size(0),
-                                   pre_o.data_ptr<float>(), pre_lse.data_ptr<float>(), B, (int)Hq, Hkv, D, BS,
-                                   (int)block_tables.size(1), (float)scale, cur_stream()),
-           "paged_decode_prefix");
 }
 
 void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -318,23 +279,6 @@ void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const
                             splits > 1 ? c32.data_ptr<float>() : nullptr, (int)splits, (long long)C.size(0),
                             cur_stream()),
            "grouped_gemm");
-}
-
-void gemm256(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R) {
-  // C[M, N] = A[M, K] . W[N, K]^T (+ R), bf16, row-major with unit inner stride.
-  CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(C); CHECK_CONTIG(W);
-  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1, "gemm256: 2-D row-major A/C");
-  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
-  TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm256: shape mismatch");
-  const void* r = nullptr;
-  if (R.has_value() && R->defined()) {
-    CHECK_BF16(*R);
-    TORCH_CHECK(R->sizes() == C.sizes() && R->strides() == C.strides(), "gemm256: residual must match C");
-    r = R->data_ptr();
-  }
-  CHECK_RC(lwc_gemm256(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
-                       cur_stream()),
-           "gemm256");
 }
 
 void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
@@ -515,18 +459,6 @@ void cosine_consensus(const at::Tensor& E, at::Tensor& S, double inv_tau, at::Te
            "cosine_consensus");
 }
 
-void vote_tally(const at::Tensor& votes, const at::Tensor& w, at::Tensor& cw, at::Tensor& conf, at::Tensor& voter_conf) {
-  CHECK_DTYPE(votes, at::kFloat); CHECK_DTYPE(w, at::kFloat); CHECK_CONTIG(votes); CHECK_CONTIG(w);
-  TORCH_CHECK(votes.dim() == 3, "vote_tally: votes must be [R, L, C]");
-  const int R = (int)votes.size(0), L = (int)votes.size(1), C = (int)votes.size(2);
-  TORCH_CHECK(w.numel() == (int64_t)R * L && cw.numel() == (int64_t)R * C && conf.numel() == (int64_t)R * C &&
-                  voter_conf.numel() == (int64_t)R * L,
-              "vote_tally: shape mismatch");
-  CHECK_RC(lwc_vote_tally(votes.data_ptr<float>(), w.data_ptr<float>(), R, L, C, cw.data_ptr<float>(),
-                          conf.data_ptr<float>(), voter_conf.data_ptr<float>(), cur_stream()),
-           "vote_tally");
-}
-
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -540,7 +472,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);
   m.def("grouped_gemm", &grouped_gemm);
-  m.def("gemm256", &gemm256);
   m.def("gemm8p", &gemm8p);
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
@@ -550,12 +481,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cascade_rows_per_tile", &lwc_cascade_rows_per_tile, "sequences per cascade super-tile for a GQA ratio G");
   m.def("set_decode_wave_min_items", &lwc_set_decode_wave_min_items,
         "B*Hkv*splits threshold of the wave-per-item decode kernel; returns the previous value");
-  m.def("paged_decode_prefix", &paged_decode_prefix);
   m.def("prefill_attention", &prefill_attention);
   m.def("silu_mul_quant_fp8", &silu_mul_quant_fp8);
   m.def("kv_gather", &kv_gather);
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);
-  m.def("vote_tally", &vote_tally);
 }

@@ -1,13 +1,10 @@
 // Scoring kernels (gfx950):
 //   K9d  pool_l2norm        : CLS / mean / last-token pooling of encoder states + L2 normalisation;
 //   K10a cosine_consensus    : S = E E^T on MFMA (16x16 tiles, one wave each) followed by a row-reduce
-//                              + softmax kernel -> per-candidate centrality and consensus weights;
-//   K10b vote_tally          : weighted vote tally, confidence and per-voter agreement, batched.
-//
-// K10b is the GPU form of the reference tally/confidence loops
-// (src/score/completions/client.rs:384-455):
-//   cw_i = sum_l w_l * vote_l[i];  conf_i = cw_i / sum_i cw_i  (0 if the sum is 0);
-//   voter confidence_l = sum_i conf_i * vote_l[i].
+//                              + softmax kernel -> per-candidate centrality and consensus weights.
+// (The voter tally of the reference, src/score/completions/client.rs:384-455, is ~L x C <= 128 x 20
+// multiply-adds per request: it runs in the C++ consensus core on the host, next to the vote
+// extraction that feeds it — a kernel launch would cost more than the arithmetic.)
 #include "common.h"
 
 namespace lwc {
@@ -99,37 +96,6 @@ __global__ void __launch_bounds__(256) consensus_reduce_kernel(const float* __re
   }
 }
 
-// votes: [R, L, C], w: [R, L] -> cw: [R, C], conf: [R, C], voter_conf: [R, L]
-__global__ void __launch_bounds__(256) vote_tally_kernel(const float* __restrict__ votes, const float* __restrict__ w,
-                                                        int L, int C, float* __restrict__ cw, float* __restrict__ conf,
-                                                        float* __restrict__ voter_conf) {
-  __shared__ float scratch[16];
-  __shared__ float sconf[2048];
-  const int r = blockIdx.x;
-  const float* V = votes + (size_t)r * L * C;
-  const float* W = w + (size_t)r * L;
-  float part = 0.f;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f;
-    for (int l = 0; l < L; ++l) s += V[(size_t)l * C + c] * W[l];
-    cw[(size_t)r * C + c] = s;
-    sconf[c] = s;
-    part += s;
-  }
-  const float tot = block_sum(part, scratch);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float cf = tot > 0.f ? sconf[c] / tot : 0.f;
-    sconf[c] = cf;
-    conf[(size_t)r * C + c] = cf;
-  }
-  __syncthreads();
-  for (int l = threadIdx.x; l < L; l += blockDim.x) {
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s += sconf[c] * V[(size_t)l * C + c];
-    voter_conf[(size_t)r * L + l] = s;
-  }
-}
-
 }  // namespace lwc
 
 extern "C" int lwc_pool_l2norm(const void* hidden, int ld, const int* cu, int nseq, int d, int mode, float* out_f32,
@@ -152,11 +118,3 @@ extern "C" int lwc_cosine_consensus(const void* E, int R, int n, int d, float* S
   return (int)hipGetLastError();
 }
 
-extern "C" int lwc_vote_tally(const float* votes, const float* w, int R, int L, int C, float* cw, float* conf,
-                              float* voter_conf, hipStream_t s) {
-  using namespace lwc;
-  if (C > 2048) return -1;
-  if (R == 0) return 0;
-  vote_tally_kernel<<<R, 256, 0, s>>>(votes, w, L, C, cw, conf, voter_conf);
-  return (int)hipGetLastError();
-}

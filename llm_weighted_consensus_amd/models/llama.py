@@ -248,41 +248,28 @@ class LlamaModel:
         gemm_plan.tune(x, self.lm_head, ws=self.g8_ws)
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
-               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1, prefix=None,
+               ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,
                cascade_tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One decode step for B sequences -> logits [B, V] bf16.  All inputs are device tensors
-        (int32), so the whole call can be captured in a hipGraph.  Attention variants:
-        ``cascade_tiles`` [T, 3] — one-launch cascade kernel (shared prompt blocks read once per
-        super-tile; the engine's large-batch path); ``prefix`` = (tiles, start_blk) — two-pass prefix +
-        suffix kernels; neither — split-K paged decode."""
+        (int32), so the whole call can be captured in a hipGraph.  Attention: ``cascade_tiles`` [T, 3] —
+        the one-launch cascade kernel (shared prompt blocks read once per super-tile; the engine's
+        large-batch path); otherwise split-K paged decode."""
         cfg = self.cfg
         x = ops.embedding(self.embed, tokens)
         B = tokens.shape[0]
-        part_o = part_lse = None
-        if num_splits > 1:
-            part_o = torch.empty(B * cfg.heads * num_splits * cfg.head_dim, dtype=torch.float32, device=x.device)
-            part_lse = torch.empty(B * cfg.heads * num_splits, dtype=torch.float32, device=x.device)
-        tiles = start_blk = pre_o = pre_lse = None
-        if prefix is not None:
-            tiles, start_blk = prefix
-            pre_o = torch.empty(B * cfg.heads * cfg.head_dim, dtype=torch.float32, device=x.device)
-            pre_lse = torch.empty(B * cfg.heads, dtype=torch.float32, device=x.device)
-
         if cascade_tiles is not None:
             def attn_fn(qkv, li):
                 return ops.paged_decode_cascade(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cascade_tiles,
                                                 cfg.heads, self.scale)
+        else:
+            part_o = part_lse = None
+            if num_splits > 1:
+                part_o = torch.empty(B * cfg.heads * num_splits * cfg.head_dim, dtype=torch.float32, device=x.device)
+                part_lse = torch.empty(B * cfg.heads * num_splits, dtype=torch.float32, device=x.device)
 
-            h = self._layers(x, cache, positions, slots, attn_fn)
-            return self._proj(h, self.lm_head)
-
-        def attn_fn(qkv, li):
-            if tiles is not None:
-                ops.paged_decode_prefix(qkv, cache.k[li], cache.v[li], block_tables, tiles, pre_o, pre_lse, cfg.heads,
-                                        self.scale)
-            return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
-                                    num_splits=num_splits, part_o=part_o, part_lse=part_lse, start_blk=start_blk,
-                                    pre_o=pre_o, pre_lse=pre_lse)
+            def attn_fn(qkv, li):
+                return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
+                                        num_splits=num_splits, part_o=part_o, part_lse=part_lse)
 
         h = self._layers(x, cache, positions, slots, attn_fn)
         return self._proj(h, self.lm_head)

@@ -121,11 +121,9 @@ def kv_block_copy(cache: torch.Tensor, pairs: torch.Tensor) -> None:
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  ctx_lens: torch.Tensor, Hq: int, scale: float, num_splits: int = 1,
                  out: Optional[torch.Tensor] = None, part_o: Optional[torch.Tensor] = None,
-                 part_lse: Optional[torch.Tensor] = None, start_blk: Optional[torch.Tensor] = None,
-                 pre_o: Optional[torch.Tensor] = None, pre_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """One-token paged GQA decode attention (K3).  q: [B, >=Hq*D] (row stride allowed).
-    With ``start_blk`` (per-row first block of the suffix pass) the prefix partials ``pre_o`` /
-    ``pre_lse`` written by :func:`paged_decode_prefix` are merged into the result."""
+                 part_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One-token paged GQA split-K decode attention (K3).  q: [B, >=Hq*D] (row stride allowed).  The
+    engine's large batches of forked candidates use :func:`paged_decode_cascade` instead."""
     B = q.shape[0]
     D = k_cache.shape[-1]
     if out is None:
@@ -134,7 +132,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
         part_o = torch.empty(B * Hq * num_splits * D, dtype=torch.float32, device=q.device)
         part_lse = torch.empty(B * Hq * num_splits, dtype=torch.float32, device=q.device)
     kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, part_o, part_lse, int(num_splits),
-                           float(scale), start_blk, pre_o, pre_lse)
+                           float(scale))
     return out
 
 
@@ -142,15 +140,6 @@ def set_decode_wave_min_items(n: int) -> int:
     """Batch threshold (B * Hkv * splits) above which decode uses the wave-per-item kernel instead of
     the 4-waves-per-sequence kernel; returns the previous value (tests force both paths)."""
     return int(kernels().set_decode_wave_min_items(int(n)))
-
-
-def paged_decode_prefix(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
-                        tiles: torch.Tensor, pre_o: torch.Tensor, pre_lse: torch.Tensor, Hq: int,
-                        scale: float) -> None:
-    """Prefix-shared (cascade) pass of decode attention: for each tile (row_start, nseq, prefix_blocks)
-    the tile's sequences attend to their SHARED first `prefix_blocks` blocks in one MFMA pass
-    (16 query rows = nseq x G heads); writes normalised partials + log2-sum-exp per (row, head)."""
-    kernels().paged_decode_prefix(q, k_cache, v_cache, block_tables, tiles, pre_o, pre_lse, int(Hq), float(scale))
 
 
 def cascade_rows_per_tile(G: int) -> int:
@@ -235,16 +224,6 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
         wgs = max(1, -(-rows // 128)) * -(-N // 128)  # lower bound on the live tiles
         splits = max(1, min(k_tiles // 8, -(-1024 // wgs))) if wgs < 512 else 1
     kernels().grouped_gemm(A, W, out, row_off, int(max_slots), a_scale, w_scale, bias, a_rows, int(splits))
-    return out
-
-
-def gemm(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
-         out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Hand-written 256x256-tile MFMA GEMM (K6): A [M, K] . W[N, K]^T (+ residual) -> [M, N] bf16
-    (same contract as F.linear without bias)."""
-    if out is None:
-        out = torch.empty(A.shape[0], W.shape[0], dtype=torch.bfloat16, device=A.device)
-    kernels().gemm256(A, W, out, residual)
     return out
 
 
@@ -409,12 +388,3 @@ def cosine_consensus(E: torch.Tensor, tau: float = 0.05):
     return S[:, :n, :n], cen, w, best
 
 
-def vote_tally(votes: torch.Tensor, weights: torch.Tensor):
-    """Batched weighted tally (K10b): votes [R, L, C], weights [R, L] ->
-    (choice_weight [R, C], confidence [R, C], voter_confidence [R, L])."""
-    R, L, C = votes.shape
-    cw = torch.empty(R, C, dtype=torch.float32, device=votes.device)
-    conf = torch.empty(R, C, dtype=torch.float32, device=votes.device)
-    vc = torch.empty(R, L, dtype=torch.float32, device=votes.device)
-    kernels().vote_tally(votes.contiguous(), weights.contiguous(), cw, conf, vc)
-    return cw, conf, vc

@@ -109,11 +109,11 @@ def grouped(dev):
             sa = torch.ones(M, device=dev)
             sw = torch.ones(1, N, device=dev)
             t_8 = timeit(lambda: ops.grouped_gemm(xq, wq, off, a_scale=sa, w_scale=sw), iters=20)
-            t_2 = timeit(lambda: ops.gemm(x, w), iters=20)
-            err = (ops.gemm(x, w).float() - F.linear(x, w).float()).abs().max().item()
+            t_2 = timeit(lambda: ops.gemm8p(x, w), iters=20)
+            err = (ops.gemm8p(x, w).float() - F.linear(x, w).float()).abs().max().item()
             fl = 2 * M * N * K / 1e12
             print(f"ggemm M={M:4d} {name:8s}: hipblaslt {t_h:7.1f} us ({fl / t_h * 1e6:6.0f} TF/s)  "
-                  f"gemm256 {t_2:7.1f} us ({fl / t_2 * 1e6:6.0f}, err {err:.3g})  "
+                  f"gemm8p {t_2:7.1f} us ({fl / t_2 * 1e6:6.0f}, err {err:.3g})  "
                   f"grouped-bf16 {t_g:7.1f} us ({fl / t_g * 1e6:6.0f})  grouped-fp8 {t_8:7.1f} us ({fl / t_8 * 1e6:6.0f})",
                   flush=True)
     # Mixtral decode MoE: T tokens x top-2 over 8 experts, d=4096, ffn=14336 (gate_up fused 28672)
@@ -130,7 +130,7 @@ def grouped(dev):
 
 
 def gemm8p_study(dev, Ms):
-    """8-phase 256x256 GEMM (csrc/kernels/gemm8p.hip) vs hipBLASLt vs the 2-phase gemm256, interleaved
+    """8-phase 256x256 GEMM (csrc/kernels/gemm8p.hip) vs hipBLASLt, interleaved
     rounds in one process (median of 3), random operands; plus the fused SwiGLU epilogue against
     hipBLASLt gate_up + silu_mul."""
     from llm_weighted_consensus_amd import ops
@@ -143,8 +143,7 @@ def gemm8p_study(dev, Ms):
         x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         o = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        fns = {"hipblaslt": lambda: torch.matmul(x, w.t(), out=o), "gemm8p": lambda: ops.gemm8p(x, w, out=o),
-               "gemm256": lambda: ops.gemm(x, w, out=o)}
+        fns = {"hipblaslt": lambda: torch.matmul(x, w.t(), out=o), "gemm8p": lambda: ops.gemm8p(x, w, out=o)}
         ref = F.linear(x, w).float()
         err = (ops.gemm8p(x, w).float() - ref).abs().max().item()
         res = {k: [] for k in fns}
@@ -246,22 +245,12 @@ def attention_prefix(dev):
         ctx = torch.full((B,), P * BS + gen + 1, device=dev, dtype=torch.int32)
         q = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
         per = 16 // (Hq // Hkv)
-        tl = [(r * N + j, min(per, N - j), P) for r in range(R) for j in range(0, N, per)]
-        tiles = torch.tensor(tl, dtype=torch.int32, device=dev)
-        start = torch.full((B,), P, dtype=torch.int32, device=dev)
-        pre_o = torch.empty(B * Hq * D, device=dev)
-        pre_lse = torch.empty(B * Hq, device=dev)
         sc = 1 / math.sqrt(D)
         for path, thr in (() if os.environ.get("MICRO_PREFIX_QUICK") else (("wg4", 1 << 30), ("wave", 0))):
             old = ops.set_decode_wave_min_items(thr)
-            t_pre = timeit(lambda: ops.paged_decode_prefix(q, kc, vc, bt, tiles, pre_o, pre_lse, Hq, sc))
-            t_suf = timeit(lambda: ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc, start_blk=start, pre_o=pre_o,
-                                                    pre_lse=pre_lse))
             t_plain = timeit(lambda: ops.paged_decode(q, kc, vc, bt, ctx, Hq, sc))
             ops.set_decode_wave_min_items(old)
-            suf_gb = B * (gen + 1) * Hkv * D * 4 / (t_suf * 1e-6) / 1e9
-            print(f"prefix-decode R={R} N={N} P={P * BS} gen={gen} [{path}]: prefix {t_pre:7.1f} us  "
-                  f"suffix {t_suf:7.1f} us ({suf_gb:5.0f} GB/s)  plain {t_plain:7.1f} us", flush=True)
+            print(f"plain decode R={R} N={N} P={P * BS} gen={gen} [{path}]: {t_plain:7.1f} us", flush=True)
         from llm_weighted_consensus_amd.engine.engine import cascade_table_size, cascade_tiles
         import numpy as np
 

@@ -48,7 +48,9 @@ def test_group_splits_candidates_and_keeps_seeds():
 
 
 def test_group_worker_death_reschedules_or_fails():
-    g = EngineGroup({"delay": 0.05}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=5)
+    # death is detected from the process exit; a long heartbeat timeout keeps a loaded CI host from
+    # declaring the SURVIVOR dead too
+    g = EngineGroup({"delay": 0.05}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60)
     try:
         sp = SamplingParams(max_tokens=50, seed=1)
         victim = g.procs[0]
