@@ -7,7 +7,8 @@ with the model's chat template, sampled by the engine (paged KV, fused sampler),
 min_p/top_a, frequency/presence/repetition penalties, logit_bias, stop, seed, logprobs/top_logprobs,
 max_tokens/max_completion_tokens, `response_format: json_schema` and forced function `tool_choice`
 (constrained decoding), `stream_options.include_usage`.  Fallback over `models` follows the
-reference's attempt order (primary model, then each fallback) among the locally served models.
+reference's attempt order (primary model, then each fallback) among the locally served models, with
+its first-chunk / other-chunk timeouts (see :class:`LocalChatClient`).
 """
 from __future__ import annotations
 
@@ -90,21 +91,31 @@ def render_chat_prompt(messages: List[Any], tools: Optional[List[C.Tool]] = None
 
 
 class LocalChatClient(ChatClient):
+    """Attempt semantics follow the reference's upstream client (src/chat/completions/client.rs:238-305,
+    347-354): the primary model, then each fallback in ``models``, among the locally served ones; an
+    attempt that fails before its first chunk (engine failure, invalid request, or no chunk within
+    ``first_chunk_timeout``) is aborted and the next model is tried; once a chunk has been delivered the
+    stream is committed, and a gap longer than ``other_chunk_timeout`` ends it with ``stream_timeout``."""
+
     def __init__(self, services: Dict[str, EngineService], default_max_tokens: int = 512,
-                 fallback: Optional[ChatClient] = None, archive=None):
+                 fallback: Optional[ChatClient] = None, archive=None, first_chunk_timeout: float = 10.0,
+                 other_chunk_timeout: float = 60.0):
         self.services = services
         self.default_max_tokens = default_max_tokens
         self.fallback = fallback
         self.archive = archive
+        self.first_chunk_timeout = first_chunk_timeout
+        self.other_chunk_timeout = other_chunk_timeout
 
     def serves(self, model: str) -> bool:
         return model in self.services
 
-    def _pick(self, req: C.ChatCompletionCreateParams) -> Optional[str]:
+    def _attempts(self, req: C.ChatCompletionCreateParams) -> List[str]:
+        out: List[str] = []
         for m in [req.model] + list(req.models or []):
-            if m in self.services:
-                return m
-        return None
+            if m in self.services and m not in out:
+                out.append(m)
+        return out
 
     def sampling_params(self, req: C.ChatCompletionCreateParams, svc: EngineService, prompt_len: int):
         tok = svc.engine.tokenizer
@@ -149,12 +160,48 @@ class LocalChatClient(ChatClient):
             request = request.model_copy()
             request.messages = list(request.messages)
             replace_completion_messages(comps, request.messages)
-        name = self._pick(request)
-        if name is None:
+        names = self._attempts(request)
+        if not names:
             if self.fallback is not None:
                 return await self.fallback.create_streaming(ctx, request)
             raise ChatError.model_not_found(request.model)
-        svc = self.services[name]
+        last_err: Optional[ChatError] = None
+        for name in names:
+            try:
+                stream = self._start(self.services[name], name, request)
+            except ChatError as e:
+                last_err = e
+                continue
+            try:
+                first = await asyncio.wait_for(stream.__anext__(), self.first_chunk_timeout)
+            except StopAsyncIteration:
+                last_err = ChatError.empty_stream()
+            except asyncio.TimeoutError:
+                last_err = ChatError.stream_timeout()
+            except ChatError as e:
+                last_err = e
+            else:
+                return self._timed(first, stream)
+            await stream.aclose()  # runs the generator's finally: the engine group is aborted
+        raise last_err
+
+    async def _timed(self, first, stream):
+        """The committed stream: ``first``, then every further chunk within ``other_chunk_timeout``."""
+        try:
+            yield first
+            while True:
+                try:
+                    chunk = await asyncio.wait_for(stream.__anext__(), self.other_chunk_timeout)
+                except StopAsyncIteration:
+                    return
+                except asyncio.TimeoutError:
+                    raise ChatError.stream_timeout()
+                yield chunk
+        finally:
+            await stream.aclose()
+
+    def _start(self, svc: EngineService, name: str, request: C.ChatCompletionCreateParams):
+        """Validate, render and submit one attempt; returns its (not yet started) chunk generator."""
         tok = svc.engine.tokenizer
         template = getattr(svc, "chat_template", None) or template_for(svc.engine.cfg.name)
         prompt = render_chat_prompt(request.messages, request.tools, template)

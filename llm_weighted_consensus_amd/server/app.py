@@ -130,6 +130,28 @@ async def _body(request: Request, model_cls):
         return None, Response(f"Failed to deserialize the JSON body into the target type: {e}", status_code=422)
 
 
+def _archived(stream: AsyncIterator, finish: Callable, store: Optional[Callable]):
+    """Pass a chunk stream through, folding it with the merge algebra; once it ends cleanly the folded
+    completion (``finish(folded_chunk)``) goes to ``store`` — streamed completions are referenceable by
+    id exactly like unary ones (reference src/chat/completions/request.rs:480-505)."""
+    if store is None:
+        return stream
+
+    async def gen():
+        agg = None
+        async for x in stream:
+            if not isinstance(x, StatusError):
+                if agg is None:
+                    agg = x.clone()
+                else:
+                    agg.push(x)
+            yield x
+        if agg is not None:
+            store(finish(agg))
+
+    return gen()
+
+
 def create_app(state: AppState) -> Starlette:
     async def chat_completions(request: Request):
         req, err = await _body(request, C.ChatCompletionCreateParams)
@@ -139,7 +161,8 @@ def create_app(state: AppState) -> Starlette:
         try:
             if req.stream:
                 stream = await state.chat.create_streaming(None, req)
-                return _sse(stream)
+                return _sse(_archived(stream, C.ChatCompletion.from_chunk,
+                                      state.archive.store_chat if state.archive is not None else None))
             resp = await state.chat.create_unary(None, req)
             if state.archive is not None:
                 state.archive.store_chat(resp)
@@ -155,21 +178,8 @@ def create_app(state: AppState) -> Starlette:
         try:
             if req.stream:
                 stream = await state.score.create_streaming(None, req)
-                agg = {}
-
-                def on_item(item):  # archive the folded stream as well
-                    if "a" not in agg:
-                        agg["a"] = item.clone()
-                    else:
-                        agg["a"].push(item)
-
-                async def archived():
-                    async for x in stream:
-                        yield x
-                    if state.archive is not None and "a" in agg:
-                        state.archive.store_score(S.ScoreCompletion.from_chunk(agg["a"]))
-
-                return _sse(archived(), on_item)
+                return _sse(_archived(stream, S.ScoreCompletion.from_chunk,
+                                      state.archive.store_score if state.archive is not None else None))
             resp = await state.score.create_unary(None, req)
             state.metrics.inc("score_answers_total")
             return _json(resp.to_obj())
@@ -185,7 +195,9 @@ def create_app(state: AppState) -> Starlette:
         state.metrics.inc("multichat_requests_total")
         try:
             if req.stream:
-                return _sse(await state.multichat.create_streaming(None, req))
+                stream = await state.multichat.create_streaming(None, req)
+                return _sse(_archived(stream, S.MultichatCompletion.from_chunk,
+                                      state.archive.store_multichat if state.archive is not None else None))
             return _json((await state.multichat.create_unary(None, req)).to_obj())
         except StatusError as e:
             return _error(e)

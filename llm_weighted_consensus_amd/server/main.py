@@ -94,7 +94,9 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         if services:
             from ..chat.local import LocalChatClient
 
-            local = LocalChatClient(services, archive=archive)
+            local = LocalChatClient(services, archive=archive,
+                                    first_chunk_timeout=cfg.first_chunk_timeout_millis / 1000.0,
+                                    other_chunk_timeout=cfg.other_chunk_timeout_millis / 1000.0)
         chat_client = RoutingChatClient(local, remote)
     tt_embed = None
     if embedders:

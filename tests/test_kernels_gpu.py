@@ -297,6 +297,71 @@ def test_sample_distribution_top_p_top_k(gpu):
         assert (cnt[:keep] - q).abs().max().item() < 0.04, (kw, cnt[:keep], q)
 
 
+def _penalised_ref(logits_bf16, counts, fpen, ppen, rpen):
+    """fp32 torch reference of the sampler's logit processing (reference src/score/llm/mod.rs:39-72):
+    for tokens already generated (count c > 0): y = y / rep if y > 0 else y * rep; y -= freq * c + pres;
+    the kernel stores the processed row back as bf16 before sampling."""
+    y = logits_bf16.float().clone()
+    c = counts.float()
+    seen = c > 0
+    y = torch.where(seen & (y > 0), y / rpen, torch.where(seen, y * rpen, y))
+    y = torch.where(seen, y - fpen * c - ppen, y)
+    return y.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("fpen,ppen,rpen", [(0.5, 0.0, 1.0), (0.0, 0.7, 1.0), (0.0, 0.0, 1.5), (0.3, 0.2, 1.3),
+                                            (0.0, 0.0, 0.7)])
+def test_sample_penalties_match_torch_distribution(gpu, fpen, ppen, rpen):
+    """frequency / presence / repetition penalties: the empirical distribution of 4096 draws of one row
+    (separate count rows, same content) matches softmax of the fp32 torch reference, and greedy picks its
+    argmax on random rows."""
+    V, B = 4096, 4096
+    base = torch.full((V,), -20.0, device=gpu)
+    base[:6] = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5], device=gpu)
+    lg1 = base.to(torch.bfloat16)
+    c1 = torch.zeros(V, dtype=torch.int16, device=gpu)
+    c1[0], c1[2], c1[4], c1[5] = 2, 1, 3, 1
+    counts = c1.expand(B, V).contiguous()
+    rows = torch.arange(B, dtype=torch.int32, device=gpu)
+    f = lambda v: torch.full((B,), float(v), device=gpu)
+    tok, *_ = _sample(lg1.expand(B, V), gpu, counts=counts, count_rows=rows, freq_pen=f(fpen), pres_pen=f(ppen),
+                      rep_pen=f(rpen))
+    q = torch.softmax(_penalised_ref(lg1, c1, fpen, ppen, rpen), -1)
+    cnt = torch.bincount(tok.long(), minlength=V).float() / B
+    assert (cnt - q).abs().max().item() < 0.04, (cnt[:6], q[:6])
+    # every row counted exactly its own draw
+    assert torch.equal(counts.long().sum(1) - c1.long().sum(), torch.ones(B, dtype=torch.long, device=gpu))
+    # greedy on random rows with random counts = argmax of the reference
+    torch.manual_seed(11)
+    Bg = 64
+    lg = _bf(Bg, V, dev=gpu, scale=2.0)
+    cg = (torch.rand(Bg, V, device=gpu) < 0.05).to(torch.int16) * torch.randint(1, 4, (Bg, V), device=gpu).to(torch.int16)
+    ref = _penalised_ref(lg, cg, fpen, ppen, rpen)
+    fg = lambda v: torch.full((Bg,), float(v), device=gpu)
+    tok, *_ = _sample(lg, gpu, temperature=0.0, counts=cg.clone(), count_rows=torch.arange(Bg, dtype=torch.int32, device=gpu),
+                      freq_pen=fg(fpen), pres_pen=fg(ppen), rep_pen=fg(rpen))
+    got = ref.gather(1, tok.long()[:, None])[:, 0]
+    assert torch.equal(got, ref.max(-1).values)  # the chosen token is a maximiser (ties allowed)
+
+
+@pytest.mark.parametrize("top_a", [0.5, 1.0, 2.0])
+def test_sample_top_a_matches_torch(gpu, top_a):
+    """top_a keeps tokens with p_i >= top_a * p_max^2 (renormalised): empirical vs the torch reference."""
+    V, B = 4096, 4096
+    base = torch.full((V,), -20.0, device=gpu)
+    base[:6] = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5], device=gpu)
+    lg1 = base.to(torch.bfloat16)
+    p = torch.softmax(lg1.float(), -1)
+    keep = p >= top_a * p.max() ** 2
+    keep[p.argmax()] = True
+    q = torch.where(keep, p, torch.zeros_like(p))
+    q = q / q.sum()
+    tok, *_ = _sample(lg1.expand(B, V), gpu, top_a=top_a)
+    cnt = torch.bincount(tok.long(), minlength=V).float() / B
+    assert cnt[~keep].sum().item() == 0.0, (top_a, cnt[:6], q[:6])
+    assert (cnt - q).abs().max().item() < 0.04, (top_a, cnt[:6], q[:6])
+
+
 def test_sample_bias_mask_penalty(gpu):
     V = 4096
     B = 3

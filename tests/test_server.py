@@ -151,3 +151,24 @@ def test_config1_cpu_canned_completions_embedding_consensus():
         r = await c.post("/embeddings", json={"input": ["a", "bb"], "model": "bge-small"})
         assert r.status_code == 200 and len(r.json()["data"]) == 2
     run(go())
+
+
+def test_streamed_chat_and_multichat_are_archived(client):
+    """A STREAMED chat completion and a streamed multichat completion are archived like unary ones: the
+    chat one can then be referenced as a message (reference src/chat/completions/request.rs:480-505)."""
+    async def go():
+        req = {"model": "m", "stream": True, "messages": [{"role": "user", "content": "hi"}]}
+        r = await client.post("/chat/completions", json=req)
+        chunks = [json.loads(e) for e in sse_events(r.text)[:-1]]
+        cid = chunks[0]["id"]
+        r2 = await client.post("/chat/completions", json={"model": "m", "messages": [
+            {"role": "chat_completion", "id": cid, "choice_index": 0}, {"role": "user", "content": "and?"}]})
+        assert r2.status_code == 200, r2.text
+        r3 = await client.post("/multichat/completions", json=dict(SCORE, stream=True))
+        mchunks = [json.loads(e) for e in sse_events(r3.text)[:-1]]
+        mid = mchunks[0]["id"]
+        return cid, mid
+
+    cid, mid = run(go())
+    archive = client._transport.app.state.lwc.archive
+    assert archive._get("chat", cid) is not None and archive._get("multichat", mid) is not None
