@@ -274,6 +274,7 @@ class ScoreClient:
         votes = [list(ch.delta.vote) if ch.delta.vote is not None else [] for ch in voter_choices]
         wts = [ch.weight if ch.weight is not None else 0.0 for ch in voter_choices]
         tally = RT.tally(votes, wts, C_len)
+        self._record_training(model, weight_data, voter_choices, tally)  # before the deltas are cleared
         aggregate.weight_data = weight_data
         usage.with_total_cost()
         aggregate.usage = usage
@@ -292,6 +293,22 @@ class ScoreClient:
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+
+    def _record_training(self, model, weight_data, voter_choices, tally) -> None:
+        """Training-table models learn online: the transcript embedding and each voting voter's agreement
+        with the consensus (its tally confidence) become a row of the model's training table."""
+        if model.training_table_id is None or not isinstance(weight_data, S.WeightDataTrainingTable):
+            return
+        data = weight_data.embeddings_response.data if weight_data.embeddings_response else None
+        if not data:
+            return
+        conf = {}
+        for j, ch in enumerate(voter_choices):
+            if ch.delta.vote is not None and ch.model_index is not None:
+                conf[int(ch.model_index)] = float(tally.voter_confidence[j])
+        tt = self.weights.training_table
+        if conf and hasattr(tt, "record"):
+            tt.record(model, list(data[0].embedding), conf)
 
     # ------------------------------------------------------------------ one voter
     def _voter_request(self, llm: Llm, request: S.ScoreCompletionCreateParams, seed: int):

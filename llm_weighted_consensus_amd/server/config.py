@@ -15,6 +15,7 @@ variables configure the local engine:
   LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)
   LWC_ARCHIVE_PATH  append-only JSONL log of completions (checkpoint/resume of the archive)
   LWC_REGISTRY_PATH JSON file persisting registered score models
+  LWC_TRAINING_TABLE_PATH  append-only JSONL of training-table rows (learned voter weights), replayed on start
   LWC_FAULT         fault injection for tests: worker_crash | slow_decode | bad_logprobs | oom
   LWC_CONSTRAINED_LOGPROBS  1: constrained (json_schema / tool-call) voters get logprobs over the allowed
                     tokens, so a key letter's vote is the exact restricted softmax over its siblings
@@ -68,6 +69,7 @@ class Config:
     prefix_caching: bool = True
     kv_fraction: float = 0.85
     archive_path: Optional[str] = None
+    training_table_path: Optional[str] = None
     registry_path: Optional[str] = None
     fault: Optional[str] = None
 
@@ -104,6 +106,7 @@ class Config:
         c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))
         c.archive_path = e.get("LWC_ARCHIVE_PATH")
         c.registry_path = e.get("LWC_REGISTRY_PATH")
+        c.training_table_path = e.get("LWC_TRAINING_TABLE_PATH")
         c.fault = e.get("LWC_FAULT")
         return c
 

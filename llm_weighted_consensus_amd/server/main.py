@@ -102,7 +102,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if embedders:
         first = next(iter(embedders.values()))
         tt_embed = lambda texts, max_tokens: first.embed_texts(texts, max_tokens)  # noqa: E731
-    score = ScoreClient(chat_client, registry, WeightFetchers(training_table=TrainingTableWeights(tt_embed)),
+    score = ScoreClient(chat_client, registry,
+                        WeightFetchers(training_table=TrainingTableWeights(tt_embed, path=cfg.training_table_path)),
                         archive=archive)
     return AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                           archive),

@@ -6,6 +6,7 @@ the fault path: an injected engine crash turns every voter into an error choice 
 the reference's AllVotesFailed status."""
 import asyncio
 import json
+import re
 
 import httpx
 import pytest
@@ -178,7 +179,7 @@ def test_constrained_voters_with_real_tokenizer(gpu, tmp_path, kind):
             msg = v["message"]
             text = msg["content"] if msg.get("content") else msg["tool_calls"][0]["function"]["arguments"]
             obj = json.loads(text)
-            assert obj["response_key"] in ("`A`", "`B`", "`C`"), text
+            assert re.fullmatch(r"`[A-T]`", obj["response_key"]), text  # keys are drawn per voter (KeyTree)
             assert msg["vote"] is not None and sum(msg["vote"]) == pytest.approx(1.0, abs=1e-6)
 
     try:
