@@ -75,14 +75,20 @@ def bench_moe(a):
         raise SystemExit(f"--tp {a.tp} needs torchrun with {a.tp} ranks (WORLD_SIZE={info.world})")
     dev = torch.device("cuda", info.local_rank)
     dcfg = decoder_config(a.decoder)
+    comm = None
+    if tp > 1:
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
+
+        # C3 over IPC peer buffers: [decode batch, hidden] bf16 per call, inside the captured decode graph
+        comm = CustomAllReduce(device=dev, max_bytes=a.requests * a.candidates * dcfg.hidden * 2)
     model = MixtralModel(dcfg, device=dev, seed=11, max_position=a.prompt_len + a.gen_len + 64, fp8=not a.bf16,
-                         tp_rank=info.rank if tp > 1 else 0, tp_size=tp)
+                         tp_rank=info.rank if tp > 1 else 0, tp_size=tp, tp_comm=comm)
     emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64)
     scorer = EmbeddingConsensus(DecoderEmbedder(emb_model, max_tokens=a.gen_len + 16), tau=0.05)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     R, N = a.requests, a.candidates
     engine = LLMEngine(model, tok, max_batch=R * N, max_model_len=a.prompt_len + a.gen_len + 16,
-                       kv_memory_fraction=0.4, use_graphs=tp == 1)
+                       kv_memory_fraction=0.4, use_graphs=model.graph_safe)
     g = torch.Generator().manual_seed(5)
 
     def step(i):

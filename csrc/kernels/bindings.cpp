@@ -36,6 +36,13 @@ int lwc_sample(const void*, int, int, int, const float*, const float*, const int
                const float*, const float*, const float*, void*, const int*, const float*, const int*,
                const unsigned int*, const int*, const unsigned long long*, const unsigned long long*, int, int,
                int, int*, float*, int*, float*, hipStream_t);
+long long lwc_ar_region_bytes(int, long long);
+int lwc_ar_alloc(long long, void**, void*);
+int lwc_ar_open(const void*, void**);
+int lwc_ar_close(void*);
+int lwc_ar_free(void*);
+int lwc_ar_handle_bytes();
+int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long long, int*, int, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
 }
@@ -461,6 +468,41 @@ void cosine_consensus(const at::Tensor& E, at::Tensor& S, double inv_tau, at::Te
 
 }  // namespace
 
+// ---- C3 custom all-reduce (allreduce.hip): IPC regions are raw device pointers held by Python as ints
+std::tuple<int64_t, py::bytes> ar_alloc(int64_t bytes) {
+  void* ptr = nullptr;
+  std::string h((size_t)lwc_ar_handle_bytes(), '\0');
+  const int rc = lwc_ar_alloc(bytes, &ptr, h.data());
+  TORCH_CHECK(rc == 0, "ar_alloc: HIP error ", rc);
+  return {reinterpret_cast<int64_t>(ptr), py::bytes(h)};
+}
+
+int64_t ar_open(const py::bytes& handle) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == lwc_ar_handle_bytes(), "ar_open: bad handle size");
+  void* ptr = nullptr;
+  const int rc = lwc_ar_open(h.data(), &ptr);
+  TORCH_CHECK(rc == 0, "ar_open: hipIpcOpenMemHandle failed with ", rc);
+  return reinterpret_cast<int64_t>(ptr);
+}
+
+void ar_close(int64_t ptr) { (void)lwc_ar_close(reinterpret_cast<void*>(ptr)); }
+void ar_free(int64_t ptr) { (void)lwc_ar_free(reinterpret_cast<void*>(ptr)); }
+int64_t ar_region_bytes(int64_t W, int64_t cap) { return lwc_ar_region_bytes((int)W, cap); }
+
+void allreduce(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& x, at::Tensor& out, int64_t cap,
+               at::Tensor& err, int64_t blocks) {
+  CHECK_BF16(x); CHECK_BF16(out); CHECK_CONTIG(x); CHECK_CONTIG(out);
+  CHECK_DTYPE(err, at::kInt);
+  TORCH_CHECK(x.numel() == out.numel(), "allreduce: x / out size mismatch");
+  TORCH_CHECK(x.numel() % 8 == 0, "allreduce: numel must be a multiple of 8");
+  std::vector<void*> b;
+  for (int64_t v : bases) b.push_back(reinterpret_cast<void*>(v));
+  CHECK_RC(lwc_allreduce(b.data(), (int)me, (int)b.size(), x.data_ptr(), out.data_ptr(), x.numel(), cap,
+                         err.data_ptr<int>(), (int)blocks, cur_stream()),
+           "allreduce");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels of llm_weighted_consensus_amd";
   m.def("rmsnorm", &rmsnorm);
@@ -487,4 +529,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);
+  m.def("ar_alloc", &ar_alloc);
+  m.def("ar_open", &ar_open);
+  m.def("ar_close", &ar_close);
+  m.def("ar_free", &ar_free);
+  m.def("ar_region_bytes", &ar_region_bytes);
+  m.def("allreduce", &allreduce);
 }

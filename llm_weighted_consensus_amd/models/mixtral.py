@@ -16,7 +16,9 @@ GEMM: half the weight bytes — what bounds a MoE decode step, which touches eve
 
 Tensor parallelism (``tp_group``): attention heads and every expert's FFN columns are split across
 the ranks (Megatron layout: q/k/v and gate|up column-parallel, o and down row-parallel); the two
-row-parallel outputs are summed with one all-reduce each (C3) before the residual norm.  The shard is
+row-parallel outputs are summed with one all-reduce each (C3) before the residual norm — the
+IPC one-shot kernel of `parallel/allreduce.py` when ``tp_comm`` is given (graph-capturable), else the
+process group's.  The shard is
 taken from the full random-init / loaded weights so any TP degree computes the same function.
 
 Expert parallelism (``ep_group``, C4, `parallel/expert.py`): the alternative to TP for the MoE layers.
@@ -59,7 +61,7 @@ class MixtralModel(LlamaModel):
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8: bool = False,
                  tp_rank: int = 0, tp_size: int = 1, tp_group=None, ep_rank: int = 0, ep_size: int = 1,
-                 ep_group=None, ep_mode: str = "padded", ep_capacity: Optional[int] = None):
+                 ep_group=None, ep_mode: str = "padded", ep_capacity: Optional[int] = None, tp_comm=None):
         if not cfg.num_experts:
             raise ValueError(f"{cfg.name} is dense; use LlamaModel")
         if ep_size > 1 and tp_size > 1:
@@ -77,6 +79,9 @@ class MixtralModel(LlamaModel):
         if cfg.heads % tp_size or cfg.kv_heads % tp_size or cfg.ffn % tp_size:
             raise ValueError(f"tp_size {tp_size} must divide heads, kv_heads and ffn")
         self.fp8, self.tp_rank, self.tp_size, self.tp_group = fp8, tp_rank, tp_size, tp_group
+        # C3 transport: a parallel.allreduce.CustomAllReduce (IPC peer buffers, one graph-capturable kernel)
+        # or None for the process group's all-reduce (RCCL / gloo; not capturable)
+        self.tp_comm = tp_comm
         self.full_cfg = cfg
         super().__init__(cfg, device=device, dtype=dtype, seed=seed, weights_path=weights_path,
                          max_position=max_position)
@@ -165,10 +170,18 @@ class MixtralModel(LlamaModel):
     # ------------------------------------------------------------------ forward pieces
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
+            if self.tp_comm is not None:
+                return self.tp_comm.all_reduce_(x)
             from ..parallel import dist as pdist
 
             pdist.all_reduce_(x, group=self.tp_group)
         return x
+
+    @property
+    def graph_safe(self) -> bool:
+        """Whether a decode step may be captured in a hipGraph: every collective inside it must be a
+        stream kernel (the IPC all-reduce), not a host-driven process-group call."""
+        return self.tp_size == 1 and self.ep_size == 1 or (self.tp_size > 1 and self.tp_comm is not None)
 
     def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
         return self._all_reduce(F.linear(attn, L.wo))

@@ -1,0 +1,152 @@
+"""C3 one-shot all-reduce over IPC-mapped peer buffers (csrc/kernels/allreduce.hip), two ranks sharing
+the test box's GPU (handles exchanged over gloo; the data path is the kernel only): results equal the
+fp32 rank-order sum rounded to bf16 on both ranks, across many calls (parity reuse), ragged sizes,
+payloads larger than a slot, and inside a replayed hipGraph; and TP=2 Mixtral logits through it match
+TP=1."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ref(world, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    xs = [torch.randn(n, generator=g).to(torch.bfloat16) for _ in range(world)]
+    acc = torch.zeros(n)
+    for x in xs:
+        acc += x.float()
+    return xs, acc.to(torch.bfloat16)
+
+
+def _ar_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllReduce(device=dev, max_bytes=1 << 20, blocks=16)
+        bad = []
+        sizes = [8, 4096, 12344, 1 << 19, (1 << 19) + 4096 * 3, 3 << 20]  # last two exceed one 1 MiB slot
+        for it in range(24):
+            n = sizes[it % len(sizes)]
+            xs, want = _ref(world, n, 1000 + it)
+            x = xs[rank].to(dev)
+            comm.all_reduce_(x)
+            if not torch.equal(x.cpu(), want):
+                bad.append(("eager", it, n))
+        # captured in a hipGraph, replayed with fresh inputs copied into the static buffer
+        n = 65536
+        static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            comm.all_reduce_(static)  # warm-up outside capture
+        torch.cuda.current_stream(dev).wait_stream(s)
+        pdist.barrier()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            comm.all_reduce_(static)
+        for it in range(10):
+            xs, want = _ref(world, n, 5000 + it)
+            static.copy_(xs[rank].to(dev))
+            graph.replay()
+            torch.cuda.synchronize(dev)
+            if not torch.equal(static.cpu(), want):
+                bad.append(("graph", it))
+        comm.check()
+        pdist.barrier()
+        comm.close()
+        q.put((rank, bad))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_allreduce_two_ranks_one_gpu(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ar_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: [], 1: []}, res
+
+
+def _tp_worker(rank, world, port, fp8, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.llama import KVCache
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllReduce(device=dev, max_bytes=1 << 20, blocks=16)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
+                         tp_rank=rank, tp_size=world, tp_comm=comm)
+        assert m.graph_safe
+        g = torch.Generator().manual_seed(9)
+        P = 29
+        toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(dev)
+        cache = KVCache(m.cfg, 8, 16, dev)
+        ar = torch.arange(P, dtype=torch.int32, device=dev)
+        lg = m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=dev), P,
+                       torch.tensor([P - 1], device=dev), cache)
+        torch.cuda.synchronize(dev)
+        comm.check()
+        q.put((rank, lg[0].float().cpu()))
+        pdist.barrier()
+        comm.close()
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_mixtral_tp2_through_ipc_allreduce(gpu):
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import KVCache
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, False, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    assert all(isinstance(v, torch.Tensor) for v in res.values()), res
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512)
+    g = torch.Generator().manual_seed(9)
+    P = 29
+    toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(gpu)
+    cache = KVCache(m.cfg, 8, 16, gpu)
+    ar = torch.arange(P, dtype=torch.int32, device=gpu)
+    lg = m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=gpu), P,
+                   torch.tensor([P - 1], device=gpu), cache)[0].float().cpu()
+    for r in range(2):
+        c = torch.nn.functional.cosine_similarity(res[r], lg, dim=0).item()
+        assert c > 0.99, (r, c)
+    assert torch.equal(res[0], res[1])
