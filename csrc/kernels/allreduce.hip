@@ -40,7 +40,7 @@ constexpr size_t kFlagsOff = 0;
 constexpr size_t kEpochOff = (size_t)kMaxRanks * kMaxBlocks * 4;  // 32 KiB
 constexpr size_t kDataOff = 64 * 1024;
 constexpr int kThreads = 512;
-constexpr long long kSpinLimit = 1LL << 22;  // x s_sleep(2): seconds, far past any healthy peer
+constexpr long long kSpinLimit = 1LL << 26;  // x s_sleep(2) (~60 ns): ~4 s, far past any healthy peer
 
 struct Params {
   uint8_t* base[kMaxRanks];  // every rank's region as mapped in THIS process (base[me] = own)
