@@ -14,5 +14,11 @@ fi
 [ "${ONLY:-}" = "small" ] && { cat gpurun_out/configs.log; exit 0; }
 timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-32} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
 rc=$?; echo "config5 rc=$rc"
+if [ $rc -eq 0 ] && [ -n "${TP2:-}" ]; then
+  # TP=2 through the IPC all-reduce; on a one-GPU box both ranks share the GPU (protocol rehearsal)
+  LWC_SHARE_ONE_GPU=${SHARE:-1} timeout -k 10 1000 python bench_configs.py moe --tp 2 --requests ${TP2_R:-16} --steps 2 \
+      >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
+  rc=$?; echo "config5 tp2 rc=$rc"
+fi
 cat gpurun_out/configs.log
 exit $rc
