@@ -105,6 +105,7 @@ class SequenceGroup:
         self.reserved_blocks = 0
         self.timer = RequestTimer()
         self.prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+        self.pf_pos = -1  # chunked prefill: prompt tokens already in the KV cache (-1 = not started)
 
     @property
     def finished(self) -> bool:
@@ -244,7 +245,7 @@ class LLMEngine:
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
                  use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
                  cascade_min_batch: int = 128, tune_gc: bool = True, constrained_logprobs: bool = False,
-                 prefix_caching: bool = False):
+                 prefix_caching: bool = False, chunked_prefill: int = 0):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -253,6 +254,11 @@ class LLMEngine:
         self.max_batch = max_batch
         self.max_model_len = max_model_len
         self.prefill_token_budget = prefill_token_budget
+        # chunked prefill (serving): admitted prompts are prefilled at most `chunked_prefill` tokens per
+        # engine step, each step also running one decode step, so running sequences never stall behind
+        # an admission (0 = whole admission batches, then decode: the throughput bench's mode)
+        self.chunked_prefill = int(chunked_prefill)
+        self.prefilling: List[SequenceGroup] = []
         self.width = (max_model_len + block_size - 1) // block_size
         if num_blocks is None:
             free, _total = torch.cuda.mem_get_info(self.device)
@@ -316,7 +322,7 @@ class LLMEngine:
         return g
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or bool(self.running) or self.inflight is not None
+        return bool(self.waiting) or bool(self.running) or bool(self.prefilling) or self.inflight is not None
 
     def step(self) -> List[TokenEvent]:
         """Run one engine iteration: admit+prefill waiting groups if any fit, else one decode step.
@@ -326,6 +332,8 @@ class LLMEngine:
         host syncs on and post-processes step t, so detokenisation, stop checks and callbacks overlap
         the GPU.  A sequence that finishes at step t has one discarded row in step t+1."""
         self.faults.on_step()
+        if self.chunked_prefill > 0:
+            return self._step_chunked()
         events: List[TokenEvent] = []
         with self.lock:
             fits = self._first_waiting_fits()
@@ -358,19 +366,20 @@ class LLMEngine:
         if not self.waiting:
             return False
         g = self.waiting[0]
-        live = sum(1 for s in self.running if not s.finished)
+        live = sum(1 for s in self.running if not s.finished) + sum(x.n for x in self.prefilling)
         return live + g.n <= self.max_batch and (self._group_reservation(g) <= self.free_blocks_unreserved
-                                                 or (not self.running and self.inflight is None))
+                                                 or (not self.running and self.inflight is None
+                                                     and not self.prefilling))
 
     def _admit(self) -> List[SequenceGroup]:
         out, tokens = [], 0
         while self.waiting:
             g = self.waiting[0]
             need = self._group_reservation(g)
-            if len(self.running) + sum(x.n for x in out) + g.n > self.max_batch:
+            if len(self.running) + sum(x.n for x in self.prefilling) + sum(x.n for x in out) + g.n > self.max_batch:
                 break
             if need > self.free_blocks_unreserved:
-                if not self.running and not out:
+                if not self.running and not out and not self.prefilling:
                     self.waiting.popleft()
                     raise RuntimeError("request needs more KV blocks than the cache holds")
                 break
@@ -487,7 +496,11 @@ class LLMEngine:
             self.cache.pool.index_copy_(2, tab, kv)
             logits_of[g.id] = row
             g.prefilled = None  # drop the reference: the cache owns the data now
-        # fork every group into its n sequences (shared prompt blocks), then sample first tokens
+        return self._start_groups(groups, logits_of)
+
+    def _start_groups(self, groups: List[SequenceGroup], logits_of: Dict[int, torch.Tensor]) -> List[TokenEvent]:
+        """Fork every prefilled group into its n sequences (shared prompt blocks), sample their first
+        tokens from the prompt's last-token logits and add them to the running batch."""
         rows, seqs = [], []
         for g in groups:
             parent = -g.id
@@ -504,6 +517,113 @@ class LLMEngine:
             if not s.finished:
                 self.running.append(s)
         return events
+
+    # ------------------------------------------------------------------ chunked prefill
+    def _step_chunked(self) -> List[TokenEvent]:
+        """One engine step in chunked-prefill mode: admit what fits, prefill one chunk of at most
+        ``chunked_prefill`` prompt tokens (several short prompts whole, a long one in pieces), start the
+        groups whose prompts completed, then one decode step of everything running."""
+        events: List[TokenEvent] = []
+        with self.lock:
+            fits = self._first_waiting_fits()
+            admitted = self._admit() if fits else []
+        self.prefilling.extend(admitted)
+        if self.prefilling:
+            events += self._drain()  # the chunk writes the block manager / KV pool: no step in flight
+            with span("prefill.chunk"):
+                events += self._prefill_chunk()
+        if self.running or self.inflight is not None:
+            events += self._decode()
+        return events
+
+    def _prefill_chunk(self) -> List[TokenEvent]:
+        bs = self.block_size
+        imported = [g for g in self.prefilling if g.prefilled is not None]
+        if imported:  # prompts prefilled elsewhere cost no compute: start them now
+            self.prefilling = [g for g in self.prefilling if g.prefilled is None]
+            return self._prefill(imported)
+        budget = self.chunked_prefill
+        items: List[Tuple[SequenceGroup, int, int]] = []
+        heads = set()
+        for g in self.prefilling:
+            if budget <= 0:
+                break
+            p = g.prompt_ids
+            head = tuple(p[:bs]) if len(p) > bs else None
+            if g.pf_pos < 0:
+                # a prompt sharing its first block with one in progress waits for it and then takes the
+                # shared head from the prefix cache (the voters of one score request)
+                if self.prefix_caching and head is not None and head in heads:
+                    continue
+                if self.prefix_caching:
+                    g.pf_pos = int(self.bm.add_sequence_cached(-g.id, p))
+                    self.stats["prefix_cache_tokens"] += g.pf_pos
+                else:
+                    self.bm.add_sequence(-g.id, len(p))
+                    g.pf_pos = 0
+            if head is not None:
+                heads.add(head)
+            n = min(budget, len(p) - g.pf_pos)
+            items.append((g, g.pf_pos, g.pf_pos + n))
+            budget -= n
+        if not items:
+            return []
+        logits = self._run_chunk(items)
+        done, logits_of = [], {}
+        for i, (g, a, e) in enumerate(items):
+            g.pf_pos = e
+            if e == len(g.prompt_ids):
+                if self.prefix_caching:
+                    self.bm.cache_prefix(-g.id, g.prompt_ids)
+                done.append(g)
+                logits_of[g.id] = logits[i]
+        if not done:
+            return []
+        ids = {g.id for g in done}
+        self.prefilling = [g for g in self.prefilling if g.id not in ids]
+        return self._start_groups(done, logits_of)
+
+    def _run_chunk(self, items: List[Tuple[SequenceGroup, int, int]]) -> torch.Tensor:
+        """Prefill prompt tokens [a, e) of each item's parent sequence (blocks allocated at its first
+        chunk); attention covers keys [0, e) — the earlier chunks come from the paged cache through the
+        key-range path of the cached-prefix prefill.  Returns the logits of each item's token e-1."""
+        dev = self.device
+        toks, pos, slots, cu, last = [], [], [], [0], []
+        for g, a, e in items:
+            p = g.prompt_ids
+            toks.extend(p[a:e])
+            pos.extend(range(a, e))
+            slots.append(slots_range(self.bm, -g.id, a, e - a))
+            cu.append(cu[-1] + e - a)
+            last.append(cu[-1] - 1)
+        ctx = None
+        if any(a > 0 for _, a, _ in items):
+            k_lens = [e for _, _, e in items]
+            ks = np.concatenate([slots_range(self.bm, -g.id, 0, e) for g, _, e in items]).astype(np.int64)
+            if ks.size and (ks.min() < 0 or ks.max() >= self.bm.num_blocks * self.block_size):
+                raise RuntimeError("chunked prefill: KV slot out of range")
+            ctx = {"k_slots": torch.from_numpy(ks).to(dev),
+                   "cu_k": torch.tensor(np.concatenate([[0], np.cumsum(k_lens)]), dtype=torch.int32, device=dev),
+                   "q_lens": [e - a for _, a, e in items], "k_lens": k_lens}
+        t_tok = torch.tensor(toks, dtype=torch.int32, device=dev)
+        t_pos = torch.tensor(pos, dtype=torch.int32, device=dev)
+        t_slots = torch.from_numpy(np.concatenate(slots)).to(dev)
+        t_cu = torch.tensor(cu, dtype=torch.int32, device=dev)
+        t_last = torch.tensor(last, dtype=torch.int64, device=dev)
+        max_len = max(e - a for _, a, e in items)
+        logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache, ctx=ctx)
+        self.stats["prefill_tokens"] += len(toks)
+        self.stats["prefill_chunks"] = self.stats.get("prefill_chunks", 0) + 1
+        return logits
+
+    def _drop_prefilling(self, g: SequenceGroup, reason: str) -> None:
+        if g.pf_pos >= 0 and self.bm.has_sequence(-g.id):
+            self.bm.free_sequence(-g.id)
+        for s in g.seqs:
+            s.finished, s.finish_reason = True, reason
+        self.free_blocks_unreserved += g.reserved_blocks
+        g.reserved_blocks = 0
+        self.prefilling = [x for x in self.prefilling if x is not g]
 
     def _prefill_waves(self, groups: List[SequenceGroup]) -> List[List[SequenceGroup]]:
         """Split one admission batch so prompts that share a head INSIDE the batch (the voters of one
@@ -927,6 +1047,9 @@ class LLMEngine:
                 for s in g.seqs:
                     s.finished, s.finish_reason = True, "abort"
                 return
+        if any(x is g for x in self.prefilling):
+            self._drop_prefilling(g, "abort")
+            return
         for s in g.seqs:
             if not s.finished:
                 self._finish(s, "abort")
@@ -939,6 +1062,13 @@ class LLMEngine:
             for g in self.waiting:
                 groups[g.id] = g
             self.waiting.clear()
+        for g in list(self.prefilling):
+            groups[g.id] = g
+            try:
+                self._drop_prefilling(g, "error")
+            except Exception:  # pragma: no cover - best effort cleanup
+                pass
+        self.prefilling = []
         for s in self.running:
             groups[s.group.id] = s.group
         for g in groups.values():

@@ -295,7 +295,7 @@ class EngineGroup:
 def build_engine(spec: dict, wid: int):
     """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
     ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8",
-    "prefix_caching", "constrained_logprobs", "tokenizer": path to a tokenizer.json}); MoE archs get the
+    "prefix_caching", "chunked_prefill", "constrained_logprobs", "tokenizer": path to a tokenizer.json}); MoE archs get the
     Mixtral model."""
     import torch
 
@@ -321,4 +321,5 @@ def build_engine(spec: dict, wid: int):
     return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
                      kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),
                      prefix_caching=bool(spec.get("prefix_caching", True)),
+                     chunked_prefill=int(spec.get("chunked_prefill", 0)),
                      constrained_logprobs=bool(spec.get("constrained_logprobs", False)))

@@ -69,7 +69,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 from ..engine.group import EngineGroup
 
                 wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
-                             prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs)
+                             prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs,
+                             chunked_prefill=cfg.chunked_prefill)
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
                                                                       dcfg.eos_token_id))
@@ -78,7 +79,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             from ..engine.group import build_engine
 
             eng = build_engine(dict(spec, device=cfg.gpu, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
-                                    prefix_caching=cfg.prefix_caching,
+                                    prefix_caching=cfg.prefix_caching, chunked_prefill=cfg.chunked_prefill,
                                     constrained_logprobs=cfg.constrained_logprobs), 0)
             services[name] = EngineService(eng, name)
             services[name].chat_template = spec.get("chat_template")
