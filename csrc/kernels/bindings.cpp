@@ -290,10 +290,11 @@ void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const
 
 void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
             at::Tensor& ws, at::Tensor& flags) {
-  // epi 0: C[M, N] = A . W^T; 1: + R; 2: C[M, N/2] = silu(gate) * up over a 32-row gate/up interleaved W.
+  // epi 0: C[M, N] = A . W^T; 1: + R; 2: C[M, N/2] = silu(gate) * up over a 32-row gate/up interleaved W;
+  // 3: + bias (R = bias [N]); 4: gelu(. + bias)
   CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(C); CHECK_CONTIG(W);
   TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1, "gemm8p: 2-D row-major A/C");
-  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8p: epi must be 0, 1 or 2");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm8p: epi must be 0..4");
   const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
   const int NC = epi == 2 ? N / 2 : N;
   TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == NC, "gemm8p: shape mismatch");
@@ -304,6 +305,12 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
     TORCH_CHECK(R.has_value() && R->defined(), "gemm8p: epi 1 needs a residual");
     CHECK_BF16(*R);
     TORCH_CHECK(R->sizes() == C.sizes() && R->strides() == C.strides(), "gemm8p: residual must match C");
+    r = R->data_ptr();
+  }
+  if (epi == 3 || epi == 4) {
+    TORCH_CHECK(R.has_value() && R->defined(), "gemm8p: bias epilogue needs a bias");
+    CHECK_BF16(*R); CHECK_CONTIG(*R);
+    TORCH_CHECK(R->numel() == N, "gemm8p: bias must have N elements");
     r = R->data_ptr();
   }
   // stream-K workspace: one fp32 256x256 partial tile and one flag per workgroup (flags zero between calls)

@@ -62,13 +62,13 @@ constexpr int kLdsB = 2 * kBufB;    // 128 KiB
 constexpr int kUA0 = 0, kUA1 = kUnitB, kUB0 = 2 * kUnitB, kUB1 = 3 * kUnitB;
 constexpr int kPartialF = 256 * 256;  // fp32 partial tile per workgroup
 
-enum Epi { EPI_PLAIN = 0, EPI_RESIDUAL = 1, EPI_SWIGLU = 2 };
+enum Epi { EPI_PLAIN = 0, EPI_RESIDUAL = 1, EPI_SWIGLU = 2, EPI_BIAS = 3, EPI_BIAS_GELU = 4 };
 
 struct Params {
   const bf16_t* A;
   const bf16_t* W;
   bf16_t* C;
-  const bf16_t* R;
+  const bf16_t* R;     // EPI_RESIDUAL: residual [M, ldc]; EPI_BIAS / EPI_BIAS_GELU: bias [N]
   float* ws;    // [8 * wpx, kPartialF] partial tiles
   int* flags;   // [8 * wpx] partial-ready flags (zero between launches)
   int M, N, K, lda, ldc;  // N = rows of W
@@ -83,6 +83,7 @@ LWC_DEVICE float4v mfma(const uint4v& a, const uint4v& b, const float4v& c) {
 }
 
 LWC_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // K-iteration range [a, e) of stream-K workgroup j (of wpx) on XCD x.
 LWC_DEVICE void sk_range(const Params& p, int x, int j, int& a, int& e) {
@@ -311,6 +312,22 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][jj][r] = silu(acc[i][jj][r]) * acc[i][jj + 2][r];
     }
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+      // bias (+ exact erf GELU) on the fp32 accumulators, before the one bf16 rounding: the encoder's
+      // FFN1 needs no separate bias_gelu pass over [M, ffn]
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int col = n0 + wc * 64 + jj * 16 + r16;
+        const float bv = col < p.N ? bf2f(p.R[col]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = acc[i][jj][r] + bv;
+            acc[i][jj][r] = EPI == EPI_BIAS_GELU ? gelu_erf(y) : y;
+          }
+      }
+    }
     bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -383,7 +400,8 @@ int device_cus() {
 // Workgroups the kernel launches (= partial slots / flags the workspace must hold): 8 x (CUs / 8).
 extern "C" int lwc_gemm8p_slots() { return 8 * (lwc::g8p::device_cus() / 8); }
 
-// epi 0: C = A W^T; 1: C = A W^T + R; 2: C[:, :N/2] = silu(gate) * up over 32-row interleaved W (N % 64 == 0).
+// epi 0: C = A W^T; 1: C = A W^T + R; 2: C[:, :N/2] = silu(gate) * up over 32-row interleaved W (N % 64 == 0);
+// 3: C = A W^T + bias (R = bias [N]); 4: C = gelu(A W^T + bias) (exact erf GELU).
 // Requires K % 64 == 0, N % 8 == 0, lda / ldc % 8 == 0 (16-byte rows); ws >= slots * 65536 floats,
 // flags >= slots ints, zero on the first call (the kernel leaves them zero).
 extern "C" int lwc_gemm8p(const void* A, const void* W, void* C, const void* R, float* ws, int* flags, int M, int N,
@@ -392,7 +410,7 @@ extern "C" int lwc_gemm8p(const void* A, const void* W, void* C, const void* R, 
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if ((long long)M * lda * 2 >= (1LL << 31) || 256LL * K * 2 >= (1LL << 31)) return -1;  // 32-bit buffer offsets
   if (epi == EPI_SWIGLU && N % 64 != 0) return -1;
-  if (epi == EPI_RESIDUAL && R == nullptr) return -1;
+  if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256, tiles = tiles_m * tiles_n, KT = K / 64;
   int wpx = device_cus() / 8;
@@ -411,6 +429,8 @@ extern "C" int lwc_gemm8p(const void* A, const void* W, void* C, const void* R, 
     case EPI_PLAIN: return launch<EPI_PLAIN>(p, s);
     case EPI_RESIDUAL: return launch<EPI_RESIDUAL>(p, s);
     case EPI_SWIGLU: return launch<EPI_SWIGLU>(p, s);
+    case EPI_BIAS: return launch<EPI_BIAS>(p, s);
+    case EPI_BIAS_GELU: return launch<EPI_BIAS_GELU>(p, s);
   }
   return -1;
 }

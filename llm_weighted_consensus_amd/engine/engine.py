@@ -259,6 +259,11 @@ class LLMEngine:
         # an admission (0 = whole admission batches, then decode: the throughput bench's mode)
         self.chunked_prefill = int(chunked_prefill)
         self.prefilling: List[SequenceGroup] = []
+        # a chunk runs when a full budget of prompt tokens is pending, nothing is decoding, or the oldest
+        # admitted prompt has waited this many decode steps (small prompts batch up instead of paying a
+        # whole-model prefill launch each per step)
+        self.chunk_max_wait = 3
+        self._chunk_wait = 0
         self.width = (max_model_len + block_size - 1) // block_size
         if num_blocks is None:
             free, _total = torch.cuda.mem_get_info(self.device)
@@ -529,22 +534,42 @@ class LLMEngine:
             admitted = self._admit() if fits else []
         self.prefilling.extend(admitted)
         if self.prefilling:
-            events += self._drain()  # the chunk writes the block manager / KV pool: no step in flight
-            with span("prefill.chunk"):
-                events += self._prefill_chunk()
+            pending = sum(len(g.prompt_ids) - max(g.pf_pos, 0) for g in self.prefilling)
+            if (pending >= self.chunked_prefill or not self.running or self._chunk_wait >= self.chunk_max_wait
+                    or any(g.prefilled is not None for g in self.prefilling)):
+                self._chunk_wait = 0
+                events += self._drain()  # the chunk writes the block manager / KV pool: no step in flight
+                with span("prefill.chunk"):
+                    events += self._prefill_chunk()
+            else:
+                self._chunk_wait += 1
         if self.running or self.inflight is not None:
             events += self._decode()
         return events
 
     def _prefill_chunk(self) -> List[TokenEvent]:
-        bs = self.block_size
         imported = [g for g in self.prefilling if g.prefilled is not None]
         if imported:  # prompts prefilled elsewhere cost no compute: start them now
             self.prefilling = [g for g in self.prefilling if g.prefilled is None]
             return self._prefill(imported)
         budget = self.chunked_prefill
+        events: List[TokenEvent] = []
+        # up to two passes per step: prompts deferred behind a shared head whose leader completes in the
+        # first pass take the head from the prefix cache in the second (the two-wave prefill, chunked)
+        for _ in range(2):
+            items, budget, deferred = self._chunk_items(budget)
+            if not items:
+                break
+            events += self._finish_chunk(items, self._run_chunk(items))
+            if not deferred or budget <= 0:
+                break
+        return events
+
+    def _chunk_items(self, budget: int):
+        bs = self.block_size
         items: List[Tuple[SequenceGroup, int, int]] = []
         heads = set()
+        deferred = False
         for g in self.prefilling:
             if budget <= 0:
                 break
@@ -554,6 +579,7 @@ class LLMEngine:
                 # a prompt sharing its first block with one in progress waits for it and then takes the
                 # shared head from the prefix cache (the voters of one score request)
                 if self.prefix_caching and head is not None and head in heads:
+                    deferred = True
                     continue
                 if self.prefix_caching:
                     g.pf_pos = int(self.bm.add_sequence_cached(-g.id, p))
@@ -566,9 +592,9 @@ class LLMEngine:
             n = min(budget, len(p) - g.pf_pos)
             items.append((g, g.pf_pos, g.pf_pos + n))
             budget -= n
-        if not items:
-            return []
-        logits = self._run_chunk(items)
+        return items, budget, deferred
+
+    def _finish_chunk(self, items, logits) -> List[TokenEvent]:
         done, logits_of = [], {}
         for i, (g, a, e) in enumerate(items):
             g.pf_pos = e

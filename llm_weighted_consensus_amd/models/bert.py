@@ -29,6 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import gemm_plan
 from .config import EncoderConfig
 
 POOL_MODES = {"cls": ops.POOL_CLS, "mean": ops.POOL_MEAN, "last": ops.POOL_LAST}
@@ -148,14 +149,15 @@ class BertEncoder:
         T = ids.shape[0]
         x = ops.layernorm(ops.embedding(self.word, ids), self.emb_ln_g, self.emb_ln_b, c.ln_eps,
                           residual=ops.embedding(self.pos_type, positions))
+        lin = gemm_plan.linear_bias  # bias (+ GELU) in the GEMM epilogue (gemm8p) or hipBLASLt, per shape
         for L in self.layers:
-            qkv = F.linear(x, L.wqkv, L.bqkv)
+            qkv = lin(x, L.wqkv, L.bqkv)
             a = ops.prefill_attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], cu, max_len, H, H, Dh, self.scale,
                                       causal=False)
-            o = F.linear(a, L.wo, L.bo)
+            o = lin(a, L.wo, L.bo)
             x = ops.layernorm(o, L.ln1_g, L.ln1_b, c.ln_eps, residual=x)
-            h = ops.bias_gelu_(F.linear(x, L.w1), L.b1)
-            y = F.linear(h, L.w2, L.b2)
+            h = lin(x, L.w1, L.b1, gelu=True)
+            y = lin(h, L.w2, L.b2)
             x = ops.layernorm(y, L.ln2_g, L.ln2_b, c.ln_eps, residual=x)
         return x
 

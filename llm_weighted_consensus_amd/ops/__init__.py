@@ -228,16 +228,26 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
 
 
 def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, swiglu: bool = False, ws=None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, swiglu: bool = False, ws=None, bias: Optional[torch.Tensor] = None,
+           gelu: bool = False) -> torch.Tensor:
     """8-phase 256x256-tile MFMA GEMM (K6, csrc/kernels/gemm8p.hip): A [M, K] . W[N, K]^T (+ residual)
     -> [M, N] bf16.  ``swiglu=True`` takes a gate/up weight laid out by :func:`swiglu_interleave` and
     returns silu(A Wg^T) * (A Wu^T) [M, N/2] from the GEMM epilogue (no [M, N] intermediate).
     ``ws`` = (partials, flags) stream-K workspace (:func:`gemm8p_workspace`); a model passes its own so
-    a captured graph owns no allocation; default: one per (device, stream), created outside capture."""
+    a captured graph owns no allocation; default: one per (device, stream), created outside capture.
+    ``bias`` [N] (+ ``gelu``: exact erf GELU) is applied to the fp32 accumulators in the epilogue (the
+    encoder's projections; FFN1's bias+GELU needs no separate pass)."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
-    epi = 2 if swiglu else (1 if residual is not None else 0)
+    if bias is not None:
+        if swiglu or residual is not None:
+            raise ValueError("gemm8p: bias epilogue combines with neither swiglu nor residual")
+        epi, residual = (4 if gelu else 3), bias
+    else:
+        if gelu:
+            raise ValueError("gemm8p: gelu needs a bias")
+        epi = 2 if swiglu else (1 if residual is not None else 0)
     part, flags = ws if ws is not None else gemm8p_workspace(A.device)
     kernels().gemm8p(A, W, out, residual, epi, part, flags)
     return out

@@ -21,7 +21,7 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import gemm8p, silu_mul
+from . import bias_gelu_, gemm8p, silu_mul
 
 MODE = os.environ.get("LWC_GEMM", "auto")
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
@@ -68,6 +68,34 @@ def swiglu(x: torch.Tensor, w_gu: torch.Tensor, block: int, ws=None) -> torch.Te
     if block == 32 and choice(M, N, K, "swiglu") == "g8" and _g8_ok(N, K, "swiglu") and x.stride(1) == 1:
         return gemm8p(x, w_gu, swiglu=True, ws=ws)
     return silu_mul(F.linear(x, w_gu), block=block)
+
+
+def _m_bucket(M: int) -> int:
+    """Encoder token counts vary per call: tune per power-of-two bucket (everything >= 64k tokens is one)."""
+    return min(1 << max(M - 1, 1).bit_length(), 1 << 16)
+
+
+def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = False, ws=None) -> torch.Tensor:
+    """x . w^T + b (optionally exact-erf GELU) — the encoder projections.  g8 applies the bias / GELU in
+    its epilogue on the fp32 accumulators; blas is hipBLASLt with the bias (+ the K9b bias_gelu pass).
+    The backend is chosen per (token bucket, N, K, epilogue) by timing both on the first call."""
+    M, K = x.shape
+    N = w.shape[0]
+    epi = "bias_gelu" if gelu else "bias"
+    key = (_m_bucket(M), N, K, epi)
+    c = MODE if MODE in ("blas", "g8") else _CHOICE.get(key)
+    ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda
+    run_g8 = lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws)  # noqa: E731
+    run_blas = (lambda: bias_gelu_(F.linear(x, w), b)) if gelu else (lambda: F.linear(x, w, b))  # noqa: E731
+    if c is None:
+        if not ok or torch.cuda.is_current_stream_capturing():
+            c = "blas"
+        else:
+            t_blas, t_g8 = _time(run_blas, iters=2, rounds=3), _time(run_g8, iters=2, rounds=3)
+            TIMINGS[key] = {"blas": t_blas, "g8": t_g8}
+            c = "g8" if t_g8 < t_blas else "blas"
+        _CHOICE[key] = c
+    return run_g8() if c == "g8" and ok else run_blas()
 
 
 def _time(fn, iters: int = 5, rounds: int = 3) -> float:
