@@ -47,13 +47,31 @@ Segment = Union[Lit, Str, Alt]
 
 
 def _trie(options: Sequence[bytes]) -> Dict:
-    root: Dict = {}
+    """Byte trie of the options: child per byte, -1 = an option ends here, -2 = the node's prefix bytes
+    (its identity across constraint instances with the same options)."""
+    root: Dict = {-2: b""}
     for o in options:
         n = root
         for b in o:
-            n = n.setdefault(b, {})
+            if b not in n:
+                n[b] = {-2: n[-2] + bytes([b])}
+            n = n[b]
         n[-1] = True  # terminal marker
     return root
+
+
+# Content ids of segment-list suffixes: equal ids <=> the same remaining grammar, whichever constraint
+# instance (voter, request) it belongs to — the key of the cross-request token-mask cache.
+_SUFFIX_IDS: Dict[tuple, int] = {}
+
+
+def _suffix_id(desc: tuple) -> int:
+    v = _SUFFIX_IDS.get(desc)
+    if v is None:
+        if len(_SUFFIX_IDS) > 1 << 16:
+            _SUFFIX_IDS.clear()
+        v = _SUFFIX_IDS[desc] = len(_SUFFIX_IDS) + 1
+    return v
 
 
 # printable ASCII minus the quote and backslash: keeps constrained text valid UTF-8 and valid JSON
@@ -68,6 +86,14 @@ class SegmentConstraint:
         self.segments = segments
         self.eos_id = eos_id
         self.tries = {i: _trie(s.options) for i, s in enumerate(segments) if isinstance(s, Alt)}
+        # suffix_ids[i] identifies segments[i:] by content
+        self.suffix_ids = [0] * (len(segments) + 1)
+        nxt = 0
+        for i in range(len(segments) - 1, -1, -1):
+            seg = segments[i]
+            d = ("L", seg.data) if isinstance(seg, Lit) else ("S", seg.max_len) if isinstance(seg, Str) \
+                else ("A", tuple(sorted(seg.options)))
+            nxt = self.suffix_ids[i] = _suffix_id((d, nxt, eos_id))
 
     # ---- FSM
     def start(self):
@@ -107,13 +133,29 @@ class SegmentConstraint:
             allowed |= nb
         else:  # Alt: trie node
             for b in local:
-                if b != -1:
+                if b >= 0:
                     allowed[b] = True
             if -1 in local:  # an option may end here
                 nb, eos = self.allowed_bytes(self._normalize((i + 1, 0)))
                 allowed |= nb
                 return allowed, eos
         return allowed, False
+
+    def accepts(self, st, b: int) -> bool:
+        """Whether byte ``b`` is allowed in state ``st`` (allowed_bytes(st)[b] without the arrays)."""
+        i, local = st
+        if i >= len(self.segments):
+            return False
+        seg = self.segments[i]
+        if isinstance(seg, Lit):
+            return seg.data[local] == b
+        if isinstance(seg, Str):
+            if _STR_ALLOWED[b] and local < seg.max_len:
+                return True
+            return self.accepts(self._normalize((i + 1, 0)), b)
+        if b in local:
+            return True
+        return -1 in local and self.accepts(self._normalize((i + 1, 0)), b)
 
     def advance(self, st, token: int):
         if token < 0 or token > 255:
@@ -196,6 +238,8 @@ class TokenVocab:
             fub[i] = arr[bad[0]] if len(bad) else 0
         self.first_unsafe, self.first_unsafe_byte = fu, fub
         self.nonempty = self.lens > 0
+        # cross-request mask cache: (grammar-suffix id, state within the segment) -> (digest, words)
+        self.masks: Dict[Any, Tuple[bytes, np.ndarray]] = {}
 
     @staticmethod
     def of(tok, vocab_size: int) -> "TokenVocab":
@@ -223,7 +267,6 @@ class TokenConstraint:
         self.fsm = fsm
         self.vocab = vocab
         self.eos_id = fsm.eos_id
-        self._masks: Dict[Any, Tuple[bytes, np.ndarray]] = {}
 
     def start(self):
         return self.fsm.start()
@@ -235,8 +278,7 @@ class TokenConstraint:
         """State after consuming ``data``, or None if the FSM rejects a byte."""
         fsm = self.fsm
         for b in data:
-            allowed, _ = fsm.allowed_bytes(st)
-            if not allowed[b]:
+            if not fsm.accepts(st, b):
                 return None
             st = fsm.advance(st, b)
         return st
@@ -249,16 +291,19 @@ class TokenConstraint:
 
     # ---- masks
     def _key(self, st):
+        """Content key of the state's token mask: the remaining grammar (suffix id) and the position in
+        the current segment — equal across voters / requests whose remaining grammar is equal."""
         i, local = st
         segs = self.fsm.segments
         if i >= len(segs):
-            return ("done",)
+            return (0, self.eos_id)
         seg = segs[i]
+        sid = self.fsm.suffix_ids[i]
         if isinstance(seg, Str):  # only the remaining length matters, and only up to the longest token
-            return (i, "str", min(seg.max_len - local, self.vocab.max_len + 1))
+            return (sid, min(seg.max_len - local, self.vocab.max_len + 1))
         if isinstance(seg, Alt):
-            return (i, "alt", id(local))
-        return (i, "lit", local)
+            return (sid, local[-2])
+        return (sid, local)
 
     def allowed_tokens(self, st) -> Tuple[np.ndarray, bool]:
         """(bool [V] allowed tokens, eos allowed) in FSM state ``st``."""
@@ -310,7 +355,7 @@ class TokenConstraint:
     def mask_entry(self, st) -> Tuple[bytes, np.ndarray]:
         """(content digest, uint32 bitmask [V/32]) for the sampler's mask table."""
         key = self._key(st)
-        hit = self._masks.get(key)
+        hit = self.vocab.masks.get(key)
         if hit is not None:
             return hit
         ok, eos = self.allowed_tokens(st)
@@ -318,7 +363,9 @@ class TokenConstraint:
             ok[self.eos_id] = True  # done, or a dead end: EOS lets the sequence stop
         words = np.packbits(ok, bitorder="little").view(np.uint32)
         hit = (hashlib.blake2b(words.tobytes(), digest_size=16).digest(), words)
-        self._masks[key] = hit
+        if len(self.vocab.masks) > 8192:
+            self.vocab.masks.clear()
+        self.vocab.masks[key] = hit
         return hit
 
 

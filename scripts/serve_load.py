@@ -57,7 +57,7 @@ def main():
     models = {"local": {"arch": a.arch, "weights": "random:1", "max_model_len": 2048, "max_batch": a.max_batch}}
     t0 = time.time()
     state = build_state(Config(models=models, kv_fraction=0.6,
-                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "2048"))))
+                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "0"))))
     print(f"# model ready in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     app = create_app(state)
     client = httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t", timeout=600)

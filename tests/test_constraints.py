@@ -133,3 +133,21 @@ def test_token_vocab_cached_per_tokenizer(tmp_path):
     assert compile_json_schema({"type": "array"}) is None
     with pytest.raises(ValueError):
         constraint_for_schema(_schema(False), tok, 607)
+
+
+def test_masks_shared_across_voters_with_equal_remaining_grammar(tmp_path):
+    """Voters of different requests (different key orders / sets) reuse each other's masks wherever their
+    REMAINING grammar is equal: the cache key is content, not the constraint instance."""
+    tok, V = _tokenizers(tmp_path)["bytelevel"]
+    a = constraint_for_schema(response_key_format(["`A`", "`B`"], False).json_schema.schema_, tok, V)
+    b = constraint_for_schema(response_key_format(["`B`", "`A`"], False).json_schema.schema_, tok, V)
+    c = constraint_for_schema(response_key_format(["`C`", "`D`"], False).json_schema.schema_, tok, V)
+    sa, sb, sc = a.start(), b.start(), c.start()
+    assert a._key(sa) == b._key(sb)            # same enum SET: the same grammar from the start
+    assert a._key(sa) != c._key(sc)            # a different enum: a different suffix
+    ea = a.mask_entry(sa)
+    assert b.mask_entry(sb) is ea              # served from the vocab-level cache
+    # after the key, every voter is in the same closing literal
+    ta = a.advance_bytes(sa, b'{"response_key":"`A`')
+    tc = c.advance_bytes(sc, b'{"response_key":"`C`')
+    assert a._key(ta) == c._key(tc) and np.array_equal(a.allowed_tokens(ta)[0], c.allowed_tokens(tc)[0])
