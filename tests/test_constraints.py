@@ -148,6 +148,6 @@ def test_masks_shared_across_voters_with_equal_remaining_grammar(tmp_path):
     ea = a.mask_entry(sa)
     assert b.mask_entry(sb) is ea              # served from the vocab-level cache
     # after the key, every voter is in the same closing literal
-    ta = a.advance_bytes(sa, b'{"response_key":"`A`')
-    tc = c.advance_bytes(sc, b'{"response_key":"`C`')
+    ta = a.advance_bytes(sa, b'{"response_key":"`A`"')
+    tc = c.advance_bytes(sc, b'{"response_key":"`C`"')
     assert a._key(ta) == c._key(tc) and np.array_equal(a.allowed_tokens(ta)[0], c.allowed_tokens(tc)[0])
