@@ -302,6 +302,8 @@ class TokenConstraint:
         if isinstance(seg, Str):  # only the remaining length matters, and only up to the longest token
             return (sid, min(seg.max_len - local, self.vocab.max_len + 1))
         if isinstance(seg, Alt):
+            if -1 in local and all(k < 0 for k in local):  # a completed option: the rest of the grammar
+                return self._key(self.fsm._normalize((i + 1, 0)))
             return (sid, local[-2])
         return (sid, local)
 
