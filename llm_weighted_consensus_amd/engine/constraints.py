@@ -309,17 +309,25 @@ class TokenConstraint:
 
     def allowed_tokens(self, st) -> Tuple[np.ndarray, bool]:
         """(bool [V] allowed tokens, eos allowed) in FSM state ``st``."""
+        sparse, dense, eos = self._allowed(st)
+        if dense is None:
+            dense = np.zeros(self.vocab.vocab_size, dtype=bool)
+            dense[sparse] = True
+        return dense, eos
+
+    def _allowed(self, st):
+        """(sorted allowed ids or None, dense bool [V] or None, eos allowed).  Literal / enum states allow a
+        handful of tokens and stay sparse (no [V] arrays on the per-step path); free-string states are
+        vectorised over the whole vocabulary."""
         fsm, tv = self.fsm, self.vocab
-        V = tv.vocab_size
-        ok = np.zeros(V, dtype=bool)
         if fsm.is_done(st):
-            return ok, True
+            return [], None, True
         i, local = st
         seg = fsm.segments[i]
         if isinstance(seg, Str):
             room = seg.max_len - local
             # tokens that stay inside the string: every byte string-safe and the length fits
-            ok |= tv.nonempty & (tv.first_unsafe == tv.lens) & (tv.lens <= room)
+            ok = tv.nonempty & (tv.first_unsafe == tv.lens) & (tv.lens <= room)
             # tokens that close the string: a safe prefix, then a byte the FSM accepts to end it
             allowed, _ = fsm.allowed_bytes(st)
             cand = np.nonzero(tv.nonempty & (tv.first_unsafe < tv.lens) & (tv.first_unsafe <= room)
@@ -328,15 +336,16 @@ class TokenConstraint:
                 k = int(tv.first_unsafe[t])
                 if self.advance_bytes((i, local + k), tv.tb[t][k:]) is not None:
                     ok[t] = True
-            return ok, False
+            return None, ok, False
         # literal / alternative states: walk the vocabulary trie guided by the FSM's allowed bytes
+        found: List[int] = []
         stack = [(st, 0, len(tv.keys), 0)]
         ids, keys = tv.ids, tv.keys
         while stack:
             cur, lo, hi, depth = stack.pop()
             while lo < hi and len(keys[lo]) == depth:  # tokens ending exactly here were fully accepted
                 if depth:
-                    ok[ids[lo]] = True
+                    found.append(ids[lo])
                 lo += 1
             if lo >= hi or fsm.is_done(cur):
                 continue
@@ -345,30 +354,78 @@ class TokenConstraint:
                 # entered a free string mid-token: finish the (few) tokens of this subtree one by one
                 for k in range(lo, hi):
                     if self.advance_bytes(cur, keys[k][depth:]) is not None:
-                        ok[ids[k]] = True
+                        found.append(ids[k])
                 continue
-            allowed, _ = fsm.allowed_bytes(cur)
-            for b in np.nonzero(allowed)[0].tolist():
+            for b in self._next_bytes(cur):
                 a, z = tv.child_range(lo, hi, depth, b)
                 if a < z:
                     stack.append((fsm.advance(cur, b), a, z, depth + 1))
-        return ok, False
+        found.sort()
+        return found, None, False
 
-    def mask_entry(self, st) -> Tuple[bytes, np.ndarray]:
-        """(content digest, uint32 bitmask [V/32]) for the sampler's mask table."""
+    def _next_bytes(self, st) -> List[int]:
+        """The bytes the FSM accepts in a literal / enum state (a few; no [256] arrays)."""
+        fsm = self.fsm
+        i, local = st
+        seg = fsm.segments[i]
+        if isinstance(seg, Lit):
+            return [seg.data[local]]
+        if isinstance(seg, Alt):
+            out = [b for b in local if b >= 0]
+            if -1 in local and i + 1 < len(fsm.segments):
+                out += [b for b in self._next_bytes_any(fsm._normalize((i + 1, 0))) if b not in out]
+            return out
+        return self._next_bytes_any(st)
+
+    def _next_bytes_any(self, st) -> List[int]:
+        if self.fsm.is_done(st):
+            return []
+        i, _ = st
+        if isinstance(self.fsm.segments[i], Str):
+            allowed, _ = self.fsm.allowed_bytes(st)
+            return np.nonzero(allowed)[0].tolist()
+        return self._next_bytes(st)
+
+    def mask_entry(self, st) -> "MaskEntry":
+        """The state's mask for the sampler's table: ``.key`` (content) and ``.words()`` (uint32 [V/32]),
+        cached per remaining-grammar state across every voter and request of this vocabulary."""
         key = self._key(st)
         hit = self.vocab.masks.get(key)
         if hit is not None:
             return hit
-        ok, eos = self.allowed_tokens(st)
-        if (eos or not ok.any()) and 0 <= self.eos_id < ok.shape[0]:
-            ok[self.eos_id] = True  # done, or a dead end: EOS lets the sequence stop
-        words = np.packbits(ok, bitorder="little").view(np.uint32)
-        hit = (hashlib.blake2b(words.tobytes(), digest_size=16).digest(), words)
+        sparse, dense, eos = self._allowed(st)
+        V = self.vocab.vocab_size
+        if sparse is not None:
+            if (eos or not sparse) and 0 <= self.eos_id < V and self.eos_id not in sparse:
+                sparse = sorted(sparse + [self.eos_id])  # done, or a dead end: EOS lets the sequence stop
+            hit = MaskEntry(("s", tuple(sparse)), V, ids=sparse)
+        else:
+            if (eos or not dense.any()) and 0 <= self.eos_id < V:
+                dense[self.eos_id] = True
+            words = np.packbits(dense, bitorder="little").view(np.uint32)
+            hit = MaskEntry(("d", hashlib.blake2b(words.tobytes(), digest_size=16).digest()), V, words=words)
         if len(self.vocab.masks) > 8192:
             self.vocab.masks.clear()
         self.vocab.masks[key] = hit
         return hit
+
+
+class MaskEntry:
+    """One token mask: a hashable content key (the allowed ids themselves for sparse masks, a digest of
+    the bits for dense ones) and the packed words, built only when the engine uploads a new table row."""
+
+    __slots__ = ("key", "V", "_ids", "_words")
+
+    def __init__(self, key, V: int, ids: Optional[List[int]] = None, words: Optional[np.ndarray] = None):
+        self.key, self.V, self._ids, self._words = key, V, ids, words
+
+    def words(self) -> np.ndarray:
+        if self._words is None:
+            w = np.zeros(self.V // 32, dtype=np.uint32)
+            ids = np.asarray(self._ids, dtype=np.int64)
+            np.bitwise_or.at(w, ids >> 5, (np.uint32(1) << (ids & 31).astype(np.uint32)))
+            self._words = w
+        return self._words
 
 
 def constraint_for_schema(schema: Any, tok, vocab_size: Optional[int] = None) -> Optional[TokenConstraint]:

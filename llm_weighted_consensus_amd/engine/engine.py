@@ -881,7 +881,8 @@ class LLMEngine:
         new: List[Tuple[int, np.ndarray]] = []
         for i in cons:
             s = seqs[i]
-            key, m = s.params.constraint.mask_entry(s.constraint_state)
+            ent = s.params.constraint.mask_entry(s.constraint_state)
+            key = ent.key
             r = self._mask_rows_of.get(key)
             if r is None:
                 if len(self._mask_rows_of) >= self._mask_limit:  # bounded: start the table over
@@ -889,7 +890,7 @@ class LLMEngine:
                     return self._constraint_masks(seqs, cons)
                 r = len(self._mask_rows_of)
                 self._mask_rows_of[key] = r
-                new.append((r, m))
+                new.append((r, ent.words()))
             rows[i] = r
         if new:
             need = max(r for r, _ in new) + 1

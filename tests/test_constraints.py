@@ -100,7 +100,7 @@ def test_ids_0_255_are_not_bytes_for_real_tokenizers(tmp_path):
     brace_ids = tok.ids_for_text("{")
     assert ok[brace_ids[0]] and brace_ids[0] != ord("{") or ok[ord("{")]
     # the mask entry packs the same set, plus nothing else
-    _, words = c.mask_entry(c.start())
+    words = c.mask_entry(c.start()).words()
     bits = np.unpackbits(words.view(np.uint8), bitorder="little").astype(bool)
     assert np.array_equal(bits[:V], ok)
 
@@ -122,7 +122,7 @@ def test_string_room_and_mask_cache(tmp_path):
     assert {c.vocab.tb[t] for t in np.nonzero(ok)[0]} == {b'"'}  # no room left: only the closing quote
     st2 = c.advance_bytes(c.start(), b'{"_think":"a')
     st3 = c.advance_bytes(c.start(), b'{"_think":"b')
-    assert c.mask_entry(st2)[0] == c.mask_entry(st3)[0]
+    assert c.mask_entry(st2).key == c.mask_entry(st3).key
     assert c._key(st2) == c._key(st3)
     assert c.advance(st, tok.eos_token_id)[0] == len(c.fsm.segments)
 
