@@ -84,7 +84,8 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
     epi = "bias_gelu" if gelu else "bias"
     key = (_m_bucket(M), N, K, epi)
     c = MODE if MODE in ("blas", "g8") else _CHOICE.get(key)
-    ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda
+    # gemm8p addresses A through 32-bit buffer offsets: operands of 2 GiB or more take the library path
+    ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda and M * x.stride(0) * 2 < (1 << 31)
     run_g8 = lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws)  # noqa: E731
     run_blas = (lambda: bias_gelu_(F.linear(x, w), b)) if gelu else (lambda: F.linear(x, w, b))  # noqa: E731
     if c is None:
