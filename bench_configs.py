@@ -83,7 +83,9 @@ def bench_moe(a):
         comm = CustomAllReduce(device=dev, max_bytes=a.requests * a.candidates * dcfg.hidden * 2)
     model = MixtralModel(dcfg, device=dev, seed=11, max_position=a.prompt_len + a.gen_len + 64, fp8=not a.bf16,
                          tp_rank=info.rank if tp > 1 else 0, tp_size=tp, tp_comm=comm)
-    emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64)
+    # config 5 is fp8 throughout: the embedder's projections too (e4m3 + per-channel scales, fp8 library GEMM)
+    emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64,
+                           fp8_dense=not a.bf16)
     scorer = EmbeddingConsensus(DecoderEmbedder(emb_model, max_tokens=a.gen_len + 16), tau=0.05)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     R, N = a.requests, a.candidates
@@ -115,7 +117,8 @@ def bench_moe(a):
     return {"metric": "consensus answers/sec (config 5: Mixtral-8x7B sampler + e5-mistral-7b embedder)",
             "value": round(R / dt, 4), "unit": "answers/s", "n_gpus": 1 if shared else tp, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-            "dtype": "bf16 activations, fp8 e4m3 expert weights" if not a.bf16 else "bf16",
+            "dtype": ("fp8 e4m3 weights (experts, attention projections, embedder projections; per-channel scales) "
+                      "x row-quantised e4m3 activations, bf16 elsewhere") if not a.bf16 else "bf16",
             "data": "synthetic prompts (random token ids), random-init weights",
             "generated_tokens_per_s": round(R * N * a.gen_len / dt, 1),
             "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": R, "candidates_per_request": N,

@@ -316,7 +316,8 @@ def build_engine(spec: dict, wid: int):
         model = MixtralModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
                              fp8=bool(spec.get("fp8", False)))
     else:
-        model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64)
+        model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
+                           fp8_dense=bool(spec.get("fp8", False)))
     tok = load_tokenizer(spec, cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
     return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
                      kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),

@@ -98,7 +98,7 @@ class _NullCache:
 
 class LlamaModel:
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
-                 weights_path: Optional[str] = None, max_position: Optional[int] = None):
+                 weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8_dense: bool = False):
         if cfg.num_experts and type(self) is LlamaModel:
             raise NotImplementedError("MoE decoders use models.mixtral.MixtralModel")
         self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
@@ -109,11 +109,21 @@ class LlamaModel:
             self._random_init(seed)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.g8_ws = None
+        # fp8 configurations (BASELINE config 5: the e5-mistral embedder): the qkv / o / gate|up / down
+        # projections in e4m3 with per-channel scales, activations quantised per row; lm_head stays bf16
+        self.fp8_dense = bool(fp8_dense) and self.device.type == "cuda"
+        if self.fp8_dense:
+            for L in self.layers:
+                if isinstance(L, LayerWeights):
+                    L.wqkv, L.wo = ops.Fp8Weight(L.wqkv), ops.Fp8Weight(L.wo)
+                    L.w_gate_up, L.w_down = ops.Fp8Weight(L.w_gate_up), ops.Fp8Weight(L.w_down)
+            torch.cuda.empty_cache()
         if self.device.type == "cuda":
             # gemm8p (ops/gemm_plan.py): the gate|up rows interleaved in blocks of 32 so its epilogue can
             # apply SwiGLU; a stream-K workspace owned by the model (never allocated inside a capture)
             for L in self.layers:
-                if isinstance(L, LayerWeights) and L.gu_block == 0 and L.w_gate_up.shape[0] % 64 == 0:
+                if (isinstance(L, LayerWeights) and not self.fp8_dense and L.gu_block == 0
+                        and L.w_gate_up.shape[0] % 64 == 0):
                     L.w_gate_up = ops.swiglu_interleave(L.w_gate_up)
                     L.gu_block = 32
             self.g8_ws = ops.new_gemm8p_workspace(self.device)
@@ -208,10 +218,14 @@ class LlamaModel:
     @property
     def _dense_residual(self) -> bool:
         cls = type(self)
-        return cls._attn_out is LlamaModel._attn_out and cls._mlp is LlamaModel._mlp
+        return (cls._attn_out is LlamaModel._attn_out and cls._mlp is LlamaModel._mlp
+                and not getattr(self, "fp8_dense", False))
 
     def _proj(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        """Dense projection on the per-shape backend (hipBLASLt or gemm8p, ops/gemm_plan.py)."""
+        """Dense projection on the per-shape backend (hipBLASLt or gemm8p, ops/gemm_plan.py; e4m3 weights:
+        row-quantised activations into the fp8 library GEMM)."""
+        if isinstance(w, ops.Fp8Weight):
+            return ops.linear_fp8(x, w)
         if self.g8_ws is None:
             return F.linear(x, w)
         return gemm_plan.linear(x, w, ws=self.g8_ws)
@@ -222,7 +236,11 @@ class LlamaModel:
 
     def _mlp(self, h: torch.Tensor, L) -> torch.Tensor:
         """Dense SwiGLU MLP: gate|up GEMM with SwiGLU (fused in gemm8p's epilogue, or hipBLASLt + K5
-        silu_mul), down GEMM."""
+        silu_mul), down GEMM.  fp8: gate|up fp8 GEMM, SwiGLU fused with the down projection's row
+        quantisation (K11e), down fp8 GEMM."""
+        if isinstance(L.w_down, ops.Fp8Weight):
+            aq, as_ = ops.silu_mul_quant_fp8(self._proj(h, L.w_gate_up), block=L.gu_block)
+            return ops.linear_fp8_q(aq, as_, L.w_down)
         return self._proj(self._act(h, L), L.w_down)
 
     def _act(self, h: torch.Tensor, L) -> torch.Tensor:
@@ -234,7 +252,7 @@ class LlamaModel:
     def tune_gemms(self, M: int) -> None:
         """Pick the GEMM backend of every decode projection at batch M by timing both (before the
         bucket's hipGraph is captured; see ops/gemm_plan.py)."""
-        if self.g8_ws is None or not isinstance(self.layers[0], LayerWeights):
+        if self.g8_ws is None or not isinstance(self.layers[0], LayerWeights) or self.fp8_dense:
             return
         cfg, L = self.cfg, self.layers[0]
         x = torch.randn(M, cfg.hidden, device=self.device).to(self.dtype)

@@ -114,6 +114,8 @@ class MixtralModel(LlamaModel):
         if self.fp8:
             w13, s13 = ops.quant_fp8_weight(w13)
             w2_s, s2 = ops.quant_fp8_weight(w2_s)
+            # the attention projections are fp8 too (config 5: fp8 MFMA throughout; router and lm_head bf16)
+            wqkv, wo_s = ops.Fp8Weight(wqkv), ops.Fp8Weight(wo_s)
         return MoELayerWeights(attn_norm, wqkv, wo_s, mlp_norm, router.contiguous(), w13, w2_s, s13, s2)
 
     def _random_init(self, seed: int) -> None:
@@ -184,7 +186,7 @@ class MixtralModel(LlamaModel):
         return self.tp_size == 1 and self.ep_size == 1 or (self.tp_size > 1 and self.tp_comm is not None)
 
     def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
-        return self._all_reduce(F.linear(attn, L.wo))
+        return self._all_reduce(self._proj(attn, L.wo))
 
     def _experts(self, x: torch.Tensor, row_off: torch.Tensor, L: MoELayerWeights,
                  scale: Optional[torch.Tensor] = None, a_rows: Optional[torch.Tensor] = None,

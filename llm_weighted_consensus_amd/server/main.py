@@ -56,7 +56,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 dcfg = decoder_config(spec["arch"])
                 mtok = int(spec.get("max_tokens", 4096))
                 enc = DecoderEmbedder(LlamaModel(dcfg, device=dev, seed=seed, weights_path=path,
-                                                 max_position=mtok + 64), max_tokens=mtok)
+                                                 max_position=mtok + 64, fp8_dense=bool(spec.get("fp8", False))),
+                                      max_tokens=mtok)
             else:
                 enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
                                   dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)

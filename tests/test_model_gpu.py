@@ -265,3 +265,29 @@ def test_engine_prefix_cache_shares_heads_within_one_batch(tiny, gpu):
     assert outs[0] == outs[1]
     saved = stats[0]["prefill_tokens"] - stats[1]["prefill_tokens"]
     assert saved == stats[1]["prefix_cache_tokens"] >= 3 * 96
+
+
+def test_fp8_dense_decoder_embedder_and_prefill(gpu):
+    """fp8 dense projections (config 5's e5-mistral embedder; e4m3 weights with per-channel scales, row-
+    quantised activations into the fp8 library GEMM): embeddings and prefill logits track the fp32
+    reference of the dequantised weights; the engine decodes with them (graphs on)."""
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.embedder import DecoderEmbedder
+    from llm_weighted_consensus_amd.models.llama import LlamaModel
+
+    m = LlamaModel(decoder_config("llama-tiny"), device=gpu, seed=3, max_position=1024, fp8_dense=True)
+    assert isinstance(m.layers[0].wqkv, ops.Fp8Weight) and not m._dense_residual
+    lists = [list(range(40, 100)), [7, 8, 9, 10]]
+    e, _ = DecoderEmbedder(m).embed(lists)
+    for i, tl in enumerate(lists):
+        r = torch.nn.functional.normalize(ref.llama_hidden(m, torch.tensor(tl, device=gpu))[-1], dim=0)
+        assert _cos(e[i], r) > 0.99
+    tok = ByteTokenizer(m.cfg.vocab_size)
+    eng = LLMEngine(m, tok, num_blocks=256, max_batch=16, max_model_len=512)
+    out = eng.generate([tok.encode("fp8 projections " * 4)], SamplingParams(temperature=0.0, max_tokens=6,
+                                                                          ignore_eos=True), n=2)
+    assert len(out[0]) == 2 and out[0][0] == out[0][1] and len(out[0][0]) == 6

@@ -40,6 +40,13 @@ def attention(q, k, v, causal, scale):
     return torch.einsum("hqk,khd->qhd", p, v.float())
 
 
+def dense(w):
+    """fp32 view of a projection weight (bf16 tensor, or an ops.Fp8Weight dequantised: q * s)."""
+    if hasattr(w, "q") and hasattr(w, "s"):
+        return w.q.float() * w.s.view(-1, 1)
+    return w.float()
+
+
 def llama_forward(model, tokens, hidden_only=False):
     """Full-sequence fp32 forward of a models.llama.LlamaModel (single sequence) -> logits [T, V]."""
     cfg = model.cfg
@@ -49,25 +56,25 @@ def llama_forward(model, tokens, hidden_only=False):
     x = model.embed[tokens.long()].float()
     for L in model.layers:
         h = rmsnorm(x, L.attn_norm, cfg.rms_eps)
-        qkv = h @ L.wqkv.float().t()
+        qkv = h @ dense(L.wqkv).t()
         q = qkv[:, : Hq * D].view(T, Hq, D)
         k = qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D)
         v = qkv[:, (Hq + Hkv) * D:].view(T, Hkv, D)
         q = rope(q, pos, model.cos, model.sin)
         k = rope(k, pos, model.cos, model.sin)
         a = attention(q, k, v, True, 1.0 / math.sqrt(D)).reshape(T, Hq * D)
-        x = x + a @ L.wo.float().t()
+        x = x + a @ dense(L.wo).t()
         h = rmsnorm(x, L.mlp_norm, cfg.rms_eps)
         if hasattr(L, "router"):
             x = x + moe_mlp(model, L, h)
         else:
-            gu = h @ L.w_gate_up.float().t()
+            gu = h @ dense(L.w_gate_up).t()
             if getattr(L, "gu_block", 0):  # gate/up rows interleaved in blocks (ops.swiglu_interleave)
                 gu = gu.view(gu.shape[0], -1, 2, L.gu_block)
                 g, u = gu[:, :, 0].reshape(gu.shape[0], -1), gu[:, :, 1].reshape(gu.shape[0], -1)
             else:
                 g, u = gu.chunk(2, dim=-1)
-            x = x + (F.silu(g) * u) @ L.w_down.float().t()
+            x = x + (F.silu(g) * u) @ dense(L.w_down).t()
     h = rmsnorm(x, model.final_norm, cfg.rms_eps)
     if hidden_only:
         return h
