@@ -26,6 +26,8 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
+int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
+                   int, int, int, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -324,6 +326,31 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
            "gemm8p");
 }
 
+void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& row_off,
+                int64_t max_slots, const c10::optional<at::Tensor>& a_rows, const at::Tensor& a_scale,
+                const at::Tensor& w_scale) {
+  // grouped fp8 GEMM on the 8-phase schedule (gemm8g.hip): A [rows_a, K] e4m3, W [G, N, K] e4m3, C [rows, N] bf16
+  CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_CONTIG(W); CHECK_DTYPE(row_off, at::kInt); CHECK_CONTIG(row_off);
+  TORCH_CHECK(A.scalar_type() == at::kFloat8_e4m3fn && W.scalar_type() == at::kFloat8_e4m3fn, "gemm8g: e4m3 A and W");
+  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1 && W.dim() == 3, "gemm8g: layouts");
+  const int G = (int)W.size(0), N = (int)W.size(1), K = (int)W.size(2);
+  TORCH_CHECK(A.size(1) == K && C.size(1) == N && row_off.numel() == G + 1, "gemm8g: shape mismatch");
+  CHECK_DTYPE(a_scale, at::kFloat); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_CONTIG(w_scale);
+  TORCH_CHECK(a_scale.numel() >= A.size(0) && w_scale.numel() == (int64_t)G * N, "gemm8g: scale shapes");
+  const int* ar = nullptr;
+  if (a_rows.has_value() && a_rows->defined()) {
+    CHECK_DTYPE(*a_rows, at::kInt); CHECK_CONTIG(*a_rows);
+    TORCH_CHECK(a_rows->numel() >= C.size(0), "gemm8g: a_rows shorter than the output rows");
+    ar = a_rows->data_ptr<int>();
+  } else {
+    TORCH_CHECK(C.size(0) <= A.size(0), "gemm8g: more output rows than A rows");
+  }
+  CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), row_off.data_ptr<int>(), ar,
+                          a_scale.data_ptr<float>(), w_scale.data_ptr<float>(), G, (int)max_slots, N, K,
+                          (int)A.stride(0), (int)C.stride(0), (int)A.size(0), cur_stream()),
+           "gemm8g_fp8");
+}
+
 void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Tensor& topk_w, at::Tensor& row_off,
                at::Tensor& src_row, at::Tensor& inv) {
   CHECK_BF16(logits); CHECK_CONTIG(logits);
@@ -536,6 +563,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);
+  m.def("gemm8g_fp8", &gemm8g_fp8);
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_open", &ar_open);
   m.def("ar_close", &ar_close);

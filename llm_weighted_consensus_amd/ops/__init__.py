@@ -12,6 +12,7 @@ Layout conventions shared with the engine:
 from __future__ import annotations
 
 import importlib
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -215,6 +216,12 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
     if rows is None:
         rows = a_rows.numel() if a_rows is not None else A.shape[0]
     G, N, K = W.shape[0], W.shape[1], W.shape[2]
+    if _use_gemm8g(A, W, rows, G, N, K, bias, splits, out):
+        # large fp8 expert batches (>= ~1 full 256-row tile per expert on average): the 8-phase kernel
+        if out is None:
+            out = torch.empty(rows, N, dtype=torch.bfloat16, device=A.device)
+        kernels().gemm8g_fp8(A, W, out, row_off, -(-rows // 256) + G, a_rows, a_scale, w_scale.contiguous())
+        return out
     if max_slots is None:
         max_slots = -(-rows // 128) + G
     if out is None:
@@ -225,6 +232,19 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
         splits = max(1, min(k_tiles // 8, -(-1024 // wgs))) if wgs < 512 else 1
     kernels().grouped_gemm(A, W, out, row_off, int(max_slots), a_scale, w_scale, bias, a_rows, int(splits))
     return out
+
+
+MOE_GEMM = os.environ.get("LWC_MOE_GEMM", "auto")  # auto | g8 (8-phase grouped fp8) | classic (128x128)
+
+
+def _use_gemm8g(A, W, rows, G, N, K, bias, splits, out) -> bool:
+    if MOE_GEMM == "classic" or A.dtype != torch.float8_e4m3fn or bias is not None or (splits or 1) > 1:
+        return False
+    if K % 128 or N % 8 or A.stride(0) % 16 or A.shape[0] * A.stride(0) >= (1 << 31) or 256 * K >= (1 << 31):
+        return False
+    if out is not None and (out.stride(1) != 1 or out.stride(0) % 8):
+        return False
+    return MOE_GEMM == "g8" or rows >= 192 * G
 
 
 def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,

@@ -640,3 +640,41 @@ def test_kv_gather_matches_cache_layout(gpu):
     k_ref = kc.permute(0, 2, 1, 3)[blk, off].reshape(len(slots), -1)
     v_ref = vc.permute(0, 2, 4, 1, 3)[blk, off // 4, off % 4].reshape(len(slots), -1)
     assert torch.equal(k, k_ref) and torch.equal(v, v_ref)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
+    """8-phase grouped fp8 GEMM (csrc/kernels/gemm8g.hip): ragged expert groups (empty, < one tile, several
+    tiles, a partial last tile), optional A-row gather, per-row / per-channel scales, vs an fp32 reference
+    and vs the 128x128 grouped kernel; rows outside every group are never written."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(11)
+    G, N, K = 5, 640, 512
+    sizes = [300, 0, 17, 700, 256]
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    A = torch.randn(rows + 37, K, device=gpu)
+    W = torch.randn(G, N, K, device=gpu) * 0.05
+    a_s = A.abs().amax(1).clamp(min=1e-6) / 448.0
+    w_s = W.abs().amax(2).clamp(min=1e-6) / 448.0
+    Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
+    Wq = (W / w_s[:, :, None]).to(torch.float8_e4m3fn)
+    a_rows = torch.randperm(rows + 37, device=gpu)[:rows].to(torch.int32) if gather else None
+    out = torch.full((rows, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+    ops.kernels().gemm8g_fp8(Aq, Wq, out, off, -(-rows // 256) + G, a_rows, a_s.float().contiguous(),
+                             w_s.float().contiguous())
+    Ar = Aq.float() * a_s[:, None]
+    if gather:
+        Ar = Ar[a_rows.long()]
+    Wr = Wq.float() * w_s[:, :, None]
+    o = off.tolist()
+    for g in range(G):
+        if o[g + 1] > o[g]:
+            _close(out[o[g]:o[g + 1]], Ar[o[g]:o[g + 1]] @ Wr[g].t(), 2e-2, 2e-2)
+    assert not torch.isnan(out).any()
+    # the routed path agrees with the 128x128 kernel on the same operands
+    monkeypatch.setattr(ops, "MOE_GEMM", "classic")
+    classic = ops.grouped_gemm(Aq, Wq, off, a_scale=a_s.float().contiguous(), w_scale=w_s.float().contiguous(),
+                               a_rows=a_rows, rows=rows, splits=1, max_slots=-(-rows // 128) + G)
+    _close(out, classic, 2e-2, 2e-2)
