@@ -675,6 +675,7 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     assert not torch.isnan(out).any()
     # the routed path agrees with the 128x128 kernel on the same operands
     monkeypatch.setattr(ops, "MOE_GEMM", "classic")
-    classic = ops.grouped_gemm(Aq, Wq, off, a_scale=a_s.float().contiguous(), w_scale=w_s.float().contiguous(),
+    Ac, sc = (Aq, a_s) if gather else (Aq[:rows], a_s[:rows])
+    classic = ops.grouped_gemm(Ac, Wq, off, a_scale=sc.float().contiguous(), w_scale=w_s.float().contiguous(),
                                a_rows=a_rows, rows=rows, splits=1, max_slots=-(-rows // 128) + G)
     _close(out, classic, 2e-2, 2e-2)
