@@ -244,7 +244,7 @@ def _use_gemm8g(A, W, rows, G, N, K, bias, splits, out) -> bool:
         return False
     if out is not None and (out.stride(1) != 1 or out.stride(0) % 8):
         return False
-    return MOE_GEMM == "g8" or rows >= 64 * G
+    return MOE_GEMM == "g8" or rows >= 32 * G
 
 
 def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
