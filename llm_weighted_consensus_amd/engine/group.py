@@ -3,8 +3,9 @@ worker/GPU), candidate router"; §5 "worker heartbeat; on GPU/worker failure, dr
 sequences to surviving GPUs").
 
 * Each worker is a spawned process that owns one GPU and one `LLMEngine` (built from a JSON-able model
-  spec by ``worker_factory``), reads requests from its own queue and sends token events back on a
-  shared queue, batched per engine step.  It stamps a shared heartbeat every loop.
+  spec by ``worker_factory``), reads requests from its own queue and sends each engine step's token
+  events back as ONE binary record through its shared-memory ring (`shm_ring.py`; no pickling).  It
+  stamps a shared heartbeat every loop; control messages (ready / fatal / error) use a queue.
 * The front end exposes the `EngineService` API (`submit / abort / close / load`, plus an
   ``engine`` facade with tokenizer / cfg / max_model_len), so `LocalChatClient` serves a whole node
   through it unchanged.
@@ -32,6 +33,7 @@ from typing import Any, Dict, List, Optional
 
 from .sampling import SamplingParams
 from .service import EngineFailure
+from .shm_ring import ShmRing, decode_events, encode_events
 
 
 @dataclass
@@ -75,8 +77,9 @@ def _resolve(path: str):
     return getattr(importlib.import_module(mod), fn)
 
 
-def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop) -> None:
+def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None) -> None:
     """Worker process: build the engine, serve requests until told to stop."""
+    ring = ShmRing(ring_name, create=False) if ring_name else None
     try:
         engine = _resolve(factory)(spec, wid)
     except BaseException as e:  # report and die: the front end marks the worker dead
@@ -123,7 +126,8 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop) -> No
                     if rid is not None:
                         ev_q.put(("error", wid, (rid, f"{type(e).__name__}: {e}")))
         if batch:
-            ev_q.put(("tokens", wid, batch))
+            if ring is None or not ring.push(encode_events(batch)):
+                ev_q.put(("tokens", wid, batch))  # no ring (or the reader is gone): the slow path
             batch = []
         for rid in [r for r, g in groups.items() if g.finished]:
             groups.pop(rid)
@@ -138,17 +142,20 @@ class _EngineFacade:
 class EngineGroup:
     def __init__(self, spec: dict, devices: List[int], factory: str = "llm_weighted_consensus_amd.engine.group:build_engine",
                  tokenizer=None, cfg=None, max_model_len: int = 4096, heartbeat_timeout: float = 30.0,
-                 start_timeout: float = 600.0):
+                 start_timeout: float = 600.0, ring_bytes: int = 32 << 20):
         self.spec, self.devices, self.factory = spec, list(devices), factory
         self.heartbeat_timeout = heartbeat_timeout
         ctx = mp.get_context("spawn")
         self.ev_q = ctx.Queue()
         self.stop = ctx.Event()
-        self.req_qs, self.hbs, self.procs = [], [], []
+        self.req_qs, self.hbs, self.procs, self.rings = [], [], [], []
         for wid, dev in enumerate(self.devices):
             q = ctx.Queue()
             hb = ctx.Value("d", time.time())
-            p = ctx.Process(target=worker_main, args=(wid, dict(spec, device=dev), factory, q, self.ev_q, hb, self.stop),
+            ring = ShmRing(cap=ring_bytes)
+            self.rings.append(ring)
+            p = ctx.Process(target=worker_main, args=(wid, dict(spec, device=dev), factory, q, self.ev_q, hb, self.stop,
+                                                      ring.name),
                             daemon=True, name=f"lwc-worker-{wid}")
             p.start()
             self.req_qs.append(q)
@@ -219,17 +226,34 @@ class EngineGroup:
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
+        self._reader.join(timeout=5)
+        for r in self.rings:
+            r.close()
+        self.rings = []
 
     # ------------------------------------------------------------------ reader / health
     def _deliver(self, req: GroupRequest, item) -> None:
         req.loop.call_soon_threadsafe(req.queue.put_nowait, item)
 
     def _read(self) -> None:
+        last_health = time.monotonic()
         while not self.stop.is_set():
+            busy = False
+            for wid, ring in enumerate(self.rings):
+                while True:
+                    rec = ring.pop()
+                    if rec is None:
+                        break
+                    busy = True
+                    self._on_tokens(wid, decode_events(rec))
             try:
-                kind, wid, payload = self.ev_q.get(timeout=0.5)
+                kind, wid, payload = self.ev_q.get_nowait()
             except pyqueue.Empty:
-                self._check_health()
+                if not busy:
+                    time.sleep(0.0003)
+                if time.monotonic() - last_health > 0.5:
+                    last_health = time.monotonic()
+                    self._check_health()
                 continue
             except (EOFError, OSError):
                 return
@@ -246,22 +270,24 @@ class EngineGroup:
                     self.failures += 1
                     self._deliver(req, EngineFailure(msg))
             elif kind == "tokens":
-                with self._lock:
-                    for (rid, idx, tid, text, lp, top, fin, reason) in payload:
-                        req = self.requests.get(rid)
-                        if req is None:
-                            continue
-                        p = next((p for p in req.portions if p.worker == wid and p.offset <= idx < p.offset + p.n),
-                                 None)
-                        if p is not None:
-                            p.emitted += 1
-                            if fin:
-                                p.finished += 1
-                                self.load_of[wid] -= 1
-                        self._deliver(req, GroupTokenEvent(idx, tid, text, lp, top, fin, reason))
-                        if all(pp.finished == pp.n for pp in req.portions):
-                            self.requests.pop(rid, None)
+                self._on_tokens(wid, payload)
             self._check_health()
+
+    def _on_tokens(self, wid: int, payload) -> None:
+        with self._lock:
+            for (rid, idx, tid, text, lp, top, fin, reason) in payload:
+                req = self.requests.get(rid)
+                if req is None:
+                    continue
+                p = next((p for p in req.portions if p.worker == wid and p.offset <= idx < p.offset + p.n), None)
+                if p is not None:
+                    p.emitted += 1
+                    if fin:
+                        p.finished += 1
+                        self.load_of[wid] -= 1
+                self._deliver(req, GroupTokenEvent(idx, tid, text, lp, top, fin, reason))
+                if all(pp.finished == pp.n for pp in req.portions):
+                    self.requests.pop(rid, None)
 
     def _check_health(self) -> None:
         now = time.time()

@@ -8,8 +8,8 @@ variables configure the local engine:
                           "max_model_len": 4096, "max_batch": 512}}   (default: none)
   LWC_EMBED_MODELS  JSON {name: {"arch": "bge-large-en-v1.5", "weights": "random:<seed>" | <path>}}
   LWC_GPU           device index for this process's engine (one process per GPU)
-  LWC_GPUS          comma list of devices: >1 entries serve each model through an EngineGroup (one
-                    worker process per GPU, candidates of a request split across them, failover)
+  LWC_GPUS          comma list of devices: serve each model through an EngineGroup (one worker process
+                    per listed GPU, candidates of a request split across them, failover; "0" = one worker)
   LWC_DEVICE        "cuda" (default) or "cpu": CPU runs embedding models only, on the fp32 reference
                     path (BASELINE config 1: canned completions + bge-small cosine consensus, no GPU)
   LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)

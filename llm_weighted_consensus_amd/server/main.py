@@ -66,7 +66,7 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         for name, spec in cfg.models.items():
             dcfg = decoder_config(spec["arch"])
             mlen = int(spec.get("max_model_len", 4096))
-            if len(cfg.gpus) > 1:  # one worker process per GPU behind one front end
+            if cfg.gpus:  # one worker process per listed GPU behind one front end (LWC_GPUS=0: a single worker)
                 from ..engine.group import EngineGroup
 
                 wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),

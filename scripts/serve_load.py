@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--choices", type=int, default=4)
     ap.add_argument("--max-batch", type=int, default=1024)
     ap.add_argument("--profile", action="store_true", help="cProfile the engine thread and the event loop")
+    ap.add_argument("--gpus", default=os.environ.get("LWC_GPUS", ""),
+                    help="comma list: serve through an EngineGroup of worker processes (e.g. '0' = one worker)")
     a = ap.parse_args()
     profs = {}
     if a.profile:
@@ -56,7 +58,8 @@ def main():
 
     models = {"local": {"arch": a.arch, "weights": "random:1", "max_model_len": 2048, "max_batch": a.max_batch}}
     t0 = time.time()
-    state = build_state(Config(models=models, kv_fraction=0.6,
+    gpus = [int(x) for x in a.gpus.split(",") if x.strip()]
+    state = build_state(Config(models=models, kv_fraction=0.6, gpus=gpus,
                                chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "0"))))
     print(f"# model ready in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     app = create_app(state)
@@ -89,7 +92,8 @@ def main():
     asyncio.run(run(min(a.concurrency, a.requests)))  # warmup: graphs, GEMM plans
     lat.clear()
     eng = state.services["local"].engine
-    p0, c0 = eng.stats["prefill_tokens"], eng.stats["prefix_cache_tokens"]
+    stats = getattr(eng, "stats", None) or {"prefill_tokens": 0, "prefix_cache_tokens": 0, "steps": 0}
+    p0, c0 = stats["prefill_tokens"], stats["prefix_cache_tokens"]
     if a.profile:
         import cProfile
 
@@ -105,14 +109,15 @@ def main():
     out = {"metric": "score requests/s through the HTTP app (local voters)", "value": round(a.requests / el, 3),
            "voter_completions_per_s": round(a.requests * a.voters / el, 2), "errors": errs,
            "latency_s": {"p50": round(pct(0.5), 3), "p90": round(pct(0.9), 3), "p99": round(pct(0.99), 3)},
-           "prefill_tokens": eng.stats["prefill_tokens"] - p0,
-           "prefix_cache_tokens": eng.stats["prefix_cache_tokens"] - c0,
+           "prefill_tokens": stats["prefill_tokens"] - p0,
+           "prefix_cache_tokens": stats["prefix_cache_tokens"] - c0,
+           "serving": f"EngineGroup workers on GPUs {gpus}" if gpus else "in-process engine",
            "config": {"arch": a.arch, "concurrency": a.concurrency, "requests": a.requests, "voters": a.voters,
                       "choices": a.choices, "output_mode": "json_schema", "data": "synthetic prompts, random-init"}}
     from llm_weighted_consensus_amd.utils.tracing import STATS
 
     out["phases"] = {k: [v[0], round(v[1], 3)] for k, v in STATS.snapshot()["phases"].items()}
-    out["engine_steps"] = eng.stats["steps"]
+    out["engine_steps"] = stats["steps"]
     print(json.dumps(out), flush=True)
     for svc in state.services.values():
         svc.close()
