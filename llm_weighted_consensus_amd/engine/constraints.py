@@ -268,6 +268,21 @@ class TokenConstraint:
         self.vocab = vocab
         self.eos_id = fsm.eos_id
 
+    def __getstate__(self):
+        # shipped to an EngineGroup worker with the request: the grammar only — the worker re-binds the
+        # vocabulary index of ITS tokenizer (bind), which also keeps its cross-request mask cache warm
+        return {"fsm": self.fsm, "eos_id": self.eos_id, "vocab_size": self.vocab.vocab_size if self.vocab else None}
+
+    def __setstate__(self, st):
+        self.fsm, self.eos_id, self.vocab = st["fsm"], st["eos_id"], None
+        self._vocab_size = st["vocab_size"]
+
+    def bind(self, tok, vocab_size: int) -> "TokenConstraint":
+        """Attach the vocabulary index of ``tok`` (after unpickling in another process)."""
+        if self.vocab is None:
+            self.vocab = TokenVocab.of(tok, vocab_size)
+        return self
+
     def start(self):
         return self.fsm.start()
 

@@ -315,6 +315,8 @@ class LLMEngine:
         """Queue a request of `n` sequences.  ``prefilled`` = (kv [L, 2, nblocks, block_elems],
         logits [V]) starts it from a prompt prefilled elsewhere (see :meth:`export_prefill`)."""
         params.validate(self.cfg.vocab_size)
+        if params.constraint is not None and hasattr(params.constraint, "bind"):
+            params.constraint.bind(self.tokenizer, self.cfg.vocab_size)  # a constraint that came through a pipe
         if len(prompt_ids) == 0:
             raise ValueError("empty prompt")
         if len(prompt_ids) + params.max_tokens > self.max_model_len:

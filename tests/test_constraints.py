@@ -151,3 +151,20 @@ def test_masks_shared_across_voters_with_equal_remaining_grammar(tmp_path):
     ta = a.advance_bytes(sa, b'{"response_key":"`A`"')
     tc = c.advance_bytes(sc, b'{"response_key":"`C`"')
     assert a._key(ta) == c._key(tc) and np.array_equal(a.allowed_tokens(ta)[0], c.allowed_tokens(tc)[0])
+
+
+def test_constraint_pickles_without_the_vocabulary(tmp_path):
+    """EngineGroup ships SamplingParams to worker processes: the constraint travels as its grammar only
+    and re-binds the worker's vocabulary index (and its warm mask cache)."""
+    import pickle
+
+    tok, V = _tokenizers(tmp_path)["bytelevel"]
+    c = constraint_for_schema(_schema(False), tok, V)
+    blob = pickle.dumps(c)
+    assert len(blob) < 4096
+    c2 = pickle.loads(blob)
+    assert c2.vocab is None
+    c2.bind(tok, V)
+    assert c2.vocab is TokenVocab.of(tok, V)
+    st = c.start()
+    assert c2.mask_entry(st) is c.mask_entry(st)
