@@ -72,6 +72,11 @@ class GroupRequest:
     failed: bool = False
 
 
+def _put_all(batch) -> None:
+    for q, ev in batch:
+        q.put_nowait(ev)
+
+
 def _resolve(path: str):
     mod, _, fn = path.partition(":")
     return getattr(importlib.import_module(mod), fn)
@@ -274,6 +279,8 @@ class EngineGroup:
             self._check_health()
 
     def _on_tokens(self, wid: int, payload) -> None:
+        # one thread-safe hand-off per client event loop per record (not one self-pipe wake-up per token)
+        per_loop: Dict[Any, list] = {}
         with self._lock:
             for (rid, idx, tid, text, lp, top, fin, reason) in payload:
                 req = self.requests.get(rid)
@@ -285,9 +292,15 @@ class EngineGroup:
                     if fin:
                         p.finished += 1
                         self.load_of[wid] -= 1
-                self._deliver(req, GroupTokenEvent(idx, tid, text, lp, top, fin, reason))
+                per_loop.setdefault(req.loop, []).append((req.queue, GroupTokenEvent(idx, tid, text, lp, top, fin,
+                                                                                     reason)))
                 if all(pp.finished == pp.n for pp in req.portions):
                     self.requests.pop(rid, None)
+        for loop, batch in per_loop.items():
+            try:
+                loop.call_soon_threadsafe(_put_all, batch)
+            except RuntimeError:  # the client's loop is gone
+                pass
 
     def _check_health(self) -> None:
         now = time.time()
