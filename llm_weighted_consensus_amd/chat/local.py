@@ -168,7 +168,7 @@ class LocalChatClient(ChatClient):
         last_err: Optional[ChatError] = None
         for name in names:
             try:
-                stream = self._start(self.services[name], name, request)
+                stream, _group = self._start(self.services[name], name, request)
             except ChatError as e:
                 last_err = e
                 continue
@@ -200,8 +200,9 @@ class LocalChatClient(ChatClient):
         finally:
             await stream.aclose()
 
-    def _start(self, svc: EngineService, name: str, request: C.ChatCompletionCreateParams):
-        """Validate, render and submit one attempt; returns its (not yet started) chunk generator."""
+    def _start(self, svc: EngineService, name: str, request: C.ChatCompletionCreateParams, embed: Optional[str] = None):
+        """Validate, render and submit one attempt; returns (its not yet started chunk generator, the
+        engine group).  ``embed``: the EngineGroup workers also embed the finished candidates."""
         tok = svc.engine.tokenizer
         template = getattr(svc, "chat_template", None) or template_for(svc.engine.cfg.name)
         prompt = render_chat_prompt(request.messages, request.tools, template)
@@ -220,12 +221,65 @@ class LocalChatClient(ChatClient):
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         try:
-            group = svc.submit(ids, sp, n, loop, q)
+            group = svc.submit(ids, sp, n, loop, q, **({"embed": embed} if embed else {}))
         except ValueError as e:
             raise ChatError.invalid_request(str(e))
         cid = f"chatcmpl-{uuid.uuid4().hex}"
         created = int(time.time())
-        return self._stream(svc, group, q, cid, created, name, len(ids), n, sp, tool_name, include_usage, tok)
+        return self._stream(svc, group, q, cid, created, name, len(ids), n, sp, tool_name, include_usage, tok), group
+
+    # ---- candidates embedded where they were generated (EngineGroup workers)
+    def _embedding_service_for(self, request: C.ChatCompletionCreateParams, embedding_model: str) -> Optional[str]:
+        for name in self._attempts(request):
+            f = getattr(self.services[name], "embeds_in_workers", None)
+            if f is not None and f(embedding_model):
+                return name
+        return None
+
+    def can_embed_in_workers(self, request: C.ChatCompletionCreateParams, embedding_model: str) -> bool:
+        return self._embedding_service_for(request, embedding_model) is not None
+
+    async def create_unary_embedded(self, ctx: Any, request: C.ChatCompletionCreateParams, embedding_model: str):
+        """n candidates from the first locally served model whose workers host ``embedding_model``: each
+        worker embeds the candidates it generated on its own GPU.  Returns (ChatCompletion, unit rows
+        [n, d] float32 numpy in choice order, embedding tokens)."""
+        name = self._embedding_service_for(request, embedding_model)
+        if name is None:
+            raise ChatError.invalid_request(f"no local model embeds with {embedding_model}")
+        if self.archive is not None:
+            from ..archive.resolve import fetch_completions_from_messages, replace_completion_messages
+
+            comps = await fetch_completions_from_messages(self.archive, ctx, request.messages)
+            request = request.model_copy()
+            request.messages = list(request.messages)
+            replace_completion_messages(comps, request.messages)
+        stream, group = self._start(self.services[name], name, request, embed=embedding_model)
+        agg = None
+        async for chunk in self._timed_first(stream):
+            if agg is None:
+                agg = chunk.clone()
+            else:
+                agg.push(chunk)
+        if agg is None:
+            raise ChatError.empty_stream()
+        try:
+            rows, ntok = await asyncio.wait_for(group.emb_future, self.other_chunk_timeout)
+        except asyncio.TimeoutError:
+            raise ChatError.stream_timeout()
+        except RuntimeError as e:
+            raise ChatError.engine(str(e))
+        return C.ChatCompletion.from_chunk(agg), rows, ntok
+
+    async def _timed_first(self, stream):
+        try:
+            first = await asyncio.wait_for(stream.__anext__(), self.first_chunk_timeout)
+        except StopAsyncIteration:
+            return
+        except asyncio.TimeoutError:
+            await stream.aclose()
+            raise ChatError.stream_timeout()
+        async for c in self._timed(first, stream):
+            yield c
 
     async def _stream(self, svc, group, q, cid, created, model, prompt_len, n, sp, tool_name, include_usage, tok):
         started = [False] * n

@@ -78,3 +78,34 @@ class EmbeddingService:
         rows = f32.double().cpu().tolist()
         return S.CreateEmbeddingResponse(data=[S.EmbeddingItem(embedding=r, index=i) for i, r in enumerate(rows)],
                                          model=self.name, usage=C.Usage(prompt_tokens=ntok, total_tokens=ntok))
+
+
+def build_embedding_service(name: str, spec: dict, dev) -> "EmbeddingService":
+    """An embedding model from a server spec ({"arch", "weights": "random:<seed>" | path, "tokenizer",
+    "max_tokens", "fp8"}) on ``dev``: BERT/BGE encoders, or a decoder arch as a last-token-pooling embedder
+    (e5-mistral).  Used by the server front end and by EngineGroup workers (candidates embedded on the
+    GPU that generated them)."""
+    import torch
+
+    from ..engine.tokenizer import HFTokenizer
+    from ..models.bert import BertEncoder
+    from ..models.config import DECODERS, decoder_config, encoder_config
+
+    w = spec.get("weights", "random:0")
+    path, seed = (None, int(w.split(":", 1)[1])) if str(w).startswith("random:") else (w, 0)
+    dev = torch.device(dev)
+    if spec["arch"] in DECODERS:  # decoder-as-embedder (e5-mistral): last-token pooling
+        if dev.type == "cpu":
+            raise ValueError(f"embedding model {name}: decoder embedders need an MI355X")
+        from ..models.embedder import DecoderEmbedder
+        from ..models.llama import LlamaModel
+
+        dcfg = decoder_config(spec["arch"])
+        mtok = int(spec.get("max_tokens", 4096))
+        enc = DecoderEmbedder(LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mtok + 64,
+                                         fp8_dense=bool(spec.get("fp8", False))), max_tokens=mtok)
+    else:
+        enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
+                          dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
+    tok = HFTokenizer(spec["tokenizer"]) if spec.get("tokenizer") else None
+    return EmbeddingService(enc, name, tokenizer=tok)

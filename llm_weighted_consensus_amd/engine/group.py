@@ -70,6 +70,18 @@ class GroupRequest:
     queue: Any
     portions: List[_Portion] = field(default_factory=list)
     failed: bool = False
+    embed: Optional[str] = None           # embedding model the workers run on their finished candidates
+    emb_parts: Dict[int, Any] = field(default_factory=dict)  # portion offset -> (unit rows [n, d], tokens)
+    emb_future: Any = None                # resolves to (rows [n, d] float32 in candidate order, tokens)
+
+
+def _set_future(fut, result, exc) -> None:
+    if fut.done():
+        return
+    if exc is not None:
+        fut.set_exception(exc)
+    else:
+        fut.set_result(result)
 
 
 def _put_all(batch) -> None:
@@ -85,6 +97,8 @@ def _resolve(path: str):
 def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None) -> None:
     """Worker process: build the engine, serve requests until told to stop."""
     ring = ShmRing(ring_name, create=False) if ring_name else None
+    embedders: Dict[str, Any] = {}
+    emb_req: Dict[int, tuple] = {}  # rid -> (model name, offset, streamed texts)
     try:
         engine = _resolve(factory)(spec, wid)
     except BaseException as e:  # report and die: the front end marks the worker dead
@@ -103,11 +117,17 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
         while msg is not None:
             kind = msg[0]
             if kind == "submit":
-                _, rid, prompt, params, n, offset = msg
+                _, rid, prompt, params, n, offset = msg[:6]
+                embed = msg[6] if len(msg) > 6 else None
+                texts = [""] * n if embed else None
+                if embed:
+                    emb_req[rid] = (embed, offset, texts)
 
-                def cb(ev, rid=rid, offset=offset):
+                def cb(ev, rid=rid, offset=offset, texts=texts):
                     batch.append((rid, ev.seq.index + offset, ev.token_id, ev.text, ev.logprob,
                                   list(ev.top_logprobs), ev.finished, ev.finish_reason))
+                    if texts is not None:
+                        texts[ev.seq.index] += ev.text
 
                 try:
                     groups[rid] = engine.add_request(prompt, params, n=n, callback=cb)
@@ -136,6 +156,19 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
             batch = []
         for rid in [r for r, g in groups.items() if g.finished]:
             groups.pop(rid)
+            if rid in emb_req:  # embed this worker's candidates on its own GPU; only the unit rows travel
+                name, offset, texts = emb_req.pop(rid)
+                try:
+                    svc = embedders.get(name)
+                    if svc is None:
+                        from ..embeddings.service import build_embedding_service
+
+                        dev = spec.get("embed_device") or f"cuda:{int(spec.get('device', 0))}"
+                        svc = embedders[name] = build_embedding_service(name, spec["embed_models"][name], dev)
+                    E, ntok = svc.embed_texts(texts)
+                    ev_q.put(("emb", wid, (rid, offset, E.float().cpu().numpy(), int(ntok))))
+                except Exception as e:  # noqa: BLE001 - reported to the request, the worker keeps serving
+                    ev_q.put(("emb_err", wid, (rid, f"{type(e).__name__}: {e}")))
 
 
 class _EngineFacade:
@@ -170,6 +203,7 @@ class EngineGroup:
         self.ready = [False] * len(self.procs)
         self.load_of = [0] * len(self.procs)
         self.requests: Dict[int, GroupRequest] = {}
+        self.emb_pending: Dict[int, GroupRequest] = {}  # finished generating, embeddings still on the way
         self._rid = itertools.count(1)
         self._lock = threading.Lock()
         self.failures = 0
@@ -193,13 +227,22 @@ class EngineGroup:
     def live_workers(self) -> List[int]:
         return [i for i, a in enumerate(self.alive) if a and self.ready[i]]
 
-    def submit(self, prompt_ids, params: SamplingParams, n: int, loop, queue) -> GroupRequest:
+    def embeds_in_workers(self, model: str) -> bool:
+        return model in (self.spec.get("embed_models") or {})
+
+    def submit(self, prompt_ids, params: SamplingParams, n: int, loop, queue, embed: Optional[str] = None) -> GroupRequest:
+        """``embed``: an embedding model every worker embeds its finished candidates with; the rows arrive
+        in ``req.emb_future`` (a future of ``loop``)."""
         self._check_health()
         live = self.live_workers()
         if not live:
             raise ValueError("no live engine workers")
+        if embed is not None and not self.embeds_in_workers(embed):
+            raise ValueError(f"embedding model {embed} is not hosted by the workers")
         rid = next(self._rid)
-        req = GroupRequest(rid, list(prompt_ids), loop, queue)
+        req = GroupRequest(rid, list(prompt_ids), loop, queue, embed=embed)
+        if embed is not None:
+            req.emb_future = loop.create_future()
         # candidate i of the request keeps seed base*1000003+i however the n candidates are split
         base = params.seed if params.seed is not None else random.getrandbits(63)
         order = sorted(live, key=lambda w: self.load_of[w])
@@ -213,7 +256,7 @@ class EngineGroup:
                 p = _Portion(w, offset, m, replace(params, seed=base, seed_offset=offset))
                 req.portions.append(p)
                 self.load_of[w] += m
-                self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset))
+                self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset, embed))
                 offset += m
         return req
 
@@ -276,7 +319,30 @@ class EngineGroup:
                     self._deliver(req, EngineFailure(msg))
             elif kind == "tokens":
                 self._on_tokens(wid, payload)
+            elif kind in ("emb", "emb_err"):
+                self._on_embeddings(kind, payload)
             self._check_health()
+
+    def _on_embeddings(self, kind: str, payload) -> None:
+        import numpy as np
+
+        rid = payload[0]
+        with self._lock:
+            req = self.emb_pending.get(rid) or self.requests.get(rid)
+            if req is None or req.emb_future is None:
+                return
+            if kind == "emb_err":
+                self.emb_pending.pop(rid, None)
+                req.loop.call_soon_threadsafe(_set_future, req.emb_future, None, RuntimeError(payload[1]))
+                return
+            _, offset, rows, ntok = payload
+            req.emb_parts[offset] = (rows, ntok)
+            if len(req.emb_parts) < len(req.portions):
+                return
+            self.emb_pending.pop(rid, None)
+        parts = [req.emb_parts[o] for o in sorted(req.emb_parts)]
+        out = (np.concatenate([r for r, _ in parts]), sum(t for _, t in parts))
+        req.loop.call_soon_threadsafe(_set_future, req.emb_future, out, None)
 
     def _on_tokens(self, wid: int, payload) -> None:
         # one thread-safe hand-off per client event loop per record (not one self-pipe wake-up per token)
@@ -296,6 +362,8 @@ class EngineGroup:
                                                                                      reason)))
                 if all(pp.finished == pp.n for pp in req.portions):
                     self.requests.pop(rid, None)
+                    if req.embed is not None and len(req.emb_parts) < len(req.portions):
+                        self.emb_pending[rid] = req
         for loop, batch in per_loop.items():
             try:
                 loop.call_soon_threadsafe(_put_all, batch)
@@ -317,6 +385,11 @@ class EngineGroup:
         self.load_of[w] = 0
         live = self.live_workers()
         with self._lock:
+            for rid, req in list(self.emb_pending.items()):  # generated, but this worker's rows never came
+                if any(p.worker == w and p.offset not in req.emb_parts for p in req.portions):
+                    self.emb_pending.pop(rid, None)
+                    req.loop.call_soon_threadsafe(_set_future, req.emb_future, None,
+                                                  RuntimeError(f"engine worker {w} {why}"))
             for rid, req in list(self.requests.items()):
                 for p in [p for p in req.portions if p.worker == w and p.finished < p.n]:
                     if p.emitted == 0 and live:
@@ -324,10 +397,13 @@ class EngineGroup:
                         t = min(live, key=lambda x: self.load_of[x])
                         p.worker = t
                         self.load_of[t] += p.n
-                        self.req_qs[t].put(("submit", rid, req.prompt_ids, p.params, p.n, p.offset))
+                        self.req_qs[t].put(("submit", rid, req.prompt_ids, p.params, p.n, p.offset, req.embed))
                     else:
                         self.requests.pop(rid, None)
                         self._deliver(req, EngineFailure(f"engine worker {w} {why}"))
+                        if req.emb_future is not None:
+                            req.loop.call_soon_threadsafe(_set_future, req.emb_future, None,
+                                                          RuntimeError(f"engine worker {w} {why}"))
                         break
 
 

@@ -127,10 +127,17 @@ class ConsensusClient:
         n = int(request.n or 1)
         if n < 2:
             raise ScoreError.expected_two_or_more_choices(n)
-        comp = await self.chat.create_unary(ctx, request)
-        texts = [c.message.content or "" for c in comp.choices]
-        loop = asyncio.get_running_loop()
-        E, ntok = await loop.run_in_executor(None, emb.embed_texts, texts)
+        local = getattr(self.chat, "local", self.chat)
+        if hasattr(local, "can_embed_in_workers") and local.can_embed_in_workers(request, embedding_model):
+            # multi-GPU: every EngineGroup worker embeds the candidates it generated on its own GPU;
+            # only the unit rows come back (no candidate text is re-encoded on the front end's GPU)
+            comp, rows, ntok = await local.create_unary_embedded(ctx, request, embedding_model)
+            E = torch.from_numpy(rows).to(emb.encoder.device)
+        else:
+            comp = await self.chat.create_unary(ctx, request)
+            texts = [c.message.content or "" for c in comp.choices]
+            loop = asyncio.get_running_loop()
+            E, ntok = await loop.run_in_executor(None, emb.embed_texts, texts)
         Eb = E.to(torch.bfloat16).unsqueeze(0).contiguous()
         if Eb.is_cuda:
             _, cen, w, best = ops.cosine_consensus(Eb, tau)

@@ -18,13 +18,6 @@ from .app import AppState, create_app
 from .config import Config
 
 
-def _weights_spec(spec: dict):
-    w = spec.get("weights", "random:0")
-    if isinstance(w, str) and w.startswith("random:"):
-        return None, int(w.split(":", 1)[1])
-    return w, 0
-
-
 def build_state(cfg: Config, chat_client=None) -> AppState:
     archive = CompletionsArchive(path=cfg.archive_path)
     registry = ModelRegistry(cfg.registry_path)
@@ -32,11 +25,10 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if cfg.models or cfg.embed_models:
         import torch
 
+        from ..embeddings.service import build_embedding_service
         from ..engine.service import EngineService
-        from ..engine.tokenizer import HFTokenizer, load_tokenizer
-        from ..embeddings.service import EmbeddingService
-        from ..models.bert import BertEncoder
-        from ..models.config import DECODERS, decoder_config, encoder_config
+        from ..engine.tokenizer import load_tokenizer
+        from ..models.config import decoder_config
 
         if cfg.device == "cpu":
             if cfg.models:
@@ -46,32 +38,18 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
             dev = torch.device("cuda", cfg.gpu)
             torch.cuda.set_device(dev)
         for name, spec in cfg.embed_models.items():
-            path, seed = _weights_spec(spec)
-            if spec["arch"] in DECODERS:  # decoder-as-embedder (e5-mistral): last-token pooling
-                if dev.type == "cpu":
-                    raise ValueError(f"embedding model {name}: decoder embedders need an MI355X")
-                from ..models.embedder import DecoderEmbedder
-                from ..models.llama import LlamaModel
-
-                dcfg = decoder_config(spec["arch"])
-                mtok = int(spec.get("max_tokens", 4096))
-                enc = DecoderEmbedder(LlamaModel(dcfg, device=dev, seed=seed, weights_path=path,
-                                                 max_position=mtok + 64, fp8_dense=bool(spec.get("fp8", False))),
-                                      max_tokens=mtok)
-            else:
-                enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
-                                  dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)
-            tok = HFTokenizer(spec["tokenizer"]) if spec.get("tokenizer") else None
-            embedders[name] = EmbeddingService(enc, name, tokenizer=tok)
+            embedders[name] = build_embedding_service(name, spec, dev)
         for name, spec in cfg.models.items():
             dcfg = decoder_config(spec["arch"])
             mlen = int(spec.get("max_model_len", 4096))
             if cfg.gpus:  # one worker process per listed GPU behind one front end (LWC_GPUS=0: a single worker)
                 from ..engine.group import EngineGroup
 
+                # the workers also host the embedding models: /consensus candidates are embedded on the GPU
+                # that generated them, only the unit rows travel to the front end
                 wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
                              prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs,
-                             chunked_prefill=cfg.chunked_prefill)
+                             chunked_prefill=cfg.chunked_prefill, embed_models=dict(cfg.embed_models))
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
                                                                       dcfg.eos_token_id))

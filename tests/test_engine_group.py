@@ -79,3 +79,38 @@ def test_group_worker_death_reschedules_or_fails():
         assert err is None and len(toks) == 3
     finally:
         g.close()
+
+
+def test_workers_embed_their_own_candidates():
+    """/consensus over an EngineGroup: each worker embeds the candidates it generated (here a CPU BERT in
+    each fake-engine worker); the front end receives unit rows in candidate order equal to embedding the
+    streamed texts locally."""
+    import torch
+
+    from llm_weighted_consensus_amd.embeddings.service import build_embedding_service
+
+    espec = {"arch": "bert-tiny", "weights": "random:1"}
+    g = EngineGroup({"delay": 0.0, "embed_models": {"e": espec}, "embed_device": "cpu"}, devices=[0, 0],
+                    factory=FACTORY)
+    try:
+        assert g.embeds_in_workers("e") and not g.embeds_in_workers("other")
+
+        async def go():
+            loop = asyncio.get_running_loop()
+            q = asyncio.Queue()
+            req = g.submit([1, 2, 3], SamplingParams(max_tokens=6, seed=9), 5, loop, q, embed="e")
+            texts, done = {i: "" for i in range(5)}, 0
+            while done < 5:
+                ev = await asyncio.wait_for(q.get(), 120)
+                texts[ev.seq.index] += ev.text
+                done += ev.finished
+            rows, ntok = await asyncio.wait_for(req.emb_future, 120)
+            return texts, rows, ntok
+
+        texts, rows, ntok = asyncio.run(go())
+        assert rows.shape[0] == 5 and ntok > 0
+        ref, _ = build_embedding_service("e", espec, "cpu").embed_texts([texts[i] for i in range(5)])
+        assert torch.allclose(torch.from_numpy(rows), ref.float(), atol=1e-5)
+        assert not g.emb_pending
+    finally:
+        g.close()

@@ -107,7 +107,7 @@ def test_engine_group_two_workers_serve_chat(gpu, monkeypatch):
 
     monkeypatch.delenv("LWC_FAULT", raising=False)
     monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    state = build_state(Config(models=MODELS, gpus=[0, 0], kv_fraction=0.04))
+    state = build_state(Config(models=MODELS, embed_models=EMBED, gpus=[0, 0], kv_fraction=0.04))
     c = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t", timeout=300)
     svc = state.services["tiny"]
 
@@ -119,6 +119,14 @@ def test_engine_group_two_workers_serve_chat(gpu, monkeypatch):
         assert sorted(x["index"] for x in ch) == list(range(6))
         r = await c.get("/metrics")
         assert 'lwc_engine_workers_alive{model="tiny"} 2' in r.text
+        # /consensus: both workers embed the candidates they generated; rows come back to the front end
+        assert svc.embeds_in_workers("bge-small")
+        r = await c.post("/consensus/completions", json={"model": "tiny", "n": 6, "max_tokens": 8, "seed": 5,
+                                                         "messages": [{"role": "user", "content": "say hi"}],
+                                                         "embedding_model": "bge-small"})
+        assert r.status_code == 200, r.text
+        ch = r.json()["choices"]
+        assert len(ch) == 6 and sum(x["confidence"] for x in ch) == pytest.approx(1.0, abs=1e-5)
 
     try:
         assert len(svc.live_workers()) == 2
