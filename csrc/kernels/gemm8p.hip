@@ -83,7 +83,15 @@ LWC_DEVICE float4v mfma(const uint4v& a, const uint4v& b, const float4v& c) {
 }
 
 LWC_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
-LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| < 1.5e-7, far below bf16's resolution): one exp, one rcp and a
+// 5-term polynomial — the libm erff's branches made the fused epilogue cost more than a separate pass.
+LWC_DEVICE float erf_as(float x) {
+  const float a = fabsf(x);
+  const float t = __frcp_rn(1.f + 0.3275911f * a);
+  const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.f - y * __expf(-a * a), x);
+}
+LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
 
 // K-iteration range [a, e) of stream-K workgroup j (of wpx) on XCD x.
 LWC_DEVICE void sk_range(const Params& p, int x, int j, int& a, int& e) {

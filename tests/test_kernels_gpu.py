@@ -679,3 +679,22 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     classic = ops.grouped_gemm(Ac, Wq, off, a_scale=sc.float().contiguous(), w_scale=w_s.float().contiguous(),
                                a_rows=a_rows, rows=rows, splits=1, max_slots=-(-rows // 128) + G)
     _close(out, classic, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (4096, 3072, 1024), (300, 4096, 1024)])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
+    """gemm8p bias / bias + exact-erf GELU epilogue on the fp32 accumulators vs an fp32 torch reference
+    (the encoder's FFN1 / projections); the planner's library path gives the same function."""
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.ops import gemm_plan
+
+    torch.manual_seed(M + N + gelu)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) * 0.05).to(torch.bfloat16)
+    b = (torch.randn(N, device=gpu) * 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t() + b.float()
+    if gelu:
+        ref = torch.nn.functional.gelu(ref)
+    _close(ops.gemm8p(A, W, bias=b, gelu=gelu), ref, 3e-2, 1e-2)
+    _close(gemm_plan.linear_bias(A, W, b, gelu=gelu), ref, 3e-2, 1e-2)
