@@ -70,38 +70,51 @@ def bench_moe(a):
     from llm_weighted_consensus_amd.parallel import dist as pdist
 
     info = pdist.init_from_env("cuda")
-    tp = info.world if a.tp > 1 else 1
-    if a.tp > 1 and info.world != a.tp:
-        raise SystemExit(f"--tp {a.tp} needs torchrun with {a.tp} ranks (WORLD_SIZE={info.world})")
+    # config 5 layout: TP groups of `tp` consecutive ranks (IPC all-reduce inside each), DP across groups
+    # (each group serves its own requests): `--tp 2` on 8 GPUs = 4 x TP2
+    tp = a.tp if info.world > 1 else 1
+    if info.world % tp:
+        raise SystemExit(f"--tp {a.tp} must divide the world size {info.world}")
+    dp = info.world // tp
+    tp_group, dp_idx, tp_rank = pdist.candidate_groups(tp) if info.world > 1 else (None, 0, 0)
     dev = torch.device("cuda", info.local_rank)
     dcfg = decoder_config(a.decoder)
     comm = None
-    if tp > 1:
+    if tp > 1 and a.tp_comm == "ipc":
         from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
 
         # C3 over IPC peer buffers: [decode batch, hidden] bf16 per call, inside the captured decode graph
-        comm = CustomAllReduce(device=dev, max_bytes=a.requests * a.candidates * dcfg.hidden * 2)
+        comm = CustomAllReduce(group=tp_group, device=dev, max_bytes=a.requests * a.candidates * dcfg.hidden * 2)
     model = MixtralModel(dcfg, device=dev, seed=11, max_position=a.prompt_len + a.gen_len + 64, fp8=not a.bf16,
-                         tp_rank=info.rank if tp > 1 else 0, tp_size=tp, tp_comm=comm)
+                         tp_rank=tp_rank, tp_size=tp, tp_group=tp_group, tp_comm=comm)
     # config 5 is fp8 throughout: the embedder's projections too (e4m3 + per-channel scales, fp8 library GEMM)
     emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64,
                            fp8_dense=not a.bf16)
     scorer = EmbeddingConsensus(DecoderEmbedder(emb_model, max_tokens=a.gen_len + 16), tau=0.05)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     R, N = a.requests, a.candidates
+    if N % tp:
+        raise SystemExit(f"--candidates {N} must be a multiple of --tp {tp}")
+    shared = os.environ.get("LWC_SHARE_ONE_GPU") == "1" and info.world > 1
+    # ranks sharing one GPU size their caches concurrently from the same free memory: split the fraction
     engine = LLMEngine(model, tok, max_batch=R * N, max_model_len=a.prompt_len + a.gen_len + 16,
-                       kv_memory_fraction=0.4, use_graphs=model.graph_safe)
-    g = torch.Generator().manual_seed(5)
+                       kv_memory_fraction=0.4 / info.world if shared else 0.4, use_graphs=model.graph_safe)
+    g = torch.Generator().manual_seed(5 + dp_idx)  # each DP group its own prompts
 
     def step(i):
         groups = []
         for r in range(R):
             p = torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=g).tolist()
-            sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True, seed=i * 977 + r)
+            sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True,
+                                seed=(i * 977 + r) * 131 + dp_idx)
             groups.append(engine.add_request(p, sp, n=N))
         while engine.has_work():
             engine.step()
-        return scorer.score([[s.tokens for s in gr.seqs] for gr in groups])
+        # the TP ranks hold the same candidates: each embeds its 1/tp share, one all-gather (C1) inside the
+        # TP group assembles all N per request, and both run the (tiny) consensus
+        n_loc = N // tp
+        return scorer.score([[s.tokens for s in gr.seqs[tp_rank * n_loc:(tp_rank + 1) * n_loc]] for gr in groups],
+                            gather=tp > 1, group=tp_group)
 
     for i in range(a.warmup):
         step(i)
@@ -111,21 +124,22 @@ def bench_moe(a):
         step(a.warmup + i)
     _sync(dev, info.enabled)
     dt = pdist.max_over_ranks((time.perf_counter() - t0) / a.steps, dev)
-    shared = os.environ.get("LWC_SHARE_ONE_GPU") == "1" and tp > 1
     if comm is not None:
         comm.check()
     return {"metric": "consensus answers/sec (config 5: Mixtral-8x7B sampler + e5-mistral-7b embedder)",
-            "value": round(R / dt, 4), "unit": "answers/s", "n_gpus": 1 if shared else tp, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "value": round(dp * R / dt, 4), "unit": "answers/s", "n_gpus": 1 if shared else info.world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak",
             "dtype": ("fp8 e4m3 weights (experts, attention projections, embedder projections; per-channel scales) "
                       "x row-quantised e4m3 activations, bf16 elsewhere") if not a.bf16 else "bf16",
             "data": "synthetic prompts (random token ids), random-init weights",
-            "generated_tokens_per_s": round(R * N * a.gen_len / dt, 1),
-            "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": R, "candidates_per_request": N,
+            "generated_tokens_per_s": round(dp * R * N * a.gen_len / dt, 1),
+            "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": dp * R, "candidates_per_request": N,
                        "seq_len": a.prompt_len + a.gen_len,
-                       "parallelism": f"tp{tp}" + (" (ranks SHARE one GPU: a rehearsal of the protocol, not a "
-                                                   "multi-GPU number)" if shared else ""),
-                       "tp_allreduce": "ipc one-shot kernel (hipGraph)" if comm is not None else "none"}}
+                       "parallelism": f"tp{tp} x dp{dp}" + (" (ranks SHARE one GPU: a rehearsal of the protocol, "
+                                                            "not a multi-GPU number)" if shared else ""),
+                       "tp_allreduce": ("ipc one-shot kernel (hipGraph)" if comm is not None else
+                                        "process group (eager)" if tp > 1 else "none")}}
 
 
 def main():
@@ -143,13 +157,18 @@ def main():
     ap.add_argument("--embedder", default="e5-mistral-7b")
     ap.add_argument("--bf16", action="store_true", help="bf16 experts instead of fp8")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0, help="moe: world size (TP groups x DP); default = --tp")
+    ap.add_argument("--tp-comm", choices=["ipc", "pg"], default="ipc",
+                    help="moe TP all-reduce: IPC one-shot kernel (graph-captured) or the process group (RCCL / gloo, "
+                         "eager); spin-waiting IPC kernels of more than one TP pair cannot share one GPU")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    if a.which == "moe" and a.tp > 1:
+    if a.which == "moe" and max(a.tp, a.gpus) > 1:
         from llm_weighted_consensus_amd.parallel import launch
 
-        # `bench_configs.py moe --tp 2` without torchrun: launch the TP ranks (this process never touches the GPU)
-        rc = launch.maybe_self_launch(a.tp, __file__)
+        # `bench_configs.py moe --tp 2 [--gpus 8]` without torchrun: launch the ranks (this process never
+        # touches the GPU); default world = the TP degree
+        rc = launch.maybe_self_launch(max(a.tp, a.gpus), __file__)
         if rc is not None:
             sys.exit(rc)
     if a.which == "encoder":
