@@ -96,6 +96,9 @@ class ScoreClient:
         self.archive = archive
         self.rng = random.Random(rng_seed)
         self.register_inline = register_inline_models
+        # which of a model's voters THIS client runs (None: all); the voter-sharded client
+        # (score/sharded.py) runs a subset per rank and combines the tallies with a collective (C2)
+        self.voter_filter = None
 
     # ------------------------------------------------------------------ model
     async def fetch_or_validate_model(self, ctx, model_param) -> Model:
@@ -130,6 +133,12 @@ class ScoreClient:
 
     # ------------------------------------------------------------------ unary
     async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
+        out = await self._unary(ctx, request)
+        if self.archive is not None:
+            self.archive.store_score(out)
+        return out
+
+    async def _unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
         agg: Optional[S.ScoreCompletionChunk] = None
         stream = await self.create_streaming(ctx, request)
         async for item in stream:
@@ -139,17 +148,13 @@ class ScoreClient:
                 agg = item.clone()
             else:
                 agg.push(item)
-        out = S.ScoreCompletion.from_chunk(agg)
-        if self.archive is not None:
-            self.archive.store_score(out)
-        return out
+        return S.ScoreCompletion.from_chunk(agg)
 
     # ------------------------------------------------------------------ streaming
     async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams) -> AsyncIterator:
         """Returns an async iterator of ScoreCompletionChunk; a trailing ScoreError item (not raised)
         signals AllVotesFailed, as the reference yields Err after the final chunk."""
-        created = int(time.time())
-        rid = response_id(created)
+        created, rid = self._new_ids()
         C_len = len(request.choices)
         if C_len < 2:
             raise ScoreError.expected_two_or_more_choices(C_len)
@@ -231,16 +236,22 @@ class ScoreClient:
         q: asyncio.Queue = asyncio.Queue()
         DONE = object()
 
-        async def run_voter(llm: Llm):
+        async def run_voter(llm: Llm, seed: int):
             try:
-                async for chunk in self._voter_stream(ctx, rid, created, indexer, llm, weights[llm.index], request):
+                async for chunk in self._voter_stream(ctx, rid, created, indexer, llm, weights[llm.index], request,
+                                                      seed):
                     await q.put(chunk)
             finally:
                 await q.put(DONE)
 
-        tasks = [asyncio.create_task(run_voter(l)) for l in model.llms]
+        # key-tree seeds drawn for every voter in model order (whichever of them this client runs), so a
+        # voter's prompt does not depend on how the voters are sharded
+        seeds = [self.rng.getrandbits(63) for _ in model.llms]
+        tasks = [asyncio.create_task(run_voter(l, seeds[j])) for j, l in enumerate(model.llms)
+                 if self.voter_filter is None or self.voter_filter(l)]
         pending = len(tasks)
         first = True
+        voter_usage = C.Usage()  # this client's voters only (the voter-sharded merge sums it over ranks)
         try:
             while pending:
                 item = await q.get()
@@ -255,6 +266,7 @@ class ScoreClient:
                     md = ch.completion_metadata
                     if md is not None and md.usage is not None:
                         usage.push(md.usage)
+                        voter_usage.push(md.usage)
                         md.usage = None
                 yield item
         finally:
@@ -270,10 +282,9 @@ class ScoreClient:
                 any_ok = True
                 break
             codes.append(ch.error.code)
-        all_error = not any_ok
         votes = [list(ch.delta.vote) if ch.delta.vote is not None else [] for ch in voter_choices]
         wts = [ch.weight if ch.weight is not None else 0.0 for ch in voter_choices]
-        tally = RT.tally(votes, wts, C_len)
+        tally, all_error, codes = self._combine(votes, wts, C_len, any_ok, codes)
         self._record_training(model, weight_data, voter_choices, tally)  # before the deltas are cleared
         aggregate.weight_data = weight_data
         usage.with_total_cost()
@@ -290,9 +301,18 @@ class ScoreClient:
             ch.logprobs = None
             ch.error = None
         self._last_tally = tally
+        self._last_voter_usage = voter_usage
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+
+    def _new_ids(self):
+        created = int(time.time())
+        return created, response_id(created)
+
+    def _combine(self, votes, wts, C_len: int, any_ok: bool, codes):
+        """Tally this client's voters: (tally, all votes failed, error codes to unify)."""
+        return RT.tally(votes, wts, C_len), not any_ok, codes
 
     def _record_training(self, model, weight_data, voter_choices, tally) -> None:
         """Training-table models learn online: the transcript embedding and each voting voter's agreement
@@ -361,8 +381,8 @@ class ScoreClient:
             error=ResponseError.from_status_error(err), model=llm.id, model_index=llm.index)])
 
     async def _voter_stream(self, ctx, rid, created, indexer, llm: Llm, weight: float,
-                            request: S.ScoreCompletionCreateParams):
-        params, tree = self._voter_request(llm, request, self.rng.getrandbits(63))
+                            request: S.ScoreCompletionCreateParams, seed: int):
+        params, tree = self._voter_request(llm, request, seed)
         C_len = len(request.choices)
         model_id = request.model
         try:

@@ -23,6 +23,10 @@ variables configure the local engine:
   LWC_CONSTRAINED_LOGPROBS  1: constrained (json_schema / tool-call) voters get logprobs over the allowed
                     tokens, so a key letter's vote is the exact restricted softmax over its siblings
                     instead of whatever of them made the raw top-k (default 0 = reference semantics)
+  LWC_SHARD_VOTERS  1: voter-sharded deployment — one server process per GPU under torchrun / a
+                    launcher (RANK / WORLD_SIZE / LOCAL_RANK); rank 0 serves HTTP and broadcasts each
+                    score request, every rank runs its share of the voters (llm index % world) on its
+                    own GPU and the tallies combine with one all-reduce (C2, score/sharded.py)
 """
 from __future__ import annotations
 
@@ -76,6 +80,7 @@ class Config:
     training_table_path: Optional[str] = None
     registry_path: Optional[str] = None
     fault: Optional[str] = None
+    shard_voters: bool = False
 
     @classmethod
     def from_env(cls, dotenv: bool = True) -> "Config":
@@ -113,6 +118,7 @@ class Config:
         c.registry_path = e.get("LWC_REGISTRY_PATH")
         c.training_table_path = e.get("LWC_TRAINING_TABLE_PATH")
         c.fault = e.get("LWC_FAULT")
+        c.shard_voters = e.get("LWC_SHARD_VOTERS", "0") == "1"
         return c
 
     def api_bases(self):

@@ -90,10 +90,44 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                     embedders=embedders, services=services, archive=archive, registry=registry)
 
 
+def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
+    """LWC_SHARD_VOTERS: swap the score client for the voter-sharded one (a collective: every rank).
+    Returns rank 0's leader (serve it) or, on the other ranks, the client to ``follow``."""
+    from ..parallel import dist as pdist
+    from ..score.sharded import ScoreLeader, ShardedScoreClient
+
+    base = state.score
+    client = ShardedScoreClient(base.chat, group=group, model_registry=base.models, weight_fetchers=base.weights,
+                                archive=base.archive, rng_seed=rng_seed)
+    if pdist.info().rank == 0:
+        state.score = ScoreLeader(client)
+        state.multichat.score = state.score
+        return state.score
+    return client
+
+
 def main(argv: Optional[list] = None) -> None:
     import uvicorn
 
     cfg = Config.from_env()
+    if cfg.shard_voters:
+        from ..parallel import dist as pdist
+        from ..score.sharded import follow
+
+        info = pdist.init_from_env("cuda" if cfg.device != "cpu" else "cpu")
+        cfg.gpu = info.local_rank
+        state = build_state(cfg)
+        lead = shard_voters(state)
+        if info.rank != 0:
+            follow(lead)
+            pdist.shutdown()
+            return
+        try:
+            uvicorn.run(create_app(state), host=cfg.address, port=cfg.port, log_level="info")
+        finally:
+            lead.close()
+            pdist.shutdown()
+        return
     state = build_state(cfg)
     uvicorn.run(create_app(state), host=cfg.address, port=cfg.port, log_level="info")
 
