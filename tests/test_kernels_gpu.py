@@ -22,15 +22,16 @@ def _close(a, b, atol, rtol=0.0):
     assert (err <= lim).all(), f"max err {err.max().item():.4g} (atol {atol}, rtol {rtol})"
 
 
-@pytest.mark.parametrize("d", [384, 1024, 4096])
+@pytest.mark.parametrize("d,rows", [(384, 37), (1024, 37), (4096, 37), (2048, 301), (4096, 258), (8192, 256)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_rmsnorm(gpu, d, with_res):
+def test_rmsnorm(gpu, d, rows, with_res):
+    """rows >= 256 at d in {2048, 4096, 8192} take the wave-per-row kernel (ragged last workgroup)."""
     from llm_weighted_consensus_amd import ops
 
-    x = _bf(37, d, dev=gpu)
+    x = _bf(rows, d, dev=gpu)
     w = _bf(d, dev=gpu, scale=0.5) + 1
     if with_res:
-        r = _bf(37, d, dev=gpu)
+        r = _bf(rows, d, dev=gpu)
         r0 = r.clone()
         y = ops.rmsnorm(x, w, 1e-5, residual=r)
         h = (x.float() + r0.float()).to(torch.bfloat16)
