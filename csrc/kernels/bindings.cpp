@@ -12,7 +12,6 @@ int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int
 int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
                       int, hipStream_t);
 int lwc_silu_mul(const void*, void*, int, int, int, hipStream_t);
-int lwc_bias_gelu(void*, const void*, int, int, hipStream_t);
 int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
 int lwc_kv_gather(const void*, const void*, const long long*, void*, void*, int, int, int, int, hipStream_t);
@@ -141,19 +140,6 @@ void silu_mul(const at::Tensor& in, at::Tensor& out, int64_t block) {
   TORCH_CHECK(in.size(-1) == 2 * F && in.numel() == 2 * out.numel(), "silu_mul: shape mismatch");
   TORCH_CHECK(block == 0 || (block % 8 == 0 && F % block == 0), "silu_mul: block must divide F, multiple of 8");
   CHECK_RC(lwc_silu_mul(in.data_ptr(), out.data_ptr(), T, F, (int)block, cur_stream()), "silu_mul");
-}
-
-void bias_gelu(at::Tensor& x, const c10::optional<at::Tensor>& bias) {
-  CHECK_BF16(x); CHECK_CONTIG(x);
-  const int F = (int)x.size(-1);
-  const int T = (int)(x.numel() / std::max(F, 1));
-  const void* b = nullptr;
-  if (bias.has_value() && bias->defined()) {
-    CHECK_BF16(*bias);
-    TORCH_CHECK(bias->numel() == F, "bias_gelu: bias length");
-    b = bias->data_ptr();
-  }
-  CHECK_RC(lwc_bias_gelu(x.data_ptr(), b, T, F, cur_stream()), "bias_gelu");
 }
 
 void embedding(const at::Tensor& table, const at::Tensor& ids, at::Tensor& out) {
@@ -543,7 +529,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("silu_mul", &silu_mul);
-  m.def("bias_gelu", &bias_gelu);
   m.def("embedding", &embedding);
   m.def("kv_block_copy", &kv_block_copy);
   m.def("paged_decode", &paged_decode);

@@ -3,7 +3,6 @@
 //                          k, v into the paged KV cache in the same pass;
 //   K5  silu_mul        : SwiGLU  out = silu(gate) * up  over a fused [T, 2F] gate_up buffer;
 //   K7  embedding_gather: token ids -> hidden rows;
-//   K9b bias_gelu       : x = gelu_erf(x + bias) in place (BERT FFN1 epilogue);
 //   K12 kv_block_copy   : copy-on-write fork of whole KV blocks (all layers, K and V).
 // All of them move 16 B per lane (Guideline 13); trig comes from a host-built cos/sin table
 // (Appendix B "Element-wise": on-device sin/cos turns RoPE VALU-bound).
@@ -90,28 +89,6 @@ __global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restric
   }
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-
-// x: [T, F] in place, bias: [F] (may be null)
-__global__ void bias_gelu_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ bias, int T, int F) {
-  const int fv = F >> 3;
-  const size_t total = (size_t)T * fv;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % fv) * 8;
-    uint4v* p = reinterpret_cast<uint4v*>(x) + i;
-    float v[8], b[8];
-    unpack8(*p, v);
-    if (bias) {
-      unpack8(*reinterpret_cast<const uint4v*>(bias + c), b);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += b[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
-    *p = pack8(v);
-  }
-}
-
 // table: [V, d]; ids: [T] (int32); out: [T, d]
 __global__ void embedding_gather_kernel(const bf16_t* __restrict__ table, const int* __restrict__ ids,
                                         bf16_t* __restrict__ out, int d, int V) {
@@ -187,14 +164,6 @@ extern "C" int lwc_silu_mul(const void* in, void* out, int T, int F, int blk, hi
   if (F % 8 != 0 || blk % 8 != 0 || F % blk != 0) return -1;
   if (T == 0) return 0;
   silu_mul_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((const bf16_t*)in, (bf16_t*)out, T, F, blk);
-  return (int)hipGetLastError();
-}
-
-extern "C" int lwc_bias_gelu(void* x, const void* bias, int T, int F, hipStream_t s) {
-  using namespace lwc;
-  if (F % 8 != 0) return -1;
-  if (T == 0) return 0;
-  bias_gelu_kernel<<<ew_grid((size_t)T * F / 8, 256), 256, 0, s>>>((bf16_t*)x, (const bf16_t*)bias, T, F);
   return (int)hipGetLastError();
 }
 

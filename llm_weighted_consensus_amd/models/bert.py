@@ -9,7 +9,7 @@ consensus scorer.  Sequences are packed (cu_seqlens) — no padding FLOPs:
       qkv = x Wqkv^T + b                               hipBLASLt (fused q|k|v)
       a   = varlen bidirectional flash attention       K9c (MFMA, LDS-tiled QK^T)
       x   = LN(x + a Wo^T + bo)                         K9a fused residual
-      h   = gelu(x W1^T + b1)                          hipBLASLt + K9b fused bias+GELU
+      h   = gelu(x W1^T + b1)                          GEMM with the bias + GELU in its epilogue (K9b)
       x   = LN(x + h W2^T + b2)
     e   = L2norm(pool(x))                               K9d (CLS for bge)
 

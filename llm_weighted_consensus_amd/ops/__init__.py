@@ -77,12 +77,6 @@ def silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None, block: i
     return out
 
 
-def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """In place x = gelu_erf(x + bias) (K9b)."""
-    kernels().bias_gelu(x, bias)
-    return x
-
-
 def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row gather table[ids] (K7); ids int32."""
     if out is None:

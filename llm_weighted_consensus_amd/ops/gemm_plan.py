@@ -21,7 +21,7 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import bias_gelu_, gemm8p, silu_mul
+from . import gemm8p, silu_mul
 
 MODE = os.environ.get("LWC_GEMM", "auto")
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
@@ -76,9 +76,13 @@ def _m_bucket(M: int) -> int:
 
 
 def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = False, ws=None) -> torch.Tensor:
-    """x . w^T + b (optionally exact-erf GELU) — the encoder projections.  g8 applies the bias / GELU in
-    its epilogue on the fp32 accumulators; blas is hipBLASLt with the bias (+ the K9b bias_gelu pass).
-    The backend is chosen per (token bucket, N, K, epilogue) by timing both on the first call."""
+    """x . w^T + b (optionally GELU) — the encoder projections.  g8 applies the bias / exact-erf GELU in
+    its epilogue on the fp32 accumulators; blas is hipBLASLt with the bias, and for GELU its bias+GELU
+    epilogue (``torch._addmm_activation``: the tanh form of GELU on the fp32 accumulator, max 8.1e-3 from
+    the fp32 erf-GELU at the bge-large FFN1 shape — the bf16 output's own rounding, 7.8e-3 for gemm8p's
+    exact erf — where GEMM + the K9b bias_gelu pass rounds twice, 1.6e-2, and runs 657 vs 510 us at
+    65536 tokens: scripts/gelu_epilogue_probe.py).  The backend is chosen per (token bucket, N, K,
+    epilogue) by timing both on the first call."""
     M, K = x.shape
     N = w.shape[0]
     epi = "bias_gelu" if gelu else "bias"
@@ -87,7 +91,8 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
     # gemm8p addresses A through 32-bit buffer offsets: operands of 2 GiB or more take the library path
     ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda and M * x.stride(0) * 2 < (1 << 31)
     run_g8 = lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws)  # noqa: E731
-    run_blas = (lambda: bias_gelu_(F.linear(x, w), b)) if gelu else (lambda: F.linear(x, w, b))  # noqa: E731
+    run_blas = ((lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu  # noqa: E731
+                else (lambda: F.linear(x, w, b)))
     if c is None:
         if not ok or torch.cuda.is_current_stream_capturing():
             c = "blas"

@@ -54,18 +54,13 @@ def test_layernorm(gpu, d):
     _close(y2, ref.layernorm(x, g, b, 1e-12), 4e-2, 2e-2)
 
 
-def test_silu_mul_gelu_embedding(gpu):
+def test_silu_mul_embedding(gpu):
     from llm_weighted_consensus_amd import ops
 
     gu = _bf(19, 2 * 1024, dev=gpu)
     y = ops.silu_mul(gu)
     g, u = gu.float().chunk(2, -1)
     _close(y, torch.nn.functional.silu(g) * u, 2e-2, 2e-2)
-    x = _bf(11, 4096, dev=gpu)
-    b = _bf(4096, dev=gpu)
-    x0 = x.clone()
-    ops.bias_gelu_(x, b)
-    _close(x, torch.nn.functional.gelu(x0.float() + b.float()), 2e-2, 2e-2)
     table = _bf(1000, 384, dev=gpu)
     ids = torch.randint(0, 1000, (77,), device=gpu, dtype=torch.int32)
     _close(ops.embedding(table, ids), table[ids.long()], 0)
