@@ -798,9 +798,12 @@ class LLMEngine:
             bk.graph = g
         bk.graph.replay()
 
-    def _launch(self, seqs: List[Sequence]) -> _Step:
+    def _launch(self, seqs: List[Sequence], sample: bool = True) -> _Step:
         """Stage inputs, replay the decode graph and launch the sampler for `seqs`; results are
-        copied to pinned host memory asynchronously (processed later by :meth:`_process`)."""
+        copied to pinned host memory asynchronously (processed later by :meth:`_process`).
+        ``sample=False`` stops after the forward: :meth:`_launch_sample` launches the sampler later
+        (constrained batches: their grammar masks need the previous step's tokens on the host, which
+        are processed while this forward runs)."""
         B = len(seqs)
         bk = self._bucket(B)
         key = (bk.B, tuple(s.id for s in seqs))
@@ -844,7 +847,19 @@ class LLMEngine:
         if copies:
             self.cache.copy_blocks(torch.tensor(copies, dtype=torch.int32, device=dev))
         self._ensure_graph(bk)
-        K = st["K"]
+        step = _Step(seqs, key, bk, parity, st["K"], None, None, None)
+        step.static = st
+        self.stats["decode_tokens"] += B
+        self.stats["steps"] += 1
+        if sample:
+            self._launch_sample(step)
+        return step
+
+    def _launch_sample(self, step: _Step) -> None:
+        """Launch the sampler of a launched forward (grammar masks from the sequences' current
+        constraint states) and the asynchronous copy of its outputs to pinned host memory."""
+        seqs, bk, parity, st = step.seqs, step.bk, step.parity, step.static
+        B, K, d = len(seqs), step.K, bk.d
         mask = mask_rows = None
         cons = [i for i, s in enumerate(seqs) if s.constraint_state is not None]
         if cons:
@@ -864,9 +879,7 @@ class LLMEngine:
         out_host.copy_(out_dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self.stats["decode_tokens"] += B
-        self.stats["steps"] += 1
-        return _Step(seqs, key, bk, parity, K, outs[0], out_host, ev)
+        step.tok_dev, step.out_host, step.event = outs[0], out_host, ev
 
     def _constraint_masks(self, seqs: List[Sequence], cons: List[int]):
         """(mask table [rows, V/32] int32 on the device, per-sequence row [B] int32).
@@ -901,10 +914,13 @@ class LLMEngine:
                                     dtype=torch.int32, device=self.device)
                 grown[:self._mask_table.shape[0]] = self._mask_table
                 self._mask_table = grown
-            idx = torch.tensor([r for r, _ in new], dtype=torch.int64)
-            vals = torch.from_numpy(np.stack([m for _, m in new]).view(np.int32))
-            self._mask_table.index_copy_(0, idx.to(self.device), vals.to(self.device))
-        return self._mask_table, torch.from_numpy(rows).to(self.device)
+            # pinned + non_blocking: a pageable upload synchronises the stream, i.e. would wait for the
+            # decode forward already queued ahead of the sampler
+            idx = torch.tensor([r for r, _ in new], dtype=torch.int64).pin_memory()
+            vals = torch.from_numpy(np.stack([m for _, m in new]).view(np.int32)).pin_memory()
+            self._mask_table.index_copy_(0, idx.to(self.device, non_blocking=True),
+                                         vals.to(self.device, non_blocking=True))
+        return self._mask_table, torch.from_numpy(rows).pin_memory().to(self.device, non_blocking=True)
 
     def _process(self, st: _Step) -> List[TokenEvent]:
         st.event.synchronize()
@@ -931,21 +947,21 @@ class LLMEngine:
 
     def _decode(self) -> List[TokenEvent]:
         events: List[TokenEvent] = []
-        # grammar masks depend on the previous token: constrained batches run unpipelined
-        sync = any(s.constraint_state is not None for s in self.running)
-        if sync and self.inflight is not None:
-            events += self._drain()
+        # grammar masks depend on the previous token: a constrained batch launches its forward first
+        # (its input tokens come from the previous step's device output), processes the previous step on
+        # the host while that forward runs, and only then launches the sampler with the new masks
+        constrained = any(s.constraint_state is not None for s in self.running)
         seqs = [s for s in self.running if not s.finished and s.n_launched < s.params.max_tokens]
         if not seqs:
             return events + self._drain()
         with span("decode.launch"):
-            cur = self._launch(seqs)
+            cur = self._launch(seqs, sample=not constrained)
         prev, self.inflight = self.inflight, cur
         if prev is not None:
             with span("decode.process"):
                 events += self._process(prev)
-        if sync:
-            events += self._drain()
+        if constrained:
+            self._launch_sample(cur)
         self.running = [s for s in self.running if not s.finished]
         return events
 
