@@ -232,12 +232,23 @@ def cascade_tiles(runs: List[Tuple[int, int, int]], per_tile: int, tiles: np.nda
     return nt
 
 
+def _h2d(x, dtype, dev) -> torch.Tensor:
+    """Host list / array -> device through pinned memory, non-blocking: a pageable upload synchronises
+    the stream, i.e. would hold the host until every queued kernel (a decode step in flight) finished."""
+    t = (torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else torch.tensor(x)).to(dtype)
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 class _Step:
     """A launched (not yet processed) decode step."""
 
     def __init__(self, seqs, key, bk, parity, K, tok_dev, out_host, event):
         self.seqs, self.key, self.bk, self.parity, self.K = seqs, key, bk, parity, K
         self.tok_dev, self.out_host, self.event = tok_dev, out_host, event
+        self.static = None  # the launch's static sampler inputs (deferred sampler launch)
+        self.first = None   # first-token step after a prefill: (pinned host outputs, groups)
 
 
 class LLMEngine:
@@ -287,6 +298,8 @@ class LLMEngine:
         self.constrained_logprobs = constrained_logprobs
         self.buckets: Dict[int, _GraphBucket] = {}
         self.inflight: Optional[_Step] = None
+        # first tokens after a prefill are sampled asynchronously and processed by the next decode step
+        self.async_first_tokens = True
         self._step_no = 0
         self._comp_cache: Tuple[object, Optional[dict]] = (None, None)
         self.waiting: Deque[SequenceGroup] = deque()
@@ -439,15 +452,15 @@ class LLMEngine:
             ks = np.concatenate([slots_range(self.bm, pid, 0, L) for pid, L in zip(parents, k_lens)]).astype(np.int64)
             if ks.size and (ks.min() < 0 or ks.max() >= self.bm.num_blocks * self.block_size):
                 raise RuntimeError("prefix-cache prefill: KV slot out of range")
-            ctx = {"k_slots": torch.from_numpy(ks).to(dev),
-                   "cu_k": torch.tensor(np.concatenate([[0], np.cumsum(k_lens)]), dtype=torch.int32, device=dev),
+            ctx = {"k_slots": _h2d(ks, torch.int64, dev),
+                   "cu_k": _h2d(np.concatenate([[0], np.cumsum(k_lens)]), torch.int32, dev),
                    "q_lens": [L - c for L, c in zip(k_lens, cached)], "k_lens": k_lens}
             self.stats["prefix_cache_tokens"] += sum(cached)
-        t_tok = torch.tensor(toks, dtype=torch.int32, device=dev)
-        t_pos = torch.tensor(pos, dtype=torch.int32, device=dev)
-        t_slots = torch.from_numpy(np.concatenate(slots)).to(dev)
-        t_cu = torch.tensor(cu, dtype=torch.int32, device=dev)
-        t_last = torch.tensor(last, dtype=torch.int64, device=dev)
+        t_tok = _h2d(toks, torch.int32, dev)
+        t_pos = _h2d(pos, torch.int32, dev)
+        t_slots = _h2d(np.concatenate(slots), torch.int32, dev)
+        t_cu = _h2d(cu, torch.int32, dev)
+        t_last = _h2d(last, torch.int64, dev)
         max_len = max(len(p) - c for p, c in zip(prompts, cached))
         logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache, ctx=ctx)
         if use_cache:
@@ -517,6 +530,10 @@ class LLMEngine:
                 rows.append(logits_of[g.id])
                 seqs.append(s)
             self.bm.free_sequence(parent)
+        if self.async_first_tokens and self.inflight is None and self.device.type == "cuda":
+            self.inflight = self._launch_first(torch.stack(rows), seqs, groups)
+            self.running.extend(seqs)
+            return []
         events = self._sample_and_advance(torch.stack(rows), seqs)
         for g in groups:
             g.timer.token()
@@ -630,14 +647,14 @@ class LLMEngine:
             ks = np.concatenate([slots_range(self.bm, -g.id, 0, e) for g, _, e in items]).astype(np.int64)
             if ks.size and (ks.min() < 0 or ks.max() >= self.bm.num_blocks * self.block_size):
                 raise RuntimeError("chunked prefill: KV slot out of range")
-            ctx = {"k_slots": torch.from_numpy(ks).to(dev),
-                   "cu_k": torch.tensor(np.concatenate([[0], np.cumsum(k_lens)]), dtype=torch.int32, device=dev),
+            ctx = {"k_slots": _h2d(ks, torch.int64, dev),
+                   "cu_k": _h2d(np.concatenate([[0], np.cumsum(k_lens)]), torch.int32, dev),
                    "q_lens": [e - a for _, a, e in items], "k_lens": k_lens}
-        t_tok = torch.tensor(toks, dtype=torch.int32, device=dev)
-        t_pos = torch.tensor(pos, dtype=torch.int32, device=dev)
-        t_slots = torch.from_numpy(np.concatenate(slots)).to(dev)
-        t_cu = torch.tensor(cu, dtype=torch.int32, device=dev)
-        t_last = torch.tensor(last, dtype=torch.int64, device=dev)
+        t_tok = _h2d(toks, torch.int32, dev)
+        t_pos = _h2d(pos, torch.int32, dev)
+        t_slots = _h2d(np.concatenate(slots), torch.int32, dev)
+        t_cu = _h2d(cu, torch.int32, dev)
+        t_last = _h2d(last, torch.int64, dev)
         max_len = max(e - a for _, a, e in items)
         logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache, ctx=ctx)
         self.stats["prefill_tokens"] += len(toks)
@@ -845,7 +862,7 @@ class LLMEngine:
             src = torch.tensor(from_prev_src, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
             d["tokens"].index_copy_(0, dst, prev.tok_dev.index_select(0, src))
         if copies:
-            self.cache.copy_blocks(torch.tensor(copies, dtype=torch.int32, device=dev))
+            self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
         self._ensure_graph(bk)
         step = _Step(seqs, key, bk, parity, st["K"], None, None, None)
         step.static = st
@@ -916,14 +933,20 @@ class LLMEngine:
                 self._mask_table = grown
             # pinned + non_blocking: a pageable upload synchronises the stream, i.e. would wait for the
             # decode forward already queued ahead of the sampler
-            idx = torch.tensor([r for r, _ in new], dtype=torch.int64).pin_memory()
-            vals = torch.from_numpy(np.stack([m for _, m in new]).view(np.int32)).pin_memory()
-            self._mask_table.index_copy_(0, idx.to(self.device, non_blocking=True),
-                                         vals.to(self.device, non_blocking=True))
-        return self._mask_table, torch.from_numpy(rows).pin_memory().to(self.device, non_blocking=True)
+            self._mask_table.index_copy_(0, _h2d([r for r, _ in new], torch.int64, self.device),
+                                         _h2d(np.stack([m for _, m in new]).view(np.int32), torch.int32, self.device))
+        return self._mask_table, _h2d(rows, torch.int32, self.device)
 
     def _process(self, st: _Step) -> List[TokenEvent]:
         st.event.synchronize()
+        if st.first is not None:  # first tokens after a prefill (:meth:`_launch_first`)
+            host, groups = st.first
+            lists = [h.tolist() for h in host]
+            events = self._advance(st.seqs, lists[0], lists[1], lists[2] if st.K else None,
+                                   lists[3] if st.K else None)
+            for g in groups:
+                g.timer.token()
+            return events
         B, K = len(st.seqs), st.K
         Kb = max(K, 1)
         Bp = st.bk.B
@@ -968,6 +991,28 @@ class LLMEngine:
     # ------------------------------------------------------------------ sampling + bookkeeping
     def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[TokenEvent]:
         """Synchronous sampling (first token after prefill)."""
+        tok, lp, tk_ids, tk_lp, K = self._sample_first(logits, seqs)
+        return self._advance(seqs, tok.cpu().tolist(), lp.cpu().tolist(),
+                             tk_ids.cpu().tolist() if K else None, tk_lp.cpu().tolist() if K else None)
+
+    def _launch_first(self, logits: torch.Tensor, seqs: List[Sequence], groups: List[SequenceGroup]) -> _Step:
+        """Asynchronous first-token sampling after a prefill: the sampler and the copy of its outputs
+        to pinned host memory are queued and the result becomes the in-flight step, processed by the
+        next decode step after it has launched its own forward — the GPU goes from the prefill
+        straight into the next decode step instead of idling while the host forks and advances."""
+        tok, lp, tk_ids, tk_lp, K = self._sample_first(logits, seqs)
+        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ((tok, lp, tk_ids, tk_lp) if K else
+                                                                               (tok, lp))]
+        for h, t in zip(host, (tok, lp, tk_ids, tk_lp)):
+            h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st = _Step(seqs, None, None, 0, K, tok, None, ev)
+        st.first = (host, groups)
+        return st
+
+    def _sample_first(self, logits: torch.Tensor, seqs: List[Sequence]):
+        """Launch the sampler over prefill last-token logits (no host sync); advances n_launched."""
         B = len(seqs)
         dev = self.device
         ps = [s.params for s in seqs]
@@ -1003,8 +1048,7 @@ class LLMEngine:
         )
         for s in seqs:
             s.n_launched += 1
-        return self._advance(seqs, tok.cpu().tolist(), lp.cpu().tolist(),
-                             tk_ids.cpu().tolist() if K else None, tk_lp.cpu().tolist() if K else None)
+        return tok, lp, tk_ids, tk_lp, K
 
     def _advance(self, seqs: List[Sequence], tok_h, lp_h, ids_h, lps_h) -> List[TokenEvent]:
         """Host bookkeeping of one sampled token per sequence: append, grammar advance, stop / length

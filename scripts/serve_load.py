@@ -126,9 +126,10 @@ def main():
         import pstats
 
         for name, pr in profs.items():
-            buf = io.StringIO()
-            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(25)
-            print(f"==== {name} (tottime)\n" + buf.getvalue()[:6000], file=sys.stderr)
+            for order, k in (("tottime", 25), ("cumulative", 45)):
+                buf = io.StringIO()
+                pstats.Stats(pr, stream=buf).sort_stats(order).print_stats(k)
+                print(f"==== {name} ({order})\n" + buf.getvalue()[:9000], file=sys.stderr)
 
 
 if __name__ == "__main__":
