@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import json as _json
 import math
+import re
 from typing import Any
 
 _enc_str = _json.encoder.py_encode_basestring  # ensure_ascii=False escaping (== serde_json)
@@ -100,8 +101,30 @@ def _enc(v: Any, out: list) -> None:
         raise TypeError(f"not JSON serialisable: {type(v)!r}")
 
 
+_C_DUMPS = _json.JSONEncoder(ensure_ascii=False, separators=(",", ":"), allow_nan=True).encode
+# a number in exponent form or a non-finite float: the only places Python's float repr and ryu differ
+# (as a whole value: after ':' ',' '[' and before ',' ']' '}'; a string that contains such text only costs
+# the exact path)
+_NEEDS_RYU = re.compile(r"[:,\[]-?(?:\d+(?:\.\d+)?e[-+]?\d+|NaN|Infinity)[,\]}]")
+
+
+def _plain(v: Any) -> Any:
+    return v.to_obj() if hasattr(v, "to_obj") else v
+
+
 def dumps(v: Any) -> str:
-    """Compact serde_json text (serde_json::to_string)."""
+    """Compact serde_json text (serde_json::to_string).  Fast path: the C encoder, whose output equals
+    serde_json's except for floats in exponent form and non-finite floats — when the text holds either
+    (or a string that merely looks like one) the exact ryu encoder runs instead."""
+    s = None
+    p = _plain(v)
+    if isinstance(p, (dict, list)):  # (a bare scalar has no delimiters for the check below)
+        try:
+            s = _C_DUMPS(p)
+        except (TypeError, ValueError):
+            s = None
+    if s is not None and not _NEEDS_RYU.search(s):
+        return s
     out: list = []
     _enc(v, out)
     return "".join(out)
