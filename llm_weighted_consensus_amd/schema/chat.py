@@ -11,7 +11,7 @@ from typing import Annotated, Any, Dict, List, Literal, Optional, Union
 
 from pydantic import Field
 
-from .base import Wire, first_some, push_opt_list, push_opt_num, push_opt_str
+from .base import Wire, push_opt_list, push_opt_num
 
 # ============================================================================ request side
 
@@ -467,8 +467,16 @@ class Logprobs(Wire):
     refusal: Optional[List[Logprob]] = None
 
     def push(self, o: "Logprobs") -> None:
-        self.content = push_opt_list(self.content, o.content)
-        self.refusal = push_opt_list(self.refusal, o.refusal)
+        if o.content is not None:
+            if self.content is None:
+                self.content = list(o.content)
+            else:
+                self.content.extend(o.content)  # owned by the aggregate: no O(n^2) re-concatenation
+        if o.refusal is not None:
+            if self.refusal is None:
+                self.refusal = list(o.refusal)
+            else:
+                self.refusal.extend(o.refusal)  # owned by the aggregate: no O(n^2) re-concatenation
 
 
 class ImageUrlOut(Wire):
@@ -485,8 +493,10 @@ class StreamToolCallFunction(Wire):
     arguments: Optional[str] = None
 
     def push(self, o: "StreamToolCallFunction") -> None:
-        self.name = first_some(self.name, o.name)
-        self.arguments = push_opt_str(self.arguments, o.arguments)
+        if o.name is not None and self.name is None:
+            self.name = o.name
+        if o.arguments is not None:
+            self.arguments = o.arguments if self.arguments is None else self.arguments + o.arguments
 
 
 class StreamToolCall(Wire):
@@ -496,12 +506,14 @@ class StreamToolCall(Wire):
     type: Optional[Literal["function"]] = None
 
     def push(self, o: "StreamToolCall") -> None:
-        self.id = first_some(self.id, o.id)
+        if o.id is not None and self.id is None:
+            self.id = o.id
         if self.function is not None and o.function is not None:
             self.function.push(o.function)
         elif self.function is None and o.function is not None:
             self.function = o.function.clone()
-        self.type = first_some(self.type, o.type)
+        if o.type is not None and self.type is None:
+            self.type = o.type
 
 
 class Delta(Wire):
@@ -513,9 +525,12 @@ class Delta(Wire):
     images: Optional[List[Image]] = None
 
     def push(self, o: "Delta") -> None:
-        self.content = push_opt_str(self.content, o.content)
-        self.refusal = push_opt_str(self.refusal, o.refusal)
-        self.role = first_some(self.role, o.role)
+        if o.content is not None:
+            self.content = o.content if self.content is None else self.content + o.content
+        if o.refusal is not None:
+            self.refusal = o.refusal if self.refusal is None else self.refusal + o.refusal
+        if o.role is not None and self.role is None:
+            self.role = o.role
         if o.tool_calls is not None:
             if self.tool_calls is None:
                 self.tool_calls = [t.clone() for t in o.tool_calls]
@@ -526,7 +541,8 @@ class Delta(Wire):
                         mine.push(t)
                     else:
                         self.tool_calls.append(t.clone())
-        self.reasoning = push_opt_str(self.reasoning, o.reasoning)
+        if o.reasoning is not None:
+            self.reasoning = o.reasoning if self.reasoning is None else self.reasoning + o.reasoning
         self.images = push_opt_list(self.images, [i.clone() for i in o.images] if o.images is not None else None)
 
     def tool_as_content(self) -> None:
@@ -549,7 +565,8 @@ class StreamChoice(Wire):
 
     def push(self, o: "StreamChoice") -> None:
         self.delta.push(o.delta)
-        self.finish_reason = first_some(self.finish_reason, o.finish_reason)
+        if o.finish_reason is not None and self.finish_reason is None:
+            self.finish_reason = o.finish_reason
         if self.logprobs is not None and o.logprobs is not None:
             self.logprobs.push(o.logprobs)
         elif self.logprobs is None and o.logprobs is not None:
@@ -579,13 +596,16 @@ class ChatCompletionChunk(Wire):
 
     def push(self, o: "ChatCompletionChunk") -> None:
         push_choices(self.choices, o.choices)
-        self.service_tier = first_some(self.service_tier, o.service_tier)
-        self.system_fingerprint = first_some(self.system_fingerprint, o.system_fingerprint)
+        if o.service_tier is not None and self.service_tier is None:
+            self.service_tier = o.service_tier
+        if o.system_fingerprint is not None and self.system_fingerprint is None:
+            self.system_fingerprint = o.system_fingerprint
         if self.usage is not None and o.usage is not None:
             self.usage.push(o.usage)
         elif self.usage is None and o.usage is not None:
             self.usage = o.usage.clone()
-        self.provider = first_some(self.provider, o.provider)
+        if o.provider is not None and self.provider is None:
+            self.provider = o.provider
 
     def with_total_cost(self) -> None:
         if self.usage is not None:

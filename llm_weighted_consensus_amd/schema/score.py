@@ -14,7 +14,7 @@ from typing import Annotated, Any, List, Literal, Optional, Union
 from pydantic import Field
 
 from ..errors import ResponseError
-from .base import Wire, first_some
+from .base import Wire
 from .chat import (Delta, FinishReason, Logprobs, Message, ServiceTier, StreamOptions, Tool,
                    UnaryChoice, UnaryMessage, UsageRequest, Usage, push_choices)
 
@@ -72,13 +72,16 @@ class CompletionMetadata(Wire):
     provider: Optional[str] = None
 
     def push(self, o: "CompletionMetadata") -> None:
-        self.service_tier = first_some(self.service_tier, o.service_tier)
-        self.system_fingerprint = first_some(self.system_fingerprint, o.system_fingerprint)
+        if o.service_tier is not None and self.service_tier is None:
+            self.service_tier = o.service_tier
+        if o.system_fingerprint is not None and self.system_fingerprint is None:
+            self.system_fingerprint = o.system_fingerprint
         if self.usage is not None and o.usage is not None:
             self.usage.push(o.usage)
         elif self.usage is None and o.usage is not None:
             self.usage = o.usage.clone()
-        self.provider = first_some(self.provider, o.provider)
+        if o.provider is not None and self.provider is None:
+            self.provider = o.provider
 
 
 class ScoreDelta(Delta):
@@ -87,7 +90,8 @@ class ScoreDelta(Delta):
 
     def push(self, o: "ScoreDelta") -> None:
         Delta.push(self, o)
-        self.vote = first_some(self.vote, list(o.vote) if o.vote is not None else None)
+        if o.vote is not None and self.vote is None:
+            self.vote = list(o.vote)
 
 
 class ScoreStreamChoice(Wire):
@@ -111,16 +115,22 @@ class ScoreStreamChoice(Wire):
 
     def push(self, o: "ScoreStreamChoice") -> None:
         self.delta.push(o.delta)
-        self.finish_reason = first_some(self.finish_reason, o.finish_reason)
+        if o.finish_reason is not None and self.finish_reason is None:
+            self.finish_reason = o.finish_reason
         if self.logprobs is not None and o.logprobs is not None:
             self.logprobs.push(o.logprobs)
         elif self.logprobs is None and o.logprobs is not None:
             self.logprobs = o.logprobs.clone()
-        self.weight = first_some(self.weight, o.weight)
-        self.confidence = first_some(self.confidence, o.confidence)
-        self.error = first_some(self.error, o.error)
-        self.model = first_some(self.model, o.model)
-        self.model_index = first_some(self.model_index, o.model_index)
+        if o.weight is not None and self.weight is None:
+            self.weight = o.weight
+        if o.confidence is not None and self.confidence is None:
+            self.confidence = o.confidence
+        if o.error is not None and self.error is None:
+            self.error = o.error
+        if o.model is not None and self.model is None:
+            self.model = o.model
+        if o.model_index is not None and self.model_index is None:
+            self.model_index = o.model_index
         if self.completion_metadata is not None and o.completion_metadata is not None:
             self.completion_metadata.push(o.completion_metadata)
         elif self.completion_metadata is None and o.completion_metadata is not None:
@@ -176,7 +186,8 @@ class ScoreCompletionChunk(Wire):
             self.usage.push(o.usage)
         elif self.usage is None and o.usage is not None:
             self.usage = o.usage.clone()
-        self.weight_data = first_some(self.weight_data, o.weight_data)
+        if o.weight_data is not None and self.weight_data is None:
+            self.weight_data = o.weight_data
 
     def tool_as_content(self) -> None:
         for c in self.choices:
@@ -257,14 +268,18 @@ class MultichatStreamChoice(Wire):
 
     def push(self, o: "MultichatStreamChoice") -> None:
         self.delta.push(o.delta)
-        self.finish_reason = first_some(self.finish_reason, o.finish_reason)
+        if o.finish_reason is not None and self.finish_reason is None:
+            self.finish_reason = o.finish_reason
         if self.logprobs is not None and o.logprobs is not None:
             self.logprobs.push(o.logprobs)
         elif self.logprobs is None and o.logprobs is not None:
             self.logprobs = o.logprobs.clone()
-        self.error = first_some(self.error, o.error)
-        self.model = first_some(self.model, o.model)
-        self.model_index = first_some(self.model_index, o.model_index)
+        if o.error is not None and self.error is None:
+            self.error = o.error
+        if o.model is not None and self.model is None:
+            self.model = o.model
+        if o.model_index is not None and self.model_index is None:
+            self.model_index = o.model_index
         if self.completion_metadata is not None and o.completion_metadata is not None:
             self.completion_metadata.push(o.completion_metadata)
         elif self.completion_metadata is None and o.completion_metadata is not None:
