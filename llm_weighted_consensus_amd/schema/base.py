@@ -20,12 +20,10 @@ from ..utils import json as sjson
 def to_obj(v: Any) -> Any:
     if isinstance(v, Wire):
         return v.to_obj()
-    if isinstance(v, list):
-        return [to_obj(x) for x in v]
-    if isinstance(v, tuple):
-        return [to_obj(x) for x in v]
+    if isinstance(v, (list, tuple)):  # scalars inline (token byte lists): no call per element
+        return [x if isinstance(x, _IMMUTABLE) else to_obj(x) for x in v]
     if isinstance(v, dict):
-        return {k: to_obj(x) for k, x in v.items()}
+        return {k: x if isinstance(x, _IMMUTABLE) else to_obj(x) for k, x in v.items()}
     return v
 
 

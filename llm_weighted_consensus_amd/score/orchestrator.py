@@ -334,7 +334,7 @@ class ScoreClient:
     def _voter_request(self, llm: Llm, request: S.ScoreCompletionCreateParams, seed: int):
         base = llm.base
         messages = list(base.prefix_messages or []) + list(request.messages) + list(base.suffix_messages or [])
-        messages = [m.model_copy(deep=True) for m in messages]
+        messages = [m.clone() for m in messages]
         max_branch = 20 if base.top_logprobs in (None, 0, 1) else int(base.top_logprobs)
         tree = RT.KeyTree(len(request.choices), max_branch, seed)
         keys = [k for k, _ in tree.keys]
