@@ -4,8 +4,8 @@ One process per GPU; `torch.distributed` backend "nccl" IS RCCL on ROCm.  On CPU
 code runs over gloo.  Collectives used by the serving/bench paths:
 
   C1 all_gather of candidate embeddings  [n_local, d] -> [world, n_local, d]
-  C2 combine of votes / tallies          one [choices+1] fp64 all-reduce + one object gather per request
-                                         (parallel/votes.py, score/sharded.py)
+  C2 combine of votes / tallies          one object all-gather of the voter choices per request, ordered
+                                         by request number (parallel/votes.py, score/sharded.py)
   C3 TP all-reduce                       (tensor-parallel decoders; IPC one-shot kernel, parallel/allreduce.py)
   C4 all_to_all_single                   (expert-parallel MoE dispatch / combine, parallel/expert.py)
   C5 broadcast / barrier                 (control)

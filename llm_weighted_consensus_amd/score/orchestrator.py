@@ -86,6 +86,13 @@ def _logprobs_for_vote(choice: S.ScoreStreamChoice):
             for l in lp.content]
 
 
+def tally_choices(voter_choices, C_len: int):
+    """Native tally (reference client.rs:384-455) over voter choices in order."""
+    votes = [list(ch.delta.vote) if ch.delta.vote is not None else [] for ch in voter_choices]
+    wts = [ch.weight if ch.weight is not None else 0.0 for ch in voter_choices]
+    return RT.tally(votes, wts, C_len)
+
+
 class ScoreClient:
     def __init__(self, chat_client, model_registry: Optional[ModelRegistry] = None,
                  weight_fetchers: Optional[WeightFetchers] = None, archive=None, rng_seed: Optional[int] = None,
@@ -154,7 +161,7 @@ class ScoreClient:
     async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams) -> AsyncIterator:
         """Returns an async iterator of ScoreCompletionChunk; a trailing ScoreError item (not raised)
         signals AllVotesFailed, as the reference yields Err after the final chunk."""
-        created, rid = self._new_ids()
+        created, rid = self._new_ids(ctx)
         C_len = len(request.choices)
         if C_len < 2:
             raise ScoreError.expected_two_or_more_choices(C_len)
@@ -282,13 +289,14 @@ class ScoreClient:
                 any_ok = True
                 break
             codes.append(ch.error.code)
-        votes = [list(ch.delta.vote) if ch.delta.vote is not None else [] for ch in voter_choices]
-        wts = [ch.weight if ch.weight is not None else 0.0 for ch in voter_choices]
-        tally, all_error, codes = self._combine(votes, wts, C_len, any_ok, codes)
+        tally, all_error, codes = await self._combine(ctx, aggregate, C_len, any_ok, codes, usage, voter_usage)
+        voter_choices = aggregate.choices[C_len:]  # (a voter-sharded combine adds the other ranks' voters)
         self._record_training(model, weight_data, voter_choices, tally)  # before the deltas are cleared
         aggregate.weight_data = weight_data
         usage.with_total_cost()
         aggregate.usage = usage
+        # choices first seen in this final chunk (another rank's voters, voter-sharded) keep their content
+        whole = ctx.get("whole", ()) if isinstance(ctx, dict) else ()
         for j, ch in enumerate(aggregate.choices):
             if ch.index < C_len:
                 ch.weight = tally.choice_weight[ch.index]
@@ -296,23 +304,26 @@ class ScoreClient:
             elif ch.delta.vote is not None:
                 vc = tally.voter_confidence[j - C_len]
                 ch.confidence = vc if ch.confidence is None else ch.confidence + vc
+            if ch.index in whole:
+                continue
             ch.delta = S.ScoreDelta()
             ch.finish_reason = None
             ch.logprobs = None
             ch.error = None
         self._last_tally = tally
-        self._last_voter_usage = voter_usage
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
 
-    def _new_ids(self):
+    def _new_ids(self, ctx=None):
         created = int(time.time())
         return created, response_id(created)
 
-    def _combine(self, votes, wts, C_len: int, any_ok: bool, codes):
-        """Tally this client's voters: (tally, all votes failed, error codes to unify)."""
-        return RT.tally(votes, wts, C_len), not any_ok, codes
+    async def _combine(self, ctx, aggregate: S.ScoreCompletionChunk, C_len: int, any_ok: bool, codes, usage,
+                       voter_usage):
+        """Tally the aggregate's voters: (tally, all votes failed, error codes to unify).  ``usage`` is
+        the request's running total, ``voter_usage`` this client's voters' share of it."""
+        return tally_choices(aggregate.choices[C_len:], C_len), not any_ok, codes
 
     def _record_training(self, model, weight_data, voter_choices, tally) -> None:
         """Training-table models learn online: the transcript embedding and each voting voter's agreement

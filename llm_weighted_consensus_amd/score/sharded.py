@@ -1,77 +1,143 @@
 """Voter-sharded scoring: one score request's voters spread over the ranks of a process group (C2).
 
 The reference fans a request's voters out as concurrent upstream streams and tallies their votes in one
-place (src/score/completions/client.rs:343-356 fan-out, :384-455 tally).  Here every rank of ``group``
-runs the SAME request (SPMD: same requests, same order, one at a time) through the ordinary
-``ScoreClient`` but only for the voters it owns (``llm.index % world == rank``, i.e. the voters whose
-models its GPU serves); the ranks then meet twice per request:
+place (src/score/completions/client.rs:343-356 fan-out, :384-455 tally).  Here every rank runs the SAME
+requests (SPMD) through the ordinary ``ScoreClient`` but only for the voters it owns
+(``llm.index % world == rank``: the voters whose models its GPU serves), and requests run CONCURRENTLY
+on every rank, as on a single server.
 
-  1. tally (parallel/votes.py ``tally_across``): one all-reduce of the [choices + 1] fp64 partial
-     choice weights — every rank ends with the global weights / confidences and its own voters'
-     confidences, exactly the single-process tally up to summation order;
-  2. response (``create_unary``): one object all-gather of every rank's voter choices and voter usage;
-     the merged response lists the provided choices (global weights) followed by every voter's choice,
-     ordered by voter index.
+C2 is ONE collective per request: when a request's local voters are done, each rank contributes its
+voter choices (votes, weights, errors, content) to an object all-gather; every rank then holds every
+voter of the request (its own under the indices it already streamed, the others' after them by voter
+index), runs the native tally over all of them and finishes the request — rank 0's response is the full
+one.  Collectives of concurrent requests must be issued in
+the same order on every rank, so they go through a per-rank combiner thread that runs them strictly in
+request sequence order (the leader numbers requests as it broadcasts them); a request that fails before
+its combine still takes its slot (an empty contribution), so the ranks never fall out of step.
 
-Ids, created timestamps and the key-tree seeds match on every rank (rank 0's id is broadcast; the seeds
-are drawn for all voters in model order on every rank), so a voter's prompt is the same whichever rank
-runs it.  Streaming is per rank (its own voters' chunks, then the global final chunk); the merged view
-is the unary response.
+Requests and their ids reach the followers over a second process group (control), so broadcasts and
+combines never interleave on one group.  Both groups are gloo: the payloads are small Python objects.
 """
 from __future__ import annotations
+
+import asyncio
+import threading
+from typing import Any, List
 
 import torch.distributed as dist
 
 from ..parallel import votes as V
 from ..schema import chat as C
 from ..schema import score as S
-from .choices import message_to_delta
-from .orchestrator import ScoreClient
+from .orchestrator import ScoreClient, tally_choices
+
+_SKIP = None  # a request's empty contribution (it failed before its combine on this rank)
+
+
+class _Combiner:
+    """Runs each request's all-gather in sequence order on a thread of its own."""
+
+    def __init__(self, group):
+        self.group = group
+        self.cv = threading.Condition()
+        self.pending = {}
+        self.next = 0
+        self.closed = False
+        self.thread = threading.Thread(target=self._run, name="c2-combiner", daemon=True)
+        self.thread.start()
+
+    async def submit(self, seq: int, payload: Any) -> List[Any]:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        with self.cv:
+            self.pending[seq] = (payload, loop, fut)
+            self.cv.notify()
+        return await fut
+
+    def _run(self) -> None:
+        while True:
+            with self.cv:
+                while self.next not in self.pending and not self.closed:
+                    self.cv.wait()
+                if self.next not in self.pending:
+                    return
+                payload, loop, fut = self.pending.pop(self.next)
+                self.next += 1
+            try:
+                res = V.gather_objects(payload, self.group)
+                loop.call_soon_threadsafe(_resolve, fut, res, None)
+            except BaseException as e:  # noqa: BLE001 — handed to the awaiting request
+                loop.call_soon_threadsafe(_resolve, fut, None, e)
+
+    def close(self) -> None:
+        with self.cv:
+            self.closed = True
+            self.cv.notify()
+        self.thread.join(timeout=60)
+
+
+def _resolve(fut, res, err) -> None:
+    if fut.done():
+        return
+    if err is not None:
+        fut.set_exception(err)
+    else:
+        fut.set_result(res)
 
 
 class ShardedScoreClient(ScoreClient):
+    """``ctx`` of every request is ``{"seq": n, "ids": (created, id)}`` (from :class:`ScoreLeader` /
+    :func:`follow`, or given by the caller, identical on every rank)."""
+
     def __init__(self, chat_client, group=None, **kw):
         super().__init__(chat_client, **kw)
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.group = group if group is not None else dist.new_group(backend="gloo")
+        self.world = dist.get_world_size(self.group)
+        self.rank = dist.get_rank(self.group)
+        self.voter_filter = lambda llm: llm.index % self.world == self.rank
         # one key-tree seed stream on every rank (rank 0's): a voter's prompt does not depend on its rank
         self.rng.seed(V.broadcast_object(self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"],
-                                         0, group))
-        self.voter_filter = lambda llm: llm.index % self.world == self.rank
+                                         0, self.group))
+        self.combiner = _Combiner(self.group)
 
-    def _new_ids(self):
-        return V.broadcast_object(super()._new_ids(), 0, self.group)
+    def _new_ids(self, ctx=None):
+        return tuple(ctx["ids"])
 
-    def _combine(self, votes, wts, C_len, any_ok, codes):
-        tally, all_error = V.tally_across(votes, wts, C_len, any_ok, self.group)
-        if all_error:  # a global decision: every rank takes this branch together
-            codes = [c for part in V.gather_objects(list(codes), self.group) for c in part]
-        return tally, all_error, codes
-
-    async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
-        C_len = len(request.choices)
-        out = await self._unary(ctx, request)
-        mine = ([c.to_obj() for c in out.choices if c.index >= C_len], self._last_voter_usage.to_obj())
-        parts = V.gather_objects(mine, self.group)
-        voters = [S.ScoreUnaryChoice.model_validate(o) for choices, _ in parts for o in choices]
-        voters.sort(key=lambda c: (c.model_index if c.model_index is not None else -1, c.index))
-        for k, c in enumerate(voters):
-            c.index = C_len + k
-        merged = out.model_copy(deep=True)
-        merged.choices = [c for c in merged.choices if c.index < C_len] + voters
-        # usage: this rank's total (voters + any training-table embedding, counted once) + the other
-        # ranks' voter usage
-        usage = out.usage.clone() if out.usage is not None else C.Usage()
-        for r, (_, u) in enumerate(parts):
+    async def _combine(self, ctx, aggregate: S.ScoreCompletionChunk, C_len: int, any_ok: bool, codes, usage,
+                       voter_usage):
+        ctx["combined"] = True
+        mine = aggregate.choices[C_len:]
+        parts = await self.combiner.submit(ctx["seq"], (any_ok, list(codes), [c.to_obj() for c in mine],
+                                                        voter_usage.to_obj()))
+        remote, n_ok, all_codes = [], 0, []
+        for r, part in enumerate(parts):
+            if part is _SKIP:
+                continue
+            ok, cds, objs, u = part
+            n_ok += bool(ok)
+            all_codes += cds
             if r != self.rank:
-                usage.push(C.Usage.model_validate(u))
-        usage.total_cost = None
-        usage.with_total_cost()
-        merged.usage = usage
-        if self.archive is not None and self.rank == 0:
-            self.archive.store_score(merged)
-        return merged
+                remote += [S.ScoreStreamChoice.model_validate(o) for o in objs]
+                usage.push(C.Usage.model_validate(u))  # the other ranks' voters (an embedding's usage: once)
+        # this rank's voters keep the indices its stream already used; the others' follow, by voter index
+        remote.sort(key=lambda c: (c.model_index if c.model_index is not None else -1, c.index))
+        for k, c in enumerate(remote):
+            c.index = C_len + len(mine) + k
+        ctx["whole"] = {c.index for c in remote}  # complete choices: the final chunk carries them as they are
+        aggregate.choices = aggregate.choices + remote
+        return tally_choices(aggregate.choices[C_len:], C_len), n_ok == 0, all_codes
+
+    async def run(self, seq: int, ids, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
+        """One request on this rank (unary); always takes its combine slot."""
+        ctx = {"seq": seq, "ids": ids}
+        try:
+            return await self.create_unary(ctx, request)
+        finally:
+            if not ctx.get("combined"):
+                await self.combiner.submit(seq, _SKIP)
+
+    def close(self) -> None:
+        self.combiner.close()
 
 
 # ---------------------------------------------------------------------------------------------
@@ -80,26 +146,31 @@ class ShardedScoreClient(ScoreClient):
 
 class ScoreLeader:
     """Rank 0's score client in a voter-sharded deployment (``LWC_SHARD_VOTERS=1``): every score
-    request is broadcast to the follower ranks (``follow``) before rank 0 runs its share, one request
-    at a time (the collectives of concurrent requests must not interleave).  Streaming requests get
-    the merged response as one chunk.  Everything else (model validation for multichat, ...) is the
-    wrapped client's."""
+    request is numbered and broadcast to the follower ranks (control group), then run here like on the
+    followers — concurrently with the other requests in flight.  Streaming requests get the merged
+    response as one chunk.  Everything else (model validation for multichat, ...) is the wrapped
+    client's."""
 
-    def __init__(self, client: ShardedScoreClient):
+    def __init__(self, client: ShardedScoreClient, control=None):
         self.client = client
-        self._lock = None
+        self.control = control if control is not None else dist.new_group(backend="gloo")
+        self._seq = 0
+        self._lock = threading.Lock()
 
     def __getattr__(self, name):
         return getattr(self.client, name)
 
-    async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
-        import asyncio
+    def _announce(self, request) -> tuple:
+        with self._lock:
+            seq = self._seq
+            self._seq += 1
+            ids = ScoreClient._new_ids(self.client)
+            V.broadcast_object((seq, ids, request), 0, self.control)
+        return seq, ids
 
-        if self._lock is None:
-            self._lock = asyncio.Lock()
-        async with self._lock:
-            V.broadcast_object(request, 0, self.client.group)
-            return await self.client.create_unary(ctx, request)
+    async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
+        seq, ids = self._announce(request)
+        return await self.client.run(seq, ids, request)
 
     async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams):
         out = await self.create_unary(ctx, request)
@@ -110,10 +181,13 @@ class ScoreLeader:
         return one()
 
     def close(self) -> None:
-        V.broadcast_object(None, 0, self.client.group)
+        V.broadcast_object(None, 0, self.control)
+        self.client.close()
 
 
 def as_chunk(out: S.ScoreCompletion) -> S.ScoreCompletionChunk:
+    from .choices import message_to_delta
+
     choices = []
     for c in out.choices:
         delta = message_to_delta(c.message)
@@ -126,21 +200,39 @@ def as_chunk(out: S.ScoreCompletion) -> S.ScoreCompletionChunk:
                                   weight_data=out.weight_data)
 
 
-def follow(client: ShardedScoreClient) -> int:
-    """Ranks > 0: run every request the leader broadcasts (their voters' share) until it sends None.
-    Returns the number of requests served.  A request that fails fails on every rank alike (the
-    all-votes-failed decision is global), so errors are dropped here — the leader reports them."""
-    import asyncio
-
+def follow(client: ShardedScoreClient, control=None) -> int:
+    """Ranks > 0: run every request the leader broadcasts (their voters' share), concurrently, until it
+    sends None; returns the number of requests run.  A failed request fails on every rank alike and the
+    leader reports it, so errors are dropped here."""
     from ..errors import StatusError
 
-    n = 0
-    while True:
-        request = V.broadcast_object(None, 0, client.group)
-        if request is None:
-            return n
-        try:
-            asyncio.run(client.create_unary(None, request))
-        except StatusError:
-            pass
-        n += 1
+    control = control if control is not None else dist.new_group(backend="gloo")
+
+    async def main() -> int:
+        loop = asyncio.get_running_loop()
+        tasks: List[asyncio.Future] = []
+        done = asyncio.Event()
+
+        async def one(seq, ids, request):
+            try:
+                await client.run(seq, ids, request)
+            except StatusError:
+                pass
+
+        def receive() -> None:
+            while True:
+                msg = V.broadcast_object(None, 0, control)
+                if msg is None:
+                    loop.call_soon_threadsafe(done.set)
+                    return
+                loop.call_soon_threadsafe(lambda m=msg: tasks.append(asyncio.ensure_future(one(*m))))
+
+        t = threading.Thread(target=receive, name="c2-follow", daemon=True)
+        t.start()
+        await done.wait()
+        await asyncio.gather(*tasks)
+        return len(tasks)
+
+    n = asyncio.run(main())
+    client.close()
+    return n

@@ -26,7 +26,8 @@ variables configure the local engine:
   LWC_SHARD_VOTERS  1: voter-sharded deployment — one server process per GPU under torchrun / a
                     launcher (RANK / WORLD_SIZE / LOCAL_RANK); rank 0 serves HTTP and broadcasts each
                     score request, every rank runs its share of the voters (llm index % world) on its
-                    own GPU and the tallies combine with one all-reduce (C2, score/sharded.py)
+                    own GPU, requests run concurrently and each combines its voters with one all-gather
+                    (C2, score/sharded.py)
 """
 from __future__ import annotations
 

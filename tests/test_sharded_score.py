@@ -1,7 +1,7 @@
 """Voter-sharded scoring over a process group (C2; gloo, world 2, CPU): a score request's voters split
 across ranks give the single-process tally, confidences, votes and usage; ids agree on every rank;
 "every vote failed" is decided globally (every rank raises, error codes unified over all ranks); a rank
-that owns no voter still takes part."""
+that owns no voter still takes part; requests run concurrently (combines ordered by request number)."""
 import asyncio
 import math
 import os
@@ -72,6 +72,13 @@ def _run(client, case):
         return {"error": e.code}
 
 
+async def _run_sharded(client, seq, case):
+    try:
+        return _summary(await client.run(seq, (1700000000, f"scrcpl-test-{seq}"), _request(case)))
+    except ScoreError as e:
+        return {"error": e.code}
+
+
 def _worker(rank, world, port, out_q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
@@ -80,7 +87,16 @@ def _worker(rank, world, port, out_q):
 
     pdist.init_from_env("cpu")
     client = ShardedScoreClient(FakeChatClient(_policy), rng_seed=7)
-    res = {case: _run(client, case) for case in CASES}
+    # one at a time (same key-tree seeds as the single-process client), then all cases concurrently
+    res = {case: asyncio.run(_run_sharded(client, i, case)) for i, case in enumerate(CASES)}
+
+    async def concurrent():
+        cases = list(CASES) * 3
+        outs = await asyncio.gather(*(_run_sharded(client, len(CASES) + i, c) for i, c in enumerate(cases)))
+        return [(c, o) for c, o in zip(cases, outs)]
+
+    res["concurrent"] = asyncio.run(concurrent())
+    client.close()
     out_q.put((rank, res))
     pdist.shutdown()
 
@@ -102,7 +118,7 @@ def test_voter_sharded_score_matches_single_process():
         assert p.exitcode == 0
     for case in ("mixed", "one_voter"):
         w, g0, g1 = want[case], got[0][case], got[1][case]
-        assert g0["id"] == g1["id"]  # rank 0's id broadcast
+        assert g0["id"] == g1["id"]  # the request's id, identical on every rank
         for g in (g0, g1):  # every rank merges the same full response
             assert g["n"] == w["n"] and g["indices"] == list(range(w["n"]))
             assert g["prompt_tokens"] == w["prompt_tokens"]
@@ -114,6 +130,13 @@ def test_voter_sharded_score_matches_single_process():
                 assert b[2] == pytest.approx(a[2])
                 assert (a[3] is None and b[3] is None) or b[3] == pytest.approx(a[3])
     assert want["all_fail"]["error"] == got[0]["all_fail"]["error"] == got[1]["all_fail"]["error"]
+    for r in (0, 1):  # concurrent requests: same shapes and tallies (seeds differ, so not the votes)
+        for case, o in got[r]["concurrent"]:
+            if case == "all_fail":
+                assert o == {"error": want["all_fail"]["error"]}
+            else:
+                assert o["n"] == want[case]["n"] and o["prompt_tokens"] == want[case]["prompt_tokens"]
+                assert sum(cf for _, _, cf in o["provided"]) == pytest.approx(1.0)
 
 
 def _serve_worker(rank, world, port, out_q):
@@ -140,6 +163,8 @@ def _serve_worker(rank, world, port, out_q):
                 await state.score.create_unary(None, _request("all_fail"))
             except ScoreError as e:
                 out.append(e.code)
+            many = await asyncio.gather(*(state.score.create_unary(None, _request("mixed")) for _ in range(6)))
+            out.append([len(m.choices) for m in many])
             return out
 
         res = asyncio.run(serve())
@@ -164,8 +189,9 @@ def test_leader_broadcasts_requests_to_followers():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    mixed, (n_chunks, idx), code = got[0]
+    mixed, (n_chunks, idx), code, many = got[0]
     assert mixed["n"] == want["n"] and [v[:2] for v in mixed["voters"]] == [v[:2] for v in want["voters"]]
     assert n_chunks == 1 and idx == [0, 1, 2, 3]
     assert code == 429 or code == want.get("error", code)
-    assert got[1] == 3  # the follower ran all three requests
+    assert many == [want["n"]] * 6  # concurrent requests: every voter of every request in the response
+    assert got[1] == 9  # the follower ran all nine requests
