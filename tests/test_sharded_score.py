@@ -51,6 +51,10 @@ CASES = {
 
 
 def _request(case):
+    if case == "one_choice":  # rejected before any voter runs: the request still takes its combine slot
+        return S.ScoreCompletionCreateParams.model_validate(dict(
+            messages=[{"role": "user", "content": "What is the capital of France?"}],
+            model={"llms": CASES["one_voter"]}, choices=["Paris"], stream=False))
     return S.ScoreCompletionCreateParams.model_validate(dict(
         messages=[{"role": "user", "content": "What is the capital of France?"}],
         model={"llms": CASES[case]}, choices=["Paris", "London", "Berlin"], stream=False))
@@ -91,7 +95,7 @@ def _worker(rank, world, port, out_q):
     res = {case: asyncio.run(_run_sharded(client, i, case)) for i, case in enumerate(CASES)}
 
     async def concurrent():
-        cases = list(CASES) * 3
+        cases = (list(CASES) + ["one_choice"]) * 3
         outs = await asyncio.gather(*(_run_sharded(client, len(CASES) + i, c) for i, c in enumerate(cases)))
         return [(c, o) for c, o in zip(cases, outs)]
 
@@ -132,7 +136,9 @@ def test_voter_sharded_score_matches_single_process():
     assert want["all_fail"]["error"] == got[0]["all_fail"]["error"] == got[1]["all_fail"]["error"]
     for r in (0, 1):  # concurrent requests: same shapes and tallies (seeds differ, so not the votes)
         for case, o in got[r]["concurrent"]:
-            if case == "all_fail":
+            if case == "one_choice":
+                assert o == {"error": 400}
+            elif case == "all_fail":
                 assert o == {"error": want["all_fail"]["error"]}
             else:
                 assert o["n"] == want[case]["n"] and o["prompt_tokens"] == want[case]["prompt_tokens"]
