@@ -63,24 +63,34 @@ struct PairRegs {
 };
 
 // Token rows at or past `ctx` (the tail of a sequence's last block, or a pair without a B block) are
-// not fetched: the lanes that own them skip the load (exec-masked, no HBM/L2 traffic) and hold zeros.
+// not fetched: each (block, head) segment is addressed through a 4 KiB buffer resource and the lanes
+// that own such rows use an offset past its end, so the hardware returns zeros without a memory request.
+// (Branch-free: the exec-masked form of the same loads made the compiler wrap every load in its own
+// branch and insert a vmcnt(0) inside one of them, draining the two-pair pipeline every pair.)
 // Their scores are masked to -inf and their V elements selected away (pair_softmax / pair_values), so
 // the values never matter; zeros only keep the registers defined.  At the bench's decode shape the
 // suffix's last block is on average half empty: ~10 % of the suffix bytes.
+constexpr int kOOB = 0x40000000;  // an offset past any segment's num_records
+
+LWC_DEVICE __amdgpu_buffer_rsrc_t seg_rsrc(const bf16_t* seg) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)seg, (short)0, kBS * kD * 2, 0x00020000);
+}
+
 LWC_DEVICE void load_pair_k(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
                             int g, int ctx = 0x7fffffff) {
   const size_t kv_head_stride = (size_t)kBS * kD;  // elements per (block, head)
   const int physA = bt[blkA];
   const int physB = hasB ? bt[blkA + 1] : physA;
-  const bf16_t* kA = p.kc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
-  const bf16_t* kB = p.kc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+  const __amdgpu_buffer_rsrc_t rA = seg_rsrc(p.kc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride);
+  const __amdgpu_buffer_rsrc_t rB = seg_rsrc(p.kc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride);
   const bool okA = blkA * kBS + r16 < ctx;
   const bool okB = hasB && (blkA + 1) * kBS + r16 < ctx;
-  const short8 z{0, 0, 0, 0, 0, 0, 0, 0};
+  const int base = (r16 * kD + 8 * g) * 2;
+  const int oA = okA ? base : kOOB, oB = okB ? base : kOOB;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    r.ka[s] = okA ? *reinterpret_cast<const short8*>(kA + r16 * kD + 32 * s + 8 * g) : z;
-    r.kb[s] = okB ? *reinterpret_cast<const short8*>(kB + r16 * kD + 32 * s + 8 * g) : z;
+    r.ka[s] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rA, oA + 64 * s, 0, 0));
+    r.kb[s] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rB, oB + 64 * s, 0, 0));
   }
 }
 
@@ -89,15 +99,16 @@ LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, i
   const size_t kv_head_stride = (size_t)kBS * kD;
   const int physA = bt[blkA];
   const int physB = hasB ? bt[blkA + 1] : physA;
-  const bf16_t* vA = p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride;
-  const bf16_t* vB = p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride;
+  const __amdgpu_buffer_rsrc_t rA = seg_rsrc(p.vc + ((size_t)physA * p.Hkv + kvh) * kv_head_stride);
+  const __amdgpu_buffer_rsrc_t rB = seg_rsrc(p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride);
   const bool okA = blkA * kBS + 4 * g < ctx;  // lane group g holds tokens 4g..4g+3
   const bool okB = hasB && (blkA + 1) * kBS + 4 * g < ctx;
-  const short4v z{0, 0, 0, 0};
+  const int base = (g * kD + r16) * 8;  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
+  const int oA = okA ? base : kOOB, oB = okB ? base : kOOB;
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
-    r.va[n] = okA ? *reinterpret_cast<const short4v*>(vA + (g * kD + 16 * n + r16) * 4) : z;
-    r.vb[n] = okB ? *reinterpret_cast<const short4v*>(vB + (g * kD + 16 * n + r16) * 4) : z;
+  for (int n = 0; n < 8; ++n) {
+    r.va[n] = __builtin_bit_cast(short4v, __builtin_amdgcn_raw_buffer_load_b64(rA, oA + 128 * n, 0, 0));
+    r.vb[n] = __builtin_bit_cast(short4v, __builtin_amdgcn_raw_buffer_load_b64(rB, oB + 128 * n, 0, 0));
   }
 }
 
