@@ -144,8 +144,10 @@ def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, w
     # Isolated timings flatter gemm8p's plain / residual kernels: in the captured decode step the qkv
     # projection measured 180.6 us on gemm8p vs 160.6 us on hipBLASLt (profiles/bench_r64.md, round 2)
     # where the isolated pair had been a near tie — so those need a clear win; the fused SwiGLU (one
-    # kernel against GEMM + silu_mul) does not.
-    margin = 1.0 if epi == "swiglu" else 0.97
+    # kernel against GEMM + silu_mul) keeps gemm8p unless the library wins clearly: the short timing
+    # runs are noisy enough to flip the choice (they did under a profiler; both choices were within
+    # 0.5 % of the step there) and a stable choice keeps box-to-box results comparable.
+    margin = 1.03 if epi == "swiglu" else 0.97
     _CHOICE[key] = "g8" if t_g8 < t_blas * margin else "blas"
     return _CHOICE[key]
 
