@@ -34,7 +34,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--requests", type=int, default=64, help="requests per GPU per step (R)")
+    ap.add_argument("--requests", type=int, default=None,
+                    help="requests per GPU per step (R); default 4096 // N: a 4096-sequence decode batch per GPU "
+                         "(R=64 at the headline's N=64, R=16 for config 4's N=256)")
     ap.add_argument("--candidates", type=int, default=64, help="candidates per request (N)")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--gen-len", type=int, default=128)
@@ -72,7 +74,8 @@ def main():
     W, rank = info.world, info.rank
     launch.check_world(a.gpus, W)
     dev = torch.device("cuda", info.local_rank)
-    N, R = a.candidates, a.requests
+    N = a.candidates
+    R = a.requests or max(1, 4096 // N)
     cp = a.cp or max(1, min(W, N // 32))
     while W % cp or N % cp:
         cp -= 1
