@@ -50,6 +50,20 @@ def main():
 
         S.EngineService._run = prof_run
 
+        from llm_weighted_consensus_amd.engine import group as G
+
+        orig_read = G.EngineGroup._read
+
+        def prof_read(self):
+            pr = profs.setdefault("group-reader", cProfile.Profile())
+            pr.enable()
+            try:
+                orig_read(self)
+            finally:
+                pr.disable()
+
+        G.EngineGroup._read = prof_read
+
     import httpx
 
     from llm_weighted_consensus_amd.server.app import create_app
