@@ -32,6 +32,7 @@
 namespace lwc {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t uint2v __attribute__((ext_vector_type(2)));
 
 LWC_DEVICE float4v mfma16(const short8& a, const short8& b, const float4v& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
@@ -59,8 +60,11 @@ struct DecodeParams {
 // K and V registers of one PAIR of 16-token blocks for one wave (K: 8 x 16 B, V: 16 x 8 B per lane).
 struct PairRegs {
   short8 ka[4], kb[4];
-  short4v va[8], vb[8];
+  uint4v v[8];  // PV B operand of dim 16n + r16: {A tokens 4g..4g+3 | B tokens 4g..4g+3}, loaded in place
 };
+
+// 8 bytes of A tokens and 8 of B tokens as one 16-byte MFMA operand (the two loads land in its halves)
+LWC_DEVICE uint4v join_v(const uint2v& a, const uint2v& b) { return uint4v{a[0], a[1], b[0], b[1]}; }
 
 // Token rows at or past `ctx` (the tail of a sequence's last block, or a pair without a B block) are
 // not fetched: each (block, head) segment is addressed through a 4 KiB buffer resource and the lanes
@@ -106,10 +110,9 @@ LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, i
   const int base = (g * kD + r16) * 8;  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
   const int oA = okA ? base : kOOB, oB = okB ? base : kOOB;
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    r.va[n] = __builtin_bit_cast(short4v, __builtin_amdgcn_raw_buffer_load_b64(rA, oA + 128 * n, 0, 0));
-    r.vb[n] = __builtin_bit_cast(short4v, __builtin_amdgcn_raw_buffer_load_b64(rB, oB + 128 * n, 0, 0));
-  }
+  for (int n = 0; n < 8; ++n)
+    r.v[n] = join_v(__builtin_bit_cast(uint2v, __builtin_amdgcn_raw_buffer_load_b64(rA, oA + 128 * n, 0, 0)),
+                    __builtin_bit_cast(uint2v, __builtin_amdgcn_raw_buffer_load_b64(rB, oB + 128 * n, 0, 0)));
 }
 
 LWC_DEVICE void load_pair(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
@@ -188,33 +191,18 @@ LWC_DEVICE void pair_values(const PairRegs& r, const short8& pf, int blkA, bool 
   const int blkB = blkA + 1;
   if (hasB && (blkB + 1) * kBS <= ctx) {  // wave-uniform
 #pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      short8 vf;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        vf[i] = r.va[n][i];
-        vf[4 + i] = r.vb[n][i];
-      }
-      o[n] = mfma16(pf, vf, o[n]);
-    }
+    for (int n = 0; n < 8; ++n) o[n] = mfma16(pf, __builtin_bit_cast(short8, r.v[n]), o[n]);
     return;
   }
-  bool okA[4], okB[4];
+  // tokens of this lane's 4-token groups inside the context: a bit mask per 16-bit element, applied to
+  // each operand with 4 ANDs (NaN bits become +0)
+  const int nA = min(max(ctx - (blkA * kBS + 4 * g), 0), 4);
+  const int nB = hasB ? min(max(ctx - (blkB * kBS + 4 * g), 0), 4) : 0;
+  const unsigned long long mA = nA >= 4 ? ~0ull : ((1ull << (16 * nA)) - 1);
+  const unsigned long long mB = nB >= 4 ? ~0ull : ((1ull << (16 * nB)) - 1);
+  const uint4v m{(uint32_t)mA, (uint32_t)(mA >> 32), (uint32_t)mB, (uint32_t)(mB >> 32)};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    okA[i] = blkA * kBS + 4 * g + i < ctx;
-    okB[i] = hasB && (blkB * kBS + 4 * g + i < ctx);
-  }
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    short8 vf;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      vf[i] = okA[i] ? r.va[n][i] : (short)0;
-      vf[4 + i] = okB[i] ? r.vb[n][i] : (short)0;
-    }
-    o[n] = mfma16(pf, vf, o[n]);
-  }
+  for (int n = 0; n < 8; ++n) o[n] = mfma16(pf, __builtin_bit_cast(short8, r.v[n] & m), o[n]);
 }
 
 // One whole pair: scores, softmax, values.
@@ -518,8 +506,8 @@ __global__ void __launch_bounds__(kCWaves * 64)
 #pragma unroll
         for (int n = 0; n < 8; ++n) {
           const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
-          r.va[n] = *reinterpret_cast<const short4v*>(pb + 2 * kSegBytes + off);
-          r.vb[n] = *reinterpret_cast<const short4v*>(pb + 3 * kSegBytes + off);
+          r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
+                          *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
         }
         attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
       }
