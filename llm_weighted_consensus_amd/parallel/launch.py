@@ -20,6 +20,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 from typing import List, Optional, Sequence
 
@@ -48,20 +49,32 @@ def launch(world: int, argv: Sequence[str], poll_s: float = 0.2) -> int:
     procs: List[subprocess.Popen] = []
     for r in range(world):
         procs.append(subprocess.Popen(list(argv), env=child_env(r, world, port)))
+    # one waiter thread per rank records exits in the order they happen: the first failure is the
+    # cause, the ranks that then lose their peers (and fail too) are not
+    exits: List[tuple] = []
+    lock = threading.Lock()
+
+    def waiter(r: int) -> None:
+        rc = procs[r].wait()
+        with lock:
+            exits.append((time.monotonic(), r, rc))
+
+    for r in range(world):
+        threading.Thread(target=waiter, args=(r,), daemon=True).start()
     status = 0
     try:
-        live = set(range(world))
-        while live:
-            for r in list(live):
-                rc = procs[r].poll()
-                if rc is None:
-                    continue
-                live.discard(r)
+        seen = 0
+        while seen < world:
+            with lock:
+                new = sorted(exits)[seen:] if len(exits) > seen else []
+            for _, r, rc in new:
+                seen += 1
                 if rc != 0 and status == 0:
                     status = rc if rc > 0 else 128 - rc
                     print(f"launch: rank {r} exited with {rc}; stopping the other ranks", file=sys.stderr)
-                    for q in live:
-                        procs[q].send_signal(signal.SIGTERM)
+                    for q in range(world):
+                        if procs[q].poll() is None:
+                            procs[q].send_signal(signal.SIGTERM)
             time.sleep(poll_s)
     finally:
         for p in procs:
