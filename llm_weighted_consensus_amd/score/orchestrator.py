@@ -24,6 +24,7 @@ import asyncio
 import random
 import time
 import uuid
+from collections import OrderedDict
 from typing import Any, AsyncIterator, Dict, List, Optional
 
 from .. import _runtime as RT
@@ -106,10 +107,34 @@ class ScoreClient:
         # which of a model's voters THIS client runs (None: all); the voter-sharded client
         # (score/sharded.py) runs a subset per rank and combines the tallies with a collective (C2)
         self.voter_filter = None
+        # inline models validated before, by their JSON text: validation + the voter / model ids (JSON +
+        # xxh3 per voter) cost ~2 ms per request when every request carries its model inline
+        self._inline_models: "OrderedDict[str, Model]" = OrderedDict()
 
     # ------------------------------------------------------------------ model
     async def fetch_or_validate_model(self, ctx, model_param) -> Model:
-        """reference client.rs:911-950."""
+        """reference client.rs:911-950.  Models are read-only after validation, so an inline model seen
+        before (same JSON text) is returned from a small LRU instead of being validated again."""
+        key = None
+        if not (isinstance(model_param, str) and len(model_param.split("/")[-1]) == 22):
+            try:
+                key = model_param if isinstance(model_param, str) else sjson.dumps(
+                    model_param.to_obj() if hasattr(model_param, "to_obj") else model_param)
+            except Exception:
+                key = None
+        if key is not None:
+            hit = self._inline_models.get(key)
+            if hit is not None:
+                self._inline_models.move_to_end(key)
+                return hit
+        m = await self._fetch_or_validate_model(ctx, model_param)
+        if key is not None:
+            self._inline_models[key] = m
+            while len(self._inline_models) > 512:
+                self._inline_models.popitem(last=False)
+        return m
+
+    async def _fetch_or_validate_model(self, ctx, model_param) -> Model:
         try:
             if isinstance(model_param, str):
                 if len(model_param) == 22:
