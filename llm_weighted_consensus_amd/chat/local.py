@@ -90,6 +90,19 @@ def render_chat_prompt(messages: List[Any], tools: Optional[List[C.Tool]] = None
     raise ValueError(f"unknown chat template {template!r} (one of {CHAT_TEMPLATES})")
 
 
+def _token_info(tok, tid: int):
+    """(text, byte list) of a token for logprob entries, cached on the tokenizer: every streamed token
+    carries itself plus its top alternatives (read-only lists, shared by the responses)."""
+    cache = tok.__dict__.get("_lwc_token_info")
+    if cache is None:
+        cache = tok.__dict__["_lwc_token_info"] = {}
+    v = cache.get(tid)
+    if v is None:
+        b = tok.token_bytes(tid)
+        v = cache[tid] = (b.decode("utf-8", errors="replace"), list(b))
+    return v
+
+
 class LocalChatClient(ChatClient):
     """Attempt semantics follow the reference's upstream client (src/chat/completions/client.rs:238-305,
     347-354): the primary model, then each fallback in ``models``, among the locally served ones; an
@@ -318,10 +331,11 @@ class LocalChatClient(ChatClient):
                         d.content = (d.content or "") + ev.text
                     started[i] = True
                     if sp.logprobs:
-                        lp = C.Logprob(token=tok.token_str(ev.token_id), bytes=list(tok.token_bytes(ev.token_id)),
-                                       logprob=ev.logprob,
-                                       top_logprobs=[C.TopLogprob(token=tok.token_str(t), bytes=list(tok.token_bytes(t)),
-                                                                  logprob=l) for t, l in ev.top_logprobs])
+                        ts, tb = _token_info(tok, ev.token_id)
+                        lp = C.Logprob(token=ts, bytes=tb, logprob=ev.logprob,
+                                       top_logprobs=[C.TopLogprob(token=a, bytes=b, logprob=l)
+                                                     for (a, b), l in ((_token_info(tok, t), l)
+                                                                       for t, l in ev.top_logprobs)])
                         if ch.logprobs is None:
                             ch.logprobs = C.Logprobs(content=[lp])
                         else:
