@@ -33,6 +33,20 @@ def main():
                     help="comma list: serve through an EngineGroup of worker processes (e.g. '0' = one worker)")
     a = ap.parse_args()
     profs = {}
+    import gc
+
+    gc_time = {0: 0.0, 1: 0.0, 2: 0.0}
+    gc_n = {0: 0, 1: 0, 2: 0}
+    _gc_t0 = [0.0]
+
+    def _gc_cb(phase, info):  # time spent in each generation's collections (stalls every thread)
+        if phase == "start":
+            _gc_t0[0] = time.perf_counter()
+        else:
+            gc_time[info["generation"]] += time.perf_counter() - _gc_t0[0]
+            gc_n[info["generation"]] += 1
+
+    gc.callbacks.append(_gc_cb)
     if a.profile:
         import cProfile
 
@@ -132,6 +146,7 @@ def main():
 
     out["phases"] = {k: [v[0], round(v[1], 3)] for k, v in STATS.snapshot()["phases"].items()}
     out["engine_steps"] = stats["steps"]
+    out["gc"] = {f"gen{k}": [gc_n[k], round(gc_time[k], 3)] for k in gc_time}
     print(json.dumps(out), flush=True)
     for svc in state.services.values():
         svc.close()
