@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import copy
+import typing
 from typing import Any, ClassVar, FrozenSet
 
 from pydantic import BaseModel, ConfigDict
@@ -57,34 +58,82 @@ def _plan(cls) -> list:
     return p
 
 
+def _list_kind(ann) -> str:
+    """'scalars' for a (optional) list of str/int/float/bool (token byte lists), 'wires' for a list of one
+    Wire class, '' otherwise."""
+    args = [a for a in typing.get_args(ann) if a is not type(None)] if typing.get_origin(ann) is typing.Union else [ann]
+    if len(args) != 1 or typing.get_origin(args[0]) not in (list, typing.List):
+        return ""
+    el = typing.get_args(args[0])
+    if len(el) != 1:
+        return ""
+    if el[0] in (str, int, float, bool):
+        return "scalars"
+    return "wires" if isinstance(el[0], type) and issubclass(el[0], Wire) else ""
+
+
+_SCALARS = frozenset(_IMMUTABLE)
+_GEN: dict = {}
+
+
+def _compile_to_obj(cls):
+    """Straight-line ``to_obj`` for one class, generated from its field plan: no loop over the plan and
+    no per-field flag tests at run time (the serving front end turns ~800 objects into dicts per scored
+    response).  Scalars are recognised by exact class; anything else (str enums included) goes through
+    the generic :func:`to_obj`, which returns scalars unchanged."""
+    src = ["def _to_obj(self):", " d = self.__dict__", " out = {}"]
+    fields = cls.model_fields
+    for name, key, keep, flat in _plan(cls):
+        src += [f" v = d[{name!r}]",
+                " if v is None:" + (f" out[{key!r}] = None" if keep else " pass"),
+                f" elif v.__class__ in _SCALARS: out[{key!r}] = v",
+                " elif isinstance(v, Wire): " + ("out.update(v.to_obj())" if flat else f"out[{key!r}] = v.to_obj()")]
+        kind = _list_kind(fields[name].annotation)
+        if kind == "scalars":  # still checked per element: a list field may be assigned anything
+            src.append(f" elif v.__class__ is list: out[{key!r}] = [x if x.__class__ in _SCALARS else _any(x) for x in v]")
+        elif kind == "wires":
+            src.append(f" elif v.__class__ is list: out[{key!r}] = [x.to_obj() if isinstance(x, Wire) else _any(x) for x in v]")
+        src.append(f" else: out[{key!r}] = _any(v)")
+    src += [" extra = self.__pydantic_extra__",
+            " if extra: out.update({k: _any(x) for k, x in extra.items()})",
+            " return out"]
+    ns = {"_SCALARS": _SCALARS, "Wire": Wire, "_any": to_obj}
+    exec("\n".join(src), ns)  # noqa: S102 - source built above from the class's own field names
+    f = ns["_to_obj"]
+    f.__qualname__ = f"{cls.__qualname__}.to_obj"
+    f._lwc_generated = True
+    return f
+
+
 class Wire(BaseModel):
     model_config = ConfigDict(extra="ignore", populate_by_name=True, validate_assignment=False,
                               protected_namespaces=())
     __keep_none__: ClassVar[FrozenSet[str]] = frozenset()
     __flatten__: ClassVar[FrozenSet[str]] = frozenset()
 
+    @classmethod
+    def __pydantic_init_subclass__(cls, **kw):
+        super().__pydantic_init_subclass__(**kw)
+        # classes that do not override to_obj get their generated one as the method itself; overrides
+        # reach it through super().to_obj() -> Wire.to_obj
+        # (compiled on first use: the field annotations of classes with forward references resolve later)
+        cur = cls.to_obj
+        if cur is Wire.to_obj or getattr(cur, "_lwc_generated", False):
+            def first_use(self, cls=cls):
+                f = _GEN.get(cls)
+                if f is None:
+                    f = _GEN[cls] = _compile_to_obj(cls)
+                cls.to_obj = f
+                return f(self)
+            first_use._lwc_generated = True
+            cls.to_obj = first_use
+
     def to_obj(self) -> dict:
-        out: dict = {}
-        d = self.__dict__
-        for name, key, keep, flat in _plan(type(self)):
-            v = d[name]
-            if v is None:
-                if keep:
-                    out[key] = None
-                continue
-            if isinstance(v, _IMMUTABLE):
-                out[key] = v
-            elif isinstance(v, Wire):
-                if flat:
-                    out.update(v.to_obj())
-                else:
-                    out[key] = v.to_obj()
-            else:
-                out[key] = to_obj(v)
-        extra = self.__pydantic_extra__
-        if extra:
-            out.update({k: to_obj(x) for k, x in extra.items()})
-        return out
+        cls = type(self)
+        f = _GEN.get(cls)
+        if f is None:
+            f = _GEN[cls] = _compile_to_obj(cls)
+        return f(self)
 
     def to_json(self) -> str:
         return sjson.dumps(self.to_obj())

@@ -69,7 +69,10 @@ def main():
         pr.disable()
         import pstats
 
-        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+        st = pstats.Stats(pr)
+        st.sort_stats("tottime").print_stats(30)
+        if "--callers" in sys.argv:
+            st.print_callers("main.py:253")
     print(f"front end: {n / el:.1f} score requests/s ({el / n * 1e3:.2f} ms wall, {cpu / n * 1e3:.2f} ms process CPU "
           f"per request, 8 voters x 16 tokens)")
 

@@ -60,3 +60,46 @@ def test_merge_extends_logprobs_in_place_without_aliasing_the_source():
     agg.push(b.clone())
     assert agg.delta.content == "abb" and [x.token for x in agg.logprobs.content] == ["a", "b", "b"]
     assert [x.token for x in a.logprobs.content] == ["a"] and [x.token for x in b.logprobs.content] == ["b"]
+
+
+def _loop_to_obj(v):
+    """The plain field-plan walk the generated per-class to_obj replaces (same output required)."""
+    from llm_weighted_consensus_amd.schema.base import _IMMUTABLE, Wire, _plan
+    if isinstance(v, Wire):
+        out = {}
+        for name, key, keep, flat in _plan(type(v)):
+            x = v.__dict__[name]
+            if x is None:
+                if keep:
+                    out[key] = None
+            elif isinstance(x, Wire) and flat:
+                out.update(_loop_to_obj(x))
+            else:
+                out[key] = x if isinstance(x, _IMMUTABLE) else _loop_to_obj(x)
+        return out
+    if isinstance(v, (list, tuple)):
+        return [_loop_to_obj(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _loop_to_obj(x) for k, x in v.items()}
+    return v
+
+
+def test_generated_to_obj_matches_the_field_walk():
+    from llm_weighted_consensus_amd.schema import score as S
+    from llm_weighted_consensus_amd.schema.base import Wire
+    lp = C.Logprobs(content=[C.Logprob(token="a", bytes=[97], logprob=-0.1,
+                                       top_logprobs=[C.TopLogprob(token="b", bytes=None, logprob=-1.0)])])
+    chunk = C.ChatCompletionChunk(id="x", created=1, model="m", choices=[
+        C.StreamChoice(delta=C.Delta(content="hi", role="assistant"), index=0, logprobs=lp, finish_reason="stop")])
+    assert chunk.to_obj() == _loop_to_obj(chunk)
+    sc = S.ScoreStreamChoice(delta=S.ScoreDelta(content="k"), index=2, weight=1.5, model="v", model_index=0)
+    got = sc.to_obj()
+    assert got["finish_reason"] is None and "error" not in got  # keep-none and the override still apply
+    # a list field assigned a tuple after validation, and a subclass with its own extra field
+    lp.content[0].bytes = (97,)
+    assert lp.to_obj()["content"][0]["bytes"] == [97]
+
+    class Extended(C.Delta):
+        extra_note: str = "n"
+    assert Extended(content="c").to_obj() == dict(_loop_to_obj(Extended(content="c")), extra_note="n")
+    assert isinstance(Extended(content="c"), Wire) and "extra_note" not in C.Delta(content="c").to_obj()
