@@ -175,8 +175,8 @@ def main():
                 "prompt_len": a.prompt_len,
                 "gen_len": a.gen_len,
                 "sampling": "temperature 0.8, top_p 0.95",
-                "parallelism": (f"cp{cp} x dp{W // cp}: candidate-parallel groups of {cp} GPUs (RCCL all-gather of "
-                                f"prompt KV + embeddings inside a group), request-parallel across groups"
+                "parallelism": (f"cp{cp} x dp{W // cp}: candidate-parallel groups of {cp} GPUs (all-gather of prompt KV "
+                                f"+ embeddings inside a group over {info.backend}), request-parallel across groups"
                                 if W > 1 else "single GPU"),
             },
         }
