@@ -12,6 +12,9 @@ rc=$?; echo "rocprof rc=$rc"; tail -5 gpurun_out/prof_bench.log
 STATS=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
 [ -n "$STATS" ] && python3 scripts/summarize_profile.py "$STATS" "bench.py $ARGS (rocprofv3 --kernel-trace --stats)" \
     gpurun_out/prof_summary.md > /dev/null
+# GPU idle gaps (host stalls) over the whole run, before the trace is dropped
+TRACE=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
+[ -n "$TRACE" ] && python3 scripts/trace_gaps.py "$TRACE" ${GAP_MS:-0.2} > gpurun_out/prof_gaps.txt
 # keep the stats, drop the multi-MB per-dispatch trace (gpurun copies back <= 64 MiB)
 find gpurun_out/prof -name "*kernel_trace.csv" -delete
 exit $rc
