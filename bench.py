@@ -97,7 +97,12 @@ def main():
     scorer = EmbeddingConsensus(encoder, tau=0.05, max_tokens=512)
     gen = torch.Generator().manual_seed(99)
 
-    def one_step(step_idx: int):
+    defer = not a.profile_steps  # the per-phase breakdown needs the score phase synchronised
+
+    def one_step(step_idx: int, prev=None):
+        """Serve one step's requests.  The consensus of the step is returned DEFERRED (its answer indices
+        still on the device): the host goes straight on to the next step's admission while the GPU runs
+        the encoder, and ``prev`` (the previous step's result) is read back once that admission is queued."""
         # identical synthetic prompts on every rank (same generator)
         all_prompts = [torch.randint(0, dcfg.vocab_size, (a.prompt_len,), generator=gen).tolist() for _ in range(G)]
         prompts = all_prompts[gidx * Rg:(gidx + 1) * Rg]  # this candidate group's requests
@@ -113,26 +118,35 @@ def main():
             sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True,
                                 seed=(step_idx * 1000003 + gidx * Rg + gi) * 131 + crank)
             groups.append(engine.add_request(p, sp, n=n_local, prefilled=shared[gi] if shared else None))
+        if prev is not None:
+            prev.resolve()
         while engine.has_work():
             engine.step()
         t1 = time.perf_counter()
         cands = [[s.tokens for s in g.seqs] for g in groups]
-        res = scorer.score(cands, gather=cp > 1, group=cgroup)
-        torch.cuda.synchronize(dev)
+        res = scorer.score(cands, gather=cp > 1, group=cgroup, defer=defer)
+        if not defer:
+            torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         return res, t1 - t0, t2 - t1
 
+    res = None
     for i in range(a.warmup):
-        one_step(i)
+        res = one_step(i, res)[0]
+    if res is not None:
+        res.resolve()
     torch.cuda.synchronize(dev)
     pdist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     gen_t = score_t = 0.0
+    res = None
     for i in range(a.steps):
-        res, tg, ts = one_step(a.warmup + i)
+        res, tg, ts = one_step(a.warmup + i, res)
         gen_t += tg
         score_t += ts
+    if res is not None:
+        res.resolve()  # every timed step's answers are on the host before the clock stops
     torch.cuda.synchronize(dev)
     pdist.barrier()
     torch.cuda.synchronize(dev)

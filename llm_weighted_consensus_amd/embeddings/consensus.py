@@ -31,6 +31,14 @@ class ConsensusResult:
     partial: bool = False
     candidate_offset: int = 0
 
+    def resolve(self) -> "ConsensusResult":
+        """A deferred result (``score(..., defer=True)``) holds ``best`` as a device tensor so the host can
+        queue more work before waiting for the encoder; this reads it back (one sync) as a list."""
+        if isinstance(self.best, torch.Tensor):
+            off = self.candidate_offset if self.partial else 0
+            self.best = [b + off for b in self.best.tolist()]
+        return self
+
 
 def consensus_reference(E: torch.Tensor, tau: float) -> ConsensusResult:
     """fp32 torch form of K10a (CPU plumbing path and the numerics oracle)."""
@@ -61,17 +69,18 @@ class EmbeddingConsensus:
     def embed(self, candidates: Sequence[Sequence[int]]):
         return self.encoder.embed(candidates, self.max_tokens)
 
-    def score_local(self, E: torch.Tensor) -> ConsensusResult:
-        """E: [R, N, d] unit rows (bf16 on the GPU: the MFMA kernel; any dtype on CPU: torch math)."""
+    def score_local(self, E: torch.Tensor, defer: bool = False) -> ConsensusResult:
+        """E: [R, N, d] unit rows (bf16 on the GPU: the MFMA kernel; any dtype on CPU: torch math).
+        ``defer``: leave ``best`` on the device (no host sync; call ``resolve()`` later)."""
         if E.is_cuda:
             S, cen, w, best = ops.cosine_consensus(E, self.tau)
-            return ConsensusResult(best.tolist(), w, cen, S)
+            return ConsensusResult(best if defer else best.tolist(), w, cen, S)
         return consensus_reference(E, self.tau)
 
     def score(self, requests: Sequence[Sequence[Sequence[int]]], gather: bool = False,
-              group=None) -> ConsensusResult:
+              group=None, defer: bool = False) -> ConsensusResult:
         """requests[r][i] = token ids of candidate i of request r (this rank's shard when gather=True;
-        every rank must hold the same R and the same shard size)."""
+        every rank must hold the same R and the same shard size).  ``defer``: see :meth:`score_local`."""
         R = len(requests)
         n_local = len(requests[0])
         flat = [c for req in requests for c in req]
@@ -87,8 +96,9 @@ class EmbeddingConsensus:
             E = pdist.guarded(gather_candidates, E, group, fallback=lambda: lost.append(1) or E)
             if lost:
                 partial, offset = True, crank * n_local
-        res = self.score_local(E.contiguous())
+        res = self.score_local(E.contiguous(), defer=defer)
         if partial:
             res.partial, res.candidate_offset = True, offset
-            res.best = [b + offset for b in res.best]
+            if not isinstance(res.best, torch.Tensor):
+                res.best = [b + offset for b in res.best]
         return res

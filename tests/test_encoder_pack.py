@@ -35,3 +35,12 @@ def test_pack_matches_per_token_loop():
         rid, rpos, rcu = _loop_pack(tls, 12, 100)
         assert ids.tolist() == rid and pos.tolist() == rpos and cu.tolist() == rcu
         assert mx == max(b - a for a, b in zip(rcu, rcu[1:]))
+
+
+def test_deferred_consensus_result_resolves_with_the_shard_offset():
+    from llm_weighted_consensus_amd.embeddings.consensus import ConsensusResult
+    z = torch.zeros(2, 4)
+    r = ConsensusResult(torch.tensor([1, 3]), z, z, z)
+    assert r.resolve().best == [1, 3] and r.resolve().best == [1, 3]  # idempotent
+    p = ConsensusResult(torch.tensor([1, 3]), z, z, z, partial=True, candidate_offset=4)
+    assert p.resolve().best == [5, 7]

@@ -435,6 +435,11 @@ def test_pool_cosine(gpu):
     _close(cen, cr, 2e-3, 1e-2)
     _close(w, torch.softmax(cr / 0.1, -1), 2e-3, 2e-2)
     assert torch.equal(best.long(), cr.argmax(-1))
+    # the bench's deferred form: answer indices stay on the device until resolve()
+    from llm_weighted_consensus_amd.embeddings.consensus import EmbeddingConsensus
+    sc = EmbeddingConsensus(encoder=None, tau=0.1)
+    lazy = sc.score_local(E, defer=True)
+    assert isinstance(lazy.best, torch.Tensor) and lazy.resolve().best == sc.score_local(E).best == cr.argmax(-1).tolist()
 
 
 def test_kv_block_copy(gpu):
