@@ -11,7 +11,7 @@ RCCL all-gather (C1) assembles [requests, N, d] on every rank before the (tiny) 
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Union
 
 import torch
 
@@ -21,7 +21,8 @@ from ..parallel import dist as pdist
 
 @dataclass
 class ConsensusResult:
-    best: List[int]                 # per request: index of the consensus candidate
+    best: Union[List[int], torch.Tensor]  # per request: index of the consensus candidate (device tensor until
+                                          # resolve() when the result was deferred)
     weights: torch.Tensor           # [R, N] softmax(centrality / tau)
     centrality: torch.Tensor        # [R, N]
     similarity: torch.Tensor        # [R, N, N]
