@@ -20,10 +20,17 @@
 //      (16 B vector stores over xGMI)
 //   3. every storing wave drains its stores (vmcnt 0), workgroup barrier, one lane: system-scope
 //      release fence, then flags[me][b] = e in every peer region (system-scope atomic store)
-//   4. lanes 0..W-1 poll this rank's flags[p][b] == e (system-scope atomic loads, bounded spin with
-//      s_sleep; on timeout an error word is set and the block stops waiting), workgroup barrier
+//   4. lanes 0..W-1 poll this rank's flags[p][b] until it is AT LEAST e (system-scope atomic loads,
+//      bounded spin with s_sleep), workgroup barrier.  "At least", not "equal": a fast peer may finish
+//      call e and publish call e+1's flag into this region before this rank's poller has read e — the
+//      call-e data slot is still intact then (the peer's call-e+1 push goes to the other parity slot and
+//      its call-e+2 push waits for this rank's call-e+1 flag).
 //   5. SUM in RANK ORDER (p = 0..W-1, this rank's own term read from x) in fp32, bf16 result to out —
 //      the same summation order on every rank, so all ranks hold bitwise-identical activations.
+// Failure: a poller that exceeds the spin bound (a dead, hung or desynchronised peer) sets the sticky
+// error word AND the block writes NaN over its whole output range instead of summing a slot that may
+// hold stale data — downstream logits are poisoned, never silently wrong; the host reads the error word
+// asynchronously one step later (parallel/allreduce.py) and fails the in-flight requests.
 // Reuse safety: parity double-buffering.  Rank r writes slot (e&1) of call e only after its call e-1
 // block b saw every peer's call-(e-1) flag, which each peer set after finishing ALL of call e-2 (stream
 // order) — the last reads of that slot.  Flags are monotonic epochs: nothing is reset between calls.
@@ -40,7 +47,7 @@ constexpr size_t kFlagsOff = 0;
 constexpr size_t kEpochOff = (size_t)kMaxRanks * kMaxBlocks * 4;  // 32 KiB
 constexpr size_t kDataOff = 64 * 1024;
 constexpr int kThreads = 512;
-constexpr long long kSpinLimit = 1LL << 26;  // x s_sleep(2) (~60 ns): ~4 s, far past any healthy peer
+constexpr long long kDefaultSpinLimit = 1LL << 26;  // x s_sleep(2) (~60 ns): ~4 s, far past any healthy peer
 
 struct Params {
   uint8_t* base[kMaxRanks];  // every rank's region as mapped in THIS process (base[me] = own)
@@ -49,6 +56,7 @@ struct Params {
   int* err;                  // device error word (0 = ok; 1 = a peer never arrived)
   long long n;               // elements (multiple of 8)
   long long cap;             // bytes per data slot
+  long long spin_limit;      // poll iterations (each ~60 ns) before a peer is declared missing
   int me, W;
 };
 
@@ -86,14 +94,18 @@ __global__ void __launch_bounds__(kThreads) allreduce_kernel(Params p) {
     for (int q = 0; q < p.W; ++q)
       if (q != p.me) __hip_atomic_store(flags_of(p.base[q], p.me, b), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 4. wait for every peer's block b of this call
+  // 4. wait for every peer's block b of this call (flags only grow: wait until flag >= e)
+  __shared__ int missing;
+  if (t == 0) missing = 0;
+  __syncthreads();
   if (t < p.W && t != p.me) {
     const int* f = flags_of(mine, t, b);
     long long spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit) {
+      if (++spins > p.spin_limit) {
         __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        missing = 1;
         break;
       }
     }
@@ -101,8 +113,14 @@ __global__ void __launch_bounds__(kThreads) allreduce_kernel(Params p) {
   __syncthreads();
   if (t == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
-  // 5. sum in rank order
   uint4v* ov = reinterpret_cast<uint4v*>(p.out);
+  if (missing) {  // a peer never arrived: poison this block's range, never sum a possibly stale slot
+    const uint32_t nan2 = 0x7FC07FC0u;  // two bf16 quiet NaNs
+    for (long long v = v0 + t; v < v1; v += kThreads) ov[v] = uint4v{nan2, nan2, nan2, nan2};
+    if (t == 0) __hip_atomic_store(epoch_p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // 5. sum in rank order
   for (long long v = v0 + t; v < v1; v += kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -151,8 +169,9 @@ extern "C" int lwc_ar_free(void* ptr) { return (int)hipFree(ptr); }
 extern "C" int lwc_ar_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 // out = sum over ranks of x (bf16 [n], n % 8 == 0, 2n <= cap); `bases` = W region pointers as mapped here.
+// spin_limit <= 0: the default bound (~4 s).
 extern "C" int lwc_allreduce(void* const* bases, int me, int W, const void* x, void* out, long long n, long long cap,
-                             int* err, int blocks, hipStream_t s) {
+                             int* err, int blocks, long long spin_limit, hipStream_t s) {
   using namespace lwc::ar;
   if (W < 1 || W > kMaxRanks || me < 0 || me >= W || n % 8 != 0 || 2 * n > cap) return -1;
   if (blocks < 1 || blocks > kMaxBlocks) return -2;
@@ -164,6 +183,7 @@ extern "C" int lwc_allreduce(void* const* bases, int me, int W, const void* x, v
   p.err = err;
   p.n = n;
   p.cap = cap;
+  p.spin_limit = spin_limit > 0 ? spin_limit : kDefaultSpinLimit;
   p.me = me;
   p.W = W;
   allreduce_kernel<<<blocks, kThreads, 0, s>>>(p);

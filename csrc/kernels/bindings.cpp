@@ -43,7 +43,7 @@ int lwc_ar_open(const void*, void**);
 int lwc_ar_close(void*);
 int lwc_ar_free(void*);
 int lwc_ar_handle_bytes();
-int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long long, int*, int, hipStream_t);
+int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long long, int*, int, long long, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
 }
@@ -511,7 +511,7 @@ void ar_free(int64_t ptr) { (void)lwc_ar_free(reinterpret_cast<void*>(ptr)); }
 int64_t ar_region_bytes(int64_t W, int64_t cap) { return lwc_ar_region_bytes((int)W, cap); }
 
 void allreduce(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& x, at::Tensor& out, int64_t cap,
-               at::Tensor& err, int64_t blocks) {
+               at::Tensor& err, int64_t blocks, int64_t spin_limit) {
   CHECK_BF16(x); CHECK_BF16(out); CHECK_CONTIG(x); CHECK_CONTIG(out);
   CHECK_DTYPE(err, at::kInt);
   TORCH_CHECK(x.numel() == out.numel(), "allreduce: x / out size mismatch");
@@ -519,7 +519,7 @@ void allreduce(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& 
   std::vector<void*> b;
   for (int64_t v : bases) b.push_back(reinterpret_cast<void*>(v));
   CHECK_RC(lwc_allreduce(b.data(), (int)me, (int)b.size(), x.data_ptr(), out.data_ptr(), x.numel(), cap,
-                         err.data_ptr<int>(), (int)blocks, cur_stream()),
+                         err.data_ptr<int>(), (int)blocks, (long long)spin_limit, cur_stream()),
            "allreduce");
 }
 

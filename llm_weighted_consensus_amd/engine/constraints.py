@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import bisect
 import hashlib
+import itertools
 import json
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
@@ -63,14 +64,19 @@ def _trie(options: Sequence[bytes]) -> Dict:
 # Content ids of segment-list suffixes: equal ids <=> the same remaining grammar, whichever constraint
 # instance (voter, request) it belongs to — the key of the cross-request token-mask cache.
 _SUFFIX_IDS: Dict[tuple, int] = {}
+_SUFFIX_LIMIT = 1 << 16
+# Ids come from an ever-increasing counter and are never reused: when the table is bounded by a clear,
+# a grammar seen afterwards gets a FRESH id, so no mask cached under an old id (TokenVocab.masks, keyed by
+# (suffix id, local state)) and no live constraint holding an old id can ever alias a different grammar.
+_SUFFIX_NEXT = itertools.count(1)
 
 
 def _suffix_id(desc: tuple) -> int:
     v = _SUFFIX_IDS.get(desc)
     if v is None:
-        if len(_SUFFIX_IDS) > 1 << 16:
+        if len(_SUFFIX_IDS) >= _SUFFIX_LIMIT:
             _SUFFIX_IDS.clear()
-        v = _SUFFIX_IDS[desc] = len(_SUFFIX_IDS) + 1
+        v = _SUFFIX_IDS[desc] = next(_SUFFIX_NEXT)
     return v
 
 
@@ -94,6 +100,11 @@ class SegmentConstraint:
             d = ("L", seg.data) if isinstance(seg, Lit) else ("S", seg.max_len) if isinstance(seg, Str) \
                 else ("A", tuple(sorted(seg.options)))
             nxt = self.suffix_ids[i] = _suffix_id((d, nxt, eos_id))
+
+    def __reduce__(self):
+        # suffix ids are process-local (this process's counter): a copy shipped to an EngineGroup worker
+        # re-derives them there from the grammar, so they never alias ids the worker assigned itself
+        return (SegmentConstraint, (self.segments, self.eos_id))
 
     # ---- FSM
     def start(self):

@@ -864,6 +864,9 @@ class LLMEngine:
         if copies:
             self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
         self._ensure_graph(bk)
+        arm = getattr(self.model, "comm_arm", None)
+        if arm is not None:
+            arm()  # TP: error word of this step's all-reduces -> pinned host memory, read one step later
         step = _Step(seqs, key, bk, parity, st["K"], None, None, None)
         step.static = st
         self.stats["decode_tokens"] += B
@@ -939,6 +942,9 @@ class LLMEngine:
 
     def _process(self, st: _Step) -> List[TokenEvent]:
         st.event.synchronize()
+        poll = getattr(self.model, "comm_poll", None)
+        if poll is not None:
+            poll()  # a TP peer that never arrived: CommFailure fails the in-flight groups (EngineService)
         if st.first is not None:  # first tokens after a prefill (:meth:`_launch_first`)
             host, groups = st.first
             lists = [h.tolist() for h in host]

@@ -151,7 +151,10 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                     if rid is not None:
                         ev_q.put(("error", wid, (rid, f"{type(e).__name__}: {e}")))
         if batch:
-            if ring is None or not ring.push(encode_events(batch)):
+            def beat():
+                hb.value = time.time()
+
+            if ring is None or not ring.push(encode_events(batch), timeout=5.0, on_wait=beat):
                 ev_q.put(("tokens", wid, batch))  # no ring (or the reader is gone): the slow path
             batch = []
         for rid in [r for r, g in groups.items() if g.finished]:
@@ -275,6 +278,8 @@ class EngineGroup:
             if p.is_alive():
                 p.kill()
         self._reader.join(timeout=5)
+        if self._reader.is_alive():  # still inside a pop: leave the segments to process exit, never
+            return                   # unmap them under a running reader
         for r in self.rings:
             r.close()
         self.rings = []

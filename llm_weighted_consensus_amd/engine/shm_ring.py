@@ -53,8 +53,10 @@ class ShmRing:
         return self.shm.name
 
     # ---- producer
-    def push(self, payload, timeout: float = 30.0) -> bool:
-        """Append one record (blocks while the ring is full, up to ``timeout`` s; False on timeout)."""
+    def push(self, payload, timeout: float = 30.0, on_wait=None) -> bool:
+        """Append one record (blocks while the ring is full, up to ``timeout`` s; False on timeout).
+        ``on_wait`` is called about every 50 ms while waiting (the worker refreshes its heartbeat: a slow
+        reader is not a dead worker)."""
         mv = memoryview(payload).cast("B")
         n = len(mv)
         need = (4 + n + 7) // 8 * 8
@@ -76,14 +78,20 @@ class ShmRing:
                 self._data[pos + 4:pos + 4 + n] = np.frombuffer(mv, np.uint8)
                 self._hdr[0] = head + need  # publish after the bytes
                 return True
+            now = time.monotonic()
             if deadline is None:
-                deadline = time.monotonic() + timeout
-            elif time.monotonic() > deadline:
+                deadline, beat = now + timeout, now
+            elif now > deadline:
                 return False
+            if on_wait is not None and now - beat > 0.05:
+                on_wait()
+                beat = now
             time.sleep(0.0002)
 
     # ---- consumer
     def pop(self) -> Optional[bytes]:
+        if self._hdr is None:  # closed
+            return None
         while True:
             head, tail = int(self._hdr[0]), int(self._hdr[1])
             if head == tail:

@@ -249,6 +249,12 @@ class LlamaModel:
             return ops.silu_mul(F.linear(h, L.w_gate_up), block=L.gu_block)
         return gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
 
+    def comm_arm(self) -> None:
+        """Tensor-parallel subclasses queue the readback of their collective's error word here."""
+
+    def comm_poll(self) -> None:
+        """Tensor-parallel subclasses raise here once a failed collective is visible on the host."""
+
     def tune_gemms(self, M: int) -> None:
         """Pick the GEMM backend of every decode projection at batch M by timing both (before the
         bucket's hipGraph is captured; see ops/gemm_plan.py)."""

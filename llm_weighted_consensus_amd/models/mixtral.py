@@ -179,6 +179,16 @@ class MixtralModel(LlamaModel):
             pdist.all_reduce_(x, group=self.tp_group)
         return x
 
+    def comm_arm(self) -> None:
+        """Queue the asynchronous readback of the TP all-reduce's error word (after a step's launch)."""
+        if self.tp_comm is not None and hasattr(self.tp_comm, "arm"):
+            self.tp_comm.arm()
+
+    def comm_poll(self) -> None:
+        """Raise parallel.allreduce.CommFailure if a completed readback shows a peer never arrived."""
+        if self.tp_comm is not None and hasattr(self.tp_comm, "poll"):
+            self.tp_comm.poll()
+
     @property
     def graph_safe(self) -> bool:
         """Whether a decode step may be captured in a hipGraph: every collective inside it must be a

@@ -12,9 +12,17 @@ latency and graph capture (RCCL's eager call is ~20-40 us host-side per call, 64
 
 The reference has no tensor parallelism (it runs no model); this serves BASELINE config 5 (Mixtral
 TP=2) in place of the round-1 eager ``dist.all_reduce``.
+
+Failure: a peer that does not arrive within the spin bound (``spin_ms``, env ``LWC_AR_SPIN_MS``; the
+kernel's default is ~4 s) makes the waiting rank poison its output with NaN and set a sticky device
+error word — never sum a stale slot.  The engine reads that word without a host sync: :meth:`arm` queues
+a copy of it into pinned memory behind each decode step, and :meth:`poll` (called once the step's
+outputs are on the host, i.e. one step later) raises :class:`CommFailure`, which fails the in-flight
+requests (``EngineService`` -> ``EngineFailure``) instead of letting NaN logits decode on.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -23,11 +31,21 @@ import torch.distributed as dist
 from .. import ops
 
 
+class CommFailure(RuntimeError):
+    """A tensor-parallel peer never arrived at an all-reduce (spin bound exceeded)."""
+
+
+# one poll iteration of the kernel's wait loop is an s_sleep(2) plus a system-scope load: ~60 ns
+_NS_PER_SPIN = 60
+
+
 class CustomAllReduce:
-    def __init__(self, group=None, device=None, max_bytes: int = 64 << 20, blocks: int = 128):
+    def __init__(self, group=None, device=None, max_bytes: int = 64 << 20, blocks: int = 128,
+                 spin_ms: Optional[float] = None):
         """Collective: every rank of ``group`` (default: the world) must construct it together.
         ``max_bytes``: largest bf16 payload per call; ``blocks``: workgroups per launch (must be equal on
-        every rank — block b of every rank reduces the same range)."""
+        every rank — block b of every rank reduces the same range); ``spin_ms``: how long a rank waits for
+        a peer before it declares it missing (default ``LWC_AR_SPIN_MS`` or the kernel's ~4 s)."""
         self.group = group
         self.W = dist.get_world_size(group)
         self.me = dist.get_rank(group)
@@ -53,6 +71,13 @@ class CustomAllReduce:
                     bases.append(p)
         self.bases = bases
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if spin_ms is None and os.environ.get("LWC_AR_SPIN_MS"):
+            spin_ms = float(os.environ["LWC_AR_SPIN_MS"])
+        self.spin_limit = 0 if spin_ms is None else max(1, int(spin_ms * 1e6 / _NS_PER_SPIN))
+        # asynchronous error readback: two pinned words (alternating steps) + the event after each copy
+        self._err_host = torch.zeros(2, dtype=torch.int32, pin_memory=self.device.type == "cuda")
+        self._err_ev: List[Optional[torch.cuda.Event]] = [None, None]
+        self._arm_no = 0
         if dist.get_backend(group) == "nccl":
             dist.barrier(group=group, device_ids=[self.device.index])
         else:
@@ -69,13 +94,36 @@ class CustomAllReduce:
         step = self.cap // 2
         for a in range(0, flat.numel(), step):  # payloads beyond one slot (large prefills): in slot-sized pieces
             piece = flat[a:a + step]
-            k.allreduce(self.bases, self.me, piece, piece, self.cap, self.err, self.blocks)
+            k.allreduce(self.bases, self.me, piece, piece, self.cap, self.err, self.blocks, self.spin_limit)
         return x
+
+    def arm(self) -> None:
+        """Queue an asynchronous copy of the error word behind the work queued so far (call after each
+        decode step's launch, outside graph capture); :meth:`poll` reads it later without a sync."""
+        if self.W == 1:
+            return
+        i = self._arm_no & 1
+        self._arm_no += 1
+        self._err_host[i:i + 1].copy_(self.err, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._err_ev[i] = ev
+
+    def poll(self) -> None:
+        """Raise :class:`CommFailure` if an armed copy that has completed shows a failed call (never
+        blocks: a copy still in flight is read by a later poll)."""
+        for i in (0, 1):
+            ev = self._err_ev[i]
+            if ev is not None and ev.query():
+                self._err_ev[i] = None
+                if int(self._err_host[i]):
+                    raise CommFailure("CustomAllReduce: a tensor-parallel peer never arrived (spin bound "
+                                      "exceeded); the step's activations were poisoned with NaN")
 
     def check(self) -> None:
         """Raise if any call so far timed out waiting for a peer (host sync; not for the hot path)."""
         if int(self.err.item()):
-            raise RuntimeError("CustomAllReduce: a peer never arrived (spin timeout)")
+            raise CommFailure("CustomAllReduce: a peer never arrived (spin timeout)")
 
     def close(self) -> None:
         k = ops.kernels()

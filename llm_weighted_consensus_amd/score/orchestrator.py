@@ -276,9 +276,9 @@ class ScoreClient:
             finally:
                 await q.put(DONE)
 
-        # key-tree seeds drawn for every voter in model order (whichever of them this client runs), so a
+        # key-tree seeds for every voter in model order (whichever of them this client runs), so a
         # voter's prompt does not depend on how the voters are sharded
-        seeds = [self.rng.getrandbits(63) for _ in model.llms]
+        seeds = self._voter_seeds(ctx, model)
         tasks = [asyncio.create_task(run_voter(l, seeds[j])) for j, l in enumerate(model.llms)
                  if self.voter_filter is None or self.voter_filter(l)]
         pending = len(tasks)
@@ -339,6 +339,16 @@ class ScoreClient:
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+
+    def _voter_seeds(self, ctx, model: Model) -> List[int]:
+        """One key-tree seed per voter, in model order.  A request context carrying ``seed`` (the
+        voter-sharded client: identical on every rank) derives them from it; otherwise they are drawn
+        from this client's generator."""
+        base = ctx.get("seed") if isinstance(ctx, dict) else None
+        if base is not None:
+            r = random.Random(int(base))
+            return [r.getrandbits(63) for _ in model.llms]
+        return [self.rng.getrandbits(63) for _ in model.llms]
 
     def _new_ids(self, ctx=None):
         created = int(time.time())

@@ -95,10 +95,17 @@ class ShardedScoreClient(ScoreClient):
         self.world = dist.get_world_size(self.group)
         self.rank = dist.get_rank(self.group)
         self.voter_filter = lambda llm: llm.index % self.world == self.rank
-        # one key-tree seed stream on every rank (rank 0's): a voter's prompt does not depend on its rank
-        self.rng.seed(V.broadcast_object(self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"],
-                                         0, self.group))
+        # one key-tree seed base on every rank (rank 0's); each request's voter seeds derive from (base,
+        # request number) — not from draws in arrival order, which concurrent requests make rank-dependent
+        self.seed_base = int(V.broadcast_object(
+            self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"], 0, self.group))
+        self.rng.seed(self.seed_base)
         self.combiner = _Combiner(self.group)
+
+    def request_ctx(self, seq: int, ids) -> dict:
+        """The per-request context every rank builds identically: sequence number (combine order), the
+        response ids, and the voters' key-tree seed base."""
+        return {"seq": seq, "ids": ids, "seed": (self.seed_base * 1000003 + seq) & ((1 << 63) - 1)}
 
     def _new_ids(self, ctx=None):
         return tuple(ctx["ids"])
@@ -129,12 +136,34 @@ class ShardedScoreClient(ScoreClient):
 
     async def run(self, seq: int, ids, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
         """One request on this rank (unary); always takes its combine slot."""
-        ctx = {"seq": seq, "ids": ids}
+        ctx = self.request_ctx(seq, ids)
         try:
             return await self.create_unary(ctx, request)
         finally:
             if not ctx.get("combined"):
                 await self.combiner.submit(seq, _SKIP)
+
+    async def open_stream(self, seq: int, ids, request: S.ScoreCompletionCreateParams):
+        """One request on this rank, streamed: pre-stream errors raise here (the HTTP layer turns them
+        into a status), then this rank's voter chunks are yielded as they arrive, and the final chunk
+        carries the other ranks' voters whole plus the tally (the unary fold of the stream equals
+        :meth:`run`).  The combine slot is always taken, also when the client abandons the stream."""
+        ctx = self.request_ctx(seq, ids)
+        try:
+            it = await self.create_streaming(ctx, request)
+        except BaseException:
+            await self.combiner.submit(seq, _SKIP)
+            raise
+
+        async def gen():
+            try:
+                async for item in it:
+                    yield item
+            finally:
+                if not ctx.get("combined"):
+                    await self.combiner.submit(seq, _SKIP)
+
+        return gen()
 
     def close(self) -> None:
         self.combiner.close()
@@ -147,20 +176,27 @@ class ShardedScoreClient(ScoreClient):
 class ScoreLeader:
     """Rank 0's score client in a voter-sharded deployment (``LWC_SHARD_VOTERS=1``): every score
     request is numbered and broadcast to the follower ranks (control group), then run here like on the
-    followers — concurrently with the other requests in flight.  Streaming requests get the merged
-    response as one chunk.  Everything else (model validation for multichat, ...) is the wrapped
-    client's."""
+    followers — concurrently with the other requests in flight.  Streaming requests stream this rank's
+    voters live, then the other ranks' voters and the tally in the final chunk.  Everything else (model
+    validation for multichat, ...) is the wrapped client's.
+
+    The broadcast is a blocking gloo call: it runs on ONE dedicated thread (FIFO, so request numbers are
+    assigned and broadcast in submission order), never on the event loop, which keeps serving while a
+    slow follower holds a broadcast."""
 
     def __init__(self, client: ShardedScoreClient, control=None):
+        from concurrent.futures import ThreadPoolExecutor
+
         self.client = client
         self.control = control if control is not None else dist.new_group(backend="gloo")
         self._seq = 0
         self._lock = threading.Lock()
+        self._announcer = ThreadPoolExecutor(max_workers=1, thread_name_prefix="c2-announce")
 
     def __getattr__(self, name):
         return getattr(self.client, name)
 
-    def _announce(self, request) -> tuple:
+    def _announce_sync(self, request) -> tuple:
         with self._lock:
             seq = self._seq
             self._seq += 1
@@ -168,36 +204,21 @@ class ScoreLeader:
             V.broadcast_object((seq, ids, request), 0, self.control)
         return seq, ids
 
+    async def _announce(self, request) -> tuple:
+        return await asyncio.get_running_loop().run_in_executor(self._announcer, self._announce_sync, request)
+
     async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
-        seq, ids = self._announce(request)
+        seq, ids = await self._announce(request)
         return await self.client.run(seq, ids, request)
 
     async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams):
-        out = await self.create_unary(ctx, request)
-
-        async def one():
-            yield as_chunk(out)
-
-        return one()
+        seq, ids = await self._announce(request)
+        return await self.client.open_stream(seq, ids, request)
 
     def close(self) -> None:
+        self._announcer.shutdown(wait=True)
         V.broadcast_object(None, 0, self.control)
         self.client.close()
-
-
-def as_chunk(out: S.ScoreCompletion) -> S.ScoreCompletionChunk:
-    from .choices import message_to_delta
-
-    choices = []
-    for c in out.choices:
-        delta = message_to_delta(c.message)
-        delta.vote = c.message.vote
-        choices.append(S.ScoreStreamChoice(
-            delta=delta, finish_reason=c.finish_reason, index=c.index, logprobs=c.logprobs, weight=c.weight,
-            confidence=c.confidence, error=c.error, model=c.model, model_index=c.model_index,
-            completion_metadata=c.completion_metadata))
-    return S.ScoreCompletionChunk(id=out.id, choices=choices, created=out.created, model=out.model, usage=out.usage,
-                                  weight_data=out.weight_data)
 
 
 def follow(client: ShardedScoreClient, control=None) -> int:

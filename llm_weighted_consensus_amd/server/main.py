@@ -90,6 +90,16 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                     embedders=embedders, services=services, archive=archive, registry=registry)
 
 
+def follower_config(cfg: Config, rank: int) -> Config:
+    """Voter-sharded ranks above 0 persist nothing: rank 0 alone appends the completions archive and the
+    training table (every rank sees the same env config; followers writing the same JSONL files would
+    store each completion again, interleave long lines, and replay each training row once per rank)."""
+    if rank > 0:
+        cfg.archive_path = None
+        cfg.training_table_path = None
+    return cfg
+
+
 def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     """LWC_SHARD_VOTERS: swap the score client for the voter-sharded one (a collective: every rank).
     Returns rank 0's leader (serve it) or, on the other ranks, the client to ``follow``."""
@@ -116,6 +126,7 @@ def main(argv: Optional[list] = None) -> None:
 
         info = pdist.init_from_env("cuda" if cfg.device != "cpu" else "cpu")
         cfg.gpu = info.local_rank
+        follower_config(cfg, info.rank)
         state = build_state(cfg)
         lead = shard_voters(state)
         if info.rank != 0:

@@ -150,3 +150,104 @@ def test_mixtral_tp2_through_ipc_allreduce(gpu):
         c = torch.nn.functional.cosine_similarity(res[r], lg, dim=0).item()
         assert c > 0.99, (r, c)
     assert torch.equal(res[0], res[1])
+
+
+def _back_to_back_worker(rank, world, port, q):
+    """flags only grow, so a fast peer may publish call e+1's flag before a slow poller read
+    e.  Back-to-back calls with no host sync must neither stall nor set the error word."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllReduce(device=dev, max_bytes=1 << 20, blocks=8, spin_ms=2000)
+        xs, want = _ref(world, 4096, 77)
+        outs = []
+        for it in range(300):  # every call waits on the previous one's result: a data dependency chain
+            x = xs[rank].to(dev) if it == 0 else outs[-1] * 0 + xs[rank].to(dev)
+            comm.all_reduce_(x)
+            outs.append(x)
+        torch.cuda.synchronize(dev)
+        bad = [] if torch.equal(outs[-1].cpu(), want) else ["value"]
+        if int(comm.err.item()):
+            bad.append("err")
+        pdist.barrier()
+        comm.close()
+        q.put((rank, bad))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_allreduce_back_to_back_no_false_timeout(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_back_to_back_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: [], 1: []}, res
+
+
+def _skip_worker(rank, world, port, q):
+    """Rank 1 skips one call: rank 0 must return within its spin bound with NaN output, the error word
+    set, and poll() raising CommFailure — no hang, no silently wrong sum."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        import time
+
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CommFailure, CustomAllReduce
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllReduce(device=dev, max_bytes=1 << 20, blocks=4, spin_ms=300)
+        xs, want = _ref(world, 8192, 5)
+        x = xs[rank].to(dev)
+        comm.all_reduce_(x)  # one healthy call
+        torch.cuda.synchronize(dev)
+        ok_first = torch.equal(x.cpu(), want)
+        pdist.barrier()
+        out = {"first": ok_first}
+        if rank == 0:
+            y = xs[0].to(dev)
+            t0 = time.perf_counter()
+            comm.all_reduce_(y)
+            comm.arm()
+            torch.cuda.synchronize(dev)
+            out["elapsed"] = time.perf_counter() - t0
+            out["all_nan"] = bool(torch.isnan(y.float()).all())
+            try:
+                comm.poll()
+                out["raised"] = False
+            except CommFailure:
+                out["raised"] = True
+        pdist.barrier()
+        q.put((rank, out))
+        comm.close()
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_allreduce_missing_peer_fails_loudly(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skip_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert isinstance(res[0], dict) and isinstance(res[1], dict), res
+    assert res[0]["first"] and res[1]["first"]
+    assert res[0]["all_nan"] and res[0]["raised"], res[0]
+    assert res[0]["elapsed"] < 5.0, res[0]  # the 300 ms bound, plus launch / sync overhead

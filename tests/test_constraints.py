@@ -168,3 +168,29 @@ def test_constraint_pickles_without_the_vocabulary(tmp_path):
     assert c2.vocab is TokenVocab.of(tok, V)
     st = c.start()
     assert c2.mask_entry(st) is c.mask_entry(st)
+
+
+def test_suffix_ids_never_reused_after_table_clear(tmp_path, monkeypatch):
+    """bounding the suffix-id table must not hand an old id to a new grammar, or the
+    vocab-level mask cache serves the old grammar's mask to it."""
+    from llm_weighted_consensus_amd.engine import constraints as C
+
+    tok, V = _tokenizers(tmp_path)["bytelevel"]
+    a = constraint_for_schema(response_key_format(["`A`", "`B`"], False).json_schema.schema_, tok, V)
+    a_ids = set(a.fsm.suffix_ids) - {0}
+    ea = a.mask_entry(a.start())  # cached under a's start key
+    monkeypatch.setattr(C, "_SUFFIX_LIMIT", 1)  # every new suffix now clears the table first
+    c = constraint_for_schema(response_key_format(["`C`", "`D`"], False).json_schema.schema_, tok, V)
+    # ids shared with `a` are equal grammar content (the closing literal); the new suffixes get fresh ids
+    assert c.fsm.suffix_ids[0] > max(a_ids)
+    assert c._key(c.start()) != a._key(a.start())
+    ec = c.mask_entry(c.start())
+    assert ec is not ea
+    ok, _ = c.allowed_tokens(c.start())
+    assert np.array_equal(ec.words(), c.mask_entry(c.start()).words())
+    # a pickled copy re-derives its ids in the receiving process instead of carrying foreign ones
+    import pickle
+
+    c2 = pickle.loads(pickle.dumps(c))
+    c2.bind(tok, V)
+    assert np.array_equal(c2.allowed_tokens(c2.start())[0], ok)

@@ -69,9 +69,9 @@ def _summary(out: S.ScoreCompletion):
             "indices": sorted(c.index for c in out.choices)}
 
 
-def _run(client, case):
+def _run(client, case, ctx=None):
     try:
-        return _summary(asyncio.run(client.create_unary(None, _request(case))))
+        return _summary(asyncio.run(client.create_unary(ctx, _request(case))))
     except ScoreError as e:
         return {"error": e.code}
 
@@ -109,7 +109,8 @@ def test_voter_sharded_score_matches_single_process():
     from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
 
     single = ScoreClient(FakeChatClient(_policy), rng_seed=7)
-    want = {case: _run(single, case) for case in CASES}
+    # the sharded client seeds request `seq`'s voters from (seed base 7, seq): the same seeds here
+    want = {case: _run(single, case, {"seed": 7 * 1000003 + i}) for i, case in enumerate(CASES)}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -163,8 +164,11 @@ def _serve_worker(rank, world, port, out_q):
     if rank == 0:
         async def serve():
             out = [_summary(await state.score.create_unary(None, _request("mixed")))]
-            chunks = [c async for c in await state.score.create_streaming(None, _request("one_voter"))]
-            out.append((len(chunks), sorted(c.index for c in chunks[0].choices)))
+            chunks = [c async for c in await state.score.create_streaming(None, _request("mixed"))]
+            agg = chunks[0].clone()
+            for c in chunks[1:]:
+                agg.push(c)
+            out.append((len(chunks), _summary(S.ScoreCompletion.from_chunk(agg))))
             try:
                 await state.score.create_unary(None, _request("all_fail"))
             except ScoreError as e:
@@ -184,7 +188,8 @@ def _serve_worker(rank, world, port, out_q):
 def test_leader_broadcasts_requests_to_followers():
     single = __import__("llm_weighted_consensus_amd.score.orchestrator", fromlist=["ScoreClient"]).ScoreClient(
         FakeChatClient(_policy), rng_seed=7)
-    want = _run(single, "mixed")
+    want = _run(single, "mixed", {"seed": 7 * 1000003 + 0})   # request 0: unary
+    want_s = _run(single, "mixed", {"seed": 7 * 1000003 + 1})  # request 1: streamed
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -195,9 +200,14 @@ def test_leader_broadcasts_requests_to_followers():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    mixed, (n_chunks, idx), code, many = got[0]
+    mixed, (n_chunks, folded), code, many = got[0]
     assert mixed["n"] == want["n"] and [v[:2] for v in mixed["voters"]] == [v[:2] for v in want["voters"]]
-    assert n_chunks == 1 and idx == [0, 1, 2, 3]
+    # streamed: initial chunk, this rank's voter chunks as they arrive, final chunk (remote voters + tally);
+    # the fold of the stream is the unary response
+    assert n_chunks >= 3
+    assert folded["n"] == want_s["n"] and folded["indices"] == want_s["indices"]
+    assert [v[:2] + v[4:] for v in folded["voters"]] == [v[:2] + v[4:] for v in want_s["voters"]]
+    assert sum(cf for _, _, cf in folded["provided"]) == pytest.approx(1.0)
     assert code == 429 or code == want.get("error", code)
     assert many == [want["n"]] * 6  # concurrent requests: every voter of every request in the response
     assert got[1] == 9  # the follower ran all nine requests
