@@ -25,6 +25,7 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
+int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
@@ -276,8 +277,9 @@ void grouped_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const
            "grouped_gemm");
 }
 
-void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
-            at::Tensor& ws, at::Tensor& flags) {
+// Operand checks shared by the MFMA GEMM cores; returns the epilogue operand (residual / bias) or null.
+const void* gemm_operands(const at::Tensor& A, const at::Tensor& W, const at::Tensor& C,
+                          const c10::optional<at::Tensor>& R, int64_t epi) {
   // epi 0: C[M, N] = A . W^T; 1: + R; 2: C[M, N/2] = silu(gate) * up over a 32-row gate/up interleaved W;
   // 3: + bias (R = bias [N]); 4: gelu(. + bias)
   CHECK_BF16(A); CHECK_BF16(W); CHECK_BF16(C); CHECK_CONTIG(W);
@@ -301,6 +303,13 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
     TORCH_CHECK(R->numel() == N, "gemm8p: bias must have N elements");
     r = R->data_ptr();
   }
+  return r;
+}
+
+void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
+            at::Tensor& ws, at::Tensor& flags) {
+  const void* r = gemm_operands(A, W, C, R, epi);
+  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
   // stream-K workspace: one fp32 256x256 partial tile and one flag per workgroup (flags zero between calls)
   const int slots = lwc_gemm8p_slots();
   CHECK_GPU(ws); CHECK_DTYPE(ws, at::kFloat); CHECK_CONTIG(ws);
@@ -310,6 +319,18 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
   CHECK_RC(lwc_gemm8p(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, ws.data_ptr<float>(), flags.data_ptr<int>(), M, N,
                       K, (int)A.stride(0), (int)C.stride(0), (int)epi, cur_stream()),
            "gemm8p");
+}
+
+// gemm4w: the 4-wave interleaved core (one wave per SIMD, data-parallel tiles of 256 x bn, bn = 256 | 192)
+void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
+            int64_t bn) {
+  const void* r = gemm_operands(A, W, C, R, epi);
+  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
+  TORCH_CHECK(bn == 256 || bn == 192, "gemm4w: bn must be 256 or 192");
+  TORCH_CHECK(epi != 2 || bn == 256, "gemm4w: SwiGLU needs bn 256");
+  CHECK_RC(lwc_gemm4w(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
+                      (int)epi, (int)bn, cur_stream()),
+           "gemm4w");
 }
 
 void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& row_off,
@@ -534,6 +555,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("paged_decode", &paged_decode);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("gemm8p", &gemm8p);
+  m.def("gemm4w", &gemm4w);
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);

@@ -1,0 +1,438 @@
+// K6 dense projection GEMM, 4-wave interleaved schedule: C = A . W^T with fused epilogues.
+//
+//   C[M, N]   = A[M, K] . W[N, K]^T (+ R)             EPI_PLAIN / EPI_RESIDUAL
+//   H[M, N/2] = silu(A . Wg^T) * (A . Wu^T)            EPI_SWIGLU (W rows gate/up interleaved in blocks of 32)
+//   C         = A . W^T + bias (then exact erf GELU)   EPI_BIAS / EPI_BIAS_GELU
+//
+// Why a second core next to gemm8p: gemm8p pairs two waves per SIMD and hands the matrix pipe back and
+// forth across s_barriers (compute segment of one wave || load segment of its partner).  Its load
+// segments (2 LDS-DMA pieces + fragment reads) outlast the 16-MFMA compute segment, so the matrix pipe
+// idles at every hand-off (profiles/gemm8p.md: SQ_WAIT_ANY 30 %, +16-37 % when the staging is removed).
+// Here ONE wave per SIMD owns a 128 x (16 NT) slice of the 256 x BN tile (BN = 16 NT x 2; NT = 8: 256
+// fp32 accumulators per lane, held in the AGPR half of gfx950's unified 512-entry register file) and
+// keeps its matrix pipe fed by itself: every load instruction sits between MFMAs (a 16x16x32 MFMA holds
+// the wave's vector issue for 8 of its 16 cycles; the other 8 issue one ds_read or one LDS-DMA piece).
+//
+// Per K tile (BK = 64) and wave: 16 NT MFMAs (8 m x NT n tiles x 2 k-steps of 32), 2 (8 + NT)
+// ds_read_b128 fragment reads, 8 + NT LDS-DMA pieces of 1 KiB (the workgroup moves the A | W tile).  LDS
+// holds two K tiles.  Register fragments are double-buffered by k-step: X = k-step 0, Y = k-step 1.
+//
+//   iteration r (tile r in LDS buffer r & 1):
+//     seg 1: 8 NT MFMAs k0(r) on X          || 8+NT ds_reads Y <- tile r           ; lgkmcnt(0), s_barrier
+//     seg 2: 4 NT MFMAs k1(r) on Y (m 0..3) || 8+NT DMA pieces tile r+2 -> buffer r & 1 ; vmcnt(8+NT), s_barrier
+//     seg 3: 4 NT MFMAs k1(r) on Y (m 4..7) || 8+NT ds_reads X <- tile r+1 (buffer (r+1) & 1)
+//   hazards: WAR — tile r+2 overwrites buffer r & 1 only after every wave's reads of tile r completed
+//            (lgkmcnt(0) + barrier closing seg 1).  RAW — tile r+1 is read in seg 3 after every wave's
+//            vmcnt wait for it (tile r+2's pieces, the youngest, may stay in flight) + the barrier closing
+//            seg 2.  vmcnt never reaches 0 inside the loop except for the last two tiles.
+//   interleave: each load is followed by its share of the segment's MFMAs, pinned by sched_barrier(0).
+//   MFMA: inline asm with the accumulator tied IN PLACE in an AGPR quad.  The builtin lets the register
+//         allocator pick the untied form (dst != srcC); with every AGPR live it then rotates the
+//         accumulators through VGPRs — ~300 v_accvgpr moves per K tile, measured in the .s.
+//
+// LDS image (per operand, per K tile): rows x 128 B, lane-linear DMA image; 16 B chunk c of row r is
+// stored at chunk c ^ ((r >> 1) & 7) (swizzle applied to the DMA source address and to the read: the 16
+// lanes of a ds_read_b128 group hit 16 distinct bank quads — gemm8p's image, SQ_LDS_BANK_CONFLICT 0).
+//
+// Work distribution: data-parallel, persistent (one workgroup per CU), tiles in rounds of 8 x wpx with
+// XCD x taking wpx consecutive tiles of the grouped (gm m-tiles) order, so its tiles share operand panels
+// in its L2.  No stream-K: the planner (ops/gemm_plan.py) gives shapes with a ragged last round to
+// gemm8p's stream-K or picks BN = 192 (qkv at M = 4096: 512 tiles = 2 whole rounds instead of 1.5).
+// Epilogue: accumulators -> bf16 (SwiGLU / bias / GELU in fp32 registers) -> LDS -> 16 B row stores (+
+// residual read in the same pass).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace lwc {
+namespace g4w {
+
+constexpr int kOpA = 256 * 128;  // A operand's K tile: 256 rows x 128 B
+
+enum Epi { EPI_PLAIN = 0, EPI_RESIDUAL = 1, EPI_SWIGLU = 2, EPI_BIAS = 3, EPI_BIAS_GELU = 4 };
+
+struct Params {
+  const bf16_t* A;
+  const bf16_t* W;
+  bf16_t* C;
+  const bf16_t* R;  // EPI_RESIDUAL: residual [M, ldc]; EPI_BIAS*: bias [N]
+  int M, N, K, lda, ldc;
+  int tiles_m, tiles_n, KT;
+  int gm;
+  int wpx, tiles;
+};
+
+template <int NT>
+struct Geo {
+  static constexpr int BN = 32 * NT;            // W rows per tile
+  static constexpr int OpB = BN * 128;          // W operand's K tile
+  static constexpr int Buf = kOpA + OpB;        // one K tile
+  static constexpr int Lds = 2 * Buf;           // two K tiles
+  static constexpr int Pieces = 8 + NT;         // LDS-DMA pieces per wave per K tile
+  static constexpr int Reads = 8 + NT;          // fragment reads per wave per k-step
+};
+
+LWC_DEVICE void mfma(float4v& d, const uint4v& a, const uint4v& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+}
+// the first non-MFMA read of an accumulator after the last (opaque) MFMA: 16 wait states
+#define G4_MFMA_DRAIN() asm volatile("s_nop 15" ::: "memory")
+#define G4_BAR() __builtin_amdgcn_s_barrier()
+#define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
+#define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+LWC_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+LWC_DEVICE float erf_as(float x) {
+  const float a = fabsf(x);
+  const float t = __frcp_rn(1.f + 0.3275911f * a);
+  const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.f - y * __expf(-a * a), x);
+}
+LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
+
+LWC_DEVICE void tile_mn(const Params& p, int t, int& m, int& n) {
+  const int group = p.gm * p.tiles_n;
+  const int first_m = (t / group) * p.gm;
+  const int gsz = min(p.tiles_m - first_m, p.gm);
+  const int in = t % group;
+  m = first_m + in % gsz;
+  n = in / gsz;
+}
+
+// Epilogue LDS image column of (row, col) for a CW-wide bf16 row: XOR swizzle by 8-column chunks (keeps
+// every 16 B chunk contiguous); CW = 96 swizzles its last 32 columns among themselves.
+template <int CW>
+LWC_DEVICE int swz(int row, int col) {
+  if constexpr (CW == 96) return col < 64 ? col ^ ((row & 7) << 3) : col ^ ((row & 3) << 3);
+  return col ^ (((row & 7) << 3) % CW);
+}
+
+template <int EPI, int NT, int VAR>
+__global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
+  using G = Geo<NT>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int KT = p.KT;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+
+  for (int round = 0;; ++round) {
+    const int tile = round * 8 * p.wpx + xcd * p.wpx + j;
+    if (tile >= p.tiles) break;
+    int tm, tn;
+    tile_mn(p, tile, tm, tn);
+    const int m0 = tm * 256, n0 = tn * G::BN;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // DMA: piece i of wave wid covers operand rows i*32 + wid*8 + lane/8, LDS chunk lane%8, which holds
+    // global chunk (lane%8) ^ ((row >> 1) & 7); (row >> 1) & 7 does not depend on i.
+    const int drow = wid * 8 + (lane >> 3);
+    const int dchk = ((lane & 7) ^ ((drow >> 1) & 7)) * 8;
+    const uint32_t voA = (uint32_t)((drow * p.lda + dchk) * 2);
+    const uint32_t voW = (uint32_t)((drow * p.K + dchk) * 2);
+    const int sA = 32 * p.lda * 2, sW = 32 * p.K * 2;  // bytes between pieces
+    const int dst0 = wid * 1024;
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.A + (size_t)m0 * p.lda), (short)0, (p.M - m0) * p.lda * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.W + (size_t)n0 * p.K), (short)0, min(p.N - n0, G::BN) * p.K * 2, 0x00020000);
+    // LDS-DMA piece k of one K tile (k < 8: A rows, else W rows)
+    auto piece = [&](uint8_t* buf, int kt, int k) {
+      if (k < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rA, (__attribute__((address_space(3))) void*)(buf + k * 4096 + dst0), 16, voA, k * sA + kt * 128, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rW, (__attribute__((address_space(3))) void*)(buf + kOpA + (k - 8) * 4096 + dst0), 16, voW,
+            (k - 8) * sW + kt * 128, 0, 0);
+    };
+    auto stage = [&](uint8_t* buf, int kt) {
+#pragma unroll
+      for (int k = 0; k < G::Pieces; ++k) piece(buf, kt, k);
+    };
+    // fragment reads: m-tile / n-tile i adds i * 16 rows = i * 2048 B; the swizzle only depends on r16
+    const int sw = (r16 >> 1) & 7;
+    const int offA0 = (wm * 128 + r16) * 128 + ((q ^ sw) << 4);
+    const int offA1 = (wm * 128 + r16) * 128 + (((4 + q) ^ sw) << 4);
+    const int offB0 = kOpA + (wn * 16 * NT + r16) * 128 + ((q ^ sw) << 4);
+    const int offB1 = kOpA + (wn * 16 * NT + r16) * 128 + (((4 + q) ^ sw) << 4);
+
+    float4v acc[8][NT];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NT; ++jj) acc[i][jj] = float4v{0.f, 0.f, 0.f, 0.f};
+    uint4v xa[8], xb[NT], ya[8], yb[NT];
+    // fragment read k of a k-step (k < NT: W n-tile k, else A m-tile k - NT)
+    auto rd1 = [&](const uint8_t* buf, int oa, int ob, uint4v(&fa)[8], uint4v(&fb)[NT], int k) {
+      if (k < NT)
+        fb[k] = *reinterpret_cast<const uint4v*>(buf + ob + k * 2048);
+      else
+        fa[k - NT] = *reinterpret_cast<const uint4v*>(buf + oa + (k - NT) * 2048);
+    };
+
+    const int nt = KT;
+    stage(smem, 0);
+    if (nt > 1) {
+      stage(smem + G::Buf, 1);
+      G4_VM(G::Pieces);
+    } else {
+      G4_VM(0);
+    }
+    G4_BAR();
+#pragma unroll
+    for (int k = 0; k < G::Reads; ++k) rd1(smem, offA0, offB0, xa, xb, k);
+
+    // K tile R: seg 1 (k-step 0 on X || read Y), seg 2 (k-step 1, m 0..3 || DMA tile R+2), seg 3 (k-step 1,
+    // m 4..7 || read X of tile R+1).  STAGE / NEXT select the steady-state body or the last two tiles'
+    // (no DMA / no next tile): straight-line bodies, no branch inside.
+    constexpr int M1 = 8 * NT, M2 = 4 * NT;  // MFMAs of seg 1, of seg 2 and 3
+    // VAR bit 0: the DMA pieces of tile R+2 go P2 into seg 2 and the rest into seg 3 (beside the X reads);
+    // bit 1: the Y reads of seg 1 are spread over its first 3/4 only, so the lgkmcnt(0) closing seg 1
+    // does not wait on a read issued just before it; bit 2: seg 2 carries 1/4 of the k-step-1 MFMAs
+    // (not 1/2), seg 3 the other 3/4 — the X reads + DMA pieces of seg 3 get more MFMAs to hide behind.
+    constexpr bool SPLIT = VAR & 1, FRONT = VAR & 2, BAL = VAR & 4;
+    constexpr int P2 = SPLIT ? G::Pieces / 2 : G::Pieces, P3 = G::Pieces - P2;
+    constexpr int F1 = FRONT ? 3 * M1 / 4 : M1;      // seg-1 MFMAs that carry the Y reads
+    constexpr int S2 = BAL ? M2 / 2 : M2;  // seg-2 MFMAs (of the 2 M2 k-step-1 MFMAs)
+    constexpr int S3 = 2 * M2 - S2;
+#define G4_TILE(R, STAGE, NEXT)                                                                     \
+  {                                                                                                 \
+    uint8_t* cur = smem + ((R) & 1) * G::Buf;                                                       \
+    uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
+    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
+      rd1(cur, offA1, offB1, ya, yb, k);                                                            \
+      _Pragma("unroll") for (int m = k * F1 / G::Reads; m < (k + 1) * F1 / G::Reads; ++m)           \
+        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
+    G4_LGKM0();                                                                                     \
+    G4_BAR();                                                                                       \
+    _Pragma("unroll") for (int k = 0; k < P2; ++k) {                                                \
+      if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
+      _Pragma("unroll") for (int m = k * S2 / P2; m < (k + 1) * S2 / P2; ++m)                       \
+        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    if constexpr (STAGE) {                                                                          \
+      G4_VM(P2);                                                                                    \
+    } else {                                                                                        \
+      G4_VM(0);                                                                                     \
+    }                                                                                               \
+    G4_BAR();                                                                                       \
+    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
+      if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
+      if constexpr (STAGE && P3 > 0) {                                                              \
+        if (k < P3) piece(cur, (R) + 2, P2 + k);                                                    \
+      }                                                                                             \
+      _Pragma("unroll") for (int m = S2 + k * S3 / G::Reads; m < S2 + (k + 1) * S3 / G::Reads; ++m) \
+        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+  }
+    // VAR 8: ONE barrier per K tile.  seg A = k-step 0 on X || Y reads of tile R; then lgkmcnt(0) (own Y
+    // reads done), vmcnt(0) (own pieces of tile R+1 landed: the only DMA in flight), barrier — after it
+    // every wave is done reading tile R's buffer (WAR) and tile R+1 is visible (RAW); seg B = k-step 1 on Y
+    // || X reads of tile R+1 AND the DMA of tile R+2 into tile R's buffer, both spread over all 8 NT
+    // MFMAs (LDS traffic per segment balanced: 2 segments x ~64 KiB instead of a 96 KiB third segment).
+#define G4_TILE1(R, STAGE, NEXT)                                                                    \
+  {                                                                                                 \
+    uint8_t* cur = smem + ((R) & 1) * G::Buf;                                                       \
+    uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
+    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
+      rd1(cur, offA1, offB1, ya, yb, k);                                                            \
+      _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
+        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    G4_LGKM0();                                                                                     \
+    G4_VM(0);                                                                                       \
+    G4_BAR();                                                                                       \
+    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
+      if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
+      if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
+      _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
+        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+  }
+    int r = 0;
+    if constexpr (VAR == 8) {
+      for (; r + 2 < nt; ++r) G4_TILE1(r, true, true)
+      if (nt >= 2) {
+        G4_TILE1(r, false, true)
+        ++r;
+      }
+      G4_TILE1(r, false, false)
+    } else {
+      for (; r + 2 < nt; ++r) G4_TILE(r, true, true)
+      if (nt >= 2) {
+        G4_TILE(r, false, true)
+        ++r;
+      }
+      G4_TILE(r, false, false)
+    }
+#undef G4_TILE
+#undef G4_TILE1
+    G4_MFMA_DRAIN();  // accumulators are read by VALU / stores from here on
+    __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
+
+    // ---- epilogue: per wave 128 rows x CW bf16 columns through LDS, then 16 B stores
+    constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
+    bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float4v t[NT];
+#pragma unroll
+      for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
+      if constexpr (EPI == EPI_SWIGLU) {
+        // n-tiles of the wave: W rows wn*128 + jj*16; 32-row blocks alternate gate / up, so gate tiles
+        // {0,1,4,5} pair with up tiles {2,3,6,7}
+#pragma unroll
+        for (int h = 0; h < NT / 4; ++h)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[h * 4 + jj][e] = silu(t[h * 4 + jj][e]) * t[h * 4 + jj + 2][e];
+      }
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+        // bias re-read per m-tile (L1 hits): loaded once before the K loop it would pin NT VGPRs through it
+        int bcol = n0 + wn * 16 * NT + r16;
+        asm volatile("" : "+v"(bcol));
+#pragma unroll
+        for (int jj = 0; jj < NT; ++jj) {
+          const int col = bcol + jj * 16;
+          const float bv = col < p.N ? bf2f(p.R[col]) : 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float y = t[jj][e] + bv;
+            t[jj][e] = EPI == EPI_BIAS_GELU ? gelu_erf(y) : y;
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < NT; ++jj) {
+        if constexpr (EPI == EPI_SWIGLU) {
+          if ((jj & 3) >= 2) continue;
+        }
+        const int oc = EPI == EPI_SWIGLU ? (jj >> 2) * 32 + (jj & 1) * 16 : jj * 16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = i * 16 + 4 * q + e, col = oc + r16;
+          ot[row * CW + swz<CW>(row, col)] = f2bf(t[jj][e]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one m-tile's values live at a time
+    }
+    __syncthreads();
+    constexpr int CPR = CW / 8;  // 16 B chunks per row
+    const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
+    const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
+#pragma unroll 4
+    for (int c = lane; c < 128 * CPR; c += 64) {
+      const int row = c / CPR, cch = c % CPR;
+      const int gm = m0 + wm * 128 + row;
+      const int gn = ncol0 + cch * 8;
+      if (gm < p.M && gn < ncols) {
+        uint4v v = *reinterpret_cast<const uint4v*>(ot + row * CW + swz<CW>(row, cch * 8));
+        if constexpr (EPI == EPI_RESIDUAL) {
+          float x[8], y[8];
+          unpack8(v, x);
+          unpack8(*reinterpret_cast<const uint4v*>(p.R + (size_t)gm * p.ldc + gn), y);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] += y[e];
+          v = pack8(x);
+        }
+        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+      }
+    }
+    __syncthreads();  // LDS free for the next tile
+  }
+}
+
+template <int EPI, int NT, int VAR>
+int launch3(const Params& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Geo<NT>::Lds);
+    attr = true;
+  }
+  gemm4w_kernel<EPI, NT, VAR><<<8 * p.wpx, 256, Geo<NT>::Lds, s>>>(p);
+  return (int)hipGetLastError();
+}
+
+int env_int(const char* name, int dflt);
+
+template <int EPI, int NT>
+int launch(const Params& p, hipStream_t s) {
+  // schedule variant (VAR bits, see the main loop): LWC_G4_VAR, an A/B knob (scripts/microbench.py g4ab);
+  // the plain epilogue carries every variant, the fused ones the default
+  const int var = env_int("LWC_G4_VAR", 1);
+  if constexpr (EPI == EPI_PLAIN) {
+    switch (var) {
+      case 0: return launch3<EPI, NT, 0>(p, s);
+      case 3: return launch3<EPI, NT, 3>(p, s);
+      case 5: return launch3<EPI, NT, 5>(p, s);
+      case 7: return launch3<EPI, NT, 7>(p, s);
+      case 8: return launch3<EPI, NT, 8>(p, s);
+      default: break;
+    }
+  }
+  return launch3<EPI, NT, 1>(p, s);
+}
+
+template <int NT>
+int dispatch(const Params& p, int epi, hipStream_t s) {
+  switch (epi) {
+    case EPI_PLAIN: return launch<EPI_PLAIN, NT>(p, s);
+    case EPI_RESIDUAL: return launch<EPI_RESIDUAL, NT>(p, s);
+    case EPI_BIAS: return launch<EPI_BIAS, NT>(p, s);
+    case EPI_BIAS_GELU: return launch<EPI_BIAS_GELU, NT>(p, s);
+    case EPI_SWIGLU:
+      if constexpr (NT == 8) return launch<EPI_SWIGLU, NT>(p, s);
+      return -1;
+  }
+  return -1;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8) cus = 256;
+  }
+  return cus;
+}
+
+}  // namespace g4w
+}  // namespace lwc
+
+// C = A . W^T (epilogue epi as lwc_gemm8p: 0 plain, 1 + residual, 2 SwiGLU over 32-row gate/up interleaved W,
+// 3 + bias, 4 gelu(. + bias)); bn = 256 or 192 (W rows per tile; SwiGLU needs 256).  Requires K % 64 == 0,
+// N % 8 == 0, lda / ldc % 8 == 0.
+extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
+                          int epi, int bn, hipStream_t s) {
+  using namespace lwc::g4w;
+  if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
+  if (bn != 256 && bn != 192) return -1;
+  if ((long long)M * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
+  if (epi == EPI_SWIGLU && (N % 64 != 0 || bn != 256)) return -1;
+  if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
+  if (M == 0 || N == 0) return 0;
+  const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
+  const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
+  Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
+           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles};
+  return bn == 256 ? dispatch<8>(p, epi, s) : dispatch<6>(p, epi, s);
+}

@@ -267,6 +267,28 @@ def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     return out
 
 
+def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
+           gelu: bool = False, bn: int = 256) -> torch.Tensor:
+    """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
+    a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
+    workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
+    (interleaved gate|up W, bn 256), ``bias`` (+ ``gelu``)."""
+    N = W.shape[0] // 2 if swiglu else W.shape[0]
+    if out is None:
+        out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
+    if bias is not None:
+        if swiglu or residual is not None:
+            raise ValueError("gemm4w: bias epilogue combines with neither swiglu nor residual")
+        epi, residual = (4 if gelu else 3), bias
+    else:
+        if gelu:
+            raise ValueError("gemm4w: gelu needs a bias")
+        epi = 2 if swiglu else (1 if residual is not None else 0)
+    kernels().gemm4w(A, W, out, residual, epi, int(bn))
+    return out
+
+
 _G8_WS: dict = {}
 
 

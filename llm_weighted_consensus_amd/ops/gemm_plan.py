@@ -1,17 +1,19 @@
 """Per-shape GEMM backend choice for the decoder projections (K6).
 
-Two backends compute ``A . W^T`` for the dense projections:
+Backends computing ``A . W^T`` for the dense projections:
 
-* ``blas`` — hipBLASLt through ``torch.nn.functional.linear`` (its own stream-K kernels);
-* ``g8``   — the hand-written 8-phase MFMA GEMM with a stream-K tail (``csrc/kernels/gemm8p.hip``),
-  which also fuses the SwiGLU of the gate|up projection, or the residual add of the o / down
-  projections (:func:`linear_add_`), into its epilogue.
+* ``blas``   — hipBLASLt through ``torch.nn.functional.linear`` (its own stream-K kernels);
+* ``g8``     — the hand-written 8-phase MFMA GEMM with a stream-K tail (``csrc/kernels/gemm8p.hip``);
+* ``g4``     — the hand-written 4-wave interleaved MFMA GEMM, 256 x 256 tiles (``csrc/kernels/gemm4w.hip``);
+* ``g4n192`` — the same core with 256 x 192 tiles (the qkv projection at decode batch 4096: 512 tiles =
+  two whole rounds of 256 CUs, where 256 x 256 tiles leave half of the second round idle).
 
-Neither wins everywhere (``profiles/gemm8p.md``: g8 is ahead on the fused gate_up+SwiGLU and the qkv
-projection at decode batch 3072, hipBLASLt on most shapes at batch 1024), so the choice is made per
-(M, N, K, epilogue) by timing both on the device, once, before a decode bucket's hipGraph is captured
-(:meth:`LlamaModel.tune_gemms`).  Untuned shapes (prefill, encode) use hipBLASLt.
-``LWC_GEMM=blas|g8`` forces one backend (``auto`` = measured, the default).
+The hand-written cores also fuse the SwiGLU of the gate|up projection, or the residual add of the o /
+down projections (:func:`linear_add_`), into their epilogue.  None wins everywhere
+(``profiles/gemm4w.md``), so the choice is made per (M, N, K, epilogue) by timing every applicable
+backend on the device, once, before a decode bucket's hipGraph is captured (:meth:`LlamaModel.tune_gemms`);
+a hand-written core within ``OWN_MARGIN`` of the library is preferred.  Untuned shapes (prefill,
+encode) use hipBLASLt.  ``LWC_GEMM=blas|g8|g4|g4n192`` forces one backend (``auto`` = measured, the default).
 """
 from __future__ import annotations
 
@@ -21,15 +23,18 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import gemm8p, silu_mul
+from . import gemm4w, gemm8p, silu_mul
 
 MODE = os.environ.get("LWC_GEMM", "auto")
+BACKENDS = ("blas", "g8", "g4", "g4n192")
+# a hand-written core is chosen unless the library is faster by more than this fraction
+OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "0.01"))
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
 TIMINGS: Dict[Tuple[int, int, int, str], Dict[str, float]] = {}
 
 
 def choice(M: int, N: int, K: int, epi: str) -> str:
-    if MODE in ("blas", "g8"):
+    if MODE in BACKENDS:
         return MODE
     return _CHOICE.get((M, N, K, epi), "blas")
 
@@ -38,12 +43,26 @@ def _g8_ok(N: int, K: int, epi: str) -> bool:
     return K % 64 == 0 and N % (64 if epi == "swiglu" else 8) == 0
 
 
+def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
+    """Whether hand-written backend ``b`` takes this call (layout and the cores' shape rules)."""
+    if b == "blas" or not _g8_ok(N, K, epi) or x.stride(1) != 1:
+        return False
+    return not (b == "g4n192" and epi == "swiglu")
+
+
+def _own(b: str, x: torch.Tensor, w: torch.Tensor, ws=None, **kw) -> torch.Tensor:
+    if b == "g8":
+        return gemm8p(x, w, ws=ws, **kw)
+    return gemm4w(x, w, bn=192 if b == "g4n192" else 256, **kw)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, ws=None) -> torch.Tensor:
     """x [M, K] . w[N, K]^T -> [M, N] bf16 on the chosen backend."""
     M, K = x.shape
     N = w.shape[0]
-    if choice(M, N, K, "plain") == "g8" and _g8_ok(N, K, "plain") and x.stride(1) == 1:
-        return gemm8p(x, w, ws=ws)
+    b = choice(M, N, K, "plain")
+    if _own_ok(b, x, N, K, "plain"):
+        return _own(b, x, w, ws)
     return F.linear(x, w)
 
 
@@ -54,9 +73,9 @@ def linear_add_(x: torch.Tensor, w: torch.Tensor, acc: torch.Tensor, ws=None) ->
     lane).  Saves the separate residual add's read and write of the [M, N] projection output."""
     M, K = x.shape
     N = w.shape[0]
-    if (choice(M, N, K, "residual") == "g8" and _g8_ok(N, K, "residual") and x.stride(1) == 1
-            and acc.is_contiguous()):
-        return gemm8p(x, w, residual=acc, out=acc, ws=ws)
+    b = choice(M, N, K, "residual")
+    if _own_ok(b, x, N, K, "residual") and acc.is_contiguous():
+        return _own(b, x, w, ws, residual=acc, out=acc)
     return acc.addmm_(x, w.t())
 
 
@@ -65,8 +84,9 @@ def swiglu(x: torch.Tensor, w_gu: torch.Tensor, block: int, ws=None) -> torch.Te
     (block 0) or interleaved in blocks of ``block`` (ops.swiglu_interleave; required by g8)."""
     M, K = x.shape
     N = w_gu.shape[0]
-    if block == 32 and choice(M, N, K, "swiglu") == "g8" and _g8_ok(N, K, "swiglu") and x.stride(1) == 1:
-        return gemm8p(x, w_gu, swiglu=True, ws=ws)
+    b = choice(M, N, K, "swiglu")
+    if block == 32 and _own_ok(b, x, N, K, "swiglu"):
+        return _own(b, x, w_gu, ws, swiglu=True)
     return silu_mul(F.linear(x, w_gu), block=block)
 
 
@@ -120,8 +140,9 @@ def _time(fn, iters: int = 5, rounds: int = 3) -> float:
 
 
 def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, ws=None) -> Optional[str]:
-    """Time both backends for this (M, N, K, epi) and record the faster (no-op under graph capture, off
-    the GPU, for an already tuned shape, or when a backend is forced)."""
+    """Time every applicable backend for this (M, N, K, epi) and record the choice (no-op under graph
+    capture, off the GPU, for an already tuned shape, or when a backend is forced).  Rounds interleave the
+    backends (one process, one device: their clock and cache states match)."""
     M, K = x.shape
     N = w.shape[0]
     key = (M, N, K, epi)
@@ -130,25 +151,27 @@ def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, w
     if not _g8_ok(N, K, epi) or (epi == "swiglu" and block != 32):
         _CHOICE[key] = "blas"
         return "blas"
-    if epi == "swiglu":
-        t_blas = _time(lambda: silu_mul(F.linear(x, w), block=block))
-        t_g8 = _time(lambda: gemm8p(x, w, swiglu=True, ws=ws))
-    elif epi == "residual":
-        acc = torch.zeros(M, N, dtype=x.dtype, device=x.device)
-        t_blas = _time(lambda: acc.addmm_(x, w.t()))
-        t_g8 = _time(lambda: gemm8p(x, w, residual=acc, out=acc, ws=ws))
-    else:
-        t_blas = _time(lambda: F.linear(x, w))
-        t_g8 = _time(lambda: gemm8p(x, w, ws=ws))
-    TIMINGS[key] = {"blas": t_blas, "g8": t_g8}
-    # Isolated timings flatter gemm8p's plain / residual kernels: in the captured decode step the qkv
-    # projection measured 180.6 us on gemm8p vs 160.6 us on hipBLASLt (profiles/bench_r64.md, round 2)
-    # where the isolated pair had been a near tie — so those need a clear win; the fused SwiGLU (one
-    # kernel against GEMM + silu_mul) keeps gemm8p unless the library wins clearly: the short timing
-    # runs are noisy enough to flip the choice (they did under a profiler; both choices were within
-    # 0.5 % of the step there) and a stable choice keeps box-to-box results comparable.
-    margin = 1.03 if epi == "swiglu" else 0.97
-    _CHOICE[key] = "g8" if t_g8 < t_blas * margin else "blas"
+    acc = torch.zeros(M, N, dtype=x.dtype, device=x.device) if epi == "residual" else None
+    runs = {}
+    for b in BACKENDS:
+        if b != "blas" and not _own_ok(b, x, N, K, epi):
+            continue
+        if epi == "swiglu":
+            runs[b] = (lambda: silu_mul(F.linear(x, w), block=block)) if b == "blas" else \
+                (lambda b=b: _own(b, x, w, ws, swiglu=True))
+        elif epi == "residual":
+            runs[b] = (lambda: acc.addmm_(x, w.t())) if b == "blas" else \
+                (lambda b=b: _own(b, x, w, ws, residual=acc, out=acc))
+        else:
+            runs[b] = (lambda: F.linear(x, w)) if b == "blas" else (lambda b=b: _own(b, x, w, ws))
+    ts = {b: [] for b in runs}
+    for _ in range(3):
+        for b, fn in runs.items():
+            ts[b].append(_time(fn, iters=3, rounds=1))
+    med = {b: sorted(t)[len(t) // 2] for b, t in ts.items()}
+    TIMINGS[key] = med
+    own = min((b for b in med if b != "blas"), key=lambda b: med[b], default=None)
+    _CHOICE[key] = own if own is not None and med[own] <= med["blas"] * (1 + OWN_MARGIN) else "blas"
     return _CHOICE[key]
 
 

@@ -25,6 +25,9 @@ def main():
         fn = lambda: ops.gemm8p(x, w, swiglu=True)  # noqa: E731
     elif kind == "g8":
         fn = lambda: ops.gemm8p(x, w)  # noqa: E731
+    elif kind.startswith("g4"):  # g4 / g4n192 (bn 192)
+        bn = 192 if kind == "g4n192" else 256
+        fn = lambda: ops.gemm4w(x, w, bn=bn)  # noqa: E731
     else:
         fn = lambda: F.linear(x, w)  # noqa: E731
     for _ in range(iters):

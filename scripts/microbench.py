@@ -203,6 +203,61 @@ def gemm8p_ab(dev):
         os.environ.pop(k, None)
 
 
+def gemm4w_ab(dev):
+    """hipBLASLt vs gemm8p vs gemm4w (bn 256 / 192) on the headline's decode shapes (M = 4096), prefill and
+    encoder shapes; interleaved rounds in one process, median of 5, random [-1, 1) operands."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    shapes = [(4096, 6144, 4096, "plain"), (4096, 4096, 4096, "res"), (4096, 28672, 4096, "swiglu"),
+              (4096, 4096, 14336, "res"), (4096, 128256, 4096, "plain"), (16384, 6144, 4096, "plain"),
+              (65536, 3072, 1024, "bias"), (65536, 4096, 1024, "gelu"), (65536, 1024, 4096, "bias"),
+              (8192, 8192, 8192, "plain")]
+    only = os.environ.get("G4_SHAPES")
+    if only:
+        shapes = [shapes[int(i)] for i in only.split(",")]
+    ws = ops.new_gemm8p_workspace(dev)
+    for M, N, K, epi in shapes:
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        b = (torch.rand(N, device=dev) - 0.5).to(torch.bfloat16)
+        acc = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+        if epi == "swiglu":
+            wi = ops.swiglu_interleave(w)
+            runs = {"blas": lambda: ops.silu_mul(F.linear(x, wi), block=32),
+                    "g8": lambda: ops.gemm8p(x, wi, swiglu=True, ws=ws),
+                    "g4": lambda: ops.gemm4w(x, wi, swiglu=True)}
+        elif epi == "res":
+            runs = {"blas": lambda: acc.addmm_(x, w.t()), "g8": lambda: ops.gemm8p(x, w, residual=acc, out=acc, ws=ws),
+                    "g4": lambda: ops.gemm4w(x, w, residual=acc, out=acc),
+                    "g4n192": lambda: ops.gemm4w(x, w, residual=acc, out=acc, bn=192)}
+        elif epi in ("bias", "gelu"):
+            g = epi == "gelu"
+            runs = {"blas": (lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if g
+                    else (lambda: F.linear(x, w, b)),
+                    "g8": lambda: ops.gemm8p(x, w, bias=b, gelu=g, ws=ws),
+                    "g4": lambda: ops.gemm4w(x, w, bias=b, gelu=g),
+                    "g4n192": lambda: ops.gemm4w(x, w, bias=b, gelu=g, bn=192)}
+        else:
+            runs = {"blas": lambda: F.linear(x, w), "g8": lambda: ops.gemm8p(x, w, ws=ws),
+                    "g4": lambda: ops.gemm4w(x, w), "g4n192": lambda: ops.gemm4w(x, w, bn=192)}
+        # gemm4w schedule variants (LWC_G4_VAR bits: 1 split DMA, 2 front-load seg-1 reads, 4 seg-2/3 balance;
+        # only the plain epilogue carries every variant)
+        for k in [k for k in runs if k.startswith("g4")]:
+            fn = runs.pop(k)
+            for v in (os.environ.get("G4_VARS", "1,3,5,7") if epi == "plain" else "1").split(","):
+                runs[f"{k}v{v}"] = (lambda fn=fn, v=v: (os.environ.__setitem__("LWC_G4_VAR", v), fn()))
+        res = {k: [] for k in runs}
+        for _ in range(5):
+            for k, fn in runs.items():
+                res[k].append(timeit(fn, iters=10, warm=2))
+        fl = 2 * M * N * K / 1e12
+        line = "  ".join(f"{k} {sorted(t)[2]:8.1f} us ({fl / sorted(t)[2] * 1e6:5.0f})" for k, t in res.items())
+        print(f"g4ab {M}x{N}x{K} {epi}: {line}", flush=True)
+        del x, w, acc
+
+
 def attention(dev):
     from llm_weighted_consensus_amd import ops
 
@@ -374,6 +429,8 @@ def main():
         gemm_backends(dev, [1024, 1536])
     if "grouped" in a.what:
         grouped(dev)
+    if "g4ab" in a.what:
+        gemm4w_ab(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:

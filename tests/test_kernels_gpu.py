@@ -521,7 +521,7 @@ def test_gemm8p(gpu, M, N, K, epi):
     assert int(ops.gemm8p_workspace(A.device)[1].abs().sum()) == 0, "stream-K flags left set"
 
 
-@pytest.mark.parametrize("backend", ["g8", "blas"])
+@pytest.mark.parametrize("backend", ["g8", "g4", "g4n192", "blas"])
 @pytest.mark.parametrize("M,N,K", [(520, 1024, 2048), (3072, 4096, 4096)])
 def test_linear_add_inplace(gpu, backend, M, N, K):
     """gemm_plan.linear_add_: acc += A W^T in place (gemm8p's residual epilogue writing over its residual
@@ -699,3 +699,38 @@ def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
         ref = torch.nn.functional.gelu(ref)
     _close(ops.gemm8p(A, W, bias=b, gelu=gelu), ref, 3e-2, 1e-2)
     _close(gemm_plan.linear_bias(A, W, b, gelu=gelu), ref, 3e-2, 1e-2)
+
+
+@pytest.mark.parametrize("bn", [256, 192])
+@pytest.mark.parametrize("M,N,K,epi", [(300, 520, 64, "plain"), (4096, 6144, 4096, "plain"), (513, 1000, 128, "res"),
+                                       (1024, 1024, 14336, "res"), (700, 2048, 1024, "swiglu"),
+                                       (257, 776, 320, "bias"), (520, 4096, 1024, "gelu"),
+                                       (64, 384, 192, "plain"), (2048, 128256 // 8, 4096, "plain")])
+def test_gemm4w(gpu, M, N, K, epi, bn):
+    """4-wave interleaved MFMA GEMM (AGPR accumulators, in-place inline-asm MFMA) vs an fp32 matmul for every
+    epilogue: ragged M / N tails, one / two / many K tiles (the peeled last iterations), both tile widths,
+    several rounds of tiles per workgroup.  Launched twice (persistent rounds must leave LDS reusable)."""
+    from llm_weighted_consensus_amd import ops
+
+    if epi == "swiglu" and bn != 256:
+        pytest.skip("SwiGLU epilogue needs bn 256")
+    torch.manual_seed(M + N + K + bn)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    for _ in range(2):
+        if epi == "swiglu":
+            F = N // 2
+            out = ops.gemm4w(A, ops.swiglu_interleave(W), swiglu=True, bn=bn)
+            _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
+        elif epi in ("bias", "gelu"):
+            b = (torch.randn(N, device=gpu) * 0.5).to(torch.bfloat16)
+            want = ref + b.float()
+            if epi == "gelu":
+                want = torch.nn.functional.gelu(want)
+            _close(ops.gemm4w(A, W, bias=b, gelu=epi == "gelu", bn=bn), want, 3e-2, 1e-2)
+        else:
+            R = torch.randn(M, N, device=gpu).to(torch.bfloat16) if epi == "res" else None
+            want = ref + (R.float() if R is not None else 0)
+            out = ops.gemm4w(A, W, residual=R, out=R if R is not None else None, bn=bn)
+            _close(out, want, 3e-2, 1e-2)
