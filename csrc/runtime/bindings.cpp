@@ -147,7 +147,14 @@ PYBIND11_MODULE(_runtime, m) {
       .def("block_table", &BlockManager::block_table)
       .def("slot", &BlockManager::slot)
       .def("refcount", &BlockManager::refcount)
-      .def("take_copies", &BlockManager::take_copies);
+      .def("take_copies", &BlockManager::take_copies)
+      .def("append_cost_total", &BlockManager::append_cost_total)
+      .def("swap_out",
+           [](BlockManager& bm, const std::vector<int64_t>& seqs) {
+             BlockManager::Swapped s = bm.swap_out(seqs);
+             return py::make_tuple(s.blocks, s.tables, s.lens);
+           })
+      .def("swap_in", &BlockManager::swap_in, py::arg("seqs"), py::arg("n"), py::arg("tables"), py::arg("lens"));
   m.def("prepare_decode", &prepare_decode, py::arg("bm"), py::arg("seqs"), py::arg("width"), py::arg("pad_to") = 0);
   m.def("prepare_decode_into", &prepare_decode_into, py::arg("bm"), py::arg("seqs"), py::arg("width"),
         py::arg("pad_to"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("slots"), py::arg("positions"));

@@ -221,6 +221,70 @@ void BlockManager::free_sequence(int64_t seq) {
   seqs_.erase(it);
 }
 
+int64_t BlockManager::append_cost_total(const std::vector<int64_t>& seqs) const {
+  int64_t n = 0;
+  for (int64_t q : seqs) n += append_cost(q);
+  return n;
+}
+
+BlockManager::Swapped BlockManager::swap_out(const std::vector<int64_t>& seqs) {
+  Swapped out;
+  std::unordered_map<int32_t, int32_t> index;
+  for (int64_t q : seqs) {
+    const Seq& s = get(q);
+    std::vector<int32_t> t;
+    t.reserve(s.blocks.size());
+    for (int32_t b : s.blocks) {
+      auto it = index.find(b);
+      if (it == index.end()) {
+        it = index.emplace(b, (int32_t)out.blocks.size()).first;
+        out.blocks.push_back(b);
+      }
+      t.push_back(it->second);
+    }
+    out.tables.push_back(std::move(t));
+    out.lens.push_back(s.len);
+  }
+  for (int64_t q : seqs) free_sequence(q);
+  return out;
+}
+
+std::vector<int32_t> BlockManager::swap_in(const std::vector<int64_t>& seqs, int n,
+                                           const std::vector<std::vector<int32_t>>& tables,
+                                           const std::vector<int64_t>& lens) {
+  if (seqs.size() != tables.size() || seqs.size() != lens.size())
+    throw std::invalid_argument("BlockManager::swap_in: seqs / tables / lens size mismatch");
+  for (int64_t q : seqs)
+    if (seqs_.count(q)) throw std::invalid_argument("BlockManager: sequence exists " + std::to_string(q));
+  for (size_t i = 0; i < tables.size(); ++i) {
+    if ((int64_t)tables[i].size() != blocks_for(lens[i]))
+      throw std::invalid_argument("BlockManager::swap_in: table does not match the length");
+    for (int32_t x : tables[i])
+      if (x < 0 || x >= n) throw std::out_of_range("BlockManager::swap_in: block index out of range");
+  }
+  if (!can_allocate(n)) throw std::runtime_error("BlockManager: out of KV blocks");
+  std::vector<int32_t> phys(n);
+  for (int i = 0; i < n; ++i) phys[i] = alloc_block();  // refcount 1 each
+  std::vector<int32_t> refs(n, 0);
+  for (const auto& t : tables)
+    for (int32_t x : t) ++refs[x];
+  for (int i = 0; i < n; ++i) {
+    if (refs[i] == 0) {  // exported but referenced by nobody: give it back
+      release(phys[i]);
+      continue;
+    }
+    ref_[phys[i]] = refs[i];
+  }
+  for (size_t i = 0; i < seqs.size(); ++i) {
+    Seq s;
+    s.blocks.reserve(tables[i].size() + 8);
+    for (int32_t x : tables[i]) s.blocks.push_back(phys[x]);
+    s.len = lens[i];
+    seqs_.emplace(seqs[i], std::move(s));
+  }
+  return phys;
+}
+
 std::vector<std::pair<int32_t, int32_t>> BlockManager::take_copies() {
   std::vector<std::pair<int32_t, int32_t>> out;
   out.swap(copies_);

@@ -49,6 +49,25 @@ class BlockManager {
   int64_t slot(int64_t seq, int64_t pos) const;
   int refcount(int32_t block) const { return ref_[block]; }
 
+  // Extra blocks one append_token on each of `seqs` may need (upper bound: every sharer of a shared
+  // partial last block is counted as a copy-on-write).
+  int64_t append_cost_total(const std::vector<int64_t>& seqs) const;
+
+  // ---- preemption by swapping (exact: the KV bytes leave and come back unchanged) ----
+  // A group of sequences (forked: they share blocks) is exported as its distinct blocks in first-use
+  // order plus, per sequence, its table as indices into that list; the sequences are then freed.  The
+  // caller copies the listed blocks' KV out BEFORE any later work can reuse them (stream order).
+  struct Swapped {
+    std::vector<int32_t> blocks;                 // distinct physical blocks, first-use order
+    std::vector<std::vector<int32_t>> tables;    // per sequence: indices into `blocks`
+    std::vector<int64_t> lens;
+  };
+  Swapped swap_out(const std::vector<int64_t>& seqs);
+  // Re-create the sequences on `n` fresh blocks with the exported structure (shared blocks shared again,
+  // refcount = number of referencing sequences); returns the new physical block of each exported index.
+  std::vector<int32_t> swap_in(const std::vector<int64_t>& seqs, int n, const std::vector<std::vector<int32_t>>& tables,
+                               const std::vector<int64_t>& lens);
+
   // Copy-on-write copies queued since the last call (src, dst); cleared by this call.
   std::vector<std::pair<int32_t, int32_t>> take_copies();
 

@@ -181,7 +181,7 @@ class LocalChatClient(ChatClient):
         last_err: Optional[ChatError] = None
         for name in names:
             try:
-                stream, _group = self._start(self.services[name], name, request)
+                stream, _group = self._start(self.services[name], name, request, ctx=ctx)
             except ChatError as e:
                 last_err = e
                 continue
@@ -213,7 +213,8 @@ class LocalChatClient(ChatClient):
         finally:
             await stream.aclose()
 
-    def _start(self, svc: EngineService, name: str, request: C.ChatCompletionCreateParams, embed: Optional[str] = None):
+    def _start(self, svc: EngineService, name: str, request: C.ChatCompletionCreateParams, embed: Optional[str] = None,
+               ctx: Any = None):
         """Validate, render and submit one attempt; returns (its not yet started chunk generator, the
         engine group).  ``embed``: the EngineGroup workers also embed the finished candidates."""
         tok = svc.engine.tokenizer
@@ -234,7 +235,10 @@ class LocalChatClient(ChatClient):
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         try:
-            group = svc.submit(ids, sp, n, loop, q, **({"embed": embed} if embed else {}))
+            kw = {"embed": embed} if embed else {}
+            if isinstance(ctx, dict) and (ctx.get("priority") or ctx.get("deadline") is not None):
+                kw["ctx"] = ctx
+            group = svc.submit(ids, sp, n, loop, q, **kw)
         except ValueError as e:
             raise ChatError.invalid_request(str(e))
         cid = f"chatcmpl-{uuid.uuid4().hex}"
@@ -306,6 +310,8 @@ class LocalChatClient(ChatClient):
                 choices: Dict[int, C.StreamChoice] = {}
                 for ev in evs:
                     if isinstance(ev, EngineFailure):
+                        if ev.kind == "deadline":
+                            raise ChatError.stream_timeout()
                         raise ChatError.engine(ev.message)
                     i = ev.seq.index
                     completion_tokens += 1

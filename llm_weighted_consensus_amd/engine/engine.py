@@ -11,8 +11,15 @@ copy-on-write fork, `prepare_decode_into`: per-step batch tables written straigh
 batch bucket into a hipGraph (torch.cuda.CUDAGraph on ROCm) so a step is one graph replay plus the
 fused sampler launch.
 
-Admission control reserves worst-case KV for (prompt + n * max_tokens), so a running sequence can
-never run out of blocks and no preemption path is needed; 288 GB of HBM3E makes this cheap.
+KV admission and over-subscription: a group is admitted against a RESERVATION of its prompt blocks plus
+``kv_reserve_tokens`` of growth per sequence (not n * max_tokens: a voter passing a large ``max_tokens``
+through, reference src/score/llm/mod.rs:44,56, would otherwise throttle the whole GPU), and the physical
+pool must hold the prompt plus one block per sequence above a watermark.  Sequences that grow past their
+reservation take blocks from the pool; when a decode step would need more blocks than are free, the
+YOUNGEST running groups are preempted by SWAPPING: their distinct KV blocks (the shared prompt blocks
+once) are copied to pinned host memory in stream order and the blocks freed; they resume, oldest first
+and before any new admission, when the pool can hold them again — KV bytes come back unchanged, so a
+preempted request produces exactly the tokens of an uninterrupted run.
 """
 from __future__ import annotations
 
@@ -106,6 +113,10 @@ class SequenceGroup:
         self.timer = RequestTimer()
         self.prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         self.pf_pos = -1  # chunked prefill: prompt tokens already in the KV cache (-1 = not started)
+        # request context (context.RequestContext): admission priority, deadline, trace id
+        self.priority = 0
+        self.deadline: Optional[float] = None
+        self.trace_id: Optional[str] = None
 
     @property
     def finished(self) -> bool:
@@ -251,12 +262,24 @@ class _Step:
         self.first = None   # first-token step after a prefill: (pinned host outputs, groups)
 
 
+@dataclass
+class _SwapRecord:
+    """A preempted group: its live sequences' KV (distinct blocks) in pinned host memory."""
+    group: "SequenceGroup"
+    seqs: List[Sequence]
+    host: torch.Tensor          # [L, 2, n, block_elems] pinned
+    tables: List[List[int]]     # per sequence: indices into the n saved blocks
+    lens: List[int]
+    event: Optional[torch.cuda.Event]
+
+
 class LLMEngine:
     def __init__(self, model, tokenizer, *, block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_memory_fraction: float = 0.85, max_batch: int = 512, max_model_len: int = 4096,
                  use_graphs: bool = True, prefill_token_budget: int = 16384, prefix_sharing: bool = True,
                  cascade_min_batch: int = 128, tune_gc: bool = True, constrained_logprobs: bool = False,
-                 prefix_caching: bool = False, chunked_prefill: int = 0):
+                 prefix_caching: bool = False, chunked_prefill: int = 0, kv_reserve_tokens: Optional[int] = 256,
+                 decode_splits: Optional[int] = None):
         self.model = model
         self.cfg = model.cfg
         self.tokenizer = tokenizer
@@ -288,6 +311,12 @@ class LLMEngine:
         self.prefix_caching = prefix_caching
         self.bm.set_prefix_caching(prefix_caching)
         self.free_blocks_unreserved = num_blocks
+        # growth reserved per sequence at admission (None: worst case, prompt + max_tokens — no preemption)
+        self.kv_reserve_tokens = kv_reserve_tokens
+        self.kv_watermark = max(1, num_blocks // 100)
+        self.swapped: Deque[_SwapRecord] = deque()
+        # split-K factor of the plain paged-decode kernel (None: chosen per batch bucket)
+        self.decode_splits = decode_splits
         self.use_graphs = use_graphs
         self.prefix_sharing = prefix_sharing
         # decode batches >= this bucket use the cascade (shared-prompt) attention kernel; smaller ones
@@ -310,10 +339,12 @@ class LLMEngine:
         self.free_count_rows = list(range(max_batch))
         self.bias: Optional[torch.Tensor] = None    # [max_batch, V] f32, lazily
         self.free_bias_rows = list(range(max_batch))
-        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_cache_tokens": 0}
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_cache_tokens": 0,
+                      "preemptions": 0, "swapped_blocks": 0}
         self._mask_rows_of: Optional[Dict[tuple, int]] = None  # mask content -> device mask table row
         self._mask_limit = 4096
         self.faults = FaultInjector.from_env()
+        self._deadlines = 0  # groups ever submitted with a deadline (expire() is a no-op until one is)
         # step() returns TokenEvents only when asked (callbacks always get theirs)
         self.collect_events = False
         if tune_gc:
@@ -324,9 +355,12 @@ class LLMEngine:
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: Seq[int], params: SamplingParams, n: int = 1,
                     callback: Optional[Callable[[TokenEvent], None]] = None,
-                    prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SequenceGroup:
+                    prefilled: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, ctx=None) -> SequenceGroup:
         """Queue a request of `n` sequences.  ``prefilled`` = (kv [L, 2, nblocks, block_elems],
-        logits [V]) starts it from a prompt prefilled elsewhere (see :meth:`export_prefill`)."""
+        logits [V]) starts it from a prompt prefilled elsewhere (see :meth:`export_prefill`).  ``ctx`` (a
+        context.RequestContext or a dict with ``priority`` / ``deadline`` / ``trace_id``): requests are
+        admitted by priority (higher first, FIFO within one) and dropped once their deadline passes
+        (:meth:`expire`)."""
         params.validate(self.cfg.vocab_size)
         if params.constraint is not None and hasattr(params.constraint, "bind"):
             params.constraint.bind(self.tokenizer, self.cfg.vocab_size)  # a constraint that came through a pipe
@@ -337,12 +371,25 @@ class LLMEngine:
                              f"max_model_len ({self.max_model_len})")
         g = SequenceGroup(self, list(prompt_ids), params, n, callback)
         g.prefilled = prefilled
+        if isinstance(ctx, dict):
+            g.priority = int(ctx.get("priority", 0) or 0)
+            g.deadline = ctx.get("deadline")
+            g.trace_id = ctx.get("trace_id")
+            g.timer.trace_id = g.trace_id
         with self.lock:
-            self.waiting.append(g)
+            if g.priority and self.waiting and self.waiting[-1].priority < g.priority:
+                # ahead of every waiting request of lower priority, behind its own priority's
+                i = next(k for k, x in enumerate(self.waiting) if x.priority < g.priority)
+                self.waiting.insert(i, g)
+            else:
+                self.waiting.append(g)
+            if g.deadline is not None:
+                self._deadlines += 1
         return g
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or bool(self.running) or bool(self.prefilling) or self.inflight is not None
+        return (bool(self.waiting) or bool(self.running) or bool(self.prefilling) or bool(self.swapped)
+                or self.inflight is not None)
 
     def step(self) -> List[TokenEvent]:
         """Run one engine iteration: admit+prefill waiting groups if any fit, else one decode step.
@@ -352,6 +399,8 @@ class LLMEngine:
         host syncs on and post-processes step t, so detokenisation, stop checks and callbacks overlap
         the GPU.  A sequence that finishes at step t has one discarded row in step t+1."""
         self.faults.on_step()
+        if self.swapped:
+            self._swap_in()
         if self.chunked_prefill > 0:
             return self._step_chunked()
         events: List[TokenEvent] = []
@@ -379,17 +428,24 @@ class LLMEngine:
     def _group_reservation(self, g: SequenceGroup) -> int:
         bs = self.block_size
         prompt_blocks = (len(g.prompt_ids) + bs - 1) // bs
-        per_child = (len(g.prompt_ids) + g.params.max_tokens + bs - 1) // bs - len(g.prompt_ids) // bs
+        grow = g.params.max_tokens if self.kv_reserve_tokens is None else min(g.params.max_tokens,
+                                                                               self.kv_reserve_tokens)
+        per_child = (len(g.prompt_ids) + grow + bs - 1) // bs - len(g.prompt_ids) // bs
         return prompt_blocks + g.n * (per_child + 1)
 
+    def _physical_need(self, g: SequenceGroup) -> int:
+        """Blocks the pool must have free to admit ``g``: its prompt, one growth block per sequence and the
+        watermark (sequences past their reservation draw on the same pool)."""
+        return (len(g.prompt_ids) + self.block_size - 1) // self.block_size + g.n + self.kv_watermark
+
     def _first_waiting_fits(self) -> bool:
-        if not self.waiting:
+        if not self.waiting or self.swapped:  # preempted groups resume before anything new is admitted
             return False
         g = self.waiting[0]
         live = sum(1 for s in self.running if not s.finished) + sum(x.n for x in self.prefilling)
-        return live + g.n <= self.max_batch and (self._group_reservation(g) <= self.free_blocks_unreserved
-                                                 or (not self.running and self.inflight is None
-                                                     and not self.prefilling))
+        idle = not self.running and self.inflight is None and not self.prefilling
+        return live + g.n <= self.max_batch and ((self._group_reservation(g) <= self.free_blocks_unreserved
+                                                  and self._physical_need(g) <= self.bm.num_free) or idle)
 
     def _admit(self) -> List[SequenceGroup]:
         out, tokens = [], 0
@@ -398,7 +454,8 @@ class LLMEngine:
             need = self._group_reservation(g)
             if len(self.running) + sum(x.n for x in self.prefilling) + sum(x.n for x in out) + g.n > self.max_batch:
                 break
-            if need > self.free_blocks_unreserved:
+            phys = self._physical_need(g) + sum(self._physical_need(x) - self.kv_watermark for x in out)
+            if need > self.free_blocks_unreserved or phys > self.bm.num_free:
                 if not self.running and not out and not self.prefilling:
                     self.waiting.popleft()
                     raise RuntimeError("request needs more KV blocks than the cache holds")
@@ -728,6 +785,8 @@ class LLMEngine:
             # split-K so that a launch has >= ~1024 (batch, kv-head, split) workgroups
             splits = max(1, min(16, -(-1024 // (Bb * self.cfg.kv_heads))))
             splits = min(splits, max(1, self.width // 4))
+            if self.decode_splits is not None:
+                splits = int(self.decode_splits)
             max_tiles = 0
             if self.prefix_sharing and Bb >= self.cascade_min_batch:
                 per = ops.cascade_rows_per_tile(self.cfg.heads // self.cfg.kv_heads)
@@ -983,6 +1042,12 @@ class LLMEngine:
         seqs = [s for s in self.running if not s.finished and s.n_launched < s.params.max_tokens]
         if not seqs:
             return events + self._drain()
+        if self.bm.append_cost_total([s.id for s in seqs]) > self.bm.num_free:
+            events += self._drain()  # nothing in flight: sequences can leave the batch
+            seqs = self._preempt_for_growth()
+            if not seqs:
+                return events
+            constrained = any(s.constraint_state is not None for s in self.running)
         with span("decode.launch"):
             cur = self._launch(seqs, sample=not constrained)
         prev, self.inflight = self.inflight, cur
@@ -993,6 +1058,64 @@ class LLMEngine:
             self._launch_sample(cur)
         self.running = [s for s in self.running if not s.finished]
         return events
+
+    # ------------------------------------------------------------------ preemption (swap)
+    def _preempt_for_growth(self) -> List[Sequence]:
+        """Swap out the youngest running groups until one decode step of the rest fits the free pool;
+        returns the sequences left to decode.  Called with no step in flight."""
+        while True:
+            seqs = [s for s in self.running if not s.finished and s.n_launched < s.params.max_tokens]
+            if not seqs or self.bm.append_cost_total([s.id for s in seqs]) <= self.bm.num_free:
+                return seqs
+            groups = sorted({s.group.id: s.group for s in self.running if not s.finished}.values(),
+                            key=lambda g: g.id)
+            if len(groups) <= 1:
+                raise RuntimeError("KV cache exhausted by a single request (raise num_blocks or lower max_tokens)")
+            self._swap_out(groups[-1])
+
+    def _swap_out(self, g: SequenceGroup) -> None:
+        live = [s for s in g.seqs if not s.finished and self.bm.has_sequence(s.id)]
+        blocks, tables, lens = self.bm.swap_out([s.id for s in live])
+        dev = self.device
+        if blocks:
+            kv = self.cache.pool.index_select(2, torch.tensor(blocks, dtype=torch.int64, device=dev))
+            host = torch.empty(kv.shape, dtype=kv.dtype, pin_memory=dev.type == "cuda")
+            host.copy_(kv, non_blocking=True)  # stream-ordered before any later write to the freed blocks
+        else:
+            host = torch.empty(0)
+        ev = None
+        if dev.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        self.swapped.append(_SwapRecord(g, live, host, [list(t) for t in tables], list(lens), ev))
+        ids = {s.id for s in live}
+        self.running = [s for s in self.running if s.id not in ids]
+        self.free_blocks_unreserved += g.reserved_blocks
+        g.reserved_blocks = 0
+        self._comp_cache = (None, None)
+        self.stats["preemptions"] += 1
+        self.stats["swapped_blocks"] += len(blocks)
+
+    def _swap_in(self) -> None:
+        """Resume preempted groups, oldest preemption first, while the pool holds them (plus one growth
+        block per sequence and the watermark)."""
+        while self.swapped:
+            rec = self.swapped[0]
+            n = rec.host.shape[2] if rec.host.dim() == 4 else 0
+            need = self._group_reservation(rec.group)
+            if (n + len(rec.seqs) + self.kv_watermark > self.bm.num_free
+                    or (need > self.free_blocks_unreserved and (self.running or self.inflight is not None))):
+                return
+            self.swapped.popleft()
+            phys = self.bm.swap_in([s.id for s in rec.seqs], n, rec.tables, rec.lens)
+            if n:
+                dev = self.device
+                kv = rec.host.to(dev, non_blocking=True)
+                self.cache.pool.index_copy_(2, torch.tensor(phys, dtype=torch.int64, device=dev), kv)
+            rec.group.reserved_blocks = need
+            self.free_blocks_unreserved -= need
+            self.running.extend(s for s in rec.seqs if not s.finished)
+            self._comp_cache = (None, None)
 
     # ------------------------------------------------------------------ sampling + bookkeeping
     def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[TokenEvent]:
@@ -1133,6 +1256,35 @@ class LLMEngine:
                 self.free_bias_rows.append(g.bias_row)
                 g.bias_row = -1
 
+    # ------------------------------------------------------------------ deadlines
+    def expire(self, now: Optional[float] = None) -> List[SequenceGroup]:
+        """Drop every group whose request deadline has passed — waiting, prefilling, preempted or
+        generating (aborted between steps) — and return them; the caller tells their clients."""
+        if not self._deadlines:
+            return []
+        now = time.monotonic() if now is None else now
+
+        def late(g):
+            return g.deadline is not None and now >= g.deadline and not g.finished
+
+        out = []
+        with self.lock:
+            for g in [g for g in self.waiting if late(g)]:
+                self.waiting.remove(g)
+                for s in g.seqs:
+                    s.finished, s.finish_reason = True, "deadline"
+                out.append(g)
+        seen = set()
+        for g in [g for g in self.prefilling if late(g)] + [r.group for r in self.swapped if late(r.group)] + \
+                [s.group for s in self.running if late(s.group)]:
+            if g.id not in seen:
+                seen.add(g.id)
+                self.abort(g)
+                for s in g.seqs:
+                    s.finish_reason = "deadline"
+                out.append(g)
+        return out
+
     # ------------------------------------------------------------------ cancellation / failure
     def abort(self, g: SequenceGroup) -> None:
         """Drop a group (client went away): frees its blocks and reservation, no more events."""
@@ -1144,6 +1296,19 @@ class LLMEngine:
                 return
         if any(x is g for x in self.prefilling):
             self._drop_prefilling(g, "abort")
+            return
+        rec = next((r for r in self.swapped if r.group is g), None)
+        if rec is not None:  # preempted: its blocks are already free, only the host copy goes
+            self.swapped.remove(rec)
+            for s in g.seqs:
+                if not s.finished:
+                    s.finished, s.finish_reason = True, "abort"
+                    if s.count_row >= 0:
+                        self.free_count_rows.append(s.count_row)
+                        s.count_row = -1
+            if g.bias_row >= 0:
+                self.free_bias_rows.append(g.bias_row)
+                g.bias_row = -1
             return
         for s in g.seqs:
             if not s.finished:
@@ -1164,6 +1329,11 @@ class LLMEngine:
             except Exception:  # pragma: no cover - best effort cleanup
                 pass
         self.prefilling = []
+        for rec in list(self.swapped):
+            groups[rec.group.id] = rec.group
+            for s in rec.seqs:
+                s.finished, s.finish_reason = True, "error"
+        self.swapped.clear()
         for s in self.running:
             groups[s.group.id] = s.group
         for g in groups.values():

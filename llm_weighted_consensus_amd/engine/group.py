@@ -89,6 +89,14 @@ def _put_all(batch) -> None:
         q.put_nowait(ev)
 
 
+def _wire_ctx(ctx) -> Optional[dict]:
+    """The part of a request context the worker's scheduler uses (priority, deadline, trace id), as a plain
+    dict.  Deadlines are time.monotonic() values: CLOCK_MONOTONIC is shared by every process of the host."""
+    if not isinstance(ctx, dict) or (not ctx.get("priority") and ctx.get("deadline") is None):
+        return None  # nothing for the scheduler
+    return {"priority": ctx.get("priority", 0), "deadline": ctx.get("deadline"), "trace_id": ctx.get("trace_id")}
+
+
 def _resolve(path: str):
     mod, _, fn = path.partition(":")
     return getattr(importlib.import_module(mod), fn)
@@ -119,6 +127,7 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
             if kind == "submit":
                 _, rid, prompt, params, n, offset = msg[:6]
                 embed = msg[6] if len(msg) > 6 else None
+                wctx = msg[7] if len(msg) > 7 else None
                 texts = [""] * n if embed else None
                 if embed:
                     emb_req[rid] = (embed, offset, texts)
@@ -130,7 +139,8 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                         texts[ev.seq.index] += ev.text
 
                 try:
-                    groups[rid] = engine.add_request(prompt, params, n=n, callback=cb)
+                    kw = {"ctx": wctx} if wctx is not None else {}
+                    groups[rid] = engine.add_request(prompt, params, n=n, callback=cb, **kw)
                 except ValueError as e:
                     ev_q.put(("error", wid, (rid, str(e))))
             elif kind == "abort":
@@ -141,6 +151,11 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                 msg = req_q.get_nowait()
             except pyqueue.Empty:
                 msg = None
+        for g in (engine.expire() if hasattr(engine, "expire") else ()):  # request deadlines (RequestContext)
+            rid = next((r for r, gg in groups.items() if gg is g), None)
+            if rid is not None:
+                groups.pop(rid, None)
+                ev_q.put(("error", wid, (rid, "request deadline exceeded", "deadline")))
         if engine.has_work():
             try:
                 engine.step()
@@ -233,7 +248,8 @@ class EngineGroup:
     def embeds_in_workers(self, model: str) -> bool:
         return model in (self.spec.get("embed_models") or {})
 
-    def submit(self, prompt_ids, params: SamplingParams, n: int, loop, queue, embed: Optional[str] = None) -> GroupRequest:
+    def submit(self, prompt_ids, params: SamplingParams, n: int, loop, queue, embed: Optional[str] = None,
+               ctx=None) -> GroupRequest:
         """``embed``: an embedding model every worker embeds its finished candidates with; the rows arrive
         in ``req.emb_future`` (a future of ``loop``)."""
         self._check_health()
@@ -259,7 +275,7 @@ class EngineGroup:
                 p = _Portion(w, offset, m, replace(params, seed=base, seed_offset=offset))
                 req.portions.append(p)
                 self.load_of[w] += m
-                self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset, embed))
+                self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset, embed, _wire_ctx(ctx)))
                 offset += m
         return req
 
@@ -316,12 +332,14 @@ class EngineGroup:
                 self.alive[wid] = False
                 self.failures += 1
             elif kind == "error":
-                rid, msg = payload
+                rid, msg = payload[:2]
+                fkind = payload[2] if len(payload) > 2 else "error"
                 with self._lock:
                     req = self.requests.pop(rid, None)
                 if req is not None:
-                    self.failures += 1
-                    self._deliver(req, EngineFailure(msg))
+                    if fkind != "deadline":
+                        self.failures += 1
+                    self._deliver(req, EngineFailure(msg, fkind))
             elif kind == "tokens":
                 self._on_tokens(wid, payload)
             elif kind in ("emb", "emb_err"):
@@ -443,4 +461,5 @@ def build_engine(spec: dict, wid: int):
                      kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),
                      prefix_caching=bool(spec.get("prefix_caching", True)),
                      chunked_prefill=int(spec.get("chunked_prefill", 0)),
-                     constrained_logprobs=bool(spec.get("constrained_logprobs", False)))
+                     constrained_logprobs=bool(spec.get("constrained_logprobs", False)),
+                     kv_reserve_tokens=spec.get("kv_reserve_tokens", 256))

@@ -21,6 +21,7 @@ from .sampling import SamplingParams
 @dataclass
 class EngineFailure:
     message: str
+    kind: str = "error"  # "error" (engine exception) | "deadline" (the request's deadline passed)
 
 
 class EngineService:
@@ -38,14 +39,15 @@ class EngineService:
 
     # ------------------------------------------------------------------ async API
     def submit(self, prompt_ids, params: SamplingParams, n: int, loop: asyncio.AbstractEventLoop,
-               queue: asyncio.Queue) -> SequenceGroup:
+               queue: asyncio.Queue, ctx=None) -> SequenceGroup:
         # events are buffered per event loop during an engine step and handed over with ONE thread-safe
         # call per loop per step (a per-token call_soon_threadsafe is a self-pipe write each, and hundreds
         # per step of them compete with the engine thread for the GIL)
         def cb(ev: TokenEvent):
             self._pending.setdefault(loop, []).append((queue, ev))
 
-        g = self.engine.add_request(prompt_ids, params, n=n, callback=cb)
+        kw = {"ctx": ctx} if ctx is not None else {}
+        g = self.engine.add_request(prompt_ids, params, n=n, callback=cb, **kw)
         g.loop, g.queue = loop, queue
         with self._cv:
             self._cv.notify()
@@ -79,6 +81,10 @@ class EngineService:
                 aborts, self._aborts = self._aborts, []
             for g in aborts:
                 eng.abort(g)
+            for g in (eng.expire() if hasattr(eng, "expire") else ()):  # request deadlines (RequestContext)
+                loop, q = getattr(g, "loop", None), getattr(g, "queue", None)
+                if loop is not None:
+                    loop.call_soon_threadsafe(q.put_nowait, EngineFailure("request deadline exceeded", "deadline"))
             self._flush()  # events an abort produced
             if not eng.has_work():
                 continue

@@ -18,6 +18,7 @@ from starlette.requests import Request
 from starlette.responses import JSONResponse, Response, StreamingResponse
 from starlette.routing import Route
 
+from ..context import RequestContext
 from ..errors import ResponseError, ScoreError, StatusError
 from ..schema import chat as C
 from ..schema import score as S
@@ -89,6 +90,8 @@ class AppState:
         self.archive = archive
         self.registry = registry
         self.metrics = Metrics()
+        # deadline of a request without an x-timeout-ms header (None: none); config LWC_REQUEST_TIMEOUT_MS
+        self.default_timeout_s: Optional[float] = None
 
 
 def _json(obj: Any, status: int = 200) -> Response:
@@ -154,16 +157,17 @@ def _archived(stream: AsyncIterator, finish: Callable, store: Optional[Callable]
 
 def create_app(state: AppState) -> Starlette:
     async def chat_completions(request: Request):
+        ctx = RequestContext.from_headers(request.headers, state.default_timeout_s)
         req, err = await _body(request, C.ChatCompletionCreateParams)
         if err is not None:
             return err
         state.metrics.inc("chat_requests_total")
         try:
             if req.stream:
-                stream = await state.chat.create_streaming(None, req)
+                stream = await state.chat.create_streaming(ctx, req)
                 return _sse(_archived(stream, C.ChatCompletion.from_chunk,
                                       state.archive.store_chat if state.archive is not None else None))
-            resp = await state.chat.create_unary(None, req)
+            resp = await state.chat.create_unary(ctx, req)
             if state.archive is not None:
                 state.archive.store_chat(resp)
             return _json(resp.to_obj())
@@ -171,22 +175,24 @@ def create_app(state: AppState) -> Starlette:
             return _error(e)
 
     async def score_completions(request: Request):
+        ctx = RequestContext.from_headers(request.headers, state.default_timeout_s)
         req, err = await _body(request, S.ScoreCompletionCreateParams)
         if err is not None:
             return err
         state.metrics.inc("score_requests_total")
         try:
             if req.stream:
-                stream = await state.score.create_streaming(None, req)
+                stream = await state.score.create_streaming(ctx, req)
                 return _sse(_archived(stream, S.ScoreCompletion.from_chunk,
                                       state.archive.store_score if state.archive is not None else None))
-            resp = await state.score.create_unary(None, req)
+            resp = await state.score.create_unary(ctx, req)
             state.metrics.inc("score_answers_total")
             return _json(resp.to_obj())
         except StatusError as e:
             return _error(e)
 
     async def multichat_completions(request: Request):
+        ctx = RequestContext.from_headers(request.headers, state.default_timeout_s)
         if state.multichat is None:
             return _error(ScoreError.not_implemented("multichat is not configured"))
         req, err = await _body(request, S.ScoreCompletionCreateParams)
@@ -195,14 +201,15 @@ def create_app(state: AppState) -> Starlette:
         state.metrics.inc("multichat_requests_total")
         try:
             if req.stream:
-                stream = await state.multichat.create_streaming(None, req)
+                stream = await state.multichat.create_streaming(ctx, req)
                 return _sse(_archived(stream, S.MultichatCompletion.from_chunk,
                                       state.archive.store_multichat if state.archive is not None else None))
-            return _json((await state.multichat.create_unary(None, req)).to_obj())
+            return _json((await state.multichat.create_unary(ctx, req)).to_obj())
         except StatusError as e:
             return _error(e)
 
     async def consensus_completions(request: Request):
+        ctx = RequestContext.from_headers(request.headers, state.default_timeout_s)
         if state.consensus is None:
             return _error(ScoreError.not_implemented("consensus is not configured"))
         try:
@@ -214,7 +221,7 @@ def create_app(state: AppState) -> Starlette:
             return Response(f"Failed to deserialize the JSON body into the target type: {e}", status_code=422)
         state.metrics.inc("consensus_requests_total")
         try:
-            out = await state.consensus.create_unary(None, req, emb_model, tau)
+            out = await state.consensus.create_unary(ctx, req, emb_model, tau)
             state.metrics.inc("consensus_answers_total")
             return _json(out.to_obj())
         except StatusError as e:

@@ -23,6 +23,11 @@ variables configure the local engine:
   LWC_CONSTRAINED_LOGPROBS  1: constrained (json_schema / tool-call) voters get logprobs over the allowed
                     tokens, so a key letter's vote is the exact restricted softmax over its siblings
                     instead of whatever of them made the raw top-k (default 0 = reference semantics)
+  LWC_KV_RESERVE_TOKENS  generation tokens reserved per sequence at admission (default 256; "none" = the
+                    whole max_tokens, no preemption): longer generations draw on the shared pool and the
+                    youngest requests are preempted by swapping their KV to host memory when it runs dry
+  LWC_REQUEST_TIMEOUT_MS  default request deadline (an x-timeout-ms header overrides it per request; the
+                    engine drops or aborts a request past its deadline); x-priority orders admission
   LWC_SHARD_VOTERS  1: voter-sharded deployment — one server process per GPU under torchrun / a
                     launcher (RANK / WORLD_SIZE / LOCAL_RANK); rank 0 serves HTTP and broadcasts each
                     score request, every rank runs its share of the voters (llm index % world) on its
@@ -82,6 +87,8 @@ class Config:
     registry_path: Optional[str] = None
     fault: Optional[str] = None
     shard_voters: bool = False
+    kv_reserve_tokens: Optional[int] = 256
+    request_timeout_ms: Optional[int] = None
 
     @classmethod
     def from_env(cls, dotenv: bool = True) -> "Config":
@@ -120,6 +127,11 @@ class Config:
         c.training_table_path = e.get("LWC_TRAINING_TABLE_PATH")
         c.fault = e.get("LWC_FAULT")
         c.shard_voters = e.get("LWC_SHARD_VOTERS", "0") == "1"
+        if "LWC_KV_RESERVE_TOKENS" in e:
+            v = e["LWC_KV_RESERVE_TOKENS"].strip().lower()
+            c.kv_reserve_tokens = None if v in ("", "none", "max") else int(v)
+        if e.get("LWC_REQUEST_TIMEOUT_MS"):
+            c.request_timeout_ms = int(e["LWC_REQUEST_TIMEOUT_MS"])
         return c
 
     def api_bases(self):

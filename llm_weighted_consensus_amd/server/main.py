@@ -49,7 +49,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 # that generated them, only the unit rows travel to the front end
                 wspec = dict(spec, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
                              prefix_caching=cfg.prefix_caching, constrained_logprobs=cfg.constrained_logprobs,
-                             chunked_prefill=cfg.chunked_prefill, embed_models=dict(cfg.embed_models))
+                             chunked_prefill=cfg.chunked_prefill, embed_models=dict(cfg.embed_models),
+                             kv_reserve_tokens=cfg.kv_reserve_tokens)
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
                                                                       dcfg.eos_token_id))
@@ -59,7 +60,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
 
             eng = build_engine(dict(spec, device=cfg.gpu, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
                                     prefix_caching=cfg.prefix_caching, chunked_prefill=cfg.chunked_prefill,
-                                    constrained_logprobs=cfg.constrained_logprobs), 0)
+                                    constrained_logprobs=cfg.constrained_logprobs,
+                                    kv_reserve_tokens=cfg.kv_reserve_tokens), 0)
             services[name] = EngineService(eng, name)
             services[name].chat_template = spec.get("chat_template")
     remote = None
@@ -85,9 +87,12 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     score = ScoreClient(chat_client, registry,
                         WeightFetchers(training_table=TrainingTableWeights(tt_embed, path=cfg.training_table_path)),
                         archive=archive)
-    return AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
-                                                                                          archive),
-                    embedders=embedders, services=services, archive=archive, registry=registry)
+    state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
+                                                                                           archive),
+                     embedders=embedders, services=services, archive=archive, registry=registry)
+    if cfg.request_timeout_ms:
+        state.default_timeout_s = cfg.request_timeout_ms / 1000.0
+    return state
 
 
 def follower_config(cfg: Config, rank: int) -> Config:

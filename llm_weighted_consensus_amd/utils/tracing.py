@@ -100,9 +100,10 @@ def span(name: str):
 class RequestTimer:
     """Queue / TTFT / TPOT of one request (a sequence group); all times host-side perf_counter."""
 
-    __slots__ = ("t_submit", "t_start", "t_first", "t_last", "tokens")
+    __slots__ = ("t_submit", "t_start", "t_first", "t_last", "tokens", "trace_id")
 
     def __init__(self):
+        self.trace_id = None  # the request context's trace id (context.RequestContext), when given
         self.t_submit = time.perf_counter()
         self.t_start: Optional[float] = None
         self.t_first: Optional[float] = None

@@ -230,3 +230,31 @@ def test_run_prefill_frees_parents_when_a_later_prompt_does_not_fit():
         with pytest.raises(RuntimeError, match="out of KV blocks"):
             LLMEngine._run_prefill(fake, prompts, [-1, -2], use_cache=use_cache)
         assert bm.num_sequences == 0 and bm.num_free == 6 and not bm.has_sequence(-1)
+
+
+def test_block_manager_swap_out_in_keeps_sharing():
+    """Preemption by swapping: a forked group leaves as its distinct blocks + per-sequence index tables
+    and comes back on fresh blocks with the same sharing (shared prompt blocks refcounted again)."""
+    from llm_weighted_consensus_amd._runtime import BlockManager
+
+    bm = BlockManager(64, 16)
+    bm.add_sequence(1, 40)
+    for c in (2, 3):
+        bm.fork(1, c)
+    bm.free_sequence(1)
+    for c in (2, 3):
+        for _ in range(30):
+            bm.append_token(c)
+    assert bm.append_cost_total([2, 3]) == 0
+    before = {c: list(bm.block_table(c)) for c in (2, 3)}
+    blocks, tables, lens = bm.swap_out([2, 3])
+    assert bm.num_free == 64 and not bm.has_sequence(2)
+    assert len(blocks) == len(set(blocks)) == len(set(before[2]) | set(before[3]))
+    assert [[blocks[i] for i in t] for t in tables] == [before[2], before[3]]
+    phys = bm.swap_in([5, 6], len(blocks), tables, lens)
+    assert [bm.length(s) for s in (5, 6)] == lens == [70, 70]
+    shared = [phys[i] for i in set(tables[0]) & set(tables[1])]
+    assert shared and all(bm.refcount(b) == 2 for b in shared)
+    for s in (5, 6):
+        bm.free_sequence(s)
+    assert bm.num_free == 64
