@@ -16,6 +16,16 @@
 //                  C: lane reg r = O[query 4g + r][dim 16n + r16]
 // so P never leaves registers.  Online softmax in the log2 domain; rows are finite-initialised
 // (-1e30) so fully-masked tiles cannot produce NaN.
+//
+// PAGED mode (mixed chunked prefill, engine/engine.py): the keys / values of sequence s are read straight
+// from the paged cache through its block table — K [NB, Hkv, 16, D] token-major, V [NB, Hkv, 4, D, 4]
+// 4-token interleaved (the decode layout) — with key positions [0, k_lens[s]) and the sequence's queries
+// the last len_q of them (a prompt chunk after its earlier chunks, or after a cached prefix).  A 32-key
+// tile is exactly two blocks: each operand tile is two contiguous 4 KiB segments.  K is staged into the
+// same swizzled row image; V keeps the interleaved layout in LDS (odd token groups XOR byte bit 7), where
+// one ds_read_b64 returns a lane's 4 consecutive keys of one dim — the PV B operand without a transpose.
+// V elements of keys past k_lens (the tail of the last block, stale bytes) are zeroed: P is 0 there, but
+// 0 x a stale Inf / NaN would not be.  No per-layer gather of the cached keys into contiguous buffers.
 #include "common.h"
 
 namespace lwc {
@@ -43,9 +53,13 @@ struct PrefillParams {
   int Hq, Hkv, nseq, max_tiles;
   float scale;
   int causal;
+  // PAGED: block tables [nseq, bt_stride] of the key cache; k_lens [nseq] key positions per sequence
+  const int* block_tables;
+  const int* k_lens;
+  int bt_stride;
 };
 
-template <int D>
+template <int D, bool PAGED>
 __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   constexpr int CPR = D / 8;                // 16-byte chunks per row
   constexpr int KS = D / 32;                // k-steps for S
@@ -60,9 +74,11 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   const int s0 = p.cu_seqlens[seq], len = p.cu_seqlens[seq + 1] - s0;
   const int q0 = qtile * kQT;
   if (q0 >= len) return;  // whole workgroup exits together (uniform)
-  // keys: the sequence's own rows, or (cached prefix) a longer key range whose last len rows are the queries
-  const int ks0 = p.cu_seqlens_k ? p.cu_seqlens_k[seq] : s0;
-  const int klen = p.cu_seqlens_k ? p.cu_seqlens_k[seq + 1] - ks0 : len;
+  // keys: the sequence's own rows, or (cached prefix / PAGED) a longer key range whose last len rows are
+  // the queries
+  const int ks0 = PAGED ? 0 : p.cu_seqlens_k ? p.cu_seqlens_k[seq] : s0;
+  const int klen = PAGED ? p.k_lens[seq] : p.cu_seqlens_k ? p.cu_seqlens_k[seq + 1] - ks0 : len;
+  const int* bt = PAGED ? p.block_tables + (size_t)seq * p.bt_stride : nullptr;
   const int qoff = klen - len;  // key position of query row 0
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -83,13 +99,58 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
 
   // staging registers
   uint4v stk[CH_PER_THREAD], stv[CH_PER_THREAD];
+  // PAGED: the two block ids of the tile being loaded, fetched one tile ahead (the block-table load is not
+  // on the critical path of the K / V loads)
+  int blk_nx[2] = {0, 0};
+  if constexpr (PAGED) {
+    blk_nx[0] = bt[0];
+    blk_nx[1] = bt[1];  // block tables hold >= 2 entries per 32-key tile
+  }
   auto gload = [&](int tile) {
+    int blk_cur[2] = {blk_nx[0], blk_nx[1]};
+    if constexpr (PAGED) {
+      if (tile + 1 < ntiles) {
+        blk_nx[0] = bt[2 * tile + 2];
+        blk_nx[1] = bt[2 * tile + 3];
+      }
+    }
+    // only the last tile of a key range needs the per-token V masking
+    const bool v_tail = PAGED && tile * kKT + kKT > klen;
 #pragma unroll
     for (int i = 0; i < CH_PER_THREAD; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int row = c / CPR, ch = c % CPR;
       const int key = tile * kKT + row;
-      if (c < CHUNKS && key < klen) {
+      if constexpr (PAGED) {
+        // K: chunk c = (key row, 16 B chunk) of the tile's two token-major block segments.  V: chunk c = byte
+        // 16c of the two interleaved segments [4 token groups][D][4] (block c / (CHUNKS / 2)).
+        if (c < CHUNKS) {
+          const int blk = row < 16 ? blk_cur[0] : blk_cur[1];
+          stk[i] = key < klen ? *reinterpret_cast<const uint4v*>(p.k + (((size_t)blk * p.Hkv + kvh) * 16 + row % 16) * D +
+                                                                 ch * 8)
+                              : uint4v{0, 0, 0, 0};
+          const int half = c / (CHUNKS / 2), b = (c % (CHUNKS / 2)) * 16;  // byte in the segment
+          const int vbase = tile * kKT + half * 16;                           // first key of the segment
+          if (vbase < klen) {
+            const int vblk = half == 0 ? blk_cur[0] : blk_cur[1];
+            uint4v v = *reinterpret_cast<const uint4v*>(reinterpret_cast<const char*>(
+                                                            p.v + ((size_t)vblk * p.Hkv + kvh) * 16 * D) + b);
+            if (v_tail) {
+              // 8 elements = 2 dims x tokens 4 grp + 0..3 (element e: token e & 3): zero the keys >= klen
+              const int t0 = vbase + 4 * (b / (D * 8));
+#pragma unroll
+              for (int w = 0; w < 4; ++w) {
+                const uint32_t lo = t0 + ((2 * w) & 3) < klen ? 0xffffu : 0u;
+                const uint32_t hi = t0 + ((2 * w + 1) & 3) < klen ? 0xffff0000u : 0u;
+                v[w] &= lo | hi;
+              }
+            }
+            stv[i] = v;
+          } else {
+            stv[i] = uint4v{0, 0, 0, 0};
+          }
+        }
+      } else if (c < CHUNKS && key < klen) {
         stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(ks0 + key) * p.k_stride + kvh * D + ch * 8);
         stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(ks0 + key) * p.v_stride + kvh * D + ch * 8);
       } else {
@@ -108,7 +169,12 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       const int row = c / CPR, ch = c % CPR;
       const int off = (row * CPR + (ch ^ (row & (CPR - 1)))) * 16;
       *reinterpret_cast<uint4v*>(kb + off) = stk[i];
-      *reinterpret_cast<uint4v*>(vb + off) = stv[i];
+      if constexpr (PAGED) {  // interleaved V image: odd token groups XOR byte bit 7 (ds_read_b64 banks)
+        const int b = c * 16;
+        *reinterpret_cast<uint4v*>(vb + (b ^ (((b / (D * 8)) & 1) << 7))) = stv[i];
+      } else {
+        *reinterpret_cast<uint4v*>(vb + off) = stv[i];
+      }
     }
   };
 
@@ -175,6 +241,22 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
     }
     // ---- O += P V, V columns via the hardware transpose read ----
     const int qq = r16 >> 2, pp = r16 & 3;
+    if constexpr (PAGED) {
+      // lane: keys 4g..4g+3 (block A half) and 16+4g..16+4g+3 (block B half) of dim 16n + r16, 8 B each
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const int off = ((g * D + 16 * n + r16) << 3) ^ ((g & 1) << 7);
+        const short4v va4 = *reinterpret_cast<const short4v*>(vb + off);
+        const short4v vb4 = *reinterpret_cast<const short4v*>(vb + TILE_BYTES / 2 + off);
+        short8 vf;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vf[r] = va4[r];
+          vf[4 + r] = vb4[r];
+        }
+        o[n] = mfma16p(pf, vf, o[n]);
+      }
+    } else
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       const int chunk = 2 * n + (pp >> 1);
@@ -232,15 +314,33 @@ extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v
   const int max_tiles = (max_seqlen + kQT - 1) / kQT;
   PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)out, cu_seqlens, cu_seqlens_k,
                   q_stride, k_stride,
-                  v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal};
+                  v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal, nullptr, nullptr, 0};
   dim3 grid(nseq * max_tiles, Hq);
   if (D == 128)
-    prefill_attn_kernel<128><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<128, false><<<grid, 256, 0, s>>>(p);
   else if (D == 64)
-    prefill_attn_kernel<64><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<64, false><<<grid, 256, 0, s>>>(p);
   else if (D == 32)
-    prefill_attn_kernel<32><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<32, false><<<grid, 256, 0, s>>>(p);
   else
     return -1;
+  return (int)hipGetLastError();
+}
+
+// Causal prefill of query chunks against a PAGED KV cache (D = 128, block size 16): sequence s has queries
+// cu_seqlens[s]..cu_seqlens[s+1] = its key positions [k_lens[s] - len_q, k_lens[s]); its keys come from
+// kc / vc through block_tables[s] (bt_stride entries per row, covering ceil(k_lens[s] / 16) blocks).
+extern "C" int lwc_prefill_attention_paged(const void* q, const void* kc, const void* vc, void* out,
+                                           const int* cu_seqlens, const int* block_tables, const int* k_lens,
+                                           int bt_stride, int nseq, int max_seqlen, int q_stride, int o_stride, int Hq,
+                                           int Hkv, int D, float scale, hipStream_t s) {
+  using namespace lwc;
+  if (Hq % Hkv != 0 || D != 128) return -1;
+  if (nseq == 0 || max_seqlen == 0) return 0;
+  const int max_tiles = (max_seqlen + kQT - 1) / kQT;
+  PrefillParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)out, cu_seqlens, nullptr,
+                  q_stride, 0, 0, o_stride, Hq, Hkv, nseq, max_tiles, scale, 1, block_tables, k_lens, bt_stride};
+  dim3 grid(nseq * max_tiles, Hq);
+  prefill_attn_kernel<128, true><<<grid, 256, 0, s>>>(p);
   return (int)hipGetLastError();
 }

@@ -34,6 +34,8 @@ int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
 int lwc_silu_mul_quant_fp8(const void*, int, int, int, void*, float*, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
+int lwc_prefill_attention_paged(const void*, const void*, const void*, void*, const int*, const int*, const int*, int, int,
+                                int, int, int, int, int, int, float, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
                const float*, const float*, const float*, void*, const int*, const float*, const int*,
                const unsigned int*, const int*, const unsigned long long*, const unsigned long long*, int, int,
@@ -434,6 +436,33 @@ void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tenso
            "prefill_attention");
 }
 
+void prefill_attention_paged(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache, at::Tensor& out,
+                             const at::Tensor& cu_seqlens, const at::Tensor& block_tables, const at::Tensor& k_lens,
+                             int64_t max_seqlen, int64_t Hq, double scale) {
+  // q [T, >=Hq*D] (row stride allowed), out [T, Hq*D]; K [NB, Hkv, 16, 128], V [NB, Hkv, 4, 128, 4];
+  // block_tables [nseq, W] int32 (W even and >= 2 * ceil(max k_len / 32): a 32-key tile reads 2 entries),
+  // k_lens [nseq] int32 (>= each sequence's query count: the queries are the last positions).
+  CHECK_BF16(q); CHECK_BF16(out); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  CHECK_DTYPE(cu_seqlens, at::kInt); CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(k_lens, at::kInt);
+  CHECK_CONTIG(block_tables); CHECK_CONTIG(k_lens);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128 && k_cache.is_contiguous(),
+              "prefill_attention_paged: K cache [NB, Hkv, 16, 128]");
+  check_v_cache(v_cache, k_cache, "prefill_attention_paged");
+  const int Hkv = (int)k_cache.size(1), D = 128;
+  const int nseq = (int)cu_seqlens.numel() - 1;
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == nseq && block_tables.size(1) % 2 == 0 &&
+                  k_lens.numel() == nseq,
+              "prefill_attention_paged: block_tables [nseq, even W] and k_lens [nseq]");
+  TORCH_CHECK(q.dim() == 2 && out.dim() == 2 && q.stride(1) == 1 && out.stride(1) == 1 && q.size(1) >= Hq * D &&
+                  out.size(1) == Hq * D && Hq % Hkv == 0,
+              "prefill_attention_paged: q / out shapes");
+  CHECK_RC(lwc_prefill_attention_paged(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(),
+                                       cu_seqlens.data_ptr<int>(), block_tables.data_ptr<int>(), k_lens.data_ptr<int>(),
+                                       (int)block_tables.size(1), nseq, (int)max_seqlen, (int)q.stride(0),
+                                       (int)out.stride(0), (int)Hq, Hkv, D, (float)scale, cur_stream()),
+           "prefill_attention_paged");
+}
+
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& top_p, const at::Tensor& top_k,
             const at::Tensor& min_p, const at::Tensor& top_a, const c10::optional<at::Tensor>& freq_pen,
             const c10::optional<at::Tensor>& pres_pen, const c10::optional<at::Tensor>& rep_pen,
@@ -565,6 +594,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_decode_wave_min_items", &lwc_set_decode_wave_min_items,
         "B*Hkv*splits threshold of the wave-per-item decode kernel; returns the previous value");
   m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_attention_paged", &prefill_attention_paged);
   m.def("silu_mul_quant_fp8", &silu_mul_quant_fp8);
   m.def("kv_gather", &kv_gather);
   m.def("sample", &sample);

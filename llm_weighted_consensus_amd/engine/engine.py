@@ -289,15 +289,12 @@ class LLMEngine:
         self.max_model_len = max_model_len
         self.prefill_token_budget = prefill_token_budget
         # chunked prefill (serving): admitted prompts are prefilled at most `chunked_prefill` tokens per
-        # engine step, each step also running one decode step, so running sequences never stall behind
-        # an admission (0 = whole admission batches, then decode: the throughput bench's mode)
+        # engine step, in the same forward as that step's decode rows, so running sequences never stall
+        # behind an admission (0 = whole admission batches, then decode: the throughput bench's mode)
         self.chunked_prefill = int(chunked_prefill)
+        if self.chunked_prefill and self.cfg.head_dim != 128:
+            raise ValueError("chunked prefill: the paged-KV prefill kernel is built for head_dim 128")
         self.prefilling: List[SequenceGroup] = []
-        # a chunk runs when a full budget of prompt tokens is pending, nothing is decoding, or the oldest
-        # admitted prompt has waited this many decode steps (small prompts batch up instead of paying a
-        # whole-model prefill launch each per step)
-        self.chunk_max_wait = 3
-        self._chunk_wait = 0
         self.width = (max_model_len + block_size - 1) // block_size
         if num_blocks is None:
             free, _total = torch.cuda.mem_get_info(self.device)
@@ -601,45 +598,124 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ chunked prefill
     def _step_chunked(self) -> List[TokenEvent]:
-        """One engine step in chunked-prefill mode: admit what fits, prefill one chunk of at most
-        ``chunked_prefill`` prompt tokens (several short prompts whole, a long one in pieces), start the
-        groups whose prompts completed, then one decode step of everything running."""
+        """One engine step in chunked-prefill mode.  Admitted prompts are prefilled at most
+        ``chunked_prefill`` tokens per step, and a step that has prompt tokens to prefill is ONE forward over
+        [every running sequence's next token || the prompt-chunk rows] (:meth:`_mixed_step`): one GEMM per
+        projection over both, decode rows on the paged decode kernel, chunk rows on the paged-KV prefill
+        kernel — running sequences advance by a token in every step, a long prompt never stalls them.
+        Steps with nothing to prefill are the plain (graph-captured) decode step."""
         events: List[TokenEvent] = []
         with self.lock:
             fits = self._first_waiting_fits()
             admitted = self._admit() if fits else []
         self.prefilling.extend(admitted)
+        imported = [g for g in self.prefilling if g.prefilled is not None]
+        if imported:  # prompts prefilled elsewhere cost no compute: start them now
+            events += self._drain()
+            self.prefilling = [g for g in self.prefilling if g.prefilled is None]
+            events += self._prefill(imported)
         if self.prefilling:
-            pending = sum(len(g.prompt_ids) - max(g.pf_pos, 0) for g in self.prefilling)
-            if (pending >= self.chunked_prefill or not self.running or self._chunk_wait >= self.chunk_max_wait
-                    or any(g.prefilled is not None for g in self.prefilling)):
-                self._chunk_wait = 0
-                events += self._drain()  # the chunk writes the block manager / KV pool: no step in flight
-                with span("prefill.chunk"):
-                    events += self._prefill_chunk()
-            else:
-                self._chunk_wait += 1
+            items, _budget, _deferred = self._chunk_items(self.chunked_prefill)
+            if items:
+                events += self._drain()  # the mixed step reads every running sequence's last token on the host
+                with span("prefill.mixed"):
+                    events += self._mixed_step(items)
+                return events
         if self.running or self.inflight is not None:
             events += self._decode()
         return events
 
-    def _prefill_chunk(self) -> List[TokenEvent]:
-        imported = [g for g in self.prefilling if g.prefilled is not None]
-        if imported:  # prompts prefilled elsewhere cost no compute: start them now
-            self.prefilling = [g for g in self.prefilling if g.prefilled is None]
-            return self._prefill(imported)
-        budget = self.chunked_prefill
-        events: List[TokenEvent] = []
-        # up to two passes per step: prompts deferred behind a shared head whose leader completes in the
-        # first pass take the head from the prefix cache in the second (the two-wave prefill, chunked)
-        for _ in range(2):
-            items, budget, deferred = self._chunk_items(budget)
-            if not items:
-                break
-            events += self._finish_chunk(items, self._run_chunk(items))
-            if not deferred or budget <= 0:
-                break
-        return events
+    def _mixed_step(self, items: List[Tuple[SequenceGroup, int, int]]) -> List[TokenEvent]:
+        """One forward over the decode rows of every running sequence and the prompt-chunk rows of
+        ``items`` ((group, a, e): prompt tokens [a, e) of the group's parent sequence); the decode rows'
+        next tokens and the first tokens of prompts completed by this chunk are sampled in one launch that
+        becomes the in-flight step.  Called with no step in flight."""
+        dev = self.device
+        self.running = [s for s in self.running if not s.finished]
+        dec = [s for s in self.running if s.n_launched < s.params.max_tokens]
+        if dec and self.bm.append_cost_total([s.id for s in dec]) > self.bm.num_free:
+            dec = self._preempt_for_growth()
+        B = len(dec)
+        toks: List[int] = []
+        pos: List[int] = []
+        slot_parts: List[np.ndarray] = []
+        dec_in = None
+        if B:
+            width = self.width
+            bt = np.zeros((B, width), np.int32)
+            cl = np.zeros(B, np.int32)
+            sl = np.zeros(B, np.int32)
+            ps = np.zeros(B, np.int32)
+            prepare_decode_into(self.bm, [s.id for s in dec], width, B, bt, cl, sl, ps)
+            toks.extend(s.tokens[-1] for s in dec)
+            pos.extend(ps.tolist())
+            slot_parts.append(sl)
+            dec_in = {"block_tables": _h2d(bt, torch.int32, dev), "ctx_lens": _h2d(cl, torch.int32, dev)}
+            if self.prefix_sharing and B >= self.cascade_min_batch:
+                per = ops.cascade_rows_per_tile(self.cfg.heads // self.cfg.kv_heads)
+                tiles = np.zeros((cascade_table_size(B, per), 3), np.int32)
+                self._cascade_plan(dec, tiles)
+                dec_in["tiles"] = _h2d(tiles, torch.int32, dev)
+            else:
+                splits = min(max(1, min(16, -(-1024 // (B * self.cfg.kv_heads)))), max(1, self.width // 4))
+                dec_in["splits"] = splits if self.decode_splits is None else int(self.decode_splits)
+        cu, k_lens, tables, last_rows = [0], [], [], []
+        for g, a, e in items:
+            p = g.prompt_ids
+            toks.extend(p[a:e])
+            pos.extend(range(a, e))
+            slot_parts.append(slots_range(self.bm, -g.id, a, e - a))
+            cu.append(cu[-1] + e - a)
+            k_lens.append(e)
+            tables.append(list(self.bm.block_table(-g.id)))
+            last_rows.append(B + cu[-1] - 1)
+        wc = 2 * -(-max(k_lens) // 32)
+        bt_c = np.zeros((len(items), wc), np.int32)
+        for i, t in enumerate(tables):
+            bt_c[i, :len(t)] = t[:wc]
+        chunk_in = {"cu_q": _h2d(cu, torch.int32, dev), "block_tables": _h2d(bt_c, torch.int32, dev),
+                    "k_lens": _h2d(k_lens, torch.int32, dev), "max_q": max(e - a for _, a, e in items),
+                    "lens": ([e - a for _, a, e in items], k_lens)}
+        copies = self.bm.take_copies()
+        if copies:
+            self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
+        rows = list(range(B)) + last_rows
+        logits = self.model.forward_mixed(_h2d(toks, torch.int32, dev), _h2d(pos, torch.int32, dev),
+                                          _h2d(np.concatenate(slot_parts), torch.int32, dev), self.cache, B, dec_in,
+                                          chunk_in, _h2d(rows, torch.int64, dev))
+        self.stats["prefill_tokens"] += cu[-1]
+        self.stats["prefill_chunks"] = self.stats.get("prefill_chunks", 0) + 1
+        self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
+        if B:
+            self.stats["decode_tokens"] += B
+            self.stats["steps"] += 1
+        # prompts completed by this chunk: register their blocks in the prefix cache, fork their sequences
+        done, pick = [], list(range(B))
+        for i, (g, a, e) in enumerate(items):
+            g.pf_pos = e
+            if e == len(g.prompt_ids):
+                if self.prefix_caching:
+                    self.bm.cache_prefix(-g.id, g.prompt_ids)
+                done.append((g, B + i))
+        children: List[Sequence] = []
+        if done:
+            ids = {g.id for g, _ in done}
+            self.prefilling = [g for g in self.prefilling if g.id not in ids]
+            for g, row in done:
+                for s in g.seqs:
+                    self.bm.fork(-g.id, s.id)
+                    self._attach_rows(s)
+                    children.append(s)
+                    pick.append(row)
+                self.bm.free_sequence(-g.id)
+        seqs = dec + children
+        if seqs:
+            sel = logits if pick == list(range(logits.shape[0])) else logits.index_select(
+                0, _h2d(pick, torch.int64, dev))
+            self.inflight = self._launch_first(sel, seqs, [g for g, _ in done])
+            self.running.extend(children)
+            self._comp_cache = (None, None)
+        return []
 
     def _chunk_items(self, budget: int):
         bs = self.block_size
@@ -669,54 +745,6 @@ class LLMEngine:
             items.append((g, g.pf_pos, g.pf_pos + n))
             budget -= n
         return items, budget, deferred
-
-    def _finish_chunk(self, items, logits) -> List[TokenEvent]:
-        done, logits_of = [], {}
-        for i, (g, a, e) in enumerate(items):
-            g.pf_pos = e
-            if e == len(g.prompt_ids):
-                if self.prefix_caching:
-                    self.bm.cache_prefix(-g.id, g.prompt_ids)
-                done.append(g)
-                logits_of[g.id] = logits[i]
-        if not done:
-            return []
-        ids = {g.id for g in done}
-        self.prefilling = [g for g in self.prefilling if g.id not in ids]
-        return self._start_groups(done, logits_of)
-
-    def _run_chunk(self, items: List[Tuple[SequenceGroup, int, int]]) -> torch.Tensor:
-        """Prefill prompt tokens [a, e) of each item's parent sequence (blocks allocated at its first
-        chunk); attention covers keys [0, e) — the earlier chunks come from the paged cache through the
-        key-range path of the cached-prefix prefill.  Returns the logits of each item's token e-1."""
-        dev = self.device
-        toks, pos, slots, cu, last = [], [], [], [0], []
-        for g, a, e in items:
-            p = g.prompt_ids
-            toks.extend(p[a:e])
-            pos.extend(range(a, e))
-            slots.append(slots_range(self.bm, -g.id, a, e - a))
-            cu.append(cu[-1] + e - a)
-            last.append(cu[-1] - 1)
-        ctx = None
-        if any(a > 0 for _, a, _ in items):
-            k_lens = [e for _, _, e in items]
-            ks = np.concatenate([slots_range(self.bm, -g.id, 0, e) for g, _, e in items]).astype(np.int64)
-            if ks.size and (ks.min() < 0 or ks.max() >= self.bm.num_blocks * self.block_size):
-                raise RuntimeError("chunked prefill: KV slot out of range")
-            ctx = {"k_slots": _h2d(ks, torch.int64, dev),
-                   "cu_k": _h2d(np.concatenate([[0], np.cumsum(k_lens)]), torch.int32, dev),
-                   "q_lens": [e - a for _, a, e in items], "k_lens": k_lens}
-        t_tok = _h2d(toks, torch.int32, dev)
-        t_pos = _h2d(pos, torch.int32, dev)
-        t_slots = _h2d(np.concatenate(slots), torch.int32, dev)
-        t_cu = _h2d(cu, torch.int32, dev)
-        t_last = _h2d(last, torch.int64, dev)
-        max_len = max(e - a for _, a, e in items)
-        logits = self.model.prefill(t_tok, t_pos, t_slots, t_cu, max_len, t_last, self.cache, ctx=ctx)
-        self.stats["prefill_tokens"] += len(toks)
-        self.stats["prefill_chunks"] = self.stats.get("prefill_chunks", 0) + 1
-        return logits
 
     def _drop_prefilling(self, g: SequenceGroup, reason: str) -> None:
         if g.pf_pos >= 0 and self.bm.has_sequence(-g.id):

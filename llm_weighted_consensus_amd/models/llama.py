@@ -339,3 +339,38 @@ class LlamaModel:
 
         h = self._layers(x, cache, positions, slots, attn_fn)
         return F.linear(h.index_select(0, last_idx), self.lm_head)
+
+    def forward_mixed(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cache: KVCache,
+                      n_dec: int, dec: Optional[dict], chunk: dict, logit_rows: torch.Tensor) -> torch.Tensor:
+        """ONE forward over [n_dec decode rows || prompt-chunk rows] (mixed chunked prefill): every projection
+        is one GEMM over both; per layer the decode rows go to the paged decode kernel (``dec``: block_tables,
+        ctx_lens and either cascade ``tiles`` or ``splits``) and the chunk rows to the paged-KV prefill kernel
+        (``chunk``: cu_q, block_tables, k_lens device tensors, max_q, host lens) — earlier chunks of a prompt
+        are read straight from the paged cache.  Returns logits of ``logit_rows`` [R, V]."""
+        cfg = self.cfg
+        Hq, D = cfg.heads, cfg.head_dim
+        x = ops.embedding(self.embed, tokens)
+        T = tokens.shape[0]
+        part_o = part_lse = None
+        splits = 1 if dec is None else int(dec.get("splits", 1))
+        if n_dec and "tiles" not in dec and splits > 1:
+            part_o = torch.empty(n_dec * Hq * splits * D, dtype=torch.float32, device=x.device)
+            part_lse = torch.empty(n_dec * Hq * splits, dtype=torch.float32, device=x.device)
+
+        def attn_fn(qkv, li):
+            out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+            if n_dec:
+                o = out[:n_dec].view(n_dec, Hq, D)
+                if "tiles" in dec:
+                    ops.paged_decode_cascade(qkv[:n_dec], cache.k[li], cache.v[li], dec["block_tables"],
+                                             dec["ctx_lens"], dec["tiles"], Hq, self.scale, out=o)
+                else:
+                    ops.paged_decode(qkv[:n_dec], cache.k[li], cache.v[li], dec["block_tables"], dec["ctx_lens"], Hq,
+                                     self.scale, num_splits=splits, out=o, part_o=part_o, part_lse=part_lse)
+            ops.prefill_attention_paged(qkv[n_dec:], cache.k[li], cache.v[li], chunk["cu_q"], chunk["block_tables"],
+                                        chunk["k_lens"], chunk["max_q"], Hq, self.scale, out=out[n_dec:],
+                                        lens=chunk.get("lens") if li == 0 else None)
+            return out
+
+        h = self._layers(x, cache, positions, slots, attn_fn)
+        return self._proj(h.index_select(0, logit_rows), self.lm_head)

@@ -178,6 +178,28 @@ def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seql
     return out
 
 
+def prefill_attention_paged(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_seqlens: torch.Tensor,
+                            block_tables: torch.Tensor, k_lens: torch.Tensor, max_seqlen: int, Hq: int, scale: float,
+                            out: Optional[torch.Tensor] = None, lens: Optional[Tuple[Sequence[int], Sequence[int]]] = None
+                            ) -> torch.Tensor:
+    """Causal attention of query chunks against the PAGED KV cache (K4, mixed chunked prefill): sequence s's
+    queries (rows cu_seqlens[s]..cu_seqlens[s+1] of q) are its key positions [k_lens[s] - len_q, k_lens[s]),
+    keys read through ``block_tables`` [nseq, W] (W even, >= 2 * ceil(max k_len / 32)) — no gather of the
+    cached keys.  ``lens`` = host-side (q lengths, k lengths), checked here before the launch."""
+    D = k_cache.shape[-1]
+    if out is None:
+        out = torch.empty(q.shape[0], Hq * D, dtype=q.dtype, device=q.device)
+    if lens is not None:
+        ql, kl = lens
+        W = block_tables.shape[1]
+        if (len(ql) != len(kl) or any(a > b for a, b in zip(ql, kl)) or sum(ql) > q.shape[0]
+                or any(-(-k // 32) * 2 > W for k in kl)):
+            raise ValueError("prefill_attention_paged: key lengths must cover the queries and fit the block tables")
+    kernels().prefill_attention_paged(q, k_cache, v_cache, out, cu_seqlens, block_tables, k_lens, int(max_seqlen),
+                                      int(Hq), float(scale))
+    return out
+
+
 def kv_gather(k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor):
     """Token rows of one layer's paged cache -> contiguous (k [n, Hkv*D], v [n, Hkv*D]) bf16, for the
     cached-prefix prefill (the cached blocks' keys/values next to the freshly written ones).  ``slots``

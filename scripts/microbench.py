@@ -344,6 +344,40 @@ def attention_prefix(dev):
               f"no-sharing full ctx {t_f:7.1f} us", flush=True)
 
 
+def prefill_attn(dev):
+    """Chunk-prefill attention: queries = the last q rows of a k-key range, keys contiguous (cached-prefix
+    path, after kv_gather) vs paged (block tables, the mixed chunked-prefill path); + the gather itself."""
+    from llm_weighted_consensus_amd import ops
+
+    Hq, Hkv, D, BS = 32, 8, 128, 16
+    sc = 1 / math.sqrt(D)
+    for n, ql, kl in [(1, 512, 512), (1, 512, 2048), (1, 512, 4096), (4, 256, 512), (1, 2048, 2048)]:
+        nbs = -(-kl // BS)
+        NB = n * nbs + 8
+        kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
+        vc = torch.randn(NB, Hkv, BS // 4, D, 4, device=dev).to(torch.bfloat16)
+        W = 2 * -(-kl // 32)
+        bt = torch.zeros(n, W, dtype=torch.int32)
+        perm = torch.randperm(NB - 8, dtype=torch.int32)
+        for i in range(n):
+            bt[i, :nbs] = perm[i * nbs:(i + 1) * nbs]
+        bt = bt.to(dev)
+        q = torch.randn(n * ql, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+        cu_q = torch.arange(n + 1, device=dev, dtype=torch.int32) * ql
+        cu_k = torch.arange(n + 1, device=dev, dtype=torch.int32) * kl
+        k_lens = torch.full((n,), kl, device=dev, dtype=torch.int32)
+        toks = torch.arange(kl, device=dev)
+        slots = torch.cat([bt[i, toks // BS].long() * BS + toks % BS for i in range(n)])
+        kf, vf = ops.kv_gather(kc, vc, slots)
+        t_g = timeit(lambda: ops.kv_gather(kc, vc, slots))
+        t_c = timeit(lambda: ops.prefill_attention(q[:, : Hq * D], kf, vf, cu_q, ql, Hq, Hkv, D, sc, True,
+                                                   cu_seqlens_k=cu_k, lens=([ql] * n, [kl] * n)))
+        t_p = timeit(lambda: ops.prefill_attention_paged(q, kc, vc, cu_q, bt, k_lens, ql, Hq, sc))
+        fl = n * 4 * Hq * D * ql * (kl - ql / 2) / 1e12
+        print(f"pfattn {n} x q{ql} k{kl}: gather {t_g:7.1f} us  contiguous {t_c:7.1f} us ({fl / t_c * 1e6:4.0f} TF/s)  "
+              f"paged {t_p:7.1f} us ({fl / t_p * 1e6:4.0f} TF/s)", flush=True)
+
+
 def moe_decode(dev):
     """Mixtral decode MoE at the config-5 batch: fp8 experts, T tokens x top-2 over 8 experts, balanced and
     router-driven (uneven) segments; time and the expert-weight bytes streamed per second."""
@@ -439,6 +473,8 @@ def main():
         gemm_layouts(dev, [int(m) for m in os.environ.get("MICRO_M", "512,1024").split(",")])
     if "attn" in a.what:
         attention(dev)
+    if "pfattn" in a.what:
+        prefill_attn(dev)
     if "prefix" in a.what:
         attention_prefix(dev)
     if "sample" in a.what:

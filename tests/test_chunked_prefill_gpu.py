@@ -1,8 +1,9 @@
-"""Chunked prefill mixed with decode (engine ``chunked_prefill``): prompts prefilled in token-budget chunks
-(earlier chunks read back from the paged cache through the key-range prefill path) give the same
-first-token logprobs and greedy continuations as whole-prompt prefill; running sequences keep decoding
-while a long prompt is being prefilled; prompts sharing a head inside one admission still compute it
-once (prefix cache); aborting a half-prefilled request releases everything."""
+"""Mixed chunked prefill (engine ``chunked_prefill``): each step is ONE forward over the running
+sequences' decode rows and a token-budget chunk of the admitted prompts (earlier chunks read from the
+paged cache by the paged-KV prefill kernel).  Chunked prompts give the same first-token logprobs and
+greedy continuations as whole-prompt prefill; running sequences advance a token in every step while a
+long (4k) prompt prefills; prompts sharing a head inside one admission still compute it once (prefix
+cache); aborting a half-prefilled request releases everything."""
 import pytest
 import torch
 
@@ -28,26 +29,42 @@ def _run(tiny, prompts, chunk, prefix_caching=False, n=2):
     eng.collect_events = True
     sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True, logprobs=True, top_logprobs=3)
     groups = [eng.add_request(p, sp, n=n) for p in prompts]
-    first_lp = {}
+    trace = {}
     while eng.has_work():
-        for ev in eng.step():
-            first_lp.setdefault((ev.seq.group.id, ev.seq.index), ev.logprob)  # events arrive in token order
-    toks = [[list(s.tokens) for s in g.seqs] for g in groups]
-    lps = [[first_lp[(g.id, s.index)] for s in g.seqs] for g in groups]
+        for ev in eng.step():  # events arrive in token order
+            trace.setdefault((ev.seq.group.id, ev.seq.index), []).append((ev.token_id, ev.logprob, dict(ev.top_logprobs)))
+    traces = [[trace[(g.id, s.index)] for s in g.seqs] for g in groups]
     assert eng.bm.num_free == 512 or prefix_caching  # prefix-cached blocks may stay resident (evictable)
-    return toks, lps, eng
+    return traces, eng
+
+
+def _assert_same_greedy(got, want, tol=2e-2):
+    """Greedy continuations of two runs agree token for token, or up to a NEAR TIE: at the first
+    differing step both runs' tokens are in the other's top-3 with log-probabilities within ``tol`` (decode
+    rows that share a forward with prompt-chunk rows run other GEMM shapes: last-bit differences can flip
+    an exact tie of the random-init model, never a clear winner).  The first token (prompt logits) and the
+    log-probabilities up to the divergence must match within ``tol``."""
+    for tg, tw in zip(got, want):
+        for a, b in zip(tg, tw):
+            assert len(a) == len(b)
+            for step, ((ta, la, topa), (tb, lb, topb)) in enumerate(zip(a, b)):
+                assert abs(la - lb) < tol, (step, la, lb)
+                if ta != tb:
+                    assert step > 0, "first tokens differ"
+                    assert tb in topa and abs(topa[tb] - la) < tol, (step, ta, tb, topa)
+                    assert ta in topb and abs(topb[ta] - lb) < tol, (step, ta, tb, topb)
+                    break
 
 
 def test_chunked_matches_whole_prompt_prefill(tiny):
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, 4000, (L,), generator=g).tolist() for L in (300, 17, 130, 64)]
-    want, lp_w, _ = _run(tiny, prompts, 0)
+    want, _ = _run(tiny, prompts, 0)
     for chunk in (48, 100):
-        got, lp_g, eng = _run(tiny, prompts, chunk)
+        got, eng = _run(tiny, prompts, chunk)
         assert eng.stats["prefill_chunks"] >= sum(len(p) for p in prompts) // chunk
-        assert got == want, chunk
-        for a, b in zip(lp_g, lp_w):
-            assert max(abs(x - y) for x, y in zip(a, b)) < 2e-2, (a, b)
+        assert eng.stats["mixed_steps"] == eng.stats["prefill_chunks"]
+        _assert_same_greedy(got, want)
 
 
 def test_decode_continues_while_a_long_prompt_prefills(tiny):
@@ -77,12 +94,10 @@ def test_chunked_with_prefix_cache_and_shared_heads(tiny):
     g = torch.Generator().manual_seed(5)
     head = torch.randint(0, 4000, (200,), generator=g).tolist()
     prompts = [head + torch.randint(0, 4000, (k,), generator=g).tolist() for k in (9, 30, 3)]
-    want, lp_w, _ = _run(tiny, prompts, 0)
-    got, lp_g, eng = _run(tiny, prompts, 64, prefix_caching=True)
+    want, _ = _run(tiny, prompts, 0)
+    got, eng = _run(tiny, prompts, 64, prefix_caching=True)
     assert eng.stats["prefix_cache_tokens"] >= 2 * 192  # the later prompts took the head from the cache
-    assert got == want
-    for a, b in zip(lp_g, lp_w):
-        assert max(abs(x - y) for x, y in zip(a, b)) < 2e-2
+    _assert_same_greedy(got, want)
 
 
 def test_abort_half_prefilled_request_releases_blocks(tiny):
@@ -99,3 +114,50 @@ def test_abort_half_prefilled_request_releases_blocks(tiny):
     eng.abort(grp)
     assert not eng.has_work() and eng.bm.num_free == 512 and eng.free_blocks_unreserved == 512
     assert all(s.finished and s.finish_reason == "abort" for s in grp.seqs)
+
+
+def test_decode_advances_every_step_during_4k_prompt(gpu):
+    """A 4096-token prompt admitted next to running sequences: every one of its 16 chunks shares a forward
+    with the decode rows (each running sequence gains a token per step), and its first tokens match a
+    whole-prompt prefill of the same prompt."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import LlamaModel
+
+    m = LlamaModel(decoder_config("llama-tiny"), device=gpu, seed=0, max_position=4608)
+    tok = ByteTokenizer(m.cfg.vocab_size)
+    g = torch.Generator().manual_seed(9)
+    long_prompt = torch.randint(0, 4000, (4096,), generator=g).tolist()
+
+    sp_long = SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True, logprobs=True, top_logprobs=3)
+    whole = LLMEngine(m, tok, num_blocks=1024, max_batch=32, max_model_len=4352)
+    whole.collect_events = True
+    want = []
+    gw = whole.add_request(long_prompt, sp_long)
+    while whole.has_work():
+        want += [(ev.token_id, ev.logprob, dict(ev.top_logprobs)) for ev in whole.step() if ev.seq.group is gw]
+
+    eng = LLMEngine(m, tok, num_blocks=1024, max_batch=32, max_model_len=4352, chunked_prefill=256)
+    sp = SamplingParams(temperature=0.0, max_tokens=64, ignore_eos=True)
+    shorts = [eng.add_request(tok.encode(f"hello {i}"), sp, n=2) for i in range(3)]
+    while len(eng.running) < 6:
+        eng.step()
+    eng.collect_events = True
+    long_ = eng.add_request(long_prompt, sp_long)
+    chunk_steps = advanced = 0
+    got = []
+    while eng.has_work():
+        before = [len(s.tokens) for gr in shorts for s in gr.seqs]
+        was_prefilling = bool(eng.prefilling) or bool(eng.waiting)
+        got += [(ev.token_id, ev.logprob, dict(ev.top_logprobs)) for ev in eng.step() if ev.seq.group is long_]
+        after = [len(s.tokens) for gr in shorts for s in gr.seqs]
+        if was_prefilling and long_.pf_pos > 0:
+            chunk_steps += 1
+            advanced += all(b > a or len(s.tokens) >= 64 for a, b, s in
+                            zip(before, after, [s for gr in shorts for s in gr.seqs]))
+    assert eng.stats["mixed_steps"] >= 16
+    assert chunk_steps >= 16 and advanced >= chunk_steps - 1, (chunk_steps, advanced)
+    _assert_same_greedy([[got]], [[want]])
+    assert all(len(s.tokens) == 64 for gr in shorts for s in gr.seqs)

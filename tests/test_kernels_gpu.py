@@ -245,6 +245,49 @@ def test_prefill_attention_key_ranges(gpu, D, Hq, Hkv):
         ops.prefill_attention(q, k, v, cu_q, max(ql), Hq, Hkv, D, sc, True, cu_seqlens_k=cu_k, lens=(ql, [1, 1, 1, 1]))
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(8, 2), (4, 4), (32, 8)])
+def test_prefill_attention_paged(gpu, Hq, Hkv):
+    """Mixed chunked prefill: query chunks at the END of each key range, keys/values read from the paged
+    cache through block tables (scattered blocks, ragged last block poisoned with NaN past k_len), q a
+    strided view of a qkv row block."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(5)
+    D, BS = 128, 16
+    ql, kl = [1, 17, 64, 70, 32, 5], [33, 17, 200, 118, 32, 300]
+    n = len(ql)
+    W = 2 * -(-max(kl) // 32)
+    NB = 4 + sum(-(-k // BS) for k in kl)
+    kc, vc = _bf(NB, Hkv, BS, D, dev=gpu), _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
+    perm = torch.randperm(NB).to(torch.int32)
+    bt = torch.zeros(n, W, dtype=torch.int32)
+    used = 0
+    for i, k in enumerate(kl):
+        nb = -(-k // BS)
+        bt[i, :nb] = perm[used:used + nb]
+        used += nb
+        if k % BS:  # slots past the key range hold garbage: the kernel must mask them
+            last = int(bt[i, nb - 1])
+            kc[last, :, k % BS:, :] = float("nan")
+            for t in range(k % BS, BS):
+                ops.v_token(vc, last, t).fill_(float("nan"))
+    bt_d = bt.to(gpu)
+    cu_q = torch.tensor([0] + list(np.cumsum(ql)), dtype=torch.int32, device=gpu)
+    k_lens = torch.tensor(kl, dtype=torch.int32, device=gpu)
+    qkv = _bf(sum(ql), (Hq + 2 * Hkv) * D, dev=gpu)
+    sc = 1 / math.sqrt(D)
+    out = ops.prefill_attention_paged(qkv, kc, vc, cu_q, bt_d, k_lens, max(ql), Hq, sc, lens=(ql, kl))
+    for i, (a, b) in enumerate(zip(ql, kl)):
+        toks = torch.arange(b, device=gpu)
+        blk = bt_d[i, toks // BS].long()
+        kk, vv = kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS)
+        q0 = int(cu_q[i])
+        o = ref.attention(qkv[q0:q0 + a, : Hq * D].reshape(a, Hq, D), kk, vv, True, sc)
+        _close(out[q0:q0 + a].view(a, Hq, D), o, 2e-2, 2e-2)
+    with pytest.raises(ValueError):  # block tables too narrow for a key range: refused on the host
+        ops.prefill_attention_paged(qkv, kc, vc, cu_q, bt_d[:, :2], k_lens, max(ql), Hq, sc, lens=(ql, kl))
+
+
 def _sample(logits, dev, n=None, **kw):
     from llm_weighted_consensus_amd import ops
 
