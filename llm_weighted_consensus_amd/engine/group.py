@@ -102,8 +102,38 @@ def _resolve(path: str):
     return getattr(importlib.import_module(mod), fn)
 
 
-def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None) -> None:
-    """Worker process: build the engine, serve requests until told to stop."""
+def _apply(engine, msg, groups: Dict[int, Any], cb_for, emb_req, on_error) -> None:
+    """Apply one front-end message to the worker's engine (shared by TP leaders and their followers)."""
+    kind = msg[0]
+    if kind == "submit":
+        _, rid, prompt, params, n, offset = msg[:6]
+        embed = msg[6] if len(msg) > 6 else None
+        wctx = msg[7] if len(msg) > 7 else None
+        cb, texts = cb_for(rid, offset, n, embed)
+        if embed and texts is not None:
+            emb_req[rid] = (embed, offset, texts)
+        try:
+            kw = {"ctx": wctx} if wctx is not None else {}
+            groups[rid] = engine.add_request(prompt, params, n=n, callback=cb, **kw)
+        except ValueError as e:
+            on_error(rid, str(e))
+    elif kind == "abort":
+        g = groups.pop(msg[1], None)
+        if g is not None:
+            engine.abort(g)
+
+
+def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None,
+                mirror_out: Optional[list] = None, mirror_in=None) -> None:
+    """Worker process: build the engine, serve requests until told to stop.
+
+    Tensor-parallel replicas (spec ``tp`` > 1): the replica's rank 0 (the leader) is the worker the front end
+    talks to; every engine iteration it forwards the messages it applied — submits, aborts, deadline expiries
+    — and whether it steps to its followers (``mirror_out`` queues), which apply the same messages and step in
+    lockstep (``mirror_in``), so every rank schedules the same batch and the all-reduce inside each forward
+    pairs up.  Only the leader streams tokens and embeds candidates."""
+    if mirror_in is not None:
+        return _follower_main(wid, spec, factory, ev_q, hb, stop, mirror_in)
     ring = ShmRing(ring_name, create=False) if ring_name else None
     embedders: Dict[str, Any] = {}
     emb_req: Dict[int, tuple] = {}  # rid -> (model name, offset, streamed texts)
@@ -115,38 +145,33 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
     ev_q.put(("ready", wid, None))
     groups: Dict[int, Any] = {}
     batch: List[tuple] = []
+
+    def cb_for(rid, offset, n, embed):
+        texts = [""] * n if embed else None
+
+        def cb(ev, rid=rid, offset=offset, texts=texts):
+            batch.append((rid, ev.seq.index + offset, ev.token_id, ev.text, ev.logprob,
+                          list(ev.top_logprobs), ev.finished, ev.finish_reason))
+            if texts is not None:
+                texts[ev.seq.index] += ev.text
+
+        return cb, texts
+
+    def on_error(rid, msg):
+        ev_q.put(("error", wid, (rid, msg)))
+
+    failed = False
     while not stop.is_set():
         hb.value = time.time()
+        applied: List[tuple] = []
         try:
             block = not engine.has_work()
             msg = req_q.get(timeout=0.2) if block else req_q.get_nowait()
         except pyqueue.Empty:
             msg = None
         while msg is not None:
-            kind = msg[0]
-            if kind == "submit":
-                _, rid, prompt, params, n, offset = msg[:6]
-                embed = msg[6] if len(msg) > 6 else None
-                wctx = msg[7] if len(msg) > 7 else None
-                texts = [""] * n if embed else None
-                if embed:
-                    emb_req[rid] = (embed, offset, texts)
-
-                def cb(ev, rid=rid, offset=offset, texts=texts):
-                    batch.append((rid, ev.seq.index + offset, ev.token_id, ev.text, ev.logprob,
-                                  list(ev.top_logprobs), ev.finished, ev.finish_reason))
-                    if texts is not None:
-                        texts[ev.seq.index] += ev.text
-
-                try:
-                    kw = {"ctx": wctx} if wctx is not None else {}
-                    groups[rid] = engine.add_request(prompt, params, n=n, callback=cb, **kw)
-                except ValueError as e:
-                    ev_q.put(("error", wid, (rid, str(e))))
-            elif kind == "abort":
-                g = groups.pop(msg[1], None)
-                if g is not None:
-                    engine.abort(g)
+            _apply(engine, msg, groups, cb_for, emb_req, on_error)
+            applied.append(msg)
             try:
                 msg = req_q.get_nowait()
             except pyqueue.Empty:
@@ -155,12 +180,20 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
             rid = next((r for r, gg in groups.items() if gg is g), None)
             if rid is not None:
                 groups.pop(rid, None)
+                applied.append(("abort", rid))
                 ev_q.put(("error", wid, (rid, "request deadline exceeded", "deadline")))
-        if engine.has_work():
+        step = engine.has_work()
+        if mirror_out and (applied or step or failed):
+            tick = ("tick", applied, step, failed)
+            for q in mirror_out:
+                q.put(tick)
+        failed = False
+        if step:
             try:
                 engine.step()
             except Exception as e:  # engine failure: fail in-flight groups, keep the worker alive
                 traceback.print_exc()
+                failed = True  # followers fail theirs at the next tick (their state stays the leader's)
                 for g in engine.fail_all(f"{type(e).__name__}: {e}"):
                     rid = next((r for r, gg in groups.items() if gg is g), None)
                     if rid is not None:
@@ -187,6 +220,43 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                     ev_q.put(("emb", wid, (rid, offset, E.float().cpu().numpy(), int(ntok))))
                 except Exception as e:  # noqa: BLE001 - reported to the request, the worker keeps serving
                     ev_q.put(("emb_err", wid, (rid, f"{type(e).__name__}: {e}")))
+    if mirror_out:
+        for q in mirror_out:
+            q.put(("stop",))
+
+
+def _follower_main(wid: int, spec: dict, factory: str, ev_q, hb, stop, mirror_in) -> None:
+    """A tensor-parallel follower rank: replay the leader's ticks (messages + step) on its own engine shard."""
+    try:
+        engine = _resolve(factory)(spec, wid)
+    except BaseException as e:
+        ev_q.put(("fatal", wid, f"follower rank {spec.get('tp_rank')}: {type(e).__name__}: {e}"))
+        return
+    groups: Dict[int, Any] = {}
+    noop = lambda rid, offset, n, embed: (None, None)  # noqa: E731 - followers stream nothing
+    while not stop.is_set():
+        hb.value = time.time()
+        try:
+            tick = mirror_in.get(timeout=0.2)
+        except pyqueue.Empty:
+            continue
+        if tick[0] == "stop":
+            return
+        _, applied, step, leader_failed = tick
+        if leader_failed:  # the leader's last step raised: fail the same groups here
+            engine.fail_all("tensor-parallel leader step failed")
+            groups.clear()
+        for msg in applied:
+            _apply(engine, msg, groups, noop, {}, lambda rid, m: None)
+        if step:
+            try:
+                engine.step()
+            except Exception as e:  # the replica's ranks no longer agree: take the replica down
+                traceback.print_exc()
+                ev_q.put(("fatal", wid, f"follower rank {spec.get('tp_rank')} step failed: {type(e).__name__}: {e}"))
+                return
+        for rid in [r for r, g in groups.items() if g.finished]:
+            groups.pop(rid)
 
 
 class _EngineFacade:
@@ -199,24 +269,53 @@ class EngineGroup:
     def __init__(self, spec: dict, devices: List[int], factory: str = "llm_weighted_consensus_amd.engine.group:build_engine",
                  tokenizer=None, cfg=None, max_model_len: int = 4096, heartbeat_timeout: float = 30.0,
                  start_timeout: float = 600.0, ring_bytes: int = 32 << 20):
-        self.spec, self.devices, self.factory = spec, list(devices), factory
+        self.spec, self.factory = spec, factory
         self.heartbeat_timeout = heartbeat_timeout
+        # tensor-parallel replicas: spec "tp" = T groups the listed GPUs in runs of T (LWC_GPUS=0,...,7 with
+        # tp 2 = four TP=2 replicas); a worker index below names a replica, served by its rank-0 process
+        tp = int(spec.get("tp", 1) or 1)
+        devices = list(devices)
+        if tp < 1 or len(devices) % tp:
+            raise ValueError(f"tp {tp} must divide the number of GPUs ({len(devices)})")
+        self.tp = tp
+        self.replicas = [devices[i:i + tp] for i in range(0, len(devices), tp)]
+        self.devices = [r[0] for r in self.replicas]
         ctx = mp.get_context("spawn")
         self.ev_q = ctx.Queue()
         self.stop = ctx.Event()
         self.req_qs, self.hbs, self.procs, self.rings = [], [], [], []
-        for wid, dev in enumerate(self.devices):
+        self.followers: List[List[tuple]] = []  # per replica: (process, heartbeat) of ranks 1..T-1
+        self.mirror_qs: List[list] = []
+        port0 = int(spec.get("tp_port", 0)) or _free_port_base(len(self.replicas))
+        for wid, devs in enumerate(self.replicas):
             q = ctx.Queue()
             hb = ctx.Value("d", time.time())
             ring = ShmRing(cap=ring_bytes)
             self.rings.append(ring)
-            p = ctx.Process(target=worker_main, args=(wid, dict(spec, device=dev), factory, q, self.ev_q, hb, self.stop,
-                                                      ring.name),
+            wspec = dict(spec, device=devs[0])
+            mirrors, fl = [], []
+            if tp > 1:
+                shared = len(set(devs)) < len(devs)  # ranks sharing a GPU (one-GPU rehearsal) split its memory
+                wspec.update(tp=tp, tp_rank=0, tp_port=port0 + wid, tp_shared=shared)
+                for r in range(1, tp):
+                    mq = ctx.Queue()
+                    fhb = ctx.Value("d", time.time())
+                    fp = ctx.Process(target=worker_main,
+                                     args=(wid, dict(wspec, device=devs[r], tp_rank=r), factory, None, self.ev_q, fhb,
+                                           self.stop, None, None, mq),
+                                     daemon=True, name=f"lwc-worker-{wid}-tp{r}")
+                    fp.start()
+                    mirrors.append(mq)
+                    fl.append((fp, fhb))
+            p = ctx.Process(target=worker_main, args=(wid, wspec, factory, q, self.ev_q, hb, self.stop, ring.name,
+                                                      mirrors or None),
                             daemon=True, name=f"lwc-worker-{wid}")
             p.start()
             self.req_qs.append(q)
             self.hbs.append(hb)
             self.procs.append(p)
+            self.followers.append(fl)
+            self.mirror_qs.append(mirrors)  # keep the queues alive: a started Process drops its args
         self.alive = [True] * len(self.procs)
         self.ready = [False] * len(self.procs)
         self.load_of = [0] * len(self.procs)
@@ -289,7 +388,7 @@ class EngineGroup:
 
     def close(self) -> None:
         self.stop.set()
-        for p in self.procs:
+        for p in self.procs + [fp for fl in self.followers for fp, _ in fl]:
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
@@ -329,8 +428,11 @@ class EngineGroup:
             if kind == "ready":
                 self.ready[wid] = True
             elif kind == "fatal":
-                self.alive[wid] = False
-                self.failures += 1
+                if self.ready[wid] and self.alive[wid]:  # a TP follower lost step with its leader
+                    self._worker_died(wid, str(payload))
+                else:
+                    self.alive[wid] = False
+                    self.failures += 1
             elif kind == "error":
                 rid, msg = payload[:2]
                 fkind = payload[2] if len(payload) > 2 else "error"
@@ -398,14 +500,22 @@ class EngineGroup:
         for w, p in enumerate(self.procs):
             if not self.alive[w]:
                 continue
-            stale = self.ready[w] and now - self.hbs[w].value > self.heartbeat_timeout
-            if not p.is_alive() or stale:
-                self._worker_died(w, "exited" if not p.is_alive() else "heartbeat timeout")
+            members = [(p, self.hbs[w])] + self.followers[w]
+            for q, hb in members:
+                stale = self.ready[w] and now - hb.value > self.heartbeat_timeout
+                if not q.is_alive() or stale:
+                    self._worker_died(w, "exited" if not q.is_alive() else "heartbeat timeout")
+                    break
 
     def _worker_died(self, w: int, why: str) -> None:
         self.alive[w] = False
         self.failures += 1
         self.load_of[w] = 0
+        for fp, _ in self.followers[w]:  # a TP replica is one unit: its other ranks cannot go on alone
+            if fp.is_alive():
+                fp.kill()
+        if self.followers[w] and self.procs[w].is_alive():
+            self.procs[w].kill()
         live = self.live_workers()
         with self._lock:
             for rid, req in list(self.emb_pending.items()):  # generated, but this worker's rows never came
@@ -430,6 +540,46 @@ class EngineGroup:
                         break
 
 
+def _free_port_base(n: int) -> int:
+    """A base port with n consecutive free TCP ports on 127.0.0.1 (TP replica rendezvous)."""
+    import socket
+
+    for _ in range(64):
+        with socket.socket() as s0:
+            s0.bind(("127.0.0.1", 0))
+            base = s0.getsockname()[1]
+        if base + n >= 65535:
+            continue
+        ok = True
+        for k in range(1, n):
+            with socket.socket() as sk:
+                try:
+                    sk.bind(("127.0.0.1", base + k))
+                except OSError:
+                    ok = False
+                    break
+        if ok:
+            return base
+    raise RuntimeError("no free port range for the TP rendezvous")
+
+
+def _tp_setup(spec: dict, dev, hidden: int):
+    """Join this rank's TP replica: a gloo group over 127.0.0.1 (control: IPC handle exchange, KV sizing)
+    and the IPC one-shot all-reduce (C3) the decoder's forward uses."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from ..parallel.allreduce import CustomAllReduce
+
+    tp, rank = int(spec["tp"]), int(spec["tp_rank"])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{int(spec['tp_port'])}", rank=rank, world_size=tp,
+                            timeout=datetime.timedelta(seconds=600))
+    rows = max(int(spec.get("max_batch", 512)), int(spec.get("chunked_prefill", 0) or 0) + 1, 1024)
+    comm = CustomAllReduce(device=dev, max_bytes=min(64 << 20, rows * hidden * 2))
+    return rank, tp, comm
+
+
 def build_engine(spec: dict, wid: int):
     """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
     ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8",
@@ -448,17 +598,41 @@ def build_engine(spec: dict, wid: int):
     w = spec.get("weights", "random:0")
     path, seed = (None, int(w.split(":", 1)[1])) if w.startswith("random:") else (w, 0)
     mlen = int(spec.get("max_model_len", 4096))
+    tp = int(spec.get("tp", 1) or 1)
+    kv_fraction = float(spec.get("kv_fraction", 0.85))
+    num_blocks = None
+    if tp > 1 and not cfg.num_experts:
+        raise ValueError(f"tp {tp}: tensor parallelism is implemented for the MoE decoders (config 5); "
+                         f"serve {cfg.name} data-parallel (one worker per GPU)")
     if cfg.num_experts:
         from ..models.mixtral import MixtralModel
 
+        tp_kw = {}
+        if tp > 1:
+            rank, tp, comm = _tp_setup(spec, dev, cfg.hidden)
+            tp_kw = dict(tp_rank=rank, tp_size=tp, tp_comm=comm)
+            if spec.get("tp_shared"):
+                kv_fraction /= tp
         model = MixtralModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
-                             fp8=bool(spec.get("fp8", False)))
+                             fp8=bool(spec.get("fp8", False)), **tp_kw)
+        if tp > 1:
+            # every rank must schedule identically: one KV pool size for the replica (the smallest rank's)
+            import torch.distributed as dist
+
+            from ..models.llama import KVCache
+
+            torch.cuda.synchronize(dev)
+            free, _total = torch.cuda.mem_get_info(dev)
+            nb = torch.tensor([max(64, int(free * kv_fraction) // KVCache.bytes_per_block(model.cfg, 16))])
+            dist.all_reduce(nb, op=dist.ReduceOp.MIN)
+            num_blocks = int(nb.item())
     else:
         model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
                            fp8_dense=bool(spec.get("fp8", False)))
     tok = load_tokenizer(spec, cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
     return LLMEngine(model, tok, max_batch=int(spec.get("max_batch", 512)), max_model_len=mlen,
-                     kv_memory_fraction=float(spec.get("kv_fraction", 0.85)),
+                     kv_memory_fraction=kv_fraction, num_blocks=num_blocks,
+                     use_graphs=getattr(model, "graph_safe", True),
                      prefix_caching=bool(spec.get("prefix_caching", True)),
                      chunked_prefill=int(spec.get("chunked_prefill", 0)),
                      constrained_logprobs=bool(spec.get("constrained_logprobs", False)),

@@ -5,7 +5,10 @@ bases are OPTIONAL here (they become the fallback tier behind the local MI355X e
 variables configure the local engine:
 
   LWC_MODELS        JSON {name: {"arch": "llama-3-8b", "weights": "random:<seed>" | <path>,
-                          "max_model_len": 4096, "max_batch": 512}}   (default: none)
+                          "max_model_len": 4096, "max_batch": 512, "fp8": false, "tp": 1}}   (default: none)
+                    "tp": T (MoE decoders, BASELINE config 5) serves each replica tensor-parallel over T
+                    consecutive LWC_GPUS entries — one process per GPU, the IPC one-shot all-reduce (C3)
+                    inside every forward, the ranks stepping in lockstep behind the replica's rank 0
   LWC_EMBED_MODELS  JSON {name: {"arch": "bge-large-en-v1.5", "weights": "random:<seed>" | <path>}}
   LWC_GPU           device index for this process's engine (one process per GPU)
   LWC_GPUS          comma list of devices: serve each model through an EngineGroup (one worker process

@@ -58,6 +58,8 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                 continue
             from ..engine.group import build_engine
 
+            if int(spec.get("tp", 1) or 1) > 1:
+                raise ValueError(f"model {name}: tp > 1 needs LWC_GPUS (one worker process per TP rank)")
             eng = build_engine(dict(spec, device=cfg.gpu, kv_fraction=cfg.kv_fraction / max(1, len(cfg.models)),
                                     prefix_caching=cfg.prefix_caching, chunked_prefill=cfg.chunked_prefill,
                                     constrained_logprobs=cfg.constrained_logprobs,

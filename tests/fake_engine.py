@@ -28,9 +28,10 @@ class _Ev:
 
 
 class FakeEngine:
-    def __init__(self, delay):
+    def __init__(self, delay, log=None):
         self.groups, self.delay = [], delay
         self.running, self.waiting = [], []
+        self.log = log  # tensor-parallel tests: one line per step (the batch each rank stepped)
 
     def add_request(self, prompt, params, n=1, callback=None):
         g = _Group(params, n, callback)
@@ -51,8 +52,12 @@ class FakeEngine:
                 ev = _Ev(s, tid)
                 if len(s.tokens) >= g.params.max_tokens:
                     s.finished, ev.finished, ev.finish_reason = True, True, "length"
-                g.callback(ev)
+                if g.callback is not None:  # tensor-parallel followers stream nothing
+                    g.callback(ev)
         self.groups = [g for g in self.groups if not g.finished]
+        if self.log is not None:
+            self.log.write(" ".join(f"{s.seed}:{len(s.tokens)}" for g in self.groups for s in g.seqs) + "\n")
+            self.log.flush()
 
     def abort(self, g):
         for s in g.seqs:
@@ -66,4 +71,7 @@ class FakeEngine:
 
 
 def make(spec, wid):
-    return FakeEngine(float(spec.get("delay", 0.0)))
+    log = None
+    if spec.get("log_dir"):
+        log = open(f"{spec['log_dir']}/w{wid}_rank{int(spec.get('tp_rank', 0))}.log", "w")
+    return FakeEngine(float(spec.get("delay", 0.0)), log)

@@ -114,3 +114,32 @@ def test_workers_embed_their_own_candidates():
         assert not g.emb_pending
     finally:
         g.close()
+
+
+def test_tp_replicas_step_in_lockstep(tmp_path):
+    """spec "tp": 2 over 4 devices = two replicas of two ranks; each follower replays its leader's ticks:
+    both ranks of a replica step the same batches (the per-step logs are identical), only the leaders
+    stream, and a killed follower takes its whole replica down (requests go to the other one)."""
+    g = EngineGroup({"delay": 0.01, "tp": 2, "log_dir": str(tmp_path)}, devices=[0, 0, 0, 0], factory=FACTORY,
+                    heartbeat_timeout=60)
+    try:
+        assert len(g.procs) == 2 and all(len(f) == 1 for f in g.followers)
+        toks, err = _collect(g, 6, SamplingParams(max_tokens=5, seed=3))
+        assert err is None and sorted(toks) == list(range(6))
+        for i, t in toks.items():
+            assert t == [(3 * 1000003 + i + k) % 1000 for k in range(5)]
+        time.sleep(0.5)  # followers write their last step
+        for w in range(2):
+            lead = (tmp_path / f"w{w}_rank0.log").read_text()
+            assert lead and lead == (tmp_path / f"w{w}_rank1.log").read_text()
+        os.kill(g.followers[0][0][0].pid, signal.SIGKILL)
+        deadline = time.time() + 60
+        while g.alive[0] and time.time() < deadline:
+            time.sleep(0.1)
+        assert g.alive == [False, True]
+        g.procs[0].join(timeout=10)
+        assert not g.procs[0].is_alive()  # the leader of the broken replica is taken down with it
+        toks, err = _collect(g, 3, SamplingParams(max_tokens=3, seed=5))
+        assert err is None and len(toks) == 3
+    finally:
+        g.close()
