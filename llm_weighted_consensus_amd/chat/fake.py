@@ -51,12 +51,21 @@ class FakeChatClient(ChatClient):
 
     async def create_streaming(self, ctx, request: C.ChatCompletionCreateParams):
         self.requests.append(request)
+        cand = ctx.get("candidates") if isinstance(ctx, dict) else None
+        first = 0
+        if cand is not None:  # a slice of a sharded request (as the local engine client serves it)
+            first, cnt, base = int(cand[0]), int(cand[1]), cand[2]
+            # the policy scripts the whole request's candidates [0, first + cnt); this slice streams its own
+            request = request.model_copy(update={"n": first + cnt,
+                                                 "seed": request.seed if request.seed is not None else base})
         plan = self.policy(request)
         if isinstance(plan, Failure) and plan.after_chunks == 0:
             raise plan.error
-        return self._gen(request, plan)
+        if cand is not None and not isinstance(plan, Failure):
+            plan = list(plan)[first:first + cnt]
+        return self._gen(request, plan, first)
 
-    async def _gen(self, request, plan):
+    async def _gen(self, request, plan, first: int = 0):
         cid = f"chatcmpl-fake-{uuid.uuid4().hex[:8]}"
         created = int(time.time())
         fail = plan if isinstance(plan, Failure) else None
@@ -85,7 +94,7 @@ class FakeChatClient(ChatClient):
                                                    top_logprobs=[C.TopLogprob(token=a, bytes=list(a.encode()), logprob=l)
                                                                  for a, l in alts])])
             yield C.ChatCompletionChunk(id=cid, created=created, model=request.model, provider="fake",
-                                        choices=[C.StreamChoice(delta=d, index=i, logprobs=lp)])
+                                        choices=[C.StreamChoice(delta=d, index=first + i, logprobs=lp)])
             emitted += 1
             if fail and emitted >= fail.after_chunks:
                 raise fail.error
@@ -96,6 +105,6 @@ class FakeChatClient(ChatClient):
                             total_tokens=sc.usage[0] + sc.usage[1], cost=0.001)
                 u.with_total_cost()
             yield C.ChatCompletionChunk(id=cid, created=created, model=request.model, provider="fake", usage=u,
-                                        choices=[C.StreamChoice(delta=C.Delta(), index=i,
+                                        choices=[C.StreamChoice(delta=C.Delta(), index=first + i,
                                                                 finish_reason="tool_calls" if sc.tool_call
                                                                 else sc.finish_reason)])

@@ -15,6 +15,7 @@ from __future__ import annotations
 import asyncio
 import time
 import uuid
+from dataclasses import replace
 from typing import Any, AsyncIterator, Dict, List, Optional
 
 from ..engine.constraints import constraint_for_schema
@@ -231,6 +232,13 @@ class LocalChatClient(ChatClient):
         n = int(request.n or 1)
         if n < 1 or n > 128:
             raise ChatError.invalid_request(f"n must be between 1 and 128: {n}")
+        first = 0
+        cand = ctx.get("candidates") if isinstance(ctx, dict) else None
+        if cand is not None:
+            # a slice of a request sharded over ranks (score/sharded.py consensus): candidates [first, first+n)
+            # of the whole request, with the seeds they have in it (base*1000003 + index) and their indices
+            first, n, base = int(cand[0]), int(cand[1]), cand[2]
+            sp = replace(sp, seed=sp.seed if sp.seed is not None else base, seed_offset=sp.seed_offset + first)
         include_usage = bool(request.stream_options and request.stream_options.include_usage) or not request.stream
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
@@ -243,7 +251,8 @@ class LocalChatClient(ChatClient):
             raise ChatError.invalid_request(str(e))
         cid = f"chatcmpl-{uuid.uuid4().hex}"
         created = int(time.time())
-        return self._stream(svc, group, q, cid, created, name, len(ids), n, sp, tool_name, include_usage, tok), group
+        return self._stream(svc, group, q, cid, created, name, len(ids), n, sp, tool_name, include_usage, tok,
+                            first), group
 
     # ---- candidates embedded where they were generated (EngineGroup workers)
     def _embedding_service_for(self, request: C.ChatCompletionCreateParams, embedding_model: str) -> Optional[str]:
@@ -298,7 +307,8 @@ class LocalChatClient(ChatClient):
         async for c in self._timed(first, stream):
             yield c
 
-    async def _stream(self, svc, group, q, cid, created, model, prompt_len, n, sp, tool_name, include_usage, tok):
+    async def _stream(self, svc, group, q, cid, created, model, prompt_len, n, sp, tool_name, include_usage, tok,
+                      first: int = 0):
         started = [False] * n
         remaining = n
         completion_tokens = 0
@@ -317,7 +327,7 @@ class LocalChatClient(ChatClient):
                     completion_tokens += 1
                     ch = choices.get(i)
                     if ch is None:
-                        ch = C.StreamChoice(delta=C.Delta(), index=i)
+                        ch = C.StreamChoice(delta=C.Delta(), index=first + i)
                         choices[i] = ch
                     d = ch.delta
                     if not started[i]:

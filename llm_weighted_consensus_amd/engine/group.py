@@ -371,7 +371,7 @@ class EngineGroup:
             for w, m in zip(order, share):
                 if m == 0:
                     continue
-                p = _Portion(w, offset, m, replace(params, seed=base, seed_offset=offset))
+                p = _Portion(w, offset, m, replace(params, seed=base, seed_offset=params.seed_offset + offset))
                 req.portions.append(p)
                 self.load_of[w] += m
                 self.req_qs[w].put(("submit", rid, req.prompt_ids, p.params, m, offset, embed, _wire_ctx(ctx)))

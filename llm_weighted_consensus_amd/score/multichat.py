@@ -121,23 +121,47 @@ class ConsensusClient:
 
     async def create_unary(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
                            tau: float = 0.05) -> S.ScoreCompletion:
+        emb = self._embedder(embedding_model)
+        self._check_n(request)
+        comp, E, ntok = await self.generate_embedded(ctx, request, embedding_model)
+        out = self.build(comp, E.to(emb.encoder.device), ntok, embedding_model, tau)
+        if self.archive is not None:
+            self.archive.store_score(out)
+        return out
+
+    def _embedder(self, embedding_model: str):
         emb = self.embedders.get(embedding_model)
         if emb is None:
             raise ScoreError(404, {"kind": "model_not_found", "error": f"embedding model not served: {embedding_model}"})
+        return emb
+
+    @staticmethod
+    def _check_n(request) -> int:
         n = int(request.n or 1)
         if n < 2:
             raise ScoreError.expected_two_or_more_choices(n)
+        return n
+
+    async def generate_embedded(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str):
+        """The request's candidates (all of them, or the ``ctx["candidates"]`` slice of a sharded request)
+        and their unit embeddings: (ChatCompletion, rows [n, d] float32 in choice order, embedding tokens)."""
+        emb = self._embedder(embedding_model)
         local = getattr(self.chat, "local", self.chat)
         if hasattr(local, "can_embed_in_workers") and local.can_embed_in_workers(request, embedding_model):
             # multi-GPU: every EngineGroup worker embeds the candidates it generated on its own GPU;
             # only the unit rows come back (no candidate text is re-encoded on the front end's GPU)
             comp, rows, ntok = await local.create_unary_embedded(ctx, request, embedding_model)
-            E = torch.from_numpy(rows).to(emb.encoder.device)
-        else:
-            comp = await self.chat.create_unary(ctx, request)
-            texts = [c.message.content or "" for c in comp.choices]
-            loop = asyncio.get_running_loop()
-            E, ntok = await loop.run_in_executor(None, emb.embed_texts, texts)
+            return comp, torch.from_numpy(rows).to(emb.encoder.device), ntok
+        comp = await self.chat.create_unary(ctx, request)
+        texts = [c.message.content or "" for c in sorted(comp.choices, key=lambda c: c.index)]
+        loop = asyncio.get_running_loop()
+        E, ntok = await loop.run_in_executor(None, emb.embed_texts, texts)
+        return comp, E.float(), ntok
+
+    @staticmethod
+    def build(comp, E: torch.Tensor, ntok: int, embedding_model: str, tau: float) -> S.ScoreCompletion:
+        """The consensus response over the candidates of ``comp`` (choice c <-> row c.index of E)."""
+        n = E.shape[0]
         Eb = E.to(torch.bfloat16).unsqueeze(0).contiguous()
         if Eb.is_cuda:
             _, cen, w, best = ops.cosine_consensus(Eb, tau)
@@ -157,12 +181,9 @@ class ConsensusClient:
                                               model=comp.model, completion_metadata=S.CompletionMetadata(
                                                   id=comp.id, created=comp.created, model=comp.model,
                                                   provider=comp.provider)))
-        out = S.ScoreCompletion(id=f"cnscpl-{uuid.uuid4().hex}-{created}", choices=choices, created=created,
-                                model=comp.model, usage=usage,
-                                weight_data=S.WeightDataTrainingTable(embeddings_response=S.CreateEmbeddingResponse(
-                                    data=[S.EmbeddingItem(embedding=[float(x) for x in r], index=i)
-                                          for i, r in enumerate(E.double().cpu().tolist())],
-                                    model=embedding_model, usage=C.Usage(prompt_tokens=ntok, total_tokens=ntok))))
-        if self.archive is not None:
-            self.archive.store_score(out)
-        return out
+        return S.ScoreCompletion(id=f"cnscpl-{uuid.uuid4().hex}-{created}", choices=choices, created=created,
+                                 model=comp.model, usage=usage,
+                                 weight_data=S.WeightDataTrainingTable(embeddings_response=S.CreateEmbeddingResponse(
+                                     data=[S.EmbeddingItem(embedding=[float(x) for x in r], index=i)
+                                           for i, r in enumerate(E.double().cpu().tolist())],
+                                     model=embedding_model, usage=C.Usage(prompt_tokens=ntok, total_tokens=ntok))))

@@ -26,6 +26,7 @@ from typing import Any, List
 
 import torch.distributed as dist
 
+from ..errors import ScoreError
 from ..parallel import votes as V
 from ..schema import chat as C
 from ..schema import score as S
@@ -64,7 +65,9 @@ class _Combiner:
                 payload, loop, fut = self.pending.pop(self.next)
                 self.next += 1
             try:
-                res = V.gather_objects(payload, self.group)
+                # a callable runs its own collectives (consensus: object + tensor all-gathers), else one
+                # object all-gather of the payload
+                res = payload() if callable(payload) else V.gather_objects(payload, self.group)
                 loop.call_soon_threadsafe(_resolve, fut, res, None)
             except BaseException as e:  # noqa: BLE001 — handed to the awaiting request
                 loop.call_soon_threadsafe(_resolve, fut, None, e)
@@ -101,6 +104,10 @@ class ShardedScoreClient(ScoreClient):
             self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"], 0, self.group))
         self.rng.seed(self.seed_base)
         self.combiner = _Combiner(self.group)
+        # C1 (consensus): candidate embedding rows all-gathered as device tensors on the world's backend
+        # (RCCL over xGMI on a GPU node; gloo — host tensors — for CPU worlds and one-GPU rehearsals)
+        self.data_group = dist.new_group()
+        self.data_backend = dist.get_backend(self.data_group)
 
     def request_ctx(self, seq: int, ids) -> dict:
         """The per-request context every rank builds identically: sequence number (combine order), the
@@ -169,6 +176,88 @@ class ShardedScoreClient(ScoreClient):
         self.combiner.close()
 
 
+class ShardedConsensusClient:
+    """/consensus/completions over the ranks of a voter-sharded deployment: rank r samples candidates
+    [first_r, first_r + n_r) of the request (contiguous split, each with the seed it has in the whole
+    request) on its own engine and embeds them on its own GPU; ONE all-gather of the unit rows (C1: device
+    tensors over RCCL) assembles the [n, d] matrix and an object all-gather the candidates' texts, so every
+    rank builds the same response — rank 0's is served.  Collectives run on the request-ordered combiner
+    shared with score requests."""
+
+    def __init__(self, base, score_client: ShardedScoreClient):
+        self.base, self.sc = base, score_client
+        self.world, self.rank = score_client.world, score_client.rank
+
+    def split(self, n: int):
+        share = [n // self.world + (1 if r < n % self.world else 0) for r in range(self.world)]
+        return sum(share[:self.rank]), share[self.rank]
+
+    def _collect(self, meta, E):
+        """Combiner thread: gather every rank's (meta, rows); rows [n, d] in candidate order on this rank's
+        device, or None when a rank failed (every rank sees the same metas, so all skip the tensor call)."""
+        import torch
+
+        metas = V.gather_objects(meta, self.sc.group)
+        if any(m is None or not m[0] for m in metas):
+            return metas, None
+        counts, d = [m[1] for m in metas], metas[0][2]
+        mx = max(counts)
+        if self.sc.data_backend != "nccl":
+            dev = torch.device("cpu")
+        else:
+            dev = E.device if E is not None else torch.device("cuda", torch.cuda.current_device())
+        pad = torch.zeros(mx, d, dtype=torch.float32, device=dev)
+        if E is not None and E.shape[0]:
+            pad[:E.shape[0]].copy_(E)
+        out = torch.empty(self.world * mx, d, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(out, pad, group=self.sc.data_group)
+        rows = torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
+        return metas, rows
+
+    async def run(self, seq: int, ids, request: C.ChatCompletionCreateParams, embedding_model: str,
+                  tau: float = 0.05) -> S.ScoreCompletion:
+        ctx = self.sc.request_ctx(seq, ids)
+        meta, E, err = None, None, None
+        try:
+            self.base._check_n(request)
+            first, cnt = self.split(int(request.n))
+            ctx["candidates"] = (first, cnt, ctx["seed"])
+            if cnt:
+                comp, E, ntok = await self.base.generate_embedded(ctx, request.model_copy(update={"n": cnt}),
+                                                                  embedding_model)
+                meta = (True, cnt, int(E.shape[1]), comp.to_obj(), int(ntok))
+            else:
+                emb = self.base._embedder(embedding_model)
+                meta = (True, 0, int(emb.encoder.cfg.hidden), None, 0)
+        except BaseException as e:  # noqa: BLE001 - every rank still takes the request's combine slot
+            err = e
+            meta = (False, 0, 0, f"{type(e).__name__}: {e}", 0)
+        metas, rows = await self.sc.combiner.submit(seq, lambda: self._collect(meta, E))
+        if err is not None:
+            raise err
+        if rows is None:
+            bad = next((r, m[3]) for r, m in enumerate(metas) if m is None or not m[0])
+            raise ScoreError(500, {"kind": "consensus_shard_failed",
+                                   "error": f"rank {bad[0]} failed to generate or embed its candidates: {bad[1]}"})
+        comps = [C.ChatCompletion.model_validate(m[3]) for m in metas if m[3] is not None]
+        merged = comps[0]
+        for c in comps[1:]:
+            merged.choices = merged.choices + c.choices
+            if merged.usage is not None and c.usage is not None:  # every rank's generation (each ran the prompt)
+                merged.usage.push(c.usage)
+            elif c.usage is not None:
+                merged.usage = c.usage.clone()
+        merged.choices.sort(key=lambda c: c.index)
+        ntok = sum(m[4] for m in metas)
+        emb = self.base._embedder(embedding_model)
+        out = self.base.build(merged, rows.to(emb.encoder.device), ntok, embedding_model, tau)
+        out.id = f"cnscpl-{ids[1].split('-', 1)[-1]}"  # one id on every rank (the leader's)
+        out.created = ids[0]
+        if self.rank == 0 and self.base.archive is not None:
+            self.base.archive.store_score(out)
+        return out
+
+
 # ---------------------------------------------------------------------------------------------
 # serving: rank 0 takes the HTTP requests and leads, the other ranks follow (SPMD)
 
@@ -196,16 +285,16 @@ class ScoreLeader:
     def __getattr__(self, name):
         return getattr(self.client, name)
 
-    def _announce_sync(self, request) -> tuple:
+    def _announce_sync(self, request, kind: str = "score") -> tuple:
         with self._lock:
             seq = self._seq
             self._seq += 1
             ids = ScoreClient._new_ids(self.client)
-            V.broadcast_object((seq, ids, request), 0, self.control)
+            V.broadcast_object((seq, ids, kind, request), 0, self.control)
         return seq, ids
 
-    async def _announce(self, request) -> tuple:
-        return await asyncio.get_running_loop().run_in_executor(self._announcer, self._announce_sync, request)
+    async def _announce(self, request, kind: str = "score") -> tuple:
+        return await asyncio.get_running_loop().run_in_executor(self._announcer, self._announce_sync, request, kind)
 
     async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
         seq, ids = await self._announce(request)
@@ -215,10 +304,26 @@ class ScoreLeader:
         seq, ids = await self._announce(request)
         return await self.client.open_stream(seq, ids, request)
 
+    async def create_consensus(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
+                               tau: float = 0.05) -> S.ScoreCompletion:
+        seq, ids = await self._announce((request, embedding_model, tau), "consensus")
+        return await self.client.consensus.run(seq, ids, request, embedding_model, tau)
+
     def close(self) -> None:
         self._announcer.shutdown(wait=True)
         V.broadcast_object(None, 0, self.control)
         self.client.close()
+
+
+class ConsensusLeader:
+    """Rank 0's /consensus/completions client in a voter-sharded deployment (see ShardedConsensusClient)."""
+
+    def __init__(self, leader: ScoreLeader):
+        self.leader = leader
+
+    async def create_unary(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
+                           tau: float = 0.05) -> S.ScoreCompletion:
+        return await self.leader.create_consensus(ctx, request, embedding_model, tau)
 
 
 def follow(client: ShardedScoreClient, control=None) -> int:
@@ -234,9 +339,12 @@ def follow(client: ShardedScoreClient, control=None) -> int:
         tasks: List[asyncio.Future] = []
         done = asyncio.Event()
 
-        async def one(seq, ids, request):
+        async def one(seq, ids, kind, request):
             try:
-                await client.run(seq, ids, request)
+                if kind == "consensus":
+                    await client.consensus.run(seq, ids, *request)
+                else:
+                    await client.run(seq, ids, request)
             except StatusError:
                 pass
 

@@ -111,14 +111,18 @@ def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     """LWC_SHARD_VOTERS: swap the score client for the voter-sharded one (a collective: every rank).
     Returns rank 0's leader (serve it) or, on the other ranks, the client to ``follow``."""
     from ..parallel import dist as pdist
-    from ..score.sharded import ScoreLeader, ShardedScoreClient
+    from ..score.sharded import ConsensusLeader, ScoreLeader, ShardedConsensusClient, ShardedScoreClient
 
     base = state.score
     client = ShardedScoreClient(base.chat, group=group, model_registry=base.models, weight_fetchers=base.weights,
                                 archive=base.archive, rng_seed=rng_seed)
+    # /consensus/completions: candidates split over the ranks, embedding rows all-gathered (C1)
+    client.consensus = ShardedConsensusClient(state.consensus, client) if state.consensus is not None else None
     if pdist.info().rank == 0:
         state.score = ScoreLeader(client)
         state.multichat.score = state.score
+        if state.consensus is not None:
+            state.consensus = ConsensusLeader(state.score)
         return state.score
     return client
 

@@ -36,7 +36,8 @@ def _rank(rank, port, q):
 
     try:
         info = pdist.init_from_env("cuda")
-        state = build_state(Config(models=MODELS, kv_fraction=0.04, gpu=info.local_rank))
+        state = build_state(Config(models=MODELS, embed_models={"e": {"arch": "bert-tiny", "weights": "random:1"}},
+                                   kv_fraction=0.04, gpu=info.local_rank))
         lead = shard_voters(state)
         if rank != 0:
             q.put((rank, follow(lead)))
@@ -57,6 +58,15 @@ def _rank(rank, port, q):
                 return await asyncio.gather(*(one(i) for i in range(5)))
 
             bodies = asyncio.run(go())
+
+            async def consensus():  # candidates split over the ranks, unit rows all-gathered (C1)
+                r = await client.post("/consensus/completions", json={
+                    "model": "tiny", "messages": [{"role": "user", "content": "Name a colour."}], "n": 6,
+                    "max_tokens": 12, "temperature": 0.9, "seed": 3, "embedding_model": "e"})
+                assert r.status_code == 200, r.text[:500]
+                return r.json()
+
+            cons = asyncio.run(consensus())
             lead.close()
             out = []
             for b in bodies:
@@ -66,6 +76,9 @@ def _rank(rank, port, q):
                             sum(1 for v in voters if v["message"].get("vote")),
                             round(sum(c["confidence"] for c in provided), 6),
                             sorted(c["index"] for c in b["choices"])))
+            out.append((sorted(c["index"] for c in cons["choices"]),
+                        round(sum(c["confidence"] for c in cons["choices"]), 5),
+                        len(cons["weight_data"]["embeddings_response"]["data"])))
             q.put((rank, out))
         for svc in state.services.values():
             svc.close()
@@ -85,7 +98,9 @@ def test_voter_sharded_serving_two_ranks_one_gpu(gpu):
     got = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert got[1] == 5, got  # the follower ran every request
+    assert got[1] == 6, got  # the follower ran every request
+    cons_indices, cons_conf, n_rows = got[0].pop()
+    assert cons_indices == list(range(6)) and cons_conf == pytest.approx(1.0) and n_rows == 6
     for n_provided, model_indices, n_votes, conf, indices in got[0]:
         assert n_provided == 3 and model_indices == [0, 1, 2, 3] and n_votes == 4, got[0]
         assert conf == pytest.approx(1.0) and indices == list(range(7))

@@ -1,0 +1,67 @@
+"""Whole-node serving layout, tensor-parallel: an LWC_MODELS spec with "tp": 2 served through the ASGI app.
+The EngineGroup runs the replica as two worker processes (here both on the one GPU of the box: the IPC
+one-shot all-reduce still crosses processes), the follower replaying the leader's ticks; the captured decode
+graph holds the all-reduce.  The TP=2 replica's greedy /chat/completions match a TP=1 worker's (up to near
+ties of the random-init model) and repeat exactly."""
+import asyncio
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SPEC = {"arch": "mixtral-tiny", "weights": "random:4", "max_model_len": 512, "max_batch": 64}
+
+
+def _serve(tp: int, bodies):
+    import httpx
+
+    from llm_weighted_consensus_amd.server.app import create_app
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+
+    spec = dict(SPEC, tp=tp)
+    state = build_state(Config(models={"moe": spec}, kv_fraction=0.2, gpus=[0] * tp, chunked_prefill=64))
+    try:
+        group = state.services["moe"]
+        assert len(group.procs) == 1 and len(group.followers[0]) == tp - 1
+
+        async def go():
+            client = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t",
+                                       timeout=300)
+            out = []
+            for b in bodies:  # sequential: the second identical request must repeat the first exactly
+                r = await client.post("/chat/completions", json=b)
+                assert r.status_code == 200, r.text
+                out.append(r.json())
+            return out
+
+        return asyncio.run(go())
+    finally:
+        for svc in state.services.values():
+            svc.close()
+
+
+def _trace(resp):
+    """Per choice: [(token, logprob, {top token: logprob})]."""
+    out = {}
+    for c in resp["choices"]:
+        out[c["index"]] = [(t["token"], t["logprob"], {x["token"]: x["logprob"] for x in t["top_logprobs"]})
+                           for t in c["logprobs"]["content"]]
+    return [out[i] for i in sorted(out)]
+
+
+@pytest.mark.timeout(600)
+def test_tp2_replica_serves_chat_like_tp1():
+    body = {"model": "moe", "messages": [{"role": "user", "content": "Name three rivers of Europe, briefly."}],
+            "n": 3, "temperature": 0, "max_tokens": 12, "logprobs": True, "top_logprobs": 3}
+    tp2 = _serve(2, [body, body])
+    tp1 = _serve(1, [body])
+    a, b, ref = _trace(tp2[0]), _trace(tp2[1]), _trace(tp1[0])
+    assert a == b  # the replica is deterministic across requests
+    assert len(a) == 3 and all(len(c) == 12 for c in a)
+    for got, want in zip(a, ref):
+        for step, ((tg, lg, topg), (tw, lw, topw)) in enumerate(zip(got, want)):
+            assert abs(lg - lw) < 3e-2, (step, lg, lw)
+            if tg != tw:  # TP sums in another order: only a near tie may flip
+                assert step > 0 and tw in topg and abs(topg[tw] - lg) < 3e-2, (step, tg, tw, topg)
+                break
