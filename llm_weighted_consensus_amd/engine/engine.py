@@ -100,6 +100,7 @@ class SequenceGroup:
     def __init__(self, engine: "LLMEngine", prompt_ids: List[int], params: SamplingParams, n: int,
                  callback: Optional[Callable[[TokenEvent], None]]):
         self.id = next(SequenceGroup._ids)
+        self._chain: Optional[List[int]] = None  # chained block hashes of the prompt (LLMEngine._block_chain)
         self.engine = engine
         self.prompt_ids = list(prompt_ids)
         self.params = params
@@ -617,7 +618,6 @@ class LLMEngine:
         if self.prefilling:
             items, _budget, _deferred = self._chunk_items(self.chunked_prefill)
             if items:
-                events += self._drain()  # the mixed step reads every running sequence's last token on the host
                 with span("prefill.mixed"):
                     events += self._mixed_step(items)
                 return events
@@ -629,13 +629,25 @@ class LLMEngine:
         """One forward over the decode rows of every running sequence and the prompt-chunk rows of
         ``items`` ((group, a, e): prompt tokens [a, e) of the group's parent sequence); the decode rows'
         next tokens and the first tokens of prompts completed by this chunk are sampled in one launch that
-        becomes the in-flight step.  Called with no step in flight."""
+        becomes the in-flight step.
+
+        Pipelined like the decode step: the forward is launched BEFORE the previous step is processed on the
+        host (the decode rows of sequences still in that step take their input token from its sampler output
+        on the device), the sampler after it (grammar masks need the previous tokens on the host).  A row of a
+        sequence that the previous step finishes is computed and discarded."""
         dev = self.device
+        events: List[TokenEvent] = []
+        prev, self.inflight = self.inflight, None
         self.running = [s for s in self.running if not s.finished]
         dec = [s for s in self.running if s.n_launched < s.params.max_tokens]
         if dec and self.bm.append_cost_total([s.id for s in dec]) > self.bm.num_free:
+            if prev is not None:  # preemption swaps KV out: nothing may be in flight
+                events += self._process(prev)
+                prev = None
+            self.running = [s for s in self.running if not s.finished]
             dec = self._preempt_for_growth()
         B = len(dec)
+        from_prev = None
         toks: List[int] = []
         pos: List[int] = []
         slot_parts: List[np.ndarray] = []
@@ -647,7 +659,11 @@ class LLMEngine:
             sl = np.zeros(B, np.int32)
             ps = np.zeros(B, np.int32)
             prepare_decode_into(self.bm, [s.id for s in dec], width, B, bt, cl, sl, ps)
-            toks.extend(s.tokens[-1] for s in dec)
+            prev_rows = {s.id: i for i, s in enumerate(prev.seqs)} if prev is not None else {}
+            src = [(i, prev_rows[s.id]) for i, s in enumerate(dec) if s.id in prev_rows]
+            if src:  # input tokens still on the device (the previous step's sampler output)
+                from_prev = (_h2d([a for a, _ in src], torch.int64, dev), _h2d([b for _, b in src], torch.int64, dev))
+            toks.extend(s.tokens[-1] if s.tokens else 0 for s in dec)
             pos.extend(ps.tolist())
             slot_parts.append(sl)
             dec_in = {"block_tables": _h2d(bt, torch.int32, dev), "ctx_lens": _h2d(cl, torch.int32, dev)}
@@ -680,9 +696,15 @@ class LLMEngine:
         if copies:
             self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
         rows = list(range(B)) + last_rows
-        logits = self.model.forward_mixed(_h2d(toks, torch.int32, dev), _h2d(pos, torch.int32, dev),
+        t_tok = _h2d(toks, torch.int32, dev)
+        if from_prev is not None:
+            t_tok.index_copy_(0, from_prev[0], prev.tok_dev.index_select(0, from_prev[1]).to(torch.int32))
+        logits = self.model.forward_mixed(t_tok, _h2d(pos, torch.int32, dev),
                                           _h2d(np.concatenate(slot_parts), torch.int32, dev), self.cache, B, dec_in,
                                           chunk_in, _h2d(rows, torch.int64, dev))
+        if prev is not None:  # host bookkeeping of the previous step while this forward runs
+            with span("decode.process"):
+                events += self._process(prev)
         self.stats["prefill_tokens"] += cu[-1]
         self.stats["prefill_chunks"] = self.stats.get("prefill_chunks", 0) + 1
         self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
@@ -693,9 +715,9 @@ class LLMEngine:
         done, pick = [], list(range(B))
         for i, (g, a, e) in enumerate(items):
             g.pf_pos = e
+            if self.prefix_caching:  # register the blocks computed so far: prompts waiting on them can start
+                self.bm.cache_prefix(-g.id, g.prompt_ids if e == len(g.prompt_ids) else g.prompt_ids[:e])
             if e == len(g.prompt_ids):
-                if self.prefix_caching:
-                    self.bm.cache_prefix(-g.id, g.prompt_ids)
                 done.append((g, B + i))
         children: List[Sequence] = []
         if done:
@@ -715,32 +737,53 @@ class LLMEngine:
             self.inflight = self._launch_first(sel, seqs, [g for g, _ in done])
             self.running.extend(children)
             self._comp_cache = (None, None)
-        return []
+        return events
+
+    def _block_chain(self, g: SequenceGroup) -> List[int]:
+        """Chained hashes of the prompt's full blocks (block i's hash covers tokens [0, 16(i+1))), computed once
+        per prompt: equal chains = a shared prefix, block for block."""
+        ch = g._chain
+        if ch is None:
+            p, bs, h = g.prompt_ids, self.block_size, 0
+            ch = []
+            for i in range((len(p) - 1) // bs):
+                h = hash((h, tuple(p[i * bs:(i + 1) * bs])))
+                ch.append(h)
+            g._chain = ch
+        return ch
 
     def _chunk_items(self, budget: int):
+        """This step's prompt chunks: (group, a, e) = prompt tokens [a, e), at most ``budget`` tokens, prompts
+        in admission order.  A prompt not started yet whose next uncached block another prompt in progress is
+        about to compute (the voters of one score request share their messages head; every request shares
+        the instructions) waits for it and then takes the shared blocks from the prefix cache — blocks are
+        registered chunk by chunk, so it waits only until the shared part is computed, not the whole prompt."""
         bs = self.block_size
         items: List[Tuple[SequenceGroup, int, int]] = []
-        heads = set()
         deferred = False
+        pending: set = set()  # chain hashes of blocks that prompts in progress have not computed yet
+        if self.prefix_caching:
+            for g in self.prefilling:
+                if g.pf_pos >= 0:
+                    ch = self._block_chain(g)
+                    pending.update(ch[g.pf_pos // bs:])
         for g in self.prefilling:
             if budget <= 0:
                 break
             p = g.prompt_ids
-            head = tuple(p[:bs]) if len(p) > bs else None
             if g.pf_pos < 0:
-                # a prompt sharing its first block with one in progress waits for it and then takes the
-                # shared head from the prefix cache (the voters of one score request)
-                if self.prefix_caching and head is not None and head in heads:
-                    deferred = True
-                    continue
                 if self.prefix_caching:
+                    ch = self._block_chain(g)
+                    k = int(self.bm.match_prefix(p)) // bs
+                    if k < len(ch) and ch[k] in pending:
+                        deferred = True
+                        continue
                     g.pf_pos = int(self.bm.add_sequence_cached(-g.id, p))
                     self.stats["prefix_cache_tokens"] += g.pf_pos
+                    pending.update(ch[g.pf_pos // bs:])
                 else:
                     self.bm.add_sequence(-g.id, len(p))
                     g.pf_pos = 0
-            if head is not None:
-                heads.add(head)
             n = min(budget, len(p) - g.pf_pos)
             items.append((g, g.pf_pos, g.pf_pos + n))
             budget -= n

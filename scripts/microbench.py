@@ -378,6 +378,22 @@ def prefill_attn(dev):
               f"paged {t_p:7.1f} us ({fl / t_p * 1e6:4.0f} TF/s)", flush=True)
 
 
+def bandwidth(dev):
+    """HBM calibration: streaming read (sum), copy (read + write), and 4 KiB-segment gathers in random order
+    (the decode attention's access pattern) — bytes moved / time."""
+    n = 1 << 30  # 2 GiB of bf16
+    x = torch.empty(n, dtype=torch.bfloat16, device=dev).normal_()
+    y = torch.empty_like(x)
+    us = timeit(lambda: x.sum(), iters=10)
+    print(f"bw read (sum)   : {2 * n / us / 1e6:7.0f} GB/s", flush=True)
+    us = timeit(lambda: y.copy_(x), iters=10)
+    print(f"bw copy (r + w) : {4 * n / us / 1e6:7.0f} GB/s", flush=True)
+    seg = x.view(-1, 2048)  # 4 KiB rows
+    idx = torch.randperm(seg.shape[0], device=dev)[: seg.shape[0] // 2]
+    us = timeit(lambda: seg.index_select(0, idx), iters=10)
+    print(f"bw 4KiB gather  : {2 * idx.numel() * 4096 / us / 1e6:7.0f} GB/s (read + write)", flush=True)
+
+
 def moe_decode(dev):
     """Mixtral decode MoE at the config-5 batch: fp8 experts, T tokens x top-2 over 8 experts, balanced and
     router-driven (uneven) segments; time and the expert-weight bytes streamed per second."""
@@ -473,6 +489,8 @@ def main():
         gemm_layouts(dev, [int(m) for m in os.environ.get("MICRO_M", "512,1024").split(",")])
     if "attn" in a.what:
         attention(dev)
+    if "bw" in a.what:
+        bandwidth(dev)
     if "pfattn" in a.what:
         prefill_attn(dev)
     if "prefix" in a.what:

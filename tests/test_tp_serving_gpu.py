@@ -2,7 +2,7 @@
 The EngineGroup runs the replica as two worker processes (here both on the one GPU of the box: the IPC
 one-shot all-reduce still crosses processes), the follower replaying the leader's ticks; the captured decode
 graph holds the all-reduce.  The TP=2 replica's greedy /chat/completions match a TP=1 worker's (up to near
-ties of the random-init model) and repeat exactly."""
+ties of the random-init model), also when repeated (prompt from the prefix cache)."""
 import asyncio
 
 import pytest
@@ -57,11 +57,16 @@ def test_tp2_replica_serves_chat_like_tp1():
     tp2 = _serve(2, [body, body])
     tp1 = _serve(1, [body])
     a, b, ref = _trace(tp2[0]), _trace(tp2[1]), _trace(tp1[0])
-    assert a == b  # the replica is deterministic across requests
     assert len(a) == 3 and all(len(c) == 12 for c in a)
-    for got, want in zip(a, ref):
-        for step, ((tg, lg, topg), (tw, lw, topw)) in enumerate(zip(got, want)):
-            assert abs(lg - lw) < 3e-2, (step, lg, lw)
-            if tg != tw:  # TP sums in another order: only a near tie may flip
-                assert step > 0 and tw in topg and abs(topg[tw] - lg) < 3e-2, (step, tg, tw, topg)
-                break
+    # the repeat takes the prompt from the prefix cache (other kernels for the head): equal up to float noise
+    for run in (a, b):
+        for got, want in zip(run, ref):
+            _same_up_to_near_tie(got, want)
+
+
+def _same_up_to_near_tie(got, want, tol=3e-2):
+    for step, ((tg, lg, topg), (tw, lw, topw)) in enumerate(zip(got, want)):
+        assert abs(lg - lw) < tol, (step, lg, lw)
+        if tg != tw:  # TP sums in another order: only a near tie may flip
+            assert step > 0 and tw in topg and abs(topg[tw] - lg) < tol, (step, tg, tw, topg)
+            break
