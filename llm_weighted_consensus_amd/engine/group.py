@@ -634,6 +634,7 @@ def build_engine(spec: dict, wid: int):
                      kv_memory_fraction=kv_fraction, num_blocks=num_blocks,
                      use_graphs=getattr(model, "graph_safe", True),
                      prefix_caching=bool(spec.get("prefix_caching", True)),
-                     chunked_prefill=int(spec.get("chunked_prefill", 0)),
+                     # the paged-KV prefill kernel of mixed steps is built for head_dim 128
+                     chunked_prefill=int(spec.get("chunked_prefill", 0)) if cfg.head_dim == 128 else 0,
                      constrained_logprobs=bool(spec.get("constrained_logprobs", False)),
                      kv_reserve_tokens=spec.get("kv_reserve_tokens", 256))

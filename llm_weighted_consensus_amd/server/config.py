@@ -18,9 +18,10 @@ variables configure the local engine:
   LWC_KV_FRACTION   fraction of free HBM given to the paged KV cache (default 0.85)
   LWC_ARCHIVE_PATH  append-only JSONL log of completions (checkpoint/resume of the archive)
   LWC_REGISTRY_PATH JSON file persisting registered score models
-  LWC_CHUNKED_PREFILL prompt tokens prefilled per engine step, interleaved with decode (e.g. 2048; default
-                    0 = whole admission batches before decoding: the higher-throughput schedule for the
-                    prefill-heavy voter load, profiles/serve_load.md)
+  LWC_CHUNKED_PREFILL prompt tokens per engine step (default 2048): each step is ONE forward over every
+                    running sequence's next token and up to this many prompt tokens (mixed chunked prefill,
+                    paged-KV prefill attention); 0 = whole admission batches before decoding.  4096 trades
+                    p99 for throughput (profiles/serve_load.md)
   LWC_TRAINING_TABLE_PATH  append-only JSONL of training-table rows (learned voter weights), replayed on start
   LWC_FAULT         fault injection for tests: worker_crash | slow_decode | bad_logprobs | oom
   LWC_CONSTRAINED_LOGPROBS  1: constrained (json_schema / tool-call) voters get logprobs over the allowed
@@ -83,7 +84,7 @@ class Config:
     device: str = "cuda"
     constrained_logprobs: bool = False
     prefix_caching: bool = True
-    chunked_prefill: int = 0
+    chunked_prefill: int = 2048
     kv_fraction: float = 0.85
     archive_path: Optional[str] = None
     training_table_path: Optional[str] = None
@@ -121,7 +122,7 @@ class Config:
         c.device = e.get("LWC_DEVICE", "cuda").lower()
         c.constrained_logprobs = e.get("LWC_CONSTRAINED_LOGPROBS", "0") == "1"
         c.prefix_caching = e.get("LWC_PREFIX_CACHE", "1") == "1"
-        c.chunked_prefill = int(e.get("LWC_CHUNKED_PREFILL", "0"))
+        c.chunked_prefill = int(e.get("LWC_CHUNKED_PREFILL", "2048"))
         if e.get("LWC_GPUS"):
             c.gpus = [int(x) for x in e["LWC_GPUS"].split(",") if x.strip()]
         c.kv_fraction = float(e.get("LWC_KV_FRACTION", "0.85"))

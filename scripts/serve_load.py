@@ -88,7 +88,7 @@ def main():
     t0 = time.time()
     gpus = [int(x) for x in a.gpus.split(",") if x.strip()]
     state = build_state(Config(models=models, kv_fraction=0.6, gpus=gpus,
-                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "0"))))
+                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "2048"))))
     print(f"# model ready in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     app = create_app(state)
     client = httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t", timeout=600)
@@ -140,6 +140,7 @@ def main():
            "prefill_tokens": stats["prefill_tokens"] - p0,
            "prefix_cache_tokens": stats["prefix_cache_tokens"] - c0,
            "serving": f"EngineGroup workers on GPUs {gpus}" if gpus else "in-process engine",
+           "chunked_prefill": int(os.environ.get("LWC_CHUNKED_PREFILL", "2048")),
            "config": {"arch": a.arch, "concurrency": a.concurrency, "requests": a.requests, "voters": a.voters,
                       "choices": a.choices, "output_mode": "json_schema", "data": "synthetic prompts, random-init"}}
     from llm_weighted_consensus_amd.utils.tracing import STATS
