@@ -49,6 +49,7 @@ int lwc_ar_handle_bytes();
 int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long long, int*, int, long long, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
+int lwc_knn_topk(const float*, int, int, const float*, int, float*, int*, float*, int*, hipStream_t);
 }
 
 namespace {
@@ -520,6 +521,23 @@ void pool_l2norm(const at::Tensor& hidden, const at::Tensor& cu_seqlens, int64_t
            "pool_l2norm");
 }
 
+std::vector<at::Tensor> knn_topk(const at::Tensor& E, const at::Tensor& q, int64_t k) {
+  // E [n, d] f32 (contiguous rows), q [d] f32 -> (values [k] f32, rows [k] int32), best first, ties to the lower row
+  CHECK_GPU(E); CHECK_GPU(q); CHECK_CONTIG(E); CHECK_CONTIG(q);
+  CHECK_DTYPE(E, at::kFloat); CHECK_DTYPE(q, at::kFloat);
+  TORCH_CHECK(E.dim() == 2 && q.numel() == E.size(1) && E.size(1) % 4 == 0, "knn_topk: E [n, d] (d % 4 == 0), q [d]");
+  const int n = (int)E.size(0), d = (int)E.size(1);
+  TORCH_CHECK(k >= 1 && k <= 64 && k <= n, "knn_topk: 1 <= k <= min(64, n)");
+  const int slabs = (n + 255) / 256;
+  auto opts = E.options();
+  at::Tensor pv = at::empty({(int64_t)slabs * k}, opts), vals = at::empty({k}, opts);
+  at::Tensor pi = at::empty({(int64_t)slabs * k}, opts.dtype(at::kInt)), rows = at::empty({k}, opts.dtype(at::kInt));
+  CHECK_RC(lwc_knn_topk(E.data_ptr<float>(), n, d, q.data_ptr<float>(), (int)k, pv.data_ptr<float>(),
+                        pi.data_ptr<int>(), vals.data_ptr<float>(), rows.data_ptr<int>(), cur_stream()),
+           "knn_topk");
+  return {vals, rows};
+}
+
 void cosine_consensus(const at::Tensor& E, at::Tensor& S, double inv_tau, at::Tensor& centrality, at::Tensor& weights,
                       at::Tensor& best) {
   // E: [R, n, d] bf16; S: [R, n_pad, n_pad] f32
@@ -600,6 +618,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);
+  m.def("knn_topk", &knn_topk);
   m.def("gemm8g_fp8", &gemm8g_fp8);
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_open", &ar_open);

@@ -2,6 +2,9 @@
 //   K9d  pool_l2norm        : CLS / mean / last-token pooling of encoder states + L2 normalisation;
 //   K10a cosine_consensus    : S = E E^T on MFMA (16x16 tiles, one wave each) followed by a row-reduce
 //                              + softmax kernel -> per-candidate centrality and consensus weights.
+//   K10c knn_topk           : training-table neighbour search — cosine of one query against every table row
+//                              and the `top` best rows, in two launches: per 256-row slab a wave-per-row dot
+//                              product into LDS and a block top-k, then one workgroup merges the slab winners.
 // (The voter tally of the reference, src/score/completions/client.rs:384-455, is ~L x C <= 128 x 20
 // multiply-adds per request: it runs in the C++ consensus core on the host, next to the vote
 // extraction that feeds it — a kernel launch would cost more than the arithmetic.)
@@ -96,7 +99,123 @@ __global__ void __launch_bounds__(256) consensus_reduce_kernel(const float* __re
   }
 }
 
+// ---- K10c: top-k rows of E [n, d] f32 by dot product with q [d] --------------------------------------
+constexpr int kKnnRows = 256;  // rows per slab (one workgroup)
+constexpr int kKnnMaxK = 64;
+
+// The k largest of vals[0..m) (LDS), in order, ties to the lower index; consumed entries become -inf.
+// Writes (value, index from idx[] or the position) to out_v / out_i.  256 threads.
+LWC_DEVICE void block_topk(float* vals, const int* idx, int m, int k, float* out_v, int* out_i, float* red_v,
+                           int* red_i) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int r = 0; r < k; ++r) {
+    float bv = -INFINITY;
+    int bp = 0x7fffffff;
+    for (int i = tid; i < m; i += 256) {
+      const float v = vals[i];
+      if (v > bv) {  // strided walk: the first hit of a value is this thread's lowest position
+        bv = v;
+        bp = i;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int op = __shfl_xor(bp, o, 64);
+      if (ov > bv || (ov == bv && op < bp)) {
+        bv = ov;
+        bp = op;
+      }
+    }
+    if (lane == 0) {
+      red_v[wid] = bv;
+      red_i[wid] = bp;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float v = red_v[0];
+      int pidx = red_i[0];
+      for (int w = 1; w < 4; ++w)
+        if (red_v[w] > v || (red_v[w] == v && red_i[w] < pidx)) {
+          v = red_v[w];
+          pidx = red_i[w];
+        }
+      out_v[r] = v;
+      out_i[r] = pidx < m ? (idx ? idx[pidx] : pidx) : -1;
+      if (pidx < m) vals[pidx] = -INFINITY;
+    }
+    __syncthreads();
+  }
+}
+
+// slab s: rows [256 s, 256 s + 256): one wave per row at a time, float4 loads along d
+__global__ void __launch_bounds__(256) knn_slab_kernel(const float* __restrict__ E, int n, int d,
+                                                       const float* __restrict__ q, int k, float* __restrict__ part_v,
+                                                       int* __restrict__ part_i) {
+  __shared__ float sims[kKnnRows];
+  __shared__ float red_v[4];
+  __shared__ int red_i[4];
+  const int s = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r0 = s * kKnnRows;
+  for (int rr = wid; rr < kKnnRows; rr += 4) {
+    const int row = r0 + rr;
+    float acc = 0.f;
+    if (row < n) {
+      const float4v* e = reinterpret_cast<const float4v*>(E + (size_t)row * d);
+      const float4v* qq = reinterpret_cast<const float4v*>(q);
+      for (int c = lane; c < d / 4; c += 64) {
+        const float4v a = e[c], b = qq[c];
+        acc += a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) sims[rr] = row < n ? acc : -INFINITY;
+  }
+  __syncthreads();
+  __shared__ float out_v[kKnnMaxK];
+  __shared__ int out_i[kKnnMaxK];
+  block_topk(sims, nullptr, kKnnRows, k, out_v, out_i, red_v, red_i);
+  for (int r = threadIdx.x; r < k; r += 256) {
+    part_v[(size_t)s * k + r] = out_v[r];
+    part_i[(size_t)s * k + r] = out_i[r] >= 0 ? r0 + out_i[r] : -1;
+  }
+}
+
+// merge: the k best of the slabs' k winners each (ties to the lower row)
+__global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict__ part_v, const int* __restrict__ part_i,
+                                                        int m, int k, float* __restrict__ vals, int* __restrict__ rows) {
+  extern __shared__ float smem_knn[];
+  float* v = smem_knn;
+  int* ix = reinterpret_cast<int*>(smem_knn + m);
+  __shared__ float red_v[4];
+  __shared__ int red_i[4];
+  __shared__ float out_v[kKnnMaxK];
+  __shared__ int out_i[kKnnMaxK];
+  for (int i = threadIdx.x; i < m; i += 256) {
+    v[i] = part_i[i] >= 0 ? part_v[i] : -INFINITY;
+    ix[i] = part_i[i];
+  }
+  __syncthreads();
+  // ties across slabs resolve by slab order = row order: slab winners are stored slab-major
+  block_topk(v, ix, m, k, out_v, out_i, red_v, red_i);
+  for (int r = threadIdx.x; r < k; r += 256) {
+    vals[r] = out_v[r];
+    rows[r] = out_i[r];
+  }
+}
+
 }  // namespace lwc
+
+extern "C" int lwc_knn_topk(const float* E, int n, int d, const float* q, int k, float* part_v, int* part_i,
+                            float* vals, int* rows, hipStream_t s) {
+  using namespace lwc;
+  if (d % 4 != 0 || k < 1 || k > kKnnMaxK || k > n) return -1;
+  const int slabs = (n + kKnnRows - 1) / kKnnRows;
+  const int m = slabs * k;
+  if ((size_t)m * 8 > 60 * 1024) return -2;  // merge image in LDS (n up to ~1.9 M rows at k = 16)
+  knn_slab_kernel<<<slabs, 256, 0, s>>>(E, n, d, q, k, part_v, part_i);
+  knn_merge_kernel<<<1, 256, (size_t)m * 8, s>>>(part_v, part_i, m, k, vals, rows);
+  return (int)hipGetLastError();
+}
 
 extern "C" int lwc_pool_l2norm(const void* hidden, int ld, const int* cu, int nseq, int d, int mode, float* out_f32,
                                void* out_bf16, hipStream_t s) {

@@ -466,6 +466,13 @@ def pool_l2norm(hidden: torch.Tensor, cu_seqlens: torch.Tensor, mode: int, out_b
     return of, ob
 
 
+def knn_topk(E: torch.Tensor, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """K10c: the ``k`` rows of ``E`` [n, d] f32 with the largest dot product with ``q`` [d] — (values [k] f32,
+    rows [k] int64), best first, ties to the lower row (torch.topk's order up to ties).  k <= 64."""
+    vals, rows = kernels().knn_topk(E.contiguous(), q.reshape(-1).contiguous().to(E.dtype), int(k))
+    return vals, rows.long()
+
+
 def cosine_consensus(E: torch.Tensor, tau: float = 0.05):
     """Embedding consensus over R requests x n candidates (K10a): S = E E^T on MFMA, then
     centrality_i = mean_{j!=i} S_ij and weights = softmax(centrality / tau).

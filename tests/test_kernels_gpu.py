@@ -777,3 +777,26 @@ def test_gemm4w(gpu, M, N, K, epi, bn):
             want = ref + (R.float() if R is not None else 0)
             out = ops.gemm4w(A, W, residual=R, out=R if R is not None else None, bn=bn)
             _close(out, want, 3e-2, 1e-2)
+
+
+@pytest.mark.parametrize("n,d,k", [(37, 1024, 5), (1000, 1024, 16), (70000, 384, 64), (300, 4096, 1)])
+def test_knn_topk(gpu, n, d, k):
+    """K10c training-table neighbour search == torch.topk of the fp32 dot products (rows with tied scores:
+    duplicates of a row, the lower row first)."""
+    from llm_weighted_consensus_amd import ops
+
+    g = torch.Generator(device=gpu).manual_seed(n)
+    E = torch.nn.functional.normalize(torch.randn(n, d, device=gpu, generator=g), dim=1)
+    q = torch.nn.functional.normalize(torch.randn(d, device=gpu, generator=g), dim=0)
+    if n > 10:
+        best = int((E @ q).argmax())
+        E[n - 3] = E[best]  # a tie with the best row
+    vals, rows = ops.knn_topk(E, q, k)
+    ref_v, _ = (E.double() @ q.double()).topk(k)
+    assert torch.allclose(vals.double(), ref_v, atol=1e-5)
+    got = (E.double() @ q.double())[rows]
+    assert torch.allclose(got, ref_v, atol=1e-5)  # the rows hold those values
+    assert len(set(rows.tolist())) == k
+    if n > 10 and k > 1:
+        r = rows.tolist()
+        assert r.index(best) < r.index(n - 3)  # ties: lower row first

@@ -95,8 +95,46 @@ def test_weights_learn_from_scored_requests_and_replay(tmp_path):
     other = _voter_weights(asyncio.run(go("Tell me a joke")))
     assert other == {"good-1": 1.0, "good-2": 1.0, "contrarian": 1.0}
     # resume: a fresh fetcher replays the JSONL and weights the next request identically
+    tt.flush()  # the journal thread has written every recorded row
     tt2 = TrainingTableWeights(_embedder, path=path)
     c2 = ScoreClient(FakeChatClient(_policy), weight_fetchers=WeightFetchers(training_table=tt2))
     again = _voter_weights(asyncio.run(c2.create_unary(None, _request("What is the capital of France?"))))
     assert next(iter(tt2.tables.values())).n >= 6
     assert again["good-1"] == pytest.approx(later["good-1"], rel=0.2) and again["contrarian"] < 1.0
+
+
+def test_table_is_a_bounded_ring_and_the_journal_compacts(tmp_path):
+    """max_rows bounds a table (the oldest rows are overwritten); the journal is rewritten from the
+    resident rows once it holds twice as many lines, and replaying it gives the same table."""
+    from llm_weighted_consensus_amd.score.weights import TrainingTable
+
+    t = TrainingTable(4, "cpu", capacity=2, max_rows=5)
+    for i in range(12):
+        t.add(torch.full((4,), float(i)), {0: i / 12})
+    assert t.n == 5 and sorted(t.E[:, 0].tolist()) == [7.0, 8.0, 9.0, 10.0, 11.0]
+    E, A = t.rows_in_order()
+    assert E[:, 0].tolist() == [7.0, 8.0, 9.0, 10.0, 11.0] and A[:, 0].tolist() == pytest.approx([i / 12 for i in range(7, 12)])
+
+    path = str(tmp_path / "tt.jsonl")
+    tt = TrainingTableWeights(_embedder, path=path, max_rows=8, compact_min_lines=10)
+
+    class M:  # the two fields record() reads
+        training_table_id = "tbl"
+        llms = [type("L", (), {"training_table_index": 0})(), type("L", (), {"training_table_index": 1})()]
+
+    g = torch.Generator().manual_seed(0)
+    embs = [torch.nn.functional.normalize(torch.randn(8, generator=g), dim=0).tolist() for _ in range(40)]
+    for i, e in enumerate(embs):
+        tt.record(M, e, {0: 0.25, 1: i / 40})
+    tt.flush()
+    assert tt.journal.compactions >= 1
+    with open(path) as f:
+        lines = [l for l in f if l.strip()]
+    assert len(lines) <= max(10, 2 * 8)
+    tt2 = TrainingTableWeights(_embedder, path=path, max_rows=8)
+    a, b = tt.tables["tbl"], tt2.tables["tbl"]
+    assert a.n == b.n == 8
+    Ea, Aa = a.rows_in_order()
+    Eb, Ab = b.rows_in_order()
+    assert torch.allclose(Ea, Eb) and torch.allclose(Aa, Ab, equal_nan=True)
+    assert torch.allclose(Ea, torch.tensor(embs[-8:]))  # the newest 8 survive, oldest first
