@@ -33,7 +33,7 @@ from typing import Any, Dict, List, Optional
 
 from .sampling import SamplingParams
 from .service import EngineFailure
-from .shm_ring import ShmRing, decode_events, encode_events
+from .shm_ring import ShmRing, decode_record, encode_embeddings, encode_events
 
 
 @dataclass
@@ -123,6 +123,21 @@ def _apply(engine, msg, groups: Dict[int, Any], cb_for, emb_req, on_error) -> No
             engine.abort(g)
 
 
+def _push(ring, record: bytes, ev_q, fallback, hb, stop) -> None:
+    """One record into the worker's ring: waits (heart-beating) while the ring is full — the front end's
+    reader drains it — and never re-sends through the pickled queue unless there is no ring at all."""
+    if ring is None:
+        ev_q.put(fallback)
+        return
+
+    def beat():
+        hb.value = time.time()
+
+    while not ring.push(record, timeout=5.0, on_wait=beat):
+        if stop.is_set():
+            return
+
+
 def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None,
                 mirror_out: Optional[list] = None, mirror_in=None) -> None:
     """Worker process: build the engine, serve requests until told to stop.
@@ -199,11 +214,7 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                     if rid is not None:
                         ev_q.put(("error", wid, (rid, f"{type(e).__name__}: {e}")))
         if batch:
-            def beat():
-                hb.value = time.time()
-
-            if ring is None or not ring.push(encode_events(batch), timeout=5.0, on_wait=beat):
-                ev_q.put(("tokens", wid, batch))  # no ring (or the reader is gone): the slow path
+            _push(ring, encode_events(batch), ev_q, ("tokens", wid, batch), hb, stop)
             batch = []
         for rid in [r for r, g in groups.items() if g.finished]:
             groups.pop(rid)
@@ -217,7 +228,9 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
                         dev = spec.get("embed_device") or f"cuda:{int(spec.get('device', 0))}"
                         svc = embedders[name] = build_embedding_service(name, spec["embed_models"][name], dev)
                     E, ntok = svc.embed_texts(texts)
-                    ev_q.put(("emb", wid, (rid, offset, E.float().cpu().numpy(), int(ntok))))
+                    rows = E.float().cpu().numpy()
+                    _push(ring, encode_embeddings(rid, offset, rows, int(ntok)), ev_q,
+                          ("emb", wid, (rid, offset, rows, int(ntok))), hb, stop)
                 except Exception as e:  # noqa: BLE001 - reported to the request, the worker keeps serving
                     ev_q.put(("emb_err", wid, (rid, f"{type(e).__name__}: {e}")))
     if mirror_out:
@@ -413,7 +426,11 @@ class EngineGroup:
                     if rec is None:
                         break
                     busy = True
-                    self._on_tokens(wid, decode_events(rec))
+                    kind, payload = decode_record(rec)
+                    if kind == "tokens":
+                        self._on_tokens(wid, payload)
+                    else:  # a worker's embedding rows, in the ring after its candidates' last tokens
+                        self._on_embeddings("emb", payload)
             try:
                 kind, wid, payload = self.ev_q.get_nowait()
             except pyqueue.Empty:

@@ -11,7 +11,9 @@ Ring layout (one per worker): [head u64][tail u64][pad to 64 B][data: cap bytes]
 written) is stored only by the producer, ``tail`` (bytes consumed) only by the consumer; each is an
 aligned 8-byte store, and a record's bytes are written before ``head`` moves past them (x86-64 keeps
 store order), so the consumer never sees a torn record.  A record is [len u32][payload], padded to 8
-bytes; a len of 0xFFFFFFFF marks "wrap to the start".
+bytes; a len of 0xFFFFFFFF marks "wrap to the start".  Payloads start with a kind word: one engine step's
+token events, or the unit embedding rows of a request portion the worker embedded (a /consensus request's
+candidates), raw float32.
 
 The reference has no counterpart (its voters are remote HTTP streams): this is the transport of the
 multi-GPU candidate fan-out (src/score/completions/client.rs:343-356) inside one node.
@@ -119,6 +121,29 @@ class ShmRing:
 # one engine step's events <-> one record
 
 
+KIND_EVENTS, KIND_EMB = 1, 2
+
+
+def encode_embeddings(rid: int, offset: int, rows: np.ndarray, ntok: int) -> bytes:
+    """A worker's unit embedding rows [n, d] float32 of one request portion as one record (no pickling)."""
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    n, d = rows.shape
+    head = np.array([KIND_EMB, n, d, 0], dtype=np.uint32)
+    meta = np.array([rid, offset, ntok], dtype=np.int64)
+    return b"".join((head.tobytes(), meta.tobytes(), rows.tobytes()))
+
+
+def decode_record(buf: bytes):
+    """("tokens", events) or ("emb", (rid, offset, rows [n, d] float32, ntok))."""
+    kind = int(np.frombuffer(buf, dtype=np.uint32, count=1)[0])
+    if kind == KIND_EMB:
+        _, n, d, _ = np.frombuffer(buf, dtype=np.uint32, count=4).tolist()
+        rid, offset, ntok = np.frombuffer(buf, dtype=np.int64, count=3, offset=16).tolist()
+        rows = np.frombuffer(buf, dtype=np.float32, count=n * d, offset=40).reshape(n, d).copy()
+        return "emb", (rid, offset, rows, ntok)
+    return "tokens", decode_events(buf)
+
+
 def encode_events(events: Sequence[tuple]) -> bytes:
     """events: (rid, idx, token_id, text, logprob, [(top_id, top_lp), ...], finished, reason)."""
     n = len(events)
@@ -137,12 +162,12 @@ def encode_events(events: Sequence[tuple]) -> bytes:
     top_ids = np.array([x[0] for x in flat], dtype=np.int32)
     top_lps = np.array([x[1] for x in flat], dtype=np.float32)
     blob = b"".join(texts)
-    head = np.array([n, len(flat), len(blob), 0], dtype=np.uint32)
+    head = np.array([KIND_EVENTS, n, len(flat), len(blob)], dtype=np.uint32)
     return b"".join((head.tobytes(), rec.tobytes(), top_ids.tobytes(), top_lps.tobytes(), blob))
 
 
 def decode_events(buf: bytes) -> List[Tuple]:
-    n, ntop, nblob, _ = np.frombuffer(buf, dtype=np.uint32, count=4).tolist()
+    _, n, ntop, nblob = np.frombuffer(buf, dtype=np.uint32, count=4).tolist()
     off = 16
     rec = np.frombuffer(buf, dtype=EVENT_DTYPE, count=n, offset=off)
     off += n * EVENT_DTYPE.itemsize

@@ -91,3 +91,18 @@ def test_cross_process_producer():
         assert got == n and p.exitcode == 0
     finally:
         r.close()
+
+
+def test_embedding_record_roundtrip_and_kinds():
+    """A worker's embedding rows travel as one raw float32 record; the reader tells the kinds apart."""
+    import numpy as np
+
+    from llm_weighted_consensus_amd.engine.shm_ring import decode_record, encode_embeddings
+
+    rows = np.random.default_rng(0).standard_normal((5, 1024)).astype(np.float32)
+    kind, (rid, off, got, ntok) = decode_record(encode_embeddings(77, 3, rows, 1234))
+    assert kind == "emb" and (rid, off, ntok) == (77, 3, 1234) and np.array_equal(got, rows)
+    ev = _events(1, 3)
+    kind, got_ev = decode_record(encode_events(ev))
+    assert kind == "tokens"
+    _same(got_ev, ev)
