@@ -530,8 +530,8 @@ std::vector<at::Tensor> knn_topk(const at::Tensor& E, const at::Tensor& q, int64
   TORCH_CHECK(k >= 1 && k <= 64 && k <= n, "knn_topk: 1 <= k <= min(64, n)");
   const int slabs = (n + 255) / 256;
   auto opts = E.options();
-  at::Tensor pv = at::empty({(int64_t)slabs * k}, opts), vals = at::empty({k}, opts);
-  at::Tensor pi = at::empty({(int64_t)slabs * k}, opts.dtype(at::kInt)), rows = at::empty({k}, opts.dtype(at::kInt));
+  at::Tensor pv = at::empty({2 * (int64_t)slabs * k}, opts), vals = at::empty({k}, opts);
+  at::Tensor pi = at::empty({2 * (int64_t)slabs * k}, opts.dtype(at::kInt)), rows = at::empty({k}, opts.dtype(at::kInt));
   CHECK_RC(lwc_knn_topk(E.data_ptr<float>(), n, d, q.data_ptr<float>(), (int)k, pv.data_ptr<float>(),
                         pi.data_ptr<int>(), vals.data_ptr<float>(), rows.data_ptr<int>(), cur_stream()),
            "knn_topk");

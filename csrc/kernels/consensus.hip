@@ -3,8 +3,9 @@
 //   K10a cosine_consensus    : S = E E^T on MFMA (16x16 tiles, one wave each) followed by a row-reduce
 //                              + softmax kernel -> per-candidate centrality and consensus weights.
 //   K10c knn_topk           : training-table neighbour search — cosine of one query against every table row
-//                              and the `top` best rows, in two launches: per 256-row slab a wave-per-row dot
-//                              product into LDS and a block top-k, then one workgroup merges the slab winners.
+//                              and the `top` best rows: per 256-row slab a wave-per-row dot
+//                              product into LDS and a block top-k, then the slab winners are merged level by
+//                              level (up to 4096 candidates per merging workgroup).
 // (The voter tally of the reference, src/score/completions/client.rs:384-455, is ~L x C <= 128 x 20
 // multiply-adds per request: it runs in the C++ consensus core on the host, next to the vote
 // extraction that feeds it — a kernel launch would cost more than the arithmetic.)
@@ -180,40 +181,62 @@ __global__ void __launch_bounds__(256) knn_slab_kernel(const float* __restrict__
   }
 }
 
-// merge: the k best of the slabs' k winners each (ties to the lower row)
-__global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict__ part_v, const int* __restrict__ part_i,
-                                                        int m, int k, float* __restrict__ vals, int* __restrict__ rows) {
-  extern __shared__ float smem_knn[];
-  float* v = smem_knn;
-  int* ix = reinterpret_cast<int*>(smem_knn + m);
+// merge: each workgroup takes the winners of `group` consecutive lists of k (list-major = row order, so
+// ties still resolve to the lower row) and writes its k best; the host repeats until one list is left
+constexpr int kKnnMergeMax = 4096;  // entries per merging workgroup (32 KiB of LDS)
+__global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict__ in_v, const int* __restrict__ in_i,
+                                                        int m, int k, int group, float* __restrict__ out_vals,
+                                                        int* __restrict__ out_rows) {
+  __shared__ float v[kKnnMergeMax];
+  __shared__ int ix[kKnnMergeMax];
   __shared__ float red_v[4];
   __shared__ int red_i[4];
   __shared__ float out_v[kKnnMaxK];
   __shared__ int out_i[kKnnMaxK];
-  for (int i = threadIdx.x; i < m; i += 256) {
-    v[i] = part_i[i] >= 0 ? part_v[i] : -INFINITY;
-    ix[i] = part_i[i];
+  const int base = blockIdx.x * group * k;
+  const int cnt = min(group * k, m - base);
+  for (int i = threadIdx.x; i < cnt; i += 256) {
+    v[i] = in_i[base + i] >= 0 ? in_v[base + i] : -INFINITY;
+    ix[i] = in_i[base + i];
   }
   __syncthreads();
-  // ties across slabs resolve by slab order = row order: slab winners are stored slab-major
-  block_topk(v, ix, m, k, out_v, out_i, red_v, red_i);
+  block_topk(v, ix, cnt, k, out_v, out_i, red_v, red_i);
   for (int r = threadIdx.x; r < k; r += 256) {
-    vals[r] = out_v[r];
-    rows[r] = out_i[r];
+    out_vals[(size_t)blockIdx.x * k + r] = out_v[r];
+    out_rows[(size_t)blockIdx.x * k + r] = out_i[r];
   }
 }
 
 }  // namespace lwc
 
+// part_v / part_i: scratch of 2 * slabs * k entries (ping-pong between merge levels)
 extern "C" int lwc_knn_topk(const float* E, int n, int d, const float* q, int k, float* part_v, int* part_i,
                             float* vals, int* rows, hipStream_t s) {
   using namespace lwc;
   if (d % 4 != 0 || k < 1 || k > kKnnMaxK || k > n) return -1;
   const int slabs = (n + kKnnRows - 1) / kKnnRows;
-  const int m = slabs * k;
-  if ((size_t)m * 8 > 60 * 1024) return -2;  // merge image in LDS (n up to ~1.9 M rows at k = 16)
+  int m = slabs * k;
   knn_slab_kernel<<<slabs, 256, 0, s>>>(E, n, d, q, k, part_v, part_i);
-  knn_merge_kernel<<<1, 256, (size_t)m * 8, s>>>(part_v, part_i, m, k, vals, rows);
+  const int group = kKnnMergeMax / k;  // >= 64 lists per merging workgroup
+  float* src_v = part_v;
+  int* src_i = part_i;
+  float* dst_v = part_v + (size_t)slabs * k;
+  int* dst_i = part_i + (size_t)slabs * k;
+  while (true) {
+    const int lists = m / k;
+    const int blocks = (lists + group - 1) / group;
+    float* ov = blocks == 1 ? vals : dst_v;
+    int* oi = blocks == 1 ? rows : dst_i;
+    knn_merge_kernel<<<blocks, 256, 0, s>>>(src_v, src_i, m, k, group, ov, oi);
+    if (blocks == 1) break;
+    m = blocks * k;
+    float* tv = src_v;
+    int* ti = src_i;
+    src_v = dst_v;
+    src_i = dst_i;
+    dst_v = tv;
+    dst_i = ti;
+  }
   return (int)hipGetLastError();
 }
 

@@ -385,13 +385,20 @@ def bandwidth(dev):
     x = torch.empty(n, dtype=torch.bfloat16, device=dev).normal_()
     y = torch.empty_like(x)
     us = timeit(lambda: x.sum(), iters=10)
-    print(f"bw read (sum)   : {2 * n / us / 1e6:7.0f} GB/s", flush=True)
+    print(f"bw read (sum)          : {2 * n / us / 1e3:7.0f} GB/s", flush=True)
+    us = timeit(lambda: x.view(-1, 4096).amax(dim=1), iters=10)
+    print(f"bw read (row amax)     : {2 * n / us / 1e3:7.0f} GB/s", flush=True)
     us = timeit(lambda: y.copy_(x), iters=10)
-    print(f"bw copy (r + w) : {4 * n / us / 1e6:7.0f} GB/s", flush=True)
+    print(f"bw copy (r + w)        : {4 * n / us / 1e3:7.0f} GB/s", flush=True)
     seg = x.view(-1, 2048)  # 4 KiB rows
     idx = torch.randperm(seg.shape[0], device=dev)[: seg.shape[0] // 2]
     us = timeit(lambda: seg.index_select(0, idx), iters=10)
-    print(f"bw 4KiB gather  : {2 * idx.numel() * 4096 / us / 1e6:7.0f} GB/s (read + write)", flush=True)
+    print(f"bw 4KiB gather (r + w) : {2 * idx.numel() * 4096 / us / 1e3:7.0f} GB/s", flush=True)
+    lg = torch.randn(4096, 128256, device=dev).to(torch.bfloat16)
+    us = timeit(lambda: lg.amax(dim=1), iters=10)
+    print(f"logits [4096, 128256] row amax: {us:7.1f} us ({lg.numel() * 2 / us / 1e3:5.0f} GB/s)", flush=True)
+    us = timeit(lambda: torch.softmax(lg, dim=1), iters=5)
+    print(f"logits [4096, 128256] softmax (r + w): {us:7.1f} us", flush=True)
 
 
 def moe_decode(dev):
