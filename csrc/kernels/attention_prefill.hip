@@ -59,15 +59,21 @@ struct PrefillParams {
   int bt_stride;
 };
 
+// The block tables come in as a const __restrict__ kernel argument (not through the params struct): the
+// compiler may then read them with SCALAR loads.  As vector loads each block id needed an s_waitcnt
+// vmcnt(0) — which also waits for the LDS-DMA of the tiles in flight and serialises the pipeline.
 template <int D, bool PAGED>
-__global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
+__global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, const int* __restrict__ block_tables) {
   constexpr int CPR = D / 8;                // 16-byte chunks per row
   constexpr int KS = D / 32;                // k-steps for S
   constexpr int NS = D / 16;                // n-subtiles for O
   constexpr int TILE_BYTES = kKT * D * 2;   // one K or V tile
-  constexpr int CHUNKS = kKT * CPR;            // 16 B chunks per K (or V) tile
-  constexpr int CH_PER_THREAD = (CHUNKS + 255) / 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];  // [buf][K|V]
+  constexpr int NST = 3;                    // LDS stages: tiles t (computing), t+1 and t+2 (in flight)
+  constexpr int INSTR = TILE_BYTES / 1024;  // 1 KiB LDS-DMA wave-instructions per operand tile
+  constexpr int PER_WAVE = 2 * INSTR / 4;   // K + V wave-instructions each of the 4 waves issues per tile
+  constexpr int RPI = 1024 / (2 * D);       // tile rows per wave-instruction
+  static_assert(PER_WAVE >= 1 && (2 * INSTR) % 4 == 0, "tile must split evenly over 4 waves");
+  __shared__ __attribute__((aligned(16))) char smem[NST * 2 * TILE_BYTES];  // [stage][K|V]
 
   const int seq = blockIdx.x / p.max_tiles, qtile = blockIdx.x % p.max_tiles;
   const int hq = blockIdx.y, kvh = hq / (p.Hq / p.Hkv);
@@ -77,10 +83,12 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   // keys: the sequence's own rows, or (cached prefix / PAGED) a longer key range whose last len rows are
   // the queries
   const int ks0 = PAGED ? 0 : p.cu_seqlens_k ? p.cu_seqlens_k[seq] : s0;
-  const int klen = PAGED ? p.k_lens[seq] : p.cu_seqlens_k ? p.cu_seqlens_k[seq + 1] - ks0 : len;
-  const int* bt = PAGED ? p.block_tables + (size_t)seq * p.bt_stride : nullptr;
+  // wave-uniform by construction; readfirstlane lets the compiler keep the DMA buffer resources in SGPRs
+  const int klen = __builtin_amdgcn_readfirstlane(PAGED ? p.k_lens[seq]
+                                                        : p.cu_seqlens_k ? p.cu_seqlens_k[seq + 1] - ks0 : len);
+  const int* bt = PAGED ? block_tables + (size_t)seq * p.bt_stride : nullptr;
   const int qoff = klen - len;  // key position of query row 0
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, g = lane >> 4;
   const int qrow = q0 + wid * 16 + r16;  // this lane's query (as B-operand column)
 
@@ -97,83 +105,53 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   const int kv_end = p.causal ? q_last + 1 + qoff : klen;
   const int ntiles = (kv_end + kKT - 1) / kKT;
 
-  // staging registers
-  uint4v stk[CH_PER_THREAD], stv[CH_PER_THREAD];
-  // PAGED: the two block ids of the tile being loaded, fetched one tile ahead (the block-table load is not
-  // on the critical path of the K / V loads)
-  int blk_nx[2] = {0, 0};
-  if constexpr (PAGED) {
-    blk_nx[0] = bt[0];
-    blk_nx[1] = bt[1];  // block tables hold >= 2 entries per 32-key tile
-  }
-  auto gload = [&](int tile) {
-    int blk_cur[2] = {blk_nx[0], blk_nx[1]};
-    if constexpr (PAGED) {
-      if (tile + 1 < ntiles) {
-        blk_nx[0] = bt[2 * tile + 2];
-        blk_nx[1] = bt[2 * tile + 3];
-      }
-    }
-    // only the last tile of a key range needs the per-token V masking
-    const bool v_tail = PAGED && tile * kKT + kKT > klen;
+  // ---- LDS-DMA staging (buffer loads straight into LDS, 16 B per lane, no register round trip) ----
+  // Wave-instruction j of a tile (j < INSTR: K image, else V image) writes the image's bytes
+  // [1 KiB * (j % INSTR), +1 KiB) lane-linearly; the image's swizzle is applied to the SOURCE address.  Keys
+  // at or past klen are out of the buffer resource's range: the hardware writes zeros, no request.
+  //  K (and non-paged V) image: row r (key in tile), 16 B chunk c at ((r * CPR) + (c ^ (r % CPR))) * 16.
+  //  Paged V image: the tile's two interleaved block segments [4 token groups][D][4], odd groups' bytes
+  //  XOR bit 7 (the layout the ds_read_b64 PV operand reads conflict-free).
+  const int lrow = lane / CPR, lpc = lane % CPR;
+  auto issue = [&](int tile, int stage) {
+    char* kb = smem + stage * 2 * TILE_BYTES;
 #pragma unroll
-    for (int i = 0; i < CH_PER_THREAD; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int row = c / CPR, ch = c % CPR;
-      const int key = tile * kKT + row;
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int j = wid + 4 * i;  // wave-uniform
+      const bool isv = j >= INSTR;
+      const int jj = isv ? j - INSTR : j;
+      char* dst = kb + (isv ? TILE_BYTES : 0) + jj * 1024;
       if constexpr (PAGED) {
-        // K: chunk c = (key row, 16 B chunk) of the tile's two token-major block segments.  V: chunk c = byte
-        // 16c of the two interleaved segments [4 token groups][D][4] (block c / (CHUNKS / 2)).
-        if (c < CHUNKS) {
-          const int blk = row < 16 ? blk_cur[0] : blk_cur[1];
-          stk[i] = key < klen ? *reinterpret_cast<const uint4v*>(p.k + (((size_t)blk * p.Hkv + kvh) * 16 + row % 16) * D +
-                                                                 ch * 8)
-                              : uint4v{0, 0, 0, 0};
-          const int half = c / (CHUNKS / 2), b = (c % (CHUNKS / 2)) * 16;  // byte in the segment
-          const int vbase = tile * kKT + half * 16;                           // first key of the segment
-          if (vbase < klen) {
-            const int vblk = half == 0 ? blk_cur[0] : blk_cur[1];
-            uint4v v = *reinterpret_cast<const uint4v*>(reinterpret_cast<const char*>(
-                                                            p.v + ((size_t)vblk * p.Hkv + kvh) * 16 * D) + b);
-            if (v_tail) {
-              // 8 elements = 2 dims x tokens 4 grp + 0..3 (element e: token e & 3): zero the keys >= klen
-              const int t0 = vbase + 4 * (b / (D * 8));
-#pragma unroll
-              for (int w = 0; w < 4; ++w) {
-                const uint32_t lo = t0 + ((2 * w) & 3) < klen ? 0xffffu : 0u;
-                const uint32_t hi = t0 + ((2 * w + 1) & 3) < klen ? 0xffff0000u : 0u;
-                v[w] &= lo | hi;
-              }
-            }
-            stv[i] = v;
-          } else {
-            stv[i] = uint4v{0, 0, 0, 0};
-          }
+        // the instruction's 1 KiB lies in one block segment: K rows jj*RPI.. or V bytes jj*1024..
+        const int half = isv ? (jj * 1024) / 4096 : (jj * RPI) / 16;
+        const int blk = bt[__builtin_amdgcn_readfirstlane(2 * tile + half)];
+        const int valid = min(max(klen - (tile * kKT + half * 16), 0), 16);  // keys of this block in range
+        const bf16_t* segp = (isv ? p.v : p.k) + ((size_t)blk * p.Hkv + kvh) * 16 * D;
+        uint32_t vo, nrec;
+        if (!isv) {
+          const int r = jj * RPI + lrow;  // key in tile
+          vo = (uint32_t)(((r % 16) * CPR + (lpc ^ (r % CPR))) * 16);
+          nrec = (uint32_t)(valid * D * 2);
+        } else {
+          const int P = jj * 1024 + lane * 16;                     // byte of the V image
+          const int bsrc = (P ^ (((P / (D * 8)) & 1) << 7)) % 4096;  // byte in the block segment
+          vo = (uint32_t)bsrc;
+          nrec = (uint32_t)(((valid + 3) / 4) * D * 8);  // whole token groups; a partial group is fixed up
         }
-      } else if (c < CHUNKS && key < klen) {
-        stk[i] = *reinterpret_cast<const uint4v*>(p.k + (size_t)(ks0 + key) * p.k_stride + kvh * D + ch * 8);
-        stv[i] = *reinterpret_cast<const uint4v*>(p.v + (size_t)(ks0 + key) * p.v_stride + kvh * D + ch * 8);
+        // readfirstlane: uniform already, but the compiler may compute it on the VALU (then every DMA became a
+        // waterfall loop over "divergent" resources)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)segp, (short)0, __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
       } else {
-        stk[i] = uint4v{0, 0, 0, 0};
-        stv[i] = uint4v{0, 0, 0, 0};
-      }
-    }
-  };
-  auto lstore = [&](int buf) {
-    char* kb = smem + buf * 2 * TILE_BYTES;
-    char* vb = kb + TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < CH_PER_THREAD; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      if (c >= CHUNKS) break;
-      const int row = c / CPR, ch = c % CPR;
-      const int off = (row * CPR + (ch ^ (row & (CPR - 1)))) * 16;
-      *reinterpret_cast<uint4v*>(kb + off) = stk[i];
-      if constexpr (PAGED) {  // interleaved V image: odd token groups XOR byte bit 7 (ds_read_b64 banks)
-        const int b = c * 16;
-        *reinterpret_cast<uint4v*>(vb + (b ^ (((b / (D * 8)) & 1) << 7))) = stv[i];
-      } else {
-        *reinterpret_cast<uint4v*>(vb + off) = stv[i];
+        const int r = jj * RPI + lrow;
+        const int key = tile * kKT + r;
+        const int stride = isv ? p.v_stride : p.k_stride;
+        const bf16_t* base = (isv ? p.v : p.k) + (size_t)ks0 * stride + kvh * D;
+        const uint32_t vo = (uint32_t)(key * stride * 2 + ((lpc ^ (r % CPR)) * 16));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)base, (short)0, (uint32_t)(klen * stride * 2), 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
       }
     }
   };
@@ -183,12 +161,35 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
   for (int n = 0; n < NS; ++n) o[n] = float4v{0.f, 0.f, 0.f, 0.f};
   float m = -1e30f, l = 0.f;
 
-  gload(0);
-  lstore(0);
-  __syncthreads();
+  issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);  // issue next tile's loads before the MFMAs (T14)
+    const int buf = t % NST;
+    // own DMA of tile t landed (tile t+1's may stay in flight), then every wave's (barrier); the barrier also
+    // ends every wave's reads of tile t-1, whose stage tile t+2 now refills
+    if (t + 1 < ntiles)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < ntiles) issue(t + 2, (t + 2) % NST);
+    if constexpr (PAGED) {
+      // the last tile's partially valid token group holds stale V bytes of keys >= klen (P is 0 there, but
+      // 0 x a stale Inf / NaN would not be): zero them (uniform branch: the last tile only)
+      const int tk = klen - t * kKT;  // keys of this tile in range
+      if (tk < kKT && (tk & 3)) {
+        char* vimg = smem + buf * 2 * TILE_BYTES + TILE_BYTES;
+        const int half = tk / 16, grp = (tk % 16) / 4;
+        if (threadIdx.x < D) {
+          for (int r = tk & 3; r < 4; ++r) {
+            const int bsrc = half * 4096 + grp * D * 8 + threadIdx.x * 8 + r * 2;
+            *reinterpret_cast<bf16_t*>(vimg + (bsrc ^ (((bsrc / (D * 8)) & 1) << 7))) = 0;
+          }
+        }
+        __syncthreads();
+      }
+    }
     const char* kb = smem + buf * 2 * TILE_BYTES;
     const char* vb = kb + TILE_BYTES;
     // ---- S^T for the two 16-key subtiles ----
@@ -273,11 +274,6 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p) {
       }
       o[n] = mfma16p(pf, vf, o[n]);
     }
-    if (t + 1 < ntiles) {
-      __syncthreads();  // everyone done reading buf^1 from the previous iteration
-      lstore(buf ^ 1);
-      __syncthreads();
-    }
   }
 
   // ---- epilogue: normalise, stage the wave's 16 x D tile through LDS, 16 B stores ----
@@ -317,11 +313,11 @@ extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v
                   v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal, nullptr, nullptr, 0};
   dim3 grid(nseq * max_tiles, Hq);
   if (D == 128)
-    prefill_attn_kernel<128, false><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<128, false><<<grid, 256, 0, s>>>(p, nullptr);
   else if (D == 64)
-    prefill_attn_kernel<64, false><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<64, false><<<grid, 256, 0, s>>>(p, nullptr);
   else if (D == 32)
-    prefill_attn_kernel<32, false><<<grid, 256, 0, s>>>(p);
+    prefill_attn_kernel<32, false><<<grid, 256, 0, s>>>(p, nullptr);
   else
     return -1;
   return (int)hipGetLastError();
@@ -341,6 +337,6 @@ extern "C" int lwc_prefill_attention_paged(const void* q, const void* kc, const 
   PrefillParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)out, cu_seqlens, nullptr,
                   q_stride, 0, 0, o_stride, Hq, Hkv, nseq, max_tiles, scale, 1, block_tables, k_lens, bt_stride};
   dim3 grid(nseq * max_tiles, Hq);
-  prefill_attn_kernel<128, true><<<grid, 256, 0, s>>>(p);
+  prefill_attn_kernel<128, true><<<grid, 256, 0, s>>>(p, block_tables);
   return (int)hipGetLastError();
 }
