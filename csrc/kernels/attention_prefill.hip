@@ -26,6 +26,8 @@
 // one ds_read_b64 returns a lane's 4 consecutive keys of one dim — the PV B operand without a transpose.
 // V elements of keys past k_lens (the tail of the last block, stale bytes) are zeroed: P is 0 there, but
 // 0 x a stale Inf / NaN would not be.  No per-layer gather of the cached keys into contiguous buffers.
+#include <type_traits>
+
 #include "common.h"
 
 namespace lwc {
@@ -39,6 +41,7 @@ LWC_DEVICE float4v mfma16p(const short8& a, const short8& b, const float4v& c) {
 }
 
 constexpr int kQT = 64;  // query rows per workgroup
+constexpr float kLazyRescale = 8.f;
 constexpr int kKT = 32;  // keys per tile
 
 struct PrefillParams {
@@ -163,8 +166,22 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
 
   issue(0, 0);
   if (ntiles > 1) issue(1, 1);
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t % NST;
+  // loop-invariant LDS read offsets of this lane (the stage base is a compile-time immediate below)
+  int kofs[KS], vofs[NS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) kofs[s] = (r16 * CPR + ((4 * s + g) ^ (r16 & (CPR - 1)))) * 16;
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    if constexpr (PAGED) {
+      vofs[n] = ((g * D + 16 * n + r16) << 3) ^ ((g & 1) << 7);
+    } else {
+      const int qq = r16 >> 2, pp = r16 & 3;
+      const int rowA = 4 * g + qq, chunk = 2 * n + (pp >> 1);
+      vofs[n] = (rowA * CPR + (chunk ^ (rowA & (CPR - 1)))) * 16 + (pp & 1) * 8;
+    }
+  }
+  auto tile_step = [&](const int t, auto stage) {
+    constexpr int buf = decltype(stage)::value;
     // own DMA of tile t landed (tile t+1's may stay in flight), then every wave's (barrier); the barrier also
     // ends every wave's reads of tile t-1, whose stage tile t+2 now refills
     if (t + 1 < ntiles)
@@ -190,50 +207,65 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
         __syncthreads();
       }
     }
-    const char* kb = smem + buf * 2 * TILE_BYTES;
+    const char* kb = smem + buf * 2 * TILE_BYTES;  // compile-time stage: LDS reads take immediate offsets
     const char* vb = kb + TILE_BYTES;
     // ---- S^T for the two 16-key subtiles ----
     float4v sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int ch = 4 * s + g;
-      const int rA = r16, rB = 16 + r16;
-      const short8 ka = *reinterpret_cast<const short8*>(kb + (rA * CPR + (ch ^ (rA & (CPR - 1)))) * 16);
-      const short8 kbv = *reinterpret_cast<const short8*>(kb + (rB * CPR + (ch ^ (rB & (CPR - 1)))) * 16);
+      const short8 ka = *reinterpret_cast<const short8*>(kb + kofs[s]);
+      const short8 kbv = *reinterpret_cast<const short8*>(kb + kofs[s] + 16 * CPR * 16);  // keys 16..31
       sa = mfma16p(ka, qf[s], sa);
       sb = mfma16p(kbv, qf[s], sb);
     }
     // ---- mask + online softmax (per query r16) ----
     float pa[4], pb[4];
     float mx = -1e30f;
+    // interior tile (every key in range and, causal, at or before the wave's first query): no mask
+    const int tlast = t * kKT + kKT - 1;
+    if (tlast < klen && (!p.causal || tlast <= q0 + wid * 16 + qoff)) {  // wave-uniform
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ka_ = t * kKT + 4 * g + r, kb_ = ka_ + 16;
-      const bool va = ka_ < klen && (!p.causal || ka_ <= qrow + qoff);
-      const bool vbk = kb_ < klen && (!p.causal || kb_ <= qrow + qoff);
-      pa[r] = va ? sa[r] * sl2 : -INFINITY;
-      pb[r] = vbk ? sb[r] * sl2 : -INFINITY;
-      mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
+      for (int r = 0; r < 4; ++r) {
+        pa[r] = sa[r] * sl2;
+        pb[r] = sb[r] * sl2;
+        mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ka_ = t * kKT + 4 * g + r, kb_ = ka_ + 16;
+        const bool va = ka_ < klen && (!p.causal || ka_ <= qrow + qoff);
+        const bool vbk = kb_ < klen && (!p.causal || kb_ <= qrow + qoff);
+        pa[r] = va ? sa[r] * sl2 : -INFINITY;
+        pb[r] = vbk ? sb[r] * sl2 : -INFINITY;
+        mx = fmaxf(mx, fmaxf(pa[r], pb[r]));
+      }
     }
     mx = row_max4(mx);
-    const float m_new = fmaxf(m, mx);
-    const float alpha = exp2f(m - m_new);
+    // lazy rescale (log2 domain): the running max only moves — and O / l are rescaled — when some row's new
+    // scores exceed it by more than kLazyRescale, so P <= 2^8 and most tiles skip the cross-lane alpha
+    // shuffles and the O multiplies
+    if (__any(mx > m + kLazyRescale)) {  // wave-uniform
+      const float m_new = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+      l *= alpha;
+      m = m_new;
+      float al[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) al[r] = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+      for (int n = 0; n < NS; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[n][r] *= al[r];
+    }
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      pa[r] = exp2f(pa[r] - m_new);
-      pb[r] = exp2f(pb[r] - m_new);
+      pa[r] = __builtin_amdgcn_exp2f(pa[r] - m);  // raw v_exp_f32: -inf -> 0, arguments <= 8
+      pb[r] = __builtin_amdgcn_exp2f(pb[r] - m);
       rs += pa[r] + pb[r];
     }
-    l = l * alpha + row_sum4(rs);
-    m = m_new;
-    float al[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) al[r] = __shfl(alpha, 4 * g + r, 64);
-#pragma unroll
-    for (int n = 0; n < NS; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[n][r] *= al[r];
+    l += row_sum4(rs);
     short8 pf;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -241,12 +273,11 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
       pf[4 + r] = (short)f2bf(pb[r]);
     }
     // ---- O += P V, V columns via the hardware transpose read ----
-    const int qq = r16 >> 2, pp = r16 & 3;
     if constexpr (PAGED) {
       // lane: keys 4g..4g+3 (block A half) and 16+4g..16+4g+3 (block B half) of dim 16n + r16, 8 B each
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
-        const int off = ((g * D + 16 * n + r16) << 3) ^ ((g & 1) << 7);
+        const int off = vofs[n];
         const short4v va4 = *reinterpret_cast<const short4v*>(vb + off);
         const short4v vb4 = *reinterpret_cast<const short4v*>(vb + TILE_BYTES / 2 + off);
         short8 vf;
@@ -260,10 +291,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
     } else
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
-      const int chunk = 2 * n + (pp >> 1);
-      const int rowA = 4 * g + qq, rowB = 16 + 4 * g + qq;
-      const int offA = (rowA * CPR + (chunk ^ (rowA & (CPR - 1)))) * 16 + (pp & 1) * 8;
-      const int offB = (rowB * CPR + (chunk ^ (rowB & (CPR - 1)))) * 16 + (pp & 1) * 8;
+      const int offA = vofs[n], offB = vofs[n] + 16 * CPR * 16;  // rows 4g+qq and 16+4g+qq: same swizzle
       const short4v va4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vb + offA));
       const short4v vb4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vb + offB));
       short8 vf;
@@ -274,6 +302,11 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
       }
       o[n] = mfma16p(pf, vf, o[n]);
     }
+  };
+  for (int t = 0; t < ntiles; t += NST) {  // unrolled by the stage count: every stage base is a constant
+    tile_step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile_step(t + 1, std::integral_constant<int, 1>{});
+    if (t + 2 < ntiles) tile_step(t + 2, std::integral_constant<int, 2>{});
   }
 
   // ---- epilogue: normalise, stage the wave's 16 x D tile through LDS, 16 B stores ----

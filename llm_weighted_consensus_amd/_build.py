@@ -61,6 +61,12 @@ def _torch_flags() -> tuple[list[str], list[str]]:
     return inc + defs, libs
 
 
+# Per-kernel-file code generation flags.  The prefill attention keeps its accumulators in VGPRs (the
+# compiler's default AGPR form moved every O accumulator AGPR <-> VGPR around each MFMA: 72 v_accvgpr per
+# 32-key tile).
+PER_FILE_FLAGS = {"attention_prefill.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def build_kernels(jobs: int = 8, force: bool = False) -> Path:
     """Compile every csrc/kernels/*.hip for gfx950 and link the torch extension."""
     kdir = CSRC / "kernels"
@@ -77,7 +83,7 @@ def build_kernels(jobs: int = 8, force: bool = False) -> Path:
         obj = obj_dir / (src.stem + ".o")
         objs.append(obj)
         if force or _stale(obj, [src, *headers]):
-            jobs_list.append(base + ["-c", str(src), "-o", str(obj)])
+            jobs_list.append(base + PER_FILE_FLAGS.get(src.name, []) + ["-c", str(src), "-o", str(obj)])
     bsrc = kdir / "bindings.cpp"
     bobj = obj_dir / "bindings.o"
     objs.append(bobj)
