@@ -61,10 +61,10 @@ def _torch_flags() -> tuple[list[str], list[str]]:
     return inc + defs, libs
 
 
-# Per-kernel-file code generation flags.  The prefill attention keeps its accumulators in VGPRs (the
+# Per-kernel-file code generation flags.  The attention kernels keep their accumulators in VGPRs (the
 # compiler's default AGPR form moved every O accumulator AGPR <-> VGPR around each MFMA: 72 v_accvgpr per
 # 32-key tile).
-PER_FILE_FLAGS = {"attention_prefill.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+PER_FILE_FLAGS = {f: ["-mllvm", "-amdgpu-mfma-vgpr-form=1"] for f in ("attention_prefill.hip", "attention_decode.hip")}
 
 
 def build_kernels(jobs: int = 8, force: bool = False) -> Path:
