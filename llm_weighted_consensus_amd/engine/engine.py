@@ -138,6 +138,11 @@ class _GraphBucket:
         self.B, self.width, self.splits, self.max_tiles = B, width, splits, max_tiles
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.logits: Optional[torch.Tensor] = None
+        # captured decode graphs by attention mode (True = cascade, False = plain split-K), sharing one
+        # memory pool, and their output logits
+        self.graphs: Dict[bool, torch.cuda.CUDAGraph] = {}
+        self.graph_logits: Dict[bool, torch.Tensor] = {}
+        self.pool = None
         segs: List[Tuple[str, int]] = [("block_tables", B * width), ("ctx_lens", B), ("slots", B), ("positions", B),
                                        ("tokens", B), ("tiles", max(1, max_tiles) * 3)]
         segs += [(n, B) for n in _F32_PARAMS + _I32_PARAMS]
@@ -667,7 +672,7 @@ class LLMEngine:
             pos.extend(ps.tolist())
             slot_parts.append(sl)
             dec_in = {"block_tables": _h2d(bt, torch.int32, dev), "ctx_lens": _h2d(cl, torch.int32, dev)}
-            if self.prefix_sharing and B >= self.cascade_min_batch:
+            if self.prefix_sharing and B >= self.cascade_min_batch and self._cascade_pays(dec):
                 per = ops.cascade_rows_per_tile(self.cfg.heads // self.cfg.kv_heads)
                 tiles = np.zeros((cascade_table_size(B, per), 3), np.int32)
                 self._cascade_plan(dec, tiles)
@@ -894,8 +899,9 @@ class LLMEngine:
         B = bk.B
         ps = [s.params for s in seqs]
         n = len(seqs)
-        st = {"tiles": np.zeros((max(1, bk.max_tiles), 3), np.int32)}
-        if bk.max_tiles:
+        st = {"tiles": np.zeros((max(1, bk.max_tiles), 3), np.int32),
+              "cascade": bool(bk.max_tiles) and self._cascade_pays(seqs)}
+        if st["cascade"]:
             self._cascade_plan(seqs, st["tiles"])
 
         def col(vals, dt, fill=0):
@@ -921,18 +927,36 @@ class LLMEngine:
         self._comp_cache = (key, st)
         return st
 
-    def _ensure_graph(self, bk: _GraphBucket) -> None:
+    def _cascade_pays(self, seqs: List[Sequence]) -> bool:
+        """Whether the cascade kernel beats plain split-K decode for this batch: at least half of its rows
+        belong to runs of >= 2 sequences forked from one prompt (candidates of one request).  Batches of
+        unrelated sequences (the voters of score requests are separate n = 1 requests) would run the cascade
+        kernel as plain decode with one wave walking 16/G whole contexts — few, long-serial workgroups."""
+        shared, i, B = 0, 0, len(seqs)
+        while i < B:
+            g = seqs[i].group
+            j = i
+            while j < B and seqs[j].group is g:
+                j += 1
+            if j - i >= 2 and len(g.prompt_ids) >= self.block_size:
+                shared += j - i
+            i = j
+        return 2 * shared >= B
+
+    def _ensure_graph(self, bk: _GraphBucket, cascade: Optional[bool] = None) -> None:
         d = bk.d
+        cascade = bool(bk.max_tiles) if cascade is None else cascade
 
         def fwd():
             return self.model.decode(d["tokens"], d["positions"], d["slots"], d["block_tables"], d["ctx_lens"],
                                      self.cache, num_splits=bk.splits,
-                                     cascade_tiles=d["tiles"] if bk.max_tiles else None)
+                                     cascade_tiles=d["tiles"] if cascade else None)
 
         if not self.use_graphs:
             bk.logits = fwd()
             return
-        if bk.graph is None:
+        g = bk.graphs.get(cascade)
+        if g is None:
             dev = self.device
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
@@ -940,10 +964,13 @@ class LLMEngine:
                 fwd()  # warm-up (hipBLASLt heuristics, allocator) outside capture
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                bk.logits = fwd()
+            with torch.cuda.graph(g, pool=bk.pool):  # the bucket's two graphs never run at once
+                bk.graph_logits[cascade] = fwd()
+            bk.pool = g.pool()
+            bk.graphs[cascade] = g
             bk.graph = g
-        bk.graph.replay()
+        bk.logits = bk.graph_logits[cascade]
+        g.replay()
 
     def _launch(self, seqs: List[Sequence], sample: bool = True) -> _Step:
         """Stage inputs, replay the decode graph and launch the sampler for `seqs`; results are
@@ -993,7 +1020,7 @@ class LLMEngine:
             d["tokens"].index_copy_(0, dst, prev.tok_dev.index_select(0, src))
         if copies:
             self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
-        self._ensure_graph(bk)
+        self._ensure_graph(bk, st["cascade"])
         arm = getattr(self.model, "comm_arm", None)
         if arm is not None:
             arm()  # TP: error word of this step's all-reduces -> pinned host memory, read one step later
