@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import gc
 import itertools
+import os
 import random
 import threading
 import time
@@ -298,6 +299,7 @@ class LLMEngine:
         # engine step, in the same forward as that step's decode rows, so running sequences never stall
         # behind an admission (0 = whole admission batches, then decode: the throughput bench's mode)
         self.chunked_prefill = int(chunked_prefill)
+        self._mixed_tuned = False
         if self.chunked_prefill and self.cfg.head_dim != 128:
             raise ValueError("chunked prefill: the paged-KV prefill kernel is built for head_dim 128")
         self.prefilling: List[SequenceGroup] = []
@@ -642,6 +644,8 @@ class LLMEngine:
         sequence that the previous step finishes is computed and discarded."""
         dev = self.device
         events: List[TokenEvent] = []
+        if not self._mixed_tuned:
+            self._tune_mixed()
         prev, self.inflight = self.inflight, None
         self.running = [s for s in self.running if not s.finished]
         dec = [s for s in self.running if s.n_launched < s.params.max_tokens]
@@ -756,6 +760,22 @@ class LLMEngine:
                 ch.append(h)
             g._chain = ch
         return ch
+
+    def _tune_mixed(self) -> None:
+        """Once, before the first mixed step (opt-in, ``LWC_GEMM_BUCKETS=1``): the GEMM backend per row-count
+        bucket of the mixed steps' projections (decode rows + up to ``chunked_prefill`` chunk rows), timed like
+        the decode buckets'.  Off by default: on the serving load (scripts/gpu_serve_bk.sh, interleaved runs)
+        it measured 28.0-28.9 vs 28.5-31.5 requests/s without — a bucket's choice is timed at its top row
+        count, and hipBLASLt's stream-K is the safer pick across the row counts below it."""
+        self._mixed_tuned = True
+        if (not hasattr(self.model, "tune_gemms") or self.device.type != "cuda"
+                or os.environ.get("LWC_GEMM_BUCKETS", "0") != "1"):
+            return
+        top = self.chunked_prefill + self.max_batch
+        buckets = [m for m in (256, 512, 1024, 1536, 2048, 2560, 3072, 4096, 6144, 8192) if m < top] + [top]
+        with span("tune_gemms"):
+            for m in buckets:
+                self.model.tune_gemms(m, bucket=True, lm_head=False)
 
     def _chunk_items(self, budget: int):
         """This step's prompt chunks: (group, a, e) = prompt tokens [a, e), at most ``budget`` tokens, prompts

@@ -4,20 +4,17 @@ This is the local generation backend that replaces the reference's upstream prov
 (reference: every voter is an OpenAI-compatible chat call, src/chat/completions/client.rs:308-332).
 
 Per layer (decode, B sequences):
-    rmsnorm(+residual)            K1 (fused residual add)
-    qkv  = x @ Wqkv^T             hipBLASLt GEMM (fused q|k|v weight)
+    rmsnorm                       K1
+    qkv  = x @ Wqkv^T             K6 (fused q|k|v weight)
     rope + paged KV write         K2 (in place, one pass)
-    attn = paged GQA decode       K3 (MFMA, split-K)
-    o    = attn @ Wo^T            hipBLASLt
-    rmsnorm(+residual)            K1
-    gu   = x @ Wgu^T              hipBLASLt (fused gate|up weight)
-    act  = silu(g) * u            K5
-    down = act @ Wd^T             hipBLASLt
-Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over the fresh
-k/v of the qkv buffer; the k/v are scattered into the paged cache in the same RoPE pass.
-
-Plain library GEMMs go to hipBLASLt through torch (allowed by the design rules); everything else
-is a hand-written HIP kernel from ``llm_weighted_consensus_amd.ops``.
+    attn = paged GQA decode       K3 (cascade for forked candidates, else split-K)
+    x   += attn @ Wo^T            K6 with the residual add in its epilogue, then K1
+    act  = silu(x Wg^T) (x Wu^T)  K6 with SwiGLU in its epilogue (fused gate|up weight), or GEMM + K5
+    x   += act @ Wd^T             K6 + residual, then K1
+K6 is chosen per shape by ops/gemm_plan.py among hipBLASLt and the hand-written cores (gemm4w, gemm8p),
+timed on the device.  Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over
+the fresh k/v of the qkv buffer; mixed chunked-prefill steps (forward_mixed) send decode rows to K3 and
+prompt-chunk rows to K4's paged-KV mode; the k/v are scattered into the paged cache in the RoPE pass.
 """
 from __future__ import annotations
 
@@ -255,21 +252,24 @@ class LlamaModel:
     def comm_poll(self) -> None:
         """Tensor-parallel subclasses raise here once a failed collective is visible on the host."""
 
-    def tune_gemms(self, M: int) -> None:
+    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True) -> None:
         """Pick the GEMM backend of every decode projection at batch M by timing both (before the
-        bucket's hipGraph is captured; see ops/gemm_plan.py)."""
+        bucket's hipGraph is captured; see ops/gemm_plan.py).  ``bucket``: M is a row-count bucket of the
+        mixed chunked-prefill steps (their M varies step to step); ``lm_head``: tune the vocabulary
+        projection too (mixed steps only project the decode rows and completed prompts' last tokens)."""
         if self.g8_ws is None or not isinstance(self.layers[0], LayerWeights) or self.fp8_dense:
             return
         cfg, L = self.cfg, self.layers[0]
         x = torch.randn(M, cfg.hidden, device=self.device).to(self.dtype)
         xa = torch.randn(M, cfg.heads * cfg.head_dim, device=self.device).to(self.dtype)
         xf = torch.randn(M, cfg.ffn, device=self.device).to(self.dtype)
-        gemm_plan.tune(x, L.wqkv, ws=self.g8_ws)
+        gemm_plan.tune(x, L.wqkv, ws=self.g8_ws, bucket=bucket)
         epi = "residual" if self._dense_residual else "plain"
-        gemm_plan.tune(xa, L.wo, epi, ws=self.g8_ws)
-        gemm_plan.tune(x, L.w_gate_up, "swiglu", L.gu_block, ws=self.g8_ws)
-        gemm_plan.tune(xf, L.w_down, epi, ws=self.g8_ws)
-        gemm_plan.tune(x, self.lm_head, ws=self.g8_ws)
+        gemm_plan.tune(xa, L.wo, epi, ws=self.g8_ws, bucket=bucket)
+        gemm_plan.tune(x, L.w_gate_up, "swiglu", L.gu_block, ws=self.g8_ws, bucket=bucket)
+        gemm_plan.tune(xf, L.w_down, epi, ws=self.g8_ws, bucket=bucket)
+        if lm_head:
+            gemm_plan.tune(x, self.lm_head, ws=self.g8_ws, bucket=bucket)
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,

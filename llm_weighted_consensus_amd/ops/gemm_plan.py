@@ -33,10 +33,24 @@ _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
 TIMINGS: Dict[Tuple[int, int, int, str], Dict[str, float]] = {}
 
 
+# row-count buckets (mixed chunked-prefill steps: decode rows + prompt-chunk rows vary every step): per
+# (N, K, epilogue) a sorted list of (M bucket, choice); a call takes the smallest tuned bucket >= its M
+_BUCKETS: Dict[Tuple[int, int, str], list] = {}
+
+
 def choice(M: int, N: int, K: int, epi: str) -> str:
     if MODE in BACKENDS:
         return MODE
-    return _CHOICE.get((M, N, K, epi), "blas")
+    c = _CHOICE.get((M, N, K, epi))
+    if c is not None:
+        return c
+    bl = _BUCKETS.get((N, K, epi))
+    if bl:
+        for mb, cb in bl:
+            if M <= mb:
+                return cb
+        return bl[-1][1]
+    return "blas"
 
 
 def _g8_ok(N: int, K: int, epi: str) -> bool:
@@ -139,15 +153,35 @@ def _time(fn, iters: int = 5, rounds: int = 3) -> float:
     return sorted(ts)[len(ts) // 2]
 
 
-def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, ws=None) -> Optional[str]:
+def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, ws=None,
+         bucket: bool = False) -> Optional[str]:
     """Time every applicable backend for this (M, N, K, epi) and record the choice (no-op under graph
     capture, off the GPU, for an already tuned shape, or when a backend is forced).  Rounds interleave the
-    backends (one process, one device: their clock and cache states match)."""
+    backends (one process, one device: their clock and cache states match).  ``bucket``: also the choice of
+    every row count up to M not tuned exactly (down to the next smaller bucket)."""
     M, K = x.shape
     N = w.shape[0]
     key = (M, N, K, epi)
-    if MODE != "auto" or key in _CHOICE or not x.is_cuda or torch.cuda.is_current_stream_capturing():
+    if MODE != "auto" or not x.is_cuda or torch.cuda.is_current_stream_capturing():
         return _CHOICE.get(key)
+    if key in _CHOICE:
+        if bucket:
+            _add_bucket(M, N, K, epi, _CHOICE[key])
+        return _CHOICE[key]
+    c = _tune(x, w, epi, block, ws, M, N, K, key)
+    if bucket:
+        _add_bucket(M, N, K, epi, c)
+    return c
+
+
+def _add_bucket(M: int, N: int, K: int, epi: str, c: str) -> None:
+    bl = _BUCKETS.setdefault((N, K, epi), [])
+    if all(mb != M for mb, _ in bl):
+        bl.append((M, c))
+        bl.sort()
+
+
+def _tune(x, w, epi, block, ws, M, N, K, key) -> str:
     if not _g8_ok(N, K, epi) or (epi == "swiglu" and block != 32):
         _CHOICE[key] = "blas"
         return "blas"
