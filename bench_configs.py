@@ -178,6 +178,11 @@ def main():
         a.requests = a.requests or 32  # 2048-sequence decode batch: amortises the expert-weight stream
         out = bench_moe(a)
     if int(os.environ.get("RANK", "0")) == 0:
+        from llm_weighted_consensus_amd import ops
+
+        for k, v in sorted(ops.FP8_TIMINGS.items()):  # dense fp8 backend choice per (rows bucket, N, K)
+            print(f"# fp8 gemm {k}: " + " ".join(f"{b}={t:.1f}us" for b, t in v.items())
+                  + f" choice={ops.FP8_CHOICE.get(k)}", file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
 
 

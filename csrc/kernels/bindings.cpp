@@ -8,6 +8,7 @@
 
 extern "C" {
 int lwc_rmsnorm(const void*, void*, const void*, void*, int, int, float, hipStream_t);
+int lwc_rmsnorm_quant_fp8(const void*, void*, const void*, void*, int, int, float, void*, float*, hipStream_t);
 int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
 int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
                       int, hipStream_t);
@@ -27,7 +28,7 @@ int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, 
 int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
-                   int, int, int, int, hipStream_t);
+                   int, int, int, int, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -50,6 +51,8 @@ int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long lo
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
 int lwc_knn_topk(const float*, int, int, const float*, int, float*, int*, float*, int*, hipStream_t);
+int lwc_vote_tally(const double*, const double*, const unsigned char*, int, int, int, double*, double*, double*,
+                   hipStream_t);
 }
 
 namespace {
@@ -90,6 +93,34 @@ void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, con
     r = residual->data_ptr();
   }
   CHECK_RC(lwc_rmsnorm(x.data_ptr(), r, w.data_ptr(), out.data_ptr(), rows, d, (float)eps, cur_stream()), "rmsnorm");
+}
+
+void rmsnorm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& w,
+                       const c10::optional<at::Tensor>& out, at::Tensor& q, at::Tensor& scale, double eps) {
+  // K1 + K11e: RMSNorm (+ residual update) whose output is also quantised per row to e4m3 (q, scale);
+  // out (the bf16 output) is optional.  d in {2048, 4096, 8192}.
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_GPU(q); CHECK_CONTIG(q); CHECK_CONTIG(scale);
+  CHECK_DTYPE(scale, at::kFloat);
+  TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn, "rmsnorm_quant_fp8: q must be e4m3fn");
+  const int d = (int)x.size(-1);
+  const int rows = (int)(x.numel() / std::max<int64_t>(d, 1));
+  TORCH_CHECK(d == 2048 || d == 4096 || d == 8192, "rmsnorm_quant_fp8: d must be 2048, 4096 or 8192");
+  TORCH_CHECK(w.numel() == d && q.numel() == x.numel() && scale.numel() >= rows, "rmsnorm_quant_fp8: shape mismatch");
+  void* r = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16(*residual); CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "rmsnorm_quant_fp8: residual shape mismatch");
+    r = residual->data_ptr();
+  }
+  void* y = nullptr;
+  if (out.has_value() && out->defined()) {
+    CHECK_BF16(*out); CHECK_CONTIG(*out);
+    TORCH_CHECK(out->numel() == x.numel(), "rmsnorm_quant_fp8: out shape mismatch");
+    y = out->data_ptr();
+  }
+  CHECK_RC(lwc_rmsnorm_quant_fp8(x.data_ptr(), r, w.data_ptr(), y, rows, d, (float)eps, q.data_ptr(),
+                                 scale.data_ptr<float>(), cur_stream()),
+           "rmsnorm_quant_fp8");
 }
 
 void layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& g,
@@ -336,15 +367,25 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
            "gemm4w");
 }
 
-void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& row_off,
+void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& row_off,
                 int64_t max_slots, const c10::optional<at::Tensor>& a_rows, const at::Tensor& a_scale,
                 const at::Tensor& w_scale) {
-  // grouped fp8 GEMM on the 8-phase schedule (gemm8g.hip): A [rows_a, K] e4m3, W [G, N, K] e4m3, C [rows, N] bf16
-  CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_CONTIG(W); CHECK_DTYPE(row_off, at::kInt); CHECK_CONTIG(row_off);
+  // grouped fp8 GEMM on the 8-phase schedule (gemm8g.hip): A [rows_a, K] e4m3, W [G, N, K] e4m3, C [rows, N] bf16;
+  // row_off None: the dense projection (G = 1, every output row)
+  CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_CONTIG(W);
   TORCH_CHECK(A.scalar_type() == at::kFloat8_e4m3fn && W.scalar_type() == at::kFloat8_e4m3fn, "gemm8g: e4m3 A and W");
   TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1 && W.dim() == 3, "gemm8g: layouts");
   const int G = (int)W.size(0), N = (int)W.size(1), K = (int)W.size(2);
-  TORCH_CHECK(A.size(1) == K && C.size(1) == N && row_off.numel() == G + 1, "gemm8g: shape mismatch");
+  const int* ro = nullptr;
+  if (row_off.has_value() && row_off->defined()) {
+    CHECK_DTYPE(*row_off, at::kInt); CHECK_CONTIG(*row_off);
+    TORCH_CHECK(row_off->numel() == G + 1, "gemm8g: row_off must have G + 1 entries");
+    ro = row_off->data_ptr<int>();
+  } else {
+    TORCH_CHECK(G == 1, "gemm8g: dense mode (no row_off) takes one weight");
+    TORCH_CHECK(max_slots >= (C.size(0) + 255) / 256, "gemm8g: dense mode needs ceil(rows / 256) slots");
+  }
+  TORCH_CHECK(A.size(1) == K && C.size(1) == N, "gemm8g: shape mismatch");
   CHECK_DTYPE(a_scale, at::kFloat); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_CONTIG(w_scale);
   TORCH_CHECK(a_scale.numel() >= A.size(0) && w_scale.numel() == (int64_t)G * N, "gemm8g: scale shapes");
   const int* ar = nullptr;
@@ -355,9 +396,9 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const a
   } else {
     TORCH_CHECK(C.size(0) <= A.size(0), "gemm8g: more output rows than A rows");
   }
-  CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), row_off.data_ptr<int>(), ar,
-                          a_scale.data_ptr<float>(), w_scale.data_ptr<float>(), G, (int)max_slots, N, K,
-                          (int)A.stride(0), (int)C.stride(0), (int)A.size(0), cur_stream()),
+  CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), ro, ar, a_scale.data_ptr<float>(),
+                          w_scale.data_ptr<float>(), G, (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0),
+                          (int)A.size(0), (int)C.size(0), cur_stream()),
            "gemm8g_fp8");
 }
 
@@ -538,6 +579,24 @@ std::vector<at::Tensor> knn_topk(const at::Tensor& E, const at::Tensor& q, int64
   return {vals, rows};
 }
 
+std::vector<at::Tensor> vote_tally(const at::Tensor& V, const at::Tensor& w, const at::Tensor& valid) {
+  // V [R, L, C] f64, w [R, L] f64, valid [R, L] u8 -> (choice weight [R, C], confidence [R, C],
+  // voter confidence [R, L]; NaN where !valid)
+  CHECK_GPU(V); CHECK_GPU(w); CHECK_GPU(valid); CHECK_CONTIG(V); CHECK_CONTIG(w); CHECK_CONTIG(valid);
+  CHECK_DTYPE(V, at::kDouble); CHECK_DTYPE(w, at::kDouble); CHECK_DTYPE(valid, at::kByte);
+  TORCH_CHECK(V.dim() == 3 && w.dim() == 2 && valid.dim() == 2, "vote_tally: V [R, L, C], w / valid [R, L]");
+  const int R = (int)V.size(0), L = (int)V.size(1), C = (int)V.size(2);
+  TORCH_CHECK(w.size(0) == R && w.size(1) == L && valid.size(0) == R && valid.size(1) == L,
+              "vote_tally: w / valid must be [R, L]");
+  TORCH_CHECK(C >= 1 && C <= 1024, "vote_tally: 1 <= choices <= 1024");
+  at::Tensor cw = at::empty({R, C}, V.options()), conf = at::empty({R, C}, V.options());
+  at::Tensor vconf = at::empty({R, L}, V.options());
+  CHECK_RC(lwc_vote_tally(V.data_ptr<double>(), w.data_ptr<double>(), valid.data_ptr<uint8_t>(), R, L, C,
+                          cw.data_ptr<double>(), conf.data_ptr<double>(), vconf.data_ptr<double>(), cur_stream()),
+           "vote_tally");
+  return {cw, conf, vconf};
+}
+
 void cosine_consensus(const at::Tensor& E, at::Tensor& S, double inv_tau, at::Tensor& centrality, at::Tensor& weights,
                       at::Tensor& best) {
   // E: [R, n, d] bf16; S: [R, n_pad, n_pad] f32
@@ -594,6 +653,7 @@ void allreduce(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels of llm_weighted_consensus_amd";
   m.def("rmsnorm", &rmsnorm);
+  m.def("rmsnorm_quant_fp8", &rmsnorm_quant_fp8);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("silu_mul", &silu_mul);
@@ -619,6 +679,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_l2norm", &pool_l2norm);
   m.def("cosine_consensus", &cosine_consensus);
   m.def("knn_topk", &knn_topk);
+  m.def("vote_tally", &vote_tally);
   m.def("gemm8g_fp8", &gemm8g_fp8);
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_open", &ar_open);

@@ -6,9 +6,12 @@
 //                              and the `top` best rows: per 256-row slab a wave-per-row dot
 //                              product into LDS and a block top-k, then the slab winners are merged level by
 //                              level (up to 4096 candidates per merging workgroup).
-// (The voter tally of the reference, src/score/completions/client.rs:384-455, is ~L x C <= 128 x 20
-// multiply-adds per request: it runs in the C++ consensus core on the host, next to the vote
-// extraction that feeds it — a kernel launch would cost more than the arithmetic.)
+//   K10b vote_tally          : the voter tally of the reference (src/score/completions/client.rs:384-455)
+//                              for R requests at once — one workgroup per request, fp64 like the host
+//                              tally and in the same summation order, so the results are bitwise equal to
+//                              the C++ consensus core.  A single request (~L x C <= 128 x 20 multiply-adds)
+//                              stays on the host (a launch costs more than the arithmetic); the serving
+//                              path batches the tallies of concurrent requests (score/tally_batch.py).
 #include "common.h"
 
 namespace lwc {
@@ -207,7 +210,63 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
   }
 }
 
+// ---- K10b: batched vote tally ---------------------------------------------------------------------
+// V: [R, L, C] f64 (padded choices are 0), w: [R, L] f64, valid: [R, L] u8 (0 = the voter has no vote:
+// errored or padding).  cw / conf: [R, C], vconf: [R, L] (NaN where !valid).
+// cw[c] = sum_l w_l V[l, c] (l ascending); conf = cw / sum_c cw (0 when the sum is not > 0);
+// vconf[l] = sum_c conf[c] V[l, c] (c ascending) — the host tally's order, term for term.
+constexpr int kTallyMaxC = 1024;
+__global__ void __launch_bounds__(256) vote_tally_kernel(const double* __restrict__ V, const double* __restrict__ w,
+                                                         const unsigned char* __restrict__ valid, int L, int C,
+                                                         double* __restrict__ cw, double* __restrict__ conf,
+                                                         double* __restrict__ vconf) {
+  __shared__ double s_cw[kTallyMaxC];
+  __shared__ double s_sum;
+  const int r = blockIdx.x;
+  const double* Vr = V + (size_t)r * L * C;
+  const double* wr = w + (size_t)r * L;
+  const unsigned char* ok = valid + (size_t)r * L;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double acc = 0.0;
+    for (int l = 0; l < L; ++l)
+      if (ok[l]) acc += Vr[(size_t)l * C + c] * wr[l];
+    s_cw[c] = acc;
+    cw[(size_t)r * C + c] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += s_cw[c];
+    s_sum = s;
+  }
+  __syncthreads();
+  const double sum = s_sum;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double v = sum > 0.0 ? s_cw[c] / sum : 0.0;
+    conf[(size_t)r * C + c] = v;
+    s_cw[c] = v;  // each thread touches only its own entries: no barrier before this overwrite
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < L; l += blockDim.x) {
+    double a = __builtin_nan("");
+    if (ok[l]) {
+      a = 0.0;
+      for (int c = 0; c < C; ++c) a += s_cw[c] * Vr[(size_t)l * C + c];
+    }
+    vconf[(size_t)r * L + l] = a;
+  }
+}
+
 }  // namespace lwc
+
+extern "C" int lwc_vote_tally(const double* V, const double* w, const unsigned char* valid, int R, int L, int C,
+                              double* cw, double* conf, double* vconf, hipStream_t s) {
+  using namespace lwc;
+  if (C < 1 || C > kTallyMaxC || L < 0) return -1;
+  if (R == 0) return 0;
+  vote_tally_kernel<<<R, 256, 0, s>>>(V, w, valid, L, C, cw, conf, vconf);
+  return (int)hipGetLastError();
+}
 
 // part_v / part_i: scratch of 2 * slabs * k entries (ping-pong between merge levels)
 extern "C" int lwc_knn_topk(const float* E, int n, int d, const float* q, int k, float* part_v, int* part_i,

@@ -46,6 +46,7 @@ struct Params {
   int G, N, K, lda, ldc;  // K in elements (= bytes), lda in elements
   int rows_a;             // rows of A (DMA bounds)
   int slots, n_tiles;     // m-tile slots per n-tile, n-tiles
+  int rows_c;             // output rows when row_off is null (dense: G = 1)
 };
 
 LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c) {
@@ -63,7 +64,8 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   if (ntile >= p.n_tiles) return;  // uniform
   int g = 0, m_begin = 0, m_end = 0;
   for (; g < p.G; ++g) {
-    const int r0 = p.row_off[g], r1 = p.row_off[g + 1];
+    // row_off == null: one dense group over rows [0, rows_c) (the dense fp8 projections, G = 1)
+    const int r0 = p.row_off ? p.row_off[g] : 0, r1 = p.row_off ? p.row_off[g + 1] : p.rows_c;
     const int nt = (r1 - r0 + 255) / 256;
     if (slot < nt) {
       m_begin = r0 + slot * 256;
@@ -239,10 +241,10 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
 
 // Grouped fp8 GEMM on the 8-phase schedule.  Requires K % 128 == 0, N % 8 == 0, lda / ldc % 16 == 0 (bytes
 // / elements: 16-byte rows), rows_a * lda < 2^31 and 256 * K < 2^31 (32-bit buffer offsets); max_slots >=
-// sum_g ceil(M_g / 256) (ceil(rows / 256) + G always is).
+// sum_g ceil(M_g / 256) (ceil(rows / 256) + G always is).  row_off == null: dense, G = 1, rows [0, rows_c).
 extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* row_off, const int* a_rows,
                               const float* a_scale, const float* w_scale, int G, int max_slots, int N, int K, int lda,
-                              int ldc, int rows_a, hipStream_t s) {
+                              int ldc, int rows_a, int rows_c, hipStream_t s) {
   using namespace lwc::g8g;
   if (K % 128 != 0 || K < 128 || N % 8 != 0 || lda % 16 != 0 || ldc % 8 != 0 || G < 1) return -1;
   if ((long long)rows_a * lda >= (1LL << 31) || 256LL * K >= (1LL << 31)) return -1;
@@ -255,7 +257,7 @@ extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* 
   }
   const int n_tiles = (N + 255) / 256;
   Params p{(const uint8_t*)A, (const uint8_t*)W, (lwc::bf16_t*)C, row_off, a_rows, a_scale, w_scale,
-           G, N, K, lda, ldc, rows_a, max_slots, n_tiles};
+           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c};
   const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * max_slots * 8);
   gemm8g_kernel<<<grid, 512, kLdsB, s>>>(p);
   return (int)hipGetLastError();

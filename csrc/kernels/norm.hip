@@ -66,10 +66,14 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16_t* __restrict_
 // contiguous), all loads issued before the first use, and the reduction is a wave reduction — no LDS, no
 // workgroup barrier.  The workgroup-per-row kernel above spends most of a 4096-wide row's time in its two
 // barriers and a single 16 B load per lane (4.4 TB/s at [4096, 4096]).
-template <int VPL, bool kResidual>
+// kQuant: the normalised row is also quantised per row to OCP e4m3 for the fp8 projection that consumes it
+// (config 5's dense fp8 layers): scale = max|bf16(y)| / 448 over the row, q = e4m3(bf16(y) / scale) —
+// exactly quant_fp8_rows(rmsnorm(x)) without writing and re-reading the bf16 row (y may be null then).
+template <int VPL, bool kResidual, bool kQuant = false>
 __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
                                                            const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
-                                                           int rows, int d, float eps) {
+                                                           int rows, int d, float eps, uint8_t* __restrict__ q = nullptr,
+                                                           float* __restrict__ qscale = nullptr) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;  // whole waves exit; no barrier below
   const int lane = threadIdx.x & 63;
@@ -104,6 +108,7 @@ __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(const bf16_t* __restr
     for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
   }
   const float inv = rsqrtf(wave_sum(ss) / (float)d + eps);
+  float amax = 0.f;
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     float a[8], wf[8], o[8];
@@ -111,7 +116,33 @@ __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(const bf16_t* __restr
     unpack8(wr[lane + 64 * k], wf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = a[j] * inv * wf[j];
-    yr[lane + 64 * k] = pack8(o);
+    const uint4v packed = pack8(o);
+    if (!kQuant || y != nullptr) yr[lane + 64 * k] = packed;
+    if (kQuant) {
+      raw[k] = packed;  // keep bf16(y) for the quantisation pass
+      float b[8];
+      unpack8(packed, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(b[j]));
+    }
+  }
+  if (kQuant) {
+    amax = wave_max(amax);
+    const float sc = fmaxf(amax, 1e-12f) / 448.f;
+    const float qi = 1.f / sc;
+    if (lane == 0) qscale[row] = sc;
+    uint2* qr = reinterpret_cast<uint2*>(q + (size_t)row * d);
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      float v[8];
+      unpack8(raw[k], v);
+      uint32_t lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * qi, v[1] * qi, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * qi, v[3] * qi, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * qi, v[5] * qi, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * qi, v[7] * qi, hi, true);
+      qr[lane + 64 * k] = make_uint2(lo, hi);
+    }
   }
 }
 
@@ -125,6 +156,18 @@ static void launch_rmsnorm_wave(const void* x, void* residual, const void* w, vo
   else
     rmsnorm_wave_kernel<VPL, false><<<grid, 256, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)w, (bf16_t*)y,
                                                          rows, d, eps);
+}
+
+template <int VPL>
+static void launch_rmsnorm_wave_q(const void* x, void* residual, const void* w, void* y, int rows, int d, float eps,
+                                  void* q, float* qscale, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (residual)
+    rmsnorm_wave_kernel<VPL, true, true><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)residual, (const bf16_t*)w,
+                                                              (bf16_t*)y, rows, d, eps, (uint8_t*)q, qscale);
+  else
+    rmsnorm_wave_kernel<VPL, false, true><<<grid, 256, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)w, (bf16_t*)y,
+                                                               rows, d, eps, (uint8_t*)q, qscale);
 }
 
 // LayerNorm with affine: y = (h - mean)/sqrt(var+eps) * g + b, h = x (+ residual);
@@ -213,6 +256,20 @@ extern "C" int lwc_rmsnorm(const void* x, void* residual, const void* w, void* y
     rmsnorm_kernel<true><<<rows, t, 0, s>>>((const bf16_t*)x, (bf16_t*)residual, (const bf16_t*)w, (bf16_t*)y, d, eps);
   else
     rmsnorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)w, (bf16_t*)y, d, eps);
+  return (int)hipGetLastError();
+}
+
+// RMSNorm (+ residual) with the per-row e4m3 quantisation of its output fused (wave per row; d in
+// {2048, 4096, 8192}); y (bf16 output) is optional.  Returns -1 for other widths (the caller runs the two
+// kernels).
+extern "C" int lwc_rmsnorm_quant_fp8(const void* x, void* residual, const void* w, void* y, int rows, int d, float eps,
+                                     void* q, float* qscale, hipStream_t s) {
+  using namespace lwc;
+  if (d != 2048 && d != 4096 && d != 8192) return -1;
+  if (rows == 0) return 0;
+  if (d == 2048) launch_rmsnorm_wave_q<4>(x, residual, w, y, rows, d, eps, q, qscale, s);
+  else if (d == 4096) launch_rmsnorm_wave_q<8>(x, residual, w, y, rows, d, eps, q, qscale, s);
+  else launch_rmsnorm_wave_q<16>(x, residual, w, y, rows, d, eps, q, qscale, s);
   return (int)hipGetLastError();
 }
 

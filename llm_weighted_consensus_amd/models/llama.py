@@ -194,7 +194,13 @@ class LlamaModel:
         # reduce the projections across ranks or route them through experts use the separate
         # residual-add + norm kernel.
         fused = self._dense_residual and self.g8_ws is not None
-        h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
+        # fp8 projections: the norms feeding them also emit the per-row e4m3 activation (ops.QAct) in the
+        # same pass, so no separate quantisation kernel re-reads the normalised rows
+        qn = isinstance(self.layers[0].wqkv, ops.Fp8Weight)
+        if qn:
+            h = ops.rmsnorm_quant_fp8(x_res, self.layers[0].attn_norm, cfg.rms_eps)
+        else:
+            h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
         for li, L in enumerate(self.layers):
             qkv = self._proj(h, L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
@@ -205,6 +211,14 @@ class LlamaModel:
                 h = ops.rmsnorm(x_res, L.mlp_norm, cfg.rms_eps)
                 gemm_plan.linear_add_(self._act(h, L), L.w_down, x_res, ws=self.g8_ws)
                 h = ops.rmsnorm(x_res, nxt, cfg.rms_eps)
+            elif qn:
+                o = self._attn_out(attn.view(T, Hq * D), L)
+                h = ops.rmsnorm_quant_fp8(o, L.mlp_norm, cfg.rms_eps, residual=x_res, keep_bf16=self._mlp_reads_bf16)
+                down = self._mlp(h, L)
+                if li + 1 < len(self.layers):
+                    h = ops.rmsnorm_quant_fp8(down, nxt, cfg.rms_eps, residual=x_res)
+                else:  # the final norm feeds the bf16 lm_head / pooling
+                    h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
             else:
                 o = self._attn_out(attn.view(T, Hq * D), L)
                 h = ops.rmsnorm(o, L.mlp_norm, cfg.rms_eps, residual=x_res)
@@ -212,15 +226,19 @@ class LlamaModel:
                 h = ops.rmsnorm(down, nxt, cfg.rms_eps, residual=x_res)
         return h
 
+    # whether _mlp reads the bf16 rows of its (fp8-quantised) input too (the MoE router does)
+    _mlp_reads_bf16 = False
+
     @property
     def _dense_residual(self) -> bool:
         cls = type(self)
         return (cls._attn_out is LlamaModel._attn_out and cls._mlp is LlamaModel._mlp
                 and not getattr(self, "fp8_dense", False))
 
-    def _proj(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        """Dense projection on the per-shape backend (hipBLASLt or gemm8p, ops/gemm_plan.py; e4m3 weights:
-        row-quantised activations into the fp8 library GEMM)."""
+    def _proj(self, x, w: torch.Tensor) -> torch.Tensor:
+        """Dense projection on the per-shape backend (ops/gemm_plan.py: hipBLASLt, gemm4w or gemm8p); e4m3
+        weights: row-quantised activations (an ops.QAct from the producing norm, or quantised here) into the
+        fp8 GEMM (gemm8g dense or the library, ops.linear_fp8_q)."""
         if isinstance(w, ops.Fp8Weight):
             return ops.linear_fp8(x, w)
         if self.g8_ws is None:

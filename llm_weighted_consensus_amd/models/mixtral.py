@@ -209,13 +209,24 @@ class MixtralModel(LlamaModel):
         gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows)
         return ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)
 
-    def _mlp_ep(self, h: torch.Tensor, L: MoELayerWeights) -> torch.Tensor:
+    _mlp_reads_bf16 = True  # the router projects the bf16 rows
+
+    @staticmethod
+    def _split_act(h):
+        """(bf16 rows, e4m3 rows | None, row scales | None) of an MLP input (ops.QAct from a fused norm)."""
+        if isinstance(h, ops.QAct):
+            return h.bf16, h.q, h.s
+        return h, None, None
+
+    def _mlp_ep(self, h, L: MoELayerWeights) -> torch.Tensor:
         """EP MoE layer: route locally, dispatch rows to the expert owners, combine locally."""
         k = self.full_cfg.experts_per_token
+        h, hq, hs = self._split_act(h)
         _ids, w, row_off, src, inv = ops.moe_route(F.linear(h, L.router), k)
         idx = src.long()
         if self.fp8:
-            hq, hs = ops.quant_fp8_rows(h)
+            if hq is None:
+                hq, hs = ops.quant_fp8_rows(h)
             xs = hq.view(torch.uint8)[idx].view(torch.float8_e4m3fn)  # e4m3 rows gathered as bytes
             ss = hs[idx]
         else:
@@ -224,15 +235,17 @@ class MixtralModel(LlamaModel):
         y = self.ep.run(xs, row_off, lambda xl, ro, sl: self._experts(xl, ro, L, sl), x_scale=ss, capacity=cap)
         return ops.moe_combine(y.contiguous(), inv, w, k)
 
-    def _mlp(self, h: torch.Tensor, L: MoELayerWeights) -> torch.Tensor:
+    def _mlp(self, h, L: MoELayerWeights) -> torch.Tensor:
         if self.ep is not None:
             return self._mlp_ep(h, L)
         k = self.full_cfg.experts_per_token
+        h, hq, hs = self._split_act(h)
         logits = F.linear(h, L.router)
         _ids, w, row_off, src, inv = ops.moe_route(logits, k)
         rows = h.shape[0] * k
         if self.fp8:
-            hq, hs = ops.quant_fp8_rows(h)
+            if hq is None:
+                hq, hs = ops.quant_fp8_rows(h)
             y = self._experts(hq, row_off, L, hs, a_rows=src, rows=rows)
         else:
             y = self._experts(h, row_off, L, a_rows=src, rows=rows)

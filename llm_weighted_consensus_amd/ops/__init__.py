@@ -58,6 +58,33 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[tor
     return out
 
 
+class QAct:
+    """A normalised activation handed to fp8 projections: per-row e4m3 rows ``q`` [M, d] with scales ``s`` [M]
+    (``q * s[:, None]`` ~= the bf16 activation) and, when a consumer needs it, the bf16 rows ``bf16``."""
+
+    __slots__ = ("bf16", "q", "s")
+
+    def __init__(self, bf16: Optional[torch.Tensor], q: torch.Tensor, s: torch.Tensor):
+        self.bf16, self.q, self.s = bf16, q, s
+
+
+def rmsnorm_quant_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+                      keep_bf16: bool = False) -> QAct:
+    """RMSNorm (+ in-place residual update, as :func:`rmsnorm`) with the per-row e4m3 quantisation of its
+    output fused into the same pass (csrc/kernels/norm.hip, wave per row): equal to
+    ``quant_fp8_rows(rmsnorm(x, ...))``.  Widths the fused kernel does not take run the two kernels."""
+    d = x.shape[-1]
+    if d not in (2048, 4096, 8192):
+        y = rmsnorm(x, w, eps, residual=residual)
+        q, s = quant_fp8_rows(y)
+        return QAct(y if keep_bf16 else None, q, s)
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(x.numel() // d, dtype=torch.float32, device=x.device)
+    y = torch.empty_like(x) if keep_bf16 else None
+    kernels().rmsnorm_quant_fp8(x, residual, w, y, q, s, float(eps))
+    return QAct(y, q, s)
+
+
 def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = layernorm(x [+ residual]) * g + b (K9a)."""
@@ -409,14 +436,73 @@ class Fp8Weight:
         self.shape = tuple(w.shape)
 
 
-def linear_fp8_q(xq: torch.Tensor, xs: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
-    """(e4m3 rows xq [M, K], row scales xs [M]) . w^T -> bf16 [M, N]: a plain fp8 library GEMM (hipBLASLt
-    through torch._scaled_mm with row-wise scales; ~1.7x the bf16 GEMM rate on gfx950, scripts/fp8_probe.py)."""
+# dense fp8 projections (config 5): "auto" times the hand-written 8-phase fp8 core (gemm8g in dense mode)
+# against hipBLASLt's row-scaled fp8 GEMM per (row bucket, N, K) on the first eager call and keeps the
+# hand-written one unless the library is faster by more than FP8_OWN_MARGIN; "g8g" / "blas" force one.
+FP8_GEMM = os.environ.get("LWC_FP8_GEMM", "auto")
+FP8_OWN_MARGIN = float(os.environ.get("LWC_FP8_OWN_MARGIN", "0.01"))
+FP8_CHOICE: dict = {}
+FP8_TIMINGS: dict = {}
+
+
+def _fp8_bucket(M: int) -> int:
+    return min(1 << max(M - 1, 1).bit_length(), 1 << 16)
+
+
+def _g8g_dense_ok(xq: torch.Tensor, w: "Fp8Weight") -> bool:
+    N, K = w.q.shape
+    M = xq.shape[0]
+    return (xq.is_cuda and xq.stride(1) == 1 and xq.stride(0) % 16 == 0 and K % 128 == 0 and N % 8 == 0
+            and M * xq.stride(0) < (1 << 31) and 256 * K < (1 << 31) and xq.dtype == torch.float8_e4m3fn)
+
+
+def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Optional[torch.Tensor] = None):
+    """Dense fp8 GEMM on the hand-written 8-phase core (csrc/kernels/gemm8g.hip, G = 1, no row table):
+    (xq [M, K] e4m3 . w.q^T) * xs[row] * w.s[col] -> bf16 [M, N]."""
+    M = xq.shape[0]
+    N, K = w.q.shape
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+    if M == 0:
+        return out
+    kernels().gemm8g_fp8(xq, w.q.view(1, N, K), out, None, -(-M // 256), None, xs.reshape(-1).contiguous(),
+                         w.s.reshape(-1))
+    return out
+
+
+def _fp8_blas(xq, xs, w):
     return torch._scaled_mm(xq, w.q.t(), scale_a=xs.view(-1, 1), scale_b=w.s, out_dtype=torch.bfloat16)
 
 
-def linear_fp8(x: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
-    """bf16 x [M, K] -> per-row e4m3 quantisation (K11e) -> fp8 GEMM -> bf16 [M, N]."""
+def linear_fp8_q(xq: torch.Tensor, xs: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
+    """(e4m3 rows xq [M, K], row scales xs [M]) . w^T -> bf16 [M, N] (K6 fp8).  The hand-written 8-phase fp8
+    core (:func:`gemm8g_dense`) or hipBLASLt's row-scaled fp8 GEMM (``torch._scaled_mm``), chosen per
+    (row bucket, N, K) by timing (see FP8_GEMM); shapes the hand-written core does not take use the library."""
+    if not _g8g_dense_ok(xq, w) or FP8_GEMM == "blas":
+        return _fp8_blas(xq, xs, w)
+    if FP8_GEMM == "g8g":
+        return gemm8g_dense(xq, xs, w)
+    M = xq.shape[0]
+    key = (_fp8_bucket(M), w.q.shape[0], w.q.shape[1])
+    c = FP8_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            c = "g8g" if M >= 256 else "blas"  # untimed shape inside a capture: no timing possible
+        else:
+            from .gemm_plan import _time
+
+            t_own = _time(lambda: gemm8g_dense(xq, xs, w), iters=3, rounds=3)
+            t_blas = _time(lambda: _fp8_blas(xq, xs, w), iters=3, rounds=3)
+            FP8_TIMINGS[key] = {"g8g": t_own, "blas": t_blas}
+            c = FP8_CHOICE[key] = "g8g" if t_own <= t_blas * (1 + FP8_OWN_MARGIN) else "blas"
+    return gemm8g_dense(xq, xs, w) if c == "g8g" else _fp8_blas(xq, xs, w)
+
+
+def linear_fp8(x, w: Fp8Weight) -> torch.Tensor:
+    """bf16 x [M, K] -> per-row e4m3 quantisation (K11e) -> fp8 GEMM -> bf16 [M, N].  A :class:`QAct`
+    (quantised by the producing norm) goes straight to the GEMM."""
+    if isinstance(x, QAct):
+        return linear_fp8_q(x.q, x.s, w)
     xq, xs = quant_fp8_rows(x)
     return linear_fp8_q(xq, xs, w)
 
@@ -471,6 +557,13 @@ def knn_topk(E: torch.Tensor, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, to
     rows [k] int64), best first, ties to the lower row (torch.topk's order up to ties).  k <= 64."""
     vals, rows = kernels().knn_topk(E.contiguous(), q.reshape(-1).contiguous().to(E.dtype), int(k))
     return vals, rows.long()
+
+
+def vote_tally(V: torch.Tensor, w: torch.Tensor, valid: torch.Tensor):
+    """K10b: the voter tally of R requests in one launch.  V [R, L, C] f64 (padded choices 0), w [R, L] f64,
+    valid [R, L] u8 (0: no vote).  Returns (choice weight [R, C], confidence [R, C], voter confidence [R, L],
+    NaN where !valid) — bitwise equal to the host tally (same fp64 summation order)."""
+    return tuple(kernels().vote_tally(V.contiguous(), w.contiguous(), valid.contiguous()))
 
 
 def cosine_consensus(E: torch.Tensor, tau: float = 0.05):

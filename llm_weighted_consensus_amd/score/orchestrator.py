@@ -107,6 +107,8 @@ class ScoreClient:
         # which of a model's voters THIS client runs (None: all); the voter-sharded client
         # (score/sharded.py) runs a subset per rank and combines the tallies with a collective (C2)
         self.voter_filter = None
+        # K10b: tallies of concurrent requests batched into one GPU launch (score/tally_batch.py; None: host)
+        self.tally_batcher = None
         # inline models validated before, by their JSON text: validation + the voter / model ids (JSON +
         # xxh3 per voter) cost ~2 ms per request when every request carries its model inline
         self._inline_models: "OrderedDict[str, Model]" = OrderedDict()
@@ -358,7 +360,12 @@ class ScoreClient:
                        voter_usage):
         """Tally the aggregate's voters: (tally, all votes failed, error codes to unify).  ``usage`` is
         the request's running total, ``voter_usage`` this client's voters' share of it."""
-        return tally_choices(aggregate.choices[C_len:], C_len), not any_ok, codes
+        return await self._tally(aggregate.choices[C_len:], C_len), not any_ok, codes
+
+    async def _tally(self, voter_choices, C_len: int):
+        if self.tally_batcher is not None:
+            return await self.tally_batcher.tally(voter_choices, C_len)
+        return tally_choices(voter_choices, C_len)
 
     def _record_training(self, model, weight_data, voter_choices, tally) -> None:
         """Training-table models learn online: the transcript embedding and each voting voter's agreement

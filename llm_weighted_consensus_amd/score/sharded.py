@@ -30,7 +30,7 @@ from ..errors import ScoreError
 from ..parallel import votes as V
 from ..schema import chat as C
 from ..schema import score as S
-from .orchestrator import ScoreClient, tally_choices
+from .orchestrator import ScoreClient
 
 _SKIP = None  # a request's empty contribution (it failed before its combine on this rank)
 
@@ -139,7 +139,7 @@ class ShardedScoreClient(ScoreClient):
             c.index = C_len + len(mine) + k
         ctx["whole"] = {c.index for c in remote}  # complete choices: the final chunk carries them as they are
         aggregate.choices = aggregate.choices + remote
-        return tally_choices(aggregate.choices[C_len:], C_len), n_ok == 0, all_codes
+        return await self._tally(aggregate.choices[C_len:], C_len), n_ok == 0, all_codes
 
     async def run(self, seq: int, ids, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
         """One request on this rank (unary); always takes its combine slot."""

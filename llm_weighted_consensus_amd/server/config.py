@@ -37,6 +37,9 @@ variables configure the local engine:
                     score request, every rank runs its share of the voters (llm index % world) on its
                     own GPU, requests run concurrently and each combines its voters with one all-gather
                     (C2, score/sharded.py)
+  LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
+                    and batches of at least N run as one vote_tally launch (K10b) on this process's GPU
+                    (default 0: the host C++ tally per request)
 """
 from __future__ import annotations
 
@@ -93,6 +96,7 @@ class Config:
     shard_voters: bool = False
     kv_reserve_tokens: Optional[int] = 256
     request_timeout_ms: Optional[int] = None
+    gpu_tally: Optional[str] = None
 
     @classmethod
     def from_env(cls, dotenv: bool = True) -> "Config":
@@ -131,6 +135,7 @@ class Config:
         c.training_table_path = e.get("LWC_TRAINING_TABLE_PATH")
         c.fault = e.get("LWC_FAULT")
         c.shard_voters = e.get("LWC_SHARD_VOTERS", "0") == "1"
+        c.gpu_tally = e.get("LWC_GPU_TALLY")
         if "LWC_KV_RESERVE_TOKENS" in e:
             v = e["LWC_KV_RESERVE_TOKENS"].strip().lower()
             c.kv_reserve_tokens = None if v in ("", "none", "max") else int(v)

@@ -89,6 +89,10 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     score = ScoreClient(chat_client, registry,
                         WeightFetchers(training_table=TrainingTableWeights(tt_embed, path=cfg.training_table_path)),
                         archive=archive)
+    if cfg.device != "cpu":
+        from ..score.tally_batch import make_batcher
+
+        score.tally_batcher = make_batcher(cfg.gpu_tally, f"cuda:{cfg.gpu}")
     state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                            archive),
                      embedders=embedders, services=services, archive=archive, registry=registry)
@@ -116,6 +120,7 @@ def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     base = state.score
     client = ShardedScoreClient(base.chat, group=group, model_registry=base.models, weight_fetchers=base.weights,
                                 archive=base.archive, rng_seed=rng_seed)
+    client.tally_batcher = base.tally_batcher
     # /consensus/completions: candidates split over the ranks, embedding rows all-gathered (C1)
     client.consensus = ShardedConsensusClient(state.consensus, client) if state.consensus is not None else None
     if pdist.info().rank == 0:

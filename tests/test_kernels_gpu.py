@@ -725,6 +725,55 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     _close(out, classic, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("d,rows", [(4096, 1), (4096, 301), (2048, 64), (8192, 257), (1024, 33)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm_quant_fp8_fused(gpu, d, rows, with_res):
+    """RMSNorm with the per-row e4m3 quantisation fused (K1 + K11e): bitwise equal to the two-kernel path
+    quant_fp8_rows(rmsnorm(x)) (same bf16 rounding before the row max), residual stream updated the same
+    way; d = 1024 takes the two-kernel fallback."""
+    from llm_weighted_consensus_amd import ops
+
+    x = _bf(rows, d, dev=gpu)
+    w = _bf(d, dev=gpu, scale=0.5) + 1
+    r = _bf(rows, d, dev=gpu) if with_res else None
+    r2 = r.clone() if with_res else None
+    y = ops.rmsnorm(x, w, 1e-5, residual=r)
+    q_ref, s_ref = ops.quant_fp8_rows(y)
+    a = ops.rmsnorm_quant_fp8(x, w, 1e-5, residual=r2, keep_bf16=True)
+    assert torch.equal(a.bf16, y)
+    assert torch.equal(a.q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(a.s, s_ref)
+    if with_res:
+        assert torch.equal(r2, r)
+    # dequantised rows track the fp32 reference within e4m3 precision
+    deq = a.q.float() * a.s[:, None]
+    _close(deq, y.float(), 0.07 * a.s.max().item() * 448 / 16 + 1e-3, 0.07)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 512, 256), (255, 640, 512), (2048, 6144, 4096), (4097, 1024, 1024)])
+def test_dense_fp8_gemm8g(gpu, M, N, K, monkeypatch):
+    """Dense fp8 projections on the hand-written 8-phase core (gemm8g, no row table): per-row activation and
+    per-channel weight scales vs an fp32 reference of the dequantised operands, and vs hipBLASLt's
+    row-scaled fp8 GEMM; the planner path (linear_fp8) forced to each backend agrees."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = ops.Fp8Weight(torch.randn(N, K, device=gpu).to(torch.bfloat16) * 0.05)
+    xq, xs = ops.quant_fp8_rows(x)
+    out = ops.gemm8g_dense(xq, xs, w)
+    ref_ = (xq.float() * xs[:, None]) @ (w.q.float() * w.s.view(-1, 1)).t()
+    _close(out, ref_, 2e-2, 2e-2)
+    blas = ops._fp8_blas(xq, xs, w)
+    _close(out, blas, 2e-2, 2e-2)
+    monkeypatch.setattr(ops, "FP8_GEMM", "g8g")
+    _close(ops.linear_fp8(x, w), out, 1e-6)
+    monkeypatch.setattr(ops, "FP8_GEMM", "auto")
+    monkeypatch.setattr(ops, "FP8_CHOICE", {})
+    _close(ops.linear_fp8(x, w), out, 2e-2, 2e-2)
+    assert len(ops.FP8_CHOICE) == 1
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (4096, 3072, 1024), (300, 4096, 1024)])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
