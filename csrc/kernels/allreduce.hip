@@ -1,4 +1,5 @@
-// C3 tensor-parallel all-reduce over IPC-mapped peer buffers (xGMI), one-shot, hipGraph-capturable.
+// C3 tensor-parallel all-reduce over IPC-mapped peer buffers (xGMI), one-shot, hipGraph-capturable; and
+// the C4 equal-split all-to-all of the expert-parallel MoE layers on the same regions and flag protocol.
 //
 // Why not only RCCL: a TP decode step all-reduces two [B, hidden] activations per layer.  An eager
 // dist.all_reduce cannot sit inside the captured decode graph, so the TP path lost its hipGraph (every
@@ -139,8 +140,110 @@ __global__ void __launch_bounds__(kThreads) allreduce_kernel(Params p) {
   if (t == 0) __hip_atomic_store(epoch_p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- C4: equal-split all-to-all on the same regions and flag protocol (expert-parallel dispatch / combine)
+// send = W chunks of `chunk` bytes (chunk q goes to rank q), recv = W chunks (chunk p came from rank p).
+// Per block b (a contiguous range of every chunk): push send chunk q's range into slot (parity, me) of
+// peer q's region, copy the own chunk locally, publish flags[me][b] = e in every peer, wait until every
+// peer's flag here is at least e, then copy slot (parity, p) -> recv chunk p.  A peer that never arrives:
+// sticky error word, and the block fills its recv ranges with all-ones bytes (NaN for bf16 / f32 / e4m3
+// payloads, -1 for integer counts) instead of copying a possibly stale slot.
+struct A2AParams {
+  uint8_t* base[kMaxRanks];
+  const uint8_t* send;
+  uint8_t* recv;
+  int* err;
+  long long chunk;  // bytes per (source, destination) chunk, multiple of 16
+  long long cap;    // bytes per data slot (>= chunk)
+  long long spin_limit;
+  int me, W;
+};
+
+__global__ void __launch_bounds__(kThreads) alltoall_kernel(A2AParams p) {
+  const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  const long long nvec = p.chunk >> 4;
+  const long long per = (nvec + nb - 1) / nb;
+  const long long v0 = (long long)b * per, v1 = min(nvec, v0 + per);
+  uint8_t* mine = p.base[p.me];
+  int* epoch_p = reinterpret_cast<int*>(mine + kEpochOff) + b;
+  const int e = __hip_atomic_load(epoch_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const int parity = e & 1;
+  const uint4v* sv = reinterpret_cast<const uint4v*>(p.send);
+  uint4v* rv = reinterpret_cast<uint4v*>(p.recv);
+  for (long long v = v0 + t; v < v1; v += kThreads) {
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q) {
+      if (q >= p.W) break;
+      const uint4v val = sv[(long long)q * nvec + v];
+      if (q == p.me) {
+        rv[(long long)q * nvec + v] = val;
+      } else {
+        uint4v* dst = reinterpret_cast<uint4v*>(p.base[q] + kDataOff + ((size_t)parity * p.W + p.me) * p.cap);
+        dst[v] = val;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    for (int q = 0; q < p.W; ++q)
+      if (q != p.me) __hip_atomic_store(flags_of(p.base[q], p.me, b), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __shared__ int missing;
+  if (t == 0) missing = 0;
+  __syncthreads();
+  if (t < p.W && t != p.me) {
+    const int* f = flags_of(mine, t, b);
+    long long spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > p.spin_limit) {
+        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        missing = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  const uint32_t ones = 0xFFFFFFFFu;
+  for (long long v = v0 + t; v < v1; v += kThreads) {
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q) {
+      if (q >= p.W) break;
+      if (q == p.me) continue;
+      rv[(long long)q * nvec + v] =
+          missing ? uint4v{ones, ones, ones, ones}
+                  : reinterpret_cast<const uint4v*>(mine + kDataOff + ((size_t)parity * p.W + q) * p.cap)[v];
+    }
+  }
+  if (t == 0) __hip_atomic_store(epoch_p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace ar
 }  // namespace lwc
+
+// recv[p] = rank p's send chunk for this rank (W chunks of `chunk` bytes each, chunk % 16 == 0, chunk <= cap).
+extern "C" int lwc_alltoall(void* const* bases, int me, int W, const void* send, void* recv, long long chunk,
+                            long long cap, int* err, int blocks, long long spin_limit, hipStream_t s) {
+  using namespace lwc::ar;
+  if (W < 1 || W > kMaxRanks || me < 0 || me >= W || chunk % 16 != 0 || chunk > cap) return -1;
+  if (blocks < 1 || blocks > kMaxBlocks) return -2;
+  if (chunk == 0) return 0;
+  A2AParams p{};
+  for (int i = 0; i < W; ++i) p.base[i] = static_cast<uint8_t*>(bases[i]);
+  p.send = static_cast<const uint8_t*>(send);
+  p.recv = static_cast<uint8_t*>(recv);
+  p.err = err;
+  p.chunk = chunk;
+  p.cap = cap;
+  p.spin_limit = spin_limit > 0 ? spin_limit : kDefaultSpinLimit;
+  p.me = me;
+  p.W = W;
+  alltoall_kernel<<<blocks, kThreads, 0, s>>>(p);
+  return (int)hipGetLastError();
+}
 
 // Bytes of a region for W ranks and `cap` bytes per slot.
 extern "C" long long lwc_ar_region_bytes(int W, long long cap) {

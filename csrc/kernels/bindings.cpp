@@ -48,6 +48,7 @@ int lwc_ar_close(void*);
 int lwc_ar_free(void*);
 int lwc_ar_handle_bytes();
 int lwc_allreduce(void* const*, int, int, const void*, void*, long long, long long, int*, int, long long, hipStream_t);
+int lwc_alltoall(void* const*, int, int, const void*, void*, long long, long long, int*, int, long long, hipStream_t);
 int lwc_pool_l2norm(const void*, int, const int*, int, int, int, float*, void*, hipStream_t);
 int lwc_cosine_consensus(const void*, int, int, int, float*, float, float*, float*, int*, hipStream_t);
 int lwc_knn_topk(const float*, int, int, const float*, int, float*, int*, float*, int*, hipStream_t);
@@ -650,6 +651,21 @@ void allreduce(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& 
            "allreduce");
 }
 
+void alltoall(const std::vector<int64_t>& bases, int64_t me, const at::Tensor& send, at::Tensor& recv, int64_t cap,
+              at::Tensor& err, int64_t blocks, int64_t spin_limit) {
+  // equal-split all-to-all of raw bytes: send / recv [W, chunk] uint8 (chunk % 16 == 0)
+  CHECK_GPU(send); CHECK_GPU(recv); CHECK_CONTIG(send); CHECK_CONTIG(recv);
+  CHECK_DTYPE(send, at::kByte); CHECK_DTYPE(recv, at::kByte); CHECK_DTYPE(err, at::kInt);
+  const int64_t W = (int64_t)bases.size();
+  TORCH_CHECK(send.dim() == 2 && send.size(0) == W && recv.sizes() == send.sizes(), "alltoall: send / recv [W, chunk]");
+  TORCH_CHECK(send.size(1) % 16 == 0 && send.size(1) <= cap, "alltoall: chunk % 16 == 0 and chunk <= cap");
+  std::vector<void*> b;
+  for (int64_t v : bases) b.push_back(reinterpret_cast<void*>(v));
+  CHECK_RC(lwc_alltoall(b.data(), (int)me, (int)W, send.data_ptr(), recv.data_ptr(), send.size(1), cap,
+                        err.data_ptr<int>(), (int)blocks, (long long)spin_limit, cur_stream()),
+           "alltoall");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels of llm_weighted_consensus_amd";
   m.def("rmsnorm", &rmsnorm);
@@ -687,4 +703,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_free", &ar_free);
   m.def("ar_region_bytes", &ar_region_bytes);
   m.def("allreduce", &allreduce);
+  m.def("alltoall", &alltoall);
 }

@@ -220,6 +220,7 @@ __global__ void __launch_bounds__(256) vote_tally_kernel(const double* __restric
                                                          const unsigned char* __restrict__ valid, int L, int C,
                                                          double* __restrict__ cw, double* __restrict__ conf,
                                                          double* __restrict__ vconf) {
+#pragma clang fp contract(off)  // separate multiply and add roundings, as the host tally computes them
   __shared__ double s_cw[kTallyMaxC];
   __shared__ double s_sum;
   const int r = blockIdx.x;

@@ -59,22 +59,34 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // ---- work item: XCD-grouped (n-tile, m-slot), then (group, m-tile) of the slot ----
   const int id = blockIdx.x, xcd = id & 7, local = id >> 3;
-  const int ntile = (local / p.slots) * 8 + xcd;
-  int slot = local % p.slots;
-  if (ntile >= p.n_tiles) return;  // uniform
-  int g = 0, m_begin = 0, m_end = 0;
-  for (; g < p.G; ++g) {
-    // row_off == null: one dense group over rows [0, rows_c) (the dense fp8 projections, G = 1)
-    const int r0 = p.row_off ? p.row_off[g] : 0, r1 = p.row_off ? p.row_off[g + 1] : p.rows_c;
-    const int nt = (r1 - r0 + 255) / 256;
-    if (slot < nt) {
-      m_begin = r0 + slot * 256;
-      m_end = r1;
-      break;
+  int g = 0, m_begin = 0, m_end = 0, ntile = 0;
+  if (p.row_off == nullptr) {
+    // dense (G = 1, rows [0, rows_c), slots = m-tiles): XCD x runs a contiguous range of the GROUPED tile
+    // order (8 m-tiles x every n-tile, m fastest), so the workgroups resident on an XCD at once share a
+    // few A and W panels in its L2 instead of each streaming its own A panel from HBM (at the embedder's
+    // 266k-row prefill the expert-style n-major order re-read A once per n-tile)
+    const int T = p.slots * p.n_tiles, per = (T + 7) / 8, t = xcd * per + local;
+    if (local >= per || t >= T) return;  // uniform
+    const int group = 8 * p.n_tiles, first_m = (t / group) * 8, gsz = min(p.slots - first_m, 8), in = t % group;
+    m_begin = (first_m + in % gsz) * 256;
+    m_end = p.rows_c;
+    ntile = in / gsz;
+  } else {
+    ntile = (local / p.slots) * 8 + xcd;
+    int slot = local % p.slots;
+    if (ntile >= p.n_tiles) return;  // uniform
+    for (; g < p.G; ++g) {
+      const int r0 = p.row_off[g], r1 = p.row_off[g + 1];
+      const int nt = (r1 - r0 + 255) / 256;
+      if (slot < nt) {
+        m_begin = r0 + slot * 256;
+        m_end = r1;
+        break;
+      }
+      slot -= nt;
     }
-    slot -= nt;
+    if (g >= p.G) return;  // surplus slot (uniform)
   }
-  if (g >= p.G) return;  // surplus slot (uniform)
   const int n0 = ntile * 256;
   const int KT = p.K / 128;
 
@@ -258,7 +270,9 @@ extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* 
   const int n_tiles = (N + 255) / 256;
   Params p{(const uint8_t*)A, (const uint8_t*)W, (lwc::bf16_t*)C, row_off, a_rows, a_scale, w_scale,
            G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c};
-  const unsigned grid = (unsigned)(((n_tiles + 7) / 8) * max_slots * 8);
+  // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: n-tile rounds of 8 x max_slots m-slots
+  const unsigned grid = row_off ? (unsigned)(((n_tiles + 7) / 8) * max_slots * 8)
+                                : (unsigned)(8 * ((n_tiles * max_slots + 7) / 8));
   gemm8g_kernel<<<grid, 512, kLdsB, s>>>(p);
   return (int)hipGetLastError();
 }

@@ -61,7 +61,8 @@ class MixtralModel(LlamaModel):
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8: bool = False,
                  tp_rank: int = 0, tp_size: int = 1, tp_group=None, ep_rank: int = 0, ep_size: int = 1,
-                 ep_group=None, ep_mode: str = "padded", ep_capacity: Optional[int] = None, tp_comm=None):
+                 ep_group=None, ep_mode: str = "padded", ep_capacity: Optional[int] = None, tp_comm=None,
+                 ep_comm=None):
         if not cfg.num_experts:
             raise ValueError(f"{cfg.name} is dense; use LlamaModel")
         if ep_size > 1 and tp_size > 1:
@@ -73,7 +74,7 @@ class MixtralModel(LlamaModel):
         if ep_size > 1:
             from ..parallel.expert import ExpertParallel
 
-            self.ep = ExpertParallel(cfg.num_experts, group=ep_group, mode=ep_mode)
+            self.ep = ExpertParallel(cfg.num_experts, group=ep_group, mode=ep_mode, comm=ep_comm)
             if self.ep.W != ep_size:
                 raise ValueError(f"ep_group has {self.ep.W} ranks, ep_size is {ep_size}")
         if cfg.heads % tp_size or cfg.kv_heads % tp_size or cfg.ffn % tp_size:
@@ -179,21 +180,32 @@ class MixtralModel(LlamaModel):
             pdist.all_reduce_(x, group=self.tp_group)
         return x
 
+    def _comms(self):
+        return [c for c in (self.tp_comm, self.ep.comm if self.ep is not None else None)
+                if c is not None and hasattr(c, "arm")]
+
     def comm_arm(self) -> None:
-        """Queue the asynchronous readback of the TP all-reduce's error word (after a step's launch)."""
-        if self.tp_comm is not None and hasattr(self.tp_comm, "arm"):
-            self.tp_comm.arm()
+        """Queue the asynchronous readback of the TP all-reduce's / EP all-to-all's error word (after a
+        step's launch)."""
+        for c in self._comms():
+            c.arm()
 
     def comm_poll(self) -> None:
         """Raise parallel.allreduce.CommFailure if a completed readback shows a peer never arrived."""
-        if self.tp_comm is not None and hasattr(self.tp_comm, "poll"):
-            self.tp_comm.poll()
+        for c in self._comms():
+            c.poll()
 
     @property
     def graph_safe(self) -> bool:
         """Whether a decode step may be captured in a hipGraph: every collective inside it must be a
         stream kernel (the IPC all-reduce), not a host-driven process-group call."""
-        return self.tp_size == 1 and self.ep_size == 1 or (self.tp_size > 1 and self.tp_comm is not None)
+        if self.tp_size == 1 and self.ep_size == 1:
+            return True
+        if self.tp_size > 1:
+            return self.tp_comm is not None
+        # EP: the padded exchange with a fixed capacity over the IPC all-to-all has no host step
+        return (self.ep is not None and self.ep.comm is not None and self.ep.mode == "padded"
+                and self.ep_capacity is not None)
 
     def _attn_out(self, attn: torch.Tensor, L) -> torch.Tensor:
         return self._all_reduce(self._proj(attn, L.wo))

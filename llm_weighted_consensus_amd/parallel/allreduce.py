@@ -134,3 +134,41 @@ class CustomAllReduce:
         if self._own:
             k.ar_free(self._own)
             self._own = 0
+
+
+class CustomAllToAll(CustomAllReduce):
+    """C4: equal-split all-to-all over the same IPC regions and epoch-flag protocol (csrc/kernels/allreduce.hip
+    ``alltoall_kernel``): chunk q of this rank's send buffer is stored straight into rank q's region over
+    xGMI, and chunk p of the receive buffer is copied out of this rank's region once rank p's flag arrives.
+    One launch per exchange, no host synchronisation, graph-capturable — the expert-parallel MoE layer's
+    dispatch and combine (parallel/expert.py, padded mode) inside a captured decode step.  ``max_bytes`` is
+    the largest per-(source, destination) chunk.  A peer that never arrives poisons the received chunks
+    (all-ones bytes: NaN for float payloads) and sets the error word read by :meth:`poll` / :meth:`check`."""
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out[p] = rank p's inp chunk for this rank; ``inp`` / ``out``: contiguous, dim 0 = W * rows (any
+        dtype; chunks are moved as bytes, padded to 16-byte multiples)."""
+        if out.shape != inp.shape or out.dtype != inp.dtype:
+            raise ValueError("CustomAllToAll: out must match inp")
+        if self.W == 1:
+            return out.copy_(inp)
+        if inp.numel() == 0:
+            return out
+        src = inp.contiguous().view(-1).view(torch.uint8).view(self.W, -1)
+        chunk = src.shape[1]
+        cp = (chunk + 15) // 16 * 16
+        if cp > self.cap:
+            raise ValueError(f"CustomAllToAll: chunk of {chunk} bytes exceeds the {self.cap}-byte slot")
+        k = ops.kernels()
+        direct = cp == chunk and out.is_contiguous()
+        if cp != chunk:
+            send = torch.zeros(self.W, cp, dtype=torch.uint8, device=inp.device)
+            send[:, :chunk].copy_(src)
+        else:
+            send = src
+        recv = out.view(-1).view(torch.uint8).view(self.W, -1) if direct else torch.empty_like(send)
+        k.alltoall(self.bases, self.me, send, recv, self.cap, self.err, self.blocks, self.spin_limit)
+        if not direct:
+            out.view(-1).view(torch.uint8).view(self.W, -1).copy_(recv[:, :chunk])
+        return out
+

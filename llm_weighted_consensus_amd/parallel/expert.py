@@ -37,18 +37,25 @@ from . import dist as pdist
 ExpertFn = Callable[[torch.Tensor, torch.Tensor, Optional[torch.Tensor]], torch.Tensor]
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None) -> None:
-    pdist.all_to_all_single(out, inp, out_splits, in_splits, group)
-
-
 class ExpertParallel:
-    def __init__(self, num_experts: int, group=None, mode: str = "padded"):
+    def __init__(self, num_experts: int, group=None, mode: str = "padded", comm=None):
+        """``comm``: a :class:`parallel.allreduce.CustomAllToAll` over the same ranks — the equal-split
+        exchanges of the padded mode then run as one IPC kernel each (graph-capturable, no RCCL call);
+        without it every exchange is a process-group all_to_all_single (RCCL or gloo)."""
         self.W = pdist.group_size(group)
         if num_experts % self.W:
             raise ValueError(f"EP degree {self.W} must divide the number of experts {num_experts}")
         if mode not in ("padded", "exact"):
             raise ValueError(f"unknown EP mode {mode!r}")
-        self.E, self.El, self.group, self.mode = num_experts, num_experts // self.W, group, mode
+        if comm is not None and comm.W != self.W:
+            raise ValueError(f"EP comm has {comm.W} ranks, the EP group {self.W}")
+        self.E, self.El, self.group, self.mode, self.comm = num_experts, num_experts // self.W, group, mode, comm
+
+    def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
+        if self.comm is not None and out_splits is None and in_splits is None:
+            self.comm.all_to_all(out, inp)
+        else:
+            pdist.all_to_all_single(out, inp, out_splits, in_splits, self.group)
 
     # ------------------------------------------------------------------
     def run(self, x_sorted: torch.Tensor, row_off: torch.Tensor, expert_fn: ExpertFn,
@@ -84,14 +91,14 @@ class ExpertParallel:
         # per-(destination, local expert) counts: tiny equal-split exchange
         cnt = (ro[1:] - ro[:-1]).view(W, El)
         rcnt = torch.empty_like(cnt)
-        _a2a(rcnt, cnt, group=self.group)                                     # [W src, El]
+        self._a2a(rcnt, cnt)                                     # [W src, El]
         recv = torch.empty_like(send)
-        _a2a(recv, send, group=self.group)
+        self._a2a(recv, send)
         rscale = None
         if x_scale is not None:
             ssend = self._take(x_scale, src.view(-1), valid.view(-1))
             rscale = torch.empty_like(ssend)
-            _a2a(rscale, ssend, group=self.group)
+            self._a2a(rscale, ssend)
         # received chunk s holds its rows for my experts 0..El-1 back to back; regroup expert-major
         dest, rvalid, row_off_local = self._expert_major(rcnt, C)
         a_rows = torch.zeros(W * C, dtype=torch.int64, device=dev)
@@ -102,7 +109,7 @@ class ExpertParallel:
         y_local = expert_fn(x_local, row_off_local, s_local)                  # [W*C, d_out] expert-major
         back = self._take(y_local, dest.clamp(max=W * C - 1), rvalid)
         ret = torch.empty_like(back)
-        _a2a(ret, back, group=self.group)                                     # [W dest, C] at the sender
+        self._a2a(ret, back)                                     # [W dest, C] at the sender
         # sorted row p went to destination r = owner(expert(p)) at slot p - base[r]
         p = torch.arange(R, device=dev)
         e = torch.searchsorted(ro[1:], p, right=True)
@@ -145,17 +152,17 @@ class ExpertParallel:
         ro = row_off.to(torch.int64)
         cnt = (ro[1:] - ro[:-1]).view(W, El)
         rcnt = torch.empty_like(cnt)
-        _a2a(rcnt, cnt, group=self.group)
+        self._a2a(rcnt, cnt)
         cnt_h, rcnt_h = cnt.cpu(), rcnt.cpu()                                 # one host sync per layer
         in_splits = cnt_h.sum(1).tolist()
         out_splits = rcnt_h.sum(1).tolist()
         n_in = sum(out_splits)
         recv = torch.empty(n_in, *x.shape[1:], dtype=x.dtype, device=dev)
-        _a2a(recv, x.contiguous(), out_splits, in_splits, group=self.group)
+        self._a2a(recv, x.contiguous(), out_splits, in_splits)
         rscale = None
         if x_scale is not None:
             rscale = torch.empty(n_in, dtype=x_scale.dtype, device=dev)
-            _a2a(rscale, x_scale.contiguous(), out_splits, in_splits, group=self.group)
+            self._a2a(rscale, x_scale.contiguous(), out_splits, in_splits)
         # rank-major -> expert-major permutation from the (small) host count matrix
         rm_off = torch.cumsum(rcnt_h.view(-1), 0) - rcnt_h.view(-1)
         order = [torch.arange(int(rm_off[s * El + e]), int(rm_off[s * El + e] + rcnt_h[s, e]))
@@ -167,5 +174,5 @@ class ExpertParallel:
         back = torch.empty(n_in, *y_local.shape[1:], dtype=y_local.dtype, device=dev)
         back[perm] = y_local[:n_in]
         out = torch.empty(x.shape[0], *y_local.shape[1:], dtype=y_local.dtype, device=dev)
-        _a2a(out, back, in_splits, out_splits, group=self.group)
+        self._a2a(out, back, in_splits, out_splits)
         return out

@@ -1,0 +1,191 @@
+"""C4 equal-split all-to-all over IPC-mapped peer buffers (csrc/kernels/allreduce.hip ``alltoall_kernel``),
+two ranks sharing the test box's GPU (handles exchanged over gloo; the data path is the kernel only):
+chunks arrive byte-exact for several dtypes and ragged chunk sizes, across many calls (parity reuse) and
+inside a replayed hipGraph; a rank that skips a call makes its peer poison the received chunks and raise
+CommFailure within the spin bound; and an expert-parallel Mixtral (EP=2) whose dispatch / combine run
+through it gives the single-rank logits, with its decode step hipGraph-safe."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+
+
+def _payload(src, dst, it, shape, dtype):
+    """Rank src's chunk for rank dst at call it (deterministic, both ranks can rebuild it)."""
+    g = torch.Generator().manual_seed(src * 1000 + dst * 100 + it)
+    if dtype in (torch.int64, torch.int32):
+        return torch.randint(-1000, 1000, shape, generator=g, dtype=dtype)
+    if dtype == torch.float8_e4m3fn:  # built as bytes (no NaN pattern 0x7f / 0xff), viewed as e4m3 on the device
+        return torch.randint(0, 127, shape, generator=g, dtype=torch.uint8)
+    return torch.randn(shape, generator=g).to(dtype)
+
+
+def _run(world, target, *args, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=timeout) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def _a2a_worker(rank, world, port, q):
+    _env(rank, world, port)
+    try:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllToAll
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllToAll(device=dev, max_bytes=1 << 20, blocks=16)
+        bad = []
+        cases = [((3, 64), torch.bfloat16), ((2, 4), torch.int64), ((5,), torch.float32), ((128, 96), torch.bfloat16),
+                 ((7, 33), torch.float8_e4m3fn), ((1000, 256), torch.bfloat16), ((1,), torch.int32)]
+        for it in range(28):
+            shape, dt = cases[it % len(cases)]
+            inp = torch.stack([_payload(rank, d, it, shape, dt) for d in range(world)]).to(dev)
+            if dt == torch.float8_e4m3fn:
+                inp = inp.view(dt)
+            out = torch.empty_like(inp)
+            comm.all_to_all(out.view(world * shape[0], *shape[1:]), inp.view(world * shape[0], *shape[1:]))
+            want = torch.stack([_payload(s, rank, it, shape, dt) for s in range(world)])
+            got = out.cpu()
+            if dt == torch.float8_e4m3fn:
+                got = got.view(torch.uint8)
+            if not torch.equal(got, want):
+                bad.append(("eager", it, shape, str(dt)))
+        # captured in a hipGraph, replayed with fresh inputs in the static buffer
+        shape = (64, 128)
+        s_in = torch.zeros(world * shape[0], shape[1], dtype=torch.bfloat16, device=dev)
+        s_out = torch.zeros_like(s_in)
+        st = torch.cuda.Stream(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(st):
+            comm.all_to_all(s_out, s_in)
+        torch.cuda.current_stream(dev).wait_stream(st)
+        pdist.barrier()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            comm.all_to_all(s_out, s_in)
+        for it in range(8):
+            s_in.copy_(torch.cat([_payload(rank, d, 500 + it, shape, torch.bfloat16) for d in range(world)]).to(dev))
+            graph.replay()
+            torch.cuda.synchronize(dev)
+            want = torch.cat([_payload(s, rank, 500 + it, shape, torch.bfloat16) for s in range(world)])
+            if not torch.equal(s_out.cpu(), want):
+                bad.append(("graph", it))
+        comm.check()
+        pdist.barrier()
+        comm.close()
+        q.put((rank, bad))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_alltoall_two_ranks_one_gpu(gpu):
+    assert _run(2, _a2a_worker) == {0: [], 1: []}
+
+
+def _skip_worker(rank, world, port, q):
+    _env(rank, world, port)
+    try:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CommFailure, CustomAllToAll
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllToAll(device=dev, max_bytes=1 << 16, blocks=4, spin_ms=300)
+        x = torch.ones(world * 16, 8, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros_like(x)
+        comm.all_to_all(out, x)
+        torch.cuda.synchronize(dev)
+        ok_first = bool(torch.equal(out.cpu(), x.cpu())) and not int(comm.err.item())
+        pdist.barrier()
+        res = {"first": ok_first}
+        if rank == 0:  # rank 1 never joins this call
+            comm.all_to_all(out, x)
+            comm.arm()
+            torch.cuda.synchronize(dev)
+            peer = out.view(world, 16, 8)[1]
+            res["nan"] = bool(torch.isnan(peer.float()).all())
+            res["own"] = bool(torch.equal(out.view(world, 16, 8)[0].cpu(), x.view(world, 16, 8)[0].cpu()))
+            try:
+                comm.poll()
+                res["raised"] = False
+            except CommFailure:
+                res["raised"] = True
+        pdist.barrier()
+        comm.close()
+        q.put((rank, res))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_alltoall_missing_peer_fails_loudly(gpu):
+    res = _run(2, _skip_worker)
+    assert res[1] == {"first": True}, res
+    assert res[0] == {"first": True, "nan": True, "own": True, "raised": True}, res
+
+
+def _ep_worker(rank, world, port, q, fp8):
+    _env(rank, world, port)
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllToAll
+        from tests.test_tp_gpu import _prefill_logits
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllToAll(device=dev, max_bytes=1 << 20, blocks=16)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
+                         ep_rank=rank, ep_size=world, ep_mode="padded", ep_capacity=64, ep_comm=comm)
+        assert m.graph_safe
+        lg = _prefill_logits(m, dev, P=23 + 9 * rank, seed=rank)
+        torch.cuda.synchronize(dev)
+        comm.check()
+        pdist.barrier()
+        comm.close()
+        q.put((rank, lg))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_mixtral_ep2_through_ipc_alltoall(gpu, fp8):
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+    from tests.test_tp_gpu import _prefill_logits
+
+    res = _run(2, _ep_worker, fp8, timeout=600)
+    assert all(isinstance(v, torch.Tensor) for v in res.values()), res
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512, fp8=fp8)
+    for r in range(2):
+        ref = _prefill_logits(m, gpu, P=23 + 9 * r, seed=r)
+        c = torch.nn.functional.cosine_similarity(res[r], ref, dim=0).item()
+        assert c > 0.999, (r, c)

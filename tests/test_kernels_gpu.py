@@ -728,9 +728,11 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
 @pytest.mark.parametrize("d,rows", [(4096, 1), (4096, 301), (2048, 64), (8192, 257), (1024, 33)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_rmsnorm_quant_fp8_fused(gpu, d, rows, with_res):
-    """RMSNorm with the per-row e4m3 quantisation fused (K1 + K11e): bitwise equal to the two-kernel path
-    quant_fp8_rows(rmsnorm(x)) (same bf16 rounding before the row max), residual stream updated the same
-    way; d = 1024 takes the two-kernel fallback."""
+    """RMSNorm with the per-row e4m3 quantisation fused (K1 + K11e): the e4m3 rows and scales are bitwise
+    quant_fp8_rows of the kernel's own bf16 output (same rounding before the row max); that output and the
+    residual update equal the plain RMSNorm (bitwise where both take the wave-per-row kernel, rows >= 256;
+    the workgroup-per-row kernel of smaller batches reduces in another order); d = 1024 takes the
+    two-kernel fallback."""
     from llm_weighted_consensus_amd import ops
 
     x = _bf(rows, d, dev=gpu)
@@ -738,11 +740,14 @@ def test_rmsnorm_quant_fp8_fused(gpu, d, rows, with_res):
     r = _bf(rows, d, dev=gpu) if with_res else None
     r2 = r.clone() if with_res else None
     y = ops.rmsnorm(x, w, 1e-5, residual=r)
-    q_ref, s_ref = ops.quant_fp8_rows(y)
     a = ops.rmsnorm_quant_fp8(x, w, 1e-5, residual=r2, keep_bf16=True)
-    assert torch.equal(a.bf16, y)
+    q_ref, s_ref = ops.quant_fp8_rows(a.bf16)
     assert torch.equal(a.q.view(torch.uint8), q_ref.view(torch.uint8))
     assert torch.equal(a.s, s_ref)
+    if rows >= 256 or d == 1024:
+        assert torch.equal(a.bf16, y)
+    else:
+        _close(a.bf16, y, 2e-2, 1e-2)
     if with_res:
         assert torch.equal(r2, r)
     # dequantised rows track the fp32 reference within e4m3 precision
