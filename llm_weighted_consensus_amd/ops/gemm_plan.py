@@ -116,26 +116,29 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
     the fp32 erf-GELU at the bge-large FFN1 shape — the bf16 output's own rounding, 7.8e-3 for gemm8p's
     exact erf — where GEMM + the K9b bias_gelu pass rounds twice, 1.6e-2, and runs 657 vs 510 us at
     65536 tokens: scripts/gelu_epilogue_probe.py).  The backend is chosen per (token bucket, N, K,
-    epilogue) by timing both on the first call."""
+    epilogue) by timing the library and both hand-written cores (gemm8p, gemm4w) on the first call."""
     M, K = x.shape
     N = w.shape[0]
     epi = "bias_gelu" if gelu else "bias"
     key = (_m_bucket(M), N, K, epi)
-    c = MODE if MODE in ("blas", "g8") else _CHOICE.get(key)
-    # gemm8p addresses A through 32-bit buffer offsets: operands of 2 GiB or more take the library path
+    c = MODE if MODE in ("blas", "g8", "g4") else _CHOICE.get(key)
+    # the hand-written cores address A through 32-bit buffer offsets: operands of 2 GiB or more take the
+    # library path
     ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda and M * x.stride(0) * 2 < (1 << 31)
-    run_g8 = lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws)  # noqa: E731
-    run_blas = ((lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu  # noqa: E731
-                else (lambda: F.linear(x, w, b)))
+    runs = {"g8": lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws),
+            "g4": lambda: gemm4w(x, w, bias=b, gelu=gelu),
+            "blas": ((lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu
+                     else (lambda: F.linear(x, w, b)))}
     if c is None:
         if not ok or torch.cuda.is_current_stream_capturing():
             c = "blas"
         else:
-            t_blas, t_g8 = _time(run_blas, iters=2, rounds=3), _time(run_g8, iters=2, rounds=3)
-            TIMINGS[key] = {"blas": t_blas, "g8": t_g8}
-            c = "g8" if t_g8 < t_blas else "blas"
+            t = {name: _time(fn, iters=2, rounds=3) for name, fn in runs.items()}
+            TIMINGS[key] = t
+            own = min(("g8", "g4"), key=lambda n: t[n])
+            c = own if t[own] <= t["blas"] * (1 + OWN_MARGIN) else "blas"
         _CHOICE[key] = c
-    return run_g8() if c == "g8" and ok else run_blas()
+    return runs[c]() if c != "blas" and ok else runs["blas"]()
 
 
 def _time(fn, iters: int = 5, rounds: int = 3) -> float:

@@ -53,6 +53,24 @@ def _moe_full(x, router, w1, w2, k):
     return (y[inv].view(T, k, y.shape[-1]) * w[..., None]).sum(1)
 
 
+class _ByteAllToAll:
+    """Stand-in with CustomAllToAll's contract (equal chunks moved as raw bytes, parallel/allreduce.py) over
+    the gloo group, to check the EP layer's routing of its exchanges through a ``comm``."""
+
+    def __init__(self, W):
+        self.W, self.calls = W, 0
+
+    def all_to_all(self, out, inp):
+        import torch.distributed as dist
+
+        self.calls += 1
+        src = inp.contiguous().view(-1).view(torch.uint8)
+        recv = torch.empty_like(src)
+        dist.all_to_all_single(recv, src)
+        out.view(-1).view(torch.uint8).copy_(recv)
+        return out
+
+
 def _worker(rank, world, port, mode, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
@@ -70,7 +88,8 @@ def _worker(rank, world, port, mode, q):
         sizes = [5, 0, 9, 3][:world]  # rank 1 has no tokens this step
         xs = [torch.randn(n, d, generator=g) for n in sizes]
         x = xs[rank]
-        ep = ExpertParallel(E, mode=mode)
+        comm = _ByteAllToAll(world) if mode == "padded-comm" else None
+        ep = ExpertParallel(E, mode="padded" if mode == "padded-comm" else mode, comm=comm)
         El = ep.El
         lw1, lw2 = w1[rank * El:(rank + 1) * El], w2[rank * El:(rank + 1) * El]
         w, row_off, src, inv = route_ref(x @ router.t(), k)
@@ -78,14 +97,17 @@ def _worker(rank, world, port, mode, q):
         T = x.shape[0]
         out = (y_sorted[inv].view(T, k, y_sorted.shape[-1]) * w[..., None]).sum(1)
         ref = _moe_full(x, router, w1, w2, k)
-        q.put((rank, bool(torch.allclose(out, ref, atol=1e-5, rtol=1e-5)), float((out - ref).abs().max())
-               if T else 0.0))
+        ok = bool(torch.allclose(out, ref, atol=1e-5, rtol=1e-5))
+        if comm is not None:  # counts, rows and returned outputs: every exchange went through the comm
+            ok = ok and comm.calls == 3
+        q.put((rank, ok, float((out - ref).abs().max()) if T else 0.0))
         pdist.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize("world,mode", [(2, "padded"), (2, "exact"), (4, "padded"), (4, "exact")])
+@pytest.mark.parametrize("world,mode", [(2, "padded"), (2, "exact"), (4, "padded"), (4, "exact"), (2, "padded-comm"),
+                                        (4, "padded-comm")])
 def test_expert_parallel_matches_full_moe(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
