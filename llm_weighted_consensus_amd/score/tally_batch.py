@@ -45,11 +45,16 @@ def _check(votes, weights, C: int) -> None:
             raise ValueError("tally: vote length != choices")
 
 
-def tally_many_gpu(items: Sequence, device) -> List[Tally]:
+def tally_many_gpu(items: Sequence, device, stream=None) -> List[Tally]:
     """K10b over ``items`` = [(votes, weights, C)] in one launch: rows are padded to the largest voter
-    count and choice count (padded voters are invalid, padded choices have zero votes)."""
+    count and choice count (padded voters are invalid, padded choices have zero votes).  ``stream``: a
+    side stream (the serving path's: the read-back then never waits behind engine work queued on the
+    device's default stream)."""
     import torch
 
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            return tally_many_gpu(items, device)
     from .. import ops
 
     for votes, wts, C in items:
@@ -86,6 +91,7 @@ class TallyBatcher:
         self._scheduled = False
         self.gpu_batches = 0  # launches so far (observability / tests)
         self.gpu_tallies = 0
+        self._stream = None  # created on the first GPU batch (a non-blocking side stream)
 
     async def tally(self, voter_choices, C_len: int):
         votes, wts = vote_rows(voter_choices)
@@ -104,7 +110,11 @@ class TallyBatcher:
             return
         if self.device is not None and len(live) >= self.min_batch:
             try:
-                res = tally_many_gpu([(v, w, c) for v, w, c, _ in live], self.device)
+                if self._stream is None:
+                    import torch
+
+                    self._stream = torch.cuda.Stream(device=self.device)
+                res = tally_many_gpu([(v, w, c) for v, w, c, _ in live], self.device, self._stream)
             except ValueError as e:  # a malformed vote: fail the requests like the host tally would
                 for *_, fut in live:
                     fut.set_exception(e)

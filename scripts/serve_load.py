@@ -88,7 +88,8 @@ def main():
     t0 = time.time()
     gpus = [int(x) for x in a.gpus.split(",") if x.strip()]
     state = build_state(Config(models=models, kv_fraction=0.6, gpus=gpus,
-                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "2048"))))
+                               chunked_prefill=int(os.environ.get("LWC_CHUNKED_PREFILL", "2048")),
+                               gpu_tally=os.environ.get("LWC_GPU_TALLY")))
     print(f"# model ready in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     app = create_app(state)
     client = httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t", timeout=600)
@@ -147,6 +148,9 @@ def main():
 
     out["phases"] = {k: [v[0], round(v[1], 3)] for k, v in STATS.snapshot()["phases"].items()}
     out["engine_steps"] = stats["steps"]
+    tb = getattr(state.score, "tally_batcher", None)
+    if tb is not None:  # K10b: tallies batched into GPU launches (LWC_GPU_TALLY)
+        out["gpu_tally"] = {"min_batch": tb.min_batch, "launches": tb.gpu_batches, "tallies": tb.gpu_tallies}
     out["gc"] = {f"gen{k}": [gc_n[k], round(gc_time[k], 3)] for k in gc_time}
     print(json.dumps(out), flush=True)
     for svc in state.services.values():

@@ -64,7 +64,7 @@ def test_batcher_groups_one_turn(monkeypatch):
     reaches min_batch (here a host stand-in for the kernel, to check the packing and unpacking)."""
     calls = []
 
-    def fake_gpu(items, device):
+    def fake_gpu(items, device, stream=None):
         calls.append(len(items))
         out = []
         for votes, wts, C in items:
@@ -73,6 +73,9 @@ def test_batcher_groups_one_turn(monkeypatch):
         return out
 
     monkeypatch.setattr(TB, "tally_many_gpu", fake_gpu)
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "Stream", lambda device=None: None)  # no device here
     rng = random.Random(1)
     reqs = [(_request(rng, 4, 6), 4) for _ in range(5)]
 
