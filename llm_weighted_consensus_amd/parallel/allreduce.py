@@ -148,8 +148,8 @@ class CustomAllToAll(CustomAllReduce):
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """out[p] = rank p's inp chunk for this rank; ``inp`` / ``out``: contiguous, dim 0 = W * rows (any
         dtype; chunks are moved as bytes, padded to 16-byte multiples)."""
-        if out.shape != inp.shape or out.dtype != inp.dtype:
-            raise ValueError("CustomAllToAll: out must match inp")
+        if out.shape != inp.shape or out.dtype != inp.dtype or not out.is_contiguous():
+            raise ValueError("CustomAllToAll: out must be a contiguous tensor matching inp")
         if self.W == 1:
             return out.copy_(inp)
         if inp.numel() == 0:
@@ -160,7 +160,7 @@ class CustomAllToAll(CustomAllReduce):
         if cp > self.cap:
             raise ValueError(f"CustomAllToAll: chunk of {chunk} bytes exceeds the {self.cap}-byte slot")
         k = ops.kernels()
-        direct = cp == chunk and out.is_contiguous()
+        direct = cp == chunk
         if cp != chunk:
             send = torch.zeros(self.W, cp, dtype=torch.uint8, device=inp.device)
             send[:, :chunk].copy_(src)
