@@ -423,7 +423,7 @@ struct CascadeParams {
 // uniform addresses the compiler may then use SCALAR loads for them (no possible clobber by the output
 // stores).  As vector loads every block-table / ctx-len read needed an s_waitcnt vmcnt(0), which drained
 // the K/V loads in flight and serialised both phases.
-template <int kCPairs, bool kPrefetch>
+template <int kCPairs>
 __global__ void __launch_bounds__(kCWaves * 64)
     paged_decode_cascade_kernel(CascadeParams p, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens,
                                 const int* __restrict__ tiles) {
@@ -456,13 +456,14 @@ __global__ void __launch_bounds__(kCWaves * 64)
   float m = -1e30f, l = 0.f;
 
   // ---- phase 1: shared prefix through LDS ----
+  auto phase1 = [&]() {
   const int* bt0 = block_tables + (size_t)row_start * p.max_blocks;
   const int pctx = pblk * kBS;
-  // LDS-DMA (global_load_lds_dwordx4) of the chunk of block pairs starting at block c0: wave-instruction
-  // (pair, round) writes 1 KiB contiguously, lane-linear; the K image's XOR swizzle is applied to the SOURCE
-  // address instead.
-  auto dma_chunk = [&](int c0) __attribute__((always_inline)) {
+  for (int c0 = 0; c0 < pblk; c0 += 2 * kCPairs) {
     const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
+    __syncthreads();  // previous chunk fully consumed
+    // LDS-DMA (global_load_lds_dwordx4): wave-instruction (pair, round) writes 1 KiB contiguously,
+    // lane-linear; the K image's XOR swizzle is applied to the SOURCE address instead.
 #pragma unroll
     for (int pi = 0; pi < kCPairs; ++pi) {
 #pragma unroll
@@ -489,45 +490,30 @@ __global__ void __launch_bounds__(kCWaves * 64)
         }
       }
     }
-  };
-  auto compute_chunk = [&](int c0) __attribute__((always_inline)) {
-    const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
-    if (nrows <= 0) return;
-    for (int pi = 0; pi < npairs; ++pi) {
-      const int blkA = c0 + 2 * pi;
-      const bool hasB = blkA + 1 < pblk;
-      const unsigned char* pb = smem + pi * kPairBytes;
-      PairRegs r;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int ch = ((4 * s + g) ^ r16) << 4;
-        r.ka[s] = *reinterpret_cast<const short8*>(pb + r16 * 256 + ch);
-        r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
-      }
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
-        r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
-                        *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
-      }
-      attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
-    }
-  };
-  // chunks after the first (prefixes longer than kCPairs pairs): stage, then attend
-  auto phase1_rest = [&]() __attribute__((always_inline)) {
-    for (int c0 = 2 * kCPairs; c0 < pblk; c0 += 2 * kCPairs) {
-      __syncthreads();  // previous chunk fully consumed
-      dma_chunk(c0);
-      __syncthreads();
-      compute_chunk(c0);
-    }
-  };
-  auto phase1 = [&]() __attribute__((always_inline)) {
-    if (pblk <= 0) return;
-    dma_chunk(0);
     __syncthreads();
-    compute_chunk(0);
-    phase1_rest();
+    if (nrows > 0) {
+      for (int pi = 0; pi < npairs; ++pi) {
+        const int blkA = c0 + 2 * pi;
+        const bool hasB = blkA + 1 < pblk;
+        const unsigned char* pb = smem + pi * kPairBytes;
+        PairRegs r;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ch = ((4 * s + g) ^ r16) << 4;
+          r.ka[s] = *reinterpret_cast<const short8*>(pb + r16 * 256 + ch);
+          r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
+          r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
+                          *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
+        }
+        attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
+      }
+    }
+  }
+
   };
 
   // ---- phase 2: each sequence's own blocks, two pairs in flight per wave ----
@@ -590,19 +576,9 @@ __global__ void __launch_bounds__(kCWaves * 64)
     }
   };
 
-  // Softmax merging is order-free.  kPrefetch: the first prefix chunk's LDS-DMA is issued BEFORE the
-  // suffix pass and consumed after it, so its HBM latency hides behind the suffix stream instead of
-  // stalling the (one-per-CU: 8 waves x ~235 VGPRs) workgroup at a barrier.  Otherwise odd workgroups
-  // stream their suffixes first.
-  if constexpr (kPrefetch) {
-    if (pblk > 0) dma_chunk(0);
-    phase2();
-    if (pblk > 0) {
-      __syncthreads();  // the DMA of every wave has landed (the barrier's fence waits on vmcnt)
-      compute_chunk(0);
-      phase1_rest();
-    }
-  } else if (tile & 1) {
+  // Softmax merging is order-free: odd workgroups stream their suffixes first, so a CU's two
+  // resident workgroups overlap one's LDS-bound prefix phase with the other's HBM-bound suffix.
+  if (tile & 1) {
     phase2();
     phase1();
   } else {
@@ -687,37 +663,26 @@ extern "C" int lwc_paged_decode_cascade(const void* q, int q_stride, const void*
   CascadeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, tiles,
                   (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale};
   static int pairs = 0;
-  static bool prefetch = true;
   if (pairs == 0) {
     const char* e = getenv("LWC_CASCADE_PAIRS");
     pairs = e ? atoi(e) : 8;
-    const void* fns[] = {(const void*)paged_decode_cascade_kernel<2, true>, (const void*)paged_decode_cascade_kernel<4, true>,
-                         (const void*)paged_decode_cascade_kernel<8, true>, (const void*)paged_decode_cascade_kernel<2, false>,
-                         (const void*)paged_decode_cascade_kernel<4, false>, (const void*)paged_decode_cascade_kernel<8, false>};
-    const int lds[] = {2, 4, 8, 2, 4, 8};
-    for (int i = 0; i < 6; ++i)
-      (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, lds[i] * kPairBytes);
+    for (int k : {2, 4, 8})
+      (void)hipFuncSetAttribute(k == 2 ? (const void*)paged_decode_cascade_kernel<2>
+                                       : k == 4 ? (const void*)paged_decode_cascade_kernel<4>
+                                                : (const void*)paged_decode_cascade_kernel<8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, k * kPairBytes);
   }
   {
-    // experiment knobs, re-read per launch: LDS pairs per chunk, and the prefix-chunk prefetch (default on)
-    const char* e = getenv("LWC_CASCADE_PAIRS");
+    const char* e = getenv("LWC_CASCADE_PAIRS");  // experiment knob, re-read per launch
     if (e) pairs = atoi(e);
-    const char* f = getenv("LWC_CASCADE_PREFETCH");
-    prefetch = !(f && f[0] == '0');
   }
   const dim3 grid(Hkv, max_tiles);
-#define LWC_CASC(P, F) \
-  paged_decode_cascade_kernel<P, F><<<grid, kCWaves * 64, P * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles)
-  if (prefetch) {
-    if (pairs == 2) LWC_CASC(2, true);
-    else if (pairs == 4) LWC_CASC(4, true);
-    else LWC_CASC(8, true);
-  } else {
-    if (pairs == 2) LWC_CASC(2, false);
-    else if (pairs == 4) LWC_CASC(4, false);
-    else LWC_CASC(8, false);
-  }
-#undef LWC_CASC
+  if (pairs == 2)
+    paged_decode_cascade_kernel<2><<<grid, kCWaves * 64, 2 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
+  else if (pairs == 4)
+    paged_decode_cascade_kernel<4><<<grid, kCWaves * 64, 4 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
+  else
+    paged_decode_cascade_kernel<8><<<grid, kCWaves * 64, 8 * kPairBytes, s>>>(p, block_tables, ctx_lens, tiles);
   return (int)hipGetLastError();
 }
 
