@@ -332,22 +332,47 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     constexpr int CPR = CW / 8;  // 16 B chunks per row
     const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
     const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-#pragma unroll 4
-    for (int c = lane; c < 128 * CPR; c += 64) {
-      const int row = c / CPR, cch = c % CPR;
-      const int gm = m0 + wm * 128 + row;
-      const int gn = ncol0 + cch * 8;
-      if (gm < p.M && gn < ncols) {
-        uint4v v = *reinterpret_cast<const uint4v*>(ot + row * CW + swz<CW>(row, cch * 8));
-        if constexpr (EPI == EPI_RESIDUAL) {
+    if constexpr (EPI == EPI_RESIDUAL) {
+      // Residual loads branch-free through a buffer resource over this wave's rows (rows past M read zeros
+      // without a request; columns past N are never stored), kGrp of them in flight per lane before the
+      // first add: loaded inside the store's bounds branch, every chunk waited its own HBM round trip
+      // (vmcnt(0) per 16 B, the epilogue's whole latency).
+      const int row0 = m0 + wm * 128;
+      const int rows_here = max(0, min(p.M - row0, 128));
+      const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
+      constexpr int kIt = 128 * CPR / 64, kGrp = 16;
+#pragma unroll 1
+      for (int g0 = 0; g0 < kIt; g0 += kGrp) {
+        uint4v rv[kGrp];
+#pragma unroll
+        for (int u = 0; u < kGrp; ++u) {
+          const int c = lane + 64 * (g0 + u);
+          const int row = c / CPR, gn = ncol0 + (c % CPR) * 8;
+          rv[u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < kGrp; ++u) {
+          const int c = lane + 64 * (g0 + u);
+          const int row = c / CPR, cch = c % CPR;
+          const int gm = row0 + row, gn = ncol0 + cch * 8;
           float x[8], y[8];
-          unpack8(v, x);
-          unpack8(*reinterpret_cast<const uint4v*>(p.R + (size_t)gm * p.ldc + gn), y);
+          unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + swz<CW>(row, cch * 8)), x);
+          unpack8(rv[u], y);
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] += y[e];
-          v = pack8(x);
+          if (gm < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = pack8(x);
         }
-        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+      }
+    } else {
+#pragma unroll 4
+      for (int c = lane; c < 128 * CPR; c += 64) {
+        const int row = c / CPR, cch = c % CPR;
+        const int gm = m0 + wm * 128 + row;
+        const int gn = ncol0 + cch * 8;
+        if (gm < p.M && gn < ncols)
+          *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
+              *reinterpret_cast<const uint4v*>(ot + row * CW + swz<CW>(row, cch * 8));
       }
     }
     __syncthreads();  // LDS free for the next tile

@@ -352,22 +352,44 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
     const int cch = lane % CPR;
     const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wc * 32 : n0 + wc * 64;
     const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-#pragma unroll 4
-    for (int k = 0; k < 128 / RPI; ++k) {
-      const int row = lane / CPR + RPI * k;
-      const int gm = m0 + wr * 128 + row;
+    if constexpr (EPI == EPI_RESIDUAL) {
+      // residual rows through a buffer resource (rows past M read zeros, no request), all of a group's loads
+      // in flight before the first add — inside the store's bounds branch each 16 B load waited its own
+      // HBM round trip
+      const int row0 = m0 + wr * 128;
+      const int rows_here = max(0, min(p.M - row0, 128));
+      const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
       const int gn = ncol0 + cch * 8;
-      if (gm < p.M && gn < ncols) {
-        uint4v v = *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ (((row & 7) << 3) % CW)));
-        if constexpr (EPI == EPI_RESIDUAL) {
+      constexpr int kIt = 128 / RPI, kGrp = kIt < 16 ? kIt : 16;
+#pragma unroll 1
+      for (int k0 = 0; k0 < kIt; k0 += kGrp) {
+        uint4v rv[kGrp];
+#pragma unroll
+        for (int u = 0; u < kGrp; ++u) {
+          const int row = lane / CPR + RPI * (k0 + u);
+          rv[u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < kGrp; ++u) {
+          const int row = lane / CPR + RPI * (k0 + u);
           float x[8], y[8];
-          unpack8(v, x);
-          unpack8(*reinterpret_cast<const uint4v*>(p.R + (size_t)gm * p.ldc + gn), y);
+          unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ (((row & 7) << 3) % CW))), x);
+          unpack8(rv[u], y);
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] += y[e];
-          v = pack8(x);
+          if (row0 + row < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)(row0 + row) * p.ldc + gn) = pack8(x);
         }
-        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+      }
+    } else {
+#pragma unroll 4
+      for (int k = 0; k < 128 / RPI; ++k) {
+        const int row = lane / CPR + RPI * k;
+        const int gm = m0 + wr * 128 + row;
+        const int gn = ncol0 + cch * 8;
+        if (gm < p.M && gn < ncols)
+          *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
+              *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ (((row & 7) << 3) % CW)));
       }
     }
     __syncthreads();  // LDS free for the next item's prologue
