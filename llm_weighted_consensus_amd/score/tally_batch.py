@@ -119,11 +119,14 @@ class TallyBatcher:
                 for *_, fut in live:
                     fut.set_exception(e)
                 return
-            self.gpu_batches += 1
-            self.gpu_tallies += len(live)
-            for (_, _, _, fut), t in zip(live, res):
-                fut.set_result(t)
-            return
+            except Exception:  # noqa: BLE001 — a device error must not strand the awaiting requests:
+                res = None     # they fall back to the host tally below
+            if res is not None:
+                self.gpu_batches += 1
+                self.gpu_tallies += len(live)
+                for (_, _, _, fut), t in zip(live, res):
+                    fut.set_result(t)
+                return
         for votes, wts, C, fut in live:
             try:
                 fut.set_result(RT.tally(votes, wts, C))

@@ -90,6 +90,29 @@ def test_batcher_groups_one_turn(monkeypatch):
     assert len(res) == 5 and len(small) == 2
 
 
+def test_batcher_device_error_falls_back_to_host(monkeypatch):
+    """A failing GPU batch (device error) must not strand the awaiting requests: they get the host tally."""
+    def broken(items, device, stream=None):
+        raise RuntimeError("HIP error")
+
+    monkeypatch.setattr(TB, "tally_many_gpu", broken)
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "Stream", lambda device=None: None)
+    rng = random.Random(4)
+    reqs = [(_request(rng, 3, 5), 3) for _ in range(4)]
+
+    async def main():
+        b = TB.TallyBatcher(device="fake", min_batch=2)
+        return b, await asyncio.wait_for(asyncio.gather(*(b.tally(ch, C) for ch, C in reqs)), 10)
+
+    b, outs = asyncio.run(main())
+    assert b.gpu_batches == 0
+    for (ch, C), t in zip(reqs, outs):
+        votes, wts = TB.vote_rows(ch)
+        _same(t.choice_weight, RT.tally(votes, wts, C).choice_weight)
+
+
 def test_make_batcher_spec():
     assert TB.make_batcher(None, "cuda:0") is None
     assert TB.make_batcher("0", "cuda:0") is None
