@@ -341,7 +341,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       const int rows_here = max(0, min(p.M - row0, 128));
       const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
-      constexpr int kIt = 128 * CPR / 64, kGrp = 16;
+      constexpr int kIt = 128 * CPR / 64;                         // chunks per lane: 32 (bn 256), 24 (bn 192)
+      constexpr int kGrp = kIt % 16 == 0 ? 16 : (kIt % 12 == 0 ? 12 : 8);  // whole groups only
+      static_assert(kIt % kGrp == 0, "residual epilogue groups must tile the wave's chunks");
 #pragma unroll 1
       for (int g0 = 0; g0 < kIt; g0 += kGrp) {
         uint4v rv[kGrp];

@@ -362,6 +362,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
           (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
       const int gn = ncol0 + cch * 8;
       constexpr int kIt = 128 / RPI, kGrp = kIt < 16 ? kIt : 16;
+      static_assert(kIt % kGrp == 0, "residual epilogue groups must tile the wave's rows");
 #pragma unroll 1
       for (int k0 = 0; k0 < kIt; k0 += kGrp) {
         uint4v rv[kGrp];
