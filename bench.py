@@ -133,6 +133,8 @@ def main():
     res = None
     for i in range(a.warmup):
         res = one_step(i, res)[0]
+        if rank == 0:  # progress on stderr (stdout carries only the JSON result line)
+            print(f"# warmup step {i + 1}/{a.warmup} done", file=sys.stderr, flush=True)
     if res is not None:
         res.resolve()
     torch.cuda.synchronize(dev)
@@ -145,6 +147,8 @@ def main():
         res, tg, ts = one_step(a.warmup + i, res)
         gen_t += tg
         score_t += ts
+        if rank == 0:
+            print(f"# timed step {i + 1}/{a.steps} done", file=sys.stderr, flush=True)
     if res is not None:
         res.resolve()  # every timed step's answers are on the host before the clock stops
     torch.cuda.synchronize(dev)
