@@ -202,9 +202,11 @@ def _tune(x, w, epi, block, ws, M, N, K, key) -> str:
         else:
             runs[b] = (lambda: F.linear(x, w)) if b == "blas" else (lambda b=b: _own(b, x, w, ws))
     ts = {b: [] for b in runs}
-    for _ in range(3):
+    # 5 interleaved rounds of 5 calls: o and gate|up are within 1-3 % between backends, and 3 x 3 calls
+    # flipped the choice from run to run (profiles/bench_r64_round3.md); runs before graph capture only
+    for _ in range(5):
         for b, fn in runs.items():
-            ts[b].append(_time(fn, iters=3, rounds=1))
+            ts[b].append(_time(fn, iters=5, rounds=1))
     med = {b: sorted(t)[len(t) // 2] for b, t in ts.items()}
     TIMINGS[key] = med
     own = min((b for b in med if b != "blas"), key=lambda b: med[b], default=None)
