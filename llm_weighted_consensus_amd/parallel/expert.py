@@ -19,6 +19,12 @@ Two exchange modes:
 * ``exact``: the per-destination row counts travel first (one tiny all-to-all + a host read), then the
   rows go with variable splits — no padding bytes.  Right for prefill (large T).
 
+Transport: each exchange is an equal-split ``all_to_all_single`` on the process group (RCCL or gloo), or —
+with ``comm`` = a :class:`parallel.allreduce.CustomAllToAll` — one IPC kernel launch that stores every chunk
+straight into its owner's peer buffer over xGMI (no RCCL call, no host step), so a padded-mode decode step
+with a fixed capacity captures into a hipGraph (``MixtralModel.graph_safe``).  A peer that never arrives
+poisons the received rows (NaN) and raises ``CommFailure`` one step later instead of hanging.
+
 The expert computation itself (``expert_fn``) receives the local rows grouped expert-major with device
 segment offsets ``row_off_local`` [El+1], exactly what the grouped MFMA GEMM (K6g) consumes.  Rows past
 ``row_off_local[-1]`` are padding and are never read back.
