@@ -38,8 +38,9 @@ variables configure the local engine:
                     own GPU, requests run concurrently and each combines its voters with one all-gather
                     (C2, score/sharded.py)
   LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
-                    and batches of at least N run as one vote_tally launch (K10b) on this process's GPU
-                    (default 0: the host C++ tally per request)
+                    and batches of at least N run as one vote_tally launch (K10b) on this process's GPU;
+                    0: the host C++ tally per request.  Default: 8 when a local engine runs in this
+                    process (it owns the GPU already), 0 otherwise (CPU, EngineGroup front end)
 """
 from __future__ import annotations
 

@@ -92,7 +92,13 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if cfg.device != "cpu":
         from ..score.tally_batch import make_batcher
 
-        score.tally_batcher = make_batcher(cfg.gpu_tally, f"cuda:{cfg.gpu}")
+        spec = cfg.gpu_tally
+        if spec is None and services and not cfg.gpus:
+            # an in-process engine already owns this process's GPU: tallies of requests that finish in the
+            # same event-loop turn go to the batched kernel when there are at least 8 of them (K10b); the
+            # EngineGroup front end (LWC_GPUS) keeps the host tally and opens no GPU context of its own
+            spec = "8"
+        score.tally_batcher = make_batcher(spec, f"cuda:{cfg.gpu}")
     state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                            archive),
                      embedders=embedders, services=services, archive=archive, registry=registry)
