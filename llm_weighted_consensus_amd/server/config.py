@@ -39,7 +39,7 @@ variables configure the local engine:
                     (C2, score/sharded.py)
   LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
                     and batches of at least N run as one vote_tally launch (K10b) on this process's GPU;
-                    0: the host C++ tally per request.  Default: 8 when a local engine runs in this
+                    0: the host C++ tally per request.  Default: 2 when a local engine runs in this
                     process (it owns the GPU already), 0 otherwise (CPU, EngineGroup front end)
 """
 from __future__ import annotations

@@ -95,9 +95,9 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
         spec = cfg.gpu_tally
         if spec is None and services and not cfg.gpus:
             # an in-process engine already owns this process's GPU: tallies of requests that finish in the
-            # same event-loop turn go to the batched kernel when there are at least 8 of them (K10b); the
+            # same event-loop turn go to the batched kernel when there are at least 2 of them (K10b); the
             # EngineGroup front end (LWC_GPUS) keeps the host tally and opens no GPU context of its own
-            spec = "8"
+            spec = "2"
         score.tally_batcher = make_batcher(spec, f"cuda:{cfg.gpu}")
     state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                            archive),
