@@ -151,3 +151,18 @@ def test_vote_tally_batcher_gpu(gpu):
         r = RT.tally(votes, wts, C)
         _same(t.choice_weight, r.choice_weight)
         _same(t.voter_confidence, r.voter_confidence)
+
+
+def test_server_wiring(monkeypatch):
+    """LWC_GPU_TALLY reaches the score client; with no local engine and no setting the host tally stays
+    (no GPU context is opened by the front end); a CPU deployment never batches."""
+    from llm_weighted_consensus_amd.server.config import Config
+    from llm_weighted_consensus_amd.server.main import build_state
+
+    monkeypatch.setenv("LWC_GPU_TALLY", "4")
+    cfg = Config.from_env(dotenv=False)
+    assert cfg.gpu_tally == "4"
+    st = build_state(cfg)
+    assert st.score.tally_batcher is not None and st.score.tally_batcher.min_batch == 4
+    assert build_state(Config()).score.tally_batcher is None
+    assert build_state(Config(device="cpu", gpu_tally="4")).score.tally_batcher is None
