@@ -29,6 +29,7 @@ import os
 import random
 import threading
 import time
+from array import array
 from collections import deque
 from dataclasses import dataclass
 from typing import Callable, Deque, Dict, List, Optional, Sequence as Seq, Tuple
@@ -67,7 +68,9 @@ class Sequence:
         self.index = index
         self.seed = seed
         self.n_launched = 0  # tokens sampled or in flight (the Philox offset of the next sample)
-        self.tokens: List[int] = []
+        # generated ids as a flat int32 array: the encoders pack thousands of them with one zero-copy view
+        # per sequence (models/packing.py) instead of converting Python ints
+        self.tokens = array("i")
         self._text: Optional[str] = None  # streamed text (callback / stop strings), else decoded on demand
         self.finished = False
         self.finish_reason: Optional[str] = None

@@ -20,18 +20,17 @@ GPU whose kernels failed to load.
 """
 from __future__ import annotations
 
-import itertools
 import math
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
-import numpy as np
 import torch
 import torch.nn.functional as F
 
 from .. import ops
 from ..ops import gemm_plan
 from .config import EncoderConfig
+from .packing import pack_ids
 
 POOL_MODES = {"cls": ops.POOL_CLS, "mean": ops.POOL_MEAN, "last": ops.POOL_LAST}
 
@@ -174,26 +173,12 @@ class BertEncoder:
         return out
 
     def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
-        """Varlen packing (ids folded into the vocab, truncated at max_tokens, empty -> [0]) with numpy:
-        thousands of candidates per consensus batch must not cost per-token Python work."""
+        """Varlen packing (ids folded into the vocab, truncated at max_tokens, empty -> [0]) with numpy
+        (models/packing.py): thousands of candidates per consensus batch must not cost per-token Python work."""
         cap = min(max_tokens or self.cfg.max_position, self.cfg.max_position)
-        V = self.cfg.vocab_size
-        lens = np.fromiter((max(1, min(len(tl), cap)) for tl in token_lists), dtype=np.int64, count=len(token_lists))
-        cu = np.zeros(len(lens) + 1, dtype=np.int64)
-        np.cumsum(lens, out=cu[1:])
-        n0 = int(lens[0]) if len(lens) else 0
-        if len(lens) and (lens == n0).all() and all(len(tl) >= n0 for tl in token_lists):
-            # one flat iterator straight into the array (half the host time of a nested-list asarray: the
-            # bench packs 4096 x 128 ids here while the GPU waits for the encoder's first kernel)
-            rows = token_lists if all(len(tl) == n0 for tl in token_lists) else (tl[:n0] for tl in token_lists)
-            ids = np.fromiter(itertools.chain.from_iterable(rows), dtype=np.int64, count=n0 * len(lens))
-        else:
-            ids = np.concatenate([np.asarray(list(tl)[:cap] or [0], dtype=np.int64) for tl in token_lists])
-        ids %= V
-        pos = np.arange(int(cu[-1]), dtype=np.int64) - np.repeat(cu[:-1], lens)
+        ids, pos, cu, max_len = pack_ids(token_lists, cap, self.cfg.vocab_size)
         dev = self.device
-        return (torch.from_numpy(ids.astype(np.int32)).to(dev), torch.from_numpy(pos.astype(np.int32)).to(dev),
-                torch.from_numpy(cu.astype(np.int32)).to(dev), int(lens.max()))
+        return (torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev), torch.from_numpy(cu).to(dev), max_len)
 
     def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
         """Embed sequences (token ids in this encoder's vocab; ids are folded into range) ->

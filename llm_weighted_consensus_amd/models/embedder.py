@@ -14,6 +14,7 @@ import torch
 
 from .. import ops
 from .config import DecoderConfig
+from .packing import pack_ids
 
 
 class DecoderEmbedder:
@@ -27,18 +28,12 @@ class DecoderEmbedder:
                                          "hidden": cfg.hidden, "pooling": "last", "name": cfg.name})()
 
     def pack(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
+        """Varlen packing keeping each sequence's END (the last token is pooled), numpy-vectorised
+        (models/packing.py)."""
         cap = min(max_tokens or self.max_tokens, self.max_tokens)
-        V = self.cfg.vocab_size
-        ids, pos, cu = [], [], [0]
-        for tl in token_lists:
-            tl = [int(t) % V for t in list(tl)[-cap:]] or [0]  # keep the END: the last token is pooled
-            ids.extend(tl)
-            pos.extend(range(len(tl)))
-            cu.append(cu[-1] + len(tl))
+        ids, pos, cu, max_len = pack_ids(token_lists, cap, self.cfg.vocab_size, tail=True)
         dev = self.device
-        max_len = max(cu[i + 1] - cu[i] for i in range(len(cu) - 1))
-        return (torch.tensor(ids, dtype=torch.int32, device=dev), torch.tensor(pos, dtype=torch.int32, device=dev),
-                torch.tensor(cu, dtype=torch.int32, device=dev), max_len)
+        return (torch.from_numpy(ids).to(dev), torch.from_numpy(pos).to(dev), torch.from_numpy(cu).to(dev), max_len)
 
     def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
         """-> (unit f32 [n, d], unit bf16 [n, d])"""
