@@ -92,20 +92,23 @@ class TallyBatcher:
         self.gpu_batches = 0  # launches so far (observability / tests)
         self.gpu_tallies = 0
         self._stream = None  # created on the first GPU batch (a non-blocking side stream)
+        self._sched_loop = None
 
     async def tally(self, voter_choices, C_len: int):
         votes, wts = vote_rows(voter_choices)
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         self._pending.append((votes, wts, C_len, fut))
-        if not self._scheduled:
-            self._scheduled = True
+        if not self._scheduled or self._sched_loop is not loop:
+            # (a flush scheduled on a loop that has since closed never runs: schedule on this one)
+            self._scheduled, self._sched_loop = True, loop
             loop.call_soon(self._flush)
         return await fut
 
     def _flush(self) -> None:
         batch, self._pending, self._scheduled = self._pending, [], False
-        live = [b for b in batch if not b[3].cancelled()]
+        # skip cancelled futures and those of an event loop that has closed (nobody can await them)
+        live = [b for b in batch if not b[3].done() and not b[3].get_loop().is_closed()]
         if not live:
             return
         if self.device is not None and len(live) >= self.min_batch:

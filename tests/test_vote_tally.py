@@ -113,6 +113,26 @@ def test_batcher_device_error_falls_back_to_host(monkeypatch):
         _same(t.choice_weight, RT.tally(votes, wts, C).choice_weight)
 
 
+def test_batcher_survives_a_closed_loop():
+    """A flush left scheduled on an event loop that closed (server restart, a test's asyncio.run) must not
+    wedge the batcher: the next loop schedules its own."""
+    rng = random.Random(5)
+    b = TB.TallyBatcher(device=None, min_batch=1)
+    loop = asyncio.new_event_loop()
+    fut = loop.create_future()
+    b._pending.append(([], [], 2, fut))
+    b._scheduled, b._sched_loop = True, loop  # as if tally() ran there and the loop closed before flushing
+    loop.close()
+    ch = _request(rng, 3, 4)
+
+    async def main():
+        return await asyncio.wait_for(b.tally(ch, 3), 5)
+
+    t = asyncio.run(main())
+    votes, wts = TB.vote_rows(ch)
+    _same(t.choice_weight, RT.tally(votes, wts, 3).choice_weight)
+
+
 def test_make_batcher_spec():
     assert TB.make_batcher(None, "cuda:0") is None
     assert TB.make_batcher("0", "cuda:0") is None
