@@ -107,9 +107,12 @@ class ExpertParallel:
             self._a2a(rscale, ssend)
         # received chunk s holds its rows for my experts 0..El-1 back to back; regroup expert-major
         dest, rvalid, row_off_local = self._expert_major(rcnt, C)
-        a_rows = torch.zeros(W * C, dtype=torch.int64, device=dev)
+        # a_rows[dest[i]] = i for every valid received row, as a scatter with the invalid rows sent to a
+        # spare slot (boolean-mask indexing would size its result on the host: no hipGraph capture)
         flat = torch.arange(W * C, device=dev)
-        a_rows[dest[rvalid]] = flat[rvalid]
+        a_rows = torch.zeros(W * C + 1, dtype=torch.int64, device=dev)
+        a_rows.scatter_(0, torch.where(rvalid, dest, torch.full_like(dest, W * C)), flat)
+        a_rows = a_rows[:W * C]
         x_local = recv[a_rows]
         s_local = rscale[a_rows] if rscale is not None else None
         y_local = expert_fn(x_local, row_off_local, s_local)                  # [W*C, d_out] expert-major

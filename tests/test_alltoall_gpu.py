@@ -189,3 +189,71 @@ def test_mixtral_ep2_through_ipc_alltoall(gpu, fp8):
         ref = _prefill_logits(m, gpu, P=23 + 9 * r, seed=r)
         c = torch.nn.functional.cosine_similarity(res[r], ref, dim=0).item()
         assert c > 0.999, (r, c)
+
+
+def _ep_prompts(rank):
+    g = torch.Generator().manual_seed(300 + rank)
+    return [torch.randint(0, 4000, (19,), generator=g).tolist() for _ in range(3)]  # same shapes on every rank
+
+
+def _run_engine(model, prompts, dev):
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+
+    cfg = model.cfg
+    eng = LLMEngine(model, ByteTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id), max_batch=8,
+                    max_model_len=256, kv_memory_fraction=0.04, use_graphs=model.graph_safe, cascade_min_batch=1 << 30)
+    groups = [eng.add_request(p, SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True), n=1) for p in prompts]
+    while eng.has_work():
+        eng.step()
+    return [list(g.seqs[0].tokens) for g in groups]
+
+
+def _ep_engine_worker(rank, world, port, q):
+    _env(rank, world, port)
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CustomAllToAll
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        comm = CustomAllToAll(device=dev, max_bytes=4 << 20, blocks=16, spin_ms=5000)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, ep_rank=rank,
+                         ep_size=world, ep_mode="padded", ep_capacity=128, ep_comm=comm)
+        assert m.graph_safe
+        toks = _run_engine(m, _ep_prompts(rank), dev)
+        torch.cuda.synchronize(dev)
+        comm.check()
+        pdist.barrier()
+        comm.close()
+        q.put((rank, toks))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ep2_engine_decode_graphs_match_ep1(gpu):
+    """Two expert-parallel engines (mixtral-tiny, 2 of 4 experts each, different prompts of the same shapes)
+    step in lockstep with their decode steps captured in hipGraphs — the IPC all-to-alls inside the graphs —
+    finish without a peer timeout, and generate greedily what a single-rank engine with every expert generates
+    for the same prompts.  (Token for token up to bf16 near-ties: the grouped expert GEMM splits K by batch
+    size, so the EP ranks' rounding can differ in the last bit and flip an argmax between two logits one ulp
+    apart; the agreement bound catches a broken exchange, which yields unrelated tokens.)"""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+    res = _run(2, _ep_engine_worker, timeout=600)
+    assert all(isinstance(v, list) for v in res.values()), res
+    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512)
+    same = total = 0
+    for r in range(2):
+        ref = _run_engine(m, _ep_prompts(r), gpu)
+        assert [len(t) for t in res[r]] == [len(t) for t in ref] == [10] * 3
+        for a, b in zip(res[r], ref):
+            n = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), len(a))  # agreeing prefix
+            same += n
+            total += len(a)
+    assert same >= 0.7 * total, (same, total, res)
