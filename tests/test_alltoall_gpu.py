@@ -235,6 +235,21 @@ def _ep_engine_worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
+def _ep1_engine_worker(rank, world, port, q):
+    """The single-rank reference, in its own process too: the engine's graphs and KV pool stay out of the
+    test runner's allocator (later kernel tests keep the memory layout they always had)."""
+    _env(rank, world, port)
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+
+        dev = torch.device("cuda", 0)
+        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512)
+        q.put((rank, [_run_engine(m, _ep_prompts(r), dev) for r in range(2)]))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
 def test_ep2_engine_decode_graphs_match_ep1(gpu):
     """Two expert-parallel engines (mixtral-tiny, 2 of 4 experts each, different prompts of the same shapes)
     step in lockstep with their decode steps captured in hipGraphs — the IPC all-to-alls inside the graphs —
@@ -242,15 +257,13 @@ def test_ep2_engine_decode_graphs_match_ep1(gpu):
     for the same prompts.  (Token for token up to bf16 near-ties: the grouped expert GEMM splits K by batch
     size, so the EP ranks' rounding can differ in the last bit and flip an argmax between two logits one ulp
     apart; the agreement bound catches a broken exchange, which yields unrelated tokens.)"""
-    from llm_weighted_consensus_amd.models.config import decoder_config
-    from llm_weighted_consensus_amd.models.mixtral import MixtralModel
-
     res = _run(2, _ep_engine_worker, timeout=600)
     assert all(isinstance(v, list) for v in res.values()), res
-    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512)
+    refs = _run(1, _ep1_engine_worker, timeout=600)[0]
+    assert isinstance(refs, list), refs
     same = total = 0
     for r in range(2):
-        ref = _run_engine(m, _ep_prompts(r), gpu)
+        ref = refs[r]
         assert [len(t) for t in res[r]] == [len(t) for t in ref] == [10] * 3
         for a, b in zip(res[r], ref):
             n = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), len(a))  # agreeing prefix
