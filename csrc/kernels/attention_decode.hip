@@ -220,7 +220,10 @@ template <bool PREFIX>
 LWC_DEVICE void load_q(short8 (&qf)[4], const DecodeParams& p, int row_seq0, int nrows, int kvh, int r16, int g) {
   const bool valid = r16 < nrows;
   const int rr = valid ? r16 : 0;
-  const int seq = PREFIX ? row_seq0 + rr / p.G : row_seq0;
+  // lanes past the wave's rows read sequence 0 (then zeroed): in the cascade kernel a wave of a short
+  // super-tile can own no sequence at all, and row_seq0 then lies past the batch — reading q there went
+  // out of bounds (it faulted only when q ended a mapped region)
+  const int seq = !valid ? 0 : (PREFIX ? row_seq0 + rr / p.G : row_seq0);
   const int hq = kvh * p.G + (PREFIX ? rr % p.G : rr);
   const bf16_t* qh = p.q + (size_t)seq * p.q_stride + (size_t)hq * kD;
 #pragma unroll
