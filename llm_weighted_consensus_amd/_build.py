@@ -95,7 +95,20 @@ def build_kernels(jobs: int = 8, force: bool = False) -> Path:
     if force or _stale(KERNELS_SO, objs):
         _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(KERNELS_SO),
               *tlibs])
+        _check_kernel_stubs(KERNELS_SO)
     return KERNELS_SO
+
+
+def _check_kernel_stubs(so: Path) -> None:
+    """Fail the build when a kernel's host-side launch stub is missing from the shared object: hipcc can drop
+    a template kernel's host instantiation without a diagnostic (seen for a lambda naming a member of a
+    dependent type inside the kernel), and the module would then fail to load only on the GPU box."""
+    r = subprocess.run(["nm", "-u", "-C", str(so)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    missing = [ln.split(None, 1)[-1] for ln in r.stdout.splitlines() if "lwc::" in ln]
+    if missing:
+        so.unlink()
+        raise RuntimeError("kernel extension has undefined symbols of its own (host stubs not emitted):\n  "
+                           + "\n  ".join(missing[:20]))
 
 
 def build_runtime(jobs: int = 8, force: bool = False) -> Path:

@@ -6,6 +6,7 @@ handling (src/score/completions/client.rs:711-906) can be exercised without a GP
 """
 from __future__ import annotations
 
+import asyncio
 import re
 import time
 import uuid
@@ -44,9 +45,11 @@ def select_keys(request: C.ChatCompletionCreateParams) -> List[Tuple[str, str]]:
 
 
 class FakeChatClient(ChatClient):
-    def __init__(self, policy: Callable[[C.ChatCompletionCreateParams], Sequence], chunk_chars: int = 3):
+    def __init__(self, policy: Callable[[C.ChatCompletionCreateParams], Sequence], chunk_chars: int = 3,
+                 delay_s: float = 0.0):
         self.policy = policy
         self.chunk_chars = chunk_chars
+        self.delay_s = delay_s  # pause before every chunk (slow voters for the failure-isolation tests)
         self.requests: List[C.ChatCompletionCreateParams] = []
 
     async def create_streaming(self, ctx, request: C.ChatCompletionCreateParams):
@@ -81,6 +84,8 @@ class FakeChatClient(ChatClient):
                 pieces.append((i, t, alts))
         emitted = 0
         for i, t, alts in pieces:
+            if self.delay_s:
+                await asyncio.sleep(self.delay_s)
             sc = choices[i]
             d = C.Delta(role="assistant")
             if sc.tool_call:

@@ -1044,9 +1044,7 @@ class LLMEngine:
         if copies:
             self.cache.copy_blocks(_h2d(copies, torch.int32, dev))
         self._ensure_graph(bk, st["cascade"])
-        arm = getattr(self.model, "comm_arm", None)
-        if arm is not None:
-            arm()  # TP: error word of this step's all-reduces -> pinned host memory, read one step later
+        self._comm_arm()  # TP: error word of this step's all-reduces -> pinned host memory, read one step later
         step = _Step(seqs, key, bk, parity, st["K"], None, None, None)
         step.static = st
         self.stats["decode_tokens"] += B
@@ -1122,9 +1120,7 @@ class LLMEngine:
 
     def _process(self, st: _Step) -> List[TokenEvent]:
         st.event.synchronize()
-        poll = getattr(self.model, "comm_poll", None)
-        if poll is not None:
-            poll()  # a TP peer that never arrived: CommFailure fails the in-flight groups (EngineService)
+        self._comm_poll()  # a TP peer that never arrived: CommFailure fails the in-flight groups (EngineService)
         if st.first is not None:  # first tokens after a prefill (:meth:`_launch_first`)
             host, groups = st.first
             lists = [h.tolist() for h in host]
@@ -1242,8 +1238,24 @@ class LLMEngine:
     def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> List[TokenEvent]:
         """Synchronous sampling (first token after prefill)."""
         tok, lp, tk_ids, tk_lp, K = self._sample_first(logits, seqs)
-        return self._advance(seqs, tok.cpu().tolist(), lp.cpu().tolist(),
-                             tk_ids.cpu().tolist() if K else None, tk_lp.cpu().tolist() if K else None)
+        self._comm_arm()
+        host = [t.cpu().tolist() for t in ((tok, lp, tk_ids, tk_lp) if K else (tok, lp))]
+        self._comm_poll()  # the .cpu() reads synchronised the stream: the armed error word is on the host
+        return self._advance(seqs, host[0], host[1], host[2] if K else None, host[3] if K else None)
+
+    def _comm_arm(self) -> None:
+        """TP / EP models: queue the readback of the collectives' error word behind the work launched so far.
+        Every step whose tokens reach the host is armed (decode replays, mixed chunked-prefill steps,
+        prefills): :meth:`_process` polls it before advancing that step's tokens, so tokens sampled from a
+        forward whose all-reduce was poisoned by a missing peer are never delivered."""
+        arm = getattr(self.model, "comm_arm", None)
+        if arm is not None:
+            arm()
+
+    def _comm_poll(self) -> None:
+        poll = getattr(self.model, "comm_poll", None)
+        if poll is not None:
+            poll()
 
     def _launch_first(self, logits: torch.Tensor, seqs: List[Sequence], groups: List[SequenceGroup]) -> _Step:
         """Asynchronous first-token sampling after a prefill: the sampler and the copy of its outputs
@@ -1255,6 +1267,7 @@ class LLMEngine:
                                                                                (tok, lp))]
         for h, t in zip(host, (tok, lp, tk_ids, tk_lp)):
             h.copy_(t, non_blocking=True)
+        self._comm_arm()  # the prefill / mixed forward's collectives: checked by _process before these tokens
         ev = torch.cuda.Event()
         ev.record()
         st = _Step(seqs, None, None, 0, K, tok, None, ev)

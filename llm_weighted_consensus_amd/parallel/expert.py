@@ -98,6 +98,7 @@ class ExpertParallel:
         cnt = (ro[1:] - ro[:-1]).view(W, El)
         rcnt = torch.empty_like(cnt)
         self._a2a(rcnt, cnt)                                     # [W src, El]
+        rcnt = self._sane_counts(rcnt, C)
         recv = torch.empty_like(send)
         self._a2a(recv, send)
         rscale = None
@@ -124,6 +125,15 @@ class ExpertParallel:
         e = torch.searchsorted(ro[1:], p, right=True)
         r = e // El
         return ret[r * C + (p - base[r])]
+
+    @staticmethod
+    def _sane_counts(rcnt: torch.Tensor, C: int) -> torch.Tensor:
+        """Received per-(source, expert) counts with every chunk that cannot be real zeroed: a peer that never
+        arrives makes the IPC all-to-all fill its chunk with all-ones bytes (-1 as int64), and a negative or
+        over-capacity count would turn into out-of-range scatter / gather indices and grouped-GEMM segments
+        (a device fault instead of the documented NaN + CommFailure).  On the device, graph-capturable."""
+        bad = (rcnt < 0).any(1, keepdim=True) | (rcnt.sum(1, keepdim=True) > C)
+        return torch.where(bad, torch.zeros((), dtype=rcnt.dtype, device=rcnt.device), rcnt)
 
     def _expert_major(self, rcnt: torch.Tensor, C: int):
         """rcnt [W src, El] -> (dest [W*C]: expert-major position of received row (s, i); valid [W*C];

@@ -270,10 +270,9 @@ class ScoreClient:
         q: asyncio.Queue = asyncio.Queue()
         DONE = object()
 
-        async def run_voter(llm: Llm, seed: int):
+        async def pump(source):
             try:
-                async for chunk in self._voter_stream(ctx, rid, created, indexer, llm, weights[llm.index], request,
-                                                      seed):
+                async for chunk in source:
                     await q.put(chunk)
             finally:
                 await q.put(DONE)
@@ -281,11 +280,10 @@ class ScoreClient:
         # key-tree seeds for every voter in model order (whichever of them this client runs), so a
         # voter's prompt does not depend on how the voters are sharded
         seeds = self._voter_seeds(ctx, model)
-        tasks = [asyncio.create_task(run_voter(l, seeds[j])) for j, l in enumerate(model.llms)
-                 if self.voter_filter is None or self.voter_filter(l)]
+        sources = self._voter_sources(ctx, rid, created, indexer, model, weights, request, seeds)
+        tasks = [asyncio.create_task(pump(src)) for src in sources]
         pending = len(tasks)
         first = True
-        voter_usage = C.Usage()  # this client's voters only (the voter-sharded merge sums it over ranks)
         try:
             while pending:
                 item = await q.get()
@@ -300,7 +298,6 @@ class ScoreClient:
                     md = ch.completion_metadata
                     if md is not None and md.usage is not None:
                         usage.push(md.usage)
-                        voter_usage.push(md.usage)
                         md.usage = None
                 yield item
         finally:
@@ -316,14 +313,12 @@ class ScoreClient:
                 any_ok = True
                 break
             codes.append(ch.error.code)
-        tally, all_error, codes = await self._combine(ctx, aggregate, C_len, any_ok, codes, usage, voter_usage)
-        voter_choices = aggregate.choices[C_len:]  # (a voter-sharded combine adds the other ranks' voters)
+        tally = await self._tally(voter_choices, C_len)
+        all_error = not any_ok
         self._record_training(model, weight_data, voter_choices, tally)  # before the deltas are cleared
         aggregate.weight_data = weight_data
         usage.with_total_cost()
         aggregate.usage = usage
-        # choices first seen in this final chunk (another rank's voters, voter-sharded) keep their content
-        whole = ctx.get("whole", ()) if isinstance(ctx, dict) else ()
         for j, ch in enumerate(aggregate.choices):
             if ch.index < C_len:
                 ch.weight = tally.choice_weight[ch.index]
@@ -331,8 +326,6 @@ class ScoreClient:
             elif ch.delta.vote is not None:
                 vc = tally.voter_confidence[j - C_len]
                 ch.confidence = vc if ch.confidence is None else ch.confidence + vc
-            if ch.index in whole:
-                continue
             ch.delta = S.ScoreDelta()
             ch.finish_reason = None
             ch.logprobs = None
@@ -341,6 +334,13 @@ class ScoreClient:
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+
+    def _voter_sources(self, ctx, rid, created, indexer, model: Model, weights, request, seeds) -> list:
+        """The request's voter chunk streams, merged by arrival order (the reference's ``select_all``,
+        client.rs:342-356): one per voter this client runs.  The voter-sharded leader adds one stream per
+        follower rank carrying that rank's voters live (score/sharded.py)."""
+        return [self._voter_stream(ctx, rid, created, indexer, l, weights[l.index], request, seeds[j])
+                for j, l in enumerate(model.llms) if self.voter_filter is None or self.voter_filter(l)]
 
     def _voter_seeds(self, ctx, model: Model) -> List[int]:
         """One key-tree seed per voter, in model order.  A request context carrying ``seed`` (the
@@ -355,12 +355,6 @@ class ScoreClient:
     def _new_ids(self, ctx=None):
         created = int(time.time())
         return created, response_id(created)
-
-    async def _combine(self, ctx, aggregate: S.ScoreCompletionChunk, C_len: int, any_ok: bool, codes, usage,
-                       voter_usage):
-        """Tally the aggregate's voters: (tally, all votes failed, error codes to unify).  ``usage`` is
-        the request's running total, ``voter_usage`` this client's voters' share of it."""
-        return await self._tally(aggregate.choices[C_len:], C_len), not any_ok, codes
 
     async def _tally(self, voter_choices, C_len: int):
         if self.tally_batcher is not None:

@@ -1,367 +1,466 @@
-"""Voter-sharded scoring: one score request's voters spread over the ranks of a process group (C2).
+"""Voter-sharded serving: one score request's voters spread over the ranks of a node (C2), with the
+reference's per-voter failure isolation and live streaming of every voter.
 
-The reference fans a request's voters out as concurrent upstream streams and tallies their votes in one
-place (src/score/completions/client.rs:343-356 fan-out, :384-455 tally).  Here every rank runs the SAME
-requests (SPMD) through the ordinary ``ScoreClient`` but only for the voters it owns
-(``llm.index % world == rank``: the voters whose models its GPU serves), and requests run CONCURRENTLY
-on every rank, as on a single server.
+The reference fans a request's voters out as concurrent upstream streams, yields every voter chunk as it
+arrives (src/score/completions/client.rs:342-382, ``select_all``), turns a failed voter into an error choice
+rather than a failed request (:711-783, 798-813) and fails the request only when every voter failed
+(:385-409, 458-463).  Here the voters run on the GPUs of the node:
 
-C2 is ONE collective per request: when a request's local voters are done, each rank contributes its
-voter choices (votes, weights, errors, content) to an object all-gather; every rank then holds every
-voter of the request (its own under the indices it already streamed, the others' after them by voter
-index), runs the native tally over all of them and finishes the request — rank 0's response is the full
-one.  Collectives of concurrent requests must be issued in
-the same order on every rank, so they go through a per-rank combiner thread that runs them strictly in
-request sequence order (the leader numbers requests as it broadcasts them); a request that fails before
-its combine still takes its slot (an empty contribution), so the ranks never fall out of step.
+* rank 0 (the **leader**) serves HTTP.  For each score request it does everything the reference does before
+  the fan-out — model validation, archive references, choice texts, weights — once, then assigns every
+  voter to a live rank (voter ``i`` -> ``live[i % len(live)]``) and sends each follower its share with the
+  resolved request, the weights and the key-tree seeds (parallel/shard_link.py: one TCP link per follower,
+  no collective);
+* a **follower** runs its voters' streams on its own engine and sends every chunk back the moment it is
+  produced, tagged with its voter (index ``C + voter * 4096 + native choice index``);
+* the leader merges its own voters and every follower's chunks into ONE stream in arrival order (remote
+  voters are streamed live, not delivered whole at the end), re-indexed through the request's
+  ``ChoiceIndexer`` exactly like local ones, and runs the tally alone.
 
-Requests and their ids reach the followers over a second process group (control), so broadcasts and
-combines never interleave on one group.  Both groups are gloo: the payloads are small Python objects.
+Failure isolation: when a follower dies (its socket closes, or its heartbeat stops for ``LWC_SHARD_DEAD_S``)
+or a request's share outlives its bound (the request deadline plus ``LWC_SHARD_GRACE_S``, else
+``LWC_SHARD_WAIT_S``), every voter of that share that had not finished becomes an error choice
+(``finish_reason: "error"``, error ``voter_shard_lost``) — a partially streamed voter keeps its index, one that
+never started gets one — and the request completes with the other voters (AllVotesFailed only when all of
+them failed).  A dead rank gets no share of later requests: they run on the survivors.
+
+/consensus/completions: candidates [first, first + n) of a request are sampled by the rank owning that slice
+(each with the seed it has in the whole request) and embedded on its GPU; the unit rows travel back over the
+link.  The slice of a follower that dies (or times out) is recomputed by the leader — same seeds, same
+candidates — so the request still completes.
 """
 from __future__ import annotations
 
 import asyncio
+import copy
+import os
 import threading
-from typing import Any, List
+import time
+from typing import Any, Dict, List, Optional
 
-import torch.distributed as dist
+import numpy as np
 
-from ..errors import ScoreError
-from ..parallel import votes as V
+from ..errors import ChatError, ResponseError, ScoreError, StatusError
+from ..parallel.shard_link import LinkClient, LinkServer
 from ..schema import chat as C
 from ..schema import score as S
-from .orchestrator import ScoreClient
+from .orchestrator import ChoiceIndexer, ScoreClient
 
-_SKIP = None  # a request's empty contribution (it failed before its combine on this rank)
-
-
-class _Combiner:
-    """Runs each request's all-gather in sequence order on a thread of its own."""
-
-    def __init__(self, group):
-        self.group = group
-        self.cv = threading.Condition()
-        self.pending = {}
-        self.next = 0
-        self.closed = False
-        self.thread = threading.Thread(target=self._run, name="c2-combiner", daemon=True)
-        self.thread.start()
-
-    async def submit(self, seq: int, payload: Any) -> List[Any]:
-        loop = asyncio.get_running_loop()
-        fut = loop.create_future()
-        with self.cv:
-            self.pending[seq] = (payload, loop, fut)
-            self.cv.notify()
-        return await fut
-
-    def _run(self) -> None:
-        while True:
-            with self.cv:
-                while self.next not in self.pending and not self.closed:
-                    self.cv.wait()
-                if self.next not in self.pending:
-                    return
-                payload, loop, fut = self.pending.pop(self.next)
-                self.next += 1
-            try:
-                # a callable runs its own collectives (consensus: object + tensor all-gathers), else one
-                # object all-gather of the payload
-                res = payload() if callable(payload) else V.gather_objects(payload, self.group)
-                loop.call_soon_threadsafe(_resolve, fut, res, None)
-            except BaseException as e:  # noqa: BLE001 — handed to the awaiting request
-                loop.call_soon_threadsafe(_resolve, fut, None, e)
-
-    def close(self) -> None:
-        with self.cv:
-            self.closed = True
-            self.cv.notify()
-        self.thread.join(timeout=60)
+_NATIVE = 1 << 12  # a follower tags choice (voter v, native index k) as C + v * _NATIVE + k
 
 
-def _resolve(fut, res, err) -> None:
-    if fut.done():
-        return
-    if err is not None:
-        fut.set_exception(err)
-    else:
-        fut.set_result(res)
+def _lost(rank: int, why: str) -> ChatError:
+    return ChatError(500, {"kind": "voter_shard_lost", "error": f"rank {rank}: {why}"})
+
+
+class _TagIndexer:
+    """A follower's indexer: the leader decodes (voter, native choice) from the index it assigns."""
+
+    def __init__(self, C_len: int):
+        self.C = C_len
+
+    def get(self, llm_index: int, native: int) -> int:
+        if not 0 <= native < _NATIVE:
+            raise ValueError(f"native choice index {native} out of range")
+        return self.C + llm_index * _NATIVE + native
+
+
+class _Share:
+    """One request's work on the followers, as the leader tracks it: link messages arrive on ``q`` (put from
+    link threads through the request's loop)."""
+
+    def __init__(self, loop, ranks):
+        self.loop = loop
+        self.q: asyncio.Queue = asyncio.Queue()
+        self.ranks = set(ranks)
+
+    def post(self, item) -> None:
+        try:
+            self.loop.call_soon_threadsafe(self.q.put_nowait, item)
+        except RuntimeError:  # the request's loop is gone (request abandoned): nothing waits
+            pass
+
+
+class _LinkHub:
+    """Routes the followers' messages to the request waiting on them (by request number) and reports a
+    dead follower to every request that still expects something from it."""
+
+    def __init__(self, link: LinkServer):
+        self.link = link
+        self.shares: Dict[int, _Share] = {}
+        self.lock = threading.Lock()
+        link.on_message = self._on_message
+        link.on_dead = self._on_dead
+
+    def open(self, seq: int, ranks) -> _Share:
+        sh = _Share(asyncio.get_running_loop(), ranks)
+        with self.lock:
+            self.shares[seq] = sh
+        return sh
+
+    def close(self, seq: int) -> None:
+        with self.lock:
+            self.shares.pop(seq, None)
+
+    def _on_message(self, rank: int, msg) -> None:
+        kind, seq = msg[0], msg[1]
+        with self.lock:
+            sh = self.shares.get(seq)
+        if sh is not None:
+            sh.post((kind, rank) + tuple(msg[2:]))
+
+    def _on_dead(self, rank: int) -> None:
+        with self.lock:
+            shares = [sh for sh in self.shares.values() if rank in sh.ranks]
+        for sh in shares:
+            sh.post(("dead", rank))
+
+
+def _bound(ctx) -> float:
+    """Seconds a request waits for its followers: its deadline plus a grace, else LWC_SHARD_WAIT_S."""
+    dl = ctx.get("deadline") if isinstance(ctx, dict) else None
+    if dl is not None:
+        return max(0.0, dl - time.monotonic()) + float(os.environ.get("LWC_SHARD_GRACE_S", "5"))
+    return float(os.environ.get("LWC_SHARD_WAIT_S", "300"))
 
 
 class ShardedScoreClient(ScoreClient):
-    """``ctx`` of every request is ``{"seq": n, "ids": (created, id)}`` (from :class:`ScoreLeader` /
-    :func:`follow`, or given by the caller, identical on every rank)."""
+    """Rank 0's score client in a voter-sharded deployment (see the module docstring)."""
 
-    def __init__(self, chat_client, group=None, **kw):
+    def __init__(self, chat_client, link: LinkServer, world: int, **kw):
         super().__init__(chat_client, **kw)
-        self.group = group if group is not None else dist.new_group(backend="gloo")
-        self.world = dist.get_world_size(self.group)
-        self.rank = dist.get_rank(self.group)
-        self.voter_filter = lambda llm: llm.index % self.world == self.rank
-        # one key-tree seed base on every rank (rank 0's); each request's voter seeds derive from (base,
-        # request number) — not from draws in arrival order, which concurrent requests make rank-dependent
-        self.seed_base = int(V.broadcast_object(
-            self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"], 0, self.group))
+        self.link, self.world = link, world
+        self.hub = _LinkHub(link)
+        self.seed_base = int(self.rng.getrandbits(63) if kw.get("rng_seed") is None else kw["rng_seed"])
         self.rng.seed(self.seed_base)
-        self.combiner = _Combiner(self.group)
-        # C1 (consensus): candidate embedding rows all-gathered as device tensors on the world's backend
-        # (RCCL over xGMI on a GPU node; gloo — host tensors — for CPU worlds and one-GPU rehearsals)
-        self.data_group = dist.new_group()
-        self.data_backend = dist.get_backend(self.data_group)
+        self._seq = 0
+        self._seq_lock = threading.Lock()
+        self.consensus = None  # ShardedConsensusClient (shard_voters)
 
-    def request_ctx(self, seq: int, ids) -> dict:
-        """The per-request context every rank builds identically: sequence number (combine order), the
-        response ids, and the voters' key-tree seed base."""
-        return {"seq": seq, "ids": ids, "seed": (self.seed_base * 1000003 + seq) & ((1 << 63) - 1)}
+    # ------------------------------------------------------------------ request numbering
+    def next_seq(self) -> int:
+        with self._seq_lock:
+            s = self._seq
+            self._seq += 1
+        return s
+
+    def request_ctx(self, seq: int, ids=None, ctx=None) -> dict:
+        """The request's context: the caller's (deadline, trace id, ...) plus its number, response ids and
+        the voters' key-tree seed base (voter seeds depend on (seed base, request number) only, so a voter's
+        prompt does not depend on which rank runs it)."""
+        out = copy.copy(ctx) if isinstance(ctx, dict) else {}
+        out.update(seq=seq, ids=ids if ids is not None else ScoreClient._new_ids(self),
+                   seed=(self.seed_base * 1000003 + seq) & ((1 << 63) - 1))
+        return out
 
     def _new_ids(self, ctx=None):
         return tuple(ctx["ids"])
 
-    async def _combine(self, ctx, aggregate: S.ScoreCompletionChunk, C_len: int, any_ok: bool, codes, usage,
-                       voter_usage):
-        ctx["combined"] = True
-        mine = aggregate.choices[C_len:]
-        parts = await self.combiner.submit(ctx["seq"], (any_ok, list(codes), [c.to_obj() for c in mine],
-                                                        voter_usage.to_obj()))
-        remote, n_ok, all_codes = [], 0, []
-        for r, part in enumerate(parts):
-            if part is _SKIP:
-                continue
-            ok, cds, objs, u = part
-            n_ok += bool(ok)
-            all_codes += cds
-            if r != self.rank:
-                remote += [S.ScoreStreamChoice.model_validate(o) for o in objs]
-                usage.push(C.Usage.model_validate(u))  # the other ranks' voters (an embedding's usage: once)
-        # this rank's voters keep the indices its stream already used; the others' follow, by voter index
-        remote.sort(key=lambda c: (c.model_index if c.model_index is not None else -1, c.index))
-        for k, c in enumerate(remote):
-            c.index = C_len + len(mine) + k
-        ctx["whole"] = {c.index for c in remote}  # complete choices: the final chunk carries them as they are
-        aggregate.choices = aggregate.choices + remote
-        return await self._tally(aggregate.choices[C_len:], C_len), n_ok == 0, all_codes
+    async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams):
+        if not (isinstance(ctx, dict) and "seq" in ctx):
+            ctx = self.request_ctx(self.next_seq(), ctx=ctx)
+        return await super().create_streaming(ctx, request)
 
-    async def run(self, seq: int, ids, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
-        """One request on this rank (unary); always takes its combine slot."""
-        ctx = self.request_ctx(seq, ids)
+    async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
+        if not (isinstance(ctx, dict) and "seq" in ctx):
+            ctx = self.request_ctx(self.next_seq(), ctx=ctx)
+        return await super().create_unary(ctx, request)
+
+    # ------------------------------------------------------------------ fan-out over the ranks
+    def _voter_sources(self, ctx, rid, created, indexer, model, weights, request, seeds) -> list:
+        live = [0] + self.link.live()
+        owner = {l.index: live[l.index % len(live)] for l in model.llms}
+        mine = [l for l in model.llms if owner[l.index] == 0]
+        shares: Dict[int, List[int]] = {}
+        for l in model.llms:
+            if owner[l.index] != 0:
+                shares.setdefault(owner[l.index], []).append(l.index)
+        sources = []
+        seq = ctx["seq"]
+        if shares:
+            share = self.hub.open(seq, shares)
+            rem = (ctx["deadline"] - time.monotonic()) if ctx.get("deadline") is not None else None
+            base = {"rid": rid, "created": created, "model": model, "request": request, "weights": list(weights),
+                    "seeds": list(seeds), "remaining": rem, "trace_id": ctx.get("trace_id"),
+                    "priority": ctx.get("priority", 0)}
+            for rank, idx in list(shares.items()):
+                if not self.link.send(rank, ("score", seq, dict(base, llms=idx))):
+                    # the rank died before taking its share: its voters run here
+                    share.ranks.discard(rank)
+                    mine += [l for l in model.llms if l.index in set(idx)]
+                    del shares[rank]
+            if shares:
+                sources.append(self._remote(ctx, share, shares, indexer, model, weights, rid, created))
+            else:
+                self.hub.close(seq)
+        pos = {l.index: j for j, l in enumerate(model.llms)}
+        sources += [self._voter_stream(ctx, rid, created, indexer, l, weights[l.index], request, seeds[pos[l.index]])
+                    for l in mine]
+        return sources
+
+    async def _remote(self, ctx, share: _Share, shares: Dict[int, List[int]], indexer: ChoiceIndexer, model,
+                      weights, rid, created):
+        """The followers' voters of one request as one chunk stream: re-indexed, weights re-stamped from the
+        leader's (training-table weights learn here only), finished voters tracked so that a lost share
+        turns exactly its unfinished voters into error choices."""
+        llms = {l.index: l for l in model.llms}
+        seen: Dict[int, Dict[int, bool]] = {i: {} for idx in shares.values() for i in idx}  # voter -> native -> done
+        pending = set(shares)
+        deadline = time.monotonic() + _bound(ctx)
         try:
-            return await self.create_unary(ctx, request)
+            while pending:
+                try:
+                    msg = await asyncio.wait_for(share.q.get(), timeout=max(0.0, deadline - time.monotonic()))
+                except asyncio.TimeoutError:
+                    msg = ("timeout", None)
+                kind, rank = msg[0], msg[1]
+                if kind == "chunk":
+                    chunk = S.ScoreCompletionChunk.model_validate(msg[2])
+                    base_c = int(msg[3])
+                    for ch in chunk.choices:
+                        v, native = divmod(ch.index - base_c, _NATIVE)
+                        ch.index = indexer.get(v, native)
+                        ch.weight = weights[v] if ch.weight is not None else None
+                        done = seen.setdefault(v, {})
+                        done[native] = done.get(native, False) or ch.finish_reason is not None
+                    yield chunk
+                elif kind == "end":
+                    pending.discard(rank)
+                    err = msg[2] if len(msg) > 2 else None
+                    if err:
+                        for c in self._lost_chunks(rid, created, model.id, indexer, llms, weights, shares[rank], seen,
+                                                   _lost(rank, err)):
+                            yield c
+                elif kind in ("dead", "timeout"):
+                    ranks = [rank] if kind == "dead" else sorted(pending)
+                    for r in ranks:
+                        if r not in pending:
+                            continue
+                        pending.discard(r)
+                        why = "follower died" if kind == "dead" else "share timed out"
+                        for c in self._lost_chunks(rid, created, model.id, indexer, llms, weights, shares[r], seen,
+                                                   _lost(r, why)):
+                            yield c
         finally:
-            if not ctx.get("combined"):
-                await self.combiner.submit(seq, _SKIP)
+            self.hub.close(ctx["seq"])
+            if pending:  # the request was abandoned: tell the followers to drop the rest of its voters
+                for r in pending:
+                    self.link.send(r, ("cancel", ctx["seq"]))
 
-    async def open_stream(self, seq: int, ids, request: S.ScoreCompletionCreateParams):
-        """One request on this rank, streamed: pre-stream errors raise here (the HTTP layer turns them
-        into a status), then this rank's voter chunks are yielded as they arrive, and the final chunk
-        carries the other ranks' voters whole plus the tally (the unary fold of the stream equals
-        :meth:`run`).  The combine slot is always taken, also when the client abandons the stream."""
-        ctx = self.request_ctx(seq, ids)
-        try:
-            it = await self.create_streaming(ctx, request)
-        except BaseException:
-            await self.combiner.submit(seq, _SKIP)
-            raise
-
-        async def gen():
-            try:
-                async for item in it:
-                    yield item
-            finally:
-                if not ctx.get("combined"):
-                    await self.combiner.submit(seq, _SKIP)
-
-        return gen()
+    @staticmethod
+    def _lost_chunks(rid, created, model_id, indexer, llms, weights, voters, seen, err: StatusError):
+        """Error choices for the unfinished voters of a lost share: a voter that streamed part of its
+        output gets the error on the choices it started (as a mid-stream error, client.rs:798-813), one
+        that never started gets one error choice (as an error before the first chunk, client.rs:711-783)."""
+        re = ResponseError.from_status_error(err)
+        choices = []
+        for v in voters:
+            l = llms[v]
+            natives = seen.get(v) or {}
+            todo = [k for k, done in natives.items() if not done] if natives else [0]
+            for k in todo:
+                choices.append(S.ScoreStreamChoice(delta=S.ScoreDelta(), finish_reason="error",
+                                                   index=indexer.get(v, k), weight=weights[v], error=re,
+                                                   model=l.id, model_index=v))
+        if choices:
+            yield S.ScoreCompletionChunk(id=rid, created=created, model=model_id, choices=choices)
 
     def close(self) -> None:
-        self.combiner.close()
+        self.link.close()
 
 
 class ShardedConsensusClient:
-    """/consensus/completions over the ranks of a voter-sharded deployment: rank r samples candidates
-    [first_r, first_r + n_r) of the request (contiguous split, each with the seed it has in the whole
-    request) on its own engine and embeds them on its own GPU; ONE all-gather of the unit rows (C1: device
-    tensors over RCCL) assembles the [n, d] matrix and an object all-gather the candidates' texts, so every
-    rank builds the same response — rank 0's is served.  Collectives run on the request-ordered combiner
-    shared with score requests."""
+    """/consensus/completions over the ranks of a voter-sharded deployment (module docstring)."""
 
     def __init__(self, base, score_client: ShardedScoreClient):
         self.base, self.sc = base, score_client
-        self.world, self.rank = score_client.world, score_client.rank
 
-    def split(self, n: int):
-        share = [n // self.world + (1 if r < n % self.world else 0) for r in range(self.world)]
-        return sum(share[:self.rank]), share[self.rank]
+    @staticmethod
+    def split(n: int, ranks: List[int]) -> List[tuple]:
+        """Contiguous candidate slices (rank, first, count) over ``ranks``."""
+        W = len(ranks)
+        share = [n // W + (1 if i < n % W else 0) for i in range(W)]
+        out, first = [], 0
+        for r, c in zip(ranks, share):
+            out.append((r, first, c))
+            first += c
+        return out
 
-    def _collect(self, meta, E):
-        """Combiner thread: gather every rank's (meta, rows); rows [n, d] in candidate order on this rank's
-        device, or None when a rank failed (every rank sees the same metas, so all skip the tensor call)."""
+    async def create_unary(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
+                           tau: float = 0.05) -> S.ScoreCompletion:
+        seq = self.sc.next_seq()
+        return await self.run(self.sc.request_ctx(seq, ctx=ctx), request, embedding_model, tau)
+
+    async def _slice(self, ctx, request, embedding_model, first: int, cnt: int):
+        c2 = dict(ctx, candidates=(first, cnt, ctx["seed"]))
+        comp, E, ntok = await self.base.generate_embedded(c2, request.model_copy(update={"n": cnt}), embedding_model)
+        return comp, E.float(), ntok
+
+    async def run(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
+                  tau: float = 0.05) -> S.ScoreCompletion:
         import torch
 
-        metas = V.gather_objects(meta, self.sc.group)
-        if any(m is None or not m[0] for m in metas):
-            return metas, None
-        counts, d = [m[1] for m in metas], metas[0][2]
-        mx = max(counts)
-        if self.sc.data_backend != "nccl":
-            dev = torch.device("cpu")
-        else:
-            dev = E.device if E is not None else torch.device("cuda", torch.cuda.current_device())
-        pad = torch.zeros(mx, d, dtype=torch.float32, device=dev)
-        if E is not None and E.shape[0]:
-            pad[:E.shape[0]].copy_(E)
-        out = torch.empty(self.world * mx, d, dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(out, pad, group=self.sc.data_group)
-        rows = torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
-        return metas, rows
-
-    async def run(self, seq: int, ids, request: C.ChatCompletionCreateParams, embedding_model: str,
-                  tau: float = 0.05) -> S.ScoreCompletion:
-        ctx = self.sc.request_ctx(seq, ids)
-        meta, E, err = None, None, None
+        self.base._check_n(request)
+        emb = self.base._embedder(embedding_model)
+        seq, ids = ctx["seq"], ctx["ids"]
+        slices = self.split(int(request.n), [0] + self.sc.link.live())
+        remote = {r: (f, c) for r, f, c in slices if r != 0 and c}
+        share = self.sc.hub.open(seq, remote) if remote else None
+        for r, (f, c) in list(remote.items()):
+            if not self.sc.link.send(r, ("consensus", seq, {"request": request, "embedding_model": embedding_model,
+                                                            "first": f, "cnt": c, "seed": ctx["seed"]})):
+                del remote[r]
+                share.ranks.discard(r)
+        local = [(f, c) for r, f, c in slices if (r == 0 or (r not in remote)) and c]
+        parts: Dict[int, tuple] = {}  # first -> (comp, rows, ntok)
         try:
-            self.base._check_n(request)
-            first, cnt = self.split(int(request.n))
-            ctx["candidates"] = (first, cnt, ctx["seed"])
-            if cnt:
-                comp, E, ntok = await self.base.generate_embedded(ctx, request.model_copy(update={"n": cnt}),
-                                                                  embedding_model)
-                meta = (True, cnt, int(E.shape[1]), comp.to_obj(), int(ntok))
-            else:
-                emb = self.base._embedder(embedding_model)
-                meta = (True, 0, int(emb.encoder.cfg.hidden), None, 0)
-        except BaseException as e:  # noqa: BLE001 - every rank still takes the request's combine slot
-            err = e
-            meta = (False, 0, 0, f"{type(e).__name__}: {e}", 0)
-        metas, rows = await self.sc.combiner.submit(seq, lambda: self._collect(meta, E))
-        if err is not None:
-            raise err
-        if rows is None:
-            bad = next((r, m[3]) for r, m in enumerate(metas) if m is None or not m[0])
-            raise ScoreError(500, {"kind": "consensus_shard_failed",
-                                   "error": f"rank {bad[0]} failed to generate or embed its candidates: {bad[1]}"})
-        comps = [C.ChatCompletion.model_validate(m[3]) for m in metas if m[3] is not None]
-        merged = comps[0]
-        for c in comps[1:]:
+            for f, c in local:
+                parts[f] = await self._slice(ctx, request, embedding_model, f, c)
+            pending = dict(remote)
+            deadline = time.monotonic() + _bound(ctx)
+            while pending:
+                try:
+                    msg = await asyncio.wait_for(share.q.get(), timeout=max(0.0, deadline - time.monotonic()))
+                except asyncio.TimeoutError:
+                    msg = ("timeout", None)
+                kind, rank = msg[0], msg[1]
+                if kind == "cons" and rank in pending:
+                    f, c = pending.pop(rank)
+                    meta, raw = msg[2], msg[3]
+                    if not meta[0]:
+                        raise ScoreError(500, {"kind": "consensus_shard_failed",
+                                               "error": f"rank {rank} failed to generate or embed its candidates: "
+                                                        f"{meta[3]}"})
+                    rows = torch.from_numpy(np.frombuffer(raw, dtype=np.float32).reshape(meta[1], meta[2]).copy())
+                    parts[f] = (C.ChatCompletion.model_validate(meta[3]), rows, int(meta[4]))
+                elif kind in ("dead", "timeout"):
+                    lost = [rank] if kind == "dead" else list(pending)
+                    for r in lost:  # recompute the lost slice here: same seeds, same candidates
+                        if r in pending:
+                            f, c = pending.pop(r)
+                            parts[f] = await self._slice(ctx, request, embedding_model, f, c)
+        finally:
+            if share is not None:
+                self.sc.hub.close(seq)
+        order = sorted(parts)
+        merged = parts[order[0]][0]
+        for f in order[1:]:
+            c = parts[f][0]
             merged.choices = merged.choices + c.choices
-            if merged.usage is not None and c.usage is not None:  # every rank's generation (each ran the prompt)
+            if merged.usage is not None and c.usage is not None:  # every slice's generation (each ran the prompt)
                 merged.usage.push(c.usage)
             elif c.usage is not None:
                 merged.usage = c.usage.clone()
         merged.choices.sort(key=lambda c: c.index)
-        ntok = sum(m[4] for m in metas)
-        emb = self.base._embedder(embedding_model)
-        out = self.base.build(merged, rows.to(emb.encoder.device), ntok, embedding_model, tau)
-        out.id = f"cnscpl-{ids[1].split('-', 1)[-1]}"  # one id on every rank (the leader's)
+        rows = torch.cat([parts[f][1].to(emb.encoder.device) for f in order])
+        ntok = sum(parts[f][2] for f in order)
+        out = self.base.build(merged, rows, ntok, embedding_model, tau)
+        out.id = f"cnscpl-{ids[1].split('-', 1)[-1]}"
         out.created = ids[0]
-        if self.rank == 0 and self.base.archive is not None:
+        if self.base.archive is not None:
             self.base.archive.store_score(out)
         return out
 
 
-# ---------------------------------------------------------------------------------------------
-# serving: rank 0 takes the HTTP requests and leads, the other ranks follow (SPMD)
-
-
-class ScoreLeader:
-    """Rank 0's score client in a voter-sharded deployment (``LWC_SHARD_VOTERS=1``): every score
-    request is numbered and broadcast to the follower ranks (control group), then run here like on the
-    followers — concurrently with the other requests in flight.  Streaming requests stream this rank's
-    voters live, then the other ranks' voters and the tally in the final chunk.  Everything else (model
-    validation for multichat, ...) is the wrapped client's.
-
-    The broadcast is a blocking gloo call: it runs on ONE dedicated thread (FIFO, so request numbers are
-    assigned and broadcast in submission order), never on the event loop, which keeps serving while a
-    slow follower holds a broadcast."""
-
-    def __init__(self, client: ShardedScoreClient, control=None):
-        from concurrent.futures import ThreadPoolExecutor
-
-        self.client = client
-        self.control = control if control is not None else dist.new_group(backend="gloo")
-        self._seq = 0
-        self._lock = threading.Lock()
-        self._announcer = ThreadPoolExecutor(max_workers=1, thread_name_prefix="c2-announce")
-
-    def __getattr__(self, name):
-        return getattr(self.client, name)
-
-    def _announce_sync(self, request, kind: str = "score") -> tuple:
-        with self._lock:
-            seq = self._seq
-            self._seq += 1
-            ids = ScoreClient._new_ids(self.client)
-            V.broadcast_object((seq, ids, kind, request), 0, self.control)
-        return seq, ids
-
-    async def _announce(self, request, kind: str = "score") -> tuple:
-        return await asyncio.get_running_loop().run_in_executor(self._announcer, self._announce_sync, request, kind)
-
-    async def create_unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
-        seq, ids = await self._announce(request)
-        return await self.client.run(seq, ids, request)
-
-    async def create_streaming(self, ctx, request: S.ScoreCompletionCreateParams):
-        seq, ids = await self._announce(request)
-        return await self.client.open_stream(seq, ids, request)
-
-    async def create_consensus(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
-                               tau: float = 0.05) -> S.ScoreCompletion:
-        seq, ids = await self._announce((request, embedding_model, tau), "consensus")
-        return await self.client.consensus.run(seq, ids, request, embedding_model, tau)
-
-    def close(self) -> None:
-        self._announcer.shutdown(wait=True)
-        V.broadcast_object(None, 0, self.control)
-        self.client.close()
-
-
 class ConsensusLeader:
-    """Rank 0's /consensus/completions client in a voter-sharded deployment (see ShardedConsensusClient)."""
+    """Rank 0's /consensus/completions client (the app calls ``create_unary``)."""
 
-    def __init__(self, leader: ScoreLeader):
-        self.leader = leader
+    def __init__(self, client: ShardedConsensusClient):
+        self.client = client
 
-    async def create_unary(self, ctx, request: C.ChatCompletionCreateParams, embedding_model: str,
-                           tau: float = 0.05) -> S.ScoreCompletion:
-        return await self.leader.create_consensus(ctx, request, embedding_model, tau)
+    async def create_unary(self, ctx, request, embedding_model: str, tau: float = 0.05) -> S.ScoreCompletion:
+        return await self.client.create_unary(ctx, request, embedding_model, tau)
 
 
-def follow(client: ShardedScoreClient, control=None) -> int:
-    """Ranks > 0: run every request the leader broadcasts (their voters' share), concurrently, until it
-    sends None; returns the number of requests run.  A failed request fails on every rank alike and the
-    leader reports it, so errors are dropped here."""
-    from ..errors import StatusError
+# ---------------------------------------------------------------------------------------------
+# followers
 
-    control = control if control is not None else dist.new_group(backend="gloo")
 
-    async def main() -> int:
-        loop = asyncio.get_running_loop()
-        tasks: List[asyncio.Future] = []
-        done = asyncio.Event()
+class ShardWorker:
+    """A follower rank: runs the voter shares and candidate slices the leader sends, streaming results back."""
 
-        async def one(seq, ids, kind, request):
-            try:
-                if kind == "consensus":
-                    await client.consensus.run(seq, ids, *request)
-                else:
-                    await client.run(seq, ids, request)
-            except StatusError:
-                pass
+    def __init__(self, score: ScoreClient, consensus, link: LinkClient):
+        self.score, self.consensus, self.link = score, consensus, link
+        self.tasks: Dict[int, asyncio.Task] = {}
 
-        def receive() -> None:
-            while True:
-                msg = V.broadcast_object(None, 0, control)
-                if msg is None:
-                    loop.call_soon_threadsafe(done.set)
+    async def _score_share(self, seq: int, p: dict) -> None:
+        request, model = p["request"], p["model"]
+        C_len = len(request.choices)
+        indexer = _TagIndexer(C_len)
+        ctx = {"trace_id": p.get("trace_id"), "priority": p.get("priority", 0), "seq": seq,
+               "deadline": time.monotonic() + p["remaining"] if p.get("remaining") is not None else None}
+        llms = {l.index: l for l in model.llms}
+        pos = {l.index: j for j, l in enumerate(model.llms)}
+        err = None
+
+        async def one(v: int) -> None:
+            l = llms[v]
+            async for chunk in self.score._voter_stream(ctx, p["rid"], p["created"], indexer, l, p["weights"][v],
+                                                        request, p["seeds"][pos[v]]):
+                if not self.link.send(("chunk", seq, chunk.to_obj(), C_len)):
+                    raise ConnectionError("leader link lost")
+
+        try:
+            await asyncio.gather(*(one(v) for v in p["llms"]))
+        except asyncio.CancelledError:
+            err = "cancelled"
+        except BaseException as e:  # noqa: BLE001 — reported to the leader, which isolates these voters
+            err = f"{type(e).__name__}: {e}"
+        self.link.send(("end", seq, err))
+
+    async def _consensus_slice(self, seq: int, p: dict) -> None:
+        meta, raw = None, b""
+        try:
+            ctx = {"seq": seq, "candidates": (p["first"], p["cnt"], p["seed"])}
+            req = p["request"].model_copy(update={"n": p["cnt"]})
+            comp, E, ntok = await self.consensus.generate_embedded(ctx, req, p["embedding_model"])
+            rows = E.float().cpu().numpy()
+            meta = (True, int(rows.shape[0]), int(rows.shape[1]), comp.to_obj(), int(ntok))
+            raw = rows.tobytes()
+        except BaseException as e:  # noqa: BLE001
+            meta = (False, 0, 0, f"{type(e).__name__}: {e}", 0)
+        self.link.send(("cons", seq, meta, raw))
+
+    def serve(self) -> int:
+        """Run until the leader says stop (or the link drops); returns the number of pieces of work run."""
+
+        async def main() -> int:
+            loop = asyncio.get_running_loop()
+            done = asyncio.Event()
+            count = [0]
+
+            def start(msg) -> None:
+                kind, seq = msg[0], msg[1]
+                if kind == "cancel":
+                    t = self.tasks.get(seq)
+                    if t is not None:
+                        t.cancel()
                     return
-                loop.call_soon_threadsafe(lambda m=msg: tasks.append(asyncio.ensure_future(one(*m))))
+                count[0] += 1
+                coro = self._score_share(seq, msg[2]) if kind == "score" else self._consensus_slice(seq, msg[2])
+                t = asyncio.ensure_future(coro)
+                self.tasks[seq] = t
+                t.add_done_callback(lambda _t, s=seq: self.tasks.pop(s, None))
 
-        t = threading.Thread(target=receive, name="c2-follow", daemon=True)
-        t.start()
-        await done.wait()
-        await asyncio.gather(*tasks)
-        return len(tasks)
+            def receive() -> None:
+                while True:
+                    msg = self.link.recv()
+                    if msg is None or msg[0] == "stop":
+                        loop.call_soon_threadsafe(done.set)
+                        return
+                    loop.call_soon_threadsafe(start, msg)
 
-    n = asyncio.run(main())
-    client.close()
-    return n
+            threading.Thread(target=receive, name="shard-follow", daemon=True).start()
+            await done.wait()
+            if self.tasks:
+                await asyncio.gather(*list(self.tasks.values()), return_exceptions=True)
+            return count[0]
+
+        n = asyncio.run(main())
+        self.link.close()
+        return n
+
+
+def follow(worker: ShardWorker) -> int:
+    """Ranks > 0: serve the leader's work until it stops; returns the number of pieces of work run."""
+    return worker.serve()

@@ -118,23 +118,28 @@ def follower_config(cfg: Config, rank: int) -> Config:
 
 
 def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
-    """LWC_SHARD_VOTERS: swap the score client for the voter-sharded one (a collective: every rank).
-    Returns rank 0's leader (serve it) or, on the other ranks, the client to ``follow``."""
-    from ..parallel import dist as pdist
-    from ..score.sharded import ConsensusLeader, ScoreLeader, ShardedConsensusClient, ShardedScoreClient
+    """LWC_SHARD_VOTERS: the voter-sharded deployment (a collective at bring-up: every rank).  The ranks open
+    their leader <-> follower links (parallel/shard_link.py); rank 0 swaps its score and consensus clients
+    for the sharded leader ones and returns its score client (serve it), the other ranks return the
+    ShardWorker to ``follow``."""
+    import torch.distributed as dist
 
+    from ..parallel.shard_link import open_links
+    from ..score.sharded import ConsensusLeader, ShardedConsensusClient, ShardedScoreClient, ShardWorker
+
+    group = group if group is not None else dist.new_group(backend="gloo")
+    link = open_links(group)
     base = state.score
-    client = ShardedScoreClient(base.chat, group=group, model_registry=base.models, weight_fetchers=base.weights,
-                                archive=base.archive, rng_seed=rng_seed)
+    if dist.get_rank(group) != 0:
+        return ShardWorker(base, state.consensus, link)
+    client = ShardedScoreClient(base.chat, link, dist.get_world_size(group), model_registry=base.models,
+                                weight_fetchers=base.weights, archive=base.archive, rng_seed=rng_seed)
     client.tally_batcher = base.tally_batcher
-    # /consensus/completions: candidates split over the ranks, embedding rows all-gathered (C1)
-    client.consensus = ShardedConsensusClient(state.consensus, client) if state.consensus is not None else None
-    if pdist.info().rank == 0:
-        state.score = ScoreLeader(client)
-        state.multichat.score = state.score
-        if state.consensus is not None:
-            state.consensus = ConsensusLeader(state.score)
-        return state.score
+    state.score = client
+    state.multichat.score = client
+    if state.consensus is not None:
+        client.consensus = ShardedConsensusClient(state.consensus, client)
+        state.consensus = ConsensusLeader(client.consensus)
     return client
 
 

@@ -136,6 +136,23 @@ def _skip_worker(rank, world, port, q):
                 res["raised"] = False
             except CommFailure:
                 res["raised"] = True
+            # the EP layer over the same exchange — the poisoned per-expert counts (all-ones bytes
+            # = -1) must not become out-of-range scatter / gather indices: the layer completes (NaN rows
+            # from the missing peer), and the error word raises CommFailure instead of a device fault
+            from llm_weighted_consensus_amd.parallel.expert import ExpertParallel
+
+            ep = ExpertParallel(4, mode="padded", comm=comm)
+            xs = torch.randn(8, 8, device=dev).to(torch.bfloat16)
+            ro = torch.tensor([0, 2, 4, 6, 8], dtype=torch.int32, device=dev)
+            y = ep.run(xs, ro, lambda xl, rol, sl: xl, capacity=8)
+            comm.arm()
+            torch.cuda.synchronize(dev)
+            res["ep_shape"] = tuple(y.shape)
+            try:
+                comm.poll()
+                res["ep_raised"] = False
+            except CommFailure:
+                res["ep_raised"] = True
         pdist.barrier()
         comm.close()
         q.put((rank, res))
@@ -147,7 +164,8 @@ def _skip_worker(rank, world, port, q):
 def test_ipc_alltoall_missing_peer_fails_loudly(gpu):
     res = _run(2, _skip_worker)
     assert res[1] == {"first": True}, res
-    assert res[0] == {"first": True, "nan": True, "own": True, "raised": True}, res
+    assert res[0] == {"first": True, "nan": True, "own": True, "raised": True, "ep_shape": (8, 8),
+                      "ep_raised": True}, res
 
 
 def _ep_worker(rank, world, port, q, fp8):

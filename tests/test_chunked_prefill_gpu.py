@@ -161,3 +161,72 @@ def test_decode_advances_every_step_during_4k_prompt(gpu):
     assert chunk_steps >= 16 and advanced >= chunk_steps - 1, (chunk_steps, advanced)
     _assert_same_greedy([[got]], [[want]])
     assert all(len(s.tokens) == 64 for gr in shorts for s in gr.seqs)
+
+
+@pytest.mark.parametrize("where", ["mixed", "prefill"])
+def test_poisoned_collective_delivers_no_tokens(tiny, monkeypatch, where):
+    """a tensor-parallel peer that never arrives poisons the forward (NaN activations) and sets
+    the collective's error word.  The engine must read that word back for EVERY step whose tokens reach the
+    host — the mixed chunked-prefill step and the whole-batch prefill as well as the graph decode step — and
+    raise CommFailure before delivering any token sampled from the poisoned forward.  Here a fake comm
+    stands in for the IPC all-reduce: the poisoned forward's logits put all mass on a sentinel token."""
+    from llm_weighted_consensus_amd.engine.engine import LLMEngine
+    from llm_weighted_consensus_amd.engine.sampling import SamplingParams
+    from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
+    from llm_weighted_consensus_amd.parallel.allreduce import CommFailure
+
+    dev = tiny.device
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    host = torch.zeros(2, dtype=torch.int32).pin_memory()
+    evs = [None, None]
+    n_arm = [0]
+    sentinel = tiny.cfg.vocab_size - 7
+
+    def arm():
+        i = n_arm[0] & 1
+        n_arm[0] += 1
+        host[i:i + 1].copy_(err, non_blocking=True)
+        e = torch.cuda.Event()
+        e.record()
+        evs[i] = e
+
+    def poll():
+        for i in (0, 1):
+            if evs[i] is not None and evs[i].query():
+                evs[i] = None
+                if int(host[i]):
+                    raise CommFailure("fake peer never arrived")
+
+    def poison(out):
+        err.fill_(1)
+        out = torch.full_like(out, -1e4)
+        out[:, sentinel] = 1e4
+        return out
+
+    monkeypatch.setattr(tiny, "comm_arm", arm, raising=False)
+    monkeypatch.setattr(tiny, "comm_poll", poll, raising=False)
+    armed = {"on": False}
+    if where == "mixed":
+        orig = tiny.forward_mixed
+        monkeypatch.setattr(tiny, "forward_mixed",
+                            lambda *a, **k: poison(orig(*a, **k)) if armed["on"] else orig(*a, **k))
+    else:
+        orig = tiny.prefill
+        monkeypatch.setattr(tiny, "prefill", lambda *a, **k: poison(orig(*a, **k)) if armed["on"] else orig(*a, **k))
+    tok = ByteTokenizer(tiny.cfg.vocab_size)
+    eng = LLMEngine(tiny, tok, num_blocks=512, max_batch=32, max_model_len=768,
+                    chunked_prefill=64 if where == "mixed" else 0)
+    eng.collect_events = True
+    sp = SamplingParams(temperature=0.0, max_tokens=40, ignore_eos=True)
+    g = torch.Generator().manual_seed(5)
+    eng.add_request(torch.randint(0, 4096, (50,), generator=g).tolist(), sp, n=2)
+    delivered = []
+    for _ in range(6):  # the first request decodes in steady state
+        delivered += eng.step()
+    assert delivered
+    armed["on"] = True
+    eng.add_request(torch.randint(0, 4096, (90,), generator=g).tolist(), sp, n=2)
+    with pytest.raises(CommFailure):
+        for _ in range(8):
+            delivered += eng.step()
+    assert all(ev.token_id != sentinel for ev in delivered), "a token sampled from the poisoned forward was delivered"

@@ -133,3 +133,13 @@ def test_route_ref_contract():
         e = int(ids[tj])
         assert int(row_off[e]) <= p < int(row_off[e + 1])
     assert torch.allclose(w.sum(-1), torch.ones(7))
+
+
+def test_sane_counts_drop_poisoned_chunks():
+    """counts received from a peer that never arrived are all-ones bytes (-1 as int64); a chunk with
+    a negative count or more rows than the capacity is zeroed before it can become an index."""
+    from llm_weighted_consensus_amd.parallel.expert import ExpertParallel
+
+    rc = torch.tensor([[2, 1], [-1, -1], [5, 4], [0, 3]], dtype=torch.int64)
+    out = ExpertParallel._sane_counts(rc, 8)
+    assert out.tolist() == [[2, 1], [0, 0], [0, 0], [0, 3]]

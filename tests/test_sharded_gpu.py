@@ -1,7 +1,8 @@
-"""Voter-sharded scoring on the GPU (C2): two ranks sharing one MI355X (LWC_SHARE_ONE_GPU=1: collectives
-over gloo), each with its own local engine of a random-init Llama voter model, serve concurrent
-/score/completions through the ASGI app on rank 0.  Every response carries every voter of its request,
-each with a parseable vote (json_schema constrained decoding) and confidences that sum to one."""
+"""Voter-sharded scoring on the GPU (C2): two ranks sharing one MI355X (LWC_SHARE_ONE_GPU=1), each with its
+own local engine of a random-init Llama voter model, serve concurrent /score/completions through the ASGI
+app on rank 0 (the follower's voters stream back over the shard link).  Every response carries every voter
+of its request, each with a parseable vote (json_schema constrained decoding) and confidences that sum to
+one; /consensus/completions splits its candidates over both engines."""
 import os
 import socket
 
@@ -59,7 +60,7 @@ def _rank(rank, port, q):
 
             bodies = asyncio.run(go())
 
-            async def consensus():  # candidates split over the ranks, unit rows all-gathered (C1)
+            async def consensus():  # candidates split over the ranks, unit rows back over the shard link
                 r = await client.post("/consensus/completions", json={
                     "model": "tiny", "messages": [{"role": "user", "content": "Name a colour."}], "n": 6,
                     "max_tokens": 12, "temperature": 0.9, "seed": 3, "embedding_model": "e"})
@@ -98,7 +99,7 @@ def test_voter_sharded_serving_two_ranks_one_gpu(gpu):
     got = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert got[1] == 6, got  # the follower ran every request
+    assert got[1] == 6, got  # the follower ran its share of every request (5 score shares + 1 consensus slice)
     cons_indices, cons_conf, n_rows = got[0].pop()
     assert cons_indices == list(range(6)) and cons_conf == pytest.approx(1.0) and n_rows == 6
     for n_provided, model_indices, n_votes, conf, indices in got[0]:

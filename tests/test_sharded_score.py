@@ -1,7 +1,14 @@
-"""Voter-sharded scoring over a process group (C2; gloo, world 2, CPU): a score request's voters split
-across ranks give the single-process tally, confidences, votes and usage; ids agree on every rank;
-"every vote failed" is decided globally (every rank raises, error codes unified over all ranks); a rank
-that owns no voter still takes part; requests run concurrently (combines ordered by request number)."""
+"""Voter-sharded scoring (C2; CPU ranks): the leader (rank 0) resolves each request once, sends every
+follower its share of voters over the shard links, merges their chunks live and tallies alone.
+
+* world 2: a request's voters split across ranks give the single-process tally, confidences, votes and
+  usage; "every vote failed" is decided over all voters (codes unified); concurrent requests; streamed
+  requests interleave the follower's voter chunks live (before the final chunk);
+* world 4, failure isolation: a follower killed mid-load turns exactly its unfinished
+  voters of the in-flight requests into ``voter_shard_lost`` error choices, those requests complete within
+  the bound, later requests run on the survivors with every voter ok, and nothing waits for a process-group
+  timeout;
+* an abandoned stream (never iterated) leaves nothing behind: the next request completes."""
 import asyncio
 import math
 import os
@@ -76,79 +83,9 @@ def _run(client, case, ctx=None):
         return {"error": e.code}
 
 
-async def _run_sharded(client, seq, case):
-    try:
-        return _summary(await client.run(seq, (1700000000, f"scrcpl-test-{seq}"), _request(case)))
-    except ScoreError as e:
-        return {"error": e.code}
-
-
-def _worker(rank, world, port, out_q):
+def _leader_worker(rank, world, port, out_q, scenario):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
-    from llm_weighted_consensus_amd.parallel import dist as pdist
-    from llm_weighted_consensus_amd.score.sharded import ShardedScoreClient
-
-    pdist.init_from_env("cpu")
-    client = ShardedScoreClient(FakeChatClient(_policy), rng_seed=7)
-    # one at a time (same key-tree seeds as the single-process client), then all cases concurrently
-    res = {case: asyncio.run(_run_sharded(client, i, case)) for i, case in enumerate(CASES)}
-
-    async def concurrent():
-        cases = (list(CASES) + ["one_choice"]) * 3
-        outs = await asyncio.gather(*(_run_sharded(client, len(CASES) + i, c) for i, c in enumerate(cases)))
-        return [(c, o) for c, o in zip(cases, outs)]
-
-    res["concurrent"] = asyncio.run(concurrent())
-    client.close()
-    out_q.put((rank, res))
-    pdist.shutdown()
-
-
-def test_voter_sharded_score_matches_single_process():
-    from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
-
-    single = ScoreClient(FakeChatClient(_policy), rng_seed=7)
-    # the sharded client seeds request `seq`'s voters from (seed base 7, seq): the same seeds here
-    want = {case: _run(single, case, {"seed": 7 * 1000003 + i}) for i, case in enumerate(CASES)}
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = dict(q.get(timeout=180) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for case in ("mixed", "one_voter"):
-        w, g0, g1 = want[case], got[0][case], got[1][case]
-        assert g0["id"] == g1["id"]  # the request's id, identical on every rank
-        for g in (g0, g1):  # every rank merges the same full response
-            assert g["n"] == w["n"] and g["indices"] == list(range(w["n"]))
-            assert g["prompt_tokens"] == w["prompt_tokens"]
-            assert g["total_cost"] == pytest.approx(w["total_cost"])
-            for (i, wt, cf), (j, wt2, cf2) in zip(w["provided"], g["provided"]):
-                assert i == j and wt2 == pytest.approx(wt) and cf2 == pytest.approx(cf)
-            for a, b in zip(w["voters"], g["voters"]):
-                assert a[0] == b[0] and a[1] == b[1] and a[4] == b[4]
-                assert b[2] == pytest.approx(a[2])
-                assert (a[3] is None and b[3] is None) or b[3] == pytest.approx(a[3])
-    assert want["all_fail"]["error"] == got[0]["all_fail"]["error"] == got[1]["all_fail"]["error"]
-    for r in (0, 1):  # concurrent requests: same shapes and tallies (seeds differ, so not the votes)
-        for case, o in got[r]["concurrent"]:
-            if case == "one_choice":
-                assert o == {"error": 400}
-            elif case == "all_fail":
-                assert o == {"error": want["all_fail"]["error"]}
-            else:
-                assert o["n"] == want[case]["n"] and o["prompt_tokens"] == want[case]["prompt_tokens"]
-                assert sum(cf for _, _, cf in o["provided"]) == pytest.approx(1.0)
-
-
-def _serve_worker(rank, world, port, out_q):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT=str(port), LWC_SHARD_DEAD_S="3", LWC_SHARD_HB_S="0.2")
     from llm_weighted_consensus_amd.parallel import dist as pdist
     from llm_weighted_consensus_amd.score.multichat import MultichatClient
     from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
@@ -157,57 +94,197 @@ def _serve_worker(rank, world, port, out_q):
     from llm_weighted_consensus_amd.server.main import shard_voters
 
     pdist.init_from_env("cpu")
-    chat = FakeChatClient(_policy)
+    policy = _policy
+    delay = 0.0
+    if scenario == "kill":
+        delay = 0.03  # slow voters: requests are in flight when rank 3 dies
+        if rank == 3:
+            seen = [0]
+
+            def policy(req, _p=_policy):  # noqa: F811 — rank 3 dies while starting its 4th voter stream
+                seen[0] += 1
+                if seen[0] == 4:
+                    os._exit(17)
+                return _p(req)
+    chat = FakeChatClient(policy, delay_s=delay)
     score = ScoreClient(chat, rng_seed=7)
     state = AppState(chat, score, MultichatClient(score, None))
     lead = shard_voters(state, rng_seed=7)
-    if rank == 0:
-        async def serve():
-            out = [_summary(await state.score.create_unary(None, _request("mixed")))]
-            chunks = [c async for c in await state.score.create_streaming(None, _request("mixed"))]
-            agg = chunks[0].clone()
-            for c in chunks[1:]:
-                agg.push(c)
-            out.append((len(chunks), _summary(S.ScoreCompletion.from_chunk(agg))))
-            try:
-                await state.score.create_unary(None, _request("all_fail"))
-            except ScoreError as e:
-                out.append(e.code)
-            many = await asyncio.gather(*(state.score.create_unary(None, _request("mixed")) for _ in range(6)))
-            out.append([len(m.choices) for m in many])
-            return out
-
-        res = asyncio.run(serve())
-        lead.close()
-    else:
+    if rank != 0:
         res = follow(lead)
+        out_q.put((rank, res))
+        pdist.shutdown()
+        return
+    try:
+        res = asyncio.run(SCENARIOS[scenario](state.score))
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+
+        res = f"ERROR {type(e).__name__}: {e}\n{traceback.format_exc()}"
+    lead.close()
     out_q.put((rank, res))
-    pdist.shutdown()
+    if scenario != "kill":
+        pdist.shutdown()
 
 
-def test_leader_broadcasts_requests_to_followers():
-    single = __import__("llm_weighted_consensus_amd.score.orchestrator", fromlist=["ScoreClient"]).ScoreClient(
-        FakeChatClient(_policy), rng_seed=7)
-    want = _run(single, "mixed", {"seed": 7 * 1000003 + 0})   # request 0: unary
-    want_s = _run(single, "mixed", {"seed": 7 * 1000003 + 1})  # request 1: streamed
+async def _equiv(client):
+    out = {}
+    for case in CASES:  # one at a time: request k's voters seeded from (7, k), as the single process
+        try:
+            out[case] = _summary(await client.create_unary(None, _request(case)))
+        except ScoreError as e:
+            out[case] = {"error": e.code}
+    cases = (list(CASES) + ["one_choice"]) * 3
+
+    async def one(c):
+        try:
+            return _summary(await client.create_unary(None, _request(c)))
+        except ScoreError as e:
+            return {"error": e.code}
+
+    out["concurrent"] = list(zip(cases, await asyncio.gather(*(one(c) for c in cases))))
+    # streamed: the follower's voters arrive live, not whole in the final chunk
+    req = _request("mixed").model_copy(update={"stream": True})
+    chunks = [c async for c in await client.create_streaming(None, req)]
+    remote = {v.index for v in client.last_model_llms if v.index % 2 == 1} if hasattr(client, "last_model_llms") \
+        else {1, 3}
+    live = [k for k, c in enumerate(chunks[:-1]) for ch in c.choices
+            if ch.model_index in remote and ch.delta.content]
+    agg = chunks[0].clone()
+    for c in chunks[1:]:
+        agg.push(c)
+    out["stream"] = {"n_chunks": len(chunks), "live_remote_chunks": len(live),
+                     "summary": _summary(S.ScoreCompletion.from_chunk(agg))}
+    # abandoned before iteration: nothing is announced, nothing waits; the next request completes
+    await client.create_streaming(None, _request("mixed").model_copy(update={"stream": True}))
+    out["after_abandon"] = _summary(await client.create_unary(None, _request("mixed")))["n"]
+    return out
+
+
+def test_voter_sharded_leader_matches_single_process():
+    from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
+
+    single = ScoreClient(FakeChatClient(_policy), rng_seed=7)
+    # the sharded leader seeds request `seq`'s voters from (seed base 7, seq): the same seeds here
+    want = {case: _run(single, case, {"seed": 7 * 1000003 + i}) for i, case in enumerate(CASES)}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_serve_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_leader_worker, args=(r, 2, port, q, "equiv")) for r in range(2)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    mixed, (n_chunks, folded), code, many = got[0]
-    assert mixed["n"] == want["n"] and [v[:2] for v in mixed["voters"]] == [v[:2] for v in want["voters"]]
-    # streamed: initial chunk, this rank's voter chunks as they arrive, final chunk (remote voters + tally);
-    # the fold of the stream is the unary response
-    assert n_chunks >= 3
-    assert folded["n"] == want_s["n"] and folded["indices"] == want_s["indices"]
-    assert [v[:2] + v[4:] for v in folded["voters"]] == [v[:2] + v[4:] for v in want_s["voters"]]
-    assert sum(cf for _, _, cf in folded["provided"]) == pytest.approx(1.0)
-    assert code == 429 or code == want.get("error", code)
-    assert many == [want["n"]] * 6  # concurrent requests: every voter of every request in the response
-    assert got[1] == 9  # the follower ran all nine requests
+    g = got[0]
+    assert isinstance(g, dict), g
+    for case in ("mixed", "one_voter"):
+        w, o = want[case], g[case]
+        assert o["n"] == w["n"] and o["indices"] == list(range(w["n"]))
+        assert o["prompt_tokens"] == w["prompt_tokens"]
+        assert o["total_cost"] == pytest.approx(w["total_cost"])
+        for (i, wt, cf), (j, wt2, cf2) in zip(w["provided"], o["provided"]):
+            assert i == j and wt2 == pytest.approx(wt) and cf2 == pytest.approx(cf)
+        for a, b in zip(w["voters"], o["voters"]):
+            assert a[0] == b[0] and a[1] == b[1] and a[4] == b[4]
+            assert b[2] == pytest.approx(a[2])
+            assert (a[3] is None and b[3] is None) or b[3] == pytest.approx(a[3])
+    assert want["all_fail"]["error"] == g["all_fail"]["error"]
+    for case, o in g["concurrent"]:  # concurrent requests: same shapes and tallies (seeds differ, not votes)
+        if case == "one_choice":
+            assert o == {"error": 400}
+        elif case == "all_fail":
+            assert o == {"error": want["all_fail"]["error"]}
+        else:
+            assert o["n"] == want[case]["n"] and o["prompt_tokens"] == want[case]["prompt_tokens"]
+            assert sum(cf for _, _, cf in o["provided"]) == pytest.approx(1.0)
+    st = g["stream"]
+    assert st["live_remote_chunks"] > 0  # the follower's voters' content arrived before the final chunk
+    assert st["summary"]["n"] == want["mixed"]["n"] and sum(cf for _, _, cf in st["summary"]["provided"]) == \
+        pytest.approx(1.0)
+    assert g["after_abandon"] == want["mixed"]["n"]
+    assert got[1] >= len(CASES)  # the follower ran its share of every request that had voters for it
+
+
+KILL_LLMS = [{"model": "a"}, {"model": "b"}, {"model": "a", "temperature": 0.5}, {"model": "b", "top_p": 0.9},
+             {"model": "a", "temperature": 0.2}, {"model": "b", "temperature": 0.3}, {"model": "a", "top_p": 0.8},
+             {"model": "b", "temperature": 0.7}]
+
+
+def _kill_request(stream=False):
+    return S.ScoreCompletionCreateParams.model_validate(dict(
+        messages=[{"role": "user", "content": "What is the capital of France? " + "x" * 40}],
+        model={"llms": KILL_LLMS}, choices=["Paris", "London", "Berlin"], stream=stream))
+
+
+async def _kill(client):
+    import time
+
+    t0 = time.monotonic()
+
+    async def one(stream):
+        if stream:
+            chunks = [c async for c in await client.create_streaming(None, _kill_request(True))]
+            agg = chunks[0].clone()
+            for c in chunks[1:]:
+                agg.push(c)
+            return S.ScoreCompletion.from_chunk(agg)
+        return await client.create_unary(None, _kill_request())
+
+    def voters(out):
+        def kind(e):
+            if e is None:
+                return None
+            m = e.message
+            err = m.get("error") if isinstance(m, dict) else None
+            return err.get("kind") if isinstance(err, dict) else (m.get("kind") if isinstance(m, dict) else e.code)
+
+        return sorted((c.model_index, c.finish_reason, kind(c.error)) for c in out.choices if c.index >= 3)
+
+    inflight = await asyncio.gather(*(one(k % 2 == 1) for k in range(4)))
+    t_inflight = time.monotonic() - t0
+    later = [await one(False), await one(True)]
+    return {"inflight": [voters(o) for o in inflight], "later": [voters(o) for o in later],
+            "t_inflight": t_inflight, "t_total": time.monotonic() - t0, "live": client.link.live(),
+            "conf": [sum(c.confidence for c in o.choices if c.index < 3) for o in inflight + later]}
+
+
+@pytest.mark.timeout(240)
+def test_killed_follower_isolated_as_error_choices():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_leader_worker, args=(r, 4, port, q, "kill")) for r in range(4)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(3):  # rank 3 dies and reports nothing
+        r, v = q.get(timeout=200)
+        got[r] = v
+    for p in procs:
+        p.join(timeout=60)
+    assert procs[3].exitcode == 17
+    g = got[0]
+    assert isinstance(g, dict), g
+    assert g["live"] == [1, 2]
+    # voters of rank 3 (voter i -> live[i % 4] at the time: i = 3, 7) in the in-flight requests: error choices
+    # of kind voter_shard_lost; every other voter finished normally
+    lost_any = False
+    for vs in g["inflight"]:
+        assert len(vs) == len(KILL_LLMS)
+        for mi, fr, err in vs:
+            if mi % 4 == 3 and err == "voter_shard_lost":
+                assert fr == "error"
+                lost_any = True
+            else:
+                assert err is None and fr in ("stop", None), (mi, fr, err)
+    assert lost_any
+    for vs in g["later"]:  # after the death: the survivors run every voter
+        assert len(vs) == len(KILL_LLMS) and all(err is None for _, _, err in vs), vs
+    assert all(c == pytest.approx(1.0) for c in g["conf"])
+    assert g["t_total"] < 60  # bounded by the link's failure detection, not a 600 s process-group timeout
+    assert got[1] >= 4 and got[2] >= 4
+
+
+SCENARIOS = {"equiv": _equiv, "kill": _kill}

@@ -5,9 +5,9 @@ gloo, requests through the real ASGI app on rank 0.
   single-process server (voters, votes, tally), the initial chunk comes first, each rank's voters arrive
   as they finish;
 * /consensus/completions: the request's candidates are split over the 8 ranks (each samples its slice with
-  the seeds the slice has in the whole request and embeds it on its own device), the unit rows are
-  all-gathered (C1) and the response equals the single-process one (candidates, weights, confidences,
-  embeddings)."""
+  the seeds the slice has in the whole request and embeds it on its own device), the unit rows come back
+  to the leader over the shard links and the response equals the single-process one (candidates,
+  weights, confidences, embeddings)."""
 import asyncio
 import json
 import math
@@ -206,4 +206,6 @@ def test_world8_sharded_serving_matches_single_process():
     for n in (12, 5):  # consensus: the 8-way split equals one process
         _same_consensus(lead[f"consensus{n}"], want[f"consensus{n}"])
     assert lead["many"] == [(200, 3 + len(LLMS))] * 3 + [(200, 9)] * 3
-    assert all(got[r] == 10 for r in range(1, WORLD))  # every follower ran all ten announced requests
+    # followers get work only for what they own: every score request (10 voters over 8 ranks), a slice of every
+    # consensus request whose candidate count reaches them (12 and 9: all ranks; 5: ranks 1-4)
+    assert all(got[r] == 5 + 1 + (1 if r < 5 else 0) + 3 for r in range(1, WORLD)), got
