@@ -459,14 +459,12 @@ __global__ void __launch_bounds__(kCWaves * 64)
   float m = -1e30f, l = 0.f;
 
   // ---- phase 1: shared prefix through LDS ----
-  auto phase1 = [&]() {
   const int* bt0 = block_tables + (size_t)row_start * p.max_blocks;
   const int pctx = pblk * kBS;
-  for (int c0 = 0; c0 < pblk; c0 += 2 * kCPairs) {
+  // LDS-DMA of prefix chunk c0 (kCPairs block pairs; global_load_lds_dwordx4): wave-instruction (pair, round)
+  // writes 1 KiB contiguously, lane-linear; the K image's XOR swizzle is applied to the SOURCE address.
+  auto issue_chunk = [&](int c0) {
     const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
-    __syncthreads();  // previous chunk fully consumed
-    // LDS-DMA (global_load_lds_dwordx4): wave-instruction (pair, round) writes 1 KiB contiguously,
-    // lane-linear; the K image's XOR swizzle is applied to the SOURCE address instead.
 #pragma unroll
     for (int pi = 0; pi < kCPairs; ++pi) {
 #pragma unroll
@@ -493,100 +491,145 @@ __global__ void __launch_bounds__(kCWaves * 64)
         }
       }
     }
-    __syncthreads();
-    if (nrows > 0) {
-      for (int pi = 0; pi < npairs; ++pi) {
-        const int blkA = c0 + 2 * pi;
-        const bool hasB = blkA + 1 < pblk;
-        const unsigned char* pb = smem + pi * kPairBytes;
-        PairRegs r;
+  };
+  // prefix pair pi of the chunk at c0, out of LDS, into `r` (a free register set) and onto the state
+  auto attend_lds = [&](PairRegs& r, int c0, int pi) {
+    const int blkA = c0 + 2 * pi;
+    const bool hasB = blkA + 1 < pblk;
+    const unsigned char* pb = smem + pi * kPairBytes;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int ch = ((4 * s + g) ^ r16) << 4;
-          r.ka[s] = *reinterpret_cast<const short8*>(pb + r16 * 256 + ch);
-          r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
-        }
+    for (int s = 0; s < 4; ++s) {
+      const int ch = ((4 * s + g) ^ r16) << 4;
+      r.ka[s] = *reinterpret_cast<const short8*>(pb + r16 * 256 + ch);
+      r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
+    }
 #pragma unroll
-        for (int n = 0; n < 8; ++n) {
-          const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
-          r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
-                          *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
+    for (int n = 0; n < 8; ++n) {
+      const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
+      r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
+                      *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
+    }
+    attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
+  };
+  auto phase1 = [&]() {
+    for (int c0 = 0; c0 < pblk; c0 += 2 * kCPairs) {
+      const int npairs = min(kCPairs, (pblk - c0 + 1) / 2);
+      __syncthreads();  // previous chunk fully consumed
+      issue_chunk(c0);
+      __syncthreads();
+      if (nrows > 0) {
+        for (int pi = 0; pi < npairs; ++pi) {
+          PairRegs r;
+          attend_lds(r, c0, pi);
         }
-        attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
       }
     }
-  }
-
   };
 
   // ---- phase 2: each sequence's own blocks, two pairs in flight per wave ----
   // Positions walk (sequence j of the wave, block pair) across the wave's sequences.  Two register
   // sets alternate (unrolled by two, so no register copies of in-flight loads): while one pair is on
   // the MFMAs the next pair's K and V are already loading — two pairs (32 KiB) in flight per wave.
-  auto phase2 = [&]() {
-    if (nrows <= 0) return;
-    DecodeParams lp{};
-    lp.kc = p.kc;
-    lp.vc = p.vc;
-    lp.Hkv = p.Hkv;
-    struct Pos {
-      int j, pair, end, ctx;
-    };
-    auto seq_pos = [&](int j) {  // first suffix pair of sequence j (or beyond), skipping empty suffixes
-      Pos q{j, pblk, 0, 0};
-      while (q.j < nseq_w) {
-        q.ctx = ctx_lens[s0 + q.j];
-        q.end = (q.ctx + kBS - 1) / kBS;
-        if (q.pair < q.end) break;
-        ++q.j;
-      }
-      return q;
-    };
-    auto next = [&](Pos q) {
-      q.pair += 2;
-      return q.pair < q.end ? q : seq_pos(q.j + 1);
-    };
-    auto load = [&](PairRegs& r, const Pos& q) {
-      const int* bt = block_tables + (size_t)(s0 + q.j) * p.max_blocks;
-      load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
-      load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
-    };
-    auto attend = [&](const PairRegs& r, const Pos& q) {
-      const bool row_on = r16 < nrows && r16 / p.G == q.j;
-      float4v sa, sb;
-      pair_scores(r, qf, sa, sb);
-      short8 pf;
-      pair_softmax(sa, sb, q.pair, q.pair + 1 < q.end, q.ctx, row_on, sl2, g, o, m, l, pf);
-      pair_values(r, pf, q.pair, q.pair + 1 < q.end, q.ctx, g, o);
-    };
-    PairRegs ra, rb;
-    Pos p0 = seq_pos(0);
-    if (p0.j >= nseq_w) return;
-    Pos p1 = next(p0);
-    load(ra, p0);
-    if (p1.j < nseq_w) load(rb, p1);
-    while (true) {
-      attend(ra, p0);
-      if (p1.j >= nseq_w) break;
-      const Pos p2 = next(p1);
-      if (p2.j < nseq_w) load(ra, p2);
-      attend(rb, p1);
-      if (p2.j >= nseq_w) break;
-      const Pos p3 = next(p2);
-      if (p3.j < nseq_w) load(rb, p3);
-      p0 = p2;
-      p1 = p3;
+  DecodeParams lp{};
+  lp.kc = p.kc;
+  lp.vc = p.vc;
+  lp.Hkv = p.Hkv;
+  struct Pos {
+    int j, pair, end, ctx;
+  };
+  auto seq_pos = [&](int j) {  // first suffix pair of sequence j (or beyond), skipping empty suffixes
+    Pos q{j, pblk, 0, 0};
+    while (q.j < nseq_w) {
+      q.ctx = ctx_lens[s0 + q.j];
+      q.end = (q.ctx + kBS - 1) / kBS;
+      if (q.pair < q.end) break;
+      ++q.j;
     }
+    return q;
+  };
+  auto next = [&](Pos q) {
+    q.pair += 2;
+    return q.pair < q.end ? q : seq_pos(q.j + 1);
+  };
+  auto load = [&](PairRegs& r, const Pos& q) {
+    const int* bt = block_tables + (size_t)(s0 + q.j) * p.max_blocks;
+    load_pair_k(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
+    load_pair_v(r, lp, bt, kvh, q.pair, q.pair + 1 < q.end, r16, g, q.ctx);
+  };
+  auto attend = [&](const PairRegs& r, const Pos& q) {
+    const bool row_on = r16 < nrows && r16 / p.G == q.j;
+    float4v sa, sb;
+    pair_scores(r, qf, sa, sb);
+    short8 pf;
+    pair_softmax(sa, sb, q.pair, q.pair + 1 < q.end, q.ctx, row_on, sl2, g, o, m, l, pf);
+    pair_values(r, pf, q.pair, q.pair + 1 < q.end, q.ctx, g, o);
   };
 
-  // Softmax merging is order-free: odd workgroups stream their suffixes first, so a CU's two
-  // resident workgroups overlap one's LDS-bound prefix phase with the other's HBM-bound suffix.
-  if (tile & 1) {
-    phase2();
+  if (pblk > 2 * kCPairs) {
+    // long shared prompt (several LDS chunks): the chunked prefix pass, then the suffixes
     phase1();
+    if (nrows > 0) {
+      PairRegs ra, rb;
+      Pos p0 = seq_pos(0);
+      if (p0.j < nseq_w) {
+        Pos p1 = next(p0);
+        load(ra, p0);
+        if (p1.j < nseq_w) load(rb, p1);
+        while (true) {
+          attend(ra, p0);
+          if (p1.j >= nseq_w) break;
+          const Pos p2 = next(p1);
+          if (p2.j < nseq_w) load(ra, p2);
+          attend(rb, p1);
+          if (p2.j >= nseq_w) break;
+          const Pos p3 = next(p2);
+          if (p3.j < nseq_w) load(rb, p3);
+          p0 = p2;
+          p1 = p3;
+        }
+      }
+    }
   } else {
-    phase1();
-    phase2();
+    // The whole shared prompt fits one LDS chunk (the common case: a few hundred prompt tokens).  Its
+    // LDS-DMA is issued first and lands while the first two suffix pairs load (both streams in flight
+    // together — the serial DMA-then-compute prefix pass left the CU's memory pipe idle: one workgroup per
+    // CU, VGPR-bound); then every prefix pair is attended out of LDS in the register set a suffix pair
+    // has just released, between the suffix pairs, while the other set's loads are in flight.  Online
+    // softmax merges in any order.
+    const int npre = (pblk + 1) / 2;
+    int pre = 0;
+    issue_chunk(0);
+    PairRegs ra, rb;
+    Pos p0{nseq_w, 0, 0, 0}, p1{nseq_w, 0, 0, 0};
+    if (nrows > 0) {
+      p0 = seq_pos(0);
+      if (p0.j < nseq_w) {
+        p1 = next(p0);
+        load(ra, p0);
+        if (p1.j < nseq_w) load(rb, p1);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's prefix DMA (and both suffix pairs) landed
+    __syncthreads();                                  // every wave's prefix DMA landed: LDS chunk readable
+    if (nrows > 0) {
+      if (p0.j < nseq_w) {
+        while (true) {
+          attend(ra, p0);
+          if (pre < npre) attend_lds(ra, 0, pre++);
+          if (p1.j >= nseq_w) break;
+          const Pos p2 = next(p1);
+          if (p2.j < nseq_w) load(ra, p2);
+          attend(rb, p1);
+          if (pre < npre) attend_lds(rb, 0, pre++);
+          if (p2.j >= nseq_w) break;
+          const Pos p3 = next(p2);
+          if (p3.j < nseq_w) load(rb, p3);
+          p0 = p2;
+          p1 = p3;
+        }
+      }
+      while (pre < npre) attend_lds(ra, 0, pre++);
+    }
   }
 
   // ---- epilogue ----

@@ -32,6 +32,10 @@ int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, cons
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
+int lwc_ep_pack(const void*, const float*, const int*, const int*, int, int, int, int, int, void*, hipStream_t);
+int lwc_ep_unpack(const void*, int, int, int, int, int, int, void*, float*, int*, int*, hipStream_t);
+int lwc_ep_back(const void*, const int*, int, int, int, void*, hipStream_t);
+int lwc_ep_combine(const void*, const int*, const int*, const float*, int, int, int, int, int, int, void*, hipStream_t);
 int lwc_silu_mul_quant_fp8(const void*, int, int, int, void*, float*, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
@@ -419,6 +423,64 @@ void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Te
            "moe_route");
 }
 
+// C4 expert-parallel exchange buffers (csrc/kernels/ep.hip): send / recv are uint8 [W, (C + 1) * RB].
+int64_t row_bytes_of(const at::Tensor& x) { return x.size(1) * (int64_t)x.element_size(); }
+
+void ep_pack(const at::Tensor& x, const c10::optional<at::Tensor>& xs, const c10::optional<at::Tensor>& src,
+             const at::Tensor& row_off, int64_t W, int64_t El, int64_t C, at::Tensor& send) {
+  CHECK_GPU(x); CHECK_CONTIG(x); CHECK_GPU(send); CHECK_CONTIG(send); CHECK_DTYPE(send, at::kByte);
+  CHECK_DTYPE(row_off, at::kInt);
+  TORCH_CHECK(x.dim() == 2 && row_off.numel() == W * El + 1, "ep_pack: x [rows, d], row_off [W*El+1]");
+  TORCH_CHECK(send.dim() == 2 && send.size(0) == W && send.size(1) % (C + 1) == 0, "ep_pack: send [W, (C+1)*RB]");
+  if (src.has_value()) { CHECK_DTYPE(*src, at::kInt); CHECK_CONTIG(*src); }
+  if (xs.has_value()) { CHECK_DTYPE(*xs, at::kFloat); TORCH_CHECK(xs->numel() == x.size(0), "ep_pack: one scale per row"); }
+  CHECK_RC(lwc_ep_pack(x.data_ptr(), opt_ptr<float>(xs), opt_ptr<int>(src), row_off.data_ptr<int>(), (int)W, (int)El,
+                       (int)C, (int)(send.size(1) / (C + 1)), (int)row_bytes_of(x), send.data_ptr(), cur_stream()),
+           "ep_pack");
+}
+
+void ep_unpack(const at::Tensor& recv, int64_t W, int64_t El, int64_t C, at::Tensor& x_local,
+               const c10::optional<at::Tensor>& s_local, at::Tensor& map, at::Tensor& row_off_local) {
+  CHECK_GPU(recv); CHECK_CONTIG(recv); CHECK_DTYPE(recv, at::kByte); CHECK_CONTIG(x_local);
+  CHECK_DTYPE(map, at::kInt); CHECK_DTYPE(row_off_local, at::kInt);
+  TORCH_CHECK(recv.dim() == 2 && recv.size(0) == W && recv.size(1) % (C + 1) == 0, "ep_unpack: recv [W, (C+1)*RB]");
+  TORCH_CHECK(x_local.dim() == 2 && x_local.size(0) == W * C && map.numel() == W * C && row_off_local.numel() == El + 1,
+              "ep_unpack: x_local [W*C, d], map [W*C], row_off_local [El+1]");
+  if (s_local.has_value()) {
+    CHECK_DTYPE(*s_local, at::kFloat);
+    TORCH_CHECK(s_local->numel() == W * C, "ep_unpack: s_local [W*C]");
+  }
+  CHECK_RC(lwc_ep_unpack(recv.data_ptr(), (int)W, (int)El, (int)C, (int)(recv.size(1) / (C + 1)),
+                         (int)row_bytes_of(x_local), s_local.has_value() ? 1 : 0, x_local.data_ptr(),
+                         s_local.has_value() ? s_local->data_ptr<float>() : nullptr, map.data_ptr<int>(),
+                         row_off_local.data_ptr<int>(), cur_stream()),
+           "ep_unpack");
+}
+
+void ep_back(const at::Tensor& y_local, const at::Tensor& map, int64_t W, int64_t C, at::Tensor& back) {
+  CHECK_GPU(y_local); CHECK_CONTIG(y_local); CHECK_CONTIG(back); CHECK_DTYPE(map, at::kInt);
+  TORCH_CHECK(y_local.dim() == 2 && y_local.size(0) >= W * C && back.dim() == 2 && back.size(0) == W * C &&
+                  back.size(1) == y_local.size(1) && back.scalar_type() == y_local.scalar_type() && map.numel() == W * C,
+              "ep_back: y_local [>= W*C, d], back [W*C, d], map [W*C]");
+  CHECK_RC(lwc_ep_back(y_local.data_ptr(), map.data_ptr<int>(), (int)W, (int)C, (int)row_bytes_of(y_local),
+                       back.data_ptr(), cur_stream()),
+           "ep_back");
+}
+
+void ep_combine(const at::Tensor& ret, const at::Tensor& row_off, const at::Tensor& inv, const at::Tensor& w,
+                int64_t El, int64_t C, int64_t k, at::Tensor& out) {
+  CHECK_BF16(ret); CHECK_BF16(out); CHECK_CONTIG(ret); CHECK_CONTIG(out);
+  CHECK_DTYPE(row_off, at::kInt); CHECK_DTYPE(inv, at::kInt); CHECK_DTYPE(w, at::kFloat);
+  const int T = (int)out.size(0), d = (int)out.size(1);
+  const int64_t E = row_off.numel() - 1;
+  TORCH_CHECK(ret.size(1) == d && ret.size(0) == (E / El) * C && inv.numel() >= (int64_t)T * k &&
+                  w.numel() >= (int64_t)T * k,
+              "ep_combine: ret [W*C, d], inv / w [T*k]");
+  CHECK_RC(lwc_ep_combine(ret.data_ptr(), row_off.data_ptr<int>(), inv.data_ptr<int>(), w.data_ptr<float>(), T, (int)E,
+                          (int)El, (int)C, (int)k, d, out.data_ptr(), cur_stream()),
+           "ep_combine");
+}
+
 void moe_combine(const at::Tensor& Y, const at::Tensor& inv, const at::Tensor& w, int64_t k, at::Tensor& out) {
   CHECK_BF16(Y); CHECK_BF16(out); CHECK_CONTIG(Y); CHECK_CONTIG(out);
   CHECK_DTYPE(inv, at::kInt); CHECK_DTYPE(w, at::kFloat);
@@ -704,4 +766,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_region_bytes", &ar_region_bytes);
   m.def("allreduce", &allreduce);
   m.def("alltoall", &alltoall);
+  m.def("ep_pack", &ep_pack);
+  m.def("ep_unpack", &ep_unpack);
+  m.def("ep_back", &ep_back);
+  m.def("ep_combine", &ep_combine);
 }

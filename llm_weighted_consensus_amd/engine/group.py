@@ -597,6 +597,21 @@ def _tp_setup(spec: dict, dev, hidden: int):
     return rank, tp, comm
 
 
+def _tp_num_blocks(model, dev, kv_fraction: float) -> int:
+    """Every rank of a TP replica must schedule identically: one KV pool size for the replica (the smallest
+    rank's)."""
+    import torch
+    import torch.distributed as dist
+
+    from ..models.llama import KVCache
+
+    torch.cuda.synchronize(dev)
+    free, _total = torch.cuda.mem_get_info(dev)
+    nb = torch.tensor([max(64, int(free * kv_fraction) // KVCache.bytes_per_block(model.cfg, 16))])
+    dist.all_reduce(nb, op=dist.ReduceOp.MIN)
+    return int(nb.item())
+
+
 def build_engine(spec: dict, wid: int):
     """Default worker factory: a decoder engine on ``spec['device']`` from a server model spec
     ({"arch", "weights": "random:<seed>" | path, "max_model_len", "max_batch", "kv_fraction", "fp8",
@@ -618,9 +633,6 @@ def build_engine(spec: dict, wid: int):
     tp = int(spec.get("tp", 1) or 1)
     kv_fraction = float(spec.get("kv_fraction", 0.85))
     num_blocks = None
-    if tp > 1 and not cfg.num_experts:
-        raise ValueError(f"tp {tp}: tensor parallelism is implemented for the MoE decoders (config 5); "
-                         f"serve {cfg.name} data-parallel (one worker per GPU)")
     if cfg.num_experts:
         from ..models.mixtral import MixtralModel
 
@@ -633,16 +645,16 @@ def build_engine(spec: dict, wid: int):
         model = MixtralModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
                              fp8=bool(spec.get("fp8", False)), **tp_kw)
         if tp > 1:
-            # every rank must schedule identically: one KV pool size for the replica (the smallest rank's)
-            import torch.distributed as dist
+            num_blocks = _tp_num_blocks(model, dev, kv_fraction)
+    elif tp > 1:
+        from ..models.tp import TPLlamaModel
 
-            from ..models.llama import KVCache
-
-            torch.cuda.synchronize(dev)
-            free, _total = torch.cuda.mem_get_info(dev)
-            nb = torch.tensor([max(64, int(free * kv_fraction) // KVCache.bytes_per_block(model.cfg, 16))])
-            dist.all_reduce(nb, op=dist.ReduceOp.MIN)
-            num_blocks = int(nb.item())
+        rank, tp, comm = _tp_setup(spec, dev, cfg.hidden)
+        if spec.get("tp_shared"):
+            kv_fraction /= tp
+        model = TPLlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
+                             fp8_dense=bool(spec.get("fp8", False)), tp_rank=rank, tp_size=tp, tp_comm=comm)
+        num_blocks = _tp_num_blocks(model, dev, kv_fraction)
     else:
         model = LlamaModel(cfg, device=dev, seed=seed, weights_path=path, max_position=mlen + 64,
                            fp8_dense=bool(spec.get("fp8", False)))

@@ -231,10 +231,20 @@ class MixtralModel(LlamaModel):
         return h, None, None
 
     def _mlp_ep(self, h, L: MoELayerWeights) -> torch.Tensor:
-        """EP MoE layer: route locally, dispatch rows to the expert owners, combine locally."""
+        """EP MoE layer: route locally, dispatch rows to the expert owners, combine locally.  Padded mode on
+        the GPU runs the exchange as the ep.hip kernels (pack through the dispatch permutation, unpack,
+        back, combine: ExpertParallel.run_combined); the torch glue stays for CPU process groups and the
+        exact (prefill) mode."""
         k = self.full_cfg.experts_per_token
         h, hq, hs = self._split_act(h)
         _ids, w, row_off, src, inv = ops.moe_route(F.linear(h, L.router), k)
+        cap = None if self.ep_capacity is None else self.ep_capacity * k
+        if h.is_cuda and self.ep.mode == "padded":
+            if self.fp8 and hq is None:
+                hq, hs = ops.quant_fp8_rows(h)
+            return self.ep.run_combined(hq if self.fp8 else h, row_off, src, inv, w, k,
+                                        lambda xl, ro, sl: self._experts(xl, ro, L, sl),
+                                        x_scale=hs if self.fp8 else None, capacity=cap)
         idx = src.long()
         if self.fp8:
             if hq is None:
@@ -243,7 +253,6 @@ class MixtralModel(LlamaModel):
             ss = hs[idx]
         else:
             xs, ss = h[idx], None
-        cap = None if self.ep_capacity is None else self.ep_capacity * k
         y = self.ep.run(xs, row_off, lambda xl, ro, sl: self._experts(xl, ro, L, sl), x_scale=ss, capacity=cap)
         return ops.moe_combine(y.contiguous(), inv, w, k)
 

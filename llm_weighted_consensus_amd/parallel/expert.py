@@ -82,6 +82,53 @@ class ExpertParallel:
             raise ValueError(f"EP capacity {capacity} < rows {x_sorted.shape[0]}")
         return self._run_padded(x_sorted, row_off, expert_fn, x_scale, max(capacity, 1))
 
+    # ------------------------------------------------------------------ padded, device kernels (C4)
+    def run_combined(self, x: torch.Tensor, row_off: torch.Tensor, src: torch.Tensor, inv: torch.Tensor,
+                     w: torch.Tensor, k: int, expert_fn: ExpertFn, x_scale: Optional[torch.Tensor] = None,
+                     capacity: Optional[int] = None) -> torch.Tensor:
+        """The whole EP MoE exchange on the device for a padded-mode layer: ``x`` [T, d] token rows (bf16, or
+        e4m3 with per-row ``x_scale``), the router's expert segments ``row_off`` [E+1], dispatch
+        permutation ``src`` [T*k] (sorted row p reads token src[p]) and ``inv`` / ``w`` [T*k] -> the MoE
+        output [T, d_out] (weighted combine over each token's k experts).  Six launches besides the expert
+        GEMMs (csrc/kernels/ep.hip): pack (gather through src + counts header), all-to-all, unpack (expert-
+        major rows + local segments), back, all-to-all, combine — graph-capturable with the IPC all-to-all.
+        ``capacity``: rows per (source, destination) chunk, >= this rank's T*k, equal on every rank."""
+        if self.mode != "padded":
+            raise ValueError("run_combined is the padded-mode device path")
+        from .. import ops
+
+        K = ops.kernels()
+        W, El, dev = self.W, self.El, x.device
+        R = src.numel()
+        if capacity is None:
+            c = torch.tensor([R], dtype=torch.int64, device=dev)
+            pdist.all_reduce_(c, "max", group=self.group)
+            capacity = int(c.item())
+        C = max(int(capacity), 1)
+        if C < R:
+            raise ValueError(f"EP capacity {C} < rows {R}")
+        xb = x.contiguous()
+        row_bytes = xb.shape[1] * xb.element_size()
+        RB = -(-max(row_bytes + (4 if x_scale is not None else 0), El * 4) // 16) * 16
+        send = torch.empty(W, (C + 1) * RB, dtype=torch.uint8, device=dev)
+        K.ep_pack(xb, x_scale, src, row_off, W, El, C, send)
+        recv = torch.empty_like(send)
+        self._a2a(recv, send)
+        x_local = torch.empty(W * C, xb.shape[1], dtype=xb.dtype, device=dev)
+        s_local = torch.empty(W * C, dtype=torch.float32, device=dev) if x_scale is not None else None
+        rmap = torch.empty(W * C, dtype=torch.int32, device=dev)
+        row_off_local = torch.empty(El + 1, dtype=torch.int32, device=dev)
+        K.ep_unpack(recv, W, El, C, x_local.view(torch.uint8) if xb.dtype == torch.float8_e4m3fn else x_local,
+                    s_local, rmap, row_off_local)
+        y_local = expert_fn(x_local, row_off_local, s_local)                  # [W*C, d_out] expert-major
+        back = torch.empty(W * C, y_local.shape[1], dtype=y_local.dtype, device=dev)
+        K.ep_back(y_local.contiguous(), rmap, W, C, back)
+        ret = torch.empty_like(back)
+        self._a2a(ret, back)
+        out = torch.empty(inv.numel() // k, y_local.shape[1], dtype=y_local.dtype, device=dev)
+        K.ep_combine(ret, row_off, inv, w.reshape(-1).contiguous(), El, C, k, out)
+        return out
+
     # ------------------------------------------------------------------ padded (no host sync)
     def _run_padded(self, x, row_off, expert_fn, x_scale, C: int):
         W, El, dev = self.W, self.El, x.device

@@ -82,7 +82,9 @@ def tally_many_gpu(items: Sequence, device, stream=None) -> List[Tally]:
 
 class TallyBatcher:
     """Collects the tallies requested during one event-loop turn; ``min_batch`` or more run as one K10b
-    launch on ``device``, fewer on the host C++ tally.  ``device=None`` keeps everything on the host."""
+    launch on ``device`` (launched and read back on a worker thread), fewer on the host C++ tally.
+    ``device=None`` keeps everything on the host.  Each item is validated on its own first: a malformed
+    vote fails only its request."""
 
     def __init__(self, device=None, min_batch: int = 8):
         self.device = device
@@ -93,6 +95,7 @@ class TallyBatcher:
         self.gpu_tallies = 0
         self._stream = None  # created on the first GPU batch (a non-blocking side stream)
         self._sched_loop = None
+        self._executor = None  # one worker thread: GPU batches launch and read back off the event loop
 
     async def tally(self, voter_choices, C_len: int):
         votes, wts = vote_rows(voter_choices)
@@ -109,28 +112,56 @@ class TallyBatcher:
         batch, self._pending, self._scheduled = self._pending, [], False
         # skip cancelled futures and those of an event loop that has closed (nobody can await them)
         live = [b for b in batch if not b[3].done() and not b[3].get_loop().is_closed()]
-        if not live:
-            return
-        if self.device is not None and len(live) >= self.min_batch:
+        good = []
+        for item in live:  # a malformed vote fails its own request only (as the host tally would)
             try:
-                if self._stream is None:
-                    import torch
+                _check(item[0], item[1], item[2])
+                good.append(item)
+            except ValueError as e:
+                item[3].set_exception(e)
+        if not good:
+            return
+        if self.device is not None and len(good) >= self.min_batch:
+            # the launch and its read-back run on a worker thread: the event loop never blocks on a device
+            # sync (it keeps streaming other requests' chunks while the batch is on the GPU)
+            loop = good[0][3].get_loop()
+            if self._executor is None:
+                from concurrent.futures import ThreadPoolExecutor
 
-                    self._stream = torch.cuda.Stream(device=self.device)
-                res = tally_many_gpu([(v, w, c) for v, w, c, _ in live], self.device, self._stream)
-            except ValueError as e:  # a malformed vote: fail the requests like the host tally would
-                for *_, fut in live:
-                    fut.set_exception(e)
-                return
-            except Exception:  # noqa: BLE001 — a device error must not strand the awaiting requests:
-                res = None     # they fall back to the host tally below
-            if res is not None:
-                self.gpu_batches += 1
-                self.gpu_tallies += len(live)
-                for (_, _, _, fut), t in zip(live, res):
-                    fut.set_result(t)
-                return
-        for votes, wts, C, fut in live:
+                self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="k10b")
+            fut = loop.run_in_executor(self._executor, self._gpu_batch, [(v, w, c) for v, w, c, _ in good])
+            fut.add_done_callback(lambda f, good=good: self._deliver(good, f))
+            return
+        self._host(good)
+
+    def _gpu_batch(self, items):
+        import contextlib
+
+        import torch
+
+        on_cuda = str(self.device).startswith("cuda")
+        with torch.cuda.device(torch.device(self.device)) if on_cuda else contextlib.nullcontext():
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(device=self.device)
+            return tally_many_gpu(items, self.device, self._stream)
+
+    def _deliver(self, good, f) -> None:
+        try:
+            res = f.result()
+        except Exception:  # noqa: BLE001 — a device error must not strand the awaiting requests:
+            self._host(good)  # they fall back to the host tally
+            return
+        self.gpu_batches += 1
+        self.gpu_tallies += len(good)
+        for (_, _, _, fut), t in zip(good, res):
+            if not fut.done():
+                fut.set_result(t)
+
+    @staticmethod
+    def _host(items) -> None:
+        for votes, wts, C, fut in items:
+            if fut.done():
+                continue
             try:
                 fut.set_result(RT.tally(votes, wts, C))
             except Exception as e:  # noqa: BLE001 — surfaced to the awaiting request

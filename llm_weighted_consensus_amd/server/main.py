@@ -92,13 +92,10 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if cfg.device != "cpu":
         from ..score.tally_batch import make_batcher
 
-        spec = cfg.gpu_tally
-        if spec is None and services and not cfg.gpus:
-            # an in-process engine already owns this process's GPU: tallies of requests that finish in the
-            # same event-loop turn go to the batched kernel when there are at least 2 of them (K10b); the
-            # EngineGroup front end (LWC_GPUS) keeps the host tally and opens no GPU context of its own
-            spec = "2"
-        score.tally_batcher = make_batcher(spec, f"cuda:{cfg.gpu}")
+        # K10b is opt-in (LWC_GPU_TALLY=N): a request's tally is ~L x C <= 128 x 20 multiply-adds, and the
+        # serving A/B measured no throughput difference beyond run-to-run spread (profiles/serve_load.md),
+        # so the host C++ tally is the default
+        score.tally_batcher = make_batcher(cfg.gpu_tally, f"cuda:{cfg.gpu}")
     state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                            archive),
                      embedders=embedders, services=services, archive=archive, registry=registry)

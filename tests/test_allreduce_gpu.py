@@ -90,21 +90,26 @@ def test_ipc_allreduce_two_ranks_one_gpu(gpu):
     assert res == {0: [], 1: []}, res
 
 
-def _tp_worker(rank, world, port, fp8, q):
+def _tp_worker(rank, world, port, fp8, q, arch="mixtral-tiny"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
     try:
         from llm_weighted_consensus_amd.models.config import decoder_config
         from llm_weighted_consensus_amd.models.llama import KVCache
         from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+        from llm_weighted_consensus_amd.models.tp import TPLlamaModel
         from llm_weighted_consensus_amd.parallel import dist as pdist
         from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
 
         pdist.init_from_env("cuda")
         dev = torch.device("cuda", 0)
         comm = CustomAllReduce(device=dev, max_bytes=1 << 20, blocks=16)
-        m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
-                         tp_rank=rank, tp_size=world, tp_comm=comm)
+        if arch.startswith("mixtral"):
+            m = MixtralModel(decoder_config(arch), device=dev, seed=4, max_position=512, fp8=fp8,
+                             tp_rank=rank, tp_size=world, tp_comm=comm)
+        else:
+            m = TPLlamaModel(decoder_config(arch), device=dev, seed=4, max_position=512, fp8_dense=fp8,
+                             tp_rank=rank, tp_size=world, tp_comm=comm)
         assert m.graph_safe
         g = torch.Generator().manual_seed(9)
         P = 29
@@ -123,22 +128,26 @@ def _tp_worker(rank, world, port, fp8, q):
         q.put((rank, repr(e)))
 
 
-def test_mixtral_tp2_through_ipc_allreduce(gpu):
+@pytest.mark.parametrize("arch", ["mixtral-tiny", "llama-tiny"])
+def test_tp2_through_ipc_allreduce(gpu, arch):
+    """TP=2 prefill logits (two ranks on one GPU, IPC one-shot all-reduce after o and after down) match TP=1:
+    the MoE decoder (experts column-split) and the dense one (TPLlamaModel: heads and FFN columns split)."""
     from llm_weighted_consensus_amd.models.config import decoder_config
-    from llm_weighted_consensus_amd.models.llama import KVCache
+    from llm_weighted_consensus_amd.models.llama import KVCache, LlamaModel
     from llm_weighted_consensus_amd.models.mixtral import MixtralModel
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, False, q)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, False, q, arch)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
     for p in procs:
         p.join(timeout=120)
     assert all(isinstance(v, torch.Tensor) for v in res.values()), res
-    m = MixtralModel(decoder_config("mixtral-tiny"), device=gpu, seed=4, max_position=512)
+    cls = MixtralModel if arch.startswith("mixtral") else LlamaModel
+    m = cls(decoder_config(arch), device=gpu, seed=4, max_position=512)
     g = torch.Generator().manual_seed(9)
     P = 29
     toks = torch.randint(0, m.cfg.vocab_size, (P,), generator=g).to(gpu)

@@ -146,7 +146,9 @@ def test_paged_decode(gpu, G, splits, decode_path):
 @pytest.mark.parametrize("G", [4, 2, 1, 8])
 def test_paged_decode_cascade(gpu, G):
     """One-launch cascade kernel (LDS-staged shared prompt + per-sequence suffix) == reference, over
-    groups spanning several super-tiles, odd prefix block counts, plain rows and NaN-poisoned slots."""
+    groups spanning several super-tiles, odd prefix block counts, plain rows and NaN-poisoned slots; a
+    prompt of one LDS chunk takes the interleaved pass (its DMA overlapping the suffix loads, its pairs
+    attended between suffix pairs), a longer one (19 blocks > 16) the chunked pass."""
     from llm_weighted_consensus_amd import ops
     from llm_weighted_consensus_amd.engine.engine import cascade_tiles
 
@@ -155,10 +157,10 @@ def test_paged_decode_cascade(gpu, G):
     Hq = Hkv * G
     per = ops.cascade_rows_per_tile(G)
     # (count, prefix blocks): a group larger than one super-tile, an odd prefix, a singleton, a
-    # group with an empty prefix (plain), and a short group
-    groups = [(per + 9, 2), (7, 5), (1, 4), (3, 0), (3, 3)]
+    # group with an empty prefix (plain), a short group, and a prompt longer than one LDS chunk
+    groups = [(per + 9, 2), (7, 5), (1, 4), (3, 0), (3, 3), (5, 19)]
     B = sum(c for c, _ in groups)
-    width = 12
+    width = 24
     NB = 4 + sum(p + c * (width - p) for c, p in groups)
     kc = _bf(NB, Hkv, BS, D, dev=gpu)
     vc = _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
@@ -194,6 +196,52 @@ def test_paged_decode_cascade(gpu, G):
     out = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D))
     assert torch.isfinite(out.float()).all()
     for b in range(B):
+        L = int(ctx[b])
+        toks = torch.arange(L, device=gpu)
+        blk = bt[b, toks // BS].long()
+        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
+                          False, 1 / math.sqrt(D))[0]
+        _close(out[b], o, 2e-2, 2e-2)
+
+
+def test_paged_decode_cascade_short_tile_q_at_allocation_end(gpu):
+    """Round-3 fault regression: a super-tile with fewer sequences than waves leaves waves that own no
+    sequence; they must not read Q rows past the batch.  q is a view ending exactly at the end of its own
+    2 MiB-multiple allocation (a caching-allocator segment of its own), B = 33 gives a last super-tile of one
+    sequence, and the result must equal the reference (an out-of-bounds read past q faulted here)."""
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.engine.engine import cascade_tiles
+
+    G, Hkv, D, BS = 4, 8, 128, 16
+    Hq = Hkv * G
+    per = ops.cascade_rows_per_tile(G)
+    B, pblk, width = per + 1, 3, 6
+    NB = pblk + B * (width - pblk) + 2
+    kc = _bf(NB, Hkv, BS, D, dev=gpu)
+    vc = _bf(NB, Hkv, BS // 4, D, 4, dev=gpu)
+    bt = torch.zeros(B, width, dtype=torch.int32)
+    ctx = torch.zeros(B, dtype=torch.int32)
+    nxt = pblk
+    for b in range(B):
+        L = pblk * BS + 5 + b % 30
+        nb = -(-L // BS)
+        bt[b, :pblk] = torch.arange(pblk, dtype=torch.int32)
+        bt[b, pblk:nb] = torch.arange(nxt, nxt + nb - pblk, dtype=torch.int32)
+        nxt += nb - pblk
+        ctx[b] = L
+    tiles_np = np.zeros((-(-B // per) + 3, 3), dtype=np.int32)
+    cascade_tiles([(0, B, pblk)], per, tiles_np)
+    assert tiles_np[1, 1] == 1  # the short last super-tile: one sequence, seven idle waves
+    stride = (Hq + 2 * Hkv) * D
+    seg = 2 << 20
+    total = -(-(B * stride * 2) // seg) * seg  # bytes: a whole number of 2 MiB pages
+    buf = torch.empty(total // 2, dtype=torch.bfloat16, device=gpu)
+    q_full = buf[buf.numel() - B * stride:].view(B, stride)
+    q_full.copy_(_bf(B, stride, dev=gpu))
+    bt, ctx, tiles = bt.to(gpu), ctx.to(gpu), torch.from_numpy(tiles_np).to(gpu)
+    out = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D))
+    torch.cuda.synchronize()
+    for b in (0, per - 1, per):
         L = int(ctx[b])
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()

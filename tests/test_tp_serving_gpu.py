@@ -12,14 +12,14 @@ pytestmark = pytest.mark.gpu
 SPEC = {"arch": "mixtral-tiny", "weights": "random:4", "max_model_len": 512, "max_batch": 64}
 
 
-def _serve(tp: int, bodies):
+def _serve(tp: int, bodies, arch="mixtral-tiny"):
     import httpx
 
     from llm_weighted_consensus_amd.server.app import create_app
     from llm_weighted_consensus_amd.server.config import Config
     from llm_weighted_consensus_amd.server.main import build_state
 
-    spec = dict(SPEC, tp=tp)
+    spec = dict(SPEC, tp=tp, arch=arch)
     state = build_state(Config(models={"moe": spec}, kv_fraction=0.2, gpus=[0] * tp, chunked_prefill=64))
     try:
         group = state.services["moe"]
@@ -51,11 +51,13 @@ def _trace(resp):
 
 
 @pytest.mark.timeout(600)
-def test_tp2_replica_serves_chat_like_tp1():
+@pytest.mark.parametrize("arch", ["mixtral-tiny", "llama-tiny"])
+def test_tp2_replica_serves_chat_like_tp1(arch):
+    """The MoE replica and the dense one (TPLlamaModel: a Llama-class voter at "tp": 2)."""
     body = {"model": "moe", "messages": [{"role": "user", "content": "Name three rivers of Europe, briefly."}],
             "n": 3, "temperature": 0, "max_tokens": 12, "logprobs": True, "top_logprobs": 3}
-    tp2 = _serve(2, [body, body])
-    tp1 = _serve(1, [body])
+    tp2 = _serve(2, [body, body], arch)
+    tp1 = _serve(1, [body], arch)
     a, b, ref = _trace(tp2[0]), _trace(tp2[1]), _trace(tp1[0])
     assert len(a) == 3 and all(len(c) == 12 for c in a)
     # the repeat takes the prompt from the prefix cache (other kernels for the head): equal up to float noise

@@ -186,3 +186,23 @@ def test_server_wiring(monkeypatch):
     assert st.score.tally_batcher is not None and st.score.tally_batcher.min_batch == 4
     assert build_state(Config()).score.tally_batcher is None
     assert build_state(Config(device="cpu", gpu_tally="4")).score.tally_batcher is None
+
+
+def test_batcher_fails_only_the_malformed_request(monkeypatch):
+    """one malformed vote (wrong length) fails its own request; the rest of the batch is tallied
+    (here on the host path: device None)."""
+    rng = random.Random(5)
+    good = [(_request(rng, 3, 4), 3) for _ in range(3)]
+    bad_ch, _ = _request(rng, 3, 4), 3
+
+    async def main():
+        b = TB.TallyBatcher(device=None, min_batch=2)
+        bad = [_Choice([1.0, 0.0], 1.0)] + list(bad_ch[1:])  # 2 entries for 3 choices
+        return await asyncio.gather(*([b.tally(ch, C) for ch, C in good] + [b.tally(bad, 3)]),
+                                    return_exceptions=True)
+
+    outs = asyncio.run(main())
+    assert isinstance(outs[-1], ValueError)
+    for (ch, C), t in zip(good, outs[:-1]):
+        votes, wts = TB.vote_rows(ch)
+        assert list(t.confidence) == list(RT.tally(votes, wts, C).confidence)
