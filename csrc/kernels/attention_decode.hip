@@ -34,6 +34,12 @@ namespace lwc {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t uint2v __attribute__((ext_vector_type(2)));
 
+// K = 16 form for PV: one block's 4 tokens per lane group (operands are 8-byte halves of the 16 B V loads)
+LWC_DEVICE float4v mfma16k16(const uint2v& a, const uint2v& b, const float4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(short4v, a), __builtin_bit_cast(short4v, b), c,
+                                                   0, 0, 0);
+}
+
 LWC_DEVICE float4v mfma16(const short8& a, const short8& b, const float4v& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
                                                  0, 0);
@@ -60,11 +66,11 @@ struct DecodeParams {
 // K and V registers of one PAIR of 16-token blocks for one wave (K: 8 x 16 B, V: 16 x 8 B per lane).
 struct PairRegs {
   short8 ka[4], kb[4];
-  uint4v v[8];  // PV B operand of dim 16n + r16: {A tokens 4g..4g+3 | B tokens 4g..4g+3}, loaded in place
+  // PV operands, loaded in place: va[m] (vb[m]) = block A's (B's) tokens 4g..4g+3 of dims 32m + 2 r16 (low
+  // 8 B: n-tile 2m) and 32m + 2 r16 + 1 (high 8 B: n-tile 2m+1) — one 16 B load each
+  uint4v va[4], vb[4];
 };
 
-// 8 bytes of A tokens and 8 of B tokens as one 16-byte MFMA operand (the two loads land in its halves)
-LWC_DEVICE uint4v join_v(const uint2v& a, const uint2v& b) { return uint4v{a[0], a[1], b[0], b[1]}; }
 
 // Token rows at or past `ctx` (the tail of a sequence's last block, or a pair without a B block) are
 // not fetched: each (block, head) segment is addressed through a 4 KiB buffer resource and the lanes
@@ -98,6 +104,13 @@ LWC_DEVICE void load_pair_k(PairRegs& r, const DecodeParams& p, const int* bt, i
   }
 }
 
+// Output dimension of accumulator n in lane r16: n-tiles pair up (2m, 2m+1) over 32 dims, the lane owning
+// two ADJACENT dims of each pair, so a lane's V operands for both tiles are ONE 16 B load per block (the
+// [BS/4][D][4] layout stores a token group's adjacent dims contiguously; the PV MFMA is the K = 16 form per
+// block, whose 8-byte B operands are the halves of that load): 8 full-line 16 B loads per pair instead of
+// 16 half-width 8 B ones.  Every epilogue writes o[n] to odim(n, r16).
+LWC_DEVICE int odim(int n, int r16) { return 32 * (n >> 1) + 2 * r16 + (n & 1); }
+
 LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
                             int g, int ctx = 0x7fffffff) {
   const size_t kv_head_stride = (size_t)kBS * kD;
@@ -107,12 +120,13 @@ LWC_DEVICE void load_pair_v(PairRegs& r, const DecodeParams& p, const int* bt, i
   const __amdgpu_buffer_rsrc_t rB = seg_rsrc(p.vc + ((size_t)physB * p.Hkv + kvh) * kv_head_stride);
   const bool okA = blkA * kBS + 4 * g < ctx;  // lane group g holds tokens 4g..4g+3
   const bool okB = hasB && (blkA + 1) * kBS + 4 * g < ctx;
-  const int base = (g * kD + r16) * 8;  // tokens 4g..4g+3 of dim 16n + r16: [BS/4][D][4] layout
+  const int base = (g * kD + 2 * r16) * 8;  // tokens 4g..4g+3 of dims 32m + 2 r16, +1: [BS/4][D][4] layout
   const int oA = okA ? base : kOOB, oB = okB ? base : kOOB;
 #pragma unroll
-  for (int n = 0; n < 8; ++n)
-    r.v[n] = join_v(__builtin_bit_cast(uint2v, __builtin_amdgcn_raw_buffer_load_b64(rA, oA + 128 * n, 0, 0)),
-                    __builtin_bit_cast(uint2v, __builtin_amdgcn_raw_buffer_load_b64(rB, oB + 128 * n, 0, 0)));
+  for (int m = 0; m < 4; ++m) {
+    r.va[m] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rA, oA + 256 * m, 0, 0));
+    r.vb[m] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rB, oB + 256 * m, 0, 0));
+  }
 }
 
 LWC_DEVICE void load_pair(PairRegs& r, const DecodeParams& p, const int* bt, int kvh, int blkA, bool hasB, int r16,
@@ -183,26 +197,48 @@ LWC_DEVICE void pair_softmax(const float4v& sa, const float4v& sb, int blkA, boo
   }
 }
 
-// O += P V for the pair.  Cache slots past the context may hold stale/uninitialised bits (possibly
-// NaN): P = 0 there, but 0 * NaN = NaN, so in a pair that reaches past the context those V
-// elements are zeroed by select, not arithmetic.  Pairs fully inside take the select-free path.
+// O += P V for the pair: per n-tile pair m, four K = 16 MFMAs (block A's and block B's 4 tokens per lane
+// group, dims 2m / 2m+1 of the lane's 16 B loads; the P operand halves are the A / B score registers).
+// Cache slots past the context may hold stale/uninitialised bits (possibly NaN): P = 0 there, but
+// 0 * NaN = NaN, so in a pair that reaches past the context those V elements are zeroed by select, not
+// arithmetic.  Pairs fully inside take the select-free path.
+LWC_DEVICE uint2v lo2(const uint4v& v) { return uint2v{v[0], v[1]}; }
+LWC_DEVICE uint2v hi2(const uint4v& v) { return uint2v{v[2], v[3]}; }
+
+LWC_DEVICE void pv_mfmas(const short8& pf, const uint4v (&va)[4], const uint4v (&vb)[4], float4v (&o)[8]) {
+  const uint4v pw = __builtin_bit_cast(uint4v, pf);
+  const uint2v pa = lo2(pw), pb = hi2(pw);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    o[2 * m] = mfma16k16(pa, lo2(va[m]), o[2 * m]);
+    o[2 * m + 1] = mfma16k16(pa, hi2(va[m]), o[2 * m + 1]);
+    o[2 * m] = mfma16k16(pb, lo2(vb[m]), o[2 * m]);
+    o[2 * m + 1] = mfma16k16(pb, hi2(vb[m]), o[2 * m + 1]);
+  }
+}
+
 LWC_DEVICE void pair_values(const PairRegs& r, const short8& pf, int blkA, bool hasB, int ctx, int g,
                             float4v (&o)[8]) {
   const int blkB = blkA + 1;
   if (hasB && (blkB + 1) * kBS <= ctx) {  // wave-uniform
-#pragma unroll
-    for (int n = 0; n < 8; ++n) o[n] = mfma16(pf, __builtin_bit_cast(short8, r.v[n]), o[n]);
+    pv_mfmas(pf, r.va, r.vb, o);
     return;
   }
-  // tokens of this lane's 4-token groups inside the context: a bit mask per 16-bit element, applied to
-  // each operand with 4 ANDs (NaN bits become +0)
+  // tokens of this lane's 4-token groups inside the context: a bit mask per 16-bit element (both dims of a
+  // 16 B load share the tokens), applied with ANDs (NaN bits become +0)
   const int nA = min(max(ctx - (blkA * kBS + 4 * g), 0), 4);
   const int nB = hasB ? min(max(ctx - (blkB * kBS + 4 * g), 0), 4) : 0;
   const unsigned long long mA = nA >= 4 ? ~0ull : ((1ull << (16 * nA)) - 1);
   const unsigned long long mB = nB >= 4 ? ~0ull : ((1ull << (16 * nB)) - 1);
-  const uint4v m{(uint32_t)mA, (uint32_t)(mA >> 32), (uint32_t)mB, (uint32_t)(mB >> 32)};
+  const uint4v qa{(uint32_t)mA, (uint32_t)(mA >> 32), (uint32_t)mA, (uint32_t)(mA >> 32)};
+  const uint4v qb{(uint32_t)mB, (uint32_t)(mB >> 32), (uint32_t)mB, (uint32_t)(mB >> 32)};
+  uint4v va[4], vb[4];
 #pragma unroll
-  for (int n = 0; n < 8; ++n) o[n] = mfma16(pf, __builtin_bit_cast(short8, r.v[n] & m), o[n]);
+  for (int m = 0; m < 4; ++m) {
+    va[m] = r.va[m] & qa;
+    vb[m] = r.vb[m] & qb;
+  }
+  pv_mfmas(pf, va, vb, o);
 }
 
 // One whole pair: scores, softmax, values.
@@ -278,7 +314,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int n = 0; n < 8; ++n)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s_o[wid][4 * g + r][16 * n + r16] = o[n][r];
+    for (int r = 0; r < 4; ++r) s_o[wid][4 * g + r][odim(n, r16)] = o[n][r];
   __syncthreads();
   // thread t: row h = t / 16 (< nrows), dims 8*(t%16) .. +8
   const int t = threadIdx.x;
@@ -377,12 +413,12 @@ __global__ void __launch_bounds__(256) paged_decode_wave_kernel(DecodeParams p, 
     if (p.num_splits > 1) {
       float* dst = p.part_o + (bh * p.num_splits + split) * kD;
 #pragma unroll
-      for (int n = 0; n < 8; ++n) dst[16 * n + r16] = o[n][i] * inv;
+      for (int n = 0; n < 8; ++n) dst[odim(n, r16)] = o[n][i] * inv;
       if (r16 == 0) p.part_lse[bh * p.num_splits + split] = li > 0.f ? mi + log2f(li) : -INFINITY;
     } else {
       bf16_t* dst = p.out + bh * kD;
 #pragma unroll
-      for (int n = 0; n < 8; ++n) dst[16 * n + r16] = f2bf(o[n][i] * inv);
+      for (int n = 0; n < 8; ++n) dst[odim(n, r16)] = f2bf(o[n][i] * inv);
     }
   }
 }
@@ -481,9 +517,8 @@ __global__ void __launch_bounds__(kCWaves * 64)
           if (seg < 2) {  // K [16 tok][256 B]: 16 B chunk XOR row
             const int row = pos >> 4, pch = pos & 15;
             src += row * 256 + ((pch ^ row) << 4);
-          } else {  // V [4 token groups][128 dim][8 B]: odd groups XOR byte bit 7 (ds_read_b64 halves)
-            const int b = pos << 4;
-            src += b ^ (((b >> 10) & 1) << 7);
+          } else {  // V [4 token groups][128 dim][8 B], linear: the 16 B reads (dims 2 r16, +1 of a group)
+            src += pos << 4;  // of one lane group span 256 contiguous bytes = every bank once
           }
           unsigned char* dst = smem + pi * kPairBytes + (rd * (kCWaves * 64) + wid * 64) * 16;
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -504,10 +539,10 @@ __global__ void __launch_bounds__(kCWaves * 64)
       r.kb[s] = *reinterpret_cast<const short8*>(pb + kSegBytes + r16 * 256 + ch);
     }
 #pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      const int off = ((g * kD + 16 * n + r16) << 3) ^ ((g & 1) << 7);
-      r.v[n] = join_v(*reinterpret_cast<const uint2v*>(pb + 2 * kSegBytes + off),
-                      *reinterpret_cast<const uint2v*>(pb + 3 * kSegBytes + off));
+    for (int m2 = 0; m2 < 4; ++m2) {
+      const int off = (g * kD + 32 * m2 + 2 * r16) << 3;
+      r.va[m2] = *reinterpret_cast<const uint4v*>(pb + 2 * kSegBytes + off);
+      r.vb[m2] = *reinterpret_cast<const uint4v*>(pb + 3 * kSegBytes + off);
     }
     attend_pair(r, blkA, hasB, pctx, qf, sl2, g, o, m, l);
   };
@@ -643,7 +678,7 @@ __global__ void __launch_bounds__(kCWaves * 64)
     const float inv = li > 0.f ? 1.f / li : 0.f;
     bf16_t* dst = p.out + ((size_t)seq * p.Hq + hq) * kD;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) dst[16 * n + r16] = f2bf(o[n][i] * inv);
+    for (int n = 0; n < 8; ++n) dst[odim(n, r16)] = f2bf(o[n][i] * inv);
   }
 }
 

@@ -4,8 +4,9 @@ One process per GPU; `torch.distributed` backend "nccl" IS RCCL on ROCm.  On CPU
 code runs over gloo.  Collectives used by the serving/bench paths:
 
   C1 all_gather of candidate embeddings  [n_local, d] -> [world, n_local, d]
-  C2 combine of votes / tallies          one object all-gather of the voter choices per request, ordered
-                                         by request number (parallel/votes.py, score/sharded.py)
+  C2 voter shares / votes                leader <-> follower TCP links, not collectives: a dead peer must
+                                         cost its voters, not the request (parallel/shard_link.py,
+                                         score/sharded.py)
   C3 TP all-reduce                       (tensor-parallel decoders; IPC one-shot kernel, parallel/allreduce.py)
   C4 all_to_all_single                   (expert-parallel MoE dispatch / combine, parallel/expert.py)
   C5 broadcast / barrier                 (control)
@@ -191,11 +192,13 @@ def world_size_seen() -> int:
     return int(t.item())
 
 
-def broadcast_object(obj, src: int = 0):
-    if not _INFO.enabled:
+def broadcast_object(obj, src: int = 0, group=None):
+    """``obj`` of group rank ``src`` on every rank of ``group`` (default: the world)."""
+    if group is None and not _INFO.enabled:
         return obj
     lst = [obj]
-    dist.broadcast_object_list(lst, src=src)
+    gsrc = dist.get_global_rank(group, src) if group is not None else src
+    dist.broadcast_object_list(lst, src=gsrc, group=group)
     return lst[0]
 
 

@@ -84,7 +84,9 @@ class LinkServer:
                 sock.close()
                 continue
             rank = int(hello[1])
-            sock.settimeout(None)
+            # one timeout for both directions: a reader that hears nothing (not even a heartbeat) for
+            # dead_s, or a send the peer stops draining, ends in socket.timeout -> the rank is dead
+            sock.settimeout(self.dead_s)
             self.conns[rank] = sock
             self.locks[rank] = threading.Lock()
             self.last_seen[rank] = time.monotonic()
@@ -105,7 +107,6 @@ class LinkServer:
         sock = self.conns[rank]
         try:
             with self.locks[rank]:
-                sock.settimeout(self.dead_s)
                 _send(sock, msg)
             return True
         except (OSError, ValueError):
@@ -224,7 +225,7 @@ def open_links(group=None, hb_s: Optional[float] = None, dead_s: Optional[float]
     ``LWC_SHARD_LINK_HOST`` (the leader's address as the followers reach it; default MASTER_ADDR)."""
     import torch.distributed as dist
 
-    from . import votes as V
+    from .dist import broadcast_object
 
     hb = float(os.environ.get("LWC_SHARD_HB_S", "0.5")) if hb_s is None else hb_s
     dead = float(os.environ.get("LWC_SHARD_DEAD_S", "10")) if dead_s is None else dead_s
@@ -232,8 +233,8 @@ def open_links(group=None, hb_s: Optional[float] = None, dead_s: Optional[float]
     if rank == 0:
         host = os.environ.get("LWC_SHARD_LINK_HOST", os.environ.get("MASTER_ADDR", "127.0.0.1"))
         srv = LinkServer(world, host, hb, dead)
-        V.broadcast_object(srv.address, 0, group)
+        broadcast_object(srv.address, 0, group)
         srv.accept_all()
         return srv
-    addr = V.broadcast_object(None, 0, group)
+    addr = broadcast_object(None, 0, group)
     return LinkClient(addr, rank, hb)

@@ -33,14 +33,21 @@ variables configure the local engine:
   LWC_REQUEST_TIMEOUT_MS  default request deadline (an x-timeout-ms header overrides it per request; the
                     engine drops or aborts a request past its deadline); x-priority orders admission
   LWC_SHARD_VOTERS  1: voter-sharded deployment — one server process per GPU under torchrun / a
-                    launcher (RANK / WORLD_SIZE / LOCAL_RANK); rank 0 serves HTTP and broadcasts each
-                    score request, every rank runs its share of the voters (llm index % world) on its
-                    own GPU, requests run concurrently and each combines its voters with one all-gather
-                    (C2, score/sharded.py)
+                    launcher (RANK / WORLD_SIZE / LOCAL_RANK); rank 0 serves HTTP, resolves each score
+                    request once and sends every live follower its share of the voters over a TCP link
+                    (voter i -> live[i % len(live)]); followers stream every voter chunk back as it is
+                    produced and rank 0 merges them live and tallies (C2, score/sharded.py,
+                    parallel/shard_link.py)
+  LWC_SHARD_HB_S    follower heartbeat period on the shard links (default 0.5 s)
+  LWC_SHARD_DEAD_S  silence after which a follower counts as dead (default 10 s; a closed socket — a
+                    follower process that exited — counts at once): its unfinished voters become error
+                    choices and later requests run on the survivors
+  LWC_SHARD_WAIT_S  bound on a request's wait for its followers when it carries no deadline (default 300 s;
+                    with a deadline: the deadline plus LWC_SHARD_GRACE_S, default 5 s)
   LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
-                    and batches of at least N run as one vote_tally launch (K10b) on this process's GPU;
-                    0: the host C++ tally per request.  Default: 2 when a local engine runs in this
-                    process (it owns the GPU already), 0 otherwise (CPU, EngineGroup front end)
+                    and batches of at least N run as one vote_tally launch (K10b) on this process's GPU
+                    (launched and read back on a worker thread); unset / 0 (the default): the host C++
+                    tally per request
 """
 from __future__ import annotations
 
