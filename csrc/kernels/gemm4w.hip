@@ -260,8 +260,63 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
+    // VAR 32: the library kernel's segment shape (hipBLASLt's MT256x256x64 DTL loop, disassembled: the same
+    // 128 MFMA / 32 ds_read_b128 / 16 LDS-DMA per K tile, two barriers).  seg A: the Y reads of tile R back
+    // to back, one per k-step-0 MFMA, then a few more MFMAs, lgkmcnt(0), barrier; seg B: the long middle —
+    // the rest of k-step 0 and most of k-step 1 — carrying the tile R+2 DMA pieces one per ~5 MFMAs at raised
+    // wave priority (s_setprio 3), vmcnt, barrier; seg C: the last k-step-1 MFMAs with the X reads of tile
+    // R+1 one per MFMA.  Waits land after sections with no loads of their own in flight behind them.
+    constexpr int HA = G::Reads + M1 / 6;        // seg A MFMAs (k-step 0)
+    constexpr int HC = G::Reads + M1 / 8;        // seg C MFMAs (k-step 1)
+    constexpr int HB = 2 * M1 - HA - HC;          // seg B MFMAs (k-step 0 rest, then k-step 1)
+#define G4_TILE_H(R, STAGE, NEXT)                                                                   \
+  {                                                                                                 \
+    uint8_t* cur = smem + ((R) & 1) * G::Buf;                                                       \
+    uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
+    _Pragma("unroll") for (int m = 0; m < HA; ++m) {                                                \
+      if (m < G::Reads) rd1(cur, offA1, offB1, ya, yb, m);                                          \
+      mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                            \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    G4_LGKM0();                                                                                     \
+    G4_BAR();                                                                                       \
+    if constexpr (STAGE) __builtin_amdgcn_s_setprio(3);                                             \
+    _Pragma("unroll") for (int q = 0; q < HB; ++q) {                                                \
+      if constexpr (STAGE) {                                                                        \
+        if (q * G::Pieces / HB != (q + 1) * G::Pieces / HB) piece(cur, (R) + 2, q * G::Pieces / HB); \
+      }                                                                                             \
+      const int m = HA + q;                                                                         \
+      if (m < M1)                                                                                   \
+        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+      else                                                                                          \
+        mfma(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    if constexpr (STAGE) {                                                                          \
+      __builtin_amdgcn_s_setprio(0);                                                                \
+      G4_VM(G::Pieces);                                                                             \
+    } else {                                                                                        \
+      G4_VM(0);                                                                                     \
+    }                                                                                               \
+    G4_BAR();                                                                                       \
+    _Pragma("unroll") for (int c = 0; c < HC; ++c) {                                                \
+      if constexpr (NEXT) {                                                                         \
+        if (c < G::Reads) rd1(nxt, offA0, offB0, xa, xb, c);                                        \
+      }                                                                                             \
+      const int m = M1 - HC + c;                                                                    \
+      mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                            \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+  }
     int r = 0;
-    if constexpr (VAR == 8) {
+    if constexpr (VAR == 32) {
+      for (; r + 2 < nt; ++r) G4_TILE_H(r, true, true)
+      if (nt >= 2) {
+        G4_TILE_H(r, false, true)
+        ++r;
+      }
+      G4_TILE_H(r, false, false)
+    } else if constexpr (VAR == 8) {
       for (; r + 2 < nt; ++r) G4_TILE1(r, true, true)
       if (nt >= 2) {
         G4_TILE1(r, false, true)
@@ -278,6 +333,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }
 #undef G4_TILE
 #undef G4_TILE1
+#undef G4_TILE_H
     G4_MFMA_DRAIN();  // accumulators are read by VALU / stores from here on
     __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
 
@@ -400,6 +456,7 @@ int launch(const Params& p, hipStream_t s) {
   // schedule variant (VAR bits, see the main loop): LWC_G4_VAR, an A/B knob (scripts/microbench.py g4ab);
   // the plain epilogue carries every variant, the fused ones the default
   const int var = env_int("LWC_G4_VAR", 1);
+  if (var == 32) return launch3<EPI, NT, 32>(p, s);
   if constexpr (EPI == EPI_PLAIN) {
     switch (var) {
       case 0: return launch3<EPI, NT, 0>(p, s);

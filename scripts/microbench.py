@@ -246,7 +246,8 @@ def gemm4w_ab(dev):
         # only the plain epilogue carries every variant)
         for k in [k for k in runs if k.startswith("g4")]:
             fn = runs.pop(k)
-            for v in (os.environ.get("G4_VARS", "1,3,5,7") if epi == "plain" else "1").split(","):
+            for v in (os.environ.get("G4_VARS", "1,3,5,7") if epi == "plain"
+                      else os.environ.get("G4_VARS_EPI", "1")).split(","):
                 runs[f"{k}v{v}"] = (lambda fn=fn, v=v: (os.environ.__setitem__("LWC_G4_VAR", v), fn()))
         res = {k: [] for k in runs}
         for _ in range(5):
