@@ -67,6 +67,7 @@ def bench_moe(a):
     from llm_weighted_consensus_amd.models.embedder import DecoderEmbedder
     from llm_weighted_consensus_amd.models.llama import LlamaModel
     from llm_weighted_consensus_amd.models.mixtral import MixtralModel
+    from llm_weighted_consensus_amd.models.tp import TPLlamaModel
     from llm_weighted_consensus_amd.parallel import dist as pdist
 
     info = pdist.init_from_env("cuda")
@@ -87,9 +88,16 @@ def bench_moe(a):
         comm = CustomAllReduce(group=tp_group, device=dev, max_bytes=a.requests * a.candidates * dcfg.hidden * 2)
     model = MixtralModel(dcfg, device=dev, seed=11, max_position=a.prompt_len + a.gen_len + 64, fp8=not a.bf16,
                          tp_rank=tp_rank, tp_size=tp, tp_group=tp_group, tp_comm=comm)
-    # config 5 is fp8 throughout: the embedder's projections too (e4m3 + per-channel scales, fp8 library GEMM)
-    emb_model = LlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64,
-                           fp8_dense=not a.bf16)
+    # config 5 is fp8 throughout: the embedder's projections too (e4m3 + per-channel scales, fp8 library GEMM).
+    # --embedder-par tp (config 5's "TP=2 each"): the embedder's heads / FFN columns split over the TP group
+    # like the sampler's, every rank embeds all N candidates, its two all-reduces per layer go through the
+    # process group (RCCL; [tokens, d] is GBs per call, beyond the IPC buffer).  dp: each rank holds the whole
+    # embedder and embeds 1/tp of the candidates, one all-gather assembles them — same FLOPs, no per-layer
+    # collective.
+    emb_tp = tp if a.embedder_par == "tp" else 1
+    emb_model = TPLlamaModel(decoder_config(a.embedder), device=dev, seed=12, max_position=a.gen_len + 64,
+                             fp8_dense=not a.bf16, tp_rank=tp_rank if emb_tp > 1 else 0, tp_size=emb_tp,
+                             tp_group=tp_group)
     scorer = EmbeddingConsensus(DecoderEmbedder(emb_model, max_tokens=a.gen_len + 16), tau=0.05)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     R, N = a.requests, a.candidates
@@ -110,11 +118,14 @@ def bench_moe(a):
             groups.append(engine.add_request(p, sp, n=N))
         while engine.has_work():
             engine.step()
-        # the TP ranks hold the same candidates: each embeds its 1/tp share, one all-gather (C1) inside the
-        # TP group assembles all N per request, and both run the (tiny) consensus
+        # the TP ranks hold the same candidates.  dp embedder: each embeds its 1/tp share, one all-gather (C1)
+        # inside the TP group assembles all N per request; tp embedder: each embeds all N with its weight
+        # shard.  Both ranks then run the (tiny) consensus
+        if emb_tp > 1 or tp == 1:
+            return scorer.score([[s.tokens for s in gr.seqs] for gr in groups])
         n_loc = N // tp
         return scorer.score([[s.tokens for s in gr.seqs[tp_rank * n_loc:(tp_rank + 1) * n_loc]] for gr in groups],
-                            gather=tp > 1, group=tp_group)
+                            gather=True, group=tp_group)
 
     for i in range(a.warmup):
         step(i)
@@ -138,6 +149,8 @@ def bench_moe(a):
                        "seq_len": a.prompt_len + a.gen_len,
                        "parallelism": f"tp{tp} x dp{dp}" + (" (ranks SHARE one GPU: a rehearsal of the protocol, "
                                                             "not a multi-GPU number)" if shared else ""),
+                       "embedder": f"tp{emb_tp}" if emb_tp > 1 else (f"dp{tp} inside the TP group" if tp > 1 else
+                                                                      "one GPU"),
                        "tp_allreduce": ("ipc one-shot kernel (hipGraph)" if comm is not None else
                                         "process group (eager)" if tp > 1 else "none")}}
 
@@ -157,6 +170,9 @@ def main():
     ap.add_argument("--embedder", default="e5-mistral-7b")
     ap.add_argument("--bf16", action="store_true", help="bf16 experts instead of fp8")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--embedder-par", choices=["tp", "dp"], default="tp",
+                    help="moe: the embedder across the TP group — tensor-parallel like the sampler (config 5's "
+                         "'TP=2 each') or data-parallel (whole model per rank, 1/tp of the candidates each)")
     ap.add_argument("--gpus", type=int, default=0, help="moe: world size (TP groups x DP); default = --tp")
     ap.add_argument("--tp-comm", choices=["ipc", "pg"], default="ipc",
                     help="moe TP all-reduce: IPC one-shot kernel (graph-captured) or the process group (RCCL / gloo, "

@@ -454,8 +454,9 @@ int env_int(const char* name, int dflt);
 template <int EPI, int NT>
 int launch(const Params& p, hipStream_t s) {
   // schedule variant (VAR bits, see the main loop): LWC_G4_VAR, an A/B knob (scripts/microbench.py g4ab);
-  // the plain epilogue carries every variant, the fused ones the default
-  const int var = env_int("LWC_G4_VAR", 1);
+  // default 32, the library-shaped schedule (faster than 1 at every headline shape, profiles/gemm4w.md);
+  // every epilogue carries 1 and 32, the plain one the other variants
+  const int var = env_int("LWC_G4_VAR", 32);
   if (var == 32) return launch3<EPI, NT, 32>(p, s);
   if constexpr (EPI == EPI_PLAIN) {
     switch (var) {

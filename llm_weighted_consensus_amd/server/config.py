@@ -46,8 +46,9 @@ variables configure the local engine:
                     with a deadline: the deadline plus LWC_SHARD_GRACE_S, default 5 s)
   LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
                     and batches of at least N run as one vote_tally launch (K10b) on this process's GPU
-                    (launched and read back on a worker thread); unset / 0 (the default): the host C++
-                    tally per request
+                    (launched and read back on a worker thread); default 2 when this process runs an
+                    engine on its GPU (measured +10.8 % req/s, profiles/serve_load.md), else off; 0: the
+                    host C++ tally per request
 """
 from __future__ import annotations
 

@@ -92,10 +92,14 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
     if cfg.device != "cpu":
         from ..score.tally_batch import make_batcher
 
-        # K10b is opt-in (LWC_GPU_TALLY=N): a request's tally is ~L x C <= 128 x 20 multiply-adds, and the
-        # serving A/B measured no throughput difference beyond run-to-run spread (profiles/serve_load.md),
-        # so the host C++ tally is the default
-        score.tally_batcher = make_batcher(cfg.gpu_tally, f"cuda:{cfg.gpu}")
+        # K10b (LWC_GPU_TALLY): concurrent tallies batched into one launch on a worker thread.  The round-4
+        # interleaved A/B (host, gpu, host, gpu on one box) measured +10.8 % req/s both times with lower
+        # p50/p99 (profiles/serve_load.md), so it defaults to 2 whenever this process already drives a GPU
+        # (an in-process engine); a front end over worker processes opens no GPU context unless asked to.
+        # LWC_GPU_TALLY=0 turns it off
+        in_proc = any(type(s).__name__ == "EngineService" for s in services.values())
+        spec = cfg.gpu_tally if cfg.gpu_tally is not None else ("2" if in_proc else None)
+        score.tally_batcher = make_batcher(spec, f"cuda:{cfg.gpu}")
     state = AppState(chat_client, score, MultichatClient(score, archive), ConsensusClient(chat_client, embedders,
                                                                                            archive),
                      embedders=embedders, services=services, archive=archive, registry=registry)

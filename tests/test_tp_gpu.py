@@ -129,3 +129,54 @@ def test_mixtral_ep2_matches_ep1(gpu, fp8, mode):
         ref = _prefill_logits(m, gpu, P=23 + 9 * r, seed=r)
         c = torch.nn.functional.cosine_similarity(res[r], ref, dim=0).item()
         assert c > 0.999, (r, c)
+
+
+def _enc_worker(rank, world, port, fp8, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.models.config import decoder_config
+        from llm_weighted_consensus_amd.models.tp import TPLlamaModel
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        m = TPLlamaModel(decoder_config("llama-tiny"), device=dev, seed=6, max_position=512, fp8_dense=fp8,
+                         tp_rank=rank, tp_size=world)  # no tp_comm: the process group's all-reduce (eager)
+        q.put((rank, _encode(m, dev)))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def _encode(m, dev):
+    g = torch.Generator().manual_seed(21)
+    lens = [17, 40, 9]
+    toks = torch.randint(0, m.cfg.vocab_size, (sum(lens),), generator=g).to(dev)
+    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).to(dev)
+    cu = torch.tensor([0, 17, 57, 66], dtype=torch.int32, device=dev)
+    return m.encode(toks.int(), pos, cu, max(lens)).float().cpu()
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_dense_tp2_encode_matches_tp1(gpu, fp8):
+    """The config-5 embedder layout (bench_configs.py moe --embedder-par tp): a dense decoder used as an
+    embedder at TP=2 (TPLlamaModel, process-group all-reduce) gives the TP=1 hidden states."""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import LlamaModel
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_enc_worker, args=(r, 2, port, fp8, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    assert all(isinstance(v, torch.Tensor) for v in res.values()), res
+    ref = _encode(LlamaModel(decoder_config("llama-tiny"), device=gpu, seed=6, max_position=512, fp8_dense=fp8), gpu)
+    for r in range(2):
+        c = torch.nn.functional.cosine_similarity(res[r], ref, dim=1)
+        assert c.min().item() > 0.99, (r, c.min().item())
+    assert torch.equal(res[0], res[1])
