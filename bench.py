@@ -92,8 +92,11 @@ def main():
     encoder = BertEncoder(ecfg, device=dev, seed=4321)
     tok = ByteTokenizer(dcfg.vocab_size, dcfg.bos_token_id, dcfg.eos_token_id)
     max_len = a.prompt_len + a.gen_len + 16
+    # LWC_SHARE_ONE_GPU=1 (multi-rank rehearsal on one GPU): the ranks size their caches from the same free
+    # memory at the same time, so each takes its share of the fraction
+    shared = os.environ.get("LWC_SHARE_ONE_GPU") == "1" and W > 1
     engine = LLMEngine(model, tok, max_batch=Rg * n_local, max_model_len=max_len, use_graphs=not a.no_graphs,
-                       kv_memory_fraction=0.5, prefix_sharing=not a.no_prefix_sharing)
+                       kv_memory_fraction=0.5 / W if shared else 0.5, prefix_sharing=not a.no_prefix_sharing)
     scorer = EmbeddingConsensus(encoder, tau=0.05, max_tokens=512)
     gen = torch.Generator().manual_seed(99)
 
@@ -172,7 +175,7 @@ def main():
             "metric": "consensus answers/sec (whole node) + embeddings/sec, N=64 Llama-3-8B@bge-large",
             "value": round(value, 4),
             "unit": "answers/s",
-            "n_gpus": W,
+            "n_gpus": 1 if shared else W,
             "backend": info.backend or "none (single process)",
             "world_size": seen,
             "steps": a.steps,
@@ -195,7 +198,9 @@ def main():
                 "sampling": "temperature 0.8, top_p 0.95",
                 "parallelism": (f"cp{cp} x dp{W // cp}: candidate-parallel groups of {cp} GPUs (all-gather of prompt KV "
                                 f"+ embeddings inside a group over {info.backend}), request-parallel across groups"
-                                if W > 1 else "single GPU"),
+                                if W > 1 else "single GPU") + (" (ranks SHARE one GPU: a rehearsal of the "
+                                                                "multi-rank path, not a multi-GPU number)"
+                                                                if shared else ""),
             },
         }
         print(json.dumps(out), flush=True)

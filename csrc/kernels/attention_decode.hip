@@ -61,6 +61,11 @@ struct DecodeParams {
   float* part_lse;      // [B, Hq, S]
   int q_stride, Hq, Hkv, G, max_blocks, num_splits;
   float scale;
+  // q rotation at load (pure decode steps: rope_kv_write left q un-rotated): rotate-half RoPE with the
+  // model's [max_pos, D/2] fp32 tables at positions[row]; null = q already rotated
+  const float* rope_cos;
+  const float* rope_sin;
+  const int* positions;
 };
 
 // K and V registers of one PAIR of 16-token blocks for one wave (K: 8 x 16 B, V: 16 x 8 B per lane).
@@ -267,6 +272,28 @@ LWC_DEVICE void load_q(short8 (&qf)[4], const DecodeParams& p, int row_seq0, int
     short8 v = *reinterpret_cast<const short8*>(qh + 32 * s + 8 * g);
     qf[s] = valid ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
   }
+  if (p.rope_cos) {
+    // the lane's dims are 32 s + 8 g + e: dim d < 64 (s = 0, 1) and its rotate-half partner d + 64 sit in
+    // qf[s] and qf[s + 2] of the SAME lane, so the rotation is register-local (rounded to bf16 as
+    // rope_kv_write rounds the q it writes back)
+    const int pos = p.positions[seq];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 32 * s + 8 * g;
+      const float4 c0 = *reinterpret_cast<const float4*>(p.rope_cos + (size_t)pos * (kD / 2) + c);
+      const float4 c1 = *reinterpret_cast<const float4*>(p.rope_cos + (size_t)pos * (kD / 2) + c + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(p.rope_sin + (size_t)pos * (kD / 2) + c);
+      const float4 s1 = *reinterpret_cast<const float4*>(p.rope_sin + (size_t)pos * (kD / 2) + c + 4);
+      const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x1 = bf2f((bf16_t)qf[s][e]), x2 = bf2f((bf16_t)qf[s + 2][e]);
+        qf[s][e] = (short)f2bf(x1 * cs[e] - x2 * sn[e]);
+        qf[s + 2][e] = (short)f2bf(x2 * cs[e] + x1 * sn[e]);
+      }
+    }
+  }
 }
 
 // blockIdx.x = sequence.  4 waves split the sequence's block pairs and combine through LDS: the
@@ -456,6 +483,9 @@ struct CascadeParams {
   bf16_t* out;       // [B, Hq, D]
   int q_stride, Hq, Hkv, G, max_blocks;
   float scale;
+  const float* rope_cos;  // as DecodeParams
+  const float* rope_sin;
+  const int* positions;
 };
 
 // The index tables come in as const __restrict__ kernel arguments (not through the params struct): with
@@ -487,6 +517,9 @@ __global__ void __launch_bounds__(kCWaves * 64)
   qp.q = p.q;
   qp.q_stride = p.q_stride;
   qp.G = p.G;
+  qp.rope_cos = p.rope_cos;
+  qp.rope_sin = p.rope_sin;
+  qp.positions = p.positions;
   load_q<true>(qf, qp, s0, nrows, kvh, r16, g);
 
   float4v o[8];
@@ -714,13 +747,15 @@ extern "C" int lwc_set_decode_wave_min_items(int n) {
 // forked prompts use the cascade kernel below).
 extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                                 const int* ctx_lens, void* out, float* part_o, float* part_lse, int B, int Hq,
-                                int Hkv, int D, int BS, int max_blocks, int num_splits, float scale, hipStream_t s) {
+                                int Hkv, int D, int BS, int max_blocks, int num_splits, float scale,
+                                const float* rope_cos, const float* rope_sin, const int* positions, hipStream_t s) {
   using namespace lwc;
   if (D != kD || BS != kBS || Hq % Hkv != 0 || Hq / Hkv > 16 || num_splits < 1) return -1;
   if (num_splits > 1 && (!part_o || !part_lse)) return -2;
   if (B == 0) return 0;
   DecodeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, (bf16_t*)out,
-                 part_o, part_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, num_splits, scale};
+                 part_o, part_lse, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, num_splits, scale,
+                 rope_cos, rope_sin, positions};
   if ((long)B * Hkv * num_splits >= g_wave_min_items) {
     const int items = B * num_splits;
     paged_decode_wave_kernel<<<dim3((items + kWaves - 1) / kWaves, Hkv), 256, 0, s>>>(p, items, block_tables,
@@ -737,12 +772,13 @@ extern "C" int lwc_paged_decode(const void* q, int q_stride, const void* kc, con
 extern "C" int lwc_paged_decode_cascade(const void* q, int q_stride, const void* kc, const void* vc,
                                         const int* block_tables, const int* ctx_lens, const int* tiles, int max_tiles,
                                         void* out, int Hq, int Hkv, int D, int BS, int max_blocks, float scale,
+                                        const float* rope_cos, const float* rope_sin, const int* positions,
                                         hipStream_t s) {
   using namespace lwc;
   if (D != kD || BS != kBS || Hq % Hkv != 0 || 16 % (Hq / Hkv) != 0) return -1;
   if (max_tiles == 0) return 0;
   CascadeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, tiles,
-                  (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale};
+                  (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale, rope_cos, rope_sin, positions};
   static int pairs = 0;
   if (pairs == 0) {
     const char* e = getenv("LWC_CASCADE_PAIRS");

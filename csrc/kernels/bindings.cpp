@@ -11,16 +11,16 @@ int lwc_rmsnorm(const void*, void*, const void*, void*, int, int, float, hipStre
 int lwc_rmsnorm_quant_fp8(const void*, void*, const void*, void*, int, int, float, void*, float*, hipStream_t);
 int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
 int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
-                      int, hipStream_t);
+                      int, int, hipStream_t);
 int lwc_silu_mul(const void*, void*, int, int, int, hipStream_t);
 int lwc_embedding_gather(const void*, const int*, void*, int, int, int, hipStream_t);
 int lwc_kv_block_copy(void*, const int*, int, int, int, long long, hipStream_t);
 int lwc_kv_gather(const void*, const void*, const long long*, void*, void*, int, int, int, int, hipStream_t);
 int lwc_paged_decode(const void*, int, const void*, const void*, const int*, const int*, void*, float*, float*, int,
-                     int, int, int, int, int, int, float, hipStream_t);
+                     int, int, int, int, int, int, float, const float*, const float*, const int*, hipStream_t);
 int lwc_set_decode_wave_min_items(int);
 int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const int*, const int*, const int*, int, void*,
-                             int, int, int, int, int, float, hipStream_t);
+                             int, int, int, int, int, float, const float*, const float*, const int*, hipStream_t);
 int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
@@ -148,7 +148,7 @@ void layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, c
 
 void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const c10::optional<at::Tensor>& slots,
                    const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& k_cache, at::Tensor& v_cache,
-                   int64_t Hq, int64_t Hkv, int64_t D) {
+                   int64_t Hq, int64_t Hkv, int64_t D, bool rope_q) {
   CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   CHECK_GPU(positions); CHECK_DTYPE(positions, at::kInt);
   CHECK_DTYPE(cos_t, at::kFloat); CHECK_DTYPE(sin_t, at::kFloat);
@@ -169,8 +169,33 @@ void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const c10::opti
   }
   CHECK_RC(lwc_rope_kv_write(qkv.data_ptr(), positions.data_ptr<int>(), sp, cos_t.data_ptr<float>(),
                              sin_t.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(), T, (int)Hq, (int)Hkv,
-                             (int)D, BS, cur_stream()),
+                             (int)D, BS, rope_q ? 1 : 0, cur_stream()),
            "rope_kv_write");
+}
+
+// Optional q rotation inside the decode kernels: (cos [max_pos, D/2] fp32, sin, positions [B] int32) all
+// given or none.
+struct QRope {
+  const float* cos = nullptr;
+  const float* sin = nullptr;
+  const int* pos = nullptr;
+};
+static QRope q_rope(const c10::optional<at::Tensor>& c, const c10::optional<at::Tensor>& s,
+                    const c10::optional<at::Tensor>& pos, int B, int D, const char* what) {
+  QRope r;
+  const bool any = (c.has_value() && c->defined()) || (s.has_value() && s->defined()) ||
+                   (pos.has_value() && pos->defined());
+  if (!any) return r;
+  TORCH_CHECK(c.has_value() && s.has_value() && pos.has_value() && c->defined() && s->defined() && pos->defined(),
+              what, ": rope needs cos, sin and positions");
+  CHECK_DTYPE(*c, at::kFloat); CHECK_DTYPE(*s, at::kFloat); CHECK_DTYPE(*pos, at::kInt);
+  CHECK_CONTIG(*c); CHECK_CONTIG(*s); CHECK_CONTIG(*pos);
+  TORCH_CHECK(c->dim() == 2 && c->size(1) == D / 2 && s->sizes() == c->sizes(), what, ": rope table shape");
+  TORCH_CHECK(pos->numel() >= B, what, ": positions shorter than the batch");
+  r.cos = c->data_ptr<float>();
+  r.sin = s->data_ptr<float>();
+  r.pos = pos->data_ptr<int>();
+  return r;
 }
 
 void silu_mul(const at::Tensor& in, at::Tensor& out, int64_t block) {
@@ -221,7 +246,8 @@ void kv_block_copy(at::Tensor& cache, const at::Tensor& pairs) {
 void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& ctx_lens, at::Tensor& out,
                   const c10::optional<at::Tensor>& part_o, const c10::optional<at::Tensor>& part_lse,
-                  int64_t num_splits, double scale) {
+                  int64_t num_splits, double scale, const c10::optional<at::Tensor>& rope_cos,
+                  const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& positions) {
   // q: [B, >= Hq*D] with row stride; out: [B, Hq, D]
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt);
@@ -241,15 +267,18 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
     po = part_o->data_ptr<float>();
     pl = part_lse->data_ptr<float>();
   }
+  const QRope qr = q_rope(rope_cos, rope_sin, positions, B, D, "paged_decode");
   CHECK_RC(lwc_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), out.data_ptr(), po, pl, B, Hq, Hkv,
-                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, cur_stream()),
+                            D, BS, (int)block_tables.size(1), (int)num_splits, (float)scale, qr.cos, qr.sin, qr.pos,
+                            cur_stream()),
            "paged_decode");
 }
 
 void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                           const at::Tensor& block_tables, const at::Tensor& ctx_lens, const at::Tensor& tiles,
-                          at::Tensor& out, int64_t Hq, double scale) {
+                          at::Tensor& out, int64_t Hq, double scale, const c10::optional<at::Tensor>& rope_cos,
+                          const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& positions) {
   // tiles: [max_tiles, 3] int32 super-tiles (row_start, nseq, prefix_blocks), nseq <= cascade_rows_per_tile(G);
   // the engine builds them on the host (rows must stay < B: the kernel trusts the table).
   CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out); CHECK_CONTIG(out);
@@ -261,10 +290,11 @@ void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const 
   const int B = (int)q.size(0), D = (int)k_cache.size(3), Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
   TORCH_CHECK(block_tables.size(0) >= B && ctx_lens.numel() >= B, "paged_decode_cascade: batch tables too short");
   TORCH_CHECK(out.numel() >= (int64_t)B * Hq * D, "paged_decode_cascade: out too small");
+  const QRope qr = q_rope(rope_cos, rope_sin, positions, B, D, "paged_decode_cascade");
   CHECK_RC(lwc_paged_decode_cascade(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                     block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), tiles.data_ptr<int>(),
                                     (int)tiles.size(0), out.data_ptr(), (int)Hq, Hkv, D, BS,
-                                    (int)block_tables.size(1), (float)scale, cur_stream()),
+                                    (int)block_tables.size(1), (float)scale, qr.cos, qr.sin, qr.pos, cur_stream()),
            "paged_decode_cascade");
 }
 

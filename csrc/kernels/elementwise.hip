@@ -15,7 +15,8 @@ namespace lwc {
 __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ positions,
                                                            const int* __restrict__ slots, const float* __restrict__ cos_t,
                                                            const float* __restrict__ sin_t, bf16_t* __restrict__ kc,
-                                                           bf16_t* __restrict__ vc, int Hq, int Hkv, int D, int BS) {
+                                                           bf16_t* __restrict__ vc, int Hq, int Hkv, int D, int BS,
+                                                           int rope_q) {
   const int t = blockIdx.x;
   const int half = D >> 1;
   const int vec_per_head_rot = half >> 3;  // threads per head for rotation (8 dims each half)
@@ -25,7 +26,9 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
   const int pos = positions[t];
   const int slot = slots ? slots[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
-  for (int i = threadIdx.x; i < n_rot; i += blockDim.x) {
+  // rope_q = 0 (pure decode steps): q stays un-rotated in qkv — the decode attention kernels rotate it as
+  // they load it — and only the k heads are rotated and cached
+  for (int i = threadIdx.x + (rope_q ? 0 : Hq * vec_per_head_rot); i < n_rot; i += blockDim.x) {
     const int h = i / vec_per_head_rot;      // 0..Hq+Hkv-1 (q heads then k heads)
     const int c = (i % vec_per_head_rot) * 8;  // first-half dim offset
     bf16_t* hp = row + h * D;
@@ -149,12 +152,13 @@ static int ew_grid(size_t work, int threads) {
 
 extern "C" int lwc_rope_kv_write(void* qkv, const int* positions, const int* slots, const float* cos_t,
                                  const float* sin_t, void* kc, void* vc, int T, int Hq, int Hkv, int D, int BS,
-                                 hipStream_t s) {
+                                 int rope_q, hipStream_t s) {
   using namespace lwc;
   if (D % 16 != 0 || T <= 0) return T == 0 ? 0 : -1;
   // (320 threads — every rotated pair of a Llama-3 token in one round — measured 27.9 vs 26.3 us at T = 4096)
-  rope_kv_write_kernel<<<T, 256, 0, s>>>((bf16_t*)qkv, positions, slots, cos_t, sin_t, (bf16_t*)kc, (bf16_t*)vc, Hq,
-                                         Hkv, D, BS);
+  // k only: Hkv * D/16 rotations (64 for Llama-3) + the V scatter, 128 threads
+  rope_kv_write_kernel<<<T, rope_q ? 256 : 128, 0, s>>>((bf16_t*)qkv, positions, slots, cos_t, sin_t, (bf16_t*)kc,
+                                                        (bf16_t*)vc, Hq, Hkv, D, BS, rope_q);
   return (int)hipGetLastError();
 }
 

@@ -96,6 +96,50 @@ LWC_DEVICE uint16_t h2bits(float f) { return __builtin_bit_cast(uint16_t, (_Floa
 #define KEYU(row, j, e) ((((e)&1) ? ((row)[j][(e) >> 1] >> 16) : ((row)[j][(e) >> 1] & 0xffffu)))
 #define GETU(row, j, e) ((float)__builtin_bit_cast(_Float16, (uint16_t)KEYU(row, j, e)))
 
+// Packed selection over the probability form (two non-negative fp16 u per register: their bit patterns
+// order like the values).  Per pair: a saturating 16-bit subtract against (threshold - 1) is >= 1 exactly
+// where key >= threshold, min(., 1) makes that a 0/1 mask, and either a packed add counts it or a packed
+// multiply by 0x3C00 turns it into fp16 0 / 1.0 for a v_dot2 that sums the kept u in fp32 — 2 VALU per
+// element instead of unpack + compare + select + add (+ the SDWA hazard nops) per element.
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+LWC_DEVICE half2v as_h2(uint32_t w) { return __builtin_bit_cast(half2v, w); }
+LWC_DEVICE void count2(uint32_t& c2, uint32_t w0, uint32_t w1, uint32_t thr1x2, uint32_t one2) {
+  uint32_t t0, t1;
+  asm("v_pk_sub_u16 %1, %3, %5 clamp\n\t"
+      "v_pk_sub_u16 %2, %4, %5 clamp\n\t"
+      "v_pk_min_u16 %1, %1, %6\n\t"
+      "v_pk_min_u16 %2, %2, %6\n\t"
+      "v_pk_add_u16 %0, %0, %1\n\t"
+      "v_pk_add_u16 %0, %0, %2"
+      : "+v"(c2), "=&v"(t0), "=&v"(t1)
+      : "v"(w0), "v"(w1), "v"(thr1x2), "v"(one2));
+}
+// Two registers (four u) per block, the whole chain in one asm block: the compiler puts a hazard nop
+// after every inline-asm result a compiled instruction reads, so the dot stays inside.  Ordering keeps
+// each v_dot2c >= 1 instruction after the multiply that feeds it (VALU write -> DOT read) and the dots
+// back to back on one accumulator (same-DOT srcC forwarding, no wait); the accumulator's final reader
+// waits through dot_read().
+LWC_DEVICE void mass2(float& acc, uint32_t w0, uint32_t w1, uint32_t thr1x2, uint32_t one2, uint32_t h1x2) {
+  uint32_t t0, t1;
+  asm("v_pk_sub_u16 %1, %3, %5 clamp\n\t"
+      "v_pk_sub_u16 %2, %4, %5 clamp\n\t"
+      "v_pk_min_u16 %1, %1, %6\n\t"
+      "v_pk_min_u16 %2, %2, %6\n\t"
+      "v_pk_mul_lo_u16 %1, %1, %7\n\t"
+      "v_pk_mul_lo_u16 %2, %2, %7\n\t"
+      "v_dot2c_f32_f16 %0, %3, %1\n\t"
+      "v_dot2c_f32_f16 %0, %4, %2"
+      : "+v"(acc), "=&v"(t0), "=&v"(t1)
+      : "v"(w0), "v"(w1), "v"(thr1x2), "v"(one2), "v"(h1x2));
+}
+// DOT write -> VALU read needs 3 wait states
+LWC_DEVICE float dot_read(float acc) {
+  float r;
+  asm("s_nop 2\n\tv_mov_b32 %0, %1" : "=v"(r) : "v"(acc));
+  return r;
+}
+LWC_DEVICE uint32_t thr1x2(uint32_t key) { return ((key - 1u) & 0xffffu) * 0x10001u; }  // key >= 1
+
 LWC_DEVICE int block_sum_i(int v, int* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -119,6 +163,9 @@ __global__ void __launch_bounds__(kSampT) sample_kernel(SampleParams p) {
   __shared__ float s_scan[kSampT / 64];
   __shared__ uint32_t s_tkey[kSampT];
   __shared__ uint32_t s_lb, s_fkey;
+  __shared__ uint32_t s_own[SLOTS * 4];
+  __shared__ float s_oexcl;
+  __shared__ int s_found;
 
   const int b = blockIdx.x;
   const int t = threadIdx.x;
@@ -331,6 +378,8 @@ OPAQUE_ROW(row);
         for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
       ymax = block_max(ym, sred);
     }
+    if (!(ymax > -INFINITY)) ymax = 0.f;  // every token masked: all u = 0 (the argmax fallback below)
+    const uint32_t kOne2 = 0x00010001u, kH1 = 0x3C003C00u;
     // ---- one exp per element: the row becomes u_i = exp((y_i - ymax)/T) in [0, 1] as packed fp16.
     // Non-negative fp16 bit patterns are order-preserving, so every later threshold search compares
     // raw 16-bit keys and sums fp16 values: no transcendental inside the searches.  The same pass
@@ -345,17 +394,27 @@ OPAQUE_ROW(row);
 #pragma unroll
         for (int e = 0; e < 8; ++e) se += __expf(GET(row, j, e) - raw_max);
     }
+    // u = 2^(y * c1 + c0), c1 = log2(e) / T, c0 ~ -ymax * c1 rounded so that the exponent of y = ymax is
+    // >= 0: with v_cvt_pkrtz (round toward zero) the max element is exactly 1.0 (0x3C00) and every other
+    // element (at least one bf16 ulp below it, far above the fp32 rounding of c0) below 1; y = -inf gives
+    // exactly 0.  One fma + one exp per element, two values per pack, their (rounded) sum by one v_dot2
+    // against (1, 1)
+    const float c1 = invT * 1.4426950408889634f;
+    float c0 = -ymax * c1;
+    if (__builtin_fmaf(ymax, c1, c0) < 0.f)  // one ulp toward +inf (c0 != 0 here)
+      c0 = __uint_as_float(__float_as_uint(c0) + (c0 > 0.f ? 1u : 0xffffffffu));
+    const half2v ones2 = {(_Float16)1.f, (_Float16)1.f};
 OPAQUE_ROW(row);
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const float y0 = GET(row, j, 2 * c), y1 = GET(row, j, 2 * c + 1);
-        const float u0 = y0 > -INFINITY ? __expf((y0 - ymax) * invT) : 0.f;
-        const float u1 = y1 > -INFINITY ? __expf((y1 - ymax) * invT) : 0.f;
-        const uint16_t h0 = h2bits(u0), h1 = h2bits(u1);
-        zloc += (float)__builtin_bit_cast(_Float16, h0) + (float)__builtin_bit_cast(_Float16, h1);
-        row[j][c] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        const auto h = __builtin_amdgcn_cvt_pkrtz(__builtin_amdgcn_exp2f(__builtin_fmaf(y0, c1, c0)),
+                                                  __builtin_amdgcn_exp2f(__builtin_fmaf(y1, c1, c0)));
+        const uint32_t w = __builtin_bit_cast(uint32_t, h);
+        zloc = __builtin_amdgcn_fdot2(as_h2(w), ones2, zloc, false);
+        row[j][c] = w;
       }
     }
     float Z;
@@ -374,16 +433,22 @@ OPAQUE_ROW(row);
     }
     // mass of the elements with key >= KEY (macro, not a lambda: a by-reference capture of `row`
     // makes it addressable and sends it to scratch)
-#define MASS_GE(KEY, OUT)                                              \
-  do {                                                                 \
-    OPAQUE_ROW(row);                                                   \
-    float _s = 0.f;                                                    \
-    _Pragma("unroll") for (int j = 0; j < SLOTS; ++j) {                \
-      _Pragma("unroll") for (int e = 0; e < 8; ++e) {                  \
-        _s += (KEYU(row, j, e) >= (KEY)) ? GETU(row, j, e) : 0.f;      \
-      }                                                                \
-    }                                                                  \
-    OUT = block_sum(_s, sred);                                         \
+#define MASS_LOCAL(KEY, OUT)                                                           \
+  do {                                                                                 \
+    OPAQUE_ROW(row);                                                                   \
+    const uint32_t _t2 = thr1x2(KEY);                                                  \
+    float _s = 0.f;                                                                    \
+    _Pragma("unroll") for (int j = 0; j < SLOTS; ++j) {                                \
+      mass2(_s, row[j][0], row[j][1], _t2, kOne2, kH1);                                \
+      mass2(_s, row[j][2], row[j][3], _t2, kOne2, kH1);                                \
+    }                                                                                  \
+    OUT = dot_read(_s);                                                                \
+  } while (0)
+#define MASS_GE(KEY, OUT)        \
+  do {                           \
+    float _l;                    \
+    MASS_LOCAL(KEY, _l);         \
+    OUT = block_sum(_l, sred);   \
   } while (0)
     uint32_t tau_k = 0;  // top-k: keep elements with key >= tau_k
     const int k = p.top_k[b];
@@ -391,13 +456,15 @@ OPAQUE_ROW(row);
       uint32_t lo = 0, hi = 0x3C00u;  // keys of [0, 1.0]
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
-        int c = 0;
+        const uint32_t t2 = thr1x2(mid);
+        uint32_t c2 = 0u;
 OPAQUE_ROW(row);
 #pragma unroll
-        for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) c += KEYU(row, j, e) >= mid;
-        if (block_sum_i(c, sredi) >= k)
+        for (int j = 0; j < SLOTS; ++j) {
+          count2(c2, row[j][0], row[j][1], t2, kOne2);
+          count2(c2, row[j][2], row[j][3], t2, kOne2);
+        }
+        if (block_sum_i((int)((c2 & 0xffffu) + (c2 >> 16)), sredi) >= k)
           lo = mid;
         else
           hi = mid - 1;
@@ -435,15 +502,10 @@ OPAQUE_ROW(row);
     for (int attempt = 0; attempt < 2; ++attempt) {
       // ---- inverse-CDF draw over {key >= tau} (order: thread-major, then slot, then element) ----
       float local = 0.f;
-      if (tau <= 1u) {
+      if (tau <= 1u)
         local = zloc;  // every positive element is kept: the thread's share of Z
-      } else {
-OPAQUE_ROW(row);
-#pragma unroll
-        for (int j = 0; j < SLOTS; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) local += (KEYU(row, j, e) >= tau) ? GETU(row, j, e) : 0.f;
-      }
+      else
+        MASS_LOCAL(tau, local);
       // exclusive scan of `local` over threads
       float incl = local;
 #pragma unroll
@@ -463,44 +525,93 @@ OPAQUE_ROW(row);
       const float excl = wave_off + incl - local;
       const float u01 = (((attempt == 0 ? ctr[0] : ctr[1]) >> 8) + 0.5f) * (1.0f / 16777216.0f);
       const float u = u01 * total;
-      int mine = 0x7fffffff;
-      uint32_t mine_key = 0x3C00u;
-      if (local > 0.f && u >= excl && u < excl + local) {
-        float acc = excl;
-        int last = -1;
-        uint32_t last_key = 0u;
-OPAQUE_ROW(row);
+      // The owner: the lowest thread whose [excl, excl + local) holds u — or, when rounding put u at or
+      // past the end, the last thread with mass (its last kept element is taken).  Its packed u go to
+      // LDS and ONE wave walks them (two elements per dword, an exclusive scan over the lanes) instead
+      // of a single lane stepping through 8 * SLOTS elements with a branch each.
+      int cand = (local > 0.f && u >= excl && u < excl + local) ? t : 0x7fffffff;
+      int lastt = local > 0.f ? t : -1;
 #pragma unroll
-        for (int j = 0; j < SLOTS; ++j)
+      for (int o = 32; o > 0; o >>= 1) {
+        cand = min(cand, __shfl_xor(cand, o, 64));
+        lastt = max(lastt, __shfl_xor(lastt, o, 64));
+      }
+      __syncthreads();
+      if (lane == 0) {
+        sredi[wid] = cand;
+        sredi[16 + wid] = lastt;
+      }
+      __syncthreads();
+      cand = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
+      lastt = lane < (kSampT / 64) ? sredi[16 + lane] : -1;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int idx = (j * kSampT + t) * 8 + e;
-            const uint32_t kk = KEYU(row, j, e);
-            if (kk >= tau && kk > 0u) {
-              last = idx;
-              last_key = kk;
-              acc += GETU(row, j, e);
-              if (mine == 0x7fffffff && u < acc) {
-                mine = idx;
-                mine_key = kk;
-              }
+      for (int o = 32; o > 0; o >>= 1) {
+        cand = min(cand, __shfl_xor(cand, o, 64));
+        lastt = max(lastt, __shfl_xor(lastt, o, 64));
+      }
+      const bool past_end = cand == 0x7fffffff;
+      const int owner = past_end ? lastt : cand;  // block-uniform
+      found = 0x7fffffff;
+      if (owner >= 0) {
+        if (t == owner) {
+#pragma unroll
+          for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s_own[j * 4 + c] = row[j][c];
+          s_oexcl = excl;
+        }
+        __syncthreads();
+        if (t < 64) {
+          constexpr int ND = SLOTS * 4, P = (ND + 63) / 64;  // lane: dwords [lane*P, lane*P + P)
+          float v[2 * P];
+          float sl = 0.f;
+#pragma unroll
+          for (int q = 0; q < P; ++q) {
+            const int d = lane * P + q;
+            const uint32_t w = d < ND ? s_own[d] : 0u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t kk = h ? (w >> 16) : (w & 0xffffu);
+              // tau >= 1: zero-mass elements are never kept
+              v[2 * q + h] = kk >= tau ? (float)__builtin_bit_cast(_Float16, (uint16_t)kk) : 0.f;
+              sl += v[2 * q + h];
             }
           }
-        if (mine == 0x7fffffff && last >= 0) {  // rounding at the top edge
-          mine = last;
-          mine_key = last_key;
+          float incl = sl;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const float n = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += n;
+          }
+          float acc = s_oexcl + incl - sl;
+          int mine = -1, lastk = -1;
+#pragma unroll
+          for (int e = 0; e < 2 * P; ++e)
+            if (v[e] > 0.f) {
+              acc += v[e];
+              lastk = e;
+              if (mine < 0 && u < acc) mine = e;
+            }
+          const unsigned long long hit = __ballot(mine >= 0 && !past_end);
+          int sel_lane, sel_e;
+          if (hit) {
+            sel_lane = __ffsll((long long)hit) - 1;
+            sel_e = __shfl(mine, sel_lane, 64);
+          } else {  // rounding at the owner's top edge, or u past the end: its last kept element
+            const unsigned long long any = __ballot(lastk >= 0);
+            sel_lane = 63 - __clzll((long long)any);
+            sel_e = __shfl(lastk, sel_lane, 64);
+          }
+          if (lane == sel_lane) {
+            const int d = lane * P + (sel_e >> 1);
+            const uint32_t w = s_own[d];
+            s_found = ((d >> 2) * kSampT + owner) * 8 + 2 * (d & 3) + (sel_e & 1);
+            s_fkey = (sel_e & 1) ? (w >> 16) : (w & 0xffffu);
+          }
         }
+        __syncthreads();
+        found = s_found;
       }
-      // the owning thread is unique except for float ties at a boundary: take the minimum
-      found = mine;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
-      __syncthreads();
-      if (lane == 0) sredi[wid] = found;
-      __syncthreads();
-      found = lane < (kSampT / 64) ? sredi[lane] : 0x7fffffff;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o, 64));
       if (found == 0x7fffffff) {
         // u landed past the last kept element through rounding: fall back to argmax (key 0x3C00: always
         // inside the nucleus)
@@ -532,10 +643,7 @@ OPAQUE_ROW(row);
         break;
       }
       if (!check) break;
-      // ---- nucleus test of the draw ----
-      __syncthreads();
-      if (mine == found) s_fkey = mine_key;
-      __syncthreads();
+      // ---- nucleus test of the draw (s_fkey: the drawn element's key, written by the walk) ----
       const uint32_t ks = s_fkey;
       float above;
       MASS_GE(ks + 1u, above);

@@ -183,9 +183,10 @@ class LlamaModel:
         self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
 
     # ------------------------------------------------------------------ forward
-    def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn) -> torch.Tensor:
+    def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True) -> torch.Tensor:
         """Runs every layer; x_res is the residual stream (updated in place); returns the final
-        normalised hidden state."""
+        normalised hidden state.  ``rope_q=False``: q leaves the qkv projection un-rotated and ``attn_fn``
+        rotates it (the decode kernels' load-time RoPE)."""
         cfg = self.cfg
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
@@ -203,7 +204,8 @@ class LlamaModel:
             h = ops.rmsnorm(x_res, self.layers[0].attn_norm, cfg.rms_eps)
         for li, L in enumerate(self.layers):
             qkv = self._proj(h, L.wqkv)
-            ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots)
+            ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
+                              rope_q=rope_q)
             attn = attn_fn(qkv, li)
             nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
             if fused:
@@ -299,10 +301,13 @@ class LlamaModel:
         cfg = self.cfg
         x = ops.embedding(self.embed, tokens)
         B = tokens.shape[0]
+        # q is rotated inside the attention kernels as they load it (rope_kv_write rotates and caches k
+        # only): q's round trip through HBM in rope_kv_write (2/3 of its bytes at GQA 4) is gone
+        rope = (self.cos, self.sin, positions)
         if cascade_tiles is not None:
             def attn_fn(qkv, li):
                 return ops.paged_decode_cascade(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cascade_tiles,
-                                                cfg.heads, self.scale)
+                                                cfg.heads, self.scale, rope=rope)
         else:
             part_o = part_lse = None
             if num_splits > 1:
@@ -311,9 +316,9 @@ class LlamaModel:
 
             def attn_fn(qkv, li):
                 return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
-                                        num_splits=num_splits, part_o=part_o, part_lse=part_lse)
+                                        num_splits=num_splits, part_o=part_o, part_lse=part_lse, rope=rope)
 
-        h = self._layers(x, cache, positions, slots, attn_fn)
+        h = self._layers(x, cache, positions, slots, attn_fn, rope_q=False)
         return self._proj(h, self.lm_head)
 
     def encode(self, tokens: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor,

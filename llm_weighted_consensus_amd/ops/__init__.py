@@ -114,10 +114,12 @@ def embedding(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
 
 def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
                   k_cache: torch.Tensor, v_cache: torch.Tensor, Hq: int, Hkv: int, D: int,
-                  slots: Optional[torch.Tensor] = None) -> None:
+                  slots: Optional[torch.Tensor] = None, rope_q: bool = True) -> None:
     """In-place rotate-half RoPE on q and k inside ``qkv`` and scatter k, v into the paged cache at
-    ``slots`` (K2).  ``slots=None`` only rotates (no cache write)."""
-    kernels().rope_kv_write(qkv, positions, slots, cos, sin, k_cache, v_cache, int(Hq), int(Hkv), int(D))
+    ``slots`` (K2).  ``slots=None`` only rotates (no cache write).  ``rope_q=False`` (pure decode steps)
+    leaves q un-rotated: the decode attention kernels rotate it as they load it (``rope=`` of
+    :func:`paged_decode` / :func:`paged_decode_cascade`), which saves q's read and write-back here."""
+    kernels().rope_kv_write(qkv, positions, slots, cos, sin, k_cache, v_cache, int(Hq), int(Hkv), int(D), bool(rope_q))
 
 
 def v_token(v_cache: torch.Tensor, block: int, t: int) -> torch.Tensor:
@@ -143,9 +145,11 @@ def kv_block_copy(cache: torch.Tensor, pairs: torch.Tensor) -> None:
 def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                  ctx_lens: torch.Tensor, Hq: int, scale: float, num_splits: int = 1,
                  out: Optional[torch.Tensor] = None, part_o: Optional[torch.Tensor] = None,
-                 part_lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 part_lse: Optional[torch.Tensor] = None,
+                 rope: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """One-token paged GQA split-K decode attention (K3).  q: [B, >=Hq*D] (row stride allowed).  The
-    engine's large batches of forked candidates use :func:`paged_decode_cascade` instead."""
+    engine's large batches of forked candidates use :func:`paged_decode_cascade` instead.  ``rope`` =
+    (cos, sin, positions [B] int32): q arrives un-rotated and is rotated at load."""
     B = q.shape[0]
     D = k_cache.shape[-1]
     if out is None:
@@ -153,8 +157,9 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
     if num_splits > 1 and (part_o is None or part_lse is None):
         part_o = torch.empty(B * Hq * num_splits * D, dtype=torch.float32, device=q.device)
         part_lse = torch.empty(B * Hq * num_splits, dtype=torch.float32, device=q.device)
+    rc, rs, rp = rope if rope is not None else (None, None, None)
     kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, part_o, part_lse, int(num_splits),
-                           float(scale))
+                           float(scale), rc, rs, rp)
     return out
 
 
@@ -171,7 +176,8 @@ def cascade_rows_per_tile(G: int) -> int:
 
 def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                          ctx_lens: torch.Tensor, tiles: torch.Tensor, Hq: int, scale: float,
-                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                         out: Optional[torch.Tensor] = None,
+                         rope: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Cascade decode attention in ONE launch (K3c): per super-tile (row_start, nseq, prefix_blocks) the
     tile's sequences read their shared first `prefix_blocks` blocks once through LDS, then each
     sequence's own blocks; softmax states merge in registers.  Every row < B must be covered by
@@ -180,7 +186,9 @@ def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.
     D = k_cache.shape[-1]
     if out is None:
         out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
-    kernels().paged_decode_cascade(q, k_cache, v_cache, block_tables, ctx_lens, tiles, out, int(Hq), float(scale))
+    rc, rs, rp = rope if rope is not None else (None, None, None)
+    kernels().paged_decode_cascade(q, k_cache, v_cache, block_tables, ctx_lens, tiles, out, int(Hq), float(scale),
+                                   rc, rs, rp)
     return out
 
 

@@ -464,7 +464,10 @@ def small(dev):
         pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
         slots = (torch.randperm(T, device=dev).to(torch.int32) * 16 + 5)
         us = timeit(lambda: ops.rope_kv_write(qkv, pos, cos, sin, cache.k[0], cache.v[0], 32, 8, 128, slots=slots))
-        print(f"rope_kv_write T={T}: {us:6.1f} us", flush=True)
+        us_k = timeit(lambda: ops.rope_kv_write(qkv, pos, cos, sin, cache.k[0], cache.v[0], 32, 8, 128, slots=slots,
+                                                rope_q=False))
+        print(f"rope_kv_write T={T}: {us:6.1f} us   k only (q rotated in the decode kernels): {us_k:6.1f} us",
+              flush=True)
     for T in (512, 3072):
         x = torch.randn(T, 4096, device=dev).to(torch.bfloat16)
         r = torch.randn(T, 4096, device=dev).to(torch.bfloat16)

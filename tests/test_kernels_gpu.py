@@ -81,7 +81,13 @@ def test_rope_kv_write(gpu):
     slots = torch.randperm(NB * BS, device=gpu)[:T].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=gpu)
     vc = torch.zeros(NB, Hkv, BS // 4, D, 4, dtype=torch.bfloat16, device=gpu)
+    q2 = qkv.clone()
+    kc2, vc2 = kc.clone(), vc.clone()
     ops.rope_kv_write(qkv, pos, cos, sin, kc, vc, Hq, Hkv, D, slots=slots)
+    # rope_q=False (pure decode steps): q untouched, k rotated and cached exactly as above
+    ops.rope_kv_write(q2, pos, cos, sin, kc2, vc2, Hq, Hkv, D, slots=slots, rope_q=False)
+    assert torch.equal(q2[:, : Hq * D], q0[:, : Hq * D])
+    assert torch.equal(q2[:, Hq * D:], qkv[:, Hq * D:]) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
     q_ref = ref.rope(q0[:, : Hq * D].view(T, Hq, D), pos, cos, sin)
     k_ref = ref.rope(q0[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D), pos, cos, sin)
     v_ref = q0[:, (Hq + Hkv) * D:].view(T, Hkv, D)
@@ -102,8 +108,28 @@ def decode_path(request, gpu):
     ops.set_decode_wave_min_items(old)
 
 
+def _q_rope(gpu, B):
+    """(cos, sin, positions) for the decode kernels' load-time RoPE: q arrives un-rotated."""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import rope_tables
+
+    cos, sin = rope_tables(decoder_config("llama-tiny"), gpu, 512)
+    pos = torch.randint(0, 500, (B,), device=gpu, dtype=torch.int32)
+    return cos, sin, pos
+
+
+def _q_ref(q_full, b, Hq, D, rope):
+    q = q_full[b, : Hq * D].view(1, Hq, D)
+    if rope is None:
+        return q
+    cos, sin, pos = rope
+    return ref.rope(q, pos[b:b + 1], cos, sin).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("rope", [False, True])
 @pytest.mark.parametrize("G,splits", [(4, 1), (4, 3), (1, 1), (8, 2)])
-def test_paged_decode(gpu, G, splits, decode_path):
+def test_paged_decode(gpu, G, splits, decode_path, rope):
+    """rope=True: q un-rotated, rotated at load (pure decode steps; rope_kv_write rope_q=False)."""
     from llm_weighted_consensus_amd import ops
 
     torch.manual_seed(0)
@@ -131,20 +157,22 @@ def test_paged_decode(gpu, G, splits, decode_path):
             for tt in range(o, BS):
                 ops.v_token(vc, last, tt).fill_(float("nan"))
     q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
-    out = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits)
+    rp = _q_rope(gpu, B) if rope else None
+    out = ops.paged_decode(q_full, kc, vc, bt, ctx, Hq, 1 / math.sqrt(D), num_splits=splits, rope=rp)
     for b in range(B):
         L = int(ctx[b])
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()
         kk = kc[blk, :, toks % BS, :]  # [L, Hkv, D]
         vv = ops.v_gather(vc, blk, toks % BS)  # [L, Hkv, D]
-        q = q_full[b, : Hq * D].view(1, Hq, D)
+        q = _q_ref(q_full, b, Hq, D, rp)
         o = ref.attention(q, kk, vv, False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("rope", [False, True])
 @pytest.mark.parametrize("G", [4, 2, 1, 8])
-def test_paged_decode_cascade(gpu, G):
+def test_paged_decode_cascade(gpu, G, rope):
     """One-launch cascade kernel (LDS-staged shared prompt + per-sequence suffix) == reference, over
     groups spanning several super-tiles, odd prefix block counts, plain rows and NaN-poisoned slots; a
     prompt of one LDS chunk takes the interleaved pass (its DMA overlapping the suffix loads, its pairs
@@ -193,13 +221,14 @@ def test_paged_decode_cascade(gpu, G):
     bt, ctx = bt.to(gpu), ctx.to(gpu)
     tiles = torch.from_numpy(tiles_np).to(gpu)
     q_full = _bf(B, (Hq + 2 * Hkv) * D, dev=gpu)
-    out = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D))
+    rp = _q_rope(gpu, B) if rope else None
+    out = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D), rope=rp)
     assert torch.isfinite(out.float()).all()
     for b in range(B):
         L = int(ctx[b])
         toks = torch.arange(L, device=gpu)
         blk = bt[b, toks // BS].long()
-        o = ref.attention(q_full[b, : Hq * D].view(1, Hq, D), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
+        o = ref.attention(_q_ref(q_full, b, Hq, D, rp), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
                           False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
 
@@ -382,6 +411,37 @@ def test_sample_distribution_top_p_top_k(gpu):
         q = p[:keep] / p[:keep].sum()
         assert cnt[keep:].sum().item() == 0.0, kw
         assert (cnt[:keep] - q).abs().max().item() < 0.04, (kw, cnt[:keep], q)
+
+
+@pytest.mark.parametrize("kw", [{}, {"top_p": 0.9}, {"top_k": 10}, {"top_p": 0.7, "top_k": 20}])
+def test_sample_distribution_full_vocab(gpu, kw):
+    """The Llama-3 vocabulary (V = 128256: the 16-slot instance the decode batch runs): 40 live tokens
+    spread over different threads, slots and lanes of the row, the rest at -20; 4096 draws (one row per
+    seed) against the fp32 torch distribution after temperature / top-p / top-k.  Exercises the packed
+    u16 threshold masses, the top-k count search and the one-wave walk over the owner's registers."""
+    V, B = 128256, 4096
+    g = torch.Generator().manual_seed(8)
+    idx = torch.randperm(V, generator=g)[:40].sort().values
+    base = torch.full((V,), -20.0)
+    base[idx] = torch.linspace(2.0, -1.0, 40)[torch.randperm(40, generator=g)]
+    lg1 = base.to(torch.bfloat16).to(gpu)
+    T = 0.8
+    p = torch.softmax(lg1.float() / T, -1)
+    order = p.argsort(descending=True)
+    keep = torch.zeros(V, dtype=torch.bool, device=gpu)
+    n = int(kw.get("top_k", 0)) or V
+    keep[order[:n]] = True
+    if "top_p" in kw:
+        ps = p[order[:n]] / p[order[:n]].sum()
+        m = int((ps.cumsum(0) < kw["top_p"]).sum().item()) + 1
+        keep = torch.zeros_like(keep)
+        keep[order[:m]] = True
+    q = torch.where(keep, p, torch.zeros_like(p))
+    q = q / q.sum()
+    tok, *_ = _sample(lg1.expand(B, V), gpu, temperature=T, **kw)
+    cnt = torch.bincount(tok.long(), minlength=V).float() / B
+    assert cnt[~keep].sum().item() == 0.0, (kw, cnt.nonzero()[:8])
+    assert (cnt - q).abs().max().item() < 0.03, (kw, (cnt - q).abs().max().item())
 
 
 def _penalised_ref(logits_bf16, counts, fpen, ppen, rpen):
