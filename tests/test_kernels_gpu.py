@@ -444,6 +444,30 @@ def test_sample_distribution_full_vocab(gpu, kw):
     assert (cnt - q).abs().max().item() < 0.03, (kw, (cnt - q).abs().max().item())
 
 
+def test_sample_denormal_tail_mass(gpu):
+    """The probability form of the row is fp16 (u = exp((y - ymax) / T) in [0, 1]): a flat tail of 128k tokens
+    whose u lie in the fp16 SUBNORMAL range (here ~3.7e-6 each, ~4-5 % of the mass together) must keep its
+    mass through the packed sums (v_dot2) and the walk, or no draw ever lands in it."""
+    V, B = 128256, 4096
+    g = torch.Generator().manual_seed(9)
+    idx = torch.randperm(V, generator=g)[:40]
+    base = torch.full((V,), -8.0)
+    base[idx] = torch.linspace(2.0, -1.0, 40)
+    lg1 = base.to(torch.bfloat16).to(gpu)
+    T = 0.8
+    p = torch.softmax(lg1.float() / T, -1)
+    live = torch.zeros(V, dtype=torch.bool, device=gpu)
+    live[idx.to(gpu)] = True
+    u_tail = torch.exp(torch.tensor((-8.0 - 2.0) / T)).item()
+    assert u_tail < 6.1e-5  # fp16 subnormal
+    tok, *_ = _sample(lg1.expand(B, V), gpu, temperature=T)
+    cnt = torch.bincount(tok.long(), minlength=V).float() / B
+    tail_ref = p[~live].sum().item()
+    assert 0.02 < tail_ref < 0.1
+    assert abs(cnt[~live].sum().item() - tail_ref) < 0.015, (cnt[~live].sum().item(), tail_ref)
+    assert (cnt[live] - p[live]).abs().max().item() < 0.03
+
+
 def _penalised_ref(logits_bf16, counts, fpen, ppen, rpen):
     """fp32 torch reference of the sampler's logit processing (reference src/score/llm/mod.rs:39-72):
     for tokens already generated (count c > 0): y = y / rep if y > 0 else y * rep; y -= freq * c + pres;
