@@ -257,18 +257,26 @@ OPAQUE_ROW(row);
         if (t == 0) s_ccount = 0;
         __syncthreads();
       }
+      // candidates are sparse (a few dozen of 128k): one float compare per element and a wave-uniform
+      // branch on its ballot; only an element position where some lane of the wave hits runs the exact
+      // key test and the LDS append (key2f(lo) is the smallest value with key >= lo, so the float test
+      // passes a superset: -0 next to +0)
+      const float thr = key2f(lo);
 OPAQUE_ROW(row);
 #pragma unroll
       for (int j = 0; j < SLOTS; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float v = GET(row, j, e);
-          const int idx = (j * kSampT + t) * 8 + e;
-          if (f2key(v) >= lo) {  // padding past V holds -inf (key 0x7f < lo): never collected
-            const int slot = atomicAdd(&s_ccount, 1);
-            if (slot < kCollect) {
-              s_cval[slot] = v;
-              s_cidx[slot] = idx;
+          const bool h = v >= thr;
+          if (__builtin_amdgcn_ballot_w64(h)) {
+            const int idx = (j * kSampT + t) * 8 + e;
+            if (h && f2key(v) >= lo) {  // padding past V holds -inf (key 0x7f < lo): never collected
+              const int slot = atomicAdd(&s_ccount, 1);
+              if (slot < kCollect) {
+                s_cval[slot] = v;
+                s_cidx[slot] = idx;
+              }
             }
           }
         }
