@@ -22,6 +22,7 @@ broadcast at start-up (:func:`open_links`).
 """
 from __future__ import annotations
 
+import logging
 import os
 import pickle
 import socket
@@ -31,6 +32,7 @@ import time
 from typing import Any, Callable, Dict, List, Optional
 
 _LEN = struct.Struct("!I")
+_log = logging.getLogger(__name__)
 
 
 def _send(sock: socket.socket, obj: Any) -> None:
@@ -130,8 +132,8 @@ class LinkServer:
                 continue
             try:
                 self.on_message(rank, msg)
-            except Exception:  # noqa: BLE001 — a bad message must not stop the link
-                pass
+            except Exception:  # noqa: BLE001 — a bad message must not stop the link; it is logged
+                _log.exception("shard link: message from rank %d dropped", rank)
 
     def _monitor(self) -> None:
         while not self._closed:

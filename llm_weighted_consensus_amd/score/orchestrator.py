@@ -304,6 +304,7 @@ class ScoreClient:
             for t in tasks:
                 if not t.done():
                     t.cancel()
+            self._release(ctx)
 
         # ---- tally (native consensus core) + final chunk (reference client.rs:384-463)
         voter_choices = aggregate.choices[C_len:]
@@ -334,6 +335,10 @@ class ScoreClient:
         yield aggregate
         if all_error:
             yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+
+    def _release(self, ctx) -> None:
+        """Called when a request's voter streams end, however they end (the voter-sharded leader drops the
+        request's follower share here, score/sharded.py)."""
 
     def _voter_sources(self, ctx, rid, created, indexer, model: Model, weights, request, seeds) -> list:
         """The request's voter chunk streams, merged by arrival order (the reference's ``select_all``,

@@ -98,9 +98,9 @@ class _LinkHub:
             self.shares[seq] = sh
         return sh
 
-    def close(self, seq: int) -> None:
+    def close(self, seq: int) -> Optional[_Share]:
         with self.lock:
-            self.shares.pop(seq, None)
+            return self.shares.pop(seq, None)
 
     def _on_message(self, rank: int, msg) -> None:
         kind, seq = msg[0], msg[1]
@@ -264,6 +264,17 @@ class ShardedScoreClient(ScoreClient):
                                                    model=l.id, model_index=v))
         if choices:
             yield S.ScoreCompletionChunk(id=rid, created=created, model=model_id, choices=choices)
+
+    def _release(self, ctx) -> None:
+        """The request's stream ended: normally ``_remote``'s own ``finally`` has already dropped the share;
+        if that stream was cancelled before it ever ran (a generator that never starts never runs its
+        ``finally``), drop it here and tell its followers to stop — no hub entry or follower work outlives the
+        request."""
+        seq = ctx.get("seq") if isinstance(ctx, dict) else None
+        sh = self.hub.close(seq) if seq is not None else None
+        if sh is not None:
+            for r in sorted(sh.ranks):
+                self.link.send(r, ("cancel", seq))
 
     def close(self) -> None:
         self.link.close()

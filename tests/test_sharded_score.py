@@ -288,3 +288,39 @@ def test_killed_follower_isolated_as_error_choices():
 
 
 SCENARIOS = {"equiv": _equiv, "kill": _kill}
+
+
+class _FakeLink:
+    """LinkServer stand-in: one live follower (rank 1), sends recorded."""
+
+    def __init__(self):
+        self.sent = []
+        self.on_message = self.on_dead = None
+
+    def live(self):
+        return [1]
+
+    def send(self, rank, msg):
+        self.sent.append((rank, msg))
+        return True
+
+
+def test_release_drops_a_share_whose_stream_never_ran():
+    """ADVICE r3 (the pattern, on the new links): a follower share whose stream was cancelled before it ever
+    ran never runs its own ``finally``; the request's ``_release`` (called from the stream's ``finally`` in
+    ScoreClient._stream) drops the share and tells its follower to stop."""
+    from llm_weighted_consensus_amd.score.sharded import ShardedScoreClient
+
+    link = _FakeLink()
+    client = ShardedScoreClient(FakeChatClient(_policy), link, world=2, rng_seed=1)
+
+    async def main():
+        client.hub.open(7, {1: [0, 2]})
+        assert 7 in client.hub.shares
+        client._release({"seq": 7})
+        assert 7 not in client.hub.shares
+        assert link.sent == [(1, ("cancel", 7))]
+        client._release({"seq": 7})  # idempotent: nothing left to drop
+        assert link.sent == [(1, ("cancel", 7))]
+
+    asyncio.run(main())
