@@ -71,7 +71,10 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
   }
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+// x * sigmoid(x) with v_rcp_f32 (1 ulp) instead of the IEEE division sequence (v_div_scale x2, v_div_fmas,
+// v_div_fixup around an rcp: ~9 VALU per element in an epilogue of 256 per lane); the result is rounded
+// to bf16 (or e4m3) anyway.  x -> -inf: rcp(inf) = 0, x * 0 = -0 as the division gives
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // in: [T, 2F] = [gate | up]; out: [T, F]
 // gate of output column c at input column (c / blk) * 2 * blk + c % blk, up at + blk (blk = F: [gate | up]

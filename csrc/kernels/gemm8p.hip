@@ -82,7 +82,10 @@ LWC_DEVICE float4v mfma(const uint4v& a, const uint4v& b, const float4v& c) {
                                                  0, 0);
 }
 
-LWC_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+// x * sigmoid(x) with v_rcp_f32 (1 ulp) instead of the IEEE division sequence (v_div_scale x2, v_div_fmas,
+// v_div_fixup around an rcp: ~9 VALU per element in an epilogue of 256 per lane); the result is rounded
+// to bf16 (or e4m3) anyway.  x -> -inf: rcp(inf) = 0, x * 0 = -0 as the division gives
+LWC_DEVICE float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 // erf by Abramowitz & Stegun 7.1.26 (|error| < 1.5e-7, far below bf16's resolution): one exp, one rcp and a
 // 5-term polynomial — the libm erff's branches made the fused epilogue cost more than a separate pass.
 LWC_DEVICE float erf_as(float x) {
