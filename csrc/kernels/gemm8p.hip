@@ -90,7 +90,7 @@ LWC_DEVICE float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-
 // 5-term polynomial — the libm erff's branches made the fused epilogue cost more than a separate pass.
 LWC_DEVICE float erf_as(float x) {
   const float a = fabsf(x);
-  const float t = __frcp_rn(1.f + 0.3275911f * a);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * a);  // v_rcp_f32 (1 ulp): __frcp_rn is a full division sequence
   const float y = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
   return copysignf(1.f - y * __expf(-a * a), x);
 }
