@@ -69,6 +69,8 @@ struct Geo {
   static constexpr int OpB = BN * 128;          // W operand's K tile
   static constexpr int Buf = kOpA + OpB;        // one K tile
   static constexpr int Lds = 2 * Buf;           // two K tiles
+  static constexpr int Stage = 16 * 16 * NT * 2; // VAR 64: one wave's 16-row epilogue staging (bytes)
+  static constexpr int LdsPap = Lds + 4 * Stage;  // VAR 64: K buffers + the four waves' staging
   static constexpr int Pieces = 8 + NT;         // LDS-DMA pieces per wave per K tile
   static constexpr int Reads = 8 + NT;          // fragment reads per wave per k-step
 };
@@ -178,9 +180,15 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     };
 
     const int nt = KT;
-    stage(smem, 0);
+    // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
+    // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
+    // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
+    constexpr bool PAP = VAR == 64;
+    if (!PAP || round == 0) {
+      stage(smem, 0);
+      if (nt > 1) stage(smem + G::Buf, 1);
+    }
     if (nt > 1) {
-      stage(smem + G::Buf, 1);
       G4_VM(G::Pieces);
     } else {
       G4_VM(0);
@@ -312,7 +320,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }                                                                                               \
   }
     int r = 0;
-    if constexpr (VAR == 32) {
+    if constexpr (VAR == 32 || VAR == 64) {
       for (; r + 2 < nt; ++r) G4_TILE_H(r, true, true)
       if (nt >= 2) {
         G4_TILE_H(r, false, true)
@@ -340,8 +348,123 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     G4_MFMA_DRAIN();  // accumulators are read by VALU / stores from here on
     __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
 
-    // ---- epilogue: per wave 128 rows x CW bf16 columns through LDS, then 16 B stores
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
+    if constexpr (PAP) {
+      // ---- epilogue, wave-local: per m-tile (16 rows) through this wave's own staging slice, no block
+      // barrier; residual chunks all loaded up front into the (dead) fragment registers
+      constexpr int CPR = CW / 8;          // 16 B chunks per row
+      constexpr int PER = 16 * CPR / 64;   // chunks per lane per m-tile: 4 (bn 256), 3 (bn 192), 2 (SwiGLU)
+      bf16_t* st = reinterpret_cast<bf16_t*>(smem + G::Lds + wid * G::Stage);
+      const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
+      const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
+      const int row0 = m0 + wm * 128;
+      // operand loads of the epilogue FIRST, then the next tile's DMA: loads return in issue order, so a
+      // residual / bias value issued after the DMA pieces could only be used once they had landed
+      uint4v rv[8][PER];
+      float bvals[NT];
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int jj = 0; jj < NT; ++jj) {
+          const int col = n0 + wn * 16 * NT + r16 + jj * 16;
+          bvals[jj] = col < p.N ? bf2f(p.R[col]) : 0.f;
+        }
+      }
+      if constexpr (EPI == EPI_RESIDUAL) {
+        const int rows_here = max(0, min(p.M - row0, 128));
+        const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int u = 0; u < PER; ++u) {
+            const int c = lane + 64 * u;
+            const int row = i * 16 + c / CPR, gn = ncol0 + (c % CPR) * 8;
+            rv[i][u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
+          }
+      }
+      // ---- the next tile's first two K tiles into the (now free) K buffers, in flight under this epilogue
+      const int ntile = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
+      if (ntile < p.tiles) {
+        int um, un;
+        tile_mn(p, ntile, um, un);
+        const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.W + (size_t)un * G::BN * p.K), (short)0, min(p.N - un * G::BN, G::BN) * p.K * 2, 0x00020000);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          if (kt == 1 && nt < 2) break;
+#pragma unroll
+          for (int k = 0; k < G::Pieces; ++k) {
+            uint8_t* buf = smem + kt * G::Buf;
+            if (k < 8)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  nA, (__attribute__((address_space(3))) void*)(buf + k * 4096 + dst0), 16, voA, k * sA + kt * 128, 0, 0);
+            else
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  nW, (__attribute__((address_space(3))) void*)(buf + kOpA + (k - 8) * 4096 + dst0), 16, voW,
+                  (k - 8) * sW + kt * 128, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float4v t[NT];
+#pragma unroll
+        for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
+        if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+          for (int h = 0; h < NT / 4; ++h)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) t[h * 4 + jj][e] = silu(t[h * 4 + jj][e]) * t[h * 4 + jj + 2][e];
+        }
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+          for (int jj = 0; jj < NT; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float y = t[jj][e] + bvals[jj];
+              t[jj][e] = EPI == EPI_BIAS_GELU ? gelu_erf(y) : y;
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < NT; ++jj) {
+          if constexpr (EPI == EPI_SWIGLU) {
+            if ((jj & 3) >= 2) continue;
+          }
+          const int oc = EPI == EPI_SWIGLU ? (jj >> 2) * 32 + (jj & 1) * 16 : jj * 16;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 4 * q + e, col = oc + r16;
+            st[row * CW + swz<CW>(row, col)] = f2bf(t[jj][e]);
+          }
+        }
+        G4_LGKM0();  // the wave's staging writes landed before its lanes read each other's values
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int c = lane + 64 * u;
+          const int row = c / CPR, cch = c % CPR;
+          const int gm = row0 + i * 16 + row, gn = ncol0 + cch * 8;
+          uint4v v = *reinterpret_cast<const uint4v*>(st + row * CW + swz<CW>(row, cch * 8));
+          if constexpr (EPI == EPI_RESIDUAL) {
+            float x[8], y[8];
+            unpack8(v, x);
+            unpack8(rv[i][u], y);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] += y[e];
+            v = pack8(x);
+          }
+          if (gm < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+        }
+        G4_LGKM0();  // the staging reads are done before the next m-tile overwrites the slice
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;  // no block barrier: the next tile's first wait + barrier orders everything
+    }
+
+    // ---- epilogue: per wave 128 rows x CW bf16 columns through LDS, then 16 B stores
     bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -442,13 +565,14 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR>
 int launch3(const Params& p, hipStream_t s) {
+  constexpr int lds = VAR == 64 ? Geo<NT>::LdsPap : Geo<NT>::Lds;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              Geo<NT>::Lds);
+                              lds);
     attr = true;
   }
-  gemm4w_kernel<EPI, NT, VAR><<<8 * p.wpx, 256, Geo<NT>::Lds, s>>>(p);
+  gemm4w_kernel<EPI, NT, VAR><<<8 * p.wpx, 256, lds, s>>>(p);
   return (int)hipGetLastError();
 }
 
@@ -461,6 +585,7 @@ int launch(const Params& p, hipStream_t s) {
   // every epilogue carries 1 and 32, the plain one the other variants
   const int var = env_int("LWC_G4_VAR", 32);
   if (var == 32) return launch3<EPI, NT, 32>(p, s);
+  if (var == 64) return launch3<EPI, NT, 64>(p, s);
   if constexpr (EPI == EPI_PLAIN) {
     switch (var) {
       case 0: return launch3<EPI, NT, 0>(p, s);

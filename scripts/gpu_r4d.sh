@@ -16,7 +16,7 @@ MICRO_PREFIX_QUICK=1 timeout -k 10 300 python3 -u scripts/microbench.py sample p
 rc=$?; echo "micro rc=$rc"; grep -v amdgpu.ids gpurun_out/micro_r4d.log | tail -14; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u scripts/microbench.py small > gpurun_out/micro_small_r4d.log 2>&1
 rc=$?; echo "micro small rc=$rc"; grep "rope\|silu" gpurun_out/micro_small_r4d.log; [ $rc -eq 0 ] || exit $rc
-G4_VARS="32" G4_VARS_EPI="32" G4_SHAPES="0,1,2,3,4" timeout -k 10 400 python3 -u scripts/microbench.py g4ab \
+G4_VARS="32,64" G4_VARS_EPI="32,64" G4_SHAPES="0,1,2,3,4" timeout -k 10 400 python3 -u scripts/microbench.py g4ab \
     > gpurun_out/micro_g4_r4d.log 2>&1
 rc=$?; echo "g4ab rc=$rc"; grep g4ab gpurun_out/micro_g4_r4d.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_r4c.sh

@@ -930,7 +930,7 @@ def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
     _close(gemm_plan.linear_bias(A, W, b, gelu=gelu), ref, 3e-2, 1e-2)
 
 
-@pytest.mark.parametrize("var", [1, 32])
+@pytest.mark.parametrize("var", [1, 32, 64])
 @pytest.mark.parametrize("bn", [256, 192])
 @pytest.mark.parametrize("M,N,K,epi", [(300, 520, 64, "plain"), (4096, 6144, 4096, "plain"), (513, 1000, 128, "res"),
                                        (1024, 1024, 14336, "res"), (700, 2048, 1024, "swiglu"),
@@ -939,7 +939,8 @@ def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
 def test_gemm4w(gpu, M, N, K, epi, bn, var, monkeypatch):
     """4-wave interleaved MFMA GEMM (AGPR accumulators, in-place inline-asm MFMA) vs an fp32 matmul for every
     epilogue: ragged M / N tails, one / two / many K tiles (the peeled last iterations), both tile widths,
-    several rounds of tiles per workgroup, both main-loop schedules (LWC_G4_VAR 1 and the library-shaped 32).
+    several rounds of tiles per workgroup, the main-loop schedules (LWC_G4_VAR 1, the library-shaped 32, and 64:
+    32 with the next tile's first K tiles issued under the wave-local epilogue of the current one).
     Launched twice (persistent rounds must leave LDS reusable)."""
     from llm_weighted_consensus_amd import ops
 
