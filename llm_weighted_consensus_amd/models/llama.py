@@ -19,6 +19,7 @@ prompt-chunk rows to K4's paged-KV mode; the k/v are scattered into the paged ca
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Optional
@@ -302,8 +303,10 @@ class LlamaModel:
         x = ops.embedding(self.embed, tokens)
         B = tokens.shape[0]
         # q is rotated inside the attention kernels as they load it (rope_kv_write rotates and caches k
-        # only): q's round trip through HBM in rope_kv_write (2/3 of its bytes at GQA 4) is gone
-        rope = (self.cos, self.sin, positions)
+        # only): q's round trip through HBM in rope_kv_write (2/3 of its bytes at GQA 4) is gone.
+        # LWC_DECODE_QROPE=0: the previous split (rope_kv_write rotates q in place), an A/B knob
+        q_at_load = os.environ.get("LWC_DECODE_QROPE", "1") != "0"
+        rope = (self.cos, self.sin, positions) if q_at_load else None
         if cascade_tiles is not None:
             def attn_fn(qkv, li):
                 return ops.paged_decode_cascade(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cascade_tiles,
@@ -318,7 +321,7 @@ class LlamaModel:
                 return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
                                         num_splits=num_splits, part_o=part_o, part_lse=part_lse, rope=rope)
 
-        h = self._layers(x, cache, positions, slots, attn_fn, rope_q=False)
+        h = self._layers(x, cache, positions, slots, attn_fn, rope_q=not q_at_load)
         return self._proj(h, self.lm_head)
 
     def encode(self, tokens: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor,
