@@ -935,7 +935,11 @@ def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
 @pytest.mark.parametrize("M,N,K,epi", [(300, 520, 64, "plain"), (4096, 6144, 4096, "plain"), (513, 1000, 128, "res"),
                                        (1024, 1024, 14336, "res"), (700, 2048, 1024, "swiglu"),
                                        (257, 776, 320, "bias"), (520, 4096, 1024, "gelu"),
-                                       (64, 384, 192, "plain"), (2048, 128256 // 8, 4096, "plain")])
+                                       (64, 384, 192, "plain"), (2048, 128256 // 8, 4096, "plain"),
+                                       # > 256 tiles: every epilogue across persistent rounds (VAR 64's
+                                       # cross-tile prefetch under the epilogue)
+                                       (4096, 4352, 256, "res"), (4352, 4096, 128, "swiglu"),
+                                       (4352, 4096, 192, "gelu")])
 def test_gemm4w(gpu, M, N, K, epi, bn, var, monkeypatch):
     """4-wave interleaved MFMA GEMM (AGPR accumulators, in-place inline-asm MFMA) vs an fp32 matmul for every
     epilogue: ragged M / N tails, one / two / many K tiles (the peeled last iterations), both tile widths,
