@@ -183,7 +183,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
-    constexpr bool PAP = VAR == 64;
+    // (the residual epilogue keeps the block-staged path: its wave-local form failed test_gemm4w numerics
+    // on the GPU — open; o / down are single-round at the decode batch, where the prefetch has no next tile)
+    constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
     if (!PAP || round == 0) {
       stage(smem, 0);
       if (nt > 1) stage(smem + G::Buf, 1);
@@ -565,7 +567,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = VAR == 64 ? Geo<NT>::LdsPap : Geo<NT>::Lds;
+  constexpr int lds = VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
