@@ -113,6 +113,16 @@ LWC_DEVICE int swz(int row, int col) {
   return col ^ (((row & 7) << 3) % CW);
 }
 
+// A buffer resource built from explicitly wave-uniform parts: for the epilogue's resources the compiler
+// could not prove uniformity and wrapped every buffer access in a readfirstlane waterfall loop
+LWC_DEVICE __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 template <int EPI, int NT, int VAR>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   using G = Geo<NT>;
@@ -183,8 +193,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
-    // (the residual epilogue keeps the block-staged path: its wave-local form failed test_gemm4w numerics
-    // on the GPU — open; o / down are single-round at the decode batch, where the prefetch has no next tile)
+    // (residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
+    // there is no next tile to prefetch, and 32 up-front residual chunks per lane would spill)
     constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
     if (!PAP || round == 0) {
       stage(smem, 0);
@@ -359,7 +369,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       bf16_t* st = reinterpret_cast<bf16_t*>(smem + G::Lds + wid * G::Stage);
       const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
       const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-      const int row0 = m0 + wm * 128;
+      const int row0 = __builtin_amdgcn_readfirstlane(m0 + wm * 128);  // uniform: buffer resources in SGPRs, no waterfall loops
+      // stores branch-free through a buffer resource over this wave's rows: a lane whose chunk lies past
+      // the last column takes an offset past the resource's end, so the hardware drops it (no exec-masked
+      // store branches between the epilogue's memory operations)
+      const int rows_c = max(0, min(p.M - row0, 128));
+      const __amdgpu_buffer_rsrc_t rC = uniform_rsrc(p.C + (size_t)row0 * p.ldc, rows_c * p.ldc * 2);
       // operand loads of the epilogue FIRST, then the next tile's DMA: loads return in issue order, so a
       // residual / bias value issued after the DMA pieces could only be used once they had landed
       uint4v rv[8][PER];
@@ -373,8 +388,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       }
       if constexpr (EPI == EPI_RESIDUAL) {
         const int rows_here = max(0, min(p.M - row0, 128));
-        const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.R + (size_t)row0 * p.ldc, rows_here * p.ldc * 2);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -458,7 +472,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             for (int e = 0; e < 8; ++e) x[e] += y[e];
             v = pack8(x);
           }
-          if (gm < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+          (void)gm;
+          const uint32_t off = gn < ncols ? (uint32_t)(((i * 16 + row) * p.ldc + gn) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
         }
         G4_LGKM0();  // the staging reads are done before the next m-tile overwrites the slice
         __builtin_amdgcn_sched_barrier(0);
@@ -521,10 +537,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       // without a request; columns past N are never stored), kGrp of them in flight per lane before the
       // first add: loaded inside the store's bounds branch, every chunk waited its own HBM round trip
       // (vmcnt(0) per 16 B, the epilogue's whole latency).
-      const int row0 = m0 + wm * 128;
+      const int row0 = __builtin_amdgcn_readfirstlane(m0 + wm * 128);  // uniform: buffer resources in SGPRs, no waterfall loops
       const int rows_here = max(0, min(p.M - row0, 128));
-      const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.R + (size_t)row0 * p.ldc, rows_here * p.ldc * 2);
       constexpr int kIt = 128 * CPR / 64;                         // chunks per lane: 32 (bn 256), 24 (bn 192)
       constexpr int kGrp = kIt % 16 == 0 ? 16 : (kIt % 12 == 0 ? 12 : 8);  // whole groups only
       static_assert(kIt % kGrp == 0, "residual epilogue groups must tile the wave's chunks");
