@@ -99,6 +99,18 @@ LWC_DEVICE float row_sum4(float v) {
 }
 
 
+// A buffer resource built from explicitly wave-uniform parts (readfirstlane of the base address and the
+// size).  Built straight from kernel arguments / tile indices, the compiler sometimes cannot prove the
+// resource uniform and wraps EVERY buffer access through it in a readfirstlane "waterfall" loop (~10
+// instructions and a branch per access, inside GEMM main loops too).
+LWC_DEVICE __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): consecutive remapped ids land on the same XCD so neighbouring tiles share L2.
 LWC_DEVICE int xcd_remap(int orig, int nwg) {

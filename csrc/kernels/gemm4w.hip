@@ -113,16 +113,6 @@ LWC_DEVICE int swz(int row, int col) {
   return col ^ (((row & 7) << 3) % CW);
 }
 
-// A buffer resource built from explicitly wave-uniform parts: for the epilogue's resources the compiler
-// could not prove uniformity and wrapped every buffer access in a readfirstlane waterfall loop
-LWC_DEVICE __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
-  const uint64_t a = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 template <int EPI, int NT, int VAR>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   using G = Geo<NT>;

@@ -114,10 +114,8 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   const int sw = (r16 >> 1) & 7;
   const int off0 = r16 * 128 + ((q ^ sw) << 4), off1 = r16 * 128 + (((4 + q) ^ sw) << 4);
 
-  const __amdgpu_buffer_rsrc_t rA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.rows_a * p.lda, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.W + ((size_t)g * p.N + n0) * p.K), (short)0, min(p.N - n0, 256) * p.K, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(p.A, p.rows_a * p.lda);
+  const __amdgpu_buffer_rsrc_t rW = uniform_rsrc(p.W + ((size_t)g * p.N + n0) * p.K, min(p.N - n0, 256) * p.K);
   auto stage = [&](int u, uint8_t* buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {

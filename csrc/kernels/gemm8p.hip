@@ -171,10 +171,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
 
     // buffer descriptors of the tile's A rows / W rows: rows past M / N fall outside num_records and
     // load as zeros (their outputs are not stored)
-    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.A + (size_t)m0 * p.lda), (short)0, (p.M - m0) * p.lda * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.W + (size_t)n0 * p.K), (short)0, min(p.N - n0, 256) * p.K * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(p.A + (size_t)m0 * p.lda, (p.M - m0) * p.lda * 2);
+    const __amdgpu_buffer_rsrc_t rW = uniform_rsrc(p.W + (size_t)n0 * p.K, min(p.N - n0, 256) * p.K * 2);
     auto stage = [&](int u, uint8_t* buf, int kt) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -361,8 +359,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(Params p) {
       // HBM round trip
       const int row0 = m0 + wr * 128;
       const int rows_here = max(0, min(p.M - row0, 128));
-      const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(p.R + (size_t)row0 * p.ldc), (short)0, rows_here * p.ldc * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.R + (size_t)row0 * p.ldc, rows_here * p.ldc * 2);
       const int gn = ncol0 + cch * 8;
       constexpr int kIt = 128 / RPI, kGrp = kIt < 16 ? kIt : 16;
       static_assert(kIt % kGrp == 0, "residual epilogue groups must tile the wave's rows");
