@@ -348,23 +348,31 @@ OPAQUE_ROW(row);
       }
       raw_lse = raw_max + __logf(block_sum(se, sred));
     }
-    // ---- greedy: argmax (lowest index on ties) ----
-    float bv = -INFINITY;
+    // ---- greedy: argmax (lowest index on ties).  The row maximum is known (the raw max; a processed row
+    // takes one max pass), so the argmax is the lowest index holding it — instead of a value-and-index
+    // compare chain with a branch per element.  (Padding past V holds -inf: it can only match
+    // a row that is -inf everywhere, whose answer, index 0, is found first.)
+    float gm = raw_max;
+    if (processed) {
+      float ym = -INFINITY;
+OPAQUE_ROW(row);
+#pragma unroll
+      for (int j = 0; j < SLOTS; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ym = fmaxf(ym, GET(row, j, e));
+      gm = block_max(ym, sred);
+    }
+    // the thread's elements visited from its highest index down, the last match wins: its lowest index,
+    // one compare + one select per element, no branch
     int bi = 0x7fffffff;
 OPAQUE_ROW(row);
 #pragma unroll
-    for (int j = 0; j < SLOTS; ++j)
+    for (int j = SLOTS - 1; j >= 0; --j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = GET(row, j, e);
-        const int idx = (j * kSampT + t) * 8 + e;
-        if (idx < p.V && (v > bv || (v == bv && idx < bi))) {
-          bv = v;
-          bi = idx;
-        }
+      for (int e = 7; e >= 0; --e) {
+        bi = GET(row, j, e) == gm ? (j * kSampT + t) * 8 + e : bi;
       }
-    const float gm = block_max(bv, sred);
-    int cand = (bv == gm) ? bi : 0x7fffffff;
+    int cand = bi;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
     __syncthreads();
