@@ -28,7 +28,7 @@ int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, 
 int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
-                   int, int, int, int, int, hipStream_t);
+                   int, int, int, int, int, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -404,7 +404,7 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
 
 void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& row_off,
                 int64_t max_slots, const c10::optional<at::Tensor>& a_rows, const at::Tensor& a_scale,
-                const at::Tensor& w_scale) {
+                const at::Tensor& w_scale, bool swiglu) {
   // grouped fp8 GEMM on the 8-phase schedule (gemm8g.hip): A [rows_a, K] e4m3, W [G, N, K] e4m3, C [rows, N] bf16;
   // row_off None: the dense projection (G = 1, every output row)
   CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_CONTIG(W);
@@ -420,7 +420,8 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
     TORCH_CHECK(G == 1, "gemm8g: dense mode (no row_off) takes one weight");
     TORCH_CHECK(max_slots >= (C.size(0) + 255) / 256, "gemm8g: dense mode needs ceil(rows / 256) slots");
   }
-  TORCH_CHECK(A.size(1) == K && C.size(1) == N, "gemm8g: shape mismatch");
+  TORCH_CHECK(A.size(1) == K && C.size(1) == (swiglu ? N / 2 : N), "gemm8g: shape mismatch");
+  TORCH_CHECK(!swiglu || N % 64 == 0, "gemm8g: SwiGLU needs whole 64-row gate / up block pairs");
   CHECK_DTYPE(a_scale, at::kFloat); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_CONTIG(w_scale);
   TORCH_CHECK(a_scale.numel() >= A.size(0) && w_scale.numel() == (int64_t)G * N, "gemm8g: scale shapes");
   const int* ar = nullptr;
@@ -433,7 +434,7 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
   }
   CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), ro, ar, a_scale.data_ptr<float>(),
                           w_scale.data_ptr<float>(), G, (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0),
-                          (int)A.size(0), (int)C.size(0), cur_stream()),
+                          (int)A.size(0), (int)C.size(0), swiglu ? 1 : 0, cur_stream()),
            "gemm8g_fp8");
 }
 

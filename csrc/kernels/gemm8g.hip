@@ -55,6 +55,12 @@ LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, c
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 0, 0, 0, 127, 0, 127);
 }
 
+LWC_DEVICE float silu8(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
+// SWIGLU: W's rows are gate / up interleaved in blocks of 32 (ops.swiglu_interleave per expert), so each
+// wave's 64 columns are one gate block and its up block; the epilogue applies the scales, then
+// silu(gate) * up, and writes [rows, N / 2] bf16 — the [rows, N] gate|up intermediate never reaches HBM.
+template <bool SWIGLU>
 __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // ---- work item: XCD-grouped (n-tile, m-slot), then (group, m-tile) of the slot ----
@@ -222,27 +228,53 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
       for (int jj = 0; jj < 4; ++jj) acc[i][jj][rr] *= as * ws[jj];
       __builtin_amdgcn_sched_barrier(0);  // one scale load in flight at a time: no 32-load VGPR burst
     }
-  constexpr int CW = 64;
-  bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
+  if constexpr (SWIGLU) {
+    // columns jj 0, 1 of the wave are gate, jj 2, 3 the matching up columns: 32 outputs per row
+    constexpr int CW = 32;
+    bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
+      for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = i * 16 + 4 * q + rr, col = jj * 16 + r16;
-        ot[row * CW + (col ^ ((row & 7) << 3))] = f2bf(acc[i][jj][rr]);
-      }
-  __syncthreads();
-  const int cch = lane % 8;
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = i * 16 + 4 * q + rr, col = jj * 16 + r16;
+          ot[row * CW + (col ^ ((row & 3) << 3))] = f2bf(silu8(acc[i][jj][rr]) * acc[i][jj + 2][rr]);
+        }
+    __syncthreads();
+    const int cch = lane % 4, nout = p.N / 2;
 #pragma unroll 4
-  for (int k = 0; k < 16; ++k) {
-    const int row = lane / 8 + 8 * k;
-    const int gm = m_begin + wr * 128 + row;
-    const int gn = n0 + wc * 64 + cch * 8;
-    if (gm < m_end && gn < p.N)
-      *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
-          *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 7) << 3)));
+    for (int k = 0; k < 8; ++k) {
+      const int row = lane / 4 + 16 * k;
+      const int gm = m_begin + wr * 128 + row;
+      const int gn = n0 / 2 + wc * 32 + cch * 8;
+      if (gm < m_end && gn < nout)
+        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
+            *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3)));
+    }
+  } else {
+    constexpr int CW = 64;
+    bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = i * 16 + 4 * q + rr, col = jj * 16 + r16;
+          ot[row * CW + (col ^ ((row & 7) << 3))] = f2bf(acc[i][jj][rr]);
+        }
+    __syncthreads();
+    const int cch = lane % 8;
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int row = lane / 8 + 8 * k;
+      const int gm = m_begin + wr * 128 + row;
+      const int gn = n0 + wc * 64 + cch * 8;
+      if (gm < m_end && gn < p.N)
+        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
+            *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 7) << 3)));
+    }
   }
 }
 
@@ -254,15 +286,17 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
 // sum_g ceil(M_g / 256) (ceil(rows / 256) + G always is).  row_off == null: dense, G = 1, rows [0, rows_c).
 extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* row_off, const int* a_rows,
                               const float* a_scale, const float* w_scale, int G, int max_slots, int N, int K, int lda,
-                              int ldc, int rows_a, int rows_c, hipStream_t s) {
+                              int ldc, int rows_a, int rows_c, int swiglu, hipStream_t s) {
   using namespace lwc::g8g;
   if (K % 128 != 0 || K < 128 || N % 8 != 0 || lda % 16 != 0 || ldc % 8 != 0 || G < 1) return -1;
   if ((long long)rows_a * lda >= (1LL << 31) || 256LL * K >= (1LL << 31)) return -1;
   if (!a_scale || !w_scale) return -2;
+  if (swiglu && N % 64 != 0) return -1;  // whole gate / up block pairs per wave
   if (max_slots <= 0) return 0;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8g_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
     attr = true;
   }
   const int n_tiles = (N + 255) / 256;
@@ -271,6 +305,9 @@ extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* 
   // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: n-tile rounds of 8 x max_slots m-slots
   const unsigned grid = row_off ? (unsigned)(((n_tiles + 7) / 8) * max_slots * 8)
                                 : (unsigned)(8 * ((n_tiles * max_slots + 7) / 8));
-  gemm8g_kernel<<<grid, 512, kLdsB, s>>>(p);
+  if (swiglu)
+    gemm8g_kernel<true><<<grid, 512, kLdsB, s>>>(p);
+  else
+    gemm8g_kernel<false><<<grid, 512, kLdsB, s>>>(p);
   return (int)hipGetLastError();
 }

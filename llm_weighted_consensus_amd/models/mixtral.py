@@ -113,6 +113,9 @@ class MixtralModel(LlamaModel):
         w2_s = w2[:, :, r * fl:(r + 1) * fl].contiguous()                                             # [E,d,fl]
         s13 = s2 = None
         if self.fp8:
+            # gate / up rows interleaved in blocks of 32 per expert: the grouped fp8 GEMM applies the SwiGLU
+            # in its epilogue (no [rows, 2F] intermediate), then one per-row e4m3 pass feeds the down GEMM
+            w13 = torch.stack([ops.swiglu_interleave(w13[e]) for e in range(w13.shape[0])])
             w13, s13 = ops.quant_fp8_weight(w13)
             w2_s, s2 = ops.quant_fp8_weight(w2_s)
             # the attention projections are fp8 too (config 5: fp8 MFMA throughout; router and lm_head bf16)
@@ -215,8 +218,9 @@ class MixtralModel(LlamaModel):
                  rows: Optional[int] = None) -> torch.Tensor:
         """Grouped expert FFN over expert-major rows (optionally gathered through ``a_rows``)."""
         if self.fp8:
-            gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows, a_scale=scale, w_scale=L.s13)
-            aq, as_ = ops.silu_mul_quant_fp8(gu)
+            act = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows, a_scale=scale, w_scale=L.s13,
+                                   swiglu=True)
+            aq, as_ = ops.quant_fp8_rows(act)
             return ops.grouped_gemm(aq, L.w2, row_off, a_scale=as_, w_scale=L.s2)
         gu = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows)
         return ops.grouped_gemm(ops.silu_mul(gu), L.w2, row_off)

@@ -255,7 +255,7 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
                  out: Optional[torch.Tensor] = None, a_scale: Optional[torch.Tensor] = None,
                  w_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
                  a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None,
-                 splits: Optional[int] = None) -> torch.Tensor:
+                 splits: Optional[int] = None, swiglu: bool = False) -> torch.Tensor:
     """Grouped GEMM on MFMA (K6g): rows [row_off[g], row_off[g+1]) of A times W[g]^T -> C [rows, N] bf16.
     ``a_rows`` [rows] gathers A's row for each output row (MoE dispatch; then ``rows`` = len(a_rows)).
     ``row_off`` lives on the device (MoE expert segments: no host sync, graph-capturable).  fp8 e4m3fn
@@ -263,16 +263,22 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
     (default: ceil(rows/128) + G, enough for any split of the rows into G groups).  ``splits`` > 1 splits
     K over that many workgroups per tile (fp32 atomics into a workspace, then one bf16 pass); default:
     chosen so a small-M launch (MoE decode down projection: 8 experts x 32 column tiles) still puts
-    ~4 workgroups on every CU."""
+    ~4 workgroups on every CU.  ``swiglu=True``: W's rows are gate / up interleaved in blocks of 32
+    (:func:`swiglu_interleave` per group) and the result is silu(gate) * up [rows, N/2] — from the 8-phase
+    kernel's epilogue when it takes the batch, else GEMM + the SwiGLU pass."""
     if rows is None:
         rows = a_rows.numel() if a_rows is not None else A.shape[0]
     G, N, K = W.shape[0], W.shape[1], W.shape[2]
-    if _use_gemm8g(A, W, rows, G, N, K, bias, splits, out):
+    if _use_gemm8g(A, W, rows, G, N, K, bias, splits, out) and (not swiglu or N % 64 == 0):
         # large fp8 expert batches (>= ~1 full 256-row tile per expert on average): the 8-phase kernel
         if out is None:
-            out = torch.empty(rows, N, dtype=torch.bfloat16, device=A.device)
-        kernels().gemm8g_fp8(A, W, out, row_off, -(-rows // 256) + G, a_rows, a_scale, w_scale.contiguous())
+            out = torch.empty(rows, N // 2 if swiglu else N, dtype=torch.bfloat16, device=A.device)
+        kernels().gemm8g_fp8(A, W, out, row_off, -(-rows // 256) + G, a_rows, a_scale, w_scale.contiguous(),
+                             bool(swiglu))
         return out
+    if swiglu:
+        return silu_mul(grouped_gemm(A, W, row_off, max_slots=max_slots, a_scale=a_scale, w_scale=w_scale,
+                                     bias=bias, a_rows=a_rows, rows=rows, splits=splits), out=out, block=32)
     if max_slots is None:
         max_slots = -(-rows // 128) + G
     if out is None:
@@ -474,7 +480,7 @@ def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Option
     if M == 0:
         return out
     kernels().gemm8g_fp8(xq, w.q.view(1, N, K), out, None, -(-M // 256), None, xs.reshape(-1).contiguous(),
-                         w.s.reshape(-1))
+                         w.s.reshape(-1), False)
     return out
 
 

@@ -839,7 +839,7 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     a_rows = torch.randperm(rows + 37, device=gpu)[:rows].to(torch.int32) if gather else None
     out = torch.full((rows, N), float("nan"), dtype=torch.bfloat16, device=gpu)
     ops.kernels().gemm8g_fp8(Aq, Wq, out, off, -(-rows // 256) + G, a_rows, a_s.float().contiguous(),
-                             w_s.float().contiguous())
+                             w_s.float().contiguous(), False)
     Ar = Aq.float() * a_s[:, None]
     if gather:
         Ar = Ar[a_rows.long()]
@@ -855,6 +855,45 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     classic = ops.grouped_gemm(Ac, Wq, off, a_scale=sc.float().contiguous(), w_scale=w_s.float().contiguous(),
                                a_rows=a_rows, rows=rows, splits=1, max_slots=-(-rows // 128) + G)
     _close(out, classic, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+@pytest.mark.parametrize("moe_gemm", ["g8", "classic"])
+def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch):
+    """MoE gate|up with the SwiGLU fused (gemm8g's epilogue; the 128x128 kernel + the SwiGLU pass when it
+    takes the batch): gate / up rows interleaved in blocks of 32 per expert, ragged groups, A-row gather,
+    per-row / per-channel scales -> silu(A Wg^T) * (A Wu^T) [rows, F] vs an fp32 reference."""
+    from llm_weighted_consensus_amd import ops
+
+    monkeypatch.setattr(ops, "MOE_GEMM", moe_gemm)
+    torch.manual_seed(13)
+    G, F, K = 4, 320, 512
+    sizes = [300, 0, 77, 520]
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    A = torch.randn(rows + 11, K, device=gpu)
+    W = torch.randn(G, 2 * F, K, device=gpu) * 0.05       # [gate (F); up (F)] per expert
+    Wi = torch.stack([ops.swiglu_interleave(W[g]) for g in range(G)])
+    a_s = A.abs().amax(1).clamp(min=1e-6) / 448.0
+    w_s = Wi.abs().amax(2).clamp(min=1e-6) / 448.0
+    Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
+    Wq = (Wi / w_s[:, :, None]).to(torch.float8_e4m3fn)
+    a_rows = torch.randperm(rows + 11, device=gpu)[:rows].to(torch.int32) if gather else None
+    Ac, sc = (Aq, a_s) if gather else (Aq[:rows], a_s[:rows])
+    out = ops.grouped_gemm(Ac, Wq, off, a_scale=sc.float().contiguous(), w_scale=w_s.float().contiguous(),
+                           a_rows=a_rows, rows=rows, swiglu=True)
+    assert out.shape == (rows, F)
+    Ar = Aq.float() * a_s[:, None]
+    if gather:
+        Ar = Ar[a_rows.long()]
+    Wr = Wq.float() * w_s[:, :, None]
+    o = off.tolist()
+    for g in range(G):
+        if o[g + 1] > o[g]:
+            y = Ar[o[g]:o[g + 1]] @ Wr[g].t()                        # interleaved gate / up columns
+            yb = y.view(-1, F // 32, 2, 32)
+            want = (torch.nn.functional.silu(yb[:, :, 0]) * yb[:, :, 1]).reshape(-1, F)
+            _close(out[o[g]:o[g + 1]], want, 3e-2, 2e-2)
 
 
 @pytest.mark.parametrize("d,rows", [(4096, 1), (4096, 301), (2048, 64), (8192, 257), (1024, 33)])
