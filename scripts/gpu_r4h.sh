@@ -13,5 +13,7 @@ timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thre
 rc=$?; echo "pytest model rc=$rc"; tail -3 gpurun_out/pytest_r4h2.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u scripts/moe_swiglu_ab.py > gpurun_out/moe_swiglu_r4h.log 2>&1
 rc=$?; echo "ab rc=$rc"; grep "T=" gpurun_out/moe_swiglu_r4h.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python3 bench_configs.py moe --requests ${MOE_R:-32} --steps 2 > gpurun_out/cfg5_r4h.log 2> gpurun_out/cfg5_r4h.err
-rc=$?; echo "config5 rc=$rc"; tail -1 gpurun_out/cfg5_r4h.log | cut -c1-200; exit $rc
+for R in 32 64; do
+  timeout -k 10 900 python3 bench_configs.py moe --requests $R --steps 2 > gpurun_out/cfg5_r4h_r$R.log 2> gpurun_out/cfg5_r4h_r$R.err
+  rc=$?; echo "config5 R=$R rc=$rc"; tail -1 gpurun_out/cfg5_r4h_r$R.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
+done
