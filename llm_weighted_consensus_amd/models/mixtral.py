@@ -55,6 +55,7 @@ class MoELayerWeights:
     w2: torch.Tensor              # [E, d, F_local]
     s13: Optional[torch.Tensor]   # fp8 per-channel scales [E, 2F_local]
     s2: Optional[torch.Tensor]    # [E, d]
+    gu_block: int = 0             # >0: w13 rows interleave gate|up in blocks of this size (fp8 path)
 
 
 class MixtralModel(LlamaModel):
@@ -120,7 +121,8 @@ class MixtralModel(LlamaModel):
             w2_s, s2 = ops.quant_fp8_weight(w2_s)
             # the attention projections are fp8 too (config 5: fp8 MFMA throughout; router and lm_head bf16)
             wqkv, wo_s = ops.Fp8Weight(wqkv), ops.Fp8Weight(wo_s)
-        return MoELayerWeights(attn_norm, wqkv, wo_s, mlp_norm, router.contiguous(), w13, w2_s, s13, s2)
+        return MoELayerWeights(attn_norm, wqkv, wo_s, mlp_norm, router.contiguous(), w13, w2_s, s13, s2,
+                               32 if self.fp8 else 0)
 
     def _random_init(self, seed: int) -> None:
         cfg, dev, dt = self.full_cfg, self.device, self.dtype

@@ -98,6 +98,11 @@ def moe_mlp(model, L, h):
     for t in range(h.shape[0]):
         for j in range(k):
             e = int(ids[t, j])
-            g, u = (h[t] @ w13[e].t()).chunk(2)
+            gu = h[t] @ w13[e].t()
+            if getattr(L, "gu_block", 0):
+                gu = gu.view(-1, 2, L.gu_block)
+                g, u = gu[:, 0].reshape(-1), gu[:, 1].reshape(-1)
+            else:
+                g, u = gu.chunk(2)
             out[t] += w[t, j] * ((F.silu(g) * u) @ w2[e].t())
     return out
