@@ -7,11 +7,23 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
+
+
+def _collect(q, procs, timeout):
+    """Gather (rank, result) pairs. Workers send numpy arrays (pickled by value): a CPU tensor put on a
+    queue is shared through a file descriptor that dies with the worker, so a worker that exits before the
+    parent reads the queue would reset the connection."""
+    out = {}
+    for _ in procs:
+        r, v = q.get(timeout=timeout)
+        out[r] = torch.from_numpy(v) if isinstance(v, np.ndarray) else v
+    return out
 
 def _free_port():
     s = socket.socket()
@@ -84,7 +96,7 @@ def test_ipc_allreduce_two_ranks_one_gpu(gpu):
     procs = [ctx.Process(target=_ar_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = _collect(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
     assert res == {0: [], 1: []}, res
@@ -120,7 +132,7 @@ def _tp_worker(rank, world, port, fp8, q, arch="mixtral-tiny"):
                        torch.tensor([P - 1], device=dev), cache)
         torch.cuda.synchronize(dev)
         comm.check()
-        q.put((rank, lg[0].float().cpu()))
+        q.put((rank, lg[0].float().cpu().numpy()))
         pdist.barrier()
         comm.close()
         pdist.shutdown()
@@ -142,7 +154,7 @@ def test_tp2_through_ipc_allreduce(gpu, arch):
     procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, False, q, arch)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in procs)
+    res = _collect(q, procs, 600)
     for p in procs:
         p.join(timeout=120)
     assert all(isinstance(v, torch.Tensor) for v in res.values()), res
@@ -198,7 +210,7 @@ def test_ipc_allreduce_back_to_back_no_false_timeout(gpu):
     procs = [ctx.Process(target=_back_to_back_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = _collect(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
     assert res == {0: [], 1: []}, res
@@ -253,7 +265,7 @@ def test_ipc_allreduce_missing_peer_fails_loudly(gpu):
     procs = [ctx.Process(target=_skip_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = _collect(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
     assert isinstance(res[0], dict) and isinstance(res[1], dict), res

@@ -8,6 +8,7 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.multiprocessing as mp
 
@@ -44,7 +45,10 @@ def _run(world, target, *args, timeout=300):
     procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=timeout) for _ in procs)
+    res = {}
+    for _ in procs:
+        r, v = q.get(timeout=timeout)
+        res[r] = torch.from_numpy(v) if isinstance(v, np.ndarray) else v
     for p in procs:
         p.join(timeout=60)
     return res
@@ -188,7 +192,7 @@ def _ep_worker(rank, world, port, q, fp8):
         comm.check()
         pdist.barrier()
         comm.close()
-        q.put((rank, lg))
+        q.put((rank, lg.float().cpu().numpy()))  # by value: a shared CPU tensor dies with its sender
         pdist.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))

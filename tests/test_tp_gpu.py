@@ -6,11 +6,23 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
+
+
+def _collect(q, procs, timeout):
+    """Gather (rank, result) pairs. Workers send numpy arrays (pickled by value): a CPU tensor put on a
+    queue is shared through a file descriptor that dies with the worker, so a worker that exits before the
+    parent reads the queue would reset the connection."""
+    out = {}
+    for _ in procs:
+        r, v = q.get(timeout=timeout)
+        out[r] = torch.from_numpy(v) if isinstance(v, np.ndarray) else v
+    return out
 
 def _free_port():
     s = socket.socket()
@@ -40,7 +52,7 @@ def _tp_worker(rank, world, port, fp8, q):
         ar = torch.arange(P, dtype=torch.int32, device=dev)
         lg = m.prefill(toks.int(), ar, ar, torch.tensor([0, P], dtype=torch.int32, device=dev), P,
                        torch.tensor([P - 1], device=dev), cache)
-        q.put((rank, lg[0].float().cpu()))
+        q.put((rank, lg[0].float().cpu().numpy()))
         pdist.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -58,7 +70,7 @@ def test_mixtral_tp2_matches_tp1(gpu, fp8):
     procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, fp8, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in procs)
+    res = _collect(q, procs, 600)
     for p in procs:
         p.join(timeout=120)
     assert all(isinstance(v, torch.Tensor) for v in res.values()), res
@@ -90,7 +102,7 @@ def _ep_worker(rank, world, port, fp8, mode, q):
         dev = torch.device("cuda", 0)
         m = MixtralModel(decoder_config("mixtral-tiny"), device=dev, seed=4, max_position=512, fp8=fp8,
                          ep_rank=rank, ep_size=world, ep_mode=mode, ep_capacity=64 if mode == "padded" else None)
-        q.put((rank, _prefill_logits(m, dev, P=23 + 9 * rank, seed=rank)))  # each rank its own prompt
+        q.put((rank, _prefill_logits(m, dev, P=23 + 9 * rank, seed=rank).float().cpu().numpy()))  # each rank its own prompt
         pdist.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -120,7 +132,7 @@ def test_mixtral_ep2_matches_ep1(gpu, fp8, mode):
     procs = [ctx.Process(target=_ep_worker, args=(r, 2, port, fp8, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in procs)
+    res = _collect(q, procs, 600)
     for p in procs:
         p.join(timeout=120)
     assert all(isinstance(v, torch.Tensor) for v in res.values()), res
@@ -143,7 +155,7 @@ def _enc_worker(rank, world, port, fp8, q):
         dev = torch.device("cuda", 0)
         m = TPLlamaModel(decoder_config("llama-tiny"), device=dev, seed=6, max_position=512, fp8_dense=fp8,
                          tp_rank=rank, tp_size=world)  # no tp_comm: the process group's all-reduce (eager)
-        q.put((rank, _encode(m, dev)))
+        q.put((rank, _encode(m, dev).numpy()))
         pdist.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -171,7 +183,7 @@ def test_dense_tp2_encode_matches_tp1(gpu, fp8):
     procs = [ctx.Process(target=_enc_worker, args=(r, 2, port, fp8, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in procs)
+    res = _collect(q, procs, 600)
     for p in procs:
         p.join(timeout=120)
     assert all(isinstance(v, torch.Tensor) for v in res.values()), res
