@@ -191,7 +191,8 @@ def main():
         a.requests = a.requests or 64
         out = bench_encoder(a)
     else:
-        a.requests = a.requests or 32  # 2048-sequence decode batch: amortises the expert-weight stream
+        a.requests = a.requests or 64  # 4096-sequence decode batch (the headline's): amortises the expert-weight stream
+        # (32 requests: 4.68 answers/s, 64: 5.12 on one MI355X, profiles/moe_round4.md)
         out = bench_moe(a)
     if int(os.environ.get("RANK", "0")) == 0:
         from llm_weighted_consensus_amd import ops

@@ -14,7 +14,7 @@ fi
 [ "${ONLY:-}" = "small" ] && { cat gpurun_out/configs.log; exit 0; }
 rc=0
 if [ "${ONLY:-}" != "tp2" ]; then
-  timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-32} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
+  timeout -k 10 1000 python bench_configs.py moe --requests ${MOE_R:-64} --steps 2 >> gpurun_out/configs.log 2>> gpurun_out/configs_err.log
   rc=$?; echo "config5 rc=$rc"
 fi
 if [ $rc -eq 0 ] && [ -n "${TP2:-}" ]; then
