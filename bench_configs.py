@@ -201,7 +201,7 @@ def main():
         for k, v in gemm_plan.table().items():  # bf16 backend choice per shape (encoder / decoder)
             print(f"# gemm {k}: " + " ".join(f"{b}={t:.1f}us" if b != "choice" else f"choice={t}"
                                              for b, t in v.items()), file=sys.stderr, flush=True)
-        for k, v in sorted(ops.FP8_TIMINGS.items()):  # dense fp8 backend choice per (rows bucket, N, K)
+        for k, v in sorted(ops.FP8_TIMINGS.items(), key=str):  # dense fp8 backend choice per (rows bucket, N, K)
             print(f"# fp8 gemm {k}: " + " ".join(f"{b}={t:.1f}us" for b, t in v.items())
                   + f" choice={ops.FP8_CHOICE.get(k)}", file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)

@@ -421,6 +421,7 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
     TORCH_CHECK(max_slots >= (C.size(0) + 255) / 256, "gemm8g: dense mode needs ceil(rows / 256) slots");
   }
   TORCH_CHECK(A.size(1) == K && C.size(1) == (swiglu ? N / 2 : N), "gemm8g: shape mismatch");
+  TORCH_CHECK(A.size(0) * A.stride(0) < (int64_t(1) << 31), "gemm8g: A spans >= 2 GiB (32-bit buffer range)");
   TORCH_CHECK(!swiglu || N % 64 == 0, "gemm8g: SwiGLU needs whole 64-row gate / up block pairs");
   CHECK_DTYPE(a_scale, at::kFloat); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_CONTIG(w_scale);
   TORCH_CHECK(a_scale.numel() >= A.size(0) && w_scale.numel() == (int64_t)G * N, "gemm8g: scale shapes");

@@ -114,6 +114,9 @@ class LlamaModel:
             for L in self.layers:
                 if isinstance(L, LayerWeights):
                     L.wqkv, L.wo = ops.Fp8Weight(L.wqkv), ops.Fp8Weight(L.wo)
+                    if L.gu_block == 0 and L.w_gate_up.shape[0] % 64 == 0:
+                        # gate|up interleaved in blocks of 32: gemm8g's epilogue applies the SwiGLU
+                        L.w_gate_up, L.gu_block = ops.swiglu_interleave(L.w_gate_up), 32
                     L.w_gate_up, L.w_down = ops.Fp8Weight(L.w_gate_up), ops.Fp8Weight(L.w_down)
             torch.cuda.empty_cache()
         if self.device.type == "cuda":
@@ -257,7 +260,7 @@ class LlamaModel:
         silu_mul), down GEMM.  fp8: gate|up fp8 GEMM, SwiGLU fused with the down projection's row
         quantisation (K11e), down fp8 GEMM."""
         if isinstance(L.w_down, ops.Fp8Weight):
-            aq, as_ = ops.silu_mul_quant_fp8(self._proj(h, L.w_gate_up), block=L.gu_block)
+            aq, as_ = ops.linear_fp8_swiglu(h, L.w_gate_up, L.gu_block)
             return ops.linear_fp8_q(aq, as_, L.w_down)
         return self._proj(self._act(h, L), L.w_down)
 

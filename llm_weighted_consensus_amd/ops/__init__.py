@@ -467,20 +467,31 @@ def _g8g_dense_ok(xq: torch.Tensor, w: "Fp8Weight") -> bool:
     N, K = w.q.shape
     M = xq.shape[0]
     return (xq.is_cuda and xq.stride(1) == 1 and xq.stride(0) % 16 == 0 and K % 128 == 0 and N % 8 == 0
-            and M * xq.stride(0) < (1 << 31) and 256 * K < (1 << 31) and xq.dtype == torch.float8_e4m3fn)
+            and M >= 0 and 256 * K < (1 << 31) and xq.dtype == torch.float8_e4m3fn)
 
 
-def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Optional[torch.Tensor] = None):
+G8G_SPAN = 1 << 31  # bytes of A one gemm8g launch may address (its buffer range is 32-bit)
+
+
+def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Optional[torch.Tensor] = None,
+                 swiglu: bool = False):
     """Dense fp8 GEMM on the hand-written 8-phase core (csrc/kernels/gemm8g.hip, G = 1, no row table):
-    (xq [M, K] e4m3 . w.q^T) * xs[row] * w.s[col] -> bf16 [M, N]."""
+    (xq [M, K] e4m3 . w.q^T) * xs[row] * w.s[col] -> bf16 [M, N]; ``swiglu``: w's rows are gate|up interleaved
+    in blocks of 32 (:func:`swiglu_interleave`) and the epilogue writes silu(gate) * up, bf16 [M, N / 2].
+    The kernel addresses A through a 32-bit buffer range: row blocks of < 2 GiB of A go one launch each
+    (the e5-mistral embedder's prefill is ~0.5 M rows)."""
     M = xq.shape[0]
     N, K = w.q.shape
     if out is None:
-        out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=xq.device)
     if M == 0:
         return out
-    kernels().gemm8g_fp8(xq, w.q.view(1, N, K), out, None, -(-M // 256), None, xs.reshape(-1).contiguous(),
-                         w.s.reshape(-1), False)
+    step = max(256, (G8G_SPAN - 1) // xq.stride(0) // 256 * 256)
+    s, ws, wq = xs.reshape(-1).contiguous(), w.s.reshape(-1), w.q.view(1, N, K)
+    for r0 in range(0, M, step):
+        r1 = min(M, r0 + step)
+        kernels().gemm8g_fp8(xq[r0:r1], wq, out[r0:r1], None, -(-(r1 - r0) // 256), None, s[r0:r1], ws,
+                             bool(swiglu))
     return out
 
 
@@ -510,6 +521,41 @@ def linear_fp8_q(xq: torch.Tensor, xs: torch.Tensor, w: Fp8Weight) -> torch.Tens
             FP8_TIMINGS[key] = {"g8g": t_own, "blas": t_blas}
             c = FP8_CHOICE[key] = "g8g" if t_own <= t_blas * (1 + FP8_OWN_MARGIN) else "blas"
     return gemm8g_dense(xq, xs, w) if c == "g8g" else _fp8_blas(xq, xs, w)
+
+
+def linear_fp8_swiglu(x, w: Fp8Weight, block: int):
+    """fp8 gate|up projection + SwiGLU + per-row e4m3 quantisation of the activation (the dense fp8 MLP's
+    middle, config 5's e5-mistral embedder): x (bf16 [M, d] or a :class:`QAct`) -> (q [M, F] e4m3,
+    scale [M] f32) for the down projection.  Two pipelines, timed per (row bucket, N, K) like
+    :func:`linear_fp8_q`: gemm8g with SwiGLU in its epilogue then one quantisation pass over [M, F] (needs
+    ``block`` == 32, the interleave the epilogue reads), or hipBLASLt's fp8 GEMM writing [M, 2F] bf16 then
+    the fused silu_mul_quant_fp8 pass — the first never writes the [M, 2F] intermediate."""
+    xq, xs = (x.q, x.s) if isinstance(x, QAct) else quant_fp8_rows(x)
+
+    def own():
+        return quant_fp8_rows(gemm8g_dense(xq, xs, w, swiglu=True))
+
+    def lib():
+        return silu_mul_quant_fp8(_fp8_blas(xq, xs, w), block)
+
+    N, K = w.q.shape
+    if block != 32 or N % 64 or not _g8g_dense_ok(xq, w) or FP8_GEMM == "blas":
+        return silu_mul_quant_fp8(linear_fp8_q(xq, xs, w), block)
+    if FP8_GEMM == "g8g":
+        return own()
+    key = ("swiglu", _fp8_bucket(xq.shape[0]), N, K)
+    c = FP8_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            c = "g8g" if xq.shape[0] >= 256 else "blas"
+        else:
+            from .gemm_plan import _time
+
+            t_own = _time(own, iters=3, rounds=3)
+            t_blas = _time(lib, iters=3, rounds=3)
+            FP8_TIMINGS[key] = {"g8g": t_own, "blas": t_blas}
+            c = FP8_CHOICE[key] = "g8g" if t_own <= t_blas * (1 + FP8_OWN_MARGIN) else "blas"
+    return own() if c == "g8g" else lib()
 
 
 def linear_fp8(x, w: Fp8Weight) -> torch.Tensor:

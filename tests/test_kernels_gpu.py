@@ -950,6 +950,51 @@ def test_dense_fp8_gemm8g(gpu, M, N, K, monkeypatch):
     assert len(ops.FP8_CHOICE) == 1
 
 
+def test_dense_fp8_gemm8g_row_blocks(gpu, monkeypatch):
+    """A beyond gemm8g's 32-bit buffer range goes as row blocks, one launch each (the embedder's ~0.5 M-row
+    prefill): with the span shrunk to force five blocks (the last one ragged) the result is unchanged."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(6)
+    M, N, K = 1200, 512, 256
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = ops.Fp8Weight(torch.randn(N, K, device=gpu).to(torch.bfloat16) * 0.05)
+    xq, xs = ops.quant_fp8_rows(x)
+    whole = ops.gemm8g_dense(xq, xs, w)
+    monkeypatch.setattr(ops, "G8G_SPAN", 256 * K + 1)
+    blocks = ops.gemm8g_dense(xq, xs, w)
+    assert torch.equal(whole, blocks)
+    ref_ = (xq.float() * xs[:, None]) @ (w.q.float() * w.s.view(-1, 1)).t()
+    _close(blocks, ref_, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (4096, 2048, 1024)])
+@pytest.mark.parametrize("backend", ["g8g", "blas", "auto"])
+def test_dense_fp8_swiglu(gpu, M, N, K, backend, monkeypatch):
+    """The dense fp8 MLP middle (ops.linear_fp8_swiglu): gate|up rows interleaved in blocks of 32, fp8 GEMM,
+    SwiGLU (gemm8g's epilogue, or hipBLASLt + the fused silu_mul_quant pass), per-row e4m3 quantisation —
+    the dequantised activation vs fp32 silu(gate) * up of the dequantised operands."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(7)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    wgu = torch.randn(N, K, device=gpu).to(torch.bfloat16) * 0.05
+    w = ops.Fp8Weight(ops.swiglu_interleave(wgu))
+    monkeypatch.setattr(ops, "FP8_GEMM", backend)
+    monkeypatch.setattr(ops, "FP8_CHOICE", {})
+    aq, as_ = ops.linear_fp8_swiglu(x, w, 32)
+    assert aq.shape == (M, N // 2) and aq.dtype == torch.float8_e4m3fn and as_.shape == (M,)
+    xq, xs = ops.quant_fp8_rows(x)
+    gu = ((xq.float() * xs[:, None]) @ (w.q.float() * w.s.view(-1, 1)).t()).view(M, -1, 2, 32)
+    g, u = gu[:, :, 0].reshape(M, -1), gu[:, :, 1].reshape(M, -1)
+    ref_ = torch.nn.functional.silu(g) * u
+    got = aq.float() * as_[:, None]
+    rel = (got - ref_).norm() / ref_.norm()
+    assert rel < 4e-2, rel  # e4m3 rounding of the activation (~2^-4 relative per element)
+    if backend == "auto":
+        assert len(ops.FP8_CHOICE) == 1
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (4096, 3072, 1024), (300, 4096, 1024)])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
