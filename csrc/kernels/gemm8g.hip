@@ -47,6 +47,7 @@ struct Params {
   int rows_a;             // rows of A (DMA bounds)
   int slots, n_tiles;     // m-tile slots per n-tile, n-tiles
   int rows_c;             // output rows when row_off is null (dense: G = 1)
+  int gn;                 // grouped: n-tiles an XCD walks per m-slot before the next slot (>= 1)
 };
 
 LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c) {
@@ -54,6 +55,11 @@ LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, c
   const v8i32 bv = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 0, 0, 0, 127, 0, 127);
 }
+
+// grouped default: an XCD takes all of its n-tiles for one m-slot before the next slot (gn = n-tiles per XCD).
+// Config 5's routed shapes, one MI355X (scripts/g8g_order_ab.py): gate|up + SwiGLU at 4096 tokens 921 -> 895 us,
+// down 468 -> 452 us vs gn = 1 (the n-tile-major order); gn = 4 was slower at gate|up.  LWC_G8G_GN overrides.
+constexpr int kDefaultGn = 1 << 20;
 
 LWC_DEVICE float silu8(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
@@ -78,8 +84,13 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     m_end = p.rows_c;
     ntile = in / gsz;
   } else {
-    ntile = (local / p.slots) * 8 + xcd;
-    int slot = local % p.slots;
+    // an XCD owns n-tiles xcd, xcd + 8, ...; it walks them in windows of gn: every m-slot (the experts'
+    // row tiles back to back) takes the window's gn n-tiles in a row, so the workgroups resident at once
+    // hold ~32/gn consecutive row tiles x gn weight panels (each expert's panel still read once, every A
+    // tile once per window instead of once per n-tile)
+    const int w = p.slots * p.gn, in = local % w;
+    ntile = ((local / w) * p.gn + in % p.gn) * 8 + xcd;
+    int slot = in / p.gn;
     if (ntile >= p.n_tiles) return;  // uniform
     for (; g < p.G; ++g) {
       const int r0 = p.row_off[g], r1 = p.row_off[g + 1];
@@ -300,10 +311,13 @@ extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* 
     attr = true;
   }
   const int n_tiles = (N + 255) / 256;
+  const char* gv = getenv("LWC_G8G_GN");
+  const int nj = (n_tiles + 7) / 8, gn = std::max(1, std::min(gv ? atoi(gv) : kDefaultGn, nj));
   Params p{(const uint8_t*)A, (const uint8_t*)W, (lwc::bf16_t*)C, row_off, a_rows, a_scale, w_scale,
-           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c};
-  // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: n-tile rounds of 8 x max_slots m-slots
-  const unsigned grid = row_off ? (unsigned)(((n_tiles + 7) / 8) * max_slots * 8)
+           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c, gn};
+  // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: per XCD, windows of gn n-tiles x
+  // max_slots m-slots
+  const unsigned grid = row_off ? (unsigned)(((nj + gn - 1) / gn) * gn * max_slots * 8)
                                 : (unsigned)(8 * ((n_tiles * max_slots + 7) / 8));
   if (swiglu)
     gemm8g_kernel<true><<<grid, 512, kLdsB, s>>>(p);
