@@ -48,6 +48,7 @@ struct Params {
   int slots, n_tiles;     // m-tile slots per n-tile, n-tiles
   int rows_c;             // output rows when row_off is null (dense: G = 1)
   int gn;                 // grouped: n-tiles an XCD walks per m-slot before the next slot (>= 1)
+  int skip_empty;         // skip the MFMAs of empty 64-row blocks (LWC_G8G_SKIP=0: A/B off)
 };
 
 LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c) {
@@ -57,8 +58,9 @@ LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, c
 }
 
 // grouped default: an XCD takes all of its n-tiles for one m-slot before the next slot (gn = n-tiles per XCD).
-// Config 5's routed shapes, one MI355X (scripts/g8g_order_ab.py): gate|up + SwiGLU at 4096 tokens 921 -> 895 us,
-// down 468 -> 452 us vs gn = 1 (the n-tile-major order); gn = 4 was slower at gate|up.  LWC_G8G_GN overrides.
+// Config 5's routed shapes at 4096 tokens, one MI355X, medians of 5 interleaved rounds (scripts/g8g_order_ab.py):
+// gate|up + SwiGLU 908.1 -> 893.4 us, down 474.3 -> 466.7 us vs gn = 1 (the n-tile-major order); with the
+// empty-block MFMA skip below as well 878.0 / 443.9 us.  LWC_G8G_GN overrides.
 constexpr int kDefaultGn = 1 << 20;
 
 LWC_DEVICE float silu8(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
@@ -172,11 +174,15 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   };
 
 #define G8_BAR() __builtin_amdgcn_s_barrier()
+  // rows of this wave row that hold data (wave-uniform): a ragged last tile of an expert (on average half of
+  // it) skips the MFMAs of its empty 64-row blocks — the barriers, LDS reads and DMA stay, so the two wave
+  // rows keep their schedule
+  const int live = p.skip_empty ? __builtin_amdgcn_readfirstlane(m_end - m_begin - wr * 128) : 256;
 #define G8_MFMA(i0, j0, bb)                          \
   G8_BAR();                                          \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
   __builtin_amdgcn_s_setprio(1);                     \
-  mma(i0, j0, bb);                                   \
+  if ((i0) * 16 < live) mma(i0, j0, bb);             \
   __builtin_amdgcn_s_setprio(0);                     \
   G8_BAR()
 #define G8_STAGE(U, R) stage(U, smem + ((R) & 1) * kBufB, (R))
@@ -314,7 +320,8 @@ extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* 
   const char* gv = getenv("LWC_G8G_GN");
   const int nj = (n_tiles + 7) / 8, gn = std::max(1, std::min(gv ? atoi(gv) : kDefaultGn, nj));
   Params p{(const uint8_t*)A, (const uint8_t*)W, (lwc::bf16_t*)C, row_off, a_rows, a_scale, w_scale,
-           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c, gn};
+           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c, gn, 1};
+  if (const char* sv = getenv("LWC_G8G_SKIP")) p.skip_empty = atoi(sv);
   // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: per XCD, windows of gn n-tiles x
   // max_slots m-slots
   const unsigned grid = row_off ? (unsigned)(((nj + gn - 1) / gn) * gn * max_slots * 8)

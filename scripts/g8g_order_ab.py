@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of gemm8g's grouped tile order (LWC_G8G_GN: n-tiles an XCD walks per m-slot) at config 5's routed
+"""A/B of gemm8g's grouped tile order (LWC_G8G_GN: n-tiles an XCD walks per m-slot) and of skipping the
+MFMAs of empty 64-row blocks in ragged tiles (LWC_G8G_SKIP) at config 5's routed
 expert shapes (Mixtral-8x7B, top-2 of 8, random routing): gate|up with the SwiGLU epilogue (N = 2F = 28672,
-K = 4096) and down (N = 4096, K = 14336).  Interleaved rounds, median of 3; outputs must be bitwise equal
+K = 4096) and down (N = 4096, K = 14336).  Interleaved rounds, median of 5; outputs must be bitwise equal
 across orders (the order moves work between workgroups, not the arithmetic)."""
 import os
 import sys
@@ -12,7 +13,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from moe_swiglu_ab import timeit  # noqa: E402
 
-GNS = (1, 2, 4, 7)
+ARMS = (("gn1,noskip", {"LWC_G8G_GN": "1", "LWC_G8G_SKIP": "0"}), ("gn1+skip", {"LWC_G8G_GN": "1", "LWC_G8G_SKIP": "1"}),
+        ("slot-major,noskip", {"LWC_G8G_GN": "64", "LWC_G8G_SKIP": "0"}),
+        ("slot-major+skip", {"LWC_G8G_GN": "64", "LWC_G8G_SKIP": "1"}))
+ROUNDS = 5
 
 
 def main():
@@ -43,16 +47,16 @@ def main():
             return ops.grouped_gemm(aq, q2, row_off, rows=rows, a_scale=as_, w_scale=s2)
 
         for name, fn, flop in (("gate|up+SwiGLU", gate_up, 2 * rows * 2 * f * d), ("down", down, 2 * rows * d * f)):
-            res = {gn: [] for gn in GNS}
+            res = {arm: [] for arm, _ in ARMS}
             outs = {}
-            for _ in range(3):
-                for gn in GNS:
-                    os.environ["LWC_G8G_GN"] = str(gn)
-                    res[gn].append(timeit(fn))
-                    outs[gn] = fn()
-            ref = outs[GNS[0]]
-            line = " ".join(f"gn={gn}: {sorted(v)[1]:7.1f} us ({flop / sorted(v)[1] / 1e6:5.0f} TF/s)"
-                            for gn, v in res.items())
+            for _ in range(ROUNDS):
+                for arm, env in ARMS:
+                    os.environ.update(env)
+                    res[arm].append(timeit(fn))
+                    outs[arm] = fn()
+            ref = outs[ARMS[0][0]]
+            line = " ".join(f"{arm}: {sorted(v)[len(v) // 2]:7.1f} us ({flop / sorted(v)[len(v) // 2] / 1e6:5.0f} TF/s)"
+                            for arm, v in res.items())
             same = all(torch.equal(ref, o) for o in outs.values())
             print(f"T={T:5d} {name:15s} {line}  bitwise-equal={same}", flush=True)
             if not same:
