@@ -28,7 +28,7 @@ int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, 
 int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
-                   int, int, int, int, int, int, hipStream_t);
+                   int, int, int, int, int, int, const void*, void*, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
@@ -403,13 +403,22 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
 }
 
 void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& row_off,
-                int64_t max_slots, const c10::optional<at::Tensor>& a_rows, const at::Tensor& a_scale,
-                const at::Tensor& w_scale, bool swiglu) {
+                int64_t max_slots, const c10::optional<at::Tensor>& a_rows, const c10::optional<at::Tensor>& a_scale,
+                const at::Tensor& w_scale, int64_t mode, const c10::optional<at::Tensor>& a_mx,
+                const c10::optional<at::Tensor>& mx_out) {
   // grouped fp8 GEMM on the 8-phase schedule (gemm8g.hip): A [rows_a, K] e4m3, W [G, N, K] e4m3, C [rows, N] bf16;
-  // row_off None: the dense projection (G = 1, every output row)
-  CHECK_GPU(A); CHECK_GPU(W); CHECK_BF16(C); CHECK_CONTIG(W);
+  // row_off None: the dense projection (G = 1, every output row).  mode 1: SwiGLU epilogue, C [rows, N / 2] bf16;
+  // mode 2: SwiGLU epilogue with MX output, C [rows, N / 2] e4m3 + mx_out [N / 256, rows, 4] e8m0 (uint8);
+  // a_mx [K / 128, rows_a, 4] e8m0: A's MX block scales (mode 0, no a_rows; a_scale unused)
+  CHECK_GPU(A); CHECK_GPU(W); CHECK_CONTIG(W);
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm8g: mode 0, 1 or 2");
   TORCH_CHECK(A.scalar_type() == at::kFloat8_e4m3fn && W.scalar_type() == at::kFloat8_e4m3fn, "gemm8g: e4m3 A and W");
   TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && C.dim() == 2 && C.stride(1) == 1 && W.dim() == 3, "gemm8g: layouts");
+  if (mode == 2) {
+    TORCH_CHECK(C.scalar_type() == at::kFloat8_e4m3fn, "gemm8g: MX output is e4m3");
+  } else {
+    CHECK_BF16(C);
+  }
   const int G = (int)W.size(0), N = (int)W.size(1), K = (int)W.size(2);
   const int* ro = nullptr;
   if (row_off.has_value() && row_off->defined()) {
@@ -420,11 +429,19 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
     TORCH_CHECK(G == 1, "gemm8g: dense mode (no row_off) takes one weight");
     TORCH_CHECK(max_slots >= (C.size(0) + 255) / 256, "gemm8g: dense mode needs ceil(rows / 256) slots");
   }
-  TORCH_CHECK(A.size(1) == K && C.size(1) == (swiglu ? N / 2 : N), "gemm8g: shape mismatch");
+  TORCH_CHECK(A.size(1) == K && C.size(1) == (mode ? N / 2 : N), "gemm8g: shape mismatch");
   TORCH_CHECK(A.size(0) * A.stride(0) < (int64_t(1) << 31), "gemm8g: A spans >= 2 GiB (32-bit buffer range)");
-  TORCH_CHECK(!swiglu || N % 64 == 0, "gemm8g: SwiGLU needs whole 64-row gate / up block pairs");
-  CHECK_DTYPE(a_scale, at::kFloat); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_CONTIG(w_scale);
-  TORCH_CHECK(a_scale.numel() >= A.size(0) && w_scale.numel() == (int64_t)G * N, "gemm8g: scale shapes");
+  TORCH_CHECK(!mode || N % 64 == 0, "gemm8g: SwiGLU needs whole 64-row gate / up block pairs");
+  CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(w_scale);
+  TORCH_CHECK(w_scale.numel() == (int64_t)G * N, "gemm8g: w_scale shape");
+  const bool mxa = a_mx.has_value() && a_mx->defined();
+  const float* as = nullptr;
+  if (!mxa) {
+    TORCH_CHECK(a_scale.has_value() && a_scale->defined(), "gemm8g: a_scale or a_mx required");
+    CHECK_DTYPE(*a_scale, at::kFloat); CHECK_CONTIG(*a_scale);
+    TORCH_CHECK(a_scale->numel() >= A.size(0), "gemm8g: a_scale shape");
+    as = a_scale->data_ptr<float>();
+  }
   const int* ar = nullptr;
   if (a_rows.has_value() && a_rows->defined()) {
     CHECK_DTYPE(*a_rows, at::kInt); CHECK_CONTIG(*a_rows);
@@ -433,9 +450,29 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
   } else {
     TORCH_CHECK(C.size(0) <= A.size(0), "gemm8g: more output rows than A rows");
   }
-  CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), ro, ar, a_scale.data_ptr<float>(),
-                          w_scale.data_ptr<float>(), G, (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0),
-                          (int)A.size(0), (int)C.size(0), swiglu ? 1 : 0, cur_stream()),
+  int s_rows = 0;
+  const void* amx = nullptr;
+  void* mxo = nullptr;
+  if (mxa) {
+    TORCH_CHECK(mode == 0 && ar == nullptr, "gemm8g: MX A takes the plain epilogue and contiguous rows");
+    CHECK_GPU(*a_mx); CHECK_CONTIG(*a_mx); CHECK_DTYPE(*a_mx, at::kByte);
+    TORCH_CHECK(a_mx->dim() == 3 && a_mx->size(0) == K / 128 && a_mx->size(1) >= A.size(0) && a_mx->size(2) == 4,
+                "gemm8g: a_mx must be [K / 128, rows_a, 4]");
+    s_rows = (int)a_mx->size(1);
+    amx = a_mx->data_ptr();
+  }
+  if (mode == 2) {
+    TORCH_CHECK(mx_out.has_value() && mx_out->defined(), "gemm8g: mode 2 writes mx_out");
+    CHECK_GPU(*mx_out); CHECK_CONTIG(*mx_out); CHECK_DTYPE(*mx_out, at::kByte);
+    TORCH_CHECK(N % 256 == 0 && mx_out->dim() == 3 && mx_out->size(0) == N / 256 && mx_out->size(1) >= C.size(0) &&
+                    mx_out->size(2) == 4 && C.stride(0) % 16 == 0,
+                "gemm8g: mx_out must be [N / 256, rows, 4] (N % 256 == 0)");
+    s_rows = (int)mx_out->size(1);
+    mxo = mx_out->data_ptr();
+  }
+  CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), ro, ar, as, w_scale.data_ptr<float>(), G,
+                          (int)max_slots, N, K, (int)A.stride(0), (int)C.stride(0), (int)A.size(0), (int)C.size(0),
+                          (int)mode, amx, mxo, s_rows, cur_stream()),
            "gemm8g_fp8");
 }
 

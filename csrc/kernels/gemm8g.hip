@@ -49,7 +49,41 @@ struct Params {
   int rows_c;             // output rows when row_off is null (dense: G = 1)
   int gn;                 // grouped: n-tiles an XCD walks per m-slot before the next slot (>= 1)
   int skip_empty;         // skip the MFMAs of empty 64-row blocks (LWC_G8G_SKIP=0: A/B off)
+  // MX activations (kMxOut producer / kMxA consumer): e8m0 block scales [K / 128][s_rows][4] bytes, block b
+  // of a 128-byte K slice = its 16-byte chunks b and b + 4 (the chunk pair one MFMA lane holds)
+  const uint8_t* a_mx;    // kMxA: scales of A (a_scale unused)
+  uint8_t* mx_out;        // kMxOut: scales of the e4m3 output (C is then e4m3 [rows, ldc bytes])
+  int s_rows;             // rows of the scale planes
 };
+
+// kernel modes: output / A operand handling
+constexpr int kPlain = 0;   // bf16 out, A per-row scaled
+constexpr int kSwiglu = 1;  // SwiGLU epilogue, bf16 out
+constexpr int kMxOut = 2;   // SwiGLU epilogue, e4m3 out with MX block scales (feeds a kMxA GEMM)
+constexpr int kMxA = 3;     // bf16 out, A carries MX block scales
+constexpr int kMxLds = 2048;  // kMxA: the two K buffers' scale tiles (256 rows x 4 blocks each)
+
+// A block-scaled: the lane's e8m0 scale is byte OP of sa (its row's scale for the lane's K block)
+template <int OP>
+LWC_DEVICE float4v mfma8s(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c,
+                          int sa) {
+  const v8i32 av = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+  const v8i32 bv = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 0, 0, OP, sa, 0, 127);
+}
+
+// max over the lane pairs (0,1) (2,3) of every quad
+LWC_DEVICE float pair_max(float x) {
+  return fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false)));
+}
+
+// e8m0 exponent of a block with max |x| = amax: the smallest e with amax * 2^-e <= 448 (e4m3's largest finite),
+// from amax's own exponent and mantissa (448 = 0.875 * 2^9), so no rounding can push a value past 448
+LWC_DEVICE int mx_exp(float amax) {
+  const int ea = __builtin_amdgcn_frexp_expf(amax);
+  const float m = __builtin_amdgcn_frexp_mantf(amax);
+  return min(127, max(-127, ea - 9 + (m > 0.875f ? 1 : 0)));
+}
 
 LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c) {
   const v8i32 av = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
@@ -68,8 +102,10 @@ LWC_DEVICE float silu8(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(
 // SWIGLU: W's rows are gate / up interleaved in blocks of 32 (ops.swiglu_interleave per expert), so each
 // wave's 64 columns are one gate block and its up block; the epilogue applies the scales, then
 // silu(gate) * up, and writes [rows, N / 2] bf16 — the [rows, N] gate|up intermediate never reaches HBM.
-template <bool SWIGLU>
+template <int MODE>
 __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
+  constexpr bool SWIGLU = MODE == kSwiglu || MODE == kMxOut;
+  constexpr bool MXA = MODE == kMxA;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // ---- work item: XCD-grouped (n-tile, m-slot), then (group, m-tile) of the slot ----
   const int id = blockIdx.x, xcd = id & 7, local = id >> 3;
@@ -133,6 +169,19 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   const int sw = (r16 >> 1) & 7;
   const int off0 = r16 * 128 + ((q ^ sw) << 4), off1 = r16 * 128 + (((4 + q) ^ sw) << 4);
 
+  // kMxA: the tile's scales, DMA'd with unit A0 as two 1-byte pieces per thread into [block][wave row][row
+  // within a 16-row fragment][fragment] order, so a lane reads its 8 fragments' scales as one 8-byte word
+  uint32_t voS[2] = {0u, 0u};
+  if constexpr (MXA) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pos = j * 512 + tid, fi = pos & 7, fr = (pos >> 3) & 15, fw = (pos >> 7) & 1, fb = pos >> 8;
+      int r = m_begin + fw * 128 + fi * 16 + fr;
+      if (r >= m_end) r = m_begin;
+      voS[j] = (uint32_t)(r * 4 + fb);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rS = uniform_rsrc(p.a_mx, MXA ? (p.K / 128) * p.s_rows * 4 : 0);
   const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(p.A, p.rows_a * p.lda);
   const __amdgpu_buffer_rsrc_t rW = uniform_rsrc(p.W + ((size_t)g * p.N + n0) * p.K, min(p.N - n0, 256) * p.K);
   auto stage = [&](int u, uint8_t* buf, int kt) {
@@ -143,6 +192,15 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voA[u][i], kt * 128, 0, 0);
       else
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, dst, 16, voW[u - 2][i], kt * 128, 0, 0);
+    }
+    if constexpr (MXA) {
+      if (u == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          auto* dst = (__attribute__((address_space(3))) void*)(smem + kLdsB + (kt & 1) * 1024 + j * 512 + wid * 64);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, dst, 1, voS[j], kt * p.s_rows * 4, 0, 0);
+        }
+      }
     }
   };
   auto rd = [&](const uint8_t* u, int row0, uint4v& f0, uint4v& f1) {
@@ -157,12 +215,24 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     for (int jj = 0; jj < 4; ++jj) acc[i][jj] = float4v{0.f, 0.f, 0.f, 0.f};
 
   uint4v a[4][2], b0[2][2], b1[2][2];
+  uint2 sc = {0u, 0u};  // kMxA: this K tile's scales of the lane's 8 row fragments (block q)
   auto mma = [&](int i0, int j0, const uint4v (&bb)[2][2]) {
+    if constexpr (MXA) {
+      const int sa = (int)(i0 == 0 ? sc.x : sc.y);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int jj = 0; jj < 2; ++jj) {
+        acc[i0 + 0][j0 + jj] = mfma8s<0>(a[0][0], a[0][1], bb[jj][0], bb[jj][1], acc[i0 + 0][j0 + jj], sa);
+        acc[i0 + 1][j0 + jj] = mfma8s<1>(a[1][0], a[1][1], bb[jj][0], bb[jj][1], acc[i0 + 1][j0 + jj], sa);
+        acc[i0 + 2][j0 + jj] = mfma8s<2>(a[2][0], a[2][1], bb[jj][0], bb[jj][1], acc[i0 + 2][j0 + jj], sa);
+        acc[i0 + 3][j0 + jj] = mfma8s<3>(a[3][0], a[3][1], bb[jj][0], bb[jj][1], acc[i0 + 3][j0 + jj], sa);
+      }
+    } else {
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-        acc[i0 + i][j0 + jj] = mfma8(a[i][0], a[i][1], bb[jj][0], bb[jj][1], acc[i0 + i][j0 + jj]);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[i0 + i][j0 + jj] = mfma8(a[i][0], a[i][1], bb[jj][0], bb[jj][1], acc[i0 + i][j0 + jj]);
+    }
   };
   auto rdA = [&](const uint8_t* buf, int u) {
 #pragma unroll
@@ -187,12 +257,18 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   G8_BAR()
 #define G8_STAGE(U, R) stage(U, smem + ((R) & 1) * kBufB, (R))
 #define G8_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+  // kMxA stages 2 more pieces with unit A0: the waits after A0 / B0 of the next tile leave 6 in flight, not 4
+#define G8_VMX() \
+  if constexpr (MXA) G8_VM(6); \
+  else G8_VM(4)
 #define G8_TILE(R, ST1, ST2, ST3, ST4, W1, W2, W4) \
   {                                                \
     uint8_t* cb = smem + ((R) & 1) * kBufB;        \
     rdB(cb, kUB0, b0);                             \
     __builtin_amdgcn_sched_barrier(0);             \
     rdA(cb, kUA0);                                 \
+    if constexpr (MXA)                             \
+      sc = *reinterpret_cast<const uint2*>(smem + kLdsB + ((R) & 1) * 1024 + ((q * 2 + wr) * 16 + r16) * 8); \
     ST1;                                           \
     W1;                                            \
     G8_MFMA(0, 0, b0);                             \
@@ -214,10 +290,11 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   if (wr == 1) G8_BAR();  // stagger the two wave rows by one barrier
   int r = 0;
   for (; r < KT - 1; ++r)
-    G8_TILE(r, G8_STAGE(0, r + 1), G8_STAGE(2, r + 1), G8_STAGE(3, r + 1), G8_STAGE(1, r + 1), G8_VM(4), G8_VM(4),
+    G8_TILE(r, G8_STAGE(0, r + 1), G8_STAGE(2, r + 1), G8_STAGE(3, r + 1), G8_STAGE(1, r + 1), G8_VMX(), G8_VMX(),
             G8_VM(4))
   G8_TILE(r, , , , , G8_VM(2), G8_VM(0), )
 #undef G8_TILE
+#undef G8_VMX
 #undef G8_VM
 #undef G8_STAGE
   if (wr == 0) G8_BAR();  // re-align the wave rows
@@ -240,7 +317,7 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     for (int rr = 0; rr < 4; ++rr) {
       int row = m_begin + wr * 128 + i * 16 + 4 * q + rr;
       if (row >= m_end) row = m_begin;
-      const float as = p.a_scale[p.a_rows ? p.a_rows[row] : row];
+      const float as = MXA ? 1.f : p.a_scale[p.a_rows ? p.a_rows[row] : row];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) acc[i][jj][rr] *= as * ws[jj];
       __builtin_amdgcn_sched_barrier(0);  // one scale load in flight at a time: no 32-load VGPR burst
@@ -260,14 +337,55 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
         }
     __syncthreads();
     const int cch = lane % 4, nout = p.N / 2;
+    if constexpr (MODE == kMxOut) {
+      // e4m3 rows with one e8m0 scale per (row, MX block): block b of the workgroup's 128 outputs (= one K
+      // slice of the down GEMM) is the 16-column chunks b and b + 4, held by waves b / 2 and 2 + b / 2 — the
+      // chunk maxima meet in LDS
+      float* amx = reinterpret_cast<float*>(smem + 65536);  // [wave row][128 rows][8 chunks]
+      const int c16 = 2 * wc + (cch >> 1);
 #pragma unroll 4
-    for (int k = 0; k < 8; ++k) {
-      const int row = lane / 4 + 16 * k;
-      const int gm = m_begin + wr * 128 + row;
-      const int gn = n0 / 2 + wc * 32 + cch * 8;
-      if (gm < m_end && gn < nout)
-        *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
-            *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3)));
+      for (int k = 0; k < 8; ++k) {
+        const int row = lane / 4 + 16 * k;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3))), v);
+        float m = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+        m = pair_max(m);
+        if ((cch & 1) == 0) amx[(wr * 128 + row) * 8 + c16] = m;
+      }
+      __syncthreads();
+      uint8_t* q8 = reinterpret_cast<uint8_t*>(p.C);
+#pragma unroll 4
+      for (int k = 0; k < 8; ++k) {
+        const int row = lane / 4 + 16 * k;
+        const int gm = m_begin + wr * 128 + row;
+        const int gn = n0 / 2 + wc * 32 + cch * 8;
+        const float* ar = amx + (wr * 128 + row) * 8;
+        const int e = mx_exp(fmaxf(ar[c16], ar[(c16 + 4) & 7]));
+        const float inv = __builtin_amdgcn_ldexpf(1.f, -e);
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3))), v);
+        uint32_t lo = 0, hi = 0;
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, hi, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+        if (gm < m_end && gn < nout) {
+          *reinterpret_cast<uint2*>(q8 + (size_t)gm * p.ldc + gn) = uint2{lo, hi};
+          if (c16 < 4 && (cch & 1) == 0) p.mx_out[((size_t)(n0 / 256) * p.s_rows + gm) * 4 + c16] = (uint8_t)(e + 127);
+        }
+      }
+    } else {
+#pragma unroll 4
+      for (int k = 0; k < 8; ++k) {
+        const int row = lane / 4 + 16 * k;
+        const int gm = m_begin + wr * 128 + row;
+        const int gn = n0 / 2 + wc * 32 + cch * 8;
+        if (gm < m_end && gn < nout)
+          *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) =
+              *reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3)));
+      }
     }
   } else {
     constexpr int CW = 64;
@@ -301,34 +419,49 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
 // Grouped fp8 GEMM on the 8-phase schedule.  Requires K % 128 == 0, N % 8 == 0, lda / ldc % 16 == 0 (bytes
 // / elements: 16-byte rows), rows_a * lda < 2^31 and 256 * K < 2^31 (32-bit buffer offsets); max_slots >=
 // sum_g ceil(M_g / 256) (ceil(rows / 256) + G always is).  row_off == null: dense, G = 1, rows [0, rows_c).
+// mode: 0 plain, 1 SwiGLU epilogue (bf16 out), 2 SwiGLU epilogue with e4m3 + MX block-scale output (C is
+// e4m3 [rows_c, ldc bytes], mx_out [N / 256][s_rows][4]); a_mx != null: A carries MX block scales
+// [K / 128][s_rows][4] (mode 0 only; a_scale unused).
 extern "C" int lwc_gemm8g_fp8(const void* A, const void* W, void* C, const int* row_off, const int* a_rows,
                               const float* a_scale, const float* w_scale, int G, int max_slots, int N, int K, int lda,
-                              int ldc, int rows_a, int rows_c, int swiglu, hipStream_t s) {
+                              int ldc, int rows_a, int rows_c, int mode, const void* a_mx, void* mx_out, int s_rows,
+                              hipStream_t s) {
   using namespace lwc::g8g;
   if (K % 128 != 0 || K < 128 || N % 8 != 0 || lda % 16 != 0 || ldc % 8 != 0 || G < 1) return -1;
   if ((long long)rows_a * lda >= (1LL << 31) || 256LL * K >= (1LL << 31)) return -1;
-  if (!a_scale || !w_scale) return -2;
+  const int swiglu = mode == 1 || mode == 2;
+  if (mode < 0 || mode > 2 || !w_scale || (!a_scale && !a_mx)) return -2;
   if (swiglu && N % 64 != 0) return -1;  // whole gate / up block pairs per wave
+  if (mode == 2 && (N % 256 != 0 || !mx_out || s_rows < rows_c || ldc % 16 != 0)) return -1;
+  if (a_mx && (mode != 0 || a_rows || s_rows < rows_a || (long long)(K / 128) * s_rows * 4 >= (1LL << 31))) return -1;
   if (max_slots <= 0) return 0;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
-    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<kPlain>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<kSwiglu>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<kMxOut>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    (void)hipFuncSetAttribute((const void*)gemm8g_kernel<kMxA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsB + kMxLds);
     attr = true;
   }
   const int n_tiles = (N + 255) / 256;
   const char* gv = getenv("LWC_G8G_GN");
   const int nj = (n_tiles + 7) / 8, gn = std::max(1, std::min(gv ? atoi(gv) : kDefaultGn, nj));
   Params p{(const uint8_t*)A, (const uint8_t*)W, (lwc::bf16_t*)C, row_off, a_rows, a_scale, w_scale,
-           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c, gn, 1};
+           G, N, K, lda, ldc, rows_a, max_slots, n_tiles, rows_c, gn, 1,
+           (const uint8_t*)a_mx, (uint8_t*)mx_out, s_rows};
   if (const char* sv = getenv("LWC_G8G_SKIP")) p.skip_empty = atoi(sv);
   // dense: 8 XCD ranges of ceil(tiles / 8) grouped tiles; grouped: per XCD, windows of gn n-tiles x
   // max_slots m-slots
   const unsigned grid = row_off ? (unsigned)(((nj + gn - 1) / gn) * gn * max_slots * 8)
                                 : (unsigned)(8 * ((n_tiles * max_slots + 7) / 8));
-  if (swiglu)
-    gemm8g_kernel<true><<<grid, 512, kLdsB, s>>>(p);
+  if (a_mx)
+    gemm8g_kernel<kMxA><<<grid, 512, kLdsB + kMxLds, s>>>(p);
+  else if (mode == 2)
+    gemm8g_kernel<kMxOut><<<grid, 512, kLdsB, s>>>(p);
+  else if (mode == 1)
+    gemm8g_kernel<kSwiglu><<<grid, 512, kLdsB, s>>>(p);
   else
-    gemm8g_kernel<false><<<grid, 512, kLdsB, s>>>(p);
+    gemm8g_kernel<kPlain><<<grid, 512, kLdsB, s>>>(p);
   return (int)hipGetLastError();
 }

@@ -220,6 +220,11 @@ class MixtralModel(LlamaModel):
                  rows: Optional[int] = None) -> torch.Tensor:
         """Grouped expert FFN over expert-major rows (optionally gathered through ``a_rows``)."""
         if self.fp8:
+            n = rows if rows is not None else (a_rows.numel() if a_rows is not None else x.shape[0])
+            if L.gu_block == 32 and ops.moe_mx_ok(x, L.w13, L.w2, n):
+                # MX middle: e4m3 + e8m0 block scales straight from the gate|up epilogue into the down MFMAs
+                aq, amx = ops.grouped_gemm_swiglu_mx(x, L.w13, row_off, scale, L.s13, a_rows=a_rows, rows=rows)
+                return ops.grouped_gemm(aq, L.w2, row_off, w_scale=L.s2, a_mx=amx)
             act = ops.grouped_gemm(x, L.w13, row_off, a_rows=a_rows, rows=rows, a_scale=scale, w_scale=L.s13,
                                    swiglu=True)
             aq, as_ = ops.quant_fp8_rows(act)

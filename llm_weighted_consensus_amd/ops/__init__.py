@@ -255,7 +255,8 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
                  out: Optional[torch.Tensor] = None, a_scale: Optional[torch.Tensor] = None,
                  w_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
                  a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None,
-                 splits: Optional[int] = None, swiglu: bool = False) -> torch.Tensor:
+                 splits: Optional[int] = None, swiglu: bool = False,
+                 a_mx: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Grouped GEMM on MFMA (K6g): rows [row_off[g], row_off[g+1]) of A times W[g]^T -> C [rows, N] bf16.
     ``a_rows`` [rows] gathers A's row for each output row (MoE dispatch; then ``rows`` = len(a_rows)).
     ``row_off`` lives on the device (MoE expert segments: no host sync, graph-capturable).  fp8 e4m3fn
@@ -265,16 +266,23 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
     chosen so a small-M launch (MoE decode down projection: 8 experts x 32 column tiles) still puts
     ~4 workgroups on every CU.  ``swiglu=True``: W's rows are gate / up interleaved in blocks of 32
     (:func:`swiglu_interleave` per group) and the result is silu(gate) * up [rows, N/2] — from the 8-phase
-    kernel's epilogue when it takes the batch, else GEMM + the SwiGLU pass."""
+    kernel's epilogue when it takes the batch, else GEMM + the SwiGLU pass.  ``a_mx`` [K/128, rows, 4] uint8:
+    A carries MX block scales (from :func:`grouped_gemm_swiglu_mx`) instead of ``a_scale`` — 8-phase kernel
+    only."""
     if rows is None:
         rows = a_rows.numel() if a_rows is not None else A.shape[0]
     G, N, K = W.shape[0], W.shape[1], W.shape[2]
+    if a_mx is not None:
+        if out is None:
+            out = torch.empty(rows, N, dtype=torch.bfloat16, device=A.device)
+        kernels().gemm8g_fp8(A, W, out, row_off, -(-rows // 256) + G, None, None, w_scale.contiguous(), 0, a_mx, None)
+        return out
     if _use_gemm8g(A, W, rows, G, N, K, bias, splits, out) and (not swiglu or N % 64 == 0):
         # large fp8 expert batches (>= ~1 full 256-row tile per expert on average): the 8-phase kernel
         if out is None:
             out = torch.empty(rows, N // 2 if swiglu else N, dtype=torch.bfloat16, device=A.device)
         kernels().gemm8g_fp8(A, W, out, row_off, -(-rows // 256) + G, a_rows, a_scale, w_scale.contiguous(),
-                             bool(swiglu))
+                             int(bool(swiglu)), None, None)
         return out
     if swiglu:
         return silu_mul(grouped_gemm(A, W, row_off, max_slots=max_slots, a_scale=a_scale, w_scale=w_scale,
@@ -292,6 +300,36 @@ def grouped_gemm(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, max_sl
 
 
 MOE_GEMM = os.environ.get("LWC_MOE_GEMM", "auto")  # auto | g8 (8-phase grouped fp8) | classic (128x128)
+# fp8 expert FFN middle in MX form (gate|up epilogue writes e4m3 + e8m0 block scales, the down GEMM's MFMAs
+# apply them): "1" (default) where both GEMMs take the 8-phase kernel, "0" = SwiGLU epilogue + row quantisation
+MOE_MX = os.environ.get("LWC_MOE_MX", "1") != "0"
+
+
+def grouped_gemm_swiglu_mx(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tensor, a_scale: torch.Tensor,
+                           w_scale: torch.Tensor, a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None):
+    """Grouped fp8 gate|up GEMM (W rows gate / up interleaved in blocks of 32) with SwiGLU in the epilogue and
+    the activation written as MX e4m3: -> (q [rows, F] e4m3, mx [F/128, rows, 4] uint8 e8m0).  Block b of each
+    128-column slice is its 16-column chunks b and b + 4 (the K chunks one MFMA lane of the down GEMM holds);
+    value = q * 2^(mx - 127).  The down GEMM takes them through ``grouped_gemm(q, W2, row_off, a_mx=mx)``, so
+    the activation never exists in bf16 in HBM and no separate quantisation pass runs."""
+    if rows is None:
+        rows = a_rows.numel() if a_rows is not None else A.shape[0]
+    G, N, K = W.shape
+    F_ = N // 2
+    q = torch.empty(rows, F_, dtype=torch.float8_e4m3fn, device=A.device)
+    mx = torch.empty(N // 256, rows, 4, dtype=torch.uint8, device=A.device)
+    kernels().gemm8g_fp8(A, W, q, row_off, -(-rows // 256) + G, a_rows, a_scale, w_scale.contiguous(), 2, None, mx)
+    return q, mx
+
+
+def moe_mx_ok(A: torch.Tensor, W13: torch.Tensor, W2: torch.Tensor, rows: int) -> bool:
+    """Whether the expert FFN runs its middle in MX form (both GEMMs on the 8-phase kernel)."""
+    if not MOE_MX or A.dtype != torch.float8_e4m3fn or W2.dtype != torch.float8_e4m3fn:
+        return False
+    G, N, K = W13.shape
+    if N % 256 or W2.shape[2] != N // 2 or not _use_gemm8g(A, W13, rows, G, N, K, None, None, None):
+        return False
+    return rows * (N // 2) < (1 << 31) and (N // 256) * rows * 4 < (1 << 31)
 
 
 def _use_gemm8g(A, W, rows, G, N, K, bias, splits, out) -> bool:
@@ -491,7 +529,7 @@ def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Option
     for r0 in range(0, M, step):
         r1 = min(M, r0 + step)
         kernels().gemm8g_fp8(xq[r0:r1], wq, out[r0:r1], None, -(-(r1 - r0) // 256), None, s[r0:r1], ws,
-                             bool(swiglu))
+                             int(bool(swiglu)), None, None)
     return out
 
 

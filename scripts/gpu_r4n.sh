@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4: MX expert FFN middle (gemm8g kMxOut -> kMxA) — numerics, Mixtral model tests, A/B, config 5.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_kernels_gpu.py -k "mx or gemm8g or grouped or moe or fp8" > gpurun_out/pytest_r4n.log 2>&1
+rc=$?; echo "pytest kernels rc=$rc"; tail -3 gpurun_out/pytest_r4n.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_model_gpu.py tests/test_tp_gpu.py tests/test_alltoall_gpu.py -k "mixtral or moe or ep" > gpurun_out/pytest_r4n2.log 2>&1
+rc=$?; echo "pytest model rc=$rc"; tail -3 gpurun_out/pytest_r4n2.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u scripts/moe_mx_ab.py > gpurun_out/moe_mx_ab.log 2>&1
+rc=$?; echo "ab rc=$rc"; grep "T=" gpurun_out/moe_mx_ab.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 bench_configs.py moe --steps 2 > gpurun_out/cfg5_r4n.log 2> gpurun_out/cfg5_r4n.err
+rc=$?; echo "config5 rc=$rc"; tail -1 gpurun_out/cfg5_r4n.log | cut -c1-200; exit $rc

@@ -839,7 +839,7 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     a_rows = torch.randperm(rows + 37, device=gpu)[:rows].to(torch.int32) if gather else None
     out = torch.full((rows, N), float("nan"), dtype=torch.bfloat16, device=gpu)
     ops.kernels().gemm8g_fp8(Aq, Wq, out, off, -(-rows // 256) + G, a_rows, a_s.float().contiguous(),
-                             w_s.float().contiguous(), False)
+                             w_s.float().contiguous(), 0, None, None)
     Ar = Aq.float() * a_s[:, None]
     if gather:
         Ar = Ar[a_rows.long()]
@@ -894,6 +894,95 @@ def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch
             yb = y.view(-1, F // 32, 2, 32)
             want = (torch.nn.functional.silu(yb[:, :, 0]) * yb[:, :, 1]).reshape(-1, F)
             _close(out[o[g]:o[g + 1]], want, 3e-2, 2e-2)
+
+
+def _mx_scale_map(mx: torch.Tensor, K: int) -> torch.Tensor:
+    """[K/128, rows, 4] e8m0 bytes -> per-element scales [rows, K]: element k of 128-slice t is in block
+    ((k % 128) // 16) % 4 (16-byte chunks b and b + 4 form block b)."""
+    blk = ((torch.arange(K, device=mx.device) % 128) // 16) % 4
+    kt = torch.arange(K, device=mx.device) // 128
+    return torch.exp2(mx.float() - 127.0)[kt, :, blk].t()
+
+
+@pytest.mark.parametrize("sizes", [[300, 0, 77, 520], [1024, 1003, 990, 1079]])
+def test_grouped_fp8_mx_a_matches_reference(gpu, sizes):
+    """The down-projection side of the MX expert FFN: gemm8g with A's e8m0 block scales applied by the
+    block-scaled MFMA (the scale tile DMA'd beside A, one scale byte per lane and row fragment via op_sel)
+    vs fp32 of the dequantised operands; ragged groups, an empty group, scales spread over 2^-9..2^9."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(17)
+    G, N, K = len(sizes), 512, 1024
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    Aq = (torch.randn(rows, K, device=gpu) * 100).clamp(-448, 448).to(torch.float8_e4m3fn)
+    mx = torch.randint(118, 137, (K // 128, rows, 4), dtype=torch.uint8, device=gpu)
+    W = torch.randn(G, N, K, device=gpu) * 0.05
+    w_s = W.abs().amax(2).clamp(min=1e-6) / 448.0
+    Wq = (W / w_s[:, :, None]).to(torch.float8_e4m3fn)
+    out = ops.grouped_gemm(Aq, Wq, off, w_scale=w_s.float().contiguous(), a_mx=mx)
+    Ar = Aq.float() * _mx_scale_map(mx, K)
+    Wr = Wq.float() * w_s[:, :, None]
+    o = off.tolist()
+    for g in range(G):
+        if o[g + 1] > o[g]:
+            _close(out[o[g]:o[g + 1]], Ar[o[g]:o[g + 1]] @ Wr[g].t(), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather):
+    """The gate|up side of the MX expert FFN: SwiGLU in gemm8g's epilogue, the activation written as e4m3
+    with one e8m0 scale per (row, block of 32) — block maxima met across waves in LDS — vs fp32; then the
+    whole middle (MX gate|up -> MX down) vs fp32 silu(gate) * up through the down projection."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(19)
+    G, F, K, D = 4, 512, 512, 256
+    sizes = [300, 0, 77, 520]
+    rows = sum(sizes)
+    off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
+    A = torch.randn(rows + 11, K, device=gpu)
+    W = torch.randn(G, 2 * F, K, device=gpu) * 0.05
+    Wi = torch.stack([ops.swiglu_interleave(W[g]) for g in range(G)])
+    a_s = A.abs().amax(1).clamp(min=1e-6) / 448.0
+    w_s = Wi.abs().amax(2).clamp(min=1e-6) / 448.0
+    Aq = (A / a_s[:, None]).to(torch.float8_e4m3fn)
+    Wq = (Wi / w_s[:, :, None]).to(torch.float8_e4m3fn)
+    a_rows = torch.randperm(rows + 11, device=gpu)[:rows].to(torch.int32) if gather else None
+    Ac, sc = (Aq, a_s) if gather else (Aq[:rows], a_s[:rows])
+    q, mx = ops.grouped_gemm_swiglu_mx(Ac, Wq, off, sc.float().contiguous(), w_s.float().contiguous(),
+                                       a_rows=a_rows, rows=rows)
+    assert q.shape == (rows, F) and mx.shape == (2 * F // 256, rows, 4)
+    Ar = Aq.float() * a_s[:, None]
+    if gather:
+        Ar = Ar[a_rows.long()]
+    Wr = Wq.float() * w_s[:, :, None]
+    want = torch.zeros(rows, F, device=gpu)
+    o = off.tolist()
+    for g in range(G):
+        if o[g + 1] > o[g]:
+            yb = (Ar[o[g]:o[g + 1]] @ Wr[g].t()).view(-1, F // 32, 2, 32)
+            want[o[g]:o[g + 1]] = (torch.nn.functional.silu(yb[:, :, 0]) * yb[:, :, 1]).reshape(-1, F)
+    got = q.float() * _mx_scale_map(mx, F)
+    rel = (got - want).norm() / want.norm()
+    assert rel < 4e-2, rel  # e4m3's 3 mantissa bits
+    # every block's scale is tight: its largest |q| lands in e4m3's top binade [256, 448]
+    blk = ((torch.arange(F, device=gpu) % 128) // 16) % 4
+    qa = q.float().abs().view(rows, F // 128, 128)
+    bmax = torch.stack([qa[:, :, blk == b].amax(-1) for b in range(4)], -1)  # [rows, F/128, 4]
+    live = bmax > 0
+    assert (bmax[live] >= 224).all()
+    # down projection from the MX activation vs fp32
+    W2 = torch.randn(G, D, F, device=gpu) * 0.05
+    s2 = W2.abs().amax(2).clamp(min=1e-6) / 448.0
+    W2q = (W2 / s2[:, :, None]).to(torch.float8_e4m3fn)
+    y = ops.grouped_gemm(q, W2q, off, w_scale=s2.float().contiguous(), a_mx=mx)
+    W2r = W2q.float() * s2[:, :, None]
+    for g in range(G):
+        if o[g + 1] > o[g]:
+            ref_ = want[o[g]:o[g + 1]] @ W2r[g].t()
+            rel = (y[o[g]:o[g + 1]].float() - ref_).norm() / ref_.norm()
+            assert rel < 5e-2, (g, rel)
 
 
 @pytest.mark.parametrize("d,rows", [(4096, 1), (4096, 301), (2048, 64), (8192, 257), (1024, 33)])
