@@ -61,7 +61,7 @@ constexpr int kPlain = 0;   // bf16 out, A per-row scaled
 constexpr int kSwiglu = 1;  // SwiGLU epilogue, bf16 out
 constexpr int kMxOut = 2;   // SwiGLU epilogue, e4m3 out with MX block scales (feeds a kMxA GEMM)
 constexpr int kMxA = 3;     // bf16 out, A carries MX block scales
-constexpr int kMxLds = 2048;  // kMxA: the two K buffers' scale tiles (256 rows x 4 blocks each)
+constexpr int kMxLds = 4096;  // kMxA: the two K buffers' scale tiles (256 rows x 4 blocks, twice: see the DMA)
 
 // A block-scaled: the lane's e8m0 scale is byte OP of sa (its row's scale for the lane's K block)
 template <int OP>
@@ -169,17 +169,14 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   const int sw = (r16 >> 1) & 7;
   const int off0 = r16 * 128 + ((q ^ sw) << 4), off1 = r16 * 128 + (((4 + q) ^ sw) << 4);
 
-  // kMxA: the tile's scales, DMA'd with unit A0 as two 1-byte pieces per thread into [block][wave row][row
-  // within a 16-row fragment][fragment] order, so a lane reads its 8 fragments' scales as one 8-byte word
-  uint32_t voS[2] = {0u, 0u};
+  // kMxA: the tile's scales ([row][4 blocks], one dword per row) DMA'd with unit A0, one dword piece per thread
+  // (an LDS-DMA lands every lane's piece on a 4-byte slot, so no narrower piece packs): threads 256..511 load
+  // a second copy, keeping every wave's vmcnt count equal; a lane then reads its 8 fragments' bytes
+  uint32_t voS = 0u;
   if constexpr (MXA) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int pos = j * 512 + tid, fi = pos & 7, fr = (pos >> 3) & 15, fw = (pos >> 7) & 1, fb = pos >> 8;
-      int r = m_begin + fw * 128 + fi * 16 + fr;
-      if (r >= m_end) r = m_begin;
-      voS[j] = (uint32_t)(r * 4 + fb);
-    }
+    int r = m_begin + (tid & 255);
+    if (r >= m_end) r = m_begin;
+    voS = (uint32_t)(r * 4);
   }
   const __amdgpu_buffer_rsrc_t rS = uniform_rsrc(p.a_mx, MXA ? (p.K / 128) * p.s_rows * 4 : 0);
   const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(p.A, p.rows_a * p.lda);
@@ -195,11 +192,9 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     }
     if constexpr (MXA) {
       if (u == 0) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          auto* dst = (__attribute__((address_space(3))) void*)(smem + kLdsB + (kt & 1) * 1024 + j * 512 + wid * 64);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, dst, 1, voS[j], kt * p.s_rows * 4, 0, 0);
-        }
+        auto* dst = (__attribute__((address_space(3))) void*)(smem + kLdsB + (kt & 1) * 2048 + (wid >> 2) * 1024 +
+                                                              (wid & 3) * 256);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, dst, 4, voS, kt * p.s_rows * 4, 0, 0);
       }
     }
   };
@@ -215,17 +210,14 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     for (int jj = 0; jj < 4; ++jj) acc[i][jj] = float4v{0.f, 0.f, 0.f, 0.f};
 
   uint4v a[4][2], b0[2][2], b1[2][2];
-  uint2 sc = {0u, 0u};  // kMxA: this K tile's scales of the lane's 8 row fragments (block q)
+  int sc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kMxA: this K tile's scale (block q) of the lane's 8 row fragments
   auto mma = [&](int i0, int j0, const uint4v (&bb)[2][2]) {
     if constexpr (MXA) {
-      const int sa = (int)(i0 == 0 ? sc.x : sc.y);
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        acc[i0 + 0][j0 + jj] = mfma8s<0>(a[0][0], a[0][1], bb[jj][0], bb[jj][1], acc[i0 + 0][j0 + jj], sa);
-        acc[i0 + 1][j0 + jj] = mfma8s<1>(a[1][0], a[1][1], bb[jj][0], bb[jj][1], acc[i0 + 1][j0 + jj], sa);
-        acc[i0 + 2][j0 + jj] = mfma8s<2>(a[2][0], a[2][1], bb[jj][0], bb[jj][1], acc[i0 + 2][j0 + jj], sa);
-        acc[i0 + 3][j0 + jj] = mfma8s<3>(a[3][0], a[3][1], bb[jj][0], bb[jj][1], acc[i0 + 3][j0 + jj], sa);
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[i0 + i][j0 + jj] = mfma8s<0>(a[i][0], a[i][1], bb[jj][0], bb[jj][1], acc[i0 + i][j0 + jj], sc[i0 + i]);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -257,9 +249,9 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
   G8_BAR()
 #define G8_STAGE(U, R) stage(U, smem + ((R) & 1) * kBufB, (R))
 #define G8_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
-  // kMxA stages 2 more pieces with unit A0: the waits after A0 / B0 of the next tile leave 6 in flight, not 4
+  // kMxA stages 1 more piece with unit A0: the waits after A0 / B0 of the next tile leave 5 in flight, not 4
 #define G8_VMX() \
-  if constexpr (MXA) G8_VM(6); \
+  if constexpr (MXA) G8_VM(5); \
   else G8_VM(4)
 #define G8_TILE(R, ST1, ST2, ST3, ST4, W1, W2, W4) \
   {                                                \
@@ -267,8 +259,10 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     rdB(cb, kUB0, b0);                             \
     __builtin_amdgcn_sched_barrier(0);             \
     rdA(cb, kUA0);                                 \
-    if constexpr (MXA)                             \
-      sc = *reinterpret_cast<const uint2*>(smem + kLdsB + ((R) & 1) * 1024 + ((q * 2 + wr) * 16 + r16) * 8); \
+    if constexpr (MXA) {                           \
+      const uint8_t* st = smem + kLdsB + ((R) & 1) * 2048 + (wr * 128 + r16) * 4 + q; \
+      _Pragma("unroll") for (int i = 0; i < 8; ++i) sc[i] = st[i * 64]; \
+    }                                              \
     ST1;                                           \
     W1;                                            \
     G8_MFMA(0, 0, b0);                             \
