@@ -50,7 +50,9 @@ struct Params {
   int gn;                 // grouped: n-tiles an XCD walks per m-slot before the next slot (>= 1)
   int skip_empty;         // skip the MFMAs of empty 64-row blocks (LWC_G8G_SKIP=0: A/B off)
   // MX activations (kMxOut producer / kMxA consumer): e8m0 block scales [K / 128][s_rows][4] bytes, block b
-  // of a 128-byte K slice = its 16-byte chunks b and b + 4 (the chunk pair one MFMA lane holds)
+  // of a 128-byte K slice = its bytes [32b, 32b + 32).  (The block-scaled MFMA takes a lane's two 16-byte
+  // fragments as K [16q, 16q + 16) and [64 + 16q, ...) of its 128 and scales K block b by the byte lane
+  // group b supplies — measured, scripts/mx_probe.py.)
   const uint8_t* a_mx;    // kMxA: scales of A (a_scale unused)
   uint8_t* mx_out;        // kMxOut: scales of the e4m3 output (C is then e4m3 [rows, ldc bytes])
   int s_rows;             // rows of the scale planes
@@ -72,9 +74,10 @@ LWC_DEVICE float4v mfma8s(const uint4v& a0, const uint4v& a1, const uint4v& b0, 
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 0, 0, OP, sa, 0, 127);
 }
 
-// max over the lane pairs (0,1) (2,3) of every quad
-LWC_DEVICE float pair_max(float x) {
-  return fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false)));
+// max over each quad of lanes
+LWC_DEVICE float quad_max(float x) {
+  x = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false)));  // ^1
+  return fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false)));  // ^2
 }
 
 // e8m0 exponent of a block with max |x| = amax: the smallest e with amax * 2^-e <= 448 (e4m3's largest finite),
@@ -332,34 +335,21 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
     __syncthreads();
     const int cch = lane % 4, nout = p.N / 2;
     if constexpr (MODE == kMxOut) {
-      // e4m3 rows with one e8m0 scale per (row, MX block): block b of the workgroup's 128 outputs (= one K
-      // slice of the down GEMM) is the 16-column chunks b and b + 4, held by waves b / 2 and 2 + b / 2 — the
-      // chunk maxima meet in LDS
-      float* amx = reinterpret_cast<float*>(smem + 65536);  // [wave row][128 rows][8 chunks]
-      const int c16 = 2 * wc + (cch >> 1);
-#pragma unroll 4
-      for (int k = 0; k < 8; ++k) {
-        const int row = lane / 4 + 16 * k;
-        float v[8];
-        unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3))), v);
-        float m = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
-        m = pair_max(m);
-        if ((cch & 1) == 0) amx[(wr * 128 + row) * 8 + c16] = m;
-      }
-      __syncthreads();
+      // e4m3 rows with one e8m0 scale per (row, MX block): the wave's 32 outputs of a row are exactly block wc of
+      // the workgroup's 128 (= one K slice of the down GEMM), held by one quad of lanes (8 each)
       uint8_t* q8 = reinterpret_cast<uint8_t*>(p.C);
 #pragma unroll 4
       for (int k = 0; k < 8; ++k) {
         const int row = lane / 4 + 16 * k;
         const int gm = m_begin + wr * 128 + row;
         const int gn = n0 / 2 + wc * 32 + cch * 8;
-        const float* ar = amx + (wr * 128 + row) * 8;
-        const int e = mx_exp(fmaxf(ar[c16], ar[(c16 + 4) & 7]));
-        const float inv = __builtin_amdgcn_ldexpf(1.f, -e);
         float v[8];
         unpack8(*reinterpret_cast<const uint4v*>(ot + row * CW + ((cch * 8) ^ ((row & 3) << 3))), v);
+        float m = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+        const int e = mx_exp(quad_max(m));
+        const float inv = __builtin_amdgcn_ldexpf(1.f, -e);
         uint32_t lo = 0, hi = 0;
         lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
         lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
@@ -367,7 +357,7 @@ __global__ void __launch_bounds__(512) gemm8g_kernel(Params p) {
         hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
         if (gm < m_end && gn < nout) {
           *reinterpret_cast<uint2*>(q8 + (size_t)gm * p.ldc + gn) = uint2{lo, hi};
-          if (c16 < 4 && (cch & 1) == 0) p.mx_out[((size_t)(n0 / 256) * p.s_rows + gm) * 4 + c16] = (uint8_t)(e + 127);
+          if (cch == 0) p.mx_out[((size_t)(n0 / 256) * p.s_rows + gm) * 4 + wc] = (uint8_t)(e + 127);
         }
       }
     } else {

@@ -309,8 +309,7 @@ def grouped_gemm_swiglu_mx(A: torch.Tensor, W: torch.Tensor, row_off: torch.Tens
                            w_scale: torch.Tensor, a_rows: Optional[torch.Tensor] = None, rows: Optional[int] = None):
     """Grouped fp8 gate|up GEMM (W rows gate / up interleaved in blocks of 32) with SwiGLU in the epilogue and
     the activation written as MX e4m3: -> (q [rows, F] e4m3, mx [F/128, rows, 4] uint8 e8m0).  Block b of each
-    128-column slice is its 16-column chunks b and b + 4 (the K chunks one MFMA lane of the down GEMM holds);
-    value = q * 2^(mx - 127).  The down GEMM takes them through ``grouped_gemm(q, W2, row_off, a_mx=mx)``, so
+    128-column slice is its columns [32b, 32b + 32); value = q * 2^(mx - 127).  The down GEMM takes them through ``grouped_gemm(q, W2, row_off, a_mx=mx)``, so
     the activation never exists in bf16 in HBM and no separate quantisation pass runs."""
     if rows is None:
         rows = a_rows.numel() if a_rows is not None else A.shape[0]

@@ -2,7 +2,7 @@
 """Probe of the block-scaled MFMA's A-scale mapping inside gemm8g's MX-A mode: A = ones, W = identity over
 one 128-wide K slice, so out[r, k] = the scale the MFMA applied to A element (r, k).  Scale bytes are unique
 per (row % 16, block); prints the measured byte grid for rows 0..31 at each 16-column chunk next to the
-byte the kernel's layout assumes (block of chunk c = c % 4)."""
+byte the kernel's layout assumes (block of 16-column chunk c = c // 2)."""
 import os
 import sys
 
@@ -27,7 +27,7 @@ def main():
     out = ops.grouped_gemm(A, W, off, w_scale=ws, a_mx=mx).float()
     meas = (torch.log2(out.clamp(min=1e-30)).round() + 127).long().cpu()
     exp = mx[0].long().cpu()
-    blk = [(c % 4) for c in range(8)]
+    blk = [c // 2 for c in range(8)]  # block b = K [32b, 32b + 32)
     bad = 0
     for row in range(32):
         got = [int(meas[row, 16 * c]) for c in range(8)]

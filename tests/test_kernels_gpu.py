@@ -898,8 +898,8 @@ def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch
 
 def _mx_scale_map(mx: torch.Tensor, K: int) -> torch.Tensor:
     """[K/128, rows, 4] e8m0 bytes -> per-element scales [rows, K]: element k of 128-slice t is in block
-    ((k % 128) // 16) % 4 (16-byte chunks b and b + 4 form block b)."""
-    blk = ((torch.arange(K, device=mx.device) % 128) // 16) % 4
+    (k % 128) // 32."""
+    blk = (torch.arange(K, device=mx.device) % 128) // 32
     kt = torch.arange(K, device=mx.device) // 128
     return torch.exp2(mx.float() - 127.0)[kt, :, blk].t()
 
@@ -932,7 +932,7 @@ def test_grouped_fp8_mx_a_matches_reference(gpu, sizes):
 @pytest.mark.parametrize("gather", [False, True])
 def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather):
     """The gate|up side of the MX expert FFN: SwiGLU in gemm8g's epilogue, the activation written as e4m3
-    with one e8m0 scale per (row, block of 32) — block maxima met across waves in LDS — vs fp32; then the
+    with one e8m0 scale per (row, block of 32; one quad of lanes per block) vs fp32; then the
     whole middle (MX gate|up -> MX down) vs fp32 silu(gate) * up through the down projection."""
     from llm_weighted_consensus_amd import ops
 
@@ -967,9 +967,7 @@ def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather):
     rel = (got - want).norm() / want.norm()
     assert rel < 4e-2, rel  # e4m3's 3 mantissa bits
     # every block's scale is tight: its largest |q| lands in e4m3's top binade [256, 448]
-    blk = ((torch.arange(F, device=gpu) % 128) // 16) % 4
-    qa = q.float().abs().view(rows, F // 128, 128)
-    bmax = torch.stack([qa[:, :, blk == b].amax(-1) for b in range(4)], -1)  # [rows, F/128, 4]
+    bmax = q.float().abs().view(rows, F // 128, 4, 32).amax(-1)  # [rows, F/128, 4]
     live = bmax > 0
     assert (bmax[live] >= 224).all()
     # down projection from the MX activation vs fp32
