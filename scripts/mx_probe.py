@@ -40,3 +40,31 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def probe_slices():
+    """The same readout for each 128-wide K slice of K = 1024, two groups (the second starting at row 37):
+    mismatching (row, chunk) counts per slice (0 everywhere = the scale tiles of later K tiles land right)."""
+    from llm_weighted_consensus_amd import ops
+
+    dev = torch.device("cuda", 0)
+    R, K, N = 256, 1024, 128
+    A = torch.ones(R, K, device=dev).to(torch.float8_e4m3fn)
+    g = torch.Generator(device=dev).manual_seed(3)
+    mx = torch.randint(110, 145, (K // 128, R, 4), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.tensor([0, 37, R], dtype=torch.int32, device=dev)
+    ws = torch.ones(2, N, device=dev)
+    for t in range(K // 128):
+        W = torch.zeros(N, K, device=dev)
+        W[torch.arange(N), 128 * t + torch.arange(N)] = 1.0
+        Wq = W.to(torch.float8_e4m3fn).view(1, N, K).expand(2, N, K).contiguous()
+        out = ops.grouped_gemm(A, Wq, off, w_scale=ws, a_mx=mx).float()
+        meas = (torch.log2(out.clamp(min=1e-30)).round() + 127).long()
+        want = mx[t].long()[:, torch.arange(N, device=dev) // 32]
+        bad = (meas != want)
+        print(f"slice {t}: mismatches {int(bad.sum())} of {bad.numel()}; rows with any: "
+              f"{bad.any(1).nonzero().flatten()[:12].tolist()}", flush=True)
+
+
+if __name__ == "__main__":
+    probe_slices()
