@@ -450,24 +450,29 @@ void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c
   } else {
     TORCH_CHECK(C.size(0) <= A.size(0), "gemm8g: more output rows than A rows");
   }
+  // scale planes [K / 128][rows][4] bytes; a row-range view of a larger tensor is accepted (the plane stride
+  // is then the full tensor's row count)
+  auto plane_rows = [](const at::Tensor& t, const char* what) {
+    CHECK_GPU(t); CHECK_DTYPE(t, at::kByte);
+    TORCH_CHECK(t.dim() == 3 && t.size(2) == 4 && t.stride(2) == 1 && t.stride(1) == 4 && t.stride(0) % 4 == 0 &&
+                    t.stride(0) / 4 >= t.size(1),
+                what, ": MX scales must be [K / 128, rows, 4] bytes with rows contiguous");
+    return (int)(t.stride(0) / 4);
+  };
   int s_rows = 0;
   const void* amx = nullptr;
   void* mxo = nullptr;
   if (mxa) {
     TORCH_CHECK(mode == 0 && ar == nullptr, "gemm8g: MX A takes the plain epilogue and contiguous rows");
-    CHECK_GPU(*a_mx); CHECK_CONTIG(*a_mx); CHECK_DTYPE(*a_mx, at::kByte);
-    TORCH_CHECK(a_mx->dim() == 3 && a_mx->size(0) == K / 128 && a_mx->size(1) >= A.size(0) && a_mx->size(2) == 4,
-                "gemm8g: a_mx must be [K / 128, rows_a, 4]");
-    s_rows = (int)a_mx->size(1);
+    s_rows = plane_rows(*a_mx, "gemm8g a_mx");
+    TORCH_CHECK(a_mx->size(0) == K / 128 && a_mx->size(1) >= A.size(0), "gemm8g: a_mx must be [K / 128, rows_a, 4]");
     amx = a_mx->data_ptr();
   }
   if (mode == 2) {
     TORCH_CHECK(mx_out.has_value() && mx_out->defined(), "gemm8g: mode 2 writes mx_out");
-    CHECK_GPU(*mx_out); CHECK_CONTIG(*mx_out); CHECK_DTYPE(*mx_out, at::kByte);
-    TORCH_CHECK(N % 256 == 0 && mx_out->dim() == 3 && mx_out->size(0) == N / 256 && mx_out->size(1) >= C.size(0) &&
-                    mx_out->size(2) == 4 && C.stride(0) % 16 == 0,
+    s_rows = plane_rows(*mx_out, "gemm8g mx_out");
+    TORCH_CHECK(N % 256 == 0 && mx_out->size(0) == N / 256 && mx_out->size(1) >= C.size(0) && C.stride(0) % 16 == 0,
                 "gemm8g: mx_out must be [N / 256, rows, 4] (N % 256 == 0)");
-    s_rows = (int)mx_out->size(1);
     mxo = mx_out->data_ptr();
   }
   CHECK_RC(lwc_gemm8g_fp8(A.data_ptr(), W.data_ptr(), C.data_ptr(), ro, ar, as, w_scale.data_ptr<float>(), G,

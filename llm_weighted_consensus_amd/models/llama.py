@@ -260,6 +260,10 @@ class LlamaModel:
         silu_mul), down GEMM.  fp8: gate|up fp8 GEMM, SwiGLU fused with the down projection's row
         quantisation (K11e), down fp8 GEMM."""
         if isinstance(L.w_down, ops.Fp8Weight):
+            if ops.dense_mx_ok(h, L.w_gate_up, L.w_down, L.gu_block):
+                # large batches (the embedder's prefill): the activation in MX form, no quantisation pass
+                aq, amx = ops.linear_fp8_swiglu_mx(h, L.w_gate_up)
+                return ops.linear_fp8_mx(aq, amx, L.w_down)
             aq, as_ = ops.linear_fp8_swiglu(h, L.w_gate_up, L.gu_block)
             return ops.linear_fp8_q(aq, as_, L.w_down)
         return self._proj(self._act(h, L), L.w_down)

@@ -595,6 +595,55 @@ def linear_fp8_swiglu(x, w: Fp8Weight, block: int):
     return own() if c == "g8g" else lib()
 
 
+# dense fp8 MLP middle in MX form (config 5's embedder prefill): gate|up on gemm8g with the SwiGLU epilogue
+# writing e4m3 + e8m0 block scales, the down projection's MFMAs applying them.  Taken from DENSE_MX_MIN_ROWS
+# rows, where gemm8g wins both projections (profiles/moe_round4.md); "LWC_DENSE_MX=0" keeps the row-scaled path
+DENSE_MX = os.environ.get("LWC_DENSE_MX", "1") != "0"
+DENSE_MX_MIN_ROWS = 16384
+
+
+def dense_mx_ok(x, w_gu: Fp8Weight, w_down: Fp8Weight, block: int) -> bool:
+    xq = x.q if isinstance(x, QAct) else x
+    M = xq.shape[0]
+    N, K = w_gu.q.shape
+    return (DENSE_MX and FP8_GEMM != "blas" and block == 32 and M >= DENSE_MX_MIN_ROWS and xq.is_cuda
+            and N % 256 == 0 and K % 128 == 0 and w_down.q.shape[1] == N // 2 and w_down.q.shape[0] % 8 == 0)
+
+
+def _row_blocks(M: int, row_bytes: int):
+    step = max(256, (G8G_SPAN - 1) // row_bytes // 256 * 256)
+    return [(r0, min(M, r0 + step)) for r0 in range(0, M, step)]
+
+
+def linear_fp8_swiglu_mx(x, w: Fp8Weight):
+    """Dense fp8 gate|up (rows interleaved in blocks of 32) + SwiGLU with the activation written in MX form:
+    -> (q [M, F] e4m3, mx [F/128, M, 4] uint8 e8m0) for :func:`linear_fp8_mx`.  Row blocks as in
+    :func:`gemm8g_dense` (the scales are per row, so the down GEMM may block its rows differently)."""
+    xq, xs = (x.q, x.s) if isinstance(x, QAct) else quant_fp8_rows(x)
+    M = xq.shape[0]
+    N, K = w.q.shape
+    q = torch.empty(M, N // 2, dtype=torch.float8_e4m3fn, device=xq.device)
+    mx = torch.empty(N // 256, M, 4, dtype=torch.uint8, device=xq.device)
+    s, ws, wq = xs.reshape(-1).contiguous(), w.s.reshape(-1), w.q.view(1, N, K)
+    for r0, r1 in _row_blocks(M, xq.stride(0)):
+        kernels().gemm8g_fp8(xq[r0:r1], wq, q[r0:r1], None, -(-(r1 - r0) // 256), None, s[r0:r1], ws, 2, None,
+                             mx[:, r0:r1])
+    return q, mx
+
+
+def linear_fp8_mx(aq: torch.Tensor, amx: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
+    """(e4m3 [M, K] with MX block scales [K/128, M, 4]) . w^T -> bf16 [M, N] on gemm8g (the scales applied by
+    the block-scaled MFMA)."""
+    M = aq.shape[0]
+    N, K = w.q.shape
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=aq.device)
+    ws, wq = w.s.reshape(-1), w.q.view(1, N, K)
+    for r0, r1 in _row_blocks(M, aq.stride(0)):
+        kernels().gemm8g_fp8(aq[r0:r1], wq, out[r0:r1], None, -(-(r1 - r0) // 256), None, None, ws, 0,
+                             amx[:, r0:r1], None)
+    return out
+
+
 def linear_fp8(x, w: Fp8Weight) -> torch.Tensor:
     """bf16 x [M, K] -> per-row e4m3 quantisation (K11e) -> fp8 GEMM -> bf16 [M, N].  A :class:`QAct`
     (quantised by the producing norm) goes straight to the GEMM."""

@@ -1059,6 +1059,34 @@ def test_dense_fp8_gemm8g_row_blocks(gpu, monkeypatch):
     _close(blocks, ref_, 2e-2, 2e-2)
 
 
+def test_dense_fp8_mlp_mx(gpu, monkeypatch):
+    """The dense fp8 MLP middle in MX form (config 5's embedder prefill): gemm8g dense SwiGLU epilogue writing
+    e4m3 + e8m0 block scales, the down projection applying them — with the row-block split forced (span shrunk)
+    so the scale planes are passed as row-range views — vs fp32 silu(gate) * up through the down projection."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(23)
+    M, F, K, D = 1200, 512, 256, 384
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    wgu = ops.Fp8Weight(ops.swiglu_interleave(torch.randn(2 * F, K, device=gpu).to(torch.bfloat16) * 0.05))
+    wd = ops.Fp8Weight(torch.randn(D, F, device=gpu).to(torch.bfloat16) * 0.05)
+    monkeypatch.setattr(ops, "DENSE_MX_MIN_ROWS", 1)
+    assert ops.dense_mx_ok(x, wgu, wd, 32)
+    q1, mx1 = ops.linear_fp8_swiglu_mx(x, wgu)
+    y1 = ops.linear_fp8_mx(q1, mx1, wd)
+    monkeypatch.setattr(ops, "G8G_SPAN", 256 * F + 1)  # row blocks of 256: five launches per projection
+    q2, mx2 = ops.linear_fp8_swiglu_mx(x, wgu)
+    y2 = ops.linear_fp8_mx(q2, mx2, wd)
+    assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8)) and torch.equal(mx1, mx2) and torch.equal(y1, y2)
+    xq, xs = ops.quant_fp8_rows(x)
+    gu = ((xq.float() * xs[:, None]) @ (wgu.q.float() * wgu.s.view(-1, 1)).t()).view(M, -1, 2, 32)
+    act = torch.nn.functional.silu(gu[:, :, 0].reshape(M, -1)) * gu[:, :, 1].reshape(M, -1)
+    got = q1.float() * _mx_scale_map(mx1, F)
+    assert ((got - act).norm() / act.norm()).item() < 4e-2
+    ref_ = act @ (wd.q.float() * wd.s.view(-1, 1)).t()
+    assert ((y1.float() - ref_).norm() / ref_.norm()).item() < 5e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (4096, 2048, 1024)])
 @pytest.mark.parametrize("backend", ["g8g", "blas", "auto"])
 def test_dense_fp8_swiglu(gpu, M, N, K, backend, monkeypatch):
