@@ -38,5 +38,9 @@ class DecoderEmbedder:
     def embed(self, token_lists: Sequence[Sequence[int]], max_tokens: Optional[int] = None):
         """-> (unit f32 [n, d], unit bf16 [n, d])"""
         ids, pos, cu, max_len = self.pack(token_lists, max_tokens)
-        h = self.model.encode(ids, pos, cu, max_len)
-        return ops.pool_l2norm(h, cu, ops.POOL_LAST)
+        # only each sequence's last token is pooled: the last layer's o projection, MLP and the final norm run
+        # on those rows alone (LlamaModel._layers ``keep``)
+        last = (cu[1:] - 1).long()
+        h = self.model.encode(ids, pos, cu, max_len, keep=last)
+        rows = torch.arange(h.shape[0] + 1, dtype=cu.dtype, device=cu.device)
+        return ops.pool_l2norm(h, rows, ops.POOL_LAST)

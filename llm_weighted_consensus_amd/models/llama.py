@@ -187,10 +187,14 @@ class LlamaModel:
         self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
 
     # ------------------------------------------------------------------ forward
-    def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True) -> torch.Tensor:
+    def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True,
+                keep: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Runs every layer; x_res is the residual stream (updated in place); returns the final
         normalised hidden state.  ``rope_q=False``: q leaves the qkv projection un-rotated and ``attn_fn``
-        rotates it (the decode kernels' load-time RoPE)."""
+        rotates it (the decode kernels' load-time RoPE).  ``keep`` (row indices): only those rows' final
+        states are wanted (a prefill's last tokens, an embedder's pooled token) — the last layer still runs
+        qkv / RoPE / the cache write / attention over every row (later tokens' keys and values), then its
+        o projection, MLP and the final norm over the kept rows only; returns [len(keep), d]."""
         cfg = self.cfg
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
@@ -211,6 +215,10 @@ class LlamaModel:
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
                               rope_q=rope_q)
             attn = attn_fn(qkv, li)
+            if keep is not None and li + 1 == len(self.layers):
+                attn = attn.reshape(T, Hq * D).index_select(0, keep)
+                x_res = x_res.index_select(0, keep)
+                T = x_res.shape[0]
             nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
             if fused:
                 gemm_plan.linear_add_(attn.view(T, Hq * D), L.wo, x_res, ws=self.g8_ws)
@@ -332,7 +340,7 @@ class LlamaModel:
         return self._proj(h, self.lm_head)
 
     def encode(self, tokens: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor,
-               max_seqlen: int) -> torch.Tensor:
+               max_seqlen: int, keep: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Cache-less causal forward of packed sequences -> final-normed hidden states [T, d] (decoder used
         as an embedder, e.g. e5-mistral: the caller pools the last token).  RoPE runs without a cache
         write (slots=None), attention is the varlen prefill kernel over the fresh k/v."""
@@ -345,7 +353,7 @@ class LlamaModel:
             return ops.prefill_attention(qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:],
                                          cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
 
-        return self._layers(x, null, positions, None, attn_fn)
+        return self._layers(x, null, positions, None, attn_fn, keep=keep)
 
     def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cu_seqlens: torch.Tensor,
                 max_seqlen: int, last_idx: torch.Tensor, cache: KVCache, ctx: Optional[dict] = None) -> torch.Tensor:
@@ -370,8 +378,8 @@ class LlamaModel:
             v = qkv[:, (Hq + Hkv) * D:]
             return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
 
-        h = self._layers(x, cache, positions, slots, attn_fn)
-        return F.linear(h.index_select(0, last_idx), self.lm_head)
+        h = self._layers(x, cache, positions, slots, attn_fn, keep=last_idx)  # last layer: o / MLP on these rows
+        return F.linear(h, self.lm_head)
 
     def forward_mixed(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cache: KVCache,
                       n_dec: int, dec: Optional[dict], chunk: dict, logit_rows: torch.Tensor) -> torch.Tensor:
