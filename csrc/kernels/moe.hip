@@ -27,7 +27,14 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
   const int tid = threadIdx.x;
   if (tid < E) s_count[tid] = 0;
   __syncthreads();
-  for (int t = tid; t < T; t += blockDim.x) {
+  // the token loop runs whole waves (inactive lanes past T) so the per-expert counts and cursors can be
+  // aggregated per wave: one LDS atomic per (wave, expert) instead of one per routed row (8192 on 8
+  // addresses at T = 4096 serialised in LDS)
+  const int lane = tid & 63;
+  const int Tw = (T + 63) & ~63;
+  for (int t0 = tid; t0 < Tw; t0 += blockDim.x) {
+    const bool live = t0 < T;
+    const int t = live ? t0 : 0;
     // fully unrolled over the compile-time bounds so the per-token arrays stay in registers
     float lv[EM];
     bool taken[EM];
@@ -67,9 +74,15 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
       if (j >= k) break;
-      topk_ids[t * k + j] = ids[j];
-      topk_w[t * k + j] = vals[j] / sum;
-      atomicAdd(&s_count[ids[j]], 1);
+      if (live) {
+        topk_ids[t * k + j] = ids[j];
+        topk_w[t * k + j] = vals[j] / sum;
+      }
+#pragma unroll
+      for (int e = 0; e < EM; ++e) {
+        const uint64_t m = __ballot(live && ids[j] == e);
+        if (m && lane == 0) atomicAdd(&s_count[e], __popcll(m));
+      }
     }
   }
   __syncthreads();
@@ -83,11 +96,25 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
     row_off[E] = acc;
   }
   __syncthreads();
-  for (int i = tid; i < T * k; i += blockDim.x) {
-    const int e = topk_ids[i];
-    const int pos = atomicAdd(&s_cursor[e], 1);
-    src_row[pos] = i / k;
-    inv[i] = pos;
+  // rows of one expert claimed per wave: the wave's lanes routed to e take consecutive slots from one atomic
+  const int TK = T * k, TKw = (TK + 63) & ~63;
+  for (int i0 = tid; i0 < TKw; i0 += blockDim.x) {
+    const bool live = i0 < TK;
+    const int e = live ? topk_ids[i0] : -1;
+    int pos = 0;
+    for (int ex = 0; ex < E; ++ex) {
+      const uint64_t m = __ballot(e == ex);
+      if (!m) continue;  // uniform
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&s_cursor[ex], __popcll(m));
+      base = __shfl(base, leader);
+      if (e == ex) pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (live) {
+      src_row[pos] = i0 / k;
+      inv[i0] = pos;
+    }
   }
 }
 

@@ -896,6 +896,34 @@ def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch
             _close(out[o[g]:o[g + 1]], want, 3e-2, 2e-2)
 
 
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (77, 8, 2), (4096, 8, 2), (300, 16, 4)])
+def test_moe_route_matches_torch(gpu, T, E, k):
+    """MoE routing (K11a, one workgroup, per-wave aggregated LDS counters / cursors): top-k ids and softmax
+    weights as torch computes them; row_off the per-expert counts' prefix sum; src_row groups every routed
+    (token, slot) under its expert; inv points each (token, slot) at its row."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(29)
+    logits = torch.randn(T, E, device=gpu).to(torch.bfloat16)
+    ids, w, row_off, src, inv = ops.moe_route(logits, k)
+    top, _ = logits.float().topk(k, dim=-1)
+    tid = ids.long()  # (bf16 ties: the kernel takes the lower expert id, torch's order is unspecified)
+    assert torch.equal(logits.float().gather(1, tid), top)
+    assert all(len(set(r)) == k for r in tid.tolist())
+    torch.testing.assert_close(w, top.softmax(-1), rtol=1e-5, atol=1e-6)
+    cnt = torch.bincount(tid.flatten(), minlength=E)
+    assert torch.equal(row_off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0).cpu()]))
+    inv_l, src_l = inv.long(), src.long()
+    tok = torch.arange(T, device=gpu).repeat_interleave(k)
+    assert torch.equal(src_l[inv_l], tok)                      # row of (t, j) holds token t
+    assert torch.equal(torch.sort(inv_l).values, torch.arange(T * k, device=gpu))  # a permutation
+    ro = row_off.long().tolist()
+    for e in range(E):                                         # expert e's rows are exactly its tokens
+        got = torch.sort(src_l[ro[e]:ro[e + 1]]).values
+        want = torch.sort(tok[tid.flatten() == e]).values
+        assert torch.equal(got, want), e
+
+
 def _mx_scale_map(mx: torch.Tensor, K: int) -> torch.Tensor:
     """[K/128, rows, 4] e8m0 bytes -> per-element scales [rows, K]: element k of 128-slice t is in block
     (k % 128) // 32."""
