@@ -64,11 +64,13 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
       ids[j] = best;
       vals[j] = bv;
     }
+    // softmax over the selected logits (vals[0] is the largest; read it once — the loop overwrites vals[0])
+    const float vmax = vals[0];
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
       if (j >= k) break;
-      vals[j] = __expf(vals[j] - vals[0]);
+      vals[j] = __expf(vals[j] - vmax);
       sum += vals[j];
     }
 #pragma unroll
