@@ -27,9 +27,10 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
   const int tid = threadIdx.x;
   if (tid < E) s_count[tid] = 0;
   __syncthreads();
-  // the token loop runs whole waves (inactive lanes past T) so the per-expert counts and cursors can be
-  // aggregated per wave: one LDS atomic per (wave, expert) instead of one per routed row (8192 on 8
-  // addresses at T = 4096 serialised in LDS)
+  // the token loop runs whole waves (inactive lanes past T) so the per-expert counts can be aggregated per
+  // wave: one LDS atomic per (wave, expert) instead of one per routed row.  (Claiming the cursor slots the
+  // same way — ballot, leader atomic, broadcast per expert — doubled the kernel's time: a chain of LDS round
+  // trips per expert; the slot pass keeps one atomic per row.)
   const int lane = tid & 63;
   const int Tw = (T + 63) & ~63;
   for (int t0 = tid; t0 < Tw; t0 += blockDim.x) {
@@ -98,25 +99,11 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
     row_off[E] = acc;
   }
   __syncthreads();
-  // rows of one expert claimed per wave: the wave's lanes routed to e take consecutive slots from one atomic
-  const int TK = T * k, TKw = (TK + 63) & ~63;
-  for (int i0 = tid; i0 < TKw; i0 += blockDim.x) {
-    const bool live = i0 < TK;
-    const int e = live ? topk_ids[i0] : -1;
-    int pos = 0;
-    for (int ex = 0; ex < E; ++ex) {
-      const uint64_t m = __ballot(e == ex);
-      if (!m) continue;  // uniform
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      int base = 0;
-      if (lane == leader) base = atomicAdd(&s_cursor[ex], __popcll(m));
-      base = __shfl(base, leader);
-      if (e == ex) pos = base + __popcll(m & ((1ull << lane) - 1ull));
-    }
-    if (live) {
-      src_row[pos] = i0 / k;
-      inv[i0] = pos;
-    }
+  for (int i = tid; i < T * k; i += blockDim.x) {
+    const int e = topk_ids[i];
+    const int pos = atomicAdd(&s_cursor[e], 1);
+    src_row[pos] = i / k;
+    inv[i] = pos;
   }
 }
 
