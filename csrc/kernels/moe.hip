@@ -27,15 +27,7 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
   const int tid = threadIdx.x;
   if (tid < E) s_count[tid] = 0;
   __syncthreads();
-  // the token loop runs whole waves (inactive lanes past T) so the per-expert counts can be aggregated per
-  // wave: one LDS atomic per (wave, expert) instead of one per routed row.  (Claiming the cursor slots the
-  // same way — ballot, leader atomic, broadcast per expert — doubled the kernel's time: a chain of LDS round
-  // trips per expert; the slot pass keeps one atomic per row.)
-  const int lane = tid & 63;
-  const int Tw = (T + 63) & ~63;
-  for (int t0 = tid; t0 < Tw; t0 += blockDim.x) {
-    const bool live = t0 < T;
-    const int t = live ? t0 : 0;
+  for (int t = tid; t < T; t += blockDim.x) {
     // fully unrolled over the compile-time bounds so the per-token arrays stay in registers
     float lv[EM];
     bool taken[EM];
@@ -77,15 +69,9 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
       if (j >= k) break;
-      if (live) {
-        topk_ids[t * k + j] = ids[j];
-        topk_w[t * k + j] = vals[j] / sum;
-      }
-#pragma unroll
-      for (int e = 0; e < EM; ++e) {
-        const uint64_t m = __ballot(live && ids[j] == e);
-        if (m && lane == 0) atomicAdd(&s_count[e], __popcll(m));
-      }
+      topk_ids[t * k + j] = ids[j];
+      topk_w[t * k + j] = vals[j] / sum;
+      atomicAdd(&s_count[ids[j]], 1);
     }
   }
   __syncthreads();
