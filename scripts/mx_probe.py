@@ -38,10 +38,6 @@ def main():
     print("rows with a mismatch (of 32):", bad)
 
 
-if __name__ == "__main__":
-    main()
-
-
 def probe_slices():
     """The same readout for each 128-wide K slice of K = 1024, two groups (the second starting at row 37):
     mismatching (row, chunk) counts per slice (0 everywhere = the scale tiles of later K tiles land right)."""
@@ -67,4 +63,5 @@ def probe_slices():
 
 
 if __name__ == "__main__":
+    main()
     probe_slices()
