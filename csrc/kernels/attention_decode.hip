@@ -486,6 +486,11 @@ struct CascadeParams {
   const float* rope_cos;  // as DecodeParams
   const float* rope_sin;
   const int* positions;
+  // MX output (the fp8 o projection's A operand): e4m3 rows [B, Hq * D] + e8m0 scales [Hq][mx_rows][4], one per
+  // 32 dims of a head (out is then unused)
+  uint8_t* out8;
+  uint8_t* mx;
+  int mx_rows;
 };
 
 // The index tables come in as const __restrict__ kernel arguments (not through the params struct): with
@@ -709,9 +714,23 @@ __global__ void __launch_bounds__(kCWaves * 64)
     const int seq = s0 + R / p.G;
     const int hq = kvh * p.G + R % p.G;
     const float inv = li > 0.f ? 1.f / li : 0.f;
-    bf16_t* dst = p.out + ((size_t)seq * p.Hq + hq) * kD;
+    if (p.out8) {
+      // block b = dims [32b, 32b + 32) = o[2b], o[2b + 1] of the 16 lanes of this DPP row (odim)
+      uint8_t* dst = p.out8 + ((size_t)seq * p.Hq + hq) * kD;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) dst[odim(n, r16)] = f2bf(o[n][i] * inv);
+      for (int b = 0; b < 4; ++b) {
+        const float v0 = o[2 * b][i] * inv, v1 = o[2 * b + 1][i] * inv;
+        const int e = mx_exp(row16_max(fmaxf(fabsf(v0), fabsf(v1))));
+        const float sc = __builtin_amdgcn_ldexpf(1.f, -e);
+        const uint32_t pk = __builtin_amdgcn_cvt_pk_fp8_f32(v0 * sc, v1 * sc, 0, false);
+        *reinterpret_cast<uint16_t*>(dst + odim(2 * b, r16)) = (uint16_t)pk;
+        if (r16 == 0) p.mx[((size_t)hq * p.mx_rows + seq) * 4 + b] = (uint8_t)(e + 127);
+      }
+    } else {
+      bf16_t* dst = p.out + ((size_t)seq * p.Hq + hq) * kD;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) dst[odim(n, r16)] = f2bf(o[n][i] * inv);
+    }
   }
 }
 
@@ -773,12 +792,14 @@ extern "C" int lwc_paged_decode_cascade(const void* q, int q_stride, const void*
                                         const int* block_tables, const int* ctx_lens, const int* tiles, int max_tiles,
                                         void* out, int Hq, int Hkv, int D, int BS, int max_blocks, float scale,
                                         const float* rope_cos, const float* rope_sin, const int* positions,
-                                        hipStream_t s) {
+                                        void* out8, void* mx, int mx_rows, hipStream_t s) {
   using namespace lwc;
   if (D != kD || BS != kBS || Hq % Hkv != 0 || 16 % (Hq / Hkv) != 0) return -1;
+  if ((out8 == nullptr) != (mx == nullptr)) return -1;
   if (max_tiles == 0) return 0;
   CascadeParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, ctx_lens, tiles,
-                  (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale, rope_cos, rope_sin, positions};
+                  (bf16_t*)out, q_stride, Hq, Hkv, Hq / Hkv, max_blocks, scale, rope_cos, rope_sin, positions,
+                  (uint8_t*)out8, (uint8_t*)mx, mx_rows};
   static int pairs = 0;
   if (pairs == 0) {
     const char* e = getenv("LWC_CASCADE_PAIRS");

@@ -20,7 +20,7 @@ int lwc_paged_decode(const void*, int, const void*, const void*, const int*, con
                      int, int, int, int, int, int, float, const float*, const float*, const int*, hipStream_t);
 int lwc_set_decode_wave_min_items(int);
 int lwc_paged_decode_cascade(const void*, int, const void*, const void*, const int*, const int*, const int*, int, void*,
-                             int, int, int, int, int, float, const float*, const float*, const int*, hipStream_t);
+                             int, int, int, int, int, float, const float*, const float*, const int*, void*, void*, int, hipStream_t);
 int lwc_cascade_rows_per_tile(int);
 int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, const float*, const void*, const int*,
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
@@ -277,11 +277,17 @@ void paged_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
 
 void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                           const at::Tensor& block_tables, const at::Tensor& ctx_lens, const at::Tensor& tiles,
-                          at::Tensor& out, int64_t Hq, double scale, const c10::optional<at::Tensor>& rope_cos,
-                          const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& positions) {
+                          const c10::optional<at::Tensor>& out, int64_t Hq, double scale,
+                          const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
+                          const c10::optional<at::Tensor>& positions, const c10::optional<at::Tensor>& out8,
+                          const c10::optional<at::Tensor>& mx) {
   // tiles: [max_tiles, 3] int32 super-tiles (row_start, nseq, prefix_blocks), nseq <= cascade_rows_per_tile(G);
   // the engine builds them on the host (rows must stay < B: the kernel trusts the table).
-  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out); CHECK_CONTIG(out);
+  // out8 + mx instead of out: e4m3 rows [B, Hq * D] with e8m0 scales [Hq, >= B, 4] (one per 32 dims of a head)
+  CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  const bool mxo = out8.has_value() && out8->defined();
+  TORCH_CHECK(mxo == (mx.has_value() && mx->defined()), "paged_decode_cascade: out8 and mx go together");
+  TORCH_CHECK(mxo || (out.has_value() && out->defined()), "paged_decode_cascade: out or out8 + mx");
   check_v_cache(v_cache, k_cache, "paged_decode_cascade");
   CHECK_DTYPE(block_tables, at::kInt); CHECK_DTYPE(ctx_lens, at::kInt); CHECK_DTYPE(tiles, at::kInt);
   CHECK_CONTIG(tiles); CHECK_CONTIG(block_tables); CHECK_CONTIG(ctx_lens);
@@ -289,12 +295,30 @@ void paged_decode_cascade(const at::Tensor& q, const at::Tensor& k_cache, const 
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode_cascade: q must be [B, >=Hq*D] rows");
   const int B = (int)q.size(0), D = (int)k_cache.size(3), Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
   TORCH_CHECK(block_tables.size(0) >= B && ctx_lens.numel() >= B, "paged_decode_cascade: batch tables too short");
-  TORCH_CHECK(out.numel() >= (int64_t)B * Hq * D, "paged_decode_cascade: out too small");
+  void* outp = nullptr;
+  void* o8 = nullptr;
+  void* mxp = nullptr;
+  int mx_rows = 0;
+  if (mxo) {
+    CHECK_GPU(*out8); CHECK_CONTIG(*out8); CHECK_GPU(*mx); CHECK_CONTIG(*mx); CHECK_DTYPE(*mx, at::kByte);
+    TORCH_CHECK(out8->scalar_type() == at::kFloat8_e4m3fn && out8->numel() >= (int64_t)B * Hq * D,
+                "paged_decode_cascade: out8 must be e4m3 [B, Hq * D]");
+    TORCH_CHECK(mx->dim() == 3 && mx->size(0) == Hq && mx->size(1) >= B && mx->size(2) == 4 && D == 128,
+                "paged_decode_cascade: mx must be [Hq, B, 4] (head_dim 128)");
+    o8 = out8->data_ptr();
+    mxp = mx->data_ptr();
+    mx_rows = (int)mx->size(1);
+  } else {
+    CHECK_BF16(*out); CHECK_CONTIG(*out);
+    TORCH_CHECK(out->numel() >= (int64_t)B * Hq * D, "paged_decode_cascade: out too small");
+    outp = out->data_ptr();
+  }
   const QRope qr = q_rope(rope_cos, rope_sin, positions, B, D, "paged_decode_cascade");
   CHECK_RC(lwc_paged_decode_cascade(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                     block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), tiles.data_ptr<int>(),
-                                    (int)tiles.size(0), out.data_ptr(), (int)Hq, Hkv, D, BS,
-                                    (int)block_tables.size(1), (float)scale, qr.cos, qr.sin, qr.pos, cur_stream()),
+                                    (int)tiles.size(0), outp, (int)Hq, Hkv, D, BS,
+                                    (int)block_tables.size(1), (float)scale, qr.cos, qr.sin, qr.pos, o8, mxp, mx_rows,
+                                    cur_stream()),
            "paged_decode_cascade");
 }
 

@@ -103,6 +103,22 @@ LWC_DEVICE float row_sum4(float v) {
 // size).  Built straight from kernel arguments / tile indices, the compiler sometimes cannot prove the
 // resource uniform and wraps EVERY buffer access through it in a readfirstlane "waterfall" loop (~10
 // instructions and a branch per access, inside GEMM main loops too).
+// e8m0 exponent of an MX block with max |x| = amax: the smallest e with amax * 2^-e <= 448 (e4m3's largest
+// finite), from amax's own exponent and mantissa (448 = 0.875 * 2^9), so no rounding pushes a value past 448
+LWC_DEVICE int mx_exp(float amax) {
+  const int ea = __builtin_amdgcn_frexp_expf(amax);
+  const float m = __builtin_amdgcn_frexp_mantf(amax);
+  return min(127, max(-127, ea - 9 + (m > 0.875f ? 1 : 0)));
+}
+
+// max over each 16-lane DPP row (quad xor 1, quad xor 2, half-row mirror, row mirror)
+LWC_DEVICE float row16_max(float x) {
+  x = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false)));
+  x = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false)));
+  x = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false)));
+  return fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, false)));
+}
+
 LWC_DEVICE __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
   const uint64_t a = (uint64_t)base;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);

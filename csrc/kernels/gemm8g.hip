@@ -80,14 +80,6 @@ LWC_DEVICE float quad_max(float x) {
   return fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false)));  // ^2
 }
 
-// e8m0 exponent of a block with max |x| = amax: the smallest e with amax * 2^-e <= 448 (e4m3's largest finite),
-// from amax's own exponent and mantissa (448 = 0.875 * 2^9), so no rounding can push a value past 448
-LWC_DEVICE int mx_exp(float amax) {
-  const int ea = __builtin_amdgcn_frexp_expf(amax);
-  const float m = __builtin_amdgcn_frexp_mantf(amax);
-  return min(127, max(-127, ea - 9 + (m > 0.875f ? 1 : 0)));
-}
-
 LWC_DEVICE float4v mfma8(const uint4v& a0, const uint4v& a1, const uint4v& b0, const uint4v& b1, const float4v& c) {
   const v8i32 av = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
   const v8i32 bv = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};

@@ -226,7 +226,7 @@ class LlamaModel:
                 gemm_plan.linear_add_(self._act(h, L), L.w_down, x_res, ws=self.g8_ws)
                 h = ops.rmsnorm(x_res, nxt, cfg.rms_eps)
             elif qn:
-                o = self._attn_out(attn.view(T, Hq * D), L)
+                o = self._attn_out(attn if isinstance(attn, ops.MXAct) else attn.view(T, Hq * D), L)
                 h = ops.rmsnorm_quant_fp8(o, L.mlp_norm, cfg.rms_eps, residual=x_res, keep_bf16=self._mlp_reads_bf16)
                 down = self._mlp(h, L)
                 if li + 1 < len(self.layers):
@@ -242,6 +242,13 @@ class LlamaModel:
 
     # whether _mlp reads the bf16 rows of its (fp8-quantised) input too (the MoE router does)
     _mlp_reads_bf16 = False
+
+    def _attn_mx(self) -> bool:
+        """Whether the decode attention hands the o projection an MX activation: fp8 o weights on gemm8g
+        (head_dim 128, every head one 128-wide K slice); LWC_ATTN_MX=0 keeps bf16 + the row quantisation."""
+        L = self.layers[0]
+        return (os.environ.get("LWC_ATTN_MX", "1") != "0" and isinstance(L.wo, ops.Fp8Weight)
+                and self.cfg.head_dim == 128 and ops.FP8_GEMM != "blas" and L.wo.q.shape[0] % 8 == 0)
 
     @property
     def _dense_residual(self) -> bool:
@@ -323,9 +330,12 @@ class LlamaModel:
         q_at_load = os.environ.get("LWC_DECODE_QROPE", "1") != "0"
         rope = (self.cos, self.sin, positions) if q_at_load else None
         if cascade_tiles is not None:
+            # fp8 o projection (config 5): the attention output leaves the kernel in MX form (ops.MXAct)
+            mx = self._attn_mx()
+
             def attn_fn(qkv, li):
                 return ops.paged_decode_cascade(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cascade_tiles,
-                                                cfg.heads, self.scale, rope=rope)
+                                                cfg.heads, self.scale, rope=rope, mx=mx)
         else:
             part_o = part_lse = None
             if num_splits > 1:

@@ -174,21 +174,39 @@ def cascade_rows_per_tile(G: int) -> int:
     return int(kernels().cascade_rows_per_tile(int(G)))
 
 
+class MXAct:
+    """An activation in MX form for a block-scaled fp8 GEMM: e4m3 rows ``q`` [M, K] and e8m0 scales ``mx``
+    [K/128, M, 4] (one per 32 consecutive values; value = q * 2^(mx - 127)); :func:`linear_fp8` takes it."""
+
+    __slots__ = ("q", "mx")
+
+    def __init__(self, q: torch.Tensor, mx: torch.Tensor):
+        self.q, self.mx = q, mx
+
+
 def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                          ctx_lens: torch.Tensor, tiles: torch.Tensor, Hq: int, scale: float,
                          out: Optional[torch.Tensor] = None,
-                         rope: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+                         rope: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None, mx: bool = False):
     """Cascade decode attention in ONE launch (K3c): per super-tile (row_start, nseq, prefix_blocks) the
     tile's sequences read their shared first `prefix_blocks` blocks once through LDS, then each
     sequence's own blocks; softmax states merge in registers.  Every row < B must be covered by
-    exactly one tile (prefix_blocks = 0 for sequences that share nothing)."""
+    exactly one tile (prefix_blocks = 0 for sequences that share nothing).  ``mx=True`` (head_dim 128): the
+    output leaves the kernel as an :class:`MXAct` [B, Hq*D] for an fp8 o projection — no bf16 rows, no
+    separate quantisation pass."""
     B = q.shape[0]
     D = k_cache.shape[-1]
+    rc, rs, rp = rope if rope is not None else (None, None, None)
+    if mx:
+        q8 = torch.empty(B, Hq * D, dtype=torch.float8_e4m3fn, device=q.device)
+        sc = torch.empty(Hq * D // 128, B, 4, dtype=torch.uint8, device=q.device)
+        kernels().paged_decode_cascade(q, k_cache, v_cache, block_tables, ctx_lens, tiles, None, int(Hq), float(scale),
+                                       rc, rs, rp, q8, sc)
+        return MXAct(q8, sc)
     if out is None:
         out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
-    rc, rs, rp = rope if rope is not None else (None, None, None)
     kernels().paged_decode_cascade(q, k_cache, v_cache, block_tables, ctx_lens, tiles, out, int(Hq), float(scale),
-                                   rc, rs, rp)
+                                   rc, rs, rp, None, None)
     return out
 
 
@@ -647,6 +665,8 @@ def linear_fp8_mx(aq: torch.Tensor, amx: torch.Tensor, w: Fp8Weight) -> torch.Te
 def linear_fp8(x, w: Fp8Weight) -> torch.Tensor:
     """bf16 x [M, K] -> per-row e4m3 quantisation (K11e) -> fp8 GEMM -> bf16 [M, N].  A :class:`QAct`
     (quantised by the producing norm) goes straight to the GEMM."""
+    if isinstance(x, MXAct):
+        return linear_fp8_mx(x.q, x.mx, w)
     if isinstance(x, QAct):
         return linear_fp8_q(x.q, x.s, w)
     xq, xs = quant_fp8_rows(x)

@@ -231,6 +231,16 @@ def test_paged_decode_cascade(gpu, G, rope):
         o = ref.attention(_q_ref(q_full, b, Hq, D, rp), kc[blk, :, toks % BS, :], ops.v_gather(vc, blk, toks % BS),
                           False, 1 / math.sqrt(D))[0]
         _close(out[b], o, 2e-2, 2e-2)
+    # MX output (the fp8 o projection's operand): e4m3 rows + one e8m0 scale per 32 dims of a head, from the
+    # same softmax state — dequantised, within e4m3 rounding of the bf16 output; every block's scale tight
+    a = ops.paged_decode_cascade(q_full, kc, vc, bt, ctx, tiles, Hq, 1 / math.sqrt(D), rope=rp, mx=True)
+    assert a.q.shape == (B, Hq * D) and a.mx.shape == (Hq * D // 128, B, 4)
+    dims = torch.arange(Hq * D, device=gpu)
+    deq = a.q.float() * torch.exp2(a.mx.float() - 127.0)[dims // 128, :, (dims % 128) // 32].t()
+    want = out.float().reshape(B, -1)
+    assert ((deq - want).norm() / want.norm()).item() < 4e-2
+    bmax = a.q.float().abs().view(B, -1, 32).amax(-1)
+    assert (bmax[bmax > 0] >= 224).all()
 
 
 def test_paged_decode_cascade_short_tile_q_at_allocation_end(gpu):
