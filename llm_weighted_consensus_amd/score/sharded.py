@@ -26,13 +26,14 @@ them failed).  A dead rank gets no share of later requests: they run on the surv
 
 /consensus/completions: candidates [first, first + n) of a request are sampled by the rank owning that slice
 (each with the seed it has in the whole request) and embedded on its GPU; the unit rows travel back over the
-link.  The slice of a follower that dies (or times out) is recomputed by the leader — same seeds, same
+link.  The slice of a follower that dies, times out or fails is recomputed by the leader — same seeds, same
 candidates — so the request still completes.
 """
 from __future__ import annotations
 
 import asyncio
 import copy
+import logging
 import os
 import threading
 import time
@@ -46,6 +47,7 @@ from ..schema import chat as C
 from ..schema import score as S
 from .orchestrator import ChoiceIndexer, ScoreClient
 
+_log = logging.getLogger(__name__)
 _NATIVE = 1 << 12  # a follower tags choice (voter v, native index k) as C + v * _NATIVE + k
 
 
@@ -206,6 +208,7 @@ class ShardedScoreClient(ScoreClient):
         llms = {l.index: l for l in model.llms}
         seen: Dict[int, Dict[int, bool]] = {i: {} for idx in shares.values() for i in idx}  # voter -> native -> done
         pending = set(shares)
+        unfinished: set = set()  # ranks whose share was given up (timed out / ended by us): told to cancel
         deadline = time.monotonic() + _bound(ctx)
         try:
             while pending:
@@ -215,6 +218,8 @@ class ShardedScoreClient(ScoreClient):
                     msg = ("timeout", None)
                 kind, rank = msg[0], msg[1]
                 if kind == "chunk":
+                    if rank not in pending:  # a share already closed (lost / timed out): its voters are final
+                        continue
                     chunk = S.ScoreCompletionChunk.model_validate(msg[2])
                     base_c = int(msg[3])
                     for ch in chunk.choices:
@@ -225,6 +230,8 @@ class ShardedScoreClient(ScoreClient):
                         done[native] = done.get(native, False) or ch.finish_reason is not None
                     yield chunk
                 elif kind == "end":
+                    if rank not in pending:
+                        continue
                     pending.discard(rank)
                     err = msg[2] if len(msg) > 2 else None
                     if err:
@@ -237,15 +244,17 @@ class ShardedScoreClient(ScoreClient):
                         if r not in pending:
                             continue
                         pending.discard(r)
+                        if kind == "timeout":
+                            unfinished.add(r)  # still alive: its voters must stop using its GPU
                         why = "follower died" if kind == "dead" else "share timed out"
                         for c in self._lost_chunks(rid, created, model.id, indexer, llms, weights, shares[r], seen,
                                                    _lost(r, why)):
                             yield c
         finally:
             self.hub.close(ctx["seq"])
-            if pending:  # the request was abandoned: tell the followers to drop the rest of its voters
-                for r in pending:
-                    self.link.send(r, ("cancel", ctx["seq"]))
+            # abandoned (pending) or given-up (timed-out) shares: tell those followers to drop their voters
+            for r in sorted(pending | unfinished):
+                self.link.send(r, ("cancel", ctx["seq"]))
 
     @staticmethod
     def _lost_chunks(rid, created, model_id, indexer, llms, weights, voters, seen, err: StatusError):
@@ -324,10 +333,11 @@ class ShardedConsensusClient:
                 share.ranks.discard(r)
         local = [(f, c) for r, f, c in slices if (r == 0 or (r not in remote)) and c]
         parts: Dict[int, tuple] = {}  # first -> (comp, rows, ntok)
+        pending = dict(remote)
+        unfinished: set = set()
         try:
             for f, c in local:
                 parts[f] = await self._slice(ctx, request, embedding_model, f, c)
-            pending = dict(remote)
             deadline = time.monotonic() + _bound(ctx)
             while pending:
                 try:
@@ -338,21 +348,26 @@ class ShardedConsensusClient:
                 if kind == "cons" and rank in pending:
                     f, c = pending.pop(rank)
                     meta, raw = msg[2], msg[3]
-                    if not meta[0]:
-                        raise ScoreError(500, {"kind": "consensus_shard_failed",
-                                               "error": f"rank {rank} failed to generate or embed its candidates: "
-                                                        f"{meta[3]}"})
-                    rows = torch.from_numpy(np.frombuffer(raw, dtype=np.float32).reshape(meta[1], meta[2]).copy())
-                    parts[f] = (C.ChatCompletion.model_validate(meta[3]), rows, int(meta[4]))
+                    if meta[0]:
+                        rows = torch.from_numpy(np.frombuffer(raw, dtype=np.float32).reshape(meta[1], meta[2]).copy())
+                        parts[f] = (C.ChatCompletion.model_validate(meta[3]), rows, int(meta[4]))
+                    else:  # the follower failed (e.g. out of memory): isolate it like a lost one
+                        _log.warning("consensus slice [%d, %d) failed on rank %d (%s): recomputed here", f, f + c,
+                                     rank, meta[3])
+                        parts[f] = await self._slice(ctx, request, embedding_model, f, c)
                 elif kind in ("dead", "timeout"):
                     lost = [rank] if kind == "dead" else list(pending)
                     for r in lost:  # recompute the lost slice here: same seeds, same candidates
                         if r in pending:
                             f, c = pending.pop(r)
+                            if kind == "timeout":
+                                unfinished.add(r)
                             parts[f] = await self._slice(ctx, request, embedding_model, f, c)
         finally:
             if share is not None:
                 self.sc.hub.close(seq)
+            for r in sorted(set(pending) | unfinished):  # abandoned or given up: free the follower's GPU
+                self.sc.link.send(r, ("cancel", seq))
         order = sorted(parts)
         merged = parts[order[0]][0]
         for f in order[1:]:
@@ -371,16 +386,6 @@ class ShardedConsensusClient:
         if self.base.archive is not None:
             self.base.archive.store_score(out)
         return out
-
-
-class ConsensusLeader:
-    """Rank 0's /consensus/completions client (the app calls ``create_unary``)."""
-
-    def __init__(self, client: ShardedConsensusClient):
-        self.client = client
-
-    async def create_unary(self, ctx, request, embedding_model: str, tau: float = 0.05) -> S.ScoreCompletion:
-        return await self.client.create_unary(ctx, request, embedding_model, tau)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -411,12 +416,18 @@ class ShardWorker:
                 if not self.link.send(("chunk", seq, chunk.to_obj(), C_len)):
                     raise ConnectionError("leader link lost")
 
+        tasks = [asyncio.ensure_future(one(v)) for v in p["llms"]]
         try:
-            await asyncio.gather(*(one(v) for v in p["llms"]))
+            for t in asyncio.as_completed(tasks):
+                await t  # the first failure ends the share: the leader isolates all of its voters at once
         except asyncio.CancelledError:
             err = "cancelled"
         except BaseException as e:  # noqa: BLE001 — reported to the leader, which isolates these voters
             err = f"{type(e).__name__}: {e}"
+        finally:
+            for t in tasks:  # no sibling keeps streaming after the share ended
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
         self.link.send(("end", seq, err))
 
     async def _consensus_slice(self, seq: int, p: dict) -> None:
@@ -470,8 +481,3 @@ class ShardWorker:
         n = asyncio.run(main())
         self.link.close()
         return n
-
-
-def follow(worker: ShardWorker) -> int:
-    """Ranks > 0: serve the leader's work until it stops; returns the number of pieces of work run."""
-    return worker.serve()

@@ -122,11 +122,11 @@ def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     """LWC_SHARD_VOTERS: the voter-sharded deployment (a collective at bring-up: every rank).  The ranks open
     their leader <-> follower links (parallel/shard_link.py); rank 0 swaps its score and consensus clients
     for the sharded leader ones and returns its score client (serve it), the other ranks return the
-    ShardWorker to ``follow``."""
+    ShardWorker to ``serve()``."""
     import torch.distributed as dist
 
     from ..parallel.shard_link import open_links
-    from ..score.sharded import ConsensusLeader, ShardedConsensusClient, ShardedScoreClient, ShardWorker
+    from ..score.sharded import ShardedConsensusClient, ShardedScoreClient, ShardWorker
 
     group = group if group is not None else dist.new_group(backend="gloo")
     link = open_links(group)
@@ -140,7 +140,7 @@ def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     state.multichat.score = client
     if state.consensus is not None:
         client.consensus = ShardedConsensusClient(state.consensus, client)
-        state.consensus = ConsensusLeader(client.consensus)
+        state.consensus = client.consensus
     return client
 
 
@@ -150,15 +150,13 @@ def main(argv: Optional[list] = None) -> None:
     cfg = Config.from_env()
     if cfg.shard_voters:
         from ..parallel import dist as pdist
-        from ..score.sharded import follow
-
         info = pdist.init_from_env("cuda" if cfg.device != "cpu" else "cpu")
         cfg.gpu = info.local_rank
         follower_config(cfg, info.rank)
         state = build_state(cfg)
         lead = shard_voters(state)
         if info.rank != 0:
-            follow(lead)
+            lead.serve()
             pdist.shutdown()
             return
         try:

@@ -30,7 +30,6 @@ def _rank(rank, port, q):
     import httpx
 
     from llm_weighted_consensus_amd.parallel import dist as pdist
-    from llm_weighted_consensus_amd.score.sharded import follow
     from llm_weighted_consensus_amd.server.app import create_app
     from llm_weighted_consensus_amd.server.config import Config
     from llm_weighted_consensus_amd.server.main import build_state, shard_voters
@@ -41,7 +40,7 @@ def _rank(rank, port, q):
                                    kv_fraction=0.04, gpu=info.local_rank))
         lead = shard_voters(state)
         if rank != 0:
-            q.put((rank, follow(lead)))
+            q.put((rank, lead.serve()))
         else:
             client = httpx.AsyncClient(transport=httpx.ASGITransport(app=create_app(state)), base_url="http://t",
                                        timeout=300)

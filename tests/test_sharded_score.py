@@ -89,7 +89,6 @@ def _leader_worker(rank, world, port, out_q, scenario):
     from llm_weighted_consensus_amd.parallel import dist as pdist
     from llm_weighted_consensus_amd.score.multichat import MultichatClient
     from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
-    from llm_weighted_consensus_amd.score.sharded import follow
     from llm_weighted_consensus_amd.server.app import AppState
     from llm_weighted_consensus_amd.server.main import shard_voters
 
@@ -111,7 +110,7 @@ def _leader_worker(rank, world, port, out_q, scenario):
     state = AppState(chat, score, MultichatClient(score, None))
     lead = shard_voters(state, rng_seed=7)
     if rank != 0:
-        res = follow(lead)
+        res = lead.serve()
         out_q.put((rank, res))
         pdist.shutdown()
         return

@@ -142,7 +142,6 @@ def _rank(rank, port, q):
 
     torch.set_num_threads(1)
     from llm_weighted_consensus_amd.parallel import dist as pdist
-    from llm_weighted_consensus_amd.score.sharded import follow
     from llm_weighted_consensus_amd.server.app import create_app
     from llm_weighted_consensus_amd.server.main import shard_voters
 
@@ -154,7 +153,7 @@ def _rank(rank, port, q):
             res = asyncio.run(_drive(create_app(state)))
             lead.close()
         else:
-            res = follow(lead)
+            res = lead.serve()
         q.put((rank, res))
     except BaseException as e:  # noqa: BLE001
         import traceback
