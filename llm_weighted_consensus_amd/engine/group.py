@@ -17,6 +17,14 @@ sequences to surviving GPUs").
 * Failure handling: a worker that exits or stops heart-beating is marked dead; each of its request
   portions that has not emitted a token yet is resubmitted to a surviving worker, the others fail
   with `EngineFailure` (the client turns that into an error choice / AllVotesFailed).
+* Recovery: a dead worker (a whole TP replica: every rank) is torn down and a replacement is spawned as a
+  FRESH child process of the front end (never a re-exec of a process that touched the GPU), with
+  exponential backoff between attempts (``respawn_backoff_s`` doubling to 30 s, at most ``max_respawns``
+  per worker).  It rebuilds its engine, says ready, and the router gives it requests again, so the node
+  regains the capacity a fault took (the reference never loses capacity for good: it retries its attempt
+  list until ``max_elapsed``, src/chat/completions/client.rs:263-305, src/main.rs:104-121).  Every worker
+  message carries its process generation, so a late message of the dead process is never taken for its
+  replacement's.
 """
 from __future__ import annotations
 
@@ -123,6 +131,17 @@ def _apply(engine, msg, groups: Dict[int, Any], cb_for, emb_req, on_error) -> No
             engine.abort(g)
 
 
+class _Tagged:
+    """A worker's view of the front end's event queue: every message carries the worker's process generation
+    (the front end drops messages of a generation it has already replaced)."""
+
+    def __init__(self, q, gen: int):
+        self.q, self.gen = q, gen
+
+    def put(self, msg) -> None:
+        self.q.put(tuple(msg) + (self.gen,))
+
+
 def _push(ring, record: bytes, ev_q, fallback, hb, stop) -> None:
     """One record into the worker's ring: waits (heart-beating) while the ring is full — the front end's
     reader drains it — and never re-sends through the pickled queue unless there is no ring at all."""
@@ -139,7 +158,7 @@ def _push(ring, record: bytes, ev_q, fallback, hb, stop) -> None:
 
 
 def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_name: Optional[str] = None,
-                mirror_out: Optional[list] = None, mirror_in=None) -> None:
+                mirror_out: Optional[list] = None, mirror_in=None, gen: int = 0) -> None:
     """Worker process: build the engine, serve requests until told to stop.
 
     Tensor-parallel replicas (spec ``tp`` > 1): the replica's rank 0 (the leader) is the worker the front end
@@ -147,6 +166,7 @@ def worker_main(wid: int, spec: dict, factory: str, req_q, ev_q, hb, stop, ring_
     — and whether it steps to its followers (``mirror_out`` queues), which apply the same messages and step in
     lockstep (``mirror_in``), so every rank schedules the same batch and the all-reduce inside each forward
     pairs up.  Only the leader streams tokens and embeds candidates."""
+    ev_q = _Tagged(ev_q, gen)
     if mirror_in is not None:
         return _follower_main(wid, spec, factory, ev_q, hb, stop, mirror_in)
     ring = ShmRing(ring_name, create=False) if ring_name else None
@@ -281,9 +301,12 @@ class _EngineFacade:
 class EngineGroup:
     def __init__(self, spec: dict, devices: List[int], factory: str = "llm_weighted_consensus_amd.engine.group:build_engine",
                  tokenizer=None, cfg=None, max_model_len: int = 4096, heartbeat_timeout: float = 30.0,
-                 start_timeout: float = 600.0, ring_bytes: int = 32 << 20):
+                 start_timeout: float = 600.0, ring_bytes: int = 32 << 20, respawn: bool = True,
+                 max_respawns: int = 8, respawn_backoff_s: float = 0.5):
         self.spec, self.factory = spec, factory
         self.heartbeat_timeout = heartbeat_timeout
+        self.ring_bytes = ring_bytes
+        self.respawn, self.max_respawns, self.respawn_backoff_s = respawn, max_respawns, respawn_backoff_s
         # tensor-parallel replicas: spec "tp" = T groups the listed GPUs in runs of T (LWC_GPUS=0,...,7 with
         # tp 2 = four TP=2 replicas); a worker index below names a replica, served by its rank-0 process
         tp = int(spec.get("tp", 1) or 1)
@@ -293,51 +316,33 @@ class EngineGroup:
         self.tp = tp
         self.replicas = [devices[i:i + tp] for i in range(0, len(devices), tp)]
         self.devices = [r[0] for r in self.replicas]
-        ctx = mp.get_context("spawn")
-        self.ev_q = ctx.Queue()
-        self.stop = ctx.Event()
-        self.req_qs, self.hbs, self.procs, self.rings = [], [], [], []
-        self.followers: List[List[tuple]] = []  # per replica: (process, heartbeat) of ranks 1..T-1
-        self.mirror_qs: List[list] = []
-        port0 = int(spec.get("tp_port", 0)) or _free_port_base(len(self.replicas))
-        for wid, devs in enumerate(self.replicas):
-            q = ctx.Queue()
-            hb = ctx.Value("d", time.time())
-            ring = ShmRing(cap=ring_bytes)
-            self.rings.append(ring)
-            wspec = dict(spec, device=devs[0])
-            mirrors, fl = [], []
-            if tp > 1:
-                shared = len(set(devs)) < len(devs)  # ranks sharing a GPU (one-GPU rehearsal) split its memory
-                wspec.update(tp=tp, tp_rank=0, tp_port=port0 + wid, tp_shared=shared)
-                for r in range(1, tp):
-                    mq = ctx.Queue()
-                    fhb = ctx.Value("d", time.time())
-                    fp = ctx.Process(target=worker_main,
-                                     args=(wid, dict(wspec, device=devs[r], tp_rank=r), factory, None, self.ev_q, fhb,
-                                           self.stop, None, None, mq),
-                                     daemon=True, name=f"lwc-worker-{wid}-tp{r}")
-                    fp.start()
-                    mirrors.append(mq)
-                    fl.append((fp, fhb))
-            p = ctx.Process(target=worker_main, args=(wid, wspec, factory, q, self.ev_q, hb, self.stop, ring.name,
-                                                      mirrors or None),
-                            daemon=True, name=f"lwc-worker-{wid}")
-            p.start()
-            self.req_qs.append(q)
-            self.hbs.append(hb)
-            self.procs.append(p)
-            self.followers.append(fl)
-            self.mirror_qs.append(mirrors)  # keep the queues alive: a started Process drops its args
-        self.alive = [True] * len(self.procs)
-        self.ready = [False] * len(self.procs)
-        self.load_of = [0] * len(self.procs)
+        self._mp = mp.get_context("spawn")
+        self.ev_q = self._mp.Queue()
+        self.stop = self._mp.Event()
+        n = len(self.replicas)
+        self.req_qs: List[Any] = [None] * n
+        self.hbs: List[Any] = [None] * n
+        self.procs: List[Any] = [None] * n
+        self.rings: List[Any] = [None] * n
+        self.retired: List[Any] = []  # rings and processes of replaced workers (closed / joined at close())
+        self.followers: List[List[tuple]] = [[] for _ in range(n)]  # per replica: (process, hb) of ranks 1..T-1
+        self.mirror_qs: List[list] = [[] for _ in range(n)]
+        self.gen = [0] * n          # process generation of each worker slot
+        self.respawns = [0] * n     # replacements started per slot
+        self.respawning = [False] * n
+        self._port0 = int(spec.get("tp_port", 0)) or (_free_port_base(n) if tp > 1 else 0)
+        self.alive = [True] * n
+        self.ready = [False] * n
+        self.load_of = [0] * n
         self.requests: Dict[int, GroupRequest] = {}
         self.emb_pending: Dict[int, GroupRequest] = {}  # finished generating, embeddings still on the way
         self._rid = itertools.count(1)
         self._lock = threading.Lock()
+        self._life = threading.RLock()  # deaths and replacements of worker slots
         self.failures = 0
         self.engine = _EngineFacade(tokenizer, cfg, max_model_len)
+        for wid in range(n):
+            self._spawn(wid, self._port0 + wid if tp > 1 else 0)
         self._reader = threading.Thread(target=self._read, name="lwc-group-reader", daemon=True)
         self._reader.start()
         deadline = time.time() + start_timeout
@@ -348,6 +353,38 @@ class EngineGroup:
             time.sleep(0.05)
         if not any(self.alive):
             raise RuntimeError("EngineGroup: every worker failed to start")
+
+    def _spawn(self, wid: int, port: int) -> None:
+        """Start worker slot ``wid``'s processes (a TP replica: its leader and followers) at generation
+        ``self.gen[wid]``: new request queue, heartbeat values and ring — nothing is shared with a previous
+        generation."""
+        ctx, devs, gen = self._mp, self.replicas[wid], self.gen[wid]
+        q = ctx.Queue()
+        hb = ctx.Value("d", time.time())
+        ring = ShmRing(cap=self.ring_bytes)
+        wspec = dict(self.spec, device=devs[0])
+        mirrors, fl = [], []
+        if self.tp > 1:
+            shared = len(set(devs)) < len(devs)  # ranks sharing a GPU (one-GPU rehearsal) split its memory
+            wspec.update(tp=self.tp, tp_rank=0, tp_port=port, tp_shared=shared)
+            for r in range(1, self.tp):
+                mq = ctx.Queue()
+                fhb = ctx.Value("d", time.time())
+                fp = ctx.Process(target=worker_main,
+                                 args=(wid, dict(wspec, device=devs[r], tp_rank=r), self.factory, None, self.ev_q, fhb,
+                                       self.stop, None, None, mq, gen),
+                                 daemon=True, name=f"lwc-worker-{wid}-tp{r}-g{gen}")
+                fp.start()
+                mirrors.append(mq)
+                fl.append((fp, fhb))
+        p = ctx.Process(target=worker_main, args=(wid, wspec, self.factory, q, self.ev_q, hb, self.stop, ring.name,
+                                                  mirrors or None, None, gen),
+                        daemon=True, name=f"lwc-worker-{wid}-g{gen}")
+        p.start()
+        self.req_qs[wid], self.hbs[wid], self.procs[wid] = q, hb, p
+        self.rings[wid] = ring
+        self.followers[wid] = fl
+        self.mirror_qs[wid] = mirrors  # keep the queues alive: a started Process drops its args
 
     # ------------------------------------------------------------------ EngineService API
     @property
@@ -401,16 +438,20 @@ class EngineGroup:
 
     def close(self) -> None:
         self.stop.set()
-        for p in self.procs + [fp for fl in self.followers for fp, _ in fl]:
+        with self._life:
+            procs = self.procs + [fp for fl in self.followers for fp, _ in fl] + \
+                [x for x in self.retired if not isinstance(x, ShmRing)]
+        for p in procs:
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
         self._reader.join(timeout=5)
         if self._reader.is_alive():  # still inside a pop: leave the segments to process exit, never
             return                   # unmap them under a running reader
-        for r in self.rings:
+        for r in self.rings + [x for x in self.retired if isinstance(x, ShmRing)]:
             r.close()
         self.rings = []
+        self.retired = []
 
     # ------------------------------------------------------------------ reader / health
     def _deliver(self, req: GroupRequest, item) -> None:
@@ -420,8 +461,8 @@ class EngineGroup:
         last_health = time.monotonic()
         while not self.stop.is_set():
             busy = False
-            for wid, ring in enumerate(self.rings):
-                while True:
+            for wid, ring in enumerate(list(self.rings)):
+                while self.rings[wid] is ring:  # a replaced worker's ring is dropped, not read on
                     rec = ring.pop()
                     if rec is None:
                         break
@@ -432,7 +473,7 @@ class EngineGroup:
                     else:  # a worker's embedding rows, in the ring after its candidates' last tokens
                         self._on_embeddings("emb", payload)
             try:
-                kind, wid, payload = self.ev_q.get_nowait()
+                kind, wid, payload, gen = self.ev_q.get_nowait()
             except pyqueue.Empty:
                 if not busy:
                     time.sleep(0.0003)
@@ -442,14 +483,17 @@ class EngineGroup:
                 continue
             except (EOFError, OSError):
                 return
+            if gen != self.gen[wid]:
+                continue  # a replaced process's last words: its requests were already failed / moved
             if kind == "ready":
                 self.ready[wid] = True
             elif kind == "fatal":
                 if self.ready[wid] and self.alive[wid]:  # a TP follower lost step with its leader
                     self._worker_died(wid, str(payload))
-                else:
+                else:  # failed to start: try again later (bounded by max_respawns)
                     self.alive[wid] = False
                     self.failures += 1
+                    self._schedule_respawn(wid, f"failed to start: {payload}")
             elif kind == "error":
                 rid, msg = payload[:2]
                 fkind = payload[2] if len(payload) > 2 else "error"
@@ -514,18 +558,63 @@ class EngineGroup:
 
     def _check_health(self) -> None:
         now = time.time()
-        for w, p in enumerate(self.procs):
-            if not self.alive[w]:
-                continue
-            members = [(p, self.hbs[w])] + self.followers[w]
-            for q, hb in members:
-                stale = self.ready[w] and now - hb.value > self.heartbeat_timeout
-                if not q.is_alive() or stale:
-                    self._worker_died(w, "exited" if not q.is_alive() else "heartbeat timeout")
-                    break
+        with self._life:
+            for w, p in enumerate(self.procs):
+                if not self.alive[w] or p is None:
+                    continue
+                members = [(p, self.hbs[w])] + self.followers[w]
+                for q, hb in members:
+                    stale = self.ready[w] and now - hb.value > self.heartbeat_timeout
+                    if not q.is_alive() or stale:
+                        self._worker_died(w, "exited" if not q.is_alive() else "heartbeat timeout")
+                        break
+
+    def _schedule_respawn(self, w: int, why: str) -> None:
+        with self._life:
+            if not self.respawn or self.stop.is_set() or self.respawning[w] or self.respawns[w] >= self.max_respawns:
+                return
+            self.respawning[w] = True
+            delay = min(30.0, self.respawn_backoff_s * (2 ** self.respawns[w]))
+            self.respawns[w] += 1
+        threading.Thread(target=self._respawn, args=(w, delay, why), name=f"lwc-respawn-{w}", daemon=True).start()
+
+    def _respawn(self, w: int, delay: float, why: str) -> None:
+        """Replace worker slot ``w`` (after ``delay``): tear down every process of the old generation, then
+        spawn fresh ones; the slot serves again once its new engine says ready."""
+        if self.stop.wait(delay):
+            return
+        with self._life:
+            old = [self.procs[w]] + [fp for fp, _ in self.followers[w]]
+        for p in old:  # a TP replica is one unit: no rank of the old generation may outlive it
+            if p is not None and p.is_alive():
+                p.kill()
+            if p is not None:
+                p.join(timeout=10)
+        with self._life:
+            if self.stop.is_set():
+                self.respawning[w] = False
+                return
+            self.retired += [r for r in (self.rings[w],) if r is not None] + [p for p in old if p is not None]
+            self.gen[w] += 1
+            self.ready[w] = False
+            port = _free_port_base(1) if self.tp > 1 else 0  # the old rendezvous port may linger
+            try:
+                self._spawn(w, port)
+            except Exception as e:  # noqa: BLE001 - e.g. no shared memory left: try again later
+                traceback.print_exc()
+                self.respawning[w] = False
+                self._schedule_respawn(w, f"respawn failed: {e}")
+                return
+            self.alive[w] = True
+            self.respawning[w] = False
+        print(f"[EngineGroup] worker {w} ({why}) replaced: generation {self.gen[w]}", flush=True)
 
     def _worker_died(self, w: int, why: str) -> None:
-        self.alive[w] = False
+        with self._life:
+            if not self.alive[w]:
+                return
+            self.alive[w] = False
+            self.ready[w] = False
         self.failures += 1
         self.load_of[w] = 0
         for fp, _ in self.followers[w]:  # a TP replica is one unit: its other ranks cannot go on alone
@@ -550,11 +639,16 @@ class EngineGroup:
                         self.req_qs[t].put(("submit", rid, req.prompt_ids, p.params, p.n, p.offset, req.embed))
                     else:
                         self.requests.pop(rid, None)
+                        for q in req.portions:  # the survivors' portions of a failed request stop too
+                            if q.worker != w and self.alive[q.worker]:
+                                self.req_qs[q.worker].put(("abort", rid))
+                                self.load_of[q.worker] -= q.n - q.finished
                         self._deliver(req, EngineFailure(f"engine worker {w} {why}"))
                         if req.emb_future is not None:
                             req.loop.call_soon_threadsafe(_set_future, req.emb_future, None,
                                                           RuntimeError(f"engine worker {w} {why}"))
                         break
+        self._schedule_respawn(w, why)
 
 
 def _free_port_base(n: int) -> int:

@@ -42,6 +42,10 @@ variables configure the local engine:
   LWC_SHARD_DEAD_S  silence after which a follower counts as dead (default 10 s; a closed socket — a
                     follower process that exited — counts at once): its unfinished voters become error
                     choices and later requests run on the survivors
+  LWC_SHARD_LINK_HOST  interface the leader's link listener binds (default loopback: one node)
+  LWC_SHARD_LINK_FILE  the leader writes its link address + secret here (mode 0600); a follower restarted
+                    outside the bring-up group (LWC_SHARD_REJOIN_RANK=<rank>) authenticates with it and is
+                    re-admitted: live ranks return to full size and later requests give it voters again
   LWC_SHARD_WAIT_S  bound on a request's wait for its followers when it carries no deadline (default 300 s;
                     with a deadline: the deadline plus LWC_SHARD_GRACE_S, default 5 s)
   LWC_GPU_TALLY     N >= 1: tallies of score requests finishing in the same event-loop turn are batched,
@@ -49,6 +53,9 @@ variables configure the local engine:
                     (launched and read back on a worker thread); default 2 when this process runs an
                     engine on its GPU (measured +10.8 % req/s, profiles/serve_load.md), else off; 0: the
                     host C++ tally per request
+  LWC_RESPAWN       1 (default): an EngineGroup worker (or a whole TP replica) that dies is replaced by a fresh
+                    child process with exponential backoff (LWC_RESPAWN_BACKOFF_S, default 0.5 s, doubling to
+                    30 s), at most LWC_MAX_RESPAWNS times per worker (default 8); 0: a dead worker stays dead
 """
 from __future__ import annotations
 
@@ -106,6 +113,9 @@ class Config:
     kv_reserve_tokens: Optional[int] = 256
     request_timeout_ms: Optional[int] = None
     gpu_tally: Optional[str] = None
+    respawn: bool = True
+    max_respawns: int = 8
+    respawn_backoff_s: float = 0.5
 
     @classmethod
     def from_env(cls, dotenv: bool = True) -> "Config":
@@ -145,6 +155,9 @@ class Config:
         c.fault = e.get("LWC_FAULT")
         c.shard_voters = e.get("LWC_SHARD_VOTERS", "0") == "1"
         c.gpu_tally = e.get("LWC_GPU_TALLY")
+        c.respawn = e.get("LWC_RESPAWN", "1") == "1"
+        c.max_respawns = int(e.get("LWC_MAX_RESPAWNS", "8"))
+        c.respawn_backoff_s = float(e.get("LWC_RESPAWN_BACKOFF_S", "0.5"))
         if "LWC_KV_RESERVE_TOKENS" in e:
             v = e["LWC_KV_RESERVE_TOKENS"].strip().lower()
             c.kv_reserve_tokens = None if v in ("", "none", "max") else int(v)

@@ -6,6 +6,8 @@ Run one process per GPU (`LWC_GPU` / `LOCAL_RANK`) behind any HTTP load balancer
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 from ..archive.store import CompletionsArchive
@@ -53,7 +55,9 @@ def build_state(cfg: Config, chat_client=None) -> AppState:
                              kv_reserve_tokens=cfg.kv_reserve_tokens)
                 services[name] = EngineGroup(wspec, cfg.gpus, cfg=dcfg, max_model_len=mlen,
                                              tokenizer=load_tokenizer(spec, dcfg.vocab_size, dcfg.bos_token_id,
-                                                                      dcfg.eos_token_id))
+                                                                      dcfg.eos_token_id),
+                                             respawn=cfg.respawn, max_respawns=cfg.max_respawns,
+                                             respawn_backoff_s=cfg.respawn_backoff_s)
                 services[name].chat_template = spec.get("chat_template")
                 continue
             from ..engine.group import build_engine
@@ -144,10 +148,26 @@ def shard_voters(state: AppState, group=None, rng_seed: Optional[int] = None):
     return client
 
 
+def rejoin_follower(state: AppState, join_file: str, rank: int):
+    """A voter-sharded follower restarted outside the bring-up process group (a supervisor restarted a dead
+    rank): authenticate to the running leader from its join file (``LWC_SHARD_LINK_FILE``) and serve its
+    work again — the leader re-admits the rank and later requests give it voters (parallel/shard_link.py)."""
+    from ..parallel.shard_link import LinkClient
+    from ..score.sharded import ShardWorker
+
+    return ShardWorker(state.score, state.consensus, LinkClient.from_join_file(join_file, rank))
+
+
 def main(argv: Optional[list] = None) -> None:
     import uvicorn
 
     cfg = Config.from_env()
+    rejoin = os.environ.get("LWC_SHARD_REJOIN_RANK")
+    if cfg.shard_voters and rejoin:  # a restarted follower: no process group, straight back onto the links
+        cfg.gpu = int(os.environ.get("LWC_GPU", rejoin))
+        follower_config(cfg, int(rejoin))
+        rejoin_follower(build_state(cfg), os.environ["LWC_SHARD_LINK_FILE"], int(rejoin)).serve()
+        return
     if cfg.shard_voters:
         from ..parallel import dist as pdist
         info = pdist.init_from_env("cuda" if cfg.device != "cpu" else "cpu")

@@ -50,7 +50,7 @@ def test_group_splits_candidates_and_keeps_seeds():
 def test_group_worker_death_reschedules_or_fails():
     # death is detected from the process exit; a long heartbeat timeout keeps a loaded CI host from
     # declaring the SURVIVOR dead too
-    g = EngineGroup({"delay": 0.05}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60)
+    g = EngineGroup({"delay": 0.05}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60, respawn=False)
     try:
         sp = SamplingParams(max_tokens=50, seed=1)
         victim = g.procs[0]
@@ -121,7 +121,7 @@ def test_tp_replicas_step_in_lockstep(tmp_path):
     both ranks of a replica step the same batches (the per-step logs are identical), only the leaders
     stream, and a killed follower takes its whole replica down (requests go to the other one)."""
     g = EngineGroup({"delay": 0.01, "tp": 2, "log_dir": str(tmp_path)}, devices=[0, 0, 0, 0], factory=FACTORY,
-                    heartbeat_timeout=60)
+                    heartbeat_timeout=60, respawn=False)
     try:
         assert len(g.procs) == 2 and all(len(f) == 1 for f in g.followers)
         toks, err = _collect(g, 6, SamplingParams(max_tokens=5, seed=3))
@@ -141,5 +141,91 @@ def test_tp_replicas_step_in_lockstep(tmp_path):
         assert not g.procs[0].is_alive()  # the leader of the broken replica is taken down with it
         toks, err = _collect(g, 3, SamplingParams(max_tokens=3, seed=5))
         assert err is None and len(toks) == 3
+    finally:
+        g.close()
+
+
+def _wait_live(g, n, timeout=120):
+    deadline = time.time() + timeout
+    while len(g.live_workers()) < n and time.time() < deadline:
+        time.sleep(0.05)
+    return g.live_workers()
+
+
+def test_dead_worker_is_respawned_and_serves_again():
+    """Recovery: a worker killed mid-load is replaced by a fresh child process;
+    live_workers() returns to full size within a bounded time and the replacement takes later requests."""
+    g = EngineGroup({"delay": 0.02}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60, respawn_backoff_s=0.2)
+    try:
+        old_pid = g.procs[0].pid
+
+        async def go():
+            loop = asyncio.get_running_loop()
+            q = asyncio.Queue()
+            g.submit([1], SamplingParams(max_tokens=40, seed=1), 4, loop, q)
+            while True:  # mid-load: worker 0 is streaming
+                ev = await asyncio.wait_for(q.get(), 120)
+                if not isinstance(ev, EngineFailure) and ev.seq.index < 2:
+                    break
+            os.kill(old_pid, signal.SIGKILL)
+            while True:
+                ev = await asyncio.wait_for(q.get(), 120)
+                if isinstance(ev, EngineFailure):
+                    return ev
+
+        ev = asyncio.run(go())
+        assert "engine worker 0" in ev.message
+        t0 = time.time()
+        assert _wait_live(g, 2) == [0, 1]
+        assert time.time() - t0 < 60
+        assert g.procs[0].pid != old_pid and g.gen[0] == 1 and g.respawns[0] == 1
+        # the replacement serves: a request split over both workers completes with the usual seeds
+        sp = SamplingParams(max_tokens=3, seed=8)
+        toks, err = _collect(g, 6, sp)
+        assert err is None and sorted(toks) == list(range(6))
+        for i, t in toks.items():
+            assert t == [(8 * 1000003 + i + k) % 1000 for k in range(3)]
+        assert g.load == 0
+    finally:
+        g.close()
+
+
+def test_tp_replica_is_rebuilt_as_new_processes(tmp_path):
+    """A TP replica whose follower died is torn down as a unit and rebuilt (new leader + follower on a fresh
+    rendezvous port); both replicas serve afterwards."""
+    g = EngineGroup({"delay": 0.01, "tp": 2, "log_dir": str(tmp_path)}, devices=[0, 0, 0, 0], factory=FACTORY,
+                    heartbeat_timeout=60, respawn_backoff_s=0.2)
+    try:
+        old = (g.procs[0].pid, g.followers[0][0][0].pid)
+        os.kill(old[1], signal.SIGKILL)
+        deadline = time.time() + 60
+        while g.gen[0] == 0 and time.time() < deadline:
+            time.sleep(0.05)
+        assert _wait_live(g, 2) == [0, 1]
+        assert g.procs[0].pid not in old and g.followers[0][0][0].pid not in old
+        toks, err = _collect(g, 6, SamplingParams(max_tokens=4, seed=2))
+        assert err is None and sorted(toks) == list(range(6))
+    finally:
+        g.close()
+
+
+def test_respawn_is_bounded():
+    """A worker that keeps dying is replaced at most max_respawns times (with backoff), then stays dead."""
+    g = EngineGroup({"delay": 0.0}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60, respawn_backoff_s=0.05,
+                    max_respawns=2)
+    try:
+        for _ in range(3):
+            _wait_live(g, 2, timeout=60)
+            gen = g.gen[0]
+            os.kill(g.procs[0].pid, signal.SIGKILL)
+            deadline = time.time() + 60
+            while g.alive[0] and time.time() < deadline:
+                g._check_health()
+                time.sleep(0.05)
+            if g.respawns[0] < 2:
+                while g.gen[0] == gen and time.time() < deadline:
+                    time.sleep(0.05)
+        time.sleep(1.0)
+        assert g.respawns[0] == 2 and not g.alive[0] and g.live_workers() == [1]
     finally:
         g.close()

@@ -83,9 +83,11 @@ def _run(client, case, ctx=None):
         return {"error": e.code}
 
 
-def _leader_worker(rank, world, port, out_q, scenario):
+def _leader_worker(rank, world, port, out_q, scenario, join_file=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), LWC_SHARD_DEAD_S="3", LWC_SHARD_HB_S="0.2")
+    if join_file:
+        os.environ["LWC_SHARD_LINK_FILE"] = join_file
     from llm_weighted_consensus_amd.parallel import dist as pdist
     from llm_weighted_consensus_amd.score.multichat import MultichatClient
     from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
@@ -95,9 +97,9 @@ def _leader_worker(rank, world, port, out_q, scenario):
     pdist.init_from_env("cpu")
     policy = _policy
     delay = 0.0
-    if scenario == "kill":
-        delay = 0.03  # slow voters: requests are in flight when rank 3 dies
-        if rank == 3:
+    if scenario in ("kill", "rejoin"):
+        delay = 0.03  # slow voters: requests are in flight when the last rank dies
+        if rank == world - 1:
             seen = [0]
 
             def policy(req, _p=_policy):  # noqa: F811 — rank 3 dies while starting its 4th voter stream
@@ -122,8 +124,22 @@ def _leader_worker(rank, world, port, out_q, scenario):
         res = f"ERROR {type(e).__name__}: {e}\n{traceback.format_exc()}"
     lead.close()
     out_q.put((rank, res))
-    if scenario != "kill":
+    if scenario not in ("kill", "rejoin"):
         pdist.shutdown()
+
+
+def _rejoin_worker(rank, join_file, out_q):
+    """A restarted follower: no process group, back onto the links from the leader's join file."""
+    os.environ.update(LWC_SHARD_HB_S="0.2")
+    from llm_weighted_consensus_amd.score.multichat import MultichatClient
+    from llm_weighted_consensus_amd.score.orchestrator import ScoreClient
+    from llm_weighted_consensus_amd.server.app import AppState
+    from llm_weighted_consensus_amd.server.main import rejoin_follower
+
+    chat = FakeChatClient(_policy, delay_s=0.0)
+    score = ScoreClient(chat, rng_seed=7)
+    state = AppState(chat, score, MultichatClient(score, None))
+    out_q.put((rank, ("rejoined", rejoin_follower(state, join_file, rank).serve())))
 
 
 async def _equiv(client):
@@ -286,7 +302,24 @@ def test_killed_follower_isolated_as_error_choices():
     assert got[1] >= 4 and got[2] >= 4
 
 
-SCENARIOS = {"equiv": _equiv, "kill": _kill}
+async def _rejoin(client):
+    """In-flight requests while rank 2 dies; wait (bounded) for the restarted rank 2 to re-join; later
+    requests use it again and every voter of them finishes."""
+    import time
+
+    first = await _kill(client)
+    t0 = time.monotonic()
+    while client.link.live() != [1, 2] and time.monotonic() - t0 < 90:
+        await asyncio.sleep(0.1)
+    t_rejoin = time.monotonic() - t0
+    live = client.link.live()
+    later = [await client.create_unary(None, _kill_request()) for _ in range(3)]
+    return {"first_live": first["live"], "live": live, "t_rejoin": t_rejoin,
+            "later_errors": [sum(c.error is not None for c in o.choices) for o in later],
+            "later_n": [sum(c.index >= 3 for c in o.choices) for o in later]}
+
+
+SCENARIOS = {"equiv": _equiv, "kill": _kill, "rejoin": _rejoin}
 
 
 class _FakeLink:
@@ -323,3 +356,33 @@ def test_release_drops_a_share_whose_stream_never_ran():
         assert link.sent == [(1, ("cancel", 7))]
 
     asyncio.run(main())
+
+
+@pytest.mark.timeout(300)
+def test_restarted_follower_rejoins_and_serves(tmp_path):
+    """Recovery: a follower dies mid-load (its voters become error choices), a restarted
+    process re-joins the running leader through the join file, live() returns to full size and later
+    requests run voters on it again."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    join_file = str(tmp_path / "links.json")
+    procs = [ctx.Process(target=_leader_worker, args=(r, 3, port, q, "rejoin", join_file)) for r in range(3)]
+    for p in procs:
+        p.start()
+    procs[2].join(timeout=200)
+    assert procs[2].exitcode == 17  # died mid-load
+    back = ctx.Process(target=_rejoin_worker, args=(2, join_file, q))
+    back.start()
+    got = {}
+    for _ in range(3):  # leader, rank 1, the re-joined rank 2
+        r, v = q.get(timeout=200)
+        got[r] = v
+    for p in procs[:2] + [back]:
+        p.join(timeout=60)
+    g = got[0]
+    assert isinstance(g, dict), g
+    assert g["first_live"] == [1] and g["live"] == [1, 2]
+    assert g["t_rejoin"] < 60
+    assert g["later_errors"] == [0, 0, 0] and all(n == len(KILL_LLMS) for n in g["later_n"])
+    assert got[2][0] == "rejoined" and got[2][1] >= 3  # the replacement ran voters of every later request
