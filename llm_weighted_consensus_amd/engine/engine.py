@@ -987,8 +987,11 @@ class LLMEngine:
                 fwd()  # warm-up (hipBLASLt heuristics, allocator) outside capture
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=bk.pool):  # the bucket's two graphs never run at once
-                bk.graph_logits[cascade] = fwd()
+            # thread_local: another thread's device work during this capture (the K10b tally batcher's
+            # launches, allocations and read-backs on its own stream, score/tally_batch.py) neither
+            # invalidates the capture nor fails itself; only this thread's calls are checked
+            with torch.cuda.graph(g, pool=bk.pool, capture_error_mode="thread_local"):
+                bk.graph_logits[cascade] = fwd()  # (the bucket's two graphs never run at once)
             bk.pool = g.pool()
             bk.graphs[cascade] = g
             bk.graph = g
