@@ -101,6 +101,7 @@ def main():
     gen = torch.Generator().manual_seed(99)
 
     defer = not a.profile_steps  # the per-phase breakdown needs the score phase synchronised
+    last_cands = [None]
 
     def one_step(step_idx: int, prev=None):
         """Serve one step's requests.  The consensus of the step is returned DEFERRED (its answer indices
@@ -131,6 +132,7 @@ def main():
         if not defer:
             torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
+        last_cands[0] = cands
         return res, t1 - t0, t2 - t1
 
     res = None
@@ -159,6 +161,13 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     elapsed = pdist.max_over_ranks(elapsed, dev)
+    # self-check (untimed, after the clock stopped): the last step's first request re-scored from all of its
+    # candidates on one device must match what the candidate-parallel path produced (C1 all-gather +
+    # consensus); the verdict is a MIN over every rank, and a mismatch fails the run
+    from llm_weighted_consensus_amd.embeddings.consensus import verify_sharded
+    verified = True
+    if res is not None and last_cands[0]:
+        verified = verify_sharded(scorer, last_cands[0][0], res, group=cgroup if cp > 1 else None)
     answers = G * a.steps
     value = answers / elapsed
     emb_per_s = G * N * a.steps / elapsed
@@ -187,6 +196,7 @@ def main():
             "dtype": "bf16",
             "data": "synthetic prompts (random token ids), random-init weights",
             "embeddings_per_s": round(emb_per_s, 2),
+            "verified": verified,
             "generated_tokens_per_s": round(G * N * a.gen_len * a.steps / elapsed, 1),
             "config": {
                 "model": f"{a.decoder} sampler + {a.encoder} scorer",
@@ -205,6 +215,10 @@ def main():
         }
         print(json.dumps(out), flush=True)
     pdist.shutdown()
+    if not verified:
+        print("# VERIFICATION FAILED: the sharded consensus differs from the single-device recomputation",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

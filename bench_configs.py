@@ -122,21 +122,34 @@ def bench_moe(a):
         # inside the TP group assembles all N per request; tp embedder: each embeds all N with its weight
         # shard.  Both ranks then run the (tiny) consensus
         if emb_tp > 1 or tp == 1:
-            return scorer.score([[s.tokens for s in gr.seqs] for gr in groups])
+            last[0] = [[s.tokens for s in gr.seqs] for gr in groups]
+            return scorer.score(last[0])
         n_loc = N // tp
-        return scorer.score([[s.tokens for s in gr.seqs[tp_rank * n_loc:(tp_rank + 1) * n_loc]] for gr in groups],
-                            gather=True, group=tp_group)
+        last[0] = [[s.tokens for s in gr.seqs[tp_rank * n_loc:(tp_rank + 1) * n_loc]] for gr in groups]
+        return scorer.score(last[0], gather=True, group=tp_group)
+
+    last = [None]
 
     for i in range(a.warmup):
         step(i)
     _sync(dev, info.enabled)
     t0 = time.perf_counter()
+    res = None
     for i in range(a.steps):
-        step(a.warmup + i)
+        res = step(a.warmup + i)
     _sync(dev, info.enabled)
     dt = pdist.max_over_ranks((time.perf_counter() - t0) / a.steps, dev)
     if comm is not None:
         comm.check()
+    # untimed self-check: the last step's first request re-scored from all of its candidates on one device
+    # (a MIN over every rank; a mismatch fails the run, see bench.py)
+    from llm_weighted_consensus_amd.embeddings.consensus import verify_sharded
+    gathered = not (emb_tp > 1 or tp == 1)
+    verified = verify_sharded(scorer, last[0][0], res, group=tp_group if gathered else None)
+    # the TP embedder's per-layer all-reduces: 2 per layer of [tokens, d] bf16 over the process group
+    ecfg = decoder_config(a.embedder)
+    emb_tokens = R * N * (a.gen_len + 1)
+    ar_bytes = 2 * ecfg.layers * emb_tokens * ecfg.hidden * 2 if emb_tp > 1 else 0
     return {"metric": "consensus answers/sec (config 5: Mixtral-8x7B sampler + e5-mistral-7b embedder)",
             "value": round(dp * R / dt, 4), "unit": "answers/s", "n_gpus": 1 if shared else info.world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
@@ -145,6 +158,8 @@ def bench_moe(a):
                       "x row-quantised e4m3 activations, bf16 elsewhere") if not a.bf16 else "bf16",
             "data": "synthetic prompts (random token ids), random-init weights",
             "generated_tokens_per_s": round(dp * R * N * a.gen_len / dt, 1),
+            "verified": verified,
+            "embedder_allreduce_bytes_per_step": ar_bytes,
             "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": dp * R, "candidates_per_request": N,
                        "seq_len": a.prompt_len + a.gen_len,
                        "parallelism": f"tp{tp} x dp{dp}" + (" (ranks SHARE one GPU: a rehearsal of the protocol, "
@@ -170,9 +185,12 @@ def main():
     ap.add_argument("--embedder", default="e5-mistral-7b")
     ap.add_argument("--bf16", action="store_true", help="bf16 experts instead of fp8")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--embedder-par", choices=["tp", "dp"], default="tp",
-                    help="moe: the embedder across the TP group — tensor-parallel like the sampler (config 5's "
-                         "'TP=2 each') or data-parallel (whole model per rank, 1/tp of the candidates each)")
+    ap.add_argument("--embedder-par", choices=["tp", "dp"], default="dp",
+                    help="moe: the embedder across the TP group — data-parallel (default: whole model per rank, "
+                         "1/tp of the candidates each, ONE all-gather of the unit rows per step; the layout "
+                         "profiles/ep_vs_tp_round4.md measured best) or tensor-parallel like the sampler (config "
+                         "5's literal 'TP=2 each': two [tokens, d] bf16 all-reduces per layer through the process "
+                         "group, their bytes per step are reported)")
     ap.add_argument("--gpus", type=int, default=0, help="moe: world size (TP groups x DP); default = --tp")
     ap.add_argument("--tp-comm", choices=["ipc", "pg"], default="ipc",
                     help="moe TP all-reduce: IPC one-shot kernel (graph-captured) or the process group (RCCL / gloo, "
@@ -205,6 +223,8 @@ def main():
             print(f"# fp8 gemm {k}: " + " ".join(f"{b}={t:.1f}us" for b, t in v.items())
                   + f" choice={ops.FP8_CHOICE.get(k)}", file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
+    if out.get("verified") is False:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -61,6 +61,44 @@ def gather_candidates(E_local: torch.Tensor, group=None) -> torch.Tensor:
     return G.permute(1, 0, 2, 3).reshape(R, -1, d).contiguous()
 
 
+def verify_sharded(scorer: "EmbeddingConsensus", local: Sequence[Sequence[int]], res: ConsensusResult,
+                   group=None, request: int = 0, atol: float = 0.03) -> bool:
+    """Self-check of a candidate-parallel consensus (a collective over every rank of the job).
+
+    ``local`` = this rank's candidates (token ids) of request ``request`` of ``res``; the candidate group
+    (``group``) exchanges them (an object all-gather over the host, independent of the C1 tensor all-gather
+    under test), embeds all N on ONE device here and recomputes the consensus with the fp32 reference.  It
+    must match what the sharded path produced: the similarity matrix within ``atol`` (a shard in the wrong
+    place, a zeroed or stale shard moves whole rows by O(1)) and the same best candidate unless the top two
+    centralities are within ``atol``.  Returns the verdict of the WHOLE job (a MIN over all ranks), so every
+    rank can fail the run when one group mismatched."""
+    import torch.distributed as tdist
+
+    on = pdist.info().enabled
+    if on and group is not None:
+        parts: List = [None] * tdist.get_world_size(group)
+        tdist.all_gather_object(parts, [list(c) for c in local], group=group)
+        full = [c for p in parts for c in p]
+    else:
+        full = [list(c) for c in local]
+    _, eb = scorer.embed(full)
+    ref = consensus_reference(eb.float().view(1, len(full), -1), scorer.tau)
+    S = res.similarity[request].float().cpu()
+    cen = res.centrality[request].float().cpu()
+    best = res.best[request] if not isinstance(res.best, torch.Tensor) else int(res.best[request])
+    ok = not res.partial and S.shape == ref.similarity[0].shape
+    if ok:
+        ok = bool((S - ref.similarity[0]).abs().max() <= atol)
+        top = torch.topk(ref.centrality[0], min(2, len(full))).values
+        ok = ok and (best == ref.best[0] or bool(top[0] - top[-1] <= atol))
+        ok = ok and bool((cen - ref.centrality[0]).abs().max() <= atol)
+    if not on:
+        return ok
+    flag = torch.tensor([1.0 if ok else 0.0], device=eb.device if eb.is_cuda else "cpu")
+    pdist.all_reduce_(flag, op="min")
+    return bool(flag.item() == 1.0)
+
+
 class EmbeddingConsensus:
     def __init__(self, encoder, tau: float = 0.05, max_tokens: Optional[int] = None):
         self.encoder = encoder

@@ -210,7 +210,32 @@ def _world8_worker(rank, world, port, out_q):
     ok &= consensus_reference(got, 0.1).best == consensus_reference(full, 0.1).best
     seen = pdist.world_size_seen()
     ok &= pdist.max_over_ranks(float(rank)) == world - 1
-    out_q.put((rank, bool(ok), seen))
+    # bench.py's end-of-run self-check (verify_sharded) through the real scorer: a CPU encoder embeds this
+    # rank's shard of every request, C1 gathers them, and the verdict (a MIN over the 8 ranks) is True; the
+    # same run with a corrupted all-gather (the group's shards swapped) is caught on every rank
+    from llm_weighted_consensus_amd.embeddings import consensus as cons
+    from llm_weighted_consensus_amd.models.bert import BertEncoder
+    from llm_weighted_consensus_amd.models.config import encoder_config
+
+    scorer = cons.EmbeddingConsensus(BertEncoder(encoder_config("bert-tiny"), device="cpu", seed=3), tau=0.05)
+    gt = torch.Generator().manual_seed(100 + gidx)  # the candidate group's requests (same on both its ranks)
+    toks = [[torch.randint(0, 1000, (10,), generator=gt).tolist() for _ in range(N)] for _ in range(R)]
+    mine = [req[crank * n_local:(crank + 1) * n_local] for req in toks]
+    res = scorer.score(mine, gather=True, group=cgroup)
+    verified = cons.verify_sharded(scorer, mine[0], res, group=cgroup)
+    real = cons.gather_candidates
+
+    def corrupt(E_local, group=None):
+        G = real(E_local, group)
+        return torch.cat([G[:, n_local:], G[:, :n_local]], dim=1)  # shards in the wrong order
+
+    cons.gather_candidates = corrupt
+    try:
+        res_bad = scorer.score(mine, gather=True, group=cgroup)
+    finally:
+        cons.gather_candidates = real
+    caught = not cons.verify_sharded(scorer, mine[0], res_bad, group=cgroup)
+    out_q.put((rank, bool(ok), seen, verified, caught))
     pdist.shutdown()
 
 
@@ -226,8 +251,10 @@ def test_bench_layout_cp2_dp4_world8_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert [r[0] for r in res] == list(range(8))
-    assert all(ok for _, ok, _ in res), res
-    assert all(seen == 8 for _, _, seen in res)
+    assert all(r[1] for r in res), res
+    assert all(r[2] == 8 for r in res)
+    assert all(r[3] for r in res), res   # the sharded consensus verified against one-device recomputation
+    assert all(r[4] for r in res), res   # and a corrupted all-gather fails the verification everywhere
 
 
 def test_guarded_reraises_local_errors_without_abort():
