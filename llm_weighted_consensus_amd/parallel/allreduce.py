@@ -13,6 +13,12 @@ latency and graph capture (RCCL's eager call is ~20-40 us host-side per call, 64
 The reference has no tensor parallelism (it runs no model); this serves BASELINE config 5 (Mixtral
 TP=2) in place of the round-1 eager ``dist.all_reduce``.
 
+Start-up self-test: the constructor (a collective) runs one call on a random tensor and compares it with
+the same reduction through the process group (an all-gather of every rank's input, summed in fp32 on the
+host); a mismatch or a raised error word raises :class:`CommFailure` before the first request, so a broken
+peer mapping (cross-device ``hipIpcOpenMemHandle``, xGMI coherence of the uncached region) fails loudly at
+bring-up instead of decoding garbage.  ``LWC_AR_SELFTEST=0`` skips it.
+
 Failure: a peer that does not arrive within the spin bound (``spin_ms``, env ``LWC_AR_SPIN_MS``; the
 kernel's default is ~4 s) makes the waiting rank poison its output with NaN and set a sticky device
 error word — never sum a stale slot.  The engine reads that word without a host sync: :meth:`arm` queues
@@ -41,7 +47,7 @@ _NS_PER_SPIN = 60
 
 class CustomAllReduce:
     def __init__(self, group=None, device=None, max_bytes: int = 64 << 20, blocks: int = 128,
-                 spin_ms: Optional[float] = None):
+                 spin_ms: Optional[float] = None, self_test: Optional[bool] = None):
         """Collective: every rank of ``group`` (default: the world) must construct it together.
         ``max_bytes``: largest bf16 payload per call; ``blocks``: workgroups per launch (must be equal on
         every rank — block b of every rank reduces the same range); ``spin_ms``: how long a rank waits for
@@ -82,6 +88,39 @@ class CustomAllReduce:
             dist.barrier(group=group, device_ids=[self.device.index])
         else:
             dist.barrier(group=group)
+        if self_test is None:
+            self_test = os.environ.get("LWC_AR_SELFTEST", "1") != "0"
+        if self_test and self.W > 1:
+            self.self_test()
+
+    # ------------------------------------------------------------------ start-up self-test
+    def _gather_ref(self, x: torch.Tensor) -> List[torch.Tensor]:
+        """Every rank's ``x`` through the process group (host copies; any backend)."""
+        nccl = dist.get_backend(self.group) == "nccl"
+        src = x if nccl else x.cpu()
+        parts = [torch.empty_like(src) for _ in range(self.W)]
+        dist.all_gather(parts, src, group=self.group)
+        return [p.cpu() for p in parts]
+
+    def self_test(self, numel: int = 1 << 16) -> None:
+        """One IPC all-reduce of a random bf16 tensor vs the fp32 sum of the process group's all-gather of the
+        same inputs (collective).  Raises :class:`CommFailure` on a mismatch or a raised error word."""
+        g = torch.Generator().manual_seed(1234 + self.me)
+        x = (torch.rand(numel, generator=g) * 2 - 1).to(torch.bfloat16)
+        ref = torch.stack([p.float() for p in self._gather_ref(x)]).sum(0)
+        y = x.to(self.device)
+        with torch.cuda.device(self.device):
+            self.all_reduce_(y)
+            torch.cuda.synchronize(self.device)
+        got = y.float().cpu()
+        bad = int(self.err.item()) != 0 or not torch.allclose(got, ref, atol=0.02 * self.W, rtol=1e-2)
+        flag = torch.tensor([1 if bad else 0], dtype=torch.int32)
+        dist.all_reduce(flag if dist.get_backend(self.group) != "nccl" else flag.to(self.device),
+                        op=dist.ReduceOp.MAX, group=self.group)
+        if bad or int(flag.item()):
+            raise CommFailure(f"{type(self).__name__} self-test failed on rank {self.me} (max error "
+                              f"{(got - ref).abs().max().item():.3g}, error word {int(self.err.item())}): the "
+                              "IPC peer mapping does not deliver the peers' data")
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         """In-place sum of a bf16 tensor over the group (one kernel launch, graph-capturable)."""
@@ -144,6 +183,25 @@ class CustomAllToAll(CustomAllReduce):
     dispatch and combine (parallel/expert.py, padded mode) inside a captured decode step.  ``max_bytes`` is
     the largest per-(source, destination) chunk.  A peer that never arrives poisons the received chunks
     (all-ones bytes: NaN for float payloads) and sets the error word read by :meth:`poll` / :meth:`check`."""
+
+    def self_test(self, rows: int = 64) -> None:
+        """One IPC all-to-all of random rows vs the chunks taken from the process group's all-gather of every
+        rank's input (collective); raises :class:`CommFailure` on any difference (bytes must match exactly)."""
+        g = torch.Generator().manual_seed(4321 + self.me)
+        x = torch.randint(-30000, 30000, (self.W * rows, 8), generator=g, dtype=torch.int16)
+        parts = self._gather_ref(x)
+        ref = torch.cat([parts[p][self.me * rows:(self.me + 1) * rows] for p in range(self.W)])
+        out = torch.empty_like(x, device=self.device)
+        with torch.cuda.device(self.device):
+            self.all_to_all(out, x.to(self.device))
+            torch.cuda.synchronize(self.device)
+        bad = int(self.err.item()) != 0 or not torch.equal(out.cpu(), ref)
+        flag = torch.tensor([1 if bad else 0], dtype=torch.int32)
+        dist.all_reduce(flag if dist.get_backend(self.group) != "nccl" else flag.to(self.device),
+                        op=dist.ReduceOp.MAX, group=self.group)
+        if bad or int(flag.item()):
+            raise CommFailure(f"CustomAllToAll self-test failed on rank {self.me} (error word "
+                              f"{int(self.err.item())}): the IPC peer mapping does not deliver the peers' chunks")
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """out[p] = rank p's inp chunk for this rank; ``inp`` / ``out``: contiguous, dim 0 = W * rows (any

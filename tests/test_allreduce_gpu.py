@@ -272,3 +272,47 @@ def test_ipc_allreduce_missing_peer_fails_loudly(gpu):
     assert res[0]["first"] and res[1]["first"]
     assert res[0]["all_nan"] and res[0]["raised"], res[0]
     assert res[0]["elapsed"] < 5.0, res[0]  # the 300 ms bound, plus launch / sync overhead
+
+
+def _selftest_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LWC_SHARE_ONE_GPU="1")
+    try:
+        from llm_weighted_consensus_amd.parallel import dist as pdist
+        from llm_weighted_consensus_amd.parallel.allreduce import CommFailure, CustomAllReduce, CustomAllToAll
+
+        pdist.init_from_env("cuda")
+        dev = torch.device("cuda", 0)
+        out = []
+        for cls in (CustomAllReduce, CustomAllToAll):
+            comm = cls(device=dev, max_bytes=1 << 20, blocks=8, spin_ms=300)  # start-up self-test passes
+            good = comm.bases
+            comm.bases = [comm._own] * world  # a broken peer mapping: every "peer" is this rank's own region
+            try:
+                comm.self_test()
+                out.append((cls.__name__, "not caught"))
+            except CommFailure:
+                out.append((cls.__name__, "caught"))
+            comm.bases = good
+            pdist.barrier()
+            comm.close()
+        q.put((rank, out))
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_ipc_collectives_self_test_catches_broken_mapping(gpu):
+    """the IPC collectives check themselves against the process group at start-up, and a
+    broken peer mapping is caught (CommFailure on every rank) instead of decoding garbage."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_selftest_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = _collect(q, procs, 300)
+    for p in procs:
+        p.join(timeout=60)
+    want = [("CustomAllReduce", "caught"), ("CustomAllToAll", "caught")]
+    assert res == {0: want, 1: want}, res
