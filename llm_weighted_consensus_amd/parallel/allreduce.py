@@ -188,7 +188,7 @@ class CustomAllToAll(CustomAllReduce):
         """One IPC all-to-all of random rows vs the chunks taken from the process group's all-gather of every
         rank's input (collective); raises :class:`CommFailure` on any difference (bytes must match exactly)."""
         g = torch.Generator().manual_seed(4321 + self.me)
-        x = torch.randint(-30000, 30000, (self.W * rows, 8), generator=g, dtype=torch.int16)
+        x = torch.randint(-(1 << 30), 1 << 30, (self.W * rows, 4), generator=g, dtype=torch.int32)  # (gloo: no int16)
         parts = self._gather_ref(x)
         ref = torch.cat([parts[p][self.me * rows:(self.me + 1) * rows] for p in range(self.W)])
         out = torch.empty_like(x, device=self.device)
