@@ -50,8 +50,10 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
       o2[j] = x2[j] * cs[j] + x1[j] * sn[j];
     }
     const uint4v n1 = pack8(o1), n2 = pack8(o2);
-    *p1 = n1;
-    *p2 = n2;
+    if (rope_q || slot < 0) {  // k-only (pure decode) steps read k from the cache only: no write-back
+      *p1 = n1;
+      *p2 = n2;
+    }
     if (h >= Hq && slot >= 0) {
       const int kh = h - Hq;
       bf16_t* dst = kc + (((size_t)blk * Hkv + kh) * BS + off) * D;
