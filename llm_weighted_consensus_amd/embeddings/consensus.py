@@ -82,7 +82,7 @@ def verify_sharded(scorer: "EmbeddingConsensus", local: Sequence[Sequence[int]],
     else:
         full = [list(c) for c in local]
     _, eb = scorer.embed(full)
-    ref = consensus_reference(eb.float().view(1, len(full), -1), scorer.tau)
+    ref = consensus_reference(eb.float().cpu().view(1, len(full), -1), scorer.tau)  # fp32 on the host
     S = res.similarity[request].float().cpu()
     cen = res.centrality[request].float().cpu()
     best = res.best[request] if not isinstance(res.best, torch.Tensor) else int(res.best[request])
