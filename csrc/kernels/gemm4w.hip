@@ -40,6 +40,21 @@
 // gemm8p's stream-K or picks BN = 192 (qkv at M = 4096: 512 tiles = 2 whole rounds instead of 1.5).
 // Epilogue: accumulators -> bf16 (SwiGLU / bias / GELU in fp32 registers) -> LDS -> 16 B row stores (+
 // residual read in the same pass).
+//
+// RMSNorm folded into the projections (the decode chain, models/llama.py): rmsnorm(x) . W^T =
+// diag(1/rms(x)) . (x . (W diag(g))^T), so with the norm weight g folded into W once at load, a
+// projection of the raw residual stream only needs its accumulator rows scaled by r = 1/rms(x) — the
+// norm pass (a read and a write of every row) disappears.
+//   RS 1 (consumer: qkv, gate|up, lm_head): r for the tile's 256 rows arrives in LDS by ONE LDS-DMA piece
+//        of wave 0, issued before the tile's first K-tile pieces (so the prologue's counted wait retires
+//        it; double-buffered by tile parity for the cross-tile prefetch of VAR 64); the epilogue scales
+//        its rows before SwiGLU / the store.
+//   RS 2 (producer: the o / down projections' residual epilogue): every wave sums the squares of its
+//        128 output columns (the bf16-rounded new residual stream) per row and stores the partial at
+//        ss[2 tn + wn][row]; the last of an m-tile's tiles_n workgroups to finish (agent-scope release /
+//        acquire around one arrival counter, cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
+//        adds the 2 tiles_n partials of its 256 rows in a fixed order and writes r = rsqrt(sum / N + eps)
+//        for the next projection, then re-arms the counter.
 #include <algorithm>
 #include <cstdlib>
 
@@ -61,6 +76,11 @@ struct Params {
   int tiles_m, tiles_n, KT;
   int gm;
   int wpx, tiles;
+  const float* rs;  // RS 1: row scales [M]
+  float* ss;        // RS 2: row sum-of-squares partials [2 tiles_n][M]
+  float* rs_out;    // RS 2: finished row scales [M]
+  int* cnt;         // RS 2: arrival counter per m-tile (zero between launches)
+  float eps;        // RS 2
 };
 
 template <int NT>
@@ -113,12 +133,21 @@ LWC_DEVICE int swz(int row, int col) {
   return col ^ (((row & 7) << 3) % CW);
 }
 
-template <int EPI, int NT, int VAR>
+template <int EPI, int NT, int VAR, int RS>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   using G = Geo<NT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
+  // RS 1: the row-scale double buffer (2 x 256 fp32) after everything else in LDS
+  constexpr int RSOFF = PAP ? G::LdsPap : G::Lds;
+  // one LDS-DMA piece (64 lanes x 16 B = 256 rows x fp32) of the row scales of m-tile rows [m, m + 256)
+  auto rs_dma = [&](int m, int par) {
+    const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.rs + m, (p.M - m) * 4);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (__attribute__((address_space(3))) void*)(smem + RSOFF + par * 1024),
+                                             16, (uint32_t)((threadIdx.x & 63) * 16), 0, 0, 0);
+  };
 
   for (int round = 0;; ++round) {
     const int tile = round * 8 * p.wpx + xcd * p.wpx + j;
@@ -131,6 +160,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r16 = lane & 15, q = lane >> 4;
     const int wm = wid >> 1, wn = wid & 1;
+    const int rs_par = round & 1;
 
     // DMA: piece i of wave wid covers operand rows i*32 + wid*8 + lane/8, LDS chunk lane%8, which holds
     // global chunk (lane%8) ^ ((row >> 1) & 7); (row >> 1) & 7 does not depend on i.
@@ -185,8 +215,10 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
     // (residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
     // there is no next tile to prefetch, and 32 up-front residual chunks per lane would spill)
-    constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
     if (!PAP || round == 0) {
+      if constexpr (RS == 1) {
+        if (wid == 0) rs_dma(m0, rs_par);  // oldest VMEM op of wave 0: the counted wait below retires it
+      }
       stage(smem, 0);
       if (nt > 1) stage(smem + G::Buf, 1);
     }
@@ -393,6 +425,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       if (ntile < p.tiles) {
         int um, un;
         tile_mn(p, ntile, um, un);
+        if constexpr (RS == 1) {
+          if (wid == 0) rs_dma(um * 256, rs_par ^ 1);  // older than the pieces below (same counted wait)
+        }
         const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
         const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
@@ -418,6 +453,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         float4v t[NT];
 #pragma unroll
         for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
+        if constexpr (RS == 1) {
+          const float4v sc = *reinterpret_cast<const float4v*>(smem + RSOFF + rs_par * 1024 +
+                                                               (wm * 128 + i * 16 + 4 * q) * 4);
+#pragma unroll
+          for (int jj = 0; jj < NT; ++jj) t[jj] *= sc;
+        }
         if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
           for (int h = 0; h < NT / 4; ++h)
@@ -479,6 +520,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       float4v t[NT];
 #pragma unroll
       for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
+      if constexpr (RS == 1) {
+        const float4v sc = *reinterpret_cast<const float4v*>(smem + RSOFF + rs_par * 1024 +
+                                                             (wm * 128 + i * 16 + 4 * q) * 4);
+#pragma unroll
+        for (int jj = 0; jj < NT; ++jj) t[jj] *= sc;
+      }
       if constexpr (EPI == EPI_SWIGLU) {
         // n-tiles of the wave: W rows wn*128 + jj*16; 32-row blocks alternate gate / up, so gate tiles
         // {0,1,4,5} pair with up tiles {2,3,6,7}
@@ -552,7 +599,23 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           unpack8(rv[u], y);
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] += y[e];
-          if (gm < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = pack8(x);
+          const uint4v v = pack8(x);
+          if (gm < p.M && gn < ncols) *reinterpret_cast<uint4v*>(p.C + (size_t)gm * p.ldc + gn) = v;
+          if constexpr (RS == 2) {
+            // the row's squares over this wave's CW columns (of the rounded values the stream now holds):
+            // the CPR lanes sharing a row are lanes 16 r' .. 16 r' + 15 (CPR = 16), a 4-step xor tree
+            static_assert(CPR == 16, "RS 2 takes 256-wide tiles");
+            float z[8];
+            unpack8(gn < ncols ? v : uint4v{0u, 0u, 0u, 0u}, z);
+            float sq = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sq += z[e] * z[e];
+            sq += __shfl_xor(sq, 8);
+            sq += __shfl_xor(sq, 4);
+            sq += __shfl_xor(sq, 2);
+            sq += __shfl_xor(sq, 1);
+            if ((lane & 15) == 0 && gm < p.M) p.ss[(size_t)(2 * tn + wn) * p.M + gm] = sq;
+          }
         }
       }
     } else {
@@ -567,54 +630,95 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       }
     }
     __syncthreads();  // LDS free for the next tile
+    if constexpr (RS == 2) {
+      // the m-tile's last arriver finishes its rows' scales: release (every wave's partial stores done,
+      // then one agent-scope release before the arrival), acquire on the last arriver before it reads
+      // the other workgroups' partials; the "I am last" flag travels through the one LDS array
+      int* last = reinterpret_cast<int*>(smem);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(p.cnt + tm, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last = old == p.tiles_n - 1;
+      }
+      __syncthreads();
+      if (*last) {
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const int row = m0 + (int)threadIdx.x;
+        if (row < p.M) {
+          float sum = 0.f;
+          for (int k = 0; k < 2 * p.tiles_n; ++k) sum += p.ss[(size_t)k * p.M + row];
+          p.rs_out[row] = rsqrtf(sum / (float)p.N + p.eps);
+        }
+        if (threadIdx.x == 0) p.cnt[tm] = 0;  // re-armed for the next launch (ordered by the kernel boundary)
+      }
+      __syncthreads();  // the flag word is LDS of the next tile
+    }
   }
 }
 
-template <int EPI, int NT, int VAR>
+template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds;
+  constexpr int lds = (VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds) + (RS == 1 ? 2048 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR, RS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm4w_kernel<EPI, NT, VAR><<<8 * p.wpx, 256, lds, s>>>(p);
+  gemm4w_kernel<EPI, NT, VAR, RS><<<8 * p.wpx, 256, lds, s>>>(p);
   return (int)hipGetLastError();
 }
 
 int env_int(const char* name, int dflt);
 
 template <int EPI, int NT>
-int launch(const Params& p, hipStream_t s) {
-  // schedule variant (VAR bits, see the main loop): LWC_G4_VAR, an A/B knob (scripts/microbench.py g4ab);
-  // default 32, the library-shaped schedule (faster than 1 at every headline shape, profiles/gemm4w.md);
-  // every epilogue carries 1 and 32, the plain one the other variants
-  const int var = env_int("LWC_G4_VAR", 32);
-  if (var == 32) return launch3<EPI, NT, 32>(p, s);
-  if (var == 64) return launch3<EPI, NT, 64>(p, s);
+int launch(const Params& p, hipStream_t s, int var, int rs) {
+  // schedule variant (VAR bits, see the main loop): the caller's, else LWC_G4_VAR, an A/B knob
+  // (scripts/microbench.py g4ab); default 32, the library-shaped schedule (faster than 1 at every headline
+  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants.
+  // rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sum-of-squares (see the file head)
+  if (var <= 0) var = env_int("LWC_G4_VAR", 32);
+  if (rs == 1) {
+    // (VAR 64 + RS 1 ran out of VGPRs in the wave-local epilogue: 256 + scratch; the row-scaled
+    // consumers take the block-staged epilogue)
+    if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) return launch3<EPI, NT, 32, 1>(p, s);
+    return -1;
+  }
+  if (rs == 2) {
+    if constexpr (EPI == EPI_RESIDUAL && NT == 8) return launch3<EPI, NT, 32, 2>(p, s);
+    return -1;
+  }
+  if (var == 32) return launch3<EPI, NT, 32, 0>(p, s);
+  if (var == 64) return launch3<EPI, NT, 64, 0>(p, s);
   if constexpr (EPI == EPI_PLAIN) {
     switch (var) {
-      case 0: return launch3<EPI, NT, 0>(p, s);
-      case 3: return launch3<EPI, NT, 3>(p, s);
-      case 5: return launch3<EPI, NT, 5>(p, s);
-      case 7: return launch3<EPI, NT, 7>(p, s);
-      case 8: return launch3<EPI, NT, 8>(p, s);
+      case 0: return launch3<EPI, NT, 0, 0>(p, s);
+      case 3: return launch3<EPI, NT, 3, 0>(p, s);
+      case 5: return launch3<EPI, NT, 5, 0>(p, s);
+      case 7: return launch3<EPI, NT, 7, 0>(p, s);
+      case 8: return launch3<EPI, NT, 8, 0>(p, s);
       default: break;
     }
   }
-  return launch3<EPI, NT, 1>(p, s);
+  return launch3<EPI, NT, 1, 0>(p, s);
 }
 
 template <int NT>
-int dispatch(const Params& p, int epi, hipStream_t s) {
+int dispatch(const Params& p, int epi, hipStream_t s, int var, int rs) {
   switch (epi) {
-    case EPI_PLAIN: return launch<EPI_PLAIN, NT>(p, s);
-    case EPI_RESIDUAL: return launch<EPI_RESIDUAL, NT>(p, s);
-    case EPI_BIAS: return launch<EPI_BIAS, NT>(p, s);
-    case EPI_BIAS_GELU: return launch<EPI_BIAS_GELU, NT>(p, s);
+    case EPI_PLAIN: return launch<EPI_PLAIN, NT>(p, s, var, rs);
+    case EPI_RESIDUAL: return launch<EPI_RESIDUAL, NT>(p, s, var, rs);
+    case EPI_BIAS: return rs ? -1 : launch<EPI_BIAS, NT>(p, s, var, 0);
+    case EPI_BIAS_GELU: return rs ? -1 : launch<EPI_BIAS_GELU, NT>(p, s, var, 0);
     case EPI_SWIGLU:
-      if constexpr (NT == 8) return launch<EPI_SWIGLU, NT>(p, s);
+      if constexpr (NT == 8) return launch<EPI_SWIGLU, NT>(p, s, var, rs);
       return -1;
   }
   return -1;
@@ -640,19 +744,25 @@ int device_cus() {
 
 // C = A . W^T (epilogue epi as lwc_gemm8p: 0 plain, 1 + residual, 2 SwiGLU over 32-row gate/up interleaved W,
 // 3 + bias, 4 gelu(. + bias)); bn = 256 or 192 (W rows per tile; SwiGLU needs 256).  Requires K % 64 == 0,
-// N % 8 == 0, lda / ldc % 8 == 0.
+// N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): rs [M] (epi 0 / 2) scales the accumulator rows;
+// ss [2 N/256][M] + rs_out [M] + cnt [ceil(M/256)] (epi 1, bn 256) make the residual epilogue produce the next
+// projection's row scales rsqrt(mean(out^2) + eps).  var: schedule variant (0 = LWC_G4_VAR / 32).
 extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
-                          int epi, int bn, hipStream_t s) {
+                          int epi, int bn, const float* rs, float* ss, float* rs_out, int* cnt, float eps, int var,
+                          hipStream_t s) {
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
   if ((long long)M * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
   if (epi == EPI_SWIGLU && (N % 64 != 0 || bn != 256)) return -1;
   if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
+  const int rsm = rs != nullptr ? 1 : (ss != nullptr ? 2 : 0);
+  if (rsm == 1 && epi != EPI_PLAIN && epi != EPI_SWIGLU) return -1;
+  if (rsm == 2 && (epi != EPI_RESIDUAL || bn != 256 || rs_out == nullptr || cnt == nullptr)) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
   const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
-           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles};
-  return bn == 256 ? dispatch<8>(p, epi, s) : dispatch<6>(p, epi, s);
+           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, rs, ss, rs_out, cnt, eps};
+  return bn == 256 ? dispatch<8>(p, epi, s, var, rsm) : dispatch<6>(p, epi, s, var, rsm);
 }

@@ -229,6 +229,25 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restric
   }
 }
 
+// rs[r] = rsqrt(mean(x[r]^2) + eps), one wave per row: the row scales of an RMSNorm folded into the next
+// projection (gemm4w RS 1) for rows no residual epilogue produced them for (the embedding rows)
+__global__ void __launch_bounds__(256) rms_rowscale_kernel(const bf16_t* __restrict__ x, float* __restrict__ rs, int rows,
+                                                           int d, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const uint4v* xr = reinterpret_cast<const uint4v*>(x + (size_t)row * d);
+  float s = 0.f;
+  for (int i = lane; i < (d >> 3); i += 64) {
+    float v[8];
+    unpack8(xr[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) rs[row] = rsqrtf(s / (float)d + eps);
+}
+
 static int norm_threads(int d) {
   // one 16-byte vector per thread when the row allows it (shortest latency per row)
   int nvec = d / 8;
@@ -284,5 +303,13 @@ extern "C" int lwc_layernorm(const void* x, const void* residual, const void* g,
   else
     layernorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)g, (const bf16_t*)b,
                                                (bf16_t*)y, d, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lwc_rms_rowscale(const void* x, float* rs, int rows, int d, float eps, hipStream_t s) {
+  using namespace lwc;
+  if (d % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  rms_rowscale_kernel<<<(rows + 3) / 4, 256, 0, s>>>((const bf16_t*)x, rs, rows, d, eps);
   return (int)hipGetLastError();
 }

@@ -12,7 +12,17 @@ Per layer (decode, B sequences):
     act  = silu(x Wg^T) (x Wu^T)  K6 with SwiGLU in its epilogue (fused gate|up weight), or GEMM + K5
     x   += act @ Wd^T             K6 + residual, then K1
 K6 is chosen per shape by ops/gemm_plan.py among hipBLASLt and the hand-written cores (gemm4w, gemm8p),
-timed on the device.  Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over
+timed on the device.
+
+Folded RMSNorm (decode chain, dense bf16 on the GPU): every norm weight is folded into the projection that
+reads it at load (W_qkv diag(g_attn), W_gate_up diag(g_mlp), W_lm_head diag(g_final); the norm weights become
+ones, so the unfolded path computes the same function), and a decode step where the chain was timed faster
+(:meth:`LlamaModel.tune_gemms`) runs NO norm kernel: the o / down projections' residual epilogues emit the
+row scales 1/rms of the new residual stream, which the next projection (qkv, gate|up, lm_head) applies to
+its accumulator rows (gemm4w RS modes, csrc/kernels/gemm4w.hip):
+    rs = rms_rowscale(embedding)                  (once)
+    qkv = gemm4w(x, W_qkv', rs)   ...   x += gemm4w(attn, W_o) -> rs
+    act = gemm4w(x, W_gu', rs, SwiGLU)   x += gemm4w(act, W_d) -> rs     ...   logits = gemm4w(x, W_lm', rs)  Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over
 the fresh k/v of the qkv buffer; mixed chunked-prefill steps (forward_mixed) send decode rows to K3 and
 prompt-chunk rows to K4's paged-KV mode; the k/v are scattered into the paged cache in the RoPE pass.
 """
@@ -129,6 +139,31 @@ class LlamaModel:
                     L.gu_block = 32
             self.g8_ws = ops.new_gemm8p_workspace(self.device)
             blas_tuning.enable()  # offline-tuned hipBLASLt / rocBLAS solutions for the library GEMMs
+        # folded RMSNorm (module docstring): the plain dense bf16 decoder on the GPU
+        self.norm_folded = False
+        self.chain: Optional[ops.NormChain] = None
+        self.chain_m: dict = {}  # decode batch M -> (use the chain, qkv tile width)
+        if (self.device.type == "cuda" and not self.fp8_dense and type(self) is LlamaModel
+                and os.environ.get("LWC_NORM_FOLD", "1") != "0" and isinstance(self.layers[0], LayerWeights)):
+            self._fold_norms()
+
+    def _fold_norms(self) -> None:
+        """W diag(g) for every projection that reads a normalised row, then g = 1 (the unfolded path computes the
+        same function).  One bf16 rounding of each folded weight (exact for the random-init unit norm weights)."""
+        def fold(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+            out = torch.empty_like(w)
+            gf = g.float()
+            for r in range(0, w.shape[0], 8192):
+                out[r:r + 8192] = (w[r:r + 8192].float() * gf).to(w.dtype)
+            return out
+
+        for L in self.layers:
+            L.wqkv, L.attn_norm = fold(L.wqkv, L.attn_norm), torch.ones_like(L.attn_norm)
+            L.w_gate_up, L.mlp_norm = fold(L.w_gate_up, L.mlp_norm), torch.ones_like(L.mlp_norm)
+        self.lm_head = fold(self.lm_head, self.final_norm)  # (a tied embedding table keeps its own copy)
+        self.final_norm = torch.ones_like(self.final_norm)
+        self.norm_folded = True
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int) -> None:
@@ -187,6 +222,29 @@ class LlamaModel:
         self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
 
     # ------------------------------------------------------------------ forward
+    def _chain_layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool,
+                      qkv_bn: int) -> torch.Tensor:
+        """The folded-RMSNorm decode chain (module docstring): x_res is updated in place; the row scales of the
+        final residual stream are left in ``self.chain.rs`` for the lm_head."""
+        cfg, ch = self.cfg, self.chain
+        T = x_res.shape[0]
+        Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
+        ops.rms_rowscale(x_res, ch.rs, cfg.rms_eps)
+        for li, L in enumerate(self.layers):
+            qkv = ops.gemm4w(x_res, L.wqkv, bn=qkv_bn, rs=ch.rs)
+            ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
+                              rope_q=rope_q)
+            attn = attn_fn(qkv, li)
+            ops.gemm4w(attn.reshape(T, Hq * D), L.wo, residual=x_res, out=x_res, chain=ch)
+            act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, rs=ch.rs)
+            ops.gemm4w(act, L.w_down, residual=x_res, out=x_res, chain=ch)
+        return x_res
+
+    def chain_ok(self, M: int) -> bool:
+        """Whether a decode step of M rows runs the folded-norm chain (timed faster at M, before capture)."""
+        c = self.chain_m.get(M)
+        return bool(c and c[0]) and self.chain is not None and M <= self.chain.max_rows
+
     def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True,
                 keep: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Runs every layer; x_res is the residual stream (updated in place); returns the final
@@ -313,6 +371,59 @@ class LlamaModel:
         gemm_plan.tune(xf, L.w_down, epi, ws=self.g8_ws, bucket=bucket)
         if lm_head:
             gemm_plan.tune(x, self.lm_head, ws=self.g8_ws, bucket=bucket)
+        if self.norm_folded and not bucket and lm_head:
+            self._tune_chain(M, x, xa, xf)
+
+    def _tune_chain(self, M: int, x, xa, xf) -> None:
+        """Decode batch M: time one layer + the lm_head as the folded-norm chain (qkv at bn 192 and 256) against
+        the unfolded path on the planner's choices (norm kernels + the best backend per projection); the
+        faster is what decode() runs at M (recorded in ``chain_m``).  ``LWC_NORM_CHAIN=1|0`` forces it."""
+        if M in self.chain_m or torch.cuda.is_current_stream_capturing():
+            return
+        cfg, L = self.cfg, self.layers[0]
+        if self.chain is None:  # once, for every decode bucket (captured graphs keep these addresses)
+            self.chain = ops.NormChain(max(M, 8192), cfg.hidden, cfg.rms_eps, self.device)
+        if M > self.chain.max_rows:
+            self.chain_m[M] = (False, 192)
+            return
+        force = os.environ.get("LWC_NORM_CHAIN")
+        x_res = x.clone()
+        ch, eps = self.chain, cfg.rms_eps
+        ones = torch.ones(cfg.hidden, device=self.device, dtype=self.dtype)
+
+        def chained(bn):
+            def run():
+                ops.rms_rowscale(x_res, ch.rs, eps)
+                ops.gemm4w(x_res, L.wqkv, bn=bn, rs=ch.rs)
+                ops.gemm4w(xa, L.wo, residual=x_res, out=x_res, chain=ch)
+                ops.gemm4w(x_res, L.w_gate_up, swiglu=True, rs=ch.rs)
+                ops.gemm4w(xf, L.w_down, residual=x_res, out=x_res, chain=ch)
+                ops.gemm4w(x_res, self.lm_head, rs=ch.rs)
+            return run
+
+        def unchained():
+            h = ops.rmsnorm(x_res, ones, eps)
+            self._proj(h, L.wqkv)
+            gemm_plan.linear_add_(xa, L.wo, x_res, ws=self.g8_ws)
+            h = ops.rmsnorm(x_res, ones, eps)
+            gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
+            gemm_plan.linear_add_(xf, L.w_down, x_res, ws=self.g8_ws)
+            h = ops.rmsnorm(x_res, ones, eps)
+            self._proj(h, self.lm_head)
+
+        runs = {192: chained(192), 256: chained(256), "base": unchained}
+        ts = {k: [] for k in runs}
+        for _ in range(3):  # interleaved rounds (one process, one device)
+            for k, fn in runs.items():
+                x_res.copy_(x)
+                ts[k].append(gemm_plan._time(fn, iters=3, rounds=1))
+        med = {k: sorted(t)[len(t) // 2] for k, t in ts.items()}
+        bn = 192 if med[192] <= med[256] else 256
+        use = med[bn] < med["base"] if force is None else force == "1"
+        self.chain_m[M] = (use, bn)
+        gemm_plan.TIMINGS[(M, cfg.hidden, 0, "norm_chain")] = {"chain192": med[192], "chain256": med[256],
+                                                                "unfolded": med["base"]}
+        gemm_plan._CHOICE[(M, cfg.hidden, 0, "norm_chain")] = f"chain{bn}" if use else "unfolded"
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,
@@ -346,6 +457,9 @@ class LlamaModel:
                 return ops.paged_decode(qkv, cache.k[li], cache.v[li], block_tables, ctx_lens, cfg.heads, self.scale,
                                         num_splits=num_splits, part_o=part_o, part_lse=part_lse, rope=rope)
 
+        if self.chain_ok(B):
+            x = self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, self.chain_m[B][1])
+            return ops.gemm4w(x, self.lm_head, rs=self.chain.rs)
         h = self._layers(x, cache, positions, slots, attn_fn, rope_q=not q_at_load)
         return self._proj(h, self.lm_head)
 

@@ -387,11 +387,17 @@ def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
 
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
-           gelu: bool = False, bn: int = 256) -> torch.Tensor:
+           gelu: bool = False, bn: int = 256, rs: Optional[torch.Tensor] = None, chain: "Optional[NormChain]" = None,
+           var: int = 0) -> torch.Tensor:
     """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
     a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
     workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
-    (interleaved gate|up W, bn 256), ``bias`` (+ ``gelu``)."""
+    (interleaved gate|up W, bn 256), ``bias`` (+ ``gelu``).
+
+    Folded RMSNorm (the decode chain, :class:`NormChain`): ``rs`` [M] fp32 scales the accumulator rows
+    (plain / SwiGLU: rmsnorm(x) . W^T with the norm weight folded into W); ``chain`` with ``residual`` makes
+    the residual epilogue also produce the next projection's row scales in ``chain.rs``.  ``var``: schedule
+    variant (0 = default)."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
@@ -403,8 +409,36 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
         if gelu:
             raise ValueError("gemm4w: gelu needs a bias")
         epi = 2 if swiglu else (1 if residual is not None else 0)
-    kernels().gemm4w(A, W, out, residual, epi, int(bn))
+    if chain is not None and epi != 1:
+        raise ValueError("gemm4w: chain= (row sums of squares) goes with the residual epilogue")
+    ss = ro = cnt = None
+    eps = 0.0
+    if chain is not None:
+        ss, ro, cnt, eps = chain.ss, chain.rs, chain.cnt, chain.eps
+    kernels().gemm4w(A, W, out, residual, epi, int(bn), rs, ss, ro, cnt, float(eps), int(var))
     return out
+
+
+class NormChain:
+    """Buffers of the folded-RMSNorm decode chain (csrc/kernels/gemm4w.hip head): ``rs`` [max_rows] fp32 row
+    scales (written by a residual GEMM's last-arriving workgroups or :func:`rms_rowscale`, read by the next
+    projection), ``ss`` [2 ceil(d/256), max_rows] fp32 partial sums of squares, ``cnt`` [ceil(max_rows/256)]
+    int32 arrival counters (zero; every launch leaves them zero).  Allocated once, outside graph capture."""
+
+    def __init__(self, max_rows: int, d: int, eps: float, device):
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("NormChain buffers must be allocated outside hipGraph capture")
+        self.max_rows, self.d, self.eps = int(max_rows), int(d), float(eps)
+        self.rs = torch.ones(self.max_rows, dtype=torch.float32, device=device)
+        self.ss = torch.zeros(2 * ((d + 255) // 256) * self.max_rows, dtype=torch.float32, device=device)
+        self.cnt = torch.zeros((self.max_rows + 255) // 256, dtype=torch.int32, device=device)
+
+
+def rms_rowscale(x: torch.Tensor, rs: torch.Tensor, eps: float) -> torch.Tensor:
+    """rs[r] = rsqrt(mean(x[r]^2) + eps) (the folded RMSNorm's row scales of rows no residual epilogue
+    produced them for, e.g. the embedding rows); returns rs."""
+    kernels().rms_rowscale(x, rs, float(eps))
+    return rs
 
 
 _G8_WS: dict = {}

@@ -1216,6 +1216,67 @@ def test_gemm4w(gpu, M, N, K, epi, bn, var, monkeypatch):
             _close(out, want, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi,bn", [(300, 4096, 256, "plain", 256), (4096 + 37, 6144, 512, "plain", 192),
+                                         (1000, 1536, 320, "swiglu", 256), (257, 128256 // 16, 128, "plain", 256)])
+def test_gemm4w_rowscale(gpu, M, N, K, epi, bn):
+    """Folded RMSNorm, consumer side (RS 1): rows of the accumulator scaled by rs[row] before the epilogue
+    (plain, SwiGLU), ragged M (the row-scale DMA past the last row reads zeros), multi-round tiles; vs the fp32
+    product of the scaled rows.  Twice: the row-scale double buffer across tiles and launches."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    rs = torch.rand(M, device=gpu) * 2 + 0.1
+    ref = rs[:, None] * (A.float() @ W.float().t())
+    for _ in range(2):
+        if epi == "swiglu":
+            F = N // 2
+            out = ops.gemm4w(A, ops.swiglu_interleave(W), swiglu=True, bn=bn, rs=rs)
+            _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
+        else:
+            _close(ops.gemm4w(A, W, bn=bn, rs=rs), ref, 3e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (300, 4096, 512), (1000, 1024, 128), (4096 + 37, 4096, 64)])
+def test_gemm4w_residual_rowsum(gpu, M, N, K):
+    """Folded RMSNorm, producer side (RS 2): the residual epilogue writes C = R + A.W^T and the m-tiles' last
+    arriving workgroups finish rs = rsqrt(mean(C^2) + eps) over the bf16 output rows (fp32 reference on the
+    returned C), leaving every arrival counter zero; three launches in a row (counters re-armed), and the
+    chain end to end: an RS 1 projection of C with the produced scales == the projection of rmsnorm(C)."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N + K)
+    eps = 1e-5
+    chain = ops.NormChain(M + 64, N, eps, gpu)
+    chain.rs.fill_(-7.0)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    for it in range(3):
+        R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+        want = R.float() + A.float() @ W.float().t()
+        C = ops.gemm4w(A, W, residual=R, out=R, chain=chain)
+        torch.cuda.synchronize()
+        _close(C, want, 3e-2, 1e-2)
+        rs_ref = torch.rsqrt(C.float().pow(2).mean(-1) + eps)
+        assert torch.allclose(chain.rs[:M], rs_ref, rtol=1e-5, atol=1e-6), (it, (chain.rs[:M] - rs_ref).abs().max())
+        assert int(chain.cnt.abs().sum()) == 0
+        assert bool((chain.rs[M:] == -7.0).all())  # rows past M untouched
+    Wn = (torch.randn(512, N, device=gpu) / N ** 0.5).to(torch.bfloat16)
+    g = torch.ones(N, device=gpu, dtype=torch.bfloat16)
+    h = ops.rmsnorm(C, g, eps)
+    _close(ops.gemm4w(C, Wn, rs=chain.rs[:M].contiguous()), h.float() @ Wn.float().t(), 3e-2, 1e-2)
+
+
+def test_rms_rowscale(gpu):
+    from llm_weighted_consensus_amd import ops
+
+    x = torch.randn(1000, 4096, device=gpu).to(torch.bfloat16)
+    rs = torch.empty(1000, device=gpu)
+    ops.rms_rowscale(x, rs, 1e-5)
+    assert torch.allclose(rs, torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5), rtol=1e-5)
+
+
 @pytest.mark.parametrize("n,d,k", [(37, 1024, 5), (1000, 1024, 16), (70000, 384, 64), (300, 4096, 1)])
 def test_knn_topk(gpu, n, d, k):
     """K10c training-table neighbour search == torch.topk of the fp32 dot products (rows with tied scores:

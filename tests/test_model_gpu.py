@@ -292,3 +292,46 @@ def test_fp8_dense_decoder_embedder_and_prefill(gpu):
     out = eng.generate([tok.encode("fp8 projections " * 4)], SamplingParams(temperature=0.0, max_tokens=6,
                                                                           ignore_eos=True), n=2)
     assert len(out[0]) == 2 and out[0][0] == out[0][1] and len(out[0][0]) == 6
+
+
+@pytest.mark.parametrize("qkv_bn", [192, 256])
+def test_folded_norm_chain_matches_unfolded(tiny, gpu, qkv_bn):
+    """Folded RMSNorm decode chain (models/llama.py, gemm4w RS modes): the norm weights live in the projection
+    weights (the model's norms are ones), the o / down residual epilogues emit the row scales the next
+    projection applies — the decode logits equal the unfolded path's (norm kernels + projections) and the fp32
+    reference forward."""
+    from llm_weighted_consensus_amd import ops
+    from llm_weighted_consensus_amd.models.llama import KVCache
+
+    m = tiny
+    assert m.norm_folded and bool((m.layers[0].attn_norm == 1).all())
+    cache = KVCache(m.cfg, 64, 16, gpu)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    toks = torch.randint(0, m.cfg.vocab_size, (36,), generator=g).to(gpu)
+    ref_logits = ref.llama_forward(m, toks)
+    P = 35
+    slots = torch.arange(P, dtype=torch.int32, device=gpu)
+    cu = torch.tensor([0, P], dtype=torch.int32, device=gpu)
+    m.prefill(toks[:P].int(), torch.arange(P, dtype=torch.int32, device=gpu), slots, cu, P,
+              torch.tensor([P - 1], device=gpu), cache)
+    B = 300  # rows: one sequence repeated (ragged last m-tile of the chain's 256-row tiles)
+    bt = torch.arange(4, dtype=torch.int32, device=gpu).view(1, 4).expand(B, 4).contiguous()
+    args = (toks[P:P + 1].int().expand(B).contiguous(), torch.full((B,), P, dtype=torch.int32, device=gpu),
+            torch.full((B,), P, dtype=torch.int32, device=gpu), bt, torch.full((B,), P + 1, dtype=torch.int32,
+                                                                                 device=gpu), cache)
+    if m.chain is None:
+        m.chain = ops.NormChain(8192, m.cfg.hidden, m.cfg.rms_eps, gpu)
+    saved = dict(m.chain_m)
+    try:
+        m.chain_m[B] = (False, qkv_bn)
+        base = m.decode(*args, num_splits=1).float()
+        m.chain_m[B] = (True, qkv_bn)
+        assert m.chain_ok(B)
+        got = m.decode(*args, num_splits=1).float()
+    finally:
+        m.chain_m.clear()
+        m.chain_m.update(saved)
+    assert _cos(got, base) > 0.9995
+    assert (got - base).abs().max() < 0.05 * base.abs().max()
+    assert _cos(got[B - 1], ref_logits[P]) > 0.995 and _cos(got[0], ref_logits[P]) > 0.995
+    assert int(m.chain.cnt.abs().sum()) == 0
