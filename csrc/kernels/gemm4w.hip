@@ -379,7 +379,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #undef G4_TILE
 #undef G4_TILE1
 #undef G4_TILE_H
-    G4_MFMA_DRAIN();  // accumulators are read by VALU / stores from here on
+    // accumulators are read by VALU / stores from here on.  The MFMAs are opaque inline asm, so the compiler
+    // takes their results as ready at once: without a barrier it hoisted v_accvgpr_read of the last MFMAs'
+    // accumulators above the drain (the row-scaled variant read stale e = 2, 3 values).  The drain, then an
+    // empty asm "writing" every accumulator: no read can move above it.
+    __builtin_amdgcn_sched_barrier(0);
+    G4_MFMA_DRAIN();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NT; ++jj) asm volatile("" : "+a"(acc[i][jj]));
     __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
