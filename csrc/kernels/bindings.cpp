@@ -26,9 +26,9 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
-int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, const float*, float*,
-               float*, int*, float, int, hipStream_t);
-int lwc_rms_rowscale(const void*, float*, int, int, float, hipStream_t);
+int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, float,
+               int, hipStream_t);
+int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, int, int, const void*, void*, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
@@ -417,49 +417,38 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
 }
 
 // gemm4w: the 4-wave interleaved core (one wave per SIMD, data-parallel tiles of 256 x bn, bn = 256 | 192).
-// Folded RMSNorm (gemm4w.hip head): rs [M] fp32 scales the accumulator rows (epi 0 / 2); ss [2 N/256, M] fp32 +
-// rs_out [M] fp32 + cnt [ceil(M/256)] int32 (zero) make the residual epilogue (epi 1) emit the next row scales.
+// Folded RMSNorm (gemm4w.hip head): rs_mode 1 (epi 0 / 2) reads ss [>= P, M] fp32 partial row sums of squares
+// and scales the accumulator rows by rsqrt(sum / K + eps); rs_mode 2 (epi 1, bn 256) writes ss [N/256, M].
 void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
-            int64_t bn, const c10::optional<at::Tensor>& rs, const c10::optional<at::Tensor>& ss,
-            const c10::optional<at::Tensor>& rs_out, const c10::optional<at::Tensor>& cnt, double eps, int64_t var) {
+            int64_t bn, const c10::optional<at::Tensor>& ss, int64_t rs_mode, int64_t P, double eps, int64_t var) {
   const void* r = gemm_operands(A, W, C, R, epi);
   const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
   TORCH_CHECK(bn == 256 || bn == 192, "gemm4w: bn must be 256 or 192");
   TORCH_CHECK(epi != 2 || bn == 256, "gemm4w: SwiGLU needs bn 256");
-  const float* rsp = nullptr;
-  float *ssp = nullptr, *rop = nullptr;
-  int* cp = nullptr;
-  if (rs.has_value() && rs->defined()) {
-    CHECK_GPU(*rs); CHECK_DTYPE(*rs, at::kFloat); CHECK_CONTIG(*rs);
-    TORCH_CHECK(epi == 0 || epi == 2, "gemm4w: row scales need the plain or SwiGLU epilogue");
-    TORCH_CHECK(rs->numel() >= M, "gemm4w: rs needs M entries");
-    rsp = rs->data_ptr<float>();
-  }
-  if (ss.has_value() && ss->defined()) {
-    TORCH_CHECK(epi == 1 && bn == 256 && rsp == nullptr, "gemm4w: row sums of squares need the residual epilogue, bn 256");
-    TORCH_CHECK(rs_out.has_value() && rs_out->defined() && cnt.has_value() && cnt->defined(), "gemm4w: ss needs rs_out, cnt");
+  float* ssp = nullptr;
+  if (rs_mode) {
+    TORCH_CHECK(ss.has_value() && ss->defined(), "gemm4w: rs_mode needs ss");
     CHECK_GPU(*ss); CHECK_DTYPE(*ss, at::kFloat); CHECK_CONTIG(*ss);
-    CHECK_GPU(*rs_out); CHECK_DTYPE(*rs_out, at::kFloat); CHECK_CONTIG(*rs_out);
-    CHECK_GPU(*cnt); CHECK_DTYPE(*cnt, at::kInt); CHECK_CONTIG(*cnt);
-    TORCH_CHECK(ss->numel() >= (int64_t)2 * ((N + 255) / 256) * M && rs_out->numel() >= M &&
-                    cnt->numel() >= (M + 255) / 256, "gemm4w: ss / rs_out / cnt too small");
-    TORCH_CHECK(C.is_contiguous(), "gemm4w: the row-sum epilogue writes a contiguous C");
+    if (rs_mode == 1) {
+      TORCH_CHECK(epi == 0 || epi == 2, "gemm4w: row scales go with the plain or SwiGLU epilogue");
+      TORCH_CHECK(P >= 1 && P <= 16 && ss->numel() >= P * (int64_t)M, "gemm4w: ss needs P (1..16) x M partials");
+    } else {
+      TORCH_CHECK(rs_mode == 2 && epi == 1 && bn == 256, "gemm4w: row sums of squares need the residual epilogue, bn 256");
+      TORCH_CHECK(ss->numel() >= (int64_t)((N + 255) / 256) * M, "gemm4w: ss needs N/256 x M partials");
+    }
     ssp = ss->data_ptr<float>();
-    rop = rs_out->data_ptr<float>();
-    cp = cnt->data_ptr<int>();
   }
   CHECK_RC(lwc_gemm4w(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
-                      (int)epi, (int)bn, rsp, ssp, rop, cp, (float)eps, (int)var, cur_stream()),
+                      (int)epi, (int)bn, ssp, (int)rs_mode, (int)P, (float)eps, (int)var, cur_stream()),
            "gemm4w");
 }
 
-// rs[r] = rsqrt(mean(x[r]^2) + eps): the row scales of the folded RMSNorm for the first projection of a chain
-void rms_rowscale(const at::Tensor& x, at::Tensor& rs, double eps) {
-  CHECK_BF16(x); CHECK_CONTIG(x); CHECK_GPU(rs); CHECK_DTYPE(rs, at::kFloat); CHECK_CONTIG(rs);
-  TORCH_CHECK(x.dim() == 2 && rs.numel() >= x.size(0), "rms_rowscale: x [M, d], rs [>= M]");
-  CHECK_RC(lwc_rms_rowscale(x.data_ptr(), rs.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (float)eps,
-                            cur_stream()),
-           "rms_rowscale");
+// ss[r] = sum(x[r]^2): the single partial of the folded RMSNorm for the first projection of a chain
+void rms_rowsumsq(const at::Tensor& x, at::Tensor& ss) {
+  CHECK_BF16(x); CHECK_CONTIG(x); CHECK_GPU(ss); CHECK_DTYPE(ss, at::kFloat); CHECK_CONTIG(ss);
+  TORCH_CHECK(x.dim() == 2 && ss.numel() >= x.size(0), "rms_rowsumsq: x [M, d], ss [>= M]");
+  CHECK_RC(lwc_rms_rowsumsq(x.data_ptr(), ss.data_ptr<float>(), (int)x.size(0), (int)x.size(1), cur_stream()),
+           "rms_rowsumsq");
 }
 
 void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& row_off,
@@ -875,7 +864,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grouped_gemm", &grouped_gemm);
   m.def("gemm8p", &gemm8p);
   m.def("gemm4w", &gemm4w);
-  m.def("rms_rowscale", &rms_rowscale);
+  m.def("rms_rowsumsq", &rms_rowsumsq);
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
   m.def("moe_combine", &moe_combine);

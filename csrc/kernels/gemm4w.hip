@@ -45,16 +45,15 @@
 // diag(1/rms(x)) . (x . (W diag(g))^T), so with the norm weight g folded into W once at load, a
 // projection of the raw residual stream only needs its accumulator rows scaled by r = 1/rms(x) — the
 // norm pass (a read and a write of every row) disappears.
-//   RS 1 (consumer: qkv, gate|up, lm_head): r for the tile's 256 rows arrives in LDS by ONE LDS-DMA piece
-//        of wave 0, issued before the tile's first K-tile pieces (so the prologue's counted wait retires
-//        it; double-buffered by tile parity for the cross-tile prefetch of VAR 64); the epilogue scales
-//        its rows before SwiGLU / the store.
-//   RS 2 (producer: the o / down projections' residual epilogue): every wave sums the squares of its
-//        128 output columns (the bf16-rounded new residual stream) per row and stores the partial at
-//        ss[2 tn + wn][row]; the last of an m-tile's tiles_n workgroups to finish (agent-scope release /
-//        acquire around one arrival counter, cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
-//        adds the 2 tiles_n partials of its 256 rows in a fixed order and writes r = rsqrt(sum / N + eps)
-//        for the next projection, then re-arms the counter.
+//   RS 2 (producer: the o / down projections' residual epilogue): each wave sums the squares of its 128
+//        output columns (the bf16-rounded new residual stream) per row, the two waves sharing rows add
+//        theirs through LDS, and the tile stores ONE partial per row: ss[tn][row] (tiles_n partials, fixed
+//        order, no atomics, no cross-workgroup hand-off).
+//   RS 1 (consumer: qkv, gate|up, lm_head): the P partials of the tile's 256 rows arrive in LDS by P LDS-DMA
+//        pieces (1 KiB each) issued before the tile's first K-tile pieces (the prologue's counted wait
+//        retires them); after the prologue barrier thread t adds row t's partials in order and keeps
+//        r = rsqrt(sum / K + eps) in LDS; the epilogue scales its rows before SwiGLU / the store.  The
+//        first projection of a chain reads P = 1 partial from rms_rowsumsq (norm.hip).
 #include <algorithm>
 #include <cstdlib>
 
@@ -76,11 +75,9 @@ struct Params {
   int tiles_m, tiles_n, KT;
   int gm;
   int wpx, tiles;
-  const float* rs;  // RS 1: row scales [M]
-  float* ss;        // RS 2: row sum-of-squares partials [2 tiles_n][M]
-  float* rs_out;    // RS 2: finished row scales [M]
-  int* cnt;         // RS 2: arrival counter per m-tile (zero between launches)
-  float eps;        // RS 2
+  float* ss;        // RS 1: row sum-of-squares partials [P][M] (read); RS 2: [tiles_n][M] (written)
+  int P;            // RS 1: partials per row (<= 16)
+  float eps;        // RS 1
 };
 
 template <int NT>
@@ -140,12 +137,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
-  // RS 1: the row-scale double buffer (2 x 256 fp32) after everything else in LDS
-  constexpr int RSOFF = PAP ? G::LdsPap : G::Lds;
-  // one LDS-DMA piece (64 lanes x 16 B = 256 rows x fp32) of the row scales of m-tile rows [m, m + 256)
-  auto rs_dma = [&](int m, int par) {
-    const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.rs + m, (p.M - m) * 4);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (__attribute__((address_space(3))) void*)(smem + RSOFF + par * 1024),
+  // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
+  // block-staged epilogue, VAR 32); RS 2: the four waves' 128 row sums (2 KiB) at the same place
+  constexpr int RSOFF = G::Lds, RSV = RSOFF + 16384;
+  // LDS-DMA piece k (64 lanes x 16 B = 256 rows x fp32) of partial k of m-tile rows [m, m + 256)
+  auto ss_dma = [&](int m, int k) {
+    const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.M + m, (p.M - m) * 4);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (__attribute__((address_space(3))) void*)(smem + RSOFF + k * 1024),
                                              16, (uint32_t)((threadIdx.x & 63) * 16), 0, 0, 0);
   };
 
@@ -160,7 +158,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r16 = lane & 15, q = lane >> 4;
     const int wm = wid >> 1, wn = wid & 1;
-    const int rs_par = round & 1;
 
     // DMA: piece i of wave wid covers operand rows i*32 + wid*8 + lane/8, LDS chunk lane%8, which holds
     // global chunk (lane%8) ^ ((row >> 1) & 7); (row >> 1) & 7 does not depend on i.
@@ -216,8 +213,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // (residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
     // there is no next tile to prefetch, and 32 up-front residual chunks per lane would spill)
     if (!PAP || round == 0) {
-      if constexpr (RS == 1) {
-        if (wid == 0) rs_dma(m0, rs_par);  // oldest VMEM op of wave 0: the counted wait below retires it
+      if constexpr (RS == 1) {  // the oldest VMEM ops of each wave: the counted wait below retires them
+        for (int k = wid; k < p.P; k += 4) ss_dma(m0, k);
       }
       stage(smem, 0);
       if (nt > 1) stage(smem + G::Buf, 1);
@@ -228,6 +225,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       G4_VM(0);
     }
     G4_BAR();
+    if constexpr (RS == 1) {
+      // row tid's scale from its partials (the main loop's first barrier publishes it to the epilogues)
+      const float* part = reinterpret_cast<const float*>(smem + RSOFF);
+      float sum = 0.f;
+      for (int k = 0; k < p.P; ++k) sum += part[k * 256 + tid];
+      reinterpret_cast<float*>(smem + RSV)[tid] = rsqrtf(sum / (float)p.K + p.eps);
+    }
 #pragma unroll
     for (int k = 0; k < G::Reads; ++k) rd1(smem, offA0, offB0, xa, xb, k);
 
@@ -434,9 +438,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       if (ntile < p.tiles) {
         int um, un;
         tile_mn(p, ntile, um, un);
-        if constexpr (RS == 1) {
-          if (wid == 0) rs_dma(um * 256, rs_par ^ 1);  // older than the pieces below (same counted wait)
-        }
+
         const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
         const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
@@ -462,12 +464,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         float4v t[NT];
 #pragma unroll
         for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
-        if constexpr (RS == 1) {
-          const float4v sc = *reinterpret_cast<const float4v*>(smem + RSOFF + rs_par * 1024 +
-                                                               (wm * 128 + i * 16 + 4 * q) * 4);
-#pragma unroll
-          for (int jj = 0; jj < NT; ++jj) t[jj] *= sc;
-        }
         if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
           for (int h = 0; h < NT / 4; ++h)
@@ -530,8 +526,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
       for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
       if constexpr (RS == 1) {
-        const float4v sc = *reinterpret_cast<const float4v*>(smem + RSOFF + rs_par * 1024 +
-                                                             (wm * 128 + i * 16 + 4 * q) * 4);
+        const float4v sc = *reinterpret_cast<const float4v*>(smem + RSV + (wm * 128 + i * 16 + 4 * q) * 4);
 #pragma unroll
         for (int jj = 0; jj < NT; ++jj) t[jj] *= sc;
       }
@@ -623,7 +618,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             sq += __shfl_xor(sq, 4);
             sq += __shfl_xor(sq, 2);
             sq += __shfl_xor(sq, 1);
-            if ((lane & 15) == 0 && gm < p.M) p.ss[(size_t)(2 * tn + wn) * p.M + gm] = sq;
+            if ((lane & 15) == 0) reinterpret_cast<float*>(smem + RSOFF)[wid * 128 + row] = sq;
           }
         }
       }
@@ -640,41 +635,24 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }
     __syncthreads();  // LDS free for the next tile
     if constexpr (RS == 2) {
-      // the m-tile's last arriver finishes its rows' scales: release (every wave's partial stores done,
-      // then one agent-scope release before the arrival), acquire on the last arriver before it reads
-      // the other workgroups' partials; the "I am last" flag travels through the one LDS array
-      int* last = reinterpret_cast<int*>(smem);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(p.cnt + tm, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last = old == p.tiles_n - 1;
-      }
-      __syncthreads();
-      if (*last) {
-        if (threadIdx.x == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the two waves of each 128-row half add their row sums (written before the barrier above) in a fixed
+      // order and store the tile's partial; the next tile's epilogue rewrites them only after its main loop
+      if (wn == 0) {
+        const float* rsum = reinterpret_cast<const float*>(smem + RSOFF);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = lane + 64 * h, gm = m0 + wm * 128 + row;
+          if (gm < p.M) p.ss[(size_t)tn * p.M + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
         }
-        __syncthreads();
-        const int row = m0 + (int)threadIdx.x;
-        if (row < p.M) {
-          float sum = 0.f;
-          for (int k = 0; k < 2 * p.tiles_n; ++k) sum += p.ss[(size_t)k * p.M + row];
-          p.rs_out[row] = rsqrtf(sum / (float)p.N + p.eps);
-        }
-        if (threadIdx.x == 0) p.cnt[tm] = 0;  // re-armed for the next launch (ordered by the kernel boundary)
       }
-      __syncthreads();  // the flag word is LDS of the next tile
     }
   }
 }
 
 template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = (VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds) + (RS == 1 ? 2048 : 0);
+  constexpr int lds = (VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
+                      (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR, RS>,
@@ -753,25 +731,24 @@ int device_cus() {
 
 // C = A . W^T (epilogue epi as lwc_gemm8p: 0 plain, 1 + residual, 2 SwiGLU over 32-row gate/up interleaved W,
 // 3 + bias, 4 gelu(. + bias)); bn = 256 or 192 (W rows per tile; SwiGLU needs 256).  Requires K % 64 == 0,
-// N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): rs [M] (epi 0 / 2) scales the accumulator rows;
-// ss [2 N/256][M] + rs_out [M] + cnt [ceil(M/256)] (epi 1, bn 256) make the residual epilogue produce the next
-// projection's row scales rsqrt(mean(out^2) + eps).  var: schedule variant (0 = LWC_G4_VAR / 32).
+// N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): ss [P][M] with P >= 1 partial row sums of
+// squares (epi 0 / 2) scales the accumulator rows by rsqrt(sum / K + eps); ss [N/256][M] (epi 1, bn 256)
+// makes the residual epilogue write those partials of its output.  var: schedule variant (0 = LWC_G4_VAR / 32).
 extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
-                          int epi, int bn, const float* rs, float* ss, float* rs_out, int* cnt, float eps, int var,
-                          hipStream_t s) {
+                          int epi, int bn, float* ss, int rs_mode, int P, float eps, int var, hipStream_t s) {
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
   if ((long long)M * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
   if (epi == EPI_SWIGLU && (N % 64 != 0 || bn != 256)) return -1;
   if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
-  const int rsm = rs != nullptr ? 1 : (ss != nullptr ? 2 : 0);
-  if (rsm == 1 && epi != EPI_PLAIN && epi != EPI_SWIGLU) return -1;
-  if (rsm == 2 && (epi != EPI_RESIDUAL || bn != 256 || rs_out == nullptr || cnt == nullptr)) return -1;
+  if (rs_mode < 0 || rs_mode > 2 || (rs_mode && ss == nullptr)) return -1;
+  if (rs_mode == 1 && ((epi != EPI_PLAIN && epi != EPI_SWIGLU) || P < 1 || P > 16)) return -1;
+  if (rs_mode == 2 && (epi != EPI_RESIDUAL || bn != 256)) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
   const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
-           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, rs, ss, rs_out, cnt, eps};
-  return bn == 256 ? dispatch<8>(p, epi, s, var, rsm) : dispatch<6>(p, epi, s, var, rsm);
+           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, ss, P, eps};
+  return bn == 256 ? dispatch<8>(p, epi, s, var, rs_mode) : dispatch<6>(p, epi, s, var, rs_mode);
 }

@@ -229,10 +229,10 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restric
   }
 }
 
-// rs[r] = rsqrt(mean(x[r]^2) + eps), one wave per row: the row scales of an RMSNorm folded into the next
-// projection (gemm4w RS 1) for rows no residual epilogue produced them for (the embedding rows)
-__global__ void __launch_bounds__(256) rms_rowscale_kernel(const bf16_t* __restrict__ x, float* __restrict__ rs, int rows,
-                                                           int d, float eps) {
+// ss[r] = sum(x[r]^2), one wave per row: the (single) partial row sum of squares an RMSNorm folded into the
+// next projection (gemm4w RS 1) reads for rows no residual epilogue produced partials for (the embedding rows)
+__global__ void __launch_bounds__(256) rms_rowsumsq_kernel(const bf16_t* __restrict__ x, float* __restrict__ ss, int rows,
+                                                           int d) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const uint4v* xr = reinterpret_cast<const uint4v*>(x + (size_t)row * d);
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(256) rms_rowscale_kernel(const bf16_t* __restr
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane == 0) rs[row] = rsqrtf(s / (float)d + eps);
+  if (lane == 0) ss[row] = s;
 }
 
 static int norm_threads(int d) {
@@ -306,10 +306,10 @@ extern "C" int lwc_layernorm(const void* x, const void* residual, const void* g,
   return (int)hipGetLastError();
 }
 
-extern "C" int lwc_rms_rowscale(const void* x, float* rs, int rows, int d, float eps, hipStream_t s) {
+extern "C" int lwc_rms_rowsumsq(const void* x, float* ss, int rows, int d, hipStream_t s) {
   using namespace lwc;
   if (d % 8 != 0) return -1;
   if (rows == 0) return 0;
-  rms_rowscale_kernel<<<(rows + 3) / 4, 256, 0, s>>>((const bf16_t*)x, rs, rows, d, eps);
+  rms_rowsumsq_kernel<<<(rows + 3) / 4, 256, 0, s>>>((const bf16_t*)x, ss, rows, d);
   return (int)hipGetLastError();
 }

@@ -18,11 +18,11 @@ Folded RMSNorm (decode chain, dense bf16 on the GPU): every norm weight is folde
 reads it at load (W_qkv diag(g_attn), W_gate_up diag(g_mlp), W_lm_head diag(g_final); the norm weights become
 ones, so the unfolded path computes the same function), and a decode step where the chain was timed faster
 (:meth:`LlamaModel.tune_gemms`) runs NO norm kernel: the o / down projections' residual epilogues emit the
-row scales 1/rms of the new residual stream, which the next projection (qkv, gate|up, lm_head) applies to
-its accumulator rows (gemm4w RS modes, csrc/kernels/gemm4w.hip):
-    rs = rms_rowscale(embedding)                  (once)
-    qkv = gemm4w(x, W_qkv', rs)   ...   x += gemm4w(attn, W_o) -> rs
-    act = gemm4w(x, W_gu', rs, SwiGLU)   x += gemm4w(act, W_d) -> rs     ...   logits = gemm4w(x, W_lm', rs)  Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over
+partial row sums of squares of the new residual stream, from which the next projection (qkv, gate|up,
+lm_head) scales its accumulator rows by 1/rms (gemm4w RS modes, csrc/kernels/gemm4w.hip):
+    ss = rms_rowsumsq(embedding)                  (once)
+    qkv = gemm4w(x, W_qkv', ss)   ...   x += gemm4w(attn, W_o) -> ss
+    act = gemm4w(x, W_gu', ss, SwiGLU)   x += gemm4w(act, W_d) -> ss     ...   logits = gemm4w(x, W_lm', ss)  Prefill uses the same layer with the varlen causal flash-attention kernel (K4) over
 the fresh k/v of the qkv buffer; mixed chunked-prefill steps (forward_mixed) send decode rows to K3 and
 prompt-chunk rows to K4's paged-KV mode; the k/v are scattered into the paged cache in the RoPE pass.
 """
@@ -224,19 +224,19 @@ class LlamaModel:
     # ------------------------------------------------------------------ forward
     def _chain_layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool,
                       qkv_bn: int) -> torch.Tensor:
-        """The folded-RMSNorm decode chain (module docstring): x_res is updated in place; the row scales of the
-        final residual stream are left in ``self.chain.rs`` for the lm_head."""
+        """The folded-RMSNorm decode chain (module docstring): x_res is updated in place; the partial row sums of
+        squares of the final residual stream are left in ``self.chain`` for the lm_head."""
         cfg, ch = self.cfg, self.chain
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
-        ops.rms_rowscale(x_res, ch.rs, cfg.rms_eps)
+        ops.rms_rowsumsq(x_res, ch)
         for li, L in enumerate(self.layers):
-            qkv = ops.gemm4w(x_res, L.wqkv, bn=qkv_bn, rs=ch.rs)
+            qkv = ops.gemm4w(x_res, L.wqkv, bn=qkv_bn, chain=ch)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
                               rope_q=rope_q)
             attn = attn_fn(qkv, li)
             ops.gemm4w(attn.reshape(T, Hq * D), L.wo, residual=x_res, out=x_res, chain=ch)
-            act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, rs=ch.rs)
+            act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
             ops.gemm4w(act, L.w_down, residual=x_res, out=x_res, chain=ch)
         return x_res
 
@@ -389,16 +389,19 @@ class LlamaModel:
         force = os.environ.get("LWC_NORM_CHAIN")
         x_res = x.clone()
         ch, eps = self.chain, cfg.rms_eps
+        if (cfg.hidden + 255) // 256 > 16:
+            self.chain_m[M] = (False, 192)
+            return
         ones = torch.ones(cfg.hidden, device=self.device, dtype=self.dtype)
 
         def chained(bn):
             def run():
-                ops.rms_rowscale(x_res, ch.rs, eps)
-                ops.gemm4w(x_res, L.wqkv, bn=bn, rs=ch.rs)
+                ops.rms_rowsumsq(x_res, ch)
+                ops.gemm4w(x_res, L.wqkv, bn=bn, chain=ch)
                 ops.gemm4w(xa, L.wo, residual=x_res, out=x_res, chain=ch)
-                ops.gemm4w(x_res, L.w_gate_up, swiglu=True, rs=ch.rs)
+                ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
                 ops.gemm4w(xf, L.w_down, residual=x_res, out=x_res, chain=ch)
-                ops.gemm4w(x_res, self.lm_head, rs=ch.rs)
+                ops.gemm4w(x_res, self.lm_head, chain=ch)
             return run
 
         def unchained():
@@ -459,7 +462,7 @@ class LlamaModel:
 
         if self.chain_ok(B):
             x = self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, self.chain_m[B][1])
-            return ops.gemm4w(x, self.lm_head, rs=self.chain.rs)
+            return ops.gemm4w(x, self.lm_head, chain=self.chain)
         h = self._layers(x, cache, positions, slots, attn_fn, rope_q=not q_at_load)
         return self._proj(h, self.lm_head)
 

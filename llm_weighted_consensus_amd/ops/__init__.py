@@ -387,17 +387,16 @@ def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
 
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
-           gelu: bool = False, bn: int = 256, rs: Optional[torch.Tensor] = None, chain: "Optional[NormChain]" = None,
-           var: int = 0) -> torch.Tensor:
+           gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0) -> torch.Tensor:
     """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
     a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
     workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
     (interleaved gate|up W, bn 256), ``bias`` (+ ``gelu``).
 
-    Folded RMSNorm (the decode chain, :class:`NormChain`): ``rs`` [M] fp32 scales the accumulator rows
-    (plain / SwiGLU: rmsnorm(x) . W^T with the norm weight folded into W); ``chain`` with ``residual`` makes
-    the residual epilogue also produce the next projection's row scales in ``chain.rs``.  ``var``: schedule
-    variant (0 = default)."""
+    Folded RMSNorm (the decode chain, :class:`NormChain`): with ``chain`` a plain / SwiGLU projection scales
+    its accumulator rows by 1/rms of its input rows from the chain's partial row sums of squares (the norm
+    weight folded into W: rmsnorm(x) . W^T), and a residual projection writes the partials of its output for
+    the next one.  ``var``: schedule variant (0 = default)."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
@@ -409,36 +408,42 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
         if gelu:
             raise ValueError("gemm4w: gelu needs a bias")
         epi = 2 if swiglu else (1 if residual is not None else 0)
-    if chain is not None and epi != 1:
-        raise ValueError("gemm4w: chain= (row sums of squares) goes with the residual epilogue")
-    ss = ro = cnt = None
-    eps = 0.0
-    if chain is not None:
-        ss, ro, cnt, eps = chain.ss, chain.rs, chain.cnt, chain.eps
-    kernels().gemm4w(A, W, out, residual, epi, int(bn), rs, ss, ro, cnt, float(eps), int(var))
+    if chain is None:
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var))
+    elif epi == 1:
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var))
+        chain.P = (N + 255) // 256
+    elif epi in (0, 2):
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 1, chain.P, chain.eps, int(var))
+    else:
+        raise ValueError("gemm4w: chain= goes with the plain, SwiGLU or residual epilogue")
     return out
 
 
 class NormChain:
-    """Buffers of the folded-RMSNorm decode chain (csrc/kernels/gemm4w.hip head): ``rs`` [max_rows] fp32 row
-    scales (written by a residual GEMM's last-arriving workgroups or :func:`rms_rowscale`, read by the next
-    projection), ``ss`` [2 ceil(d/256), max_rows] fp32 partial sums of squares, ``cnt`` [ceil(max_rows/256)]
-    int32 arrival counters (zero; every launch leaves them zero).  Allocated once, outside graph capture."""
+    """Buffers of the folded-RMSNorm decode chain (csrc/kernels/gemm4w.hip head): ``ss`` [16, max_rows] fp32
+    partial row sums of squares of the residual stream — written by a residual projection (``P`` = its
+    N / 256 partials) or :func:`rms_rowsumsq` (P = 1), read by the next plain / SwiGLU projection, which scales
+    its rows by rsqrt(sum / K + eps).  Allocated once, outside graph capture (captured graphs keep its address)."""
 
     def __init__(self, max_rows: int, d: int, eps: float, device):
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             raise RuntimeError("NormChain buffers must be allocated outside hipGraph capture")
+        if (d + 255) // 256 > 16:
+            raise ValueError("NormChain: at most 16 partials per row (d <= 4096)")
         self.max_rows, self.d, self.eps = int(max_rows), int(d), float(eps)
-        self.rs = torch.ones(self.max_rows, dtype=torch.float32, device=device)
-        self.ss = torch.zeros(2 * ((d + 255) // 256) * self.max_rows, dtype=torch.float32, device=device)
-        self.cnt = torch.zeros((self.max_rows + 255) // 256, dtype=torch.int32, device=device)
+        self.ss = torch.zeros(16, self.max_rows, dtype=torch.float32, device=device)
+        self.P = 1
+
+    def scales(self, M: int) -> torch.Tensor:
+        """The row scales the consumers apply, for tests: rsqrt(sum of the P partials / d + eps)."""
+        return torch.rsqrt(self.ss[:self.P, :M].sum(0) / self.d + self.eps)
 
 
-def rms_rowscale(x: torch.Tensor, rs: torch.Tensor, eps: float) -> torch.Tensor:
-    """rs[r] = rsqrt(mean(x[r]^2) + eps) (the folded RMSNorm's row scales of rows no residual epilogue
-    produced them for, e.g. the embedding rows); returns rs."""
-    kernels().rms_rowscale(x, rs, float(eps))
-    return rs
+def rms_rowsumsq(x: torch.Tensor, chain: "NormChain") -> None:
+    """Start a chain: chain.ss[0] = the row sums of squares of x (one partial, P = 1)."""
+    kernels().rms_rowsumsq(x, chain.ss)
+    chain.P = 1
 
 
 _G8_WS: dict = {}

@@ -479,6 +479,57 @@ def small(dev):
         print(f"silu_mul T={T}: {us:6.1f} us", flush=True)
 
 
+def chain_ab(dev):
+    """Folded-RMSNorm decode chain at the headline's decode batch (Llama-3-8B shapes, M = 4096; random
+    operands): per projection the unfolded backends (hipBLASLt / gemm4w, + the norm kernel) vs the row-scaled
+    gemm4w modes, then one whole layer + lm_head both ways.  Interleaved rounds, median of 5."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    M, d, Fd, V, QKV = int(os.environ.get("CHAIN_M", "4096")), 4096, 14336, 128256, 6144
+    r = lambda *s: ((torch.rand(*s, device=dev) * 2 - 1) / s[-1] ** 0.5).to(torch.bfloat16)  # noqa: E731
+    x = (torch.rand(M, d, device=dev) * 2 - 1).to(torch.bfloat16)
+    xa, xf = r(M, d) * 8, r(M, Fd) * 8
+    wqkv, wo, wgu, wd, wl = r(QKV, d), r(d, d), ops.swiglu_interleave(r(2 * Fd, d)), r(d, Fd), r(V, d)
+    ones = torch.ones(d, device=dev, dtype=torch.bfloat16)
+    ch = ops.NormChain(M, d, 1e-5, dev)
+    acc = x.clone()
+    ops.rms_rowsumsq(acc, ch)
+    runs = {
+        "rmsnorm": lambda: ops.rmsnorm(acc, ones, 1e-5),
+        "rowsumsq": lambda: ops.rms_rowsumsq(acc, ch),
+        "qkv blas": lambda: F.linear(x, wqkv),
+        "qkv g4n192": lambda: ops.gemm4w(x, wqkv, bn=192),
+        "qkv g4n192 rs": lambda: ops.gemm4w(x, wqkv, bn=192, chain=ch),
+        "qkv g4 rs": lambda: ops.gemm4w(x, wqkv, chain=ch),
+        "o blas res": lambda: acc.addmm_(xa, wo.t()),
+        "o g4 res": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc),
+        "o g4 res+ss": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc, chain=ch),
+        "gu g4": lambda: ops.gemm4w(x, wgu, swiglu=True),
+        "gu g4 rs": lambda: ops.gemm4w(x, wgu, swiglu=True, chain=ch),
+        "down blas res": lambda: acc.addmm_(xf, wd.t()),
+        "down g4 res": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc),
+        "down g4 res+ss": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc, chain=ch),
+        "lm blas": lambda: F.linear(x, wl),
+        "lm g4": lambda: ops.gemm4w(x, wl),
+        "lm g4 v64": lambda: ops.gemm4w(x, wl, var=64),
+        "lm g4 rs": lambda: ops.gemm4w(x, wl, chain=ch),
+    }
+    res = {k: [] for k in runs}
+    for _ in range(5):
+        for k, fn in runs.items():
+            res[k].append(timeit(fn, iters=10, warm=2))
+    for k, t in res.items():
+        print(f"chain {M} {k}: {sorted(t)[2]:8.1f} us", flush=True)
+    med = {k: sorted(t)[2] for k, t in res.items()}
+    base = (2 * med["rmsnorm"] + min(med["qkv blas"], med["qkv g4n192"]) + med["o blas res"] + med["gu g4"]
+            + med["down blas res"])
+    chain = med["qkv g4n192 rs"] + med["o g4 res+ss"] + med["gu g4 rs"] + med["down g4 res+ss"]
+    print(f"chain {M} per layer: unfolded {base:.1f} us, chain {chain:.1f} us; lm_head: unfolded "
+          f"{med['rmsnorm'] + med['lm blas']:.1f}, chain {med['lm g4 rs']:.1f}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="*", default=["gemm", "attn", "sample", "small"])
@@ -492,6 +543,8 @@ def main():
         grouped(dev)
     if "g4ab" in a.what:
         gemm4w_ab(dev)
+    if "chain" in a.what:
+        chain_ab(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:

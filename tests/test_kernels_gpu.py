@@ -1216,40 +1216,44 @@ def test_gemm4w(gpu, M, N, K, epi, bn, var, monkeypatch):
             _close(out, want, 3e-2, 1e-2)
 
 
-@pytest.mark.parametrize("M,N,K,epi,bn", [(300, 4096, 256, "plain", 256), (4096 + 37, 6144, 512, "plain", 192),
-                                         (1000, 1536, 320, "swiglu", 256), (257, 128256 // 16, 128, "plain", 256)])
-def test_gemm4w_rowscale(gpu, M, N, K, epi, bn):
-    """Folded RMSNorm, consumer side (RS 1): rows of the accumulator scaled by rs[row] before the epilogue
-    (plain, SwiGLU), ragged M (the row-scale DMA past the last row reads zeros), multi-round tiles; vs the fp32
-    product of the scaled rows.  Twice: the row-scale double buffer across tiles and launches."""
+@pytest.mark.parametrize("M,N,K,epi,bn,P", [(300, 4096, 256, "plain", 256, 1), (4096 + 37, 6144, 512, "plain", 192, 16),
+                                           (1000, 1536, 320, "swiglu", 256, 3), (257, 128256 // 16, 128, "plain", 256, 2)])
+def test_gemm4w_rowscale(gpu, M, N, K, epi, bn, P):
+    """Folded RMSNorm, consumer side (RS 1): P partial row sums of squares [P, M] arrive by LDS-DMA, the
+    prologue reduces them to r = rsqrt(sum / K + eps) and the epilogue scales the accumulator rows (plain,
+    SwiGLU), ragged M (partials past the last row read zeros), multi-round tiles; vs the fp32 product of the
+    scaled rows.  Twice (the LDS regions across rounds and launches)."""
     from llm_weighted_consensus_amd import ops
 
     torch.manual_seed(M + N + K)
     A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
-    rs = torch.rand(M, device=gpu) * 2 + 0.1
+    chain = ops.NormChain(M + 64, 256 * P, 1e-5, gpu)
+    chain.ss[:P, :M] = torch.rand(P, M, device=gpu) * K / P + 0.01
+    chain.P = P
+    rs = torch.rsqrt(chain.ss[:P, :M].sum(0) / K + 1e-5)
     ref = rs[:, None] * (A.float() @ W.float().t())
     for _ in range(2):
         if epi == "swiglu":
             F = N // 2
-            out = ops.gemm4w(A, ops.swiglu_interleave(W), swiglu=True, bn=bn, rs=rs)
+            out = ops.gemm4w(A, ops.swiglu_interleave(W), swiglu=True, bn=bn, chain=chain)
             _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
         else:
-            _close(ops.gemm4w(A, W, bn=bn, rs=rs), ref, 3e-2, 1e-2)
+            _close(ops.gemm4w(A, W, bn=bn, chain=chain), ref, 3e-2, 1e-2)
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (300, 4096, 512), (1000, 1024, 128), (4096 + 37, 4096, 64)])
 def test_gemm4w_residual_rowsum(gpu, M, N, K):
-    """Folded RMSNorm, producer side (RS 2): the residual epilogue writes C = R + A.W^T and the m-tiles' last
-    arriving workgroups finish rs = rsqrt(mean(C^2) + eps) over the bf16 output rows (fp32 reference on the
-    returned C), leaving every arrival counter zero; three launches in a row (counters re-armed), and the
-    chain end to end: an RS 1 projection of C with the produced scales == the projection of rmsnorm(C)."""
+    """Folded RMSNorm, producer side (RS 2): the residual epilogue writes C = R + A.W^T and the N/256 partial
+    row sums of squares of the bf16 output (fp32 reference on the returned C); three launches in a row; then
+    the chain end to end: an RS 1 projection of C with those partials == the projection of rmsnorm(C), and a
+    chain started by rms_rowsumsq gives the same scales."""
     from llm_weighted_consensus_amd import ops
 
     torch.manual_seed(M + N + K)
     eps = 1e-5
     chain = ops.NormChain(M + 64, N, eps, gpu)
-    chain.rs.fill_(-7.0)
+    chain.ss.fill_(-7.0)
     A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
     for it in range(3):
@@ -1258,23 +1262,18 @@ def test_gemm4w_residual_rowsum(gpu, M, N, K):
         C = ops.gemm4w(A, W, residual=R, out=R, chain=chain)
         torch.cuda.synchronize()
         _close(C, want, 3e-2, 1e-2)
-        rs_ref = torch.rsqrt(C.float().pow(2).mean(-1) + eps)
-        assert torch.allclose(chain.rs[:M], rs_ref, rtol=1e-5, atol=1e-6), (it, (chain.rs[:M] - rs_ref).abs().max())
-        assert int(chain.cnt.abs().sum()) == 0
-        assert bool((chain.rs[M:] == -7.0).all())  # rows past M untouched
+        P = N // 256
+        assert chain.P == P
+        parts = C.float().pow(2).view(M, P, 256).sum(-1).t()
+        assert torch.allclose(chain.ss[:P, :M], parts, rtol=1e-5, atol=1e-4), (it, (chain.ss[:P, :M] - parts).abs().max())
+        assert bool((chain.ss[:P, M:] == -7.0).all())  # rows past M untouched
     Wn = (torch.randn(512, N, device=gpu) / N ** 0.5).to(torch.bfloat16)
-    g = torch.ones(N, device=gpu, dtype=torch.bfloat16)
-    h = ops.rmsnorm(C, g, eps)
-    _close(ops.gemm4w(C, Wn, rs=chain.rs[:M].contiguous()), h.float() @ Wn.float().t(), 3e-2, 1e-2)
-
-
-def test_rms_rowscale(gpu):
-    from llm_weighted_consensus_amd import ops
-
-    x = torch.randn(1000, 4096, device=gpu).to(torch.bfloat16)
-    rs = torch.empty(1000, device=gpu)
-    ops.rms_rowscale(x, rs, 1e-5)
-    assert torch.allclose(rs, torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5), rtol=1e-5)
+    h = ops.rmsnorm(C, torch.ones(N, device=gpu, dtype=torch.bfloat16), eps)
+    want = h.float() @ Wn.float().t()
+    _close(ops.gemm4w(C, Wn, chain=chain), want, 3e-2, 1e-2)
+    ops.rms_rowsumsq(C, chain)
+    assert chain.P == 1 and torch.allclose(chain.ss[0, :M], C.float().pow(2).sum(-1), rtol=1e-5)
+    _close(ops.gemm4w(C, Wn, chain=chain), want, 3e-2, 1e-2)
 
 
 @pytest.mark.parametrize("n,d,k", [(37, 1024, 5), (1000, 1024, 16), (70000, 384, 64), (300, 4096, 1)])
