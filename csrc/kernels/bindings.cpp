@@ -26,8 +26,8 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
                      int, int, int, int, int, int, long long, int, float*, int, long long, hipStream_t);
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
-int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, float,
-               int, hipStream_t);
+int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, int,
+               float, int, hipStream_t);
 int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, int, int, const void*, void*, int, hipStream_t);
@@ -429,17 +429,19 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
   if (rs_mode) {
     TORCH_CHECK(ss.has_value() && ss->defined(), "gemm4w: rs_mode needs ss");
     CHECK_GPU(*ss); CHECK_DTYPE(*ss, at::kFloat); CHECK_CONTIG(*ss);
+    TORCH_CHECK(ss->dim() == 2 && ss->size(1) >= M && ss->size(1) % 4 == 0, "gemm4w: ss [partials, >= M (x4)]");
     if (rs_mode == 1) {
       TORCH_CHECK(epi == 0 || epi == 2, "gemm4w: row scales go with the plain or SwiGLU epilogue");
-      TORCH_CHECK(P >= 1 && P <= 16 && ss->numel() >= P * (int64_t)M, "gemm4w: ss needs P (1..16) x M partials");
+      TORCH_CHECK(P >= 1 && P <= 16 && ss->size(0) >= P, "gemm4w: ss needs P (1..16) partials");
     } else {
       TORCH_CHECK(rs_mode == 2 && epi == 1 && bn == 256, "gemm4w: row sums of squares need the residual epilogue, bn 256");
-      TORCH_CHECK(ss->numel() >= (int64_t)((N + 255) / 256) * M, "gemm4w: ss needs N/256 x M partials");
+      TORCH_CHECK(ss->size(0) >= (N + 255) / 256, "gemm4w: ss needs N/256 partials");
     }
     ssp = ss->data_ptr<float>();
   }
   CHECK_RC(lwc_gemm4w(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
-                      (int)epi, (int)bn, ssp, (int)rs_mode, (int)P, (float)eps, (int)var, cur_stream()),
+                      (int)epi, (int)bn, ssp, ssp ? (int)ss->size(1) : 0, (int)rs_mode, (int)P, (float)eps, (int)var,
+                      cur_stream()),
            "gemm4w");
 }
 

@@ -75,8 +75,9 @@ struct Params {
   int tiles_m, tiles_n, KT;
   int gm;
   int wpx, tiles;
-  float* ss;        // RS 1: row sum-of-squares partials [P][M] (read); RS 2: [tiles_n][M] (written)
+  float* ss;        // RS 1: row sum-of-squares partials [P][ssld] (read); RS 2: [tiles_n][ssld] (written)
   int P;            // RS 1: partials per row (<= 16)
+  int ssld;         // floats between partials (a multiple of 4: 16-byte aligned LDS-DMA sources)
   float eps;        // RS 1
 };
 
@@ -142,7 +143,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   constexpr int RSOFF = G::Lds, RSV = RSOFF + 16384;
   // LDS-DMA piece k (64 lanes x 16 B = 256 rows x fp32) of partial k of m-tile rows [m, m + 256)
   auto ss_dma = [&](int m, int k) {
-    const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.M + m, (p.M - m) * 4);
+    const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.ssld + m, (p.M - m) * 4);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (__attribute__((address_space(3))) void*)(smem + RSOFF + k * 1024),
                                              16, (uint32_t)((threadIdx.x & 63) * 16), 0, 0, 0);
   };
@@ -642,7 +643,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int row = lane + 64 * h, gm = m0 + wm * 128 + row;
-          if (gm < p.M) p.ss[(size_t)tn * p.M + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
+          if (gm < p.M) p.ss[(size_t)tn * p.ssld + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
         }
       }
     }
@@ -731,24 +732,24 @@ int device_cus() {
 
 // C = A . W^T (epilogue epi as lwc_gemm8p: 0 plain, 1 + residual, 2 SwiGLU over 32-row gate/up interleaved W,
 // 3 + bias, 4 gelu(. + bias)); bn = 256 or 192 (W rows per tile; SwiGLU needs 256).  Requires K % 64 == 0,
-// N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): ss [P][M] with P >= 1 partial row sums of
-// squares (epi 0 / 2) scales the accumulator rows by rsqrt(sum / K + eps); ss [N/256][M] (epi 1, bn 256)
+// N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): ss [P][ssld] with P >= 1 partial row sums of
+// squares (epi 0 / 2) scales the accumulator rows by rsqrt(sum / K + eps); ss [N/256][ssld] (epi 1, bn 256)
 // makes the residual epilogue write those partials of its output.  var: schedule variant (0 = LWC_G4_VAR / 32).
 extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
-                          int epi, int bn, float* ss, int rs_mode, int P, float eps, int var, hipStream_t s) {
+                          int epi, int bn, float* ss, int ssld, int rs_mode, int P, float eps, int var, hipStream_t s) {
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
   if ((long long)M * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
   if (epi == EPI_SWIGLU && (N % 64 != 0 || bn != 256)) return -1;
   if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
-  if (rs_mode < 0 || rs_mode > 2 || (rs_mode && ss == nullptr)) return -1;
+  if (rs_mode < 0 || rs_mode > 2 || (rs_mode && (ss == nullptr || ssld < M || ssld % 4 != 0))) return -1;
   if (rs_mode == 1 && ((epi != EPI_PLAIN && epi != EPI_SWIGLU) || P < 1 || P > 16)) return -1;
   if (rs_mode == 2 && (epi != EPI_RESIDUAL || bn != 256)) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
   const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
-           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, ss, P, eps};
+           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, ss, P, ssld, eps};
   return bn == 256 ? dispatch<8>(p, epi, s, var, rs_mode) : dispatch<6>(p, epi, s, var, rs_mode);
 }

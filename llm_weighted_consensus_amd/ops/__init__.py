@@ -432,7 +432,8 @@ class NormChain:
         if (d + 255) // 256 > 16:
             raise ValueError("NormChain: at most 16 partials per row (d <= 4096)")
         self.max_rows, self.d, self.eps = int(max_rows), int(d), float(eps)
-        self.ss = torch.zeros(16, self.max_rows, dtype=torch.float32, device=device)
+        # rows padded to a multiple of 64 floats: every partial's LDS-DMA source is 16-byte aligned
+        self.ss = torch.zeros(16, (self.max_rows + 63) // 64 * 64, dtype=torch.float32, device=device)
         self.P = 1
 
     def scales(self, M: int) -> torch.Tensor:
