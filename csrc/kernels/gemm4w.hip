@@ -137,10 +137,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  constexpr bool PAP = VAR == 64 && EPI != EPI_RESIDUAL;
+  // the wave-local epilogue (VAR 64) for the residual epilogue only with RS 2: the plain residual form of it
+  // spilled (256 VGPRs + 220 B scratch), the RS 2 form compiles at 233 VGPRs
+  constexpr bool PAP = VAR == 64 && (EPI != EPI_RESIDUAL || RS == 2);
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
   // block-staged epilogue, VAR 32); RS 2: the four waves' 128 row sums (2 KiB) at the same place
-  constexpr int RSOFF = G::Lds, RSV = RSOFF + 16384;
+  constexpr int RSOFF = PAP ? G::LdsPap : G::Lds, RSV = RSOFF + 16384;
   // LDS-DMA piece k (64 lanes x 16 B = 256 rows x fp32) of partial k of m-tile rows [m, m + 256)
   auto ss_dma = [&](int m, int k) {
     const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.ssld + m, (p.M - m) * 4);
@@ -211,8 +213,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
-    // (residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
-    // there is no next tile to prefetch, and 32 up-front residual chunks per lane would spill)
+    // (plain residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
+    // there is no next tile to prefetch, and its 32 up-front residual chunks per lane spilled; the RS 2 form of
+    // the chain takes this path: no block barriers between the staging and the stores)
     if (!PAP || round == 0) {
       if constexpr (RS == 1) {  // the oldest VMEM ops of each wave: the counted wait below retires them
         for (int k = wid; k < p.P; k += 4) ss_dma(m0, k);
@@ -509,12 +512,35 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             for (int e = 0; e < 8; ++e) x[e] += y[e];
             v = pack8(x);
           }
+          if constexpr (RS == 2) {  // as in the block-staged epilogue: the row's squares over the wave's columns
+            float z[8];
+            unpack8(gn < ncols ? v : uint4v{0u, 0u, 0u, 0u}, z);
+            float sq = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sq += z[e] * z[e];
+            sq += __shfl_xor(sq, 8);
+            sq += __shfl_xor(sq, 4);
+            sq += __shfl_xor(sq, 2);
+            sq += __shfl_xor(sq, 1);
+            if ((lane & 15) == 0) reinterpret_cast<float*>(smem + RSOFF)[wid * 128 + i * 16 + row] = sq;
+          }
           (void)gm;
           const uint32_t off = gn < ncols ? (uint32_t)(((i * 16 + row) * p.ldc + gn) * 2) : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
         }
         G4_LGKM0();  // the staging reads are done before the next m-tile overwrites the slice
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (RS == 2) {
+        __syncthreads();  // both waves of each row half wrote their row sums
+        if (wn == 0) {
+          const float* rsum = reinterpret_cast<const float*>(smem + RSOFF);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = lane + 64 * h, gm = m0 + wm * 128 + row;
+            if (gm < p.M) p.ss[(size_t)tn * p.ssld + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
+          }
+        }
       }
       continue;  // no block barrier: the next tile's first wait + barrier orders everything
     }
@@ -652,7 +678,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = (VAR == 64 && EPI != EPI_RESIDUAL ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
+  constexpr int lds = (VAR == 64 && (EPI != EPI_RESIDUAL || RS == 2) ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
                       (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
   static bool attr = false;
   if (!attr) {
@@ -680,7 +706,9 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
     return -1;
   }
   if (rs == 2) {
-    if constexpr (EPI == EPI_RESIDUAL && NT == 8) return launch3<EPI, NT, 32, 2>(p, s);
+    if constexpr (EPI == EPI_RESIDUAL && NT == 8) {
+      return var == 64 ? launch3<EPI, NT, 64, 2>(p, s) : launch3<EPI, NT, 32, 2>(p, s);
+    }
     return -1;
   }
   if (var == 32) return launch3<EPI, NT, 32, 0>(p, s);

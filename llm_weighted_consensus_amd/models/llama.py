@@ -223,7 +223,7 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ forward
     def _chain_layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool,
-                      qkv_bn: int) -> torch.Tensor:
+                      qkv_bn: int, res_var: int = 0) -> torch.Tensor:
         """The folded-RMSNorm decode chain (module docstring): x_res is updated in place; the partial row sums of
         squares of the final residual stream are left in ``self.chain`` for the lm_head."""
         cfg, ch = self.cfg, self.chain
@@ -235,9 +235,9 @@ class LlamaModel:
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
                               rope_q=rope_q)
             attn = attn_fn(qkv, li)
-            ops.gemm4w(attn.reshape(T, Hq * D), L.wo, residual=x_res, out=x_res, chain=ch)
+            ops.gemm4w(attn.reshape(T, Hq * D), L.wo, residual=x_res, out=x_res, chain=ch, var=res_var)
             act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
-            ops.gemm4w(act, L.w_down, residual=x_res, out=x_res, chain=ch)
+            ops.gemm4w(act, L.w_down, residual=x_res, out=x_res, chain=ch, var=res_var)
         return x_res
 
     def chain_ok(self, M: int) -> bool:
@@ -384,23 +384,23 @@ class LlamaModel:
         if self.chain is None:  # once, for every decode bucket (captured graphs keep these addresses)
             self.chain = ops.NormChain(max(M, 8192), cfg.hidden, cfg.rms_eps, self.device)
         if M > self.chain.max_rows:
-            self.chain_m[M] = (False, 192)
+            self.chain_m[M] = (False, 192, 0)
             return
         force = os.environ.get("LWC_NORM_CHAIN")
         x_res = x.clone()
         ch, eps = self.chain, cfg.rms_eps
         if (cfg.hidden + 255) // 256 > 16:
-            self.chain_m[M] = (False, 192)
+            self.chain_m[M] = (False, 192, 0)
             return
         ones = torch.ones(cfg.hidden, device=self.device, dtype=self.dtype)
 
-        def chained(bn):
+        def chained(bn, rv):
             def run():
                 ops.rms_rowsumsq(x_res, ch)
                 ops.gemm4w(x_res, L.wqkv, bn=bn, chain=ch)
-                ops.gemm4w(xa, L.wo, residual=x_res, out=x_res, chain=ch)
+                ops.gemm4w(xa, L.wo, residual=x_res, out=x_res, chain=ch, var=rv)
                 ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
-                ops.gemm4w(xf, L.w_down, residual=x_res, out=x_res, chain=ch)
+                ops.gemm4w(xf, L.w_down, residual=x_res, out=x_res, chain=ch, var=rv)
                 ops.gemm4w(x_res, self.lm_head, chain=ch)
             return run
 
@@ -414,19 +414,21 @@ class LlamaModel:
             h = ops.rmsnorm(x_res, ones, eps)
             self._proj(h, self.lm_head)
 
-        runs = {192: chained(192), 256: chained(256), "base": unchained}
+        runs = {(bn, rv): chained(bn, rv) for bn in (192, 256) for rv in (32, 64)}
+        runs["base"] = unchained
         ts = {k: [] for k in runs}
         for _ in range(3):  # interleaved rounds (one process, one device)
             for k, fn in runs.items():
                 x_res.copy_(x)
                 ts[k].append(gemm_plan._time(fn, iters=3, rounds=1))
         med = {k: sorted(t)[len(t) // 2] for k, t in ts.items()}
-        bn = 192 if med[192] <= med[256] else 256
-        use = med[bn] < med["base"] if force is None else force == "1"
-        self.chain_m[M] = (use, bn)
-        gemm_plan.TIMINGS[(M, cfg.hidden, 0, "norm_chain")] = {"chain192": med[192], "chain256": med[256],
-                                                                "unfolded": med["base"]}
-        gemm_plan._CHOICE[(M, cfg.hidden, 0, "norm_chain")] = f"chain{bn}" if use else "unfolded"
+        best = min((k for k in med if k != "base"), key=lambda k: med[k])
+        use = med[best] < med["base"] if force is None else force == "1"
+        self.chain_m[M] = (use, best[0], best[1])
+        gemm_plan.TIMINGS[(M, cfg.hidden, 0, "norm_chain")] = dict(
+            {f"chain_bn{k[0]}_v{k[1]}": v for k, v in med.items() if k != "base"}, unfolded=med["base"])
+        gemm_plan._CHOICE[(M, cfg.hidden, 0, "norm_chain")] = (f"chain_bn{best[0]}_v{best[1]}" if use
+                                                                else "unfolded")
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,
@@ -461,7 +463,8 @@ class LlamaModel:
                                         num_splits=num_splits, part_o=part_o, part_lse=part_lse, rope=rope)
 
         if self.chain_ok(B):
-            x = self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, self.chain_m[B][1])
+            _, bn, rv = self.chain_m[B]
+            x = self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, bn, rv)
             return ops.gemm4w(x, self.lm_head, chain=self.chain)
         h = self._layers(x, cache, positions, slots, attn_fn, rope_q=not q_at_load)
         return self._proj(h, self.lm_head)

@@ -506,11 +506,13 @@ def chain_ab(dev):
         "o blas res": lambda: acc.addmm_(xa, wo.t()),
         "o g4 res": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc),
         "o g4 res+ss": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc, chain=ch),
+        "o g4 res+ss v64": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc, chain=ch, var=64),
         "gu g4": lambda: ops.gemm4w(x, wgu, swiglu=True),
         "gu g4 rs": lambda: ops.gemm4w(x, wgu, swiglu=True, chain=ch),
         "down blas res": lambda: acc.addmm_(xf, wd.t()),
         "down g4 res": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc),
         "down g4 res+ss": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc, chain=ch),
+        "down g4 res+ss v64": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc, chain=ch, var=64),
         "lm blas": lambda: F.linear(x, wl),
         "lm g4": lambda: ops.gemm4w(x, wl),
         "lm g4 v64": lambda: ops.gemm4w(x, wl, var=64),
@@ -525,7 +527,8 @@ def chain_ab(dev):
     med = {k: sorted(t)[2] for k, t in res.items()}
     base = (2 * med["rmsnorm"] + min(med["qkv blas"], med["qkv g4n192"]) + med["o blas res"] + med["gu g4"]
             + med["down blas res"])
-    chain = med["qkv g4n192 rs"] + med["o g4 res+ss"] + med["gu g4 rs"] + med["down g4 res+ss"]
+    chain = (med["qkv g4n192 rs"] + min(med["o g4 res+ss"], med["o g4 res+ss v64"]) + med["gu g4 rs"]
+             + min(med["down g4 res+ss"], med["down g4 res+ss v64"]))
     print(f"chain {M} per layer: unfolded {base:.1f} us, chain {chain:.1f} us; lm_head: unfolded "
           f"{med['rmsnorm'] + med['lm blas']:.1f}, chain {med['lm g4 rs']:.1f}", flush=True)
 

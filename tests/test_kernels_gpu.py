@@ -1242,10 +1242,12 @@ def test_gemm4w_rowscale(gpu, M, N, K, epi, bn, P):
             _close(ops.gemm4w(A, W, bn=bn, chain=chain), ref, 3e-2, 1e-2)
 
 
+@pytest.mark.parametrize("var", [32, 64])
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (300, 4096, 512), (1000, 1024, 128), (4096 + 37, 4096, 64)])
-def test_gemm4w_residual_rowsum(gpu, M, N, K):
+def test_gemm4w_residual_rowsum(gpu, M, N, K, var):
     """Folded RMSNorm, producer side (RS 2): the residual epilogue writes C = R + A.W^T and the N/256 partial
-    row sums of squares of the bf16 output (fp32 reference on the returned C); three launches in a row; then
+    row sums of squares of the bf16 output (fp32 reference on the returned C), with the block-staged (32) and the
+    wave-local (64) epilogue; three launches in a row; then
     the chain end to end: an RS 1 projection of C with those partials == the projection of rmsnorm(C), and a
     chain started by rms_rowsumsq gives the same scales."""
     from llm_weighted_consensus_amd import ops
@@ -1259,7 +1261,7 @@ def test_gemm4w_residual_rowsum(gpu, M, N, K):
     for it in range(3):
         R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
         want = R.float() + A.float() @ W.float().t()
-        C = ops.gemm4w(A, W, residual=R, out=R, chain=chain)
+        C = ops.gemm4w(A, W, residual=R, out=R, chain=chain, var=var)
         torch.cuda.synchronize()
         _close(C, want, 3e-2, 1e-2)
         P = N // 256

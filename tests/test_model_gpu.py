@@ -323,9 +323,9 @@ def test_folded_norm_chain_matches_unfolded(tiny, gpu, qkv_bn):
         m.chain = ops.NormChain(8192, m.cfg.hidden, m.cfg.rms_eps, gpu)
     saved = dict(m.chain_m)
     try:
-        m.chain_m[B] = (False, qkv_bn)
+        m.chain_m[B] = (False, qkv_bn, 0)
         base = m.decode(*args, num_splits=1).float()
-        m.chain_m[B] = (True, qkv_bn)
+        m.chain_m[B] = (True, qkv_bn, 64 if qkv_bn == 256 else 32)
         assert m.chain_ok(B)
         got = m.decode(*args, num_splits=1).float()
     finally:
