@@ -232,8 +232,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     if constexpr (RS == 1) {
       // row tid's scale from its partials (the main loop's first barrier publishes it to the epilogues)
       const float* part = reinterpret_cast<const float*>(smem + RSOFF);
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = part[k * 256 + tid];  // all 16 in flight (the region is always 16 KiB)
       float sum = 0.f;
-      for (int k = 0; k < p.P; ++k) sum += part[k * 256 + tid];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sum += k < p.P ? v[k] : 0.f;  // fixed order: deterministic
       reinterpret_cast<float*>(smem + RSV)[tid] = rsqrtf(sum / (float)p.K + p.eps);
     }
 #pragma unroll

@@ -222,28 +222,54 @@ class LlamaModel:
         self.lm_head = t("lm_head.weight") if "lm_head.weight" in sd else self.embed
 
     # ------------------------------------------------------------------ forward
+    def _residual_into(self, inp: torch.Tensor, w: torch.Tensor, x_res: torch.Tensor, mode: str) -> None:
+        """x_res += inp . w^T, leaving the partial row sums of squares of the new x_res in ``self.chain`` per
+        ``mode``: "own32" / "own64" — gemm4w's residual epilogue writes them (RS 2, schedule 32 / 64);
+        "sumsq" — the planner's residual GEMM, then one rms_rowsumsq pass; "plain" — no partials (the next
+        consumer normalises with the norm kernel)."""
+        if mode in ("own32", "own64"):
+            ops.gemm4w(inp, w, residual=x_res, out=x_res, chain=self.chain, var=32 if mode == "own32" else 64)
+            return
+        gemm_plan.linear_add_(inp, w, x_res, ws=self.g8_ws)
+        if mode == "sumsq":
+            ops.rms_rowsumsq(x_res, self.chain)
+
     def _chain_layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool,
-                      qkv_bn: int, res_var: int = 0) -> torch.Tensor:
-        """The folded-RMSNorm decode chain (module docstring): x_res is updated in place; the partial row sums of
-        squares of the final residual stream are left in ``self.chain`` for the lm_head."""
+                      plan: dict) -> torch.Tensor:
+        """Decode layers + lm_head with the folded norms per ``plan`` (:meth:`_tune_chain`): at each norm point
+        ("attn": qkv, "mlp": gate|up, "final": lm_head) either the consumer scales its rows from the chain's
+        partials ("fold") or the norm kernel (weights ones: the norms are in the projections) runs first;
+        the producers of folded points leave partials by ``plan["o"]`` / ``plan["down"]``.  Returns logits."""
         cfg, ch = self.cfg, self.chain
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
-        ops.rms_rowsumsq(x_res, ch)
+        ones, eps = self.final_norm, cfg.rms_eps  # (every norm weight is ones after folding)
+        if plan["attn"]:
+            ops.rms_rowsumsq(x_res, ch)
+        nl = len(self.layers)
         for li, L in enumerate(self.layers):
-            qkv = ops.gemm4w(x_res, L.wqkv, bn=qkv_bn, chain=ch)
+            if plan["attn"]:
+                qkv = ops.gemm4w(x_res, L.wqkv, bn=plan["qkv_bn"], chain=ch)
+            else:
+                qkv = self._proj(ops.rmsnorm(x_res, ones, eps), L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
                               rope_q=rope_q)
-            attn = attn_fn(qkv, li)
-            ops.gemm4w(attn.reshape(T, Hq * D), L.wo, residual=x_res, out=x_res, chain=ch, var=res_var)
-            act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
-            ops.gemm4w(act, L.w_down, residual=x_res, out=x_res, chain=ch, var=res_var)
-        return x_res
+            attn = attn_fn(qkv, li).reshape(T, Hq * D)
+            self._residual_into(attn, L.wo, x_res, plan["o"] if plan["mlp"] else "plain")
+            if plan["mlp"]:
+                act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
+            else:
+                act = gemm_plan.swiglu(ops.rmsnorm(x_res, ones, eps), L.w_gate_up, L.gu_block, ws=self.g8_ws)
+            nxt = plan["attn"] if li + 1 < nl else plan["final"]
+            self._residual_into(act, L.w_down, x_res, plan["down"] if nxt else "plain")
+        if plan["final"]:
+            return ops.gemm4w(x_res, self.lm_head, chain=ch)
+        return self._proj(ops.rmsnorm(x_res, ones, eps), self.lm_head)
 
     def chain_ok(self, M: int) -> bool:
-        """Whether a decode step of M rows runs the folded-norm chain (timed faster at M, before capture)."""
+        """Whether a decode step of M rows folds at least one norm (timed faster at M, before capture)."""
         c = self.chain_m.get(M)
-        return bool(c and c[0]) and self.chain is not None and M <= self.chain.max_rows
+        return bool(c and (c["attn"] or c["mlp"] or c["final"])) and self.chain is not None and M <= self.chain.max_rows
 
     def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True,
                 keep: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -375,60 +401,79 @@ class LlamaModel:
             self._tune_chain(M, x, xa, xf)
 
     def _tune_chain(self, M: int, x, xa, xf) -> None:
-        """Decode batch M: time one layer + the lm_head as the folded-norm chain (qkv at bn 192 and 256) against
-        the unfolded path on the planner's choices (norm kernels + the best backend per projection); the
-        faster is what decode() runs at M (recorded in ``chain_m``).  ``LWC_NORM_CHAIN=1|0`` forces it."""
+        """Decode batch M: decide, per norm point, between the norm kernel + the best projection backend and the
+        folded norm (the consumer's row-scaled gemm4w, the producer leaving partial row sums of squares by its
+        own residual epilogue or by one rms_rowsumsq pass after the planner's GEMM).  Every candidate is
+        timed alone (interleaved rounds, median), the plan is the cheaper side at each point and is recorded
+        in ``chain_m`` (``LWC_NORM_CHAIN=0|1`` forces all-unfolded / all-folded)."""
         if M in self.chain_m or torch.cuda.is_current_stream_capturing():
             return
         cfg, L = self.cfg, self.layers[0]
+        none = {"attn": False, "mlp": False, "final": False, "qkv_bn": 192, "o": "plain", "down": "plain"}
+        if (cfg.hidden + 255) // 256 > 16:
+            self.chain_m[M] = none
+            return
         if self.chain is None:  # once, for every decode bucket (captured graphs keep these addresses)
             self.chain = ops.NormChain(max(M, 8192), cfg.hidden, cfg.rms_eps, self.device)
         if M > self.chain.max_rows:
-            self.chain_m[M] = (False, 192, 0)
+            self.chain_m[M] = none
             return
-        force = os.environ.get("LWC_NORM_CHAIN")
-        x_res = x.clone()
         ch, eps = self.chain, cfg.rms_eps
-        if (cfg.hidden + 255) // 256 > 16:
-            self.chain_m[M] = (False, 192, 0)
-            return
-        ones = torch.ones(cfg.hidden, device=self.device, dtype=self.dtype)
+        x_res = x.clone()
+        ones = self.final_norm
+        ops.rms_rowsumsq(x_res, ch)  # valid partials for the row-scaled candidates
+        P0 = ch.P
+        w = {"qkv": L.wqkv, "o": L.wo, "gu": L.w_gate_up, "down": L.w_down, "lm": self.lm_head}
 
-        def chained(bn, rv):
+        def fold(name, **kw):
             def run():
-                ops.rms_rowsumsq(x_res, ch)
-                ops.gemm4w(x_res, L.wqkv, bn=bn, chain=ch)
-                ops.gemm4w(xa, L.wo, residual=x_res, out=x_res, chain=ch, var=rv)
-                ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
-                ops.gemm4w(xf, L.w_down, residual=x_res, out=x_res, chain=ch, var=rv)
-                ops.gemm4w(x_res, self.lm_head, chain=ch)
+                ch.P = P0
+                ops.gemm4w(x, w[name], chain=ch, **kw)
             return run
 
-        def unchained():
-            h = ops.rmsnorm(x_res, ones, eps)
-            self._proj(h, L.wqkv)
-            gemm_plan.linear_add_(xa, L.wo, x_res, ws=self.g8_ws)
-            h = ops.rmsnorm(x_res, ones, eps)
-            gemm_plan.swiglu(h, L.w_gate_up, L.gu_block, ws=self.g8_ws)
-            gemm_plan.linear_add_(xf, L.w_down, x_res, ws=self.g8_ws)
-            h = ops.rmsnorm(x_res, ones, eps)
-            self._proj(h, self.lm_head)
+        def res(name, inp, var):
+            return lambda: ops.gemm4w(inp, w[name], residual=x_res, out=x_res, chain=ch, var=var)
 
-        runs = {(bn, rv): chained(bn, rv) for bn in (192, 256) for rv in (32, 64)}
-        runs["base"] = unchained
+        runs = {
+            "norm": lambda: ops.rmsnorm(x_res, ones, eps),
+            "sumsq": lambda: ops.rms_rowsumsq(x_res, ch),
+            "qkv": lambda: self._proj(x, L.wqkv),
+            "qkv_rs192": fold("qkv", bn=192), "qkv_rs256": fold("qkv", bn=256),
+            "o": lambda: gemm_plan.linear_add_(xa, L.wo, x_res, ws=self.g8_ws),
+            "o_own32": res("o", xa, 32), "o_own64": res("o", xa, 64),
+            "gu": lambda: gemm_plan.swiglu(x, L.w_gate_up, L.gu_block, ws=self.g8_ws),
+            "gu_rs": fold("gu", swiglu=True),
+            "down": lambda: gemm_plan.linear_add_(xf, L.w_down, x_res, ws=self.g8_ws),
+            "down_own32": res("down", xf, 32), "down_own64": res("down", xf, 64),
+            "lm": lambda: self._proj(x, self.lm_head), "lm_rs": fold("lm"),
+        }
         ts = {k: [] for k in runs}
-        for _ in range(3):  # interleaved rounds (one process, one device)
+        for _ in range(3):  # interleaved rounds (one process, one device: matched clocks and caches)
             for k, fn in runs.items():
-                x_res.copy_(x)
                 ts[k].append(gemm_plan._time(fn, iters=3, rounds=1))
-        med = {k: sorted(t)[len(t) // 2] for k, t in ts.items()}
-        best = min((k for k in med if k != "base"), key=lambda k: med[k])
-        use = med[best] < med["base"] if force is None else force == "1"
-        self.chain_m[M] = (use, best[0], best[1])
-        gemm_plan.TIMINGS[(M, cfg.hidden, 0, "norm_chain")] = dict(
-            {f"chain_bn{k[0]}_v{k[1]}": v for k, v in med.items() if k != "base"}, unfolded=med["base"])
-        gemm_plan._CHOICE[(M, cfg.hidden, 0, "norm_chain")] = (f"chain_bn{best[0]}_v{best[1]}" if use
-                                                                else "unfolded")
+        t = {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
+        ch.P = P0
+
+        def producer(name):  # the cheapest way to leave partials, and its cost over the plain residual GEMM
+            opts = {"own32": t[f"{name}_own32"], "own64": t[f"{name}_own64"], "sumsq": t[name] + t["sumsq"]}
+            best = min(opts, key=opts.get)
+            return best, opts[best] - t[name]
+
+        o_mode, o_extra = producer("o")
+        d_mode, d_extra = producer("down")
+        qkv_bn = 192 if t["qkv_rs192"] <= t["qkv_rs256"] else 256
+        # each point: folded (consumer + producer's extra) vs the norm kernel + the consumer's best backend
+        attn = t[f"qkv_rs{qkv_bn}"] + d_extra < t["norm"] + t["qkv"]
+        mlp = t["gu_rs"] + o_extra < t["norm"] + t["gu"]
+        final = t["lm_rs"] + d_extra < t["norm"] + t["lm"]
+        force = os.environ.get("LWC_NORM_CHAIN")
+        if force is not None:
+            attn = mlp = final = force == "1"
+        plan = {"attn": attn, "mlp": mlp, "final": final, "qkv_bn": qkv_bn, "o": o_mode, "down": d_mode}
+        self.chain_m[M] = plan
+        key = (M, cfg.hidden, 0, "norm_chain")
+        gemm_plan.TIMINGS[key] = t
+        gemm_plan._CHOICE[key] = ",".join(f"{k}={v}" for k, v in plan.items())
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,
@@ -463,9 +508,7 @@ class LlamaModel:
                                         num_splits=num_splits, part_o=part_o, part_lse=part_lse, rope=rope)
 
         if self.chain_ok(B):
-            _, bn, rv = self.chain_m[B]
-            x = self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, bn, rv)
-            return ops.gemm4w(x, self.lm_head, chain=self.chain)
+            return self._chain_layers(x, cache, positions, slots, attn_fn, not q_at_load, self.chain_m[B])
         h = self._layers(x, cache, positions, slots, attn_fn, rope_q=not q_at_load)
         return self._proj(h, self.lm_head)
 

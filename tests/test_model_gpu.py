@@ -299,7 +299,8 @@ def test_folded_norm_chain_matches_unfolded(tiny, gpu, qkv_bn):
     """Folded RMSNorm decode chain (models/llama.py, gemm4w RS modes): the norm weights live in the projection
     weights (the model's norms are ones), the o / down residual epilogues emit the row scales the next
     projection applies — the decode logits equal the unfolded path's (norm kernels + projections) and the fp32
-    reference forward."""
+    reference forward.  qkv_bn 192: both producers gemm4w RS 2 (schedules 32 / 64); 256: the down
+    producer by rms_rowsumsq after the planner's residual GEMM."""
     from llm_weighted_consensus_amd import ops
     from llm_weighted_consensus_amd.models.llama import KVCache
 
@@ -323,9 +324,11 @@ def test_folded_norm_chain_matches_unfolded(tiny, gpu, qkv_bn):
         m.chain = ops.NormChain(8192, m.cfg.hidden, m.cfg.rms_eps, gpu)
     saved = dict(m.chain_m)
     try:
-        m.chain_m[B] = (False, qkv_bn, 0)
+        m.chain_m[B] = {"attn": False, "mlp": False, "final": False, "qkv_bn": qkv_bn, "o": "plain", "down": "plain"}
+        assert not m.chain_ok(B)
         base = m.decode(*args, num_splits=1).float()
-        m.chain_m[B] = (True, qkv_bn, 64 if qkv_bn == 256 else 32)
+        m.chain_m[B] = {"attn": True, "mlp": True, "final": True, "qkv_bn": qkv_bn,
+                        "o": "own64" if qkv_bn == 256 else "own32", "down": "sumsq" if qkv_bn == 256 else "own64"}
         assert m.chain_ok(B)
         got = m.decode(*args, num_splits=1).float()
     finally:
