@@ -10,4 +10,4 @@ timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cach
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_g4h.log; [ $rc -eq 0 ] || exit $rc
 G4_VARS="1,32" G4_VARS_EPI="1,32" G4_SHAPES="0,1,2,3,4" timeout -k 10 600 python -u scripts/microbench.py g4ab > gpurun_out/micro_g4h.log 2>&1
 rc=$?; echo "micro rc=$rc"; grep -v amdgpu.ids gpurun_out/micro_g4h.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_serve_r4.sh
+bash scripts/history/gpu_serve_r4.sh

@@ -19,4 +19,4 @@ rc=$?; echo "micro small rc=$rc"; grep "rope\|silu" gpurun_out/micro_small_r4d.l
 G4_VARS="32,64" G4_VARS_EPI="32,64" G4_SHAPES="0,1,2,3,4" timeout -k 10 400 python3 -u scripts/microbench.py g4ab \
     > gpurun_out/micro_g4_r4d.log 2>&1
 rc=$?; echo "g4ab rc=$rc"; grep g4ab gpurun_out/micro_g4_r4d.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_r4c.sh
+bash scripts/history/gpu_r4c.sh
