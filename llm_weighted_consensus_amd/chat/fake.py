@@ -14,6 +14,7 @@ from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
 from ..errors import StatusError
+from ..context import COALESCE
 from ..schema import chat as C
 from .base import ChatClient
 
@@ -83,6 +84,26 @@ class FakeChatClient(ChatClient):
             for t, alts in toks:
                 pieces.append((i, t, alts))
         emitted = 0
+        if COALESCE.get() and not fail and not any(sc.tool_call for sc in choices) and pieces:
+            # a unary request (context.COALESCE): each choice's pieces merged into one chunk, as the local
+            # engine client merges a flush's tokens (the fold is the same)
+            for i, sc in enumerate(choices):
+                mine = [(t, alts) for j, t, alts in pieces if j == i]
+                if self.delay_s:
+                    await asyncio.sleep(self.delay_s * len(mine))
+                lp = None
+                if any(a is not None for _, a in mine):
+                    lp = C.Logprobs(content=[C.Logprob.trusted(token=t, bytes=list(t.encode()),
+                                                               logprob=float(alts[0][1]) if alts else 0.0,
+                                                               top_logprobs=[C.TopLogprob.trusted(
+                                                                   token=a, bytes=list(a.encode()), logprob=float(l))
+                                                                   for a, l in alts])
+                                             for t, alts in mine if alts is not None])
+                yield C.ChatCompletionChunk(id=cid, created=created, model=request.model, provider="fake",
+                                            choices=[C.StreamChoice(delta=C.Delta(role="assistant",
+                                                                                  content="".join(t for t, _ in mine)),
+                                                                    index=first + i, logprobs=lp)])
+            pieces = []
         for i, t, alts in pieces:
             if self.delay_s:
                 await asyncio.sleep(self.delay_s)

@@ -21,6 +21,7 @@ from typing import Any, AsyncIterator, Dict, List, Optional
 from ..engine.constraints import constraint_for_schema
 from ..engine.sampling import SamplingParams
 from ..engine.service import EngineFailure, EngineService
+from ..context import COALESCE, COALESCE_FLUSH_S
 from ..errors import ChatError
 from ..schema import chat as C
 from ..utils import json as sjson
@@ -312,12 +313,18 @@ class LocalChatClient(ChatClient):
         started = [False] * n
         remaining = n
         completion_tokens = 0
+        # unary requests (context.COALESCE): one chunk per flush instead of per engine step — at the first
+        # tokens, then at least every COALESCE_FLUSH_S, and at the end
+        coalesce = COALESCE.get()
+        last_flush = None
+        choices: Dict[int, C.StreamChoice] = {}
         try:
             while remaining > 0:
                 evs = [await q.get()]
                 while not q.empty():
                     evs.append(q.get_nowait())
-                choices: Dict[int, C.StreamChoice] = {}
+                if not coalesce:
+                    choices = {}
                 for ev in evs:
                     if isinstance(ev, EngineFailure):
                         if ev.kind == "deadline":
@@ -348,10 +355,10 @@ class LocalChatClient(ChatClient):
                     started[i] = True
                     if sp.logprobs:
                         ts, tb = _token_info(tok, ev.token_id)
-                        lp = C.Logprob(token=ts, bytes=tb, logprob=ev.logprob,
-                                       top_logprobs=[C.TopLogprob(token=a, bytes=b, logprob=l)
-                                                     for (a, b), l in ((_token_info(tok, t), l)
-                                                                       for t, l in ev.top_logprobs)])
+                        lp = C.Logprob.trusted(token=ts, bytes=tb, logprob=float(ev.logprob),
+                                               top_logprobs=[C.TopLogprob.trusted(token=a, bytes=b, logprob=float(l))
+                                                             for (a, b), l in ((_token_info(tok, t), l)
+                                                                               for t, l in ev.top_logprobs)])
                         if ch.logprobs is None:
                             ch.logprobs = C.Logprobs(content=[lp])
                         else:
@@ -362,8 +369,14 @@ class LocalChatClient(ChatClient):
                         if reason == "abort":
                             reason = "error"
                         ch.finish_reason = "tool_calls" if (tool_name is not None and reason == "stop") else reason
+                if coalesce:
+                    now = time.monotonic()
+                    if remaining > 0 and last_flush is not None and now - last_flush < COALESCE_FLUSH_S:
+                        continue
+                    last_flush = now
                 chunk = C.ChatCompletionChunk(id=cid, choices=[choices[k] for k in sorted(choices)], created=created,
                                               model=model, provider="local")
+                choices = {}
                 if remaining == 0 and include_usage:
                     chunk.usage = C.Usage(completion_tokens=completion_tokens, prompt_tokens=prompt_len,
                                           total_tokens=prompt_len + completion_tokens, cost=0.0)

@@ -19,9 +19,18 @@ request number and seeds) and so code written against a plain dict context keeps
 """
 from __future__ import annotations
 
+import contextvars
 import time
 import uuid
 from typing import Any, Mapping, Optional
+
+# Set while a UNARY request is served (score/orchestrator.py create_unary; asyncio tasks inherit it): a
+# response that is the fold of a chunk stream does not need one chunk per token.  The voter streams then
+# merge each voter's output and the local chat clients emit merged chunks (a flush at the first tokens, at
+# the end, and at least every COALESCE_FLUSH_S, so the first-chunk / other-chunk timeouts keep their meaning);
+# chunk push is associative, so the folded response is the same.
+COALESCE: contextvars.ContextVar = contextvars.ContextVar("lwc_coalesce", default=False)
+COALESCE_FLUSH_S = 1.0
 
 
 class RequestContext(dict):

@@ -157,6 +157,19 @@ class Wire(BaseModel):
     def parse(cls, obj: Any):
         return cls.model_validate(obj)
 
+    @classmethod
+    def trusted(cls, **fields):
+        """An instance from values the caller guarantees are already valid and complete (every field given,
+        engine-produced token data): no validation pass — the per-token logprob objects of the local chat
+        client are the serving front end's most numerous allocation."""
+        new = cls.__new__(cls)
+        _set = object.__setattr__
+        _set(new, "__dict__", fields)
+        _set(new, "__pydantic_fields_set__", set(fields))
+        _set(new, "__pydantic_extra__", None)
+        _set(new, "__pydantic_private__", None)
+        return new
+
 
 # --- merge helpers (reference chat/completions/response.rs:812-872) -------------------------------
 

@@ -573,14 +573,15 @@ class StreamChoice(Wire):
             self.logprobs = o.logprobs.clone()
 
 
-def push_choices(mine: list, others: list) -> None:
-    """O(C) find-by-index merge used by every chunk type (reference response.rs:56-78)."""
+def push_choices(mine: list, others: list, owned: bool = False) -> None:
+    """O(C) find-by-index merge used by every chunk type (reference response.rs:56-78).  ``owned``: the
+    caller hands ``others`` over (nothing else holds them): a new choice is taken as is, not deep-copied."""
     for oc in others:
         tgt = next((c for c in mine if c.index == oc.index), None)
         if tgt is not None:
             tgt.push(oc)
         else:
-            mine.append(oc.clone())
+            mine.append(oc if owned else oc.clone())
 
 
 class ChatCompletionChunk(Wire):

@@ -180,8 +180,8 @@ class ScoreCompletionChunk(Wire):
     usage: Optional[Usage] = None
     weight_data: Optional[WeightData] = None
 
-    def push(self, o: "ScoreCompletionChunk") -> None:
-        push_choices(self.choices, o.choices)
+    def push(self, o: "ScoreCompletionChunk", owned: bool = False) -> None:
+        push_choices(self.choices, o.choices, owned)
         if self.usage is not None and o.usage is not None:
             self.usage.push(o.usage)
         elif self.usage is None and o.usage is not None:

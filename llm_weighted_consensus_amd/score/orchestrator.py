@@ -28,6 +28,7 @@ from collections import OrderedDict
 from typing import Any, AsyncIterator, Dict, List, Optional
 
 from .. import _runtime as RT
+from ..context import COALESCE
 from ..archive import resolve as AR
 from ..errors import ChatError, ResponseError, ScoreError, StatusError
 from ..schema import chat as C
@@ -46,6 +47,12 @@ SELECT_PROMPT_STRUCTURED = "Select the response:\n\n{choices}"
 def response_id(created: int) -> str:
     return f"scrcpl-{uuid.uuid4().hex}-{created}"
 
+
+
+# (context.COALESCE, set by create_unary: the voter streams of a unary request yield each voter's output
+# already merged, at most two chunks per voter, instead of one chunk per token — the unary response is the
+# fold of the stream, reference client.rs:71-91, and push is associative)
+_COALESCE = COALESCE
 
 class ChoiceIndexer:
     """(voter index, native choice index) -> global choice index, first-arrival order from `start`
@@ -174,14 +181,18 @@ class ScoreClient:
 
     async def _unary(self, ctx, request: S.ScoreCompletionCreateParams) -> S.ScoreCompletion:
         agg: Optional[S.ScoreCompletionChunk] = None
-        stream = await self.create_streaming(ctx, request)
-        async for item in stream:
-            if isinstance(item, StatusError):
-                raise item
-            if agg is None:
-                agg = item.clone()
-            else:
-                agg.push(item)
+        tok = _COALESCE.set(True)
+        try:
+            stream = await self.create_streaming(ctx, request)
+            async for item in stream:
+                if isinstance(item, StatusError):
+                    raise item
+                if agg is None:  # (coalesced: the stream's own aggregate, handed over whole)
+                    agg = item
+                else:
+                    agg.push(item)
+        finally:
+            _COALESCE.reset(tok)
         return S.ScoreCompletion.from_chunk(agg)
 
     # ------------------------------------------------------------------ streaming
@@ -284,11 +295,19 @@ class ScoreClient:
         tasks = [asyncio.create_task(pump(src)) for src in sources]
         pending = len(tasks)
         first = True
+        coalesce = _COALESCE.get()
         try:
             while pending:
                 item = await q.get()
                 if item is DONE:
                     pending -= 1
+                    continue
+                if coalesce:  # unary: the items are ours alone; nothing is yielded until the end
+                    for ch in item.choices:
+                        md = ch.completion_metadata
+                        if md is not None and md.usage is not None:
+                            usage.push(md.usage)
+                    aggregate.push(item, owned=True)
                     continue
                 if first:
                     first = False
@@ -320,6 +339,23 @@ class ScoreClient:
         aggregate.weight_data = weight_data
         usage.with_total_cost()
         aggregate.usage = usage
+        if coalesce:
+            # the unary fold of what the stream would have yielded — initial, every voter chunk, then the final
+            # patch below pushed onto them (first non-None wins): the aggregate itself with the patch's fields
+            # filled where it has none
+            for j, ch in enumerate(aggregate.choices):
+                if ch.index < C_len:
+                    if ch.weight is None:
+                        ch.weight = tally.choice_weight[ch.index]
+                    if ch.confidence is None:
+                        ch.confidence = tally.confidence[ch.index]
+                elif ch.delta.vote is not None and ch.confidence is None:
+                    ch.confidence = tally.voter_confidence[j - C_len]
+            self._last_tally = tally
+            yield aggregate
+            if all_error:
+                yield ScoreError.all_votes_failed(RT.unify_error_codes(codes))
+            return
         for j, ch in enumerate(aggregate.choices):
             if ch.index < C_len:
                 ch.weight = tally.choice_weight[ch.index]
@@ -432,6 +468,77 @@ class ScoreClient:
             delta=S.ScoreDelta(), finish_reason="error", index=indexer.get(llm.index, 0), weight=weight,
             error=ResponseError.from_status_error(err), model=llm.id, model_index=llm.index)])
 
+    async def _coalesced(self, it, nxt, rid, created, model_id, indexer, llm: Llm, weight: float):
+        """One voter's whole stream merged (unary requests, ``_COALESCE``): the chat chunks are folded with
+        ChatCompletionChunk.push, and what the per-chunk conversion below (``_voter_stream``) would attach to
+        each choice is tracked per choice — the first effective finish reason (``error`` on the choices of the
+        chunk a mid-stream error ended), the error, and the completion metadata of the chunks that carried the
+        choice (usage summed over those chunks only) — so the two chunks returned, (aggregate, finished part),
+        fold to exactly what the per-token chunks fold to."""
+        chat_agg = None
+        fin: Dict[int, str] = {}
+        err: Dict[int, Any] = {}
+        meta: Dict[int, S.CompletionMetadata] = {}
+        while nxt is not None:
+            chat_chunk, nxt = nxt, None
+            error = None
+            try:
+                nxt = await it.__anext__()
+            except StopAsyncIteration:
+                pass
+            except StatusError as e:
+                error = ResponseError.from_status_error(e)
+            except Exception as e:
+                error = ResponseError.from_status_error(ChatError.engine(repr(e)))
+            u = chat_chunk.usage
+            for c in chat_chunk.choices:
+                i = c.index
+                eff = "error" if error is not None else c.finish_reason
+                if eff is not None and i not in fin:
+                    fin[i] = eff
+                if error is not None and i not in err:
+                    err[i] = error
+                m = meta.get(i)
+                if m is None:
+                    meta[i] = S.CompletionMetadata(id=chat_chunk.id, created=chat_chunk.created, model=chat_chunk.model,
+                                                   service_tier=chat_chunk.service_tier,
+                                                   system_fingerprint=chat_chunk.system_fingerprint,
+                                                   provider=chat_chunk.provider,
+                                                   usage=u.clone() if u is not None else None)
+                else:
+                    if chat_chunk.service_tier is not None and m.service_tier is None:
+                        m.service_tier = chat_chunk.service_tier
+                    if chat_chunk.system_fingerprint is not None and m.system_fingerprint is None:
+                        m.system_fingerprint = chat_chunk.system_fingerprint
+                    if chat_chunk.provider is not None and m.provider is None:
+                        m.provider = chat_chunk.provider
+                    if u is not None:
+                        if m.usage is None:
+                            m.usage = u.clone()
+                        else:
+                            m.usage.push(u)
+            if chat_agg is None:  # chat clients yield fresh chunks they never touch again: merged in place
+                chat_agg = chat_chunk
+            else:
+                chat_agg.push(chat_chunk)
+        if chat_agg is None:
+            return None, None
+        agg = S.ScoreCompletionChunk(id=rid, created=created, model=model_id, choices=[])
+        for c in chat_agg.choices:
+            agg.choices.append(S.ScoreStreamChoice(
+                delta=S.ScoreDelta(**{k: getattr(c.delta, k) for k in C.Delta.model_fields}),
+                finish_reason=fin.get(c.index), index=indexer.get(llm.index, c.index), logprobs=c.logprobs,
+                weight=weight, error=err.get(c.index), model=llm.id, model_index=llm.index,
+                completion_metadata=meta[c.index]))
+        if llm.base.output_mode == "tool_call":
+            agg.tool_as_content()
+        done = [c for c in agg.choices if c.has_finish_reason_or_usage()]
+        final = None
+        if done:
+            final = agg.clone_without_choices()
+            final.choices = done
+        return agg, final
+
     async def _voter_stream(self, ctx, rid, created, indexer, llm: Llm, weight: float,
                             request: S.ScoreCompletionCreateParams, seed: int):
         params, tree = self._voter_request(llm, request, seed)
@@ -452,6 +559,14 @@ class ScoreClient:
             return
         final: Optional[S.ScoreCompletionChunk] = None
         agg: Optional[S.ScoreCompletionChunk] = None
+        if _COALESCE.get():
+            agg, final = await self._coalesced(it, nxt, rid, created, model_id, indexer, llm, weight)
+            if agg is not None:  # (the yielded chunks share agg's choice objects: agg is only read below)
+                rest = agg.clone_without_choices()
+                rest.choices = [c for c in agg.choices if not c.has_finish_reason_or_usage()]
+                if rest.choices:
+                    yield rest
+            nxt = None
         while nxt is not None:
             chat_chunk, nxt = nxt, None
             error = None

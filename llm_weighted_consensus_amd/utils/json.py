@@ -112,19 +112,36 @@ def _plain(v: Any) -> Any:
     return v.to_obj() if hasattr(v, "to_obj") else v
 
 
+# a JSON string literal (skipped as a whole) or a number in exponent form / a non-finite float
+_FIX_FLOATS = re.compile(r'"(?:[^"\\]|\\.)*"|(-?\d+(?:\.\d+)?e[-+]?\d+|NaN|-?Infinity)')
+
+
+def _fix_float(m: "re.Match") -> str:
+    t = m.group(1)
+    if t is None:
+        return m.group(0)  # a string literal, unchanged
+    if t in ("NaN", "Infinity", "-Infinity"):
+        return "null"
+    return ryu_f64(float(t))
+
+
 def dumps(v: Any) -> str:
-    """Compact serde_json text (serde_json::to_string).  Fast path: the C encoder, whose output equals
-    serde_json's except for floats in exponent form and non-finite floats — when the text holds either
-    (or a string that merely looks like one) the exact ryu encoder runs instead."""
+    """Compact serde_json text (serde_json::to_string).  The C encoder's output equals serde_json's except for
+    floats in exponent form (Python ``1e-05``, ryu ``1e-5``) and non-finite floats (serde_json: null); those
+    are rewritten in one C-regex pass that skips string literals (logprobs of confident tokens are often in
+    exponent form, so this is the common case, not a fallback).  Values the C encoder refuses take the exact
+    Python encoder."""
     s = None
     p = _plain(v)
-    if isinstance(p, (dict, list)):  # (a bare scalar has no delimiters for the check below)
+    if isinstance(p, (dict, list)):  # (a bare scalar: the exact encoder)
         try:
             s = _C_DUMPS(p)
         except (TypeError, ValueError):
             s = None
-    if s is not None and not _NEEDS_RYU.search(s):
-        return s
+    if s is not None:
+        if "e" not in s and "N" not in s and "I" not in s:
+            return s  # no exponent, no NaN / Infinity anywhere: nothing to rewrite
+        return _FIX_FLOATS.sub(_fix_float, s) if _NEEDS_RYU.search(s) else s
     out: list = []
     _enc(v, out)
     return "".join(out)

@@ -70,7 +70,7 @@ def main():
         import pstats
 
         st = pstats.Stats(pr)
-        st.sort_stats("tottime").print_stats(30)
+        st.sort_stats(os.environ.get("PROF_SORT", "tottime")).print_stats(int(os.environ.get("PROF_N", "30")))
         if "--callers" in sys.argv:
             st.print_callers("main.py:253")
     print(f"front end: {n / el:.1f} score requests/s ({el / n * 1e3:.2f} ms wall, {cpu / n * 1e3:.2f} ms process CPU "
