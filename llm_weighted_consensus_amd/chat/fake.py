@@ -45,6 +45,18 @@ def select_keys(request: C.ChatCompletionCreateParams) -> List[Tuple[str, str]]:
     return CHOICE_MAP.findall(text)
 
 
+_BYTES: dict = {}
+
+
+def _token_bytes(t: str) -> list:
+    """UTF-8 byte list of a token text, cached (read-only lists shared by the chunks, as chat/local.py's
+    _token_info)."""
+    b = _BYTES.get(t)
+    if b is None:
+        b = _BYTES[t] = list(t.encode())
+    return b
+
+
 class FakeChatClient(ChatClient):
     def __init__(self, policy: Callable[[C.ChatCompletionCreateParams], Sequence], chunk_chars: int = 3,
                  delay_s: float = 0.0):
@@ -93,10 +105,11 @@ class FakeChatClient(ChatClient):
                     await asyncio.sleep(self.delay_s * len(mine))
                 lp = None
                 if any(a is not None for _, a in mine):
-                    lp = C.Logprobs(content=[C.Logprob.trusted(token=t, bytes=list(t.encode()),
+                    tb = _token_bytes  # (cached per token text, as the local client caches per token id)
+                    lp = C.Logprobs(content=[C.Logprob.trusted(token=t, bytes=tb(t),
                                                                logprob=float(alts[0][1]) if alts else 0.0,
                                                                top_logprobs=[C.TopLogprob.trusted(
-                                                                   token=a, bytes=list(a.encode()), logprob=float(l))
+                                                                   token=a, bytes=tb(a), logprob=float(l))
                                                                    for a, l in alts])
                                              for t, alts in mine if alts is not None])
                 yield C.ChatCompletionChunk(id=cid, created=created, model=request.model, provider="fake",

@@ -62,9 +62,16 @@ def main():
 
         pr = cProfile.Profile()
         pr.enable()
-    t, c = time.perf_counter(), time.process_time()
-    asyncio.run(run(n))
-    el, cpu = time.perf_counter() - t, time.process_time() - c
+    rounds = int(os.environ.get("FRONTEND_ROUNDS", "1" if prof else "5"))
+    per = []
+    for _ in range(rounds):  # the container's CPU time per request is noisy: min and median over rounds
+        t, c = time.perf_counter(), time.process_time()
+        asyncio.run(run(n))
+        el, cpu = time.perf_counter() - t, time.process_time() - c
+        per.append((cpu / n * 1e3, el))
+    cpus = sorted(p for p, _ in per)
+    el = min(e for _, e in per)
+    cpu = cpus[0] * n / 1e3
     if pr is not None:
         pr.disable()
         import pstats
@@ -74,7 +81,8 @@ def main():
         if "--callers" in sys.argv:
             st.print_callers("main.py:253")
     print(f"front end: {n / el:.1f} score requests/s ({el / n * 1e3:.2f} ms wall, {cpu / n * 1e3:.2f} ms process CPU "
-          f"per request, 8 voters x 16 tokens)")
+          f"per request, 8 voters x 16 tokens; best of {rounds} rounds, median "
+          f"{cpus[len(cpus) // 2]:.2f} ms CPU)")
 
 
 if __name__ == "__main__":
