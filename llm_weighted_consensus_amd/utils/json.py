@@ -139,8 +139,8 @@ def dumps(v: Any) -> str:
         except (TypeError, ValueError):
             s = None
     if s is not None:
-        if "e" not in s and "N" not in s and "I" not in s:
-            return s  # no exponent, no NaN / Infinity anywhere: nothing to rewrite
+        if "e-" not in s and "e+" not in s and "NaN" not in s and "Infinity" not in s:
+            return s  # (Python writes every exponent with a sign): nothing anywhere to rewrite
         return _FIX_FLOATS.sub(_fix_float, s) if _NEEDS_RYU.search(s) else s
     out: list = []
     _enc(v, out)
