@@ -60,6 +60,11 @@ struct PrefillParams {
   const int* block_tables;
   const int* k_lens;
   int bt_stride;
+  // MX output (D = 128; the fp8 o projection's A operand, as the decode cascade kernel writes it): e4m3 rows
+  // out8 [T, Hq * D] (row stride o_stride bytes) + e8m0 scales mx [Hq][mx_rows][4], one per 32 dims
+  uint8_t* out8;
+  uint8_t* mx;
+  int mx_rows;
 };
 
 // The block tables come in as a const __restrict__ kernel argument (not through the params struct): the
@@ -323,6 +328,39 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(PrefillParams p, cons
 #pragma unroll
     for (int r = 0; r < 4; ++r) ot[(4 * g + r) * D + 16 * n + r16] = f2bf(o[n][r] * linv[r]);
   __syncthreads();
+  if constexpr (D == 128) {
+    if (p.out8 != nullptr) {  // uniform
+      // lane: row lane / 4 of the wave's 16, 32-dim block lane % 4 -> 32 e4m3 bytes + one e8m0 scale
+      const int row = lane >> 2, b = lane & 3;
+      const int qr = q0 + wid * 16 + row;
+      float v[32];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4v*>(ot + row * D + 32 * b + 8 * c), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[8 * c + j] = f[j];
+      }
+      float amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+      const int e = mx_exp(amax);
+      const float sc = __builtin_amdgcn_ldexpf(1.f, -e);
+      uint32_t w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t x = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i] * sc, v[4 * i + 1] * sc, 0, false);
+        w[i] = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2] * sc, v[4 * i + 3] * sc, x, true);
+      }
+      if (qr < len) {
+        uint8_t* dst = p.out8 + (size_t)(s0 + qr) * p.o_stride + hq * D + 32 * b;
+        *reinterpret_cast<uint4v*>(dst) = uint4v{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<uint4v*>(dst + 16) = uint4v{w[4], w[5], w[6], w[7]};
+        p.mx[((size_t)hq * p.mx_rows + s0 + qr) * 4 + b] = (uint8_t)(e + 127);
+      }
+      return;
+    }
+  }
   for (int c = lane; c < 16 * CPR; c += 64) {
     const int row = c / CPR, ch = c % CPR;
     const int qr = q0 + wid * 16 + row;
@@ -343,7 +381,8 @@ extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v
   const int max_tiles = (max_seqlen + kQT - 1) / kQT;
   PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)out, cu_seqlens, cu_seqlens_k,
                   q_stride, k_stride,
-                  v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal, nullptr, nullptr, 0};
+                  v_stride, o_stride, Hq, Hkv, nseq, max_tiles, scale, causal, nullptr, nullptr, 0,
+                  nullptr, nullptr, 0};
   dim3 grid(nseq * max_tiles, Hq);
   if (D == 128)
     prefill_attn_kernel<128, false><<<grid, 256, 0, s>>>(p, nullptr);
@@ -353,6 +392,25 @@ extern "C" int lwc_prefill_attention(const void* q, const void* k, const void* v
     prefill_attn_kernel<32, false><<<grid, 256, 0, s>>>(p, nullptr);
   else
     return -1;
+  return (int)hipGetLastError();
+}
+
+// The same with the output in MX form (D = 128, keys = queries): out8 [T, Hq * 128] e4m3 (row stride o8_stride
+// bytes), mx [Hq][mx_rows >= T][4] e8m0 — what the fp8 o projection's block-scaled MFMAs read, so the bf16
+// output and its row quantisation pass are gone.
+extern "C" int lwc_prefill_attention_mx(const void* q, const void* k, const void* v, void* out8, void* mx,
+                                        int mx_rows, const int* cu_seqlens, int nseq, int max_seqlen, int q_stride,
+                                        int k_stride, int v_stride, int o8_stride, int Hq, int Hkv, float scale,
+                                        int causal, hipStream_t s) {
+  using namespace lwc;
+  if (Hq % Hkv != 0 || o8_stride % 16 != 0) return -1;
+  if (nseq == 0 || max_seqlen == 0) return 0;
+  const int max_tiles = (max_seqlen + kQT - 1) / kQT;
+  PrefillParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, nullptr, cu_seqlens, nullptr, q_stride,
+                  k_stride, v_stride, o8_stride, Hq, Hkv, nseq, max_tiles, scale, causal, nullptr, nullptr, 0,
+                  (uint8_t*)out8, (uint8_t*)mx, mx_rows};
+  dim3 grid(nseq * max_tiles, Hq);
+  prefill_attn_kernel<128, false><<<grid, 256, 0, s>>>(p, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -368,7 +426,8 @@ extern "C" int lwc_prefill_attention_paged(const void* q, const void* kc, const 
   if (nseq == 0 || max_seqlen == 0) return 0;
   const int max_tiles = (max_seqlen + kQT - 1) / kQT;
   PrefillParams p{(const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, (bf16_t*)out, cu_seqlens, nullptr,
-                  q_stride, 0, 0, o_stride, Hq, Hkv, nseq, max_tiles, scale, 1, block_tables, k_lens, bt_stride};
+                  q_stride, 0, 0, o_stride, Hq, Hkv, nseq, max_tiles, scale, 1, block_tables, k_lens, bt_stride,
+                  nullptr, nullptr, 0};
   dim3 grid(nseq * max_tiles, Hq);
   prefill_attn_kernel<128, true><<<grid, 256, 0, s>>>(p, block_tables);
   return (int)hipGetLastError();

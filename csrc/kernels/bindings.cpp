@@ -32,6 +32,8 @@ int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, int, int, const void*, void*, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
+int lwc_moe_router(const void*, int, const void*, int, int, int, int, int*, float*, int*, int*, int*, void*,
+                   hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
 int lwc_quant_fp8_rows(const void*, int, int, void*, float*, hipStream_t);
 int lwc_ep_pack(const void*, const float*, const int*, const int*, int, int, int, int, int, void*, hipStream_t);
@@ -41,6 +43,8 @@ int lwc_ep_combine(const void*, const int*, const int*, const float*, int, int, 
 int lwc_silu_mul_quant_fp8(const void*, int, int, int, void*, float*, hipStream_t);
 int lwc_prefill_attention(const void*, const void*, const void*, void*, const int*, const int*, int, int, int, int, int, int, int,
                           int, int, float, int, hipStream_t);
+int lwc_prefill_attention_mx(const void*, const void*, const void*, void*, void*, int, const int*, int, int, int, int,
+                             int, int, int, int, float, int, hipStream_t);
 int lwc_prefill_attention_paged(const void*, const void*, const void*, void*, const int*, const int*, const int*, int, int,
                                 int, int, int, int, int, int, float, hipStream_t);
 int lwc_sample(const void*, int, int, int, const float*, const float*, const int*, const float*, const float*,
@@ -548,6 +552,28 @@ void moe_route(const at::Tensor& logits, int64_t k, at::Tensor& topk_ids, at::Te
            "moe_route");
 }
 
+void moe_router(const at::Tensor& h, const at::Tensor& router, int64_t k, at::Tensor& topk_ids, at::Tensor& topk_w,
+                at::Tensor& row_off, at::Tensor& src_row, at::Tensor& inv, const c10::optional<at::Tensor>& logits) {
+  CHECK_BF16(h); CHECK_BF16(router); CHECK_CONTIG(router);
+  TORCH_CHECK(h.dim() == 2 && router.dim() == 2 && h.size(1) == router.size(1) && h.stride(1) == 1,
+              "moe_router: h [T, d] (unit column stride), router [E, d]");
+  const int T = (int)h.size(0), E = (int)router.size(0), d = (int)h.size(1);
+  for (const at::Tensor* t : {&topk_ids, &row_off, &src_row, &inv}) {
+    CHECK_GPU(*t); CHECK_DTYPE(*t, at::kInt); CHECK_CONTIG(*t);
+  }
+  CHECK_DTYPE(topk_w, at::kFloat); CHECK_CONTIG(topk_w);
+  TORCH_CHECK(topk_ids.numel() >= (int64_t)T * k && topk_w.numel() >= (int64_t)T * k && src_row.numel() >= (int64_t)T * k &&
+              inv.numel() >= (int64_t)T * k && row_off.numel() == E + 1, "moe_router: output sizes");
+  if (logits.has_value()) {
+    CHECK_BF16(*logits); CHECK_CONTIG(*logits);
+    TORCH_CHECK(logits->numel() == (int64_t)T * E, "moe_router: logits [T, E]");
+  }
+  CHECK_RC(lwc_moe_router(h.data_ptr(), (int)h.stride(0), router.data_ptr(), T, E, d, (int)k, topk_ids.data_ptr<int>(),
+                          topk_w.data_ptr<float>(), row_off.data_ptr<int>(), src_row.data_ptr<int>(),
+                          inv.data_ptr<int>(), logits.has_value() ? logits->data_ptr() : nullptr, cur_stream()),
+           "moe_router");
+}
+
 // C4 expert-parallel exchange buffers (csrc/kernels/ep.hip): send / recv are uint8 [W, (C + 1) * RB].
 int64_t row_bytes_of(const at::Tensor& x) { return x.size(1) * (int64_t)x.element_size(); }
 
@@ -664,6 +690,29 @@ void prefill_attention(const at::Tensor& q, const at::Tensor& k, const at::Tenso
                                  (int)out.stride(0), (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0,
                                  cur_stream()),
            "prefill_attention");
+}
+
+void prefill_attention_mx(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out8, at::Tensor& mx,
+                          const at::Tensor& cu_seqlens, int64_t max_seqlen, int64_t Hq, int64_t Hkv, double scale,
+                          bool causal) {
+  // D = 128; out8 [T, Hq*128] e4m3 (uint8 view, 16-B aligned row stride), mx [Hq, >= T, 4] uint8 contiguous
+  CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_DTYPE(cu_seqlens, at::kInt);
+  CHECK_GPU(out8); CHECK_GPU(mx); CHECK_CONTIG(mx);
+  TORCH_CHECK(out8.element_size() == 1 && mx.element_size() == 1, "prefill_attention_mx: byte outputs");
+  TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.dim() == 2 && out8.dim() == 2, "prefill_attention_mx: 2-D views");
+  TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1 && out8.stride(1) == 1 && out8.stride(0) % 16 == 0,
+              "prefill_attention_mx: unit inner stride, 16-B row stride of out8");
+  TORCH_CHECK(q.size(1) == Hq * 128 && k.size(1) == Hkv * 128 && v.size(1) == Hkv * 128 && out8.size(1) == Hq * 128 &&
+                  out8.size(0) == q.size(0),
+              "prefill_attention_mx: head shape mismatch (head_dim 128)");
+  TORCH_CHECK(mx.dim() == 3 && mx.size(0) == Hq && mx.size(1) >= q.size(0) && mx.size(2) == 4,
+              "prefill_attention_mx: mx [Hq, >= T, 4]");
+  const int nseq = (int)cu_seqlens.numel() - 1;
+  CHECK_RC(lwc_prefill_attention_mx(q.data_ptr(), k.data_ptr(), v.data_ptr(), out8.data_ptr(), mx.data_ptr(),
+                                    (int)mx.size(1), cu_seqlens.data_ptr<int>(), nseq, (int)max_seqlen,
+                                    (int)q.stride(0), (int)k.stride(0), (int)v.stride(0), (int)out8.stride(0), (int)Hq,
+                                    (int)Hkv, (float)scale, causal ? 1 : 0, cur_stream()),
+           "prefill_attention_mx");
 }
 
 void prefill_attention_paged(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache, at::Tensor& out,
@@ -869,6 +918,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rms_rowsumsq", &rms_rowsumsq);
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
+  m.def("moe_router", &moe_router);
   m.def("moe_combine", &moe_combine);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("paged_decode_cascade", &paged_decode_cascade);
@@ -876,6 +926,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_decode_wave_min_items", &lwc_set_decode_wave_min_items,
         "B*Hkv*splits threshold of the wave-per-item decode kernel; returns the previous value");
   m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_attention_mx", &prefill_attention_mx);
   m.def("prefill_attention_paged", &prefill_attention_paged);
   m.def("silu_mul_quant_fp8", &silu_mul_quant_fp8);
   m.def("kv_gather", &kv_gather);

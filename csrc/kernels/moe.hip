@@ -1,12 +1,13 @@
 // K11 Mixture-of-experts plumbing (Mixtral-8x7B, BASELINE config 5) + fp8 activation quantisation.
 //
-//   moe_route   : router logits [T, E] -> top-k experts per token, their softmax weights
-//                 (Mixtral: softmax over all E, keep top-k, renormalise == softmax over the top-k
-//                 logits), per-expert segments row_off[E+1] and the dispatch permutation
-//                   src_row[pos] = token of expert-sorted row pos,   inv[t*k + j] = pos of (t, j).
-//                 One workgroup: counts in LDS, prefix in LDS, slots by LDS atomics.  Row order inside
-//                 an expert segment is arbitrary (atomics) but every row is computed independently,
-//                 so results are deterministic.  Everything stays on the device (graph-capturable).
+//   moe_router  : h [T, d] . router^T (the router GEMV, wave-per-TPW-tokens, reduce-scatter) fused with
+//                 the top-k: experts per token and their softmax weights (Mixtral: softmax over all E,
+//                 keep top-k, renormalise == softmax over the top-k logits); then
+//   moe_permute : per-expert segments row_off[E+1] and the dispatch permutation
+//                   src_row[pos] = token of expert-sorted row pos,   inv[t*k + j] = pos of (t, j)
+//                 (one workgroup: counts in LDS, prefix, slots by LDS atomics).
+//   moe_route   : the same from precomputed logits [T, E] (thread-per-token top-k + moe_permute).
+//                 Everything stays on the device (graph-capturable).
 //   moe_combine : out[t] = sum_j w[t, j] * Y[inv[t*k + j]]   (expert outputs back to token order)
 //   quant_fp8_rows : per-row dynamic e4m3 (OCP) quantisation: scale = amax / 448.
 // The expert GEMMs themselves are the grouped MFMA GEMM (gemm.hip) reading A through src_row.
@@ -17,63 +18,148 @@ namespace lwc {
 constexpr int kMaxExperts = 64;
 constexpr int kMaxTopK = 8;
 
+// Repeated arg-max top-k (ties -> lower expert id) + softmax over the selected logits of one token.
+// lv[EM]: the token's logits (experts >= E already -inf).  Writes ids / weights of (t, 0..k-1).
 template <int EM, int KM>
-__global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restrict__ logits, int T, int E, int k,
-                                                         int* __restrict__ topk_ids, float* __restrict__ topk_w,
-                                                         int* __restrict__ row_off, int* __restrict__ src_row,
-                                                         int* __restrict__ inv) {
+LWC_DEVICE void route_token(const float (&lv)[EM], int E, int k, int t, int* __restrict__ topk_ids,
+                            float* __restrict__ topk_w) {
+  bool taken[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) taken[e] = e >= E;
+  int ids[KM];
+  float vals[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    if (j >= k) break;
+    int best = 0;
+    float bv = -INFINITY;
+    bool found = false;
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      if (!taken[e] && (!found || lv[e] > bv)) {
+        best = e;
+        bv = lv[e];
+        found = true;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EM; ++e) taken[e] |= e == best;
+    ids[j] = best;
+    vals[j] = bv;
+  }
+  // softmax over the selected logits (vals[0] is the largest; read it once — the loop overwrites vals[0])
+  const float vmax = vals[0];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    if (j >= k) break;
+    vals[j] = __expf(vals[j] - vmax);
+    sum += vals[j];
+  }
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    if (j >= k) break;
+    topk_ids[t * k + j] = ids[j];
+    topk_w[t * k + j] = vals[j] / sum;
+  }
+}
+
+// top-k of precomputed router logits [T, E] bf16: one thread per token, many workgroups
+template <int EM, int KM>
+__global__ void __launch_bounds__(256) moe_topk_kernel(const bf16_t* __restrict__ logits, int T, int E, int k,
+                                                       int* __restrict__ topk_ids, float* __restrict__ topk_w) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  float lv[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) lv[e] = e < E ? bf2f(logits[(size_t)t * E + e]) : -INFINITY;
+  route_token<EM, KM>(lv, E, k, t, topk_ids, topk_w);
+}
+
+// Router GEMV fused with the top-k (K11a): logits[t, e] = <h[t, :], router[e, :]> for TPW tokens per wave.
+// A lane walks the row in 16-byte chunks (lane, lane + 64, ...) keeping EM x TPW fp32 partials; the wave
+// then reduce-SCATTERS them (each xor step trades half of the remaining partials with the partner lane), so
+// after log2(EM*TPW) steps lane l holds the full sum of value (l >> (6 - log2(EM*TPW))) — 63 shuffles for
+// 64 sums instead of 6 per sum.  The logit is rounded to bf16 as the unfused F.linear (bf16 out) would
+// hold it, so both paths pick the same experts.  The router rows (E x d bf16, 64 KB for Mixtral) are
+// re-read by every wave from L1/L2; h is read once.  256 threads = 4 waves = 4 * TPW tokens per block.
+template <int EM, int KM, int TPW>
+__global__ void __launch_bounds__(256) moe_router_kernel(const bf16_t* __restrict__ h, int ldh,
+                                                         const bf16_t* __restrict__ router, int T, int E, int d,
+                                                         int k, int* __restrict__ topk_ids,
+                                                         float* __restrict__ topk_w, bf16_t* __restrict__ logits) {
+  constexpr int NV = EM * TPW;
+  static_assert(NV <= 64 && (NV & (NV - 1)) == 0, "EM * TPW must be a power of two <= 64");
+  __shared__ float s_l[4][NV];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int t0 = (blockIdx.x * 4 + wv) * TPW;
+  float acc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) acc[i] = 0.f;
+  const int nc = d >> 3;
+  // rows past T / experts past E read a clamped (valid) row; their sums are never used
+  const bf16_t* hrow[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) hrow[j] = h + (size_t)min(t0 + j, T - 1) * ldh;
+#pragma unroll 1
+  for (int c = lane; c < nc; c += 64) {
+    float hv[TPW][8];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) unpack8(*reinterpret_cast<const uint4v*>(hrow[j] + c * 8), hv[j]);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      float rv[8];
+      unpack8(*reinterpret_cast<const uint4v*>(router + (size_t)min(e, E - 1) * d + c * 8), rv);
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) acc[j * EM + e] = fmaf(hv[j][x], rv[x], acc[j * EM + e]);
+    }
+  }
+  // reduce-scatter over the wave: step with xor mask m keeps half of the n live partials
+#pragma unroll
+  for (int n = NV, m = 32; n > 1; n >>= 1, m >>= 1) {
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float keep = up ? acc[i + n / 2] : acc[i];
+      const float send = up ? acc[i] : acc[i + n / 2];
+      acc[i] = keep + __shfl_xor(send, m);
+    }
+  }
+  constexpr int SH = 64 / NV;  // lanes sharing one value after the scatter: finish with a plain xor-sum
+#pragma unroll
+  for (int m = SH / 2; m >= 1; m >>= 1) acc[0] += __shfl_xor(acc[0], m);
+  if (lane % SH == 0) {
+    const int v = lane / SH;  // value index = token * EM + expert
+    s_l[wv][v] = bf2f(f2bf(acc[0]));
+  }
+  __syncthreads();
+  if (lane < TPW && t0 + lane < T) {
+    const int t = t0 + lane;
+    float lv[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      lv[e] = e < E ? s_l[wv][lane * EM + e] : -INFINITY;
+      if (logits != nullptr && e < E) logits[(size_t)t * E + e] = f2bf(lv[e]);
+    }
+    route_token<EM, KM>(lv, E, k, t, topk_ids, topk_w);
+  }
+}
+
+// Expert segments + dispatch permutation from topk_ids (one workgroup: LDS counts, prefix, LDS cursors).
+// Row order inside an expert segment is arbitrary (atomics), but every row is computed independently, so
+// results are deterministic.
+__global__ void __launch_bounds__(1024) moe_permute_kernel(const int* __restrict__ topk_ids, int n, int k, int E,
+                                                           int* __restrict__ row_off, int* __restrict__ src_row,
+                                                           int* __restrict__ inv) {
   __shared__ int s_count[kMaxExperts];
   __shared__ int s_cursor[kMaxExperts];
   const int tid = threadIdx.x;
   if (tid < E) s_count[tid] = 0;
   __syncthreads();
-  for (int t = tid; t < T; t += blockDim.x) {
-    // fully unrolled over the compile-time bounds so the per-token arrays stay in registers
-    float lv[EM];
-    bool taken[EM];
-#pragma unroll
-    for (int e = 0; e < EM; ++e) {
-      lv[e] = e < E ? bf2f(logits[(size_t)t * E + e]) : -INFINITY;
-      taken[e] = e >= E;
-    }
-    int ids[KM];
-    float vals[KM];
-#pragma unroll
-    for (int j = 0; j < KM; ++j) {  // repeated arg-max (ties -> lower expert id)
-      if (j >= k) break;
-      int best = 0;
-      float bv = -INFINITY;
-      bool found = false;
-#pragma unroll
-      for (int e = 0; e < EM; ++e) {
-        if (!taken[e] && (!found || lv[e] > bv)) {
-          best = e;
-          bv = lv[e];
-          found = true;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < EM; ++e) taken[e] |= e == best;
-      ids[j] = best;
-      vals[j] = bv;
-    }
-    // softmax over the selected logits (vals[0] is the largest; read it once — the loop overwrites vals[0])
-    const float vmax = vals[0];
-    float sum = 0.f;
-#pragma unroll
-    for (int j = 0; j < KM; ++j) {
-      if (j >= k) break;
-      vals[j] = __expf(vals[j] - vmax);
-      sum += vals[j];
-    }
-#pragma unroll
-    for (int j = 0; j < KM; ++j) {
-      if (j >= k) break;
-      topk_ids[t * k + j] = ids[j];
-      topk_w[t * k + j] = vals[j] / sum;
-      atomicAdd(&s_count[ids[j]], 1);
-    }
-  }
+#pragma unroll 8
+  for (int i = tid; i < n; i += 1024) atomicAdd(&s_count[topk_ids[i]], 1);
   __syncthreads();
   if (tid == 0) {
     int acc = 0;
@@ -85,9 +171,9 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16_t* __restric
     row_off[E] = acc;
   }
   __syncthreads();
-  for (int i = tid; i < T * k; i += blockDim.x) {
-    const int e = topk_ids[i];
-    const int pos = atomicAdd(&s_cursor[e], 1);
+#pragma unroll 8
+  for (int i = tid; i < n; i += 1024) {
+    const int pos = atomicAdd(&s_cursor[topk_ids[i]], 1);
     src_row[pos] = i / k;
     inv[i] = pos;
   }
@@ -230,14 +316,40 @@ extern "C" int lwc_moe_route(const void* logits, int T, int E, int k, int* topk_
     (void)hipMemsetAsync(row_off, 0, sizeof(int) * (E + 1), s);
     return (int)hipGetLastError();
   }
+  const dim3 grid((T + 255) / 256);
+  const bf16_t* lg = (const bf16_t*)logits;
   if (E <= 8 && k <= 2)
-    moe_route_kernel<8, 2><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w, row_off, src_row, inv);
+    moe_topk_kernel<8, 2><<<grid, 256, 0, s>>>(lg, T, E, k, topk_ids, topk_w);
   else if (E <= 16)
-    moe_route_kernel<16, kMaxTopK><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w, row_off,
-                                                       src_row, inv);
+    moe_topk_kernel<16, kMaxTopK><<<grid, 256, 0, s>>>(lg, T, E, k, topk_ids, topk_w);
   else
-    moe_route_kernel<kMaxExperts, kMaxTopK><<<1, 1024, 0, s>>>((const bf16_t*)logits, T, E, k, topk_ids, topk_w,
-                                                               row_off, src_row, inv);
+    moe_topk_kernel<kMaxExperts, kMaxTopK><<<grid, 256, 0, s>>>(lg, T, E, k, topk_ids, topk_w);
+  moe_permute_kernel<<<1, 1024, 0, s>>>(topk_ids, T * k, k, E, row_off, src_row, inv);
+  return (int)hipGetLastError();
+}
+
+// Router GEMV + top-k + permutation: h [T, d] bf16 (row stride ldh), router [E, d] bf16.  logits (optional,
+// [T, E] bf16) receives the rounded logits.  E <= 16; d % 8 == 0.
+extern "C" int lwc_moe_router(const void* h, int ldh, const void* router, int T, int E, int d, int k, int* topk_ids,
+                              float* topk_w, int* row_off, int* src_row, int* inv, void* logits, hipStream_t s) {
+  using namespace lwc;
+  if (E > 16 || k > kMaxTopK || k > E || k < 1 || d % 8 != 0 || ldh % 8 != 0) return -1;
+  if (T == 0) {
+    (void)hipMemsetAsync(row_off, 0, sizeof(int) * (E + 1), s);
+    return (int)hipGetLastError();
+  }
+  const bf16_t* hp = (const bf16_t*)h;
+  const bf16_t* rp = (const bf16_t*)router;
+  if (E <= 8 && k <= 2)
+    moe_router_kernel<8, 2, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+                                                                (bf16_t*)logits);
+  else if (E <= 8)
+    moe_router_kernel<8, kMaxTopK, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+                                                                       (bf16_t*)logits);
+  else
+    moe_router_kernel<16, kMaxTopK, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+                                                                        (bf16_t*)logits);
+  moe_permute_kernel<<<1, 1024, 0, s>>>(topk_ids, T * k, k, E, row_off, src_row, inv);
   return (int)hipGetLastError();
 }
 

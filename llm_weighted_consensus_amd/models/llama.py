@@ -300,7 +300,8 @@ class LlamaModel:
                               rope_q=rope_q)
             attn = attn_fn(qkv, li)
             if keep is not None and li + 1 == len(self.layers):
-                attn = attn.reshape(T, Hq * D).index_select(0, keep)
+                attn = attn.index_select(keep) if isinstance(attn, ops.MXAct) else \
+                    attn.reshape(T, Hq * D).index_select(0, keep)
                 x_res = x_res.index_select(0, keep)
                 T = x_res.shape[0]
             nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
@@ -328,7 +329,7 @@ class LlamaModel:
     _mlp_reads_bf16 = False
 
     def _attn_mx(self) -> bool:
-        """Whether the decode attention hands the o projection an MX activation: fp8 o weights on gemm8g
+        """Whether the attention kernels (decode cascade, prefill) hand the o projection an MX activation: fp8 o weights on gemm8g
         (head_dim 128, every head one 128-wide K slice); LWC_ATTN_MX=0 keeps bf16 + the row quantisation."""
         L = self.layers[0]
         return (os.environ.get("LWC_ATTN_MX", "1") != "0" and isinstance(L.wo, ops.Fp8Weight)
@@ -522,9 +523,13 @@ class LlamaModel:
         null = _NullCache(cfg, self.device)
         x = ops.embedding(self.embed, tokens)
 
+        mx = self._attn_mx()  # fp8 o projection: the attention epilogue writes its MX operand
+
         def attn_fn(qkv, li):
-            return ops.prefill_attention(qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:],
-                                         cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
+            q, k, v = qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+            if mx:
+                return ops.prefill_attention_mx(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, self.scale, causal=True)
+            return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
 
         return self._layers(x, null, positions, None, attn_fn, keep=keep)
 
@@ -540,6 +545,7 @@ class LlamaModel:
         cfg = self.cfg
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
         x = ops.embedding(self.embed, tokens)
+        mx = self._attn_mx()  # fp8 o projection: the attention epilogue writes its MX operand
 
         def attn_fn(qkv, li):
             q = qkv[:, : Hq * D]
@@ -549,6 +555,8 @@ class LlamaModel:
                                              cu_seqlens_k=ctx["cu_k"], lens=(ctx["q_lens"], ctx["k_lens"]))
             k = qkv[:, Hq * D:(Hq + Hkv) * D]
             v = qkv[:, (Hq + Hkv) * D:]
+            if mx:
+                return ops.prefill_attention_mx(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, self.scale, causal=True)
             return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
 
         h = self._layers(x, cache, positions, slots, attn_fn, keep=last_idx)  # last layer: o / MLP on these rows

@@ -4,8 +4,8 @@ tensor-parallel degree 2).
 Attention, KV cache, prefill/decode/cascade paths are the Llama ones (`LlamaModel`); only the MLP
 changes.  Per layer, for the T tokens of a step:
 
-    logits = h Wr^T                      [T, E]        hipBLASLt (tiny)
-    route  = top-k softmax, segments     K11a moe_route (one workgroup, all on the device)
+    route  = h Wr^T, top-k softmax       K11a moe_router: the router GEMV fused with the top-k (many
+             segments + permutation         workgroups), then one workgroup for segments / permutation
     gu     = grouped GEMM over experts   K6g, A rows gathered through src_row (no permute copy)
     act    = silu(g) * u                 K5
     y      = grouped GEMM over experts   K6g
@@ -248,7 +248,7 @@ class MixtralModel(LlamaModel):
         exact (prefill) mode."""
         k = self.full_cfg.experts_per_token
         h, hq, hs = self._split_act(h)
-        _ids, w, row_off, src, inv = ops.moe_route(F.linear(h, L.router), k)
+        _ids, w, row_off, src, inv = ops.route(h, L.router, k)
         cap = None if self.ep_capacity is None else self.ep_capacity * k
         if h.is_cuda and self.ep.mode == "padded":
             if self.fp8 and hq is None:
@@ -272,8 +272,7 @@ class MixtralModel(LlamaModel):
             return self._mlp_ep(h, L)
         k = self.full_cfg.experts_per_token
         h, hq, hs = self._split_act(h)
-        logits = F.linear(h, L.router)
-        _ids, w, row_off, src, inv = ops.moe_route(logits, k)
+        _ids, w, row_off, src, inv = ops.route(h, L.router, k)
         rows = h.shape[0] * k
         if self.fp8:
             if hq is None:

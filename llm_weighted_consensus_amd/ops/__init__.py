@@ -183,6 +183,11 @@ class MXAct:
     def __init__(self, q: torch.Tensor, mx: torch.Tensor):
         self.q, self.mx = q, mx
 
+    def index_select(self, rows: torch.Tensor) -> "MXAct":
+        """The activation of ``rows`` only (a prefill's kept last tokens)."""
+        q = self.q.view(torch.uint8).index_select(0, rows).view(self.q.dtype)
+        return MXAct(q, self.mx.index_select(1, rows).contiguous())
+
 
 def paged_decode_cascade(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                          ctx_lens: torch.Tensor, tiles: torch.Tensor, Hq: int, scale: float,
@@ -229,6 +234,19 @@ def prefill_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seql
     kernels().prefill_attention(q, k, v, out, cu_seqlens, int(max_seqlen), int(Hq), int(Hkv), int(D), float(scale),
                                 bool(causal), cu_seqlens_k)
     return out
+
+
+def prefill_attention_mx(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor,
+                         max_seqlen: int, Hq: int, Hkv: int, scale: float, causal: bool) -> "MXAct":
+    """:func:`prefill_attention` (head_dim 128, keys = queries) with the output in MX form for the fp8 o
+    projection: e4m3 rows [T, Hq*128] + e8m0 scales [Hq, T, 4] straight from the kernel's epilogue (the
+    decode cascade kernel's format) — no bf16 output, no row quantisation pass."""
+    T = q.shape[0]
+    q8 = torch.empty(T, Hq * 128, dtype=torch.float8_e4m3fn, device=q.device)
+    mx = torch.empty(Hq, T, 4, dtype=torch.uint8, device=q.device)
+    kernels().prefill_attention_mx(q, k, v, q8.view(torch.uint8), mx, cu_seqlens, int(max_seqlen), int(Hq), int(Hkv),
+                                   float(scale), bool(causal))
+    return MXAct(q8, mx)
 
 
 def prefill_attention_paged(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_seqlens: torch.Tensor,
@@ -494,6 +512,32 @@ def moe_route(logits: torch.Tensor, k: int):
     inv = torch.empty(T * k, dtype=torch.int32, device=dev)
     kernels().moe_route(logits.contiguous(), int(k), ids, w, row_off, src, inv)
     return ids, w, row_off, src, inv
+
+
+def moe_router(h: torch.Tensor, router: torch.Tensor, k: int, want_logits: bool = False):
+    """Router GEMV fused with :func:`moe_route` (K11a): h [T, d] bf16 . router [E, d]^T -> the same five
+    tensors (plus the bf16 logits [T, E] with ``want_logits``).  The logits are rounded to bf16 inside the
+    kernel as ``F.linear`` would hold them, so expert choices match the unfused path.  E <= 16."""
+    T = h.shape[0]
+    E = router.shape[0]
+    dev = h.device
+    ids = torch.empty(T, k, dtype=torch.int32, device=dev)
+    w = torch.empty(T, k, dtype=torch.float32, device=dev)
+    row_off = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    src = torch.empty(T * k, dtype=torch.int32, device=dev)
+    inv = torch.empty(T * k, dtype=torch.int32, device=dev)
+    logits = torch.empty(T, E, dtype=torch.bfloat16, device=dev) if want_logits else None
+    kernels().moe_router(h, router.contiguous(), int(k), ids, w, row_off, src, inv, logits)
+    out = (ids, w, row_off, src, inv)
+    return out + (logits,) if want_logits else out
+
+
+def route(h: torch.Tensor, router: torch.Tensor, k: int):
+    """MoE routing of bf16 rows: the fused router kernel on the GPU (E <= 16, d % 8 == 0), else the
+    router projection + :func:`moe_route`."""
+    if h.is_cuda and router.shape[0] <= 16 and h.shape[1] % 8 == 0 and h.stride(1) == 1 and h.stride(0) % 8 == 0:
+        return moe_router(h, router, k)
+    return moe_route(torch.nn.functional.linear(h, router), k)
 
 
 def moe_combine(Y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, k: int,

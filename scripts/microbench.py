@@ -479,6 +479,40 @@ def small(dev):
         print(f"silu_mul T={T}: {us:6.1f} us", flush=True)
 
 
+def route_ab(dev):
+    """Config-5 MoE plumbing at the decode batch (T = 4096 tokens, Mixtral d = 4096, 8 experts, top-2):
+    the router projection + route (unfused: F.linear then moe_route) vs the fused moe_router kernel, and
+    the other small per-layer kernels around the experts.  Median of 5 interleaved rounds."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    T, d, E = int(os.environ.get("ROUTE_T", "4096")), 4096, 8
+    h = torch.randn(T, d, device=dev).to(torch.bfloat16)
+    r = torch.randn(T, d, device=dev).to(torch.bfloat16)
+    router = (torch.randn(E, d, device=dev) * 0.05).to(torch.bfloat16)
+    ones = torch.ones(d, device=dev, dtype=torch.bfloat16)
+    lg = F.linear(h, router)
+    _ids, w, _ro, _src, inv = ops.moe_route(lg, 2)
+    Y = torch.randn(2 * T, d, device=dev).to(torch.bfloat16)
+    runs = {
+        "router F.linear": lambda: F.linear(h, router),
+        "moe_route (logits)": lambda: ops.moe_route(lg, 2),
+        "unfused (linear + route)": lambda: ops.moe_route(F.linear(h, router), 2),
+        "fused moe_router": lambda: ops.moe_router(h, router, 2),
+        "rmsnorm+res+q (bf16 kept)": lambda: ops.rmsnorm_quant_fp8(h, ones, 1e-5, residual=r, keep_bf16=True),
+        "rmsnorm+res": lambda: ops.rmsnorm(h, ones, 1e-5, residual=r),
+        "quant_fp8_rows": lambda: ops.quant_fp8_rows(h),
+        "moe_combine": lambda: ops.moe_combine(Y, inv, w, 2),
+    }
+    res = {k: [] for k in runs}
+    for _ in range(5):
+        for k, fn in runs.items():
+            res[k].append(timeit(fn, iters=20, warm=3))
+    for k, t in res.items():
+        print(f"route T={T} {k}: {sorted(t)[2]:8.1f} us", flush=True)
+
+
 def chain_ab(dev):
     """Folded-RMSNorm decode chain at the headline's decode batch (Llama-3-8B shapes, M = 4096; random
     operands): per projection the unfolded backends (hipBLASLt / gemm4w, + the norm kernel) vs the row-scaled
@@ -548,6 +582,8 @@ def main():
         gemm4w_ab(dev)
     if "chain" in a.what:
         chain_ab(dev)
+    if "route" in a.what:
+        route_ab(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:

@@ -310,6 +310,39 @@ def test_prefill_attention(gpu, D, Hq, Hkv, causal):
         _close(out[s0:s0 + L].view(L, Hq, D), o, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("Hq,Hkv,causal", [(8, 2, True), (4, 4, False)])
+def test_prefill_attention_mx_matches_fp32(gpu, Hq, Hkv, causal):
+    """MX epilogue of the prefill kernel (the fp8 o projection's operand, config 5's embedder / prefill):
+    e4m3 rows + one e8m0 scale per 32 dims of a head.  Dequantised it is within e4m3 rounding of the fp32
+    attention oracle (per-sequence relative Frobenius norm), every block's scale is tight (block amax lands
+    in the top binade of e4m3), and the kept-row selection picks whole rows + their scales."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(3)
+    D = 128
+    lens = [1, 17, 64, 100, 130]
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=gpu)
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, dev=gpu)
+    q, k, v = qkv[:, : Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    a = ops.prefill_attention_mx(q, k, v, cu, max(lens), Hq, Hkv, 1 / math.sqrt(D), causal)
+    assert a.q.shape == (T, Hq * D) and a.mx.shape == (Hq, T, 4)
+    dims = torch.arange(Hq * D, device=gpu)
+    deq = a.q.float() * torch.exp2(a.mx.float() - 127.0)[dims // 128, :, (dims % 128) // 32].t()
+    for i, L in enumerate(lens):
+        s0 = int(cu[i])
+        o = ref.attention(q[s0:s0 + L].reshape(L, Hq, D).float(), k[s0:s0 + L].reshape(L, Hkv, D).float(),
+                          v[s0:s0 + L].reshape(L, Hkv, D).float(), causal, 1 / math.sqrt(D)).reshape(L, -1)
+        got = deq[s0:s0 + L]
+        assert ((got - o).norm() / o.norm()).item() < 4e-2, i
+    bmax = a.q.float().abs().view(T, -1, 32).amax(-1)
+    assert (bmax[bmax > 0] >= 224).all()
+    keep = torch.tensor([0, 17, 80, T - 1], device=gpu)
+    sub = a.index_select(keep)
+    assert torch.equal(sub.q.view(torch.uint8), a.q.view(torch.uint8)[keep])
+    assert torch.equal(sub.mx, a.mx[:, keep])
+
+
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 4, 4)])
 def test_prefill_attention_key_ranges(gpu, D, Hq, Hkv):
     """Cached-prefix prefill: each sequence's queries are the LAST rows of a longer key range (causal
@@ -933,6 +966,58 @@ def test_moe_route_matches_torch(gpu, T, E, k):
         got = torch.sort(src_l[ro[e]:ro[e + 1]]).values
         want = torch.sort(tok[tid.flatten() == e]).values
         assert torch.equal(got, want), e
+
+
+def _check_permutation(gpu, ids, row_off, src, inv, T, E, k):
+    tid = ids.long()
+    cnt = torch.bincount(tid.flatten(), minlength=E)
+    assert torch.equal(row_off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0).cpu()]))
+    inv_l, src_l = inv.long(), src.long()
+    tok = torch.arange(T, device=gpu).repeat_interleave(k)
+    assert torch.equal(src_l[inv_l], tok)
+    assert torch.equal(torch.sort(inv_l).values, torch.arange(T * k, device=gpu))
+    ro = row_off.long().tolist()
+    for e in range(E):
+        got = torch.sort(src_l[ro[e]:ro[e + 1]]).values
+        want = torch.sort(tok[tid.flatten() == e]).values
+        assert torch.equal(got, want), e
+
+
+@pytest.mark.parametrize("T,E,k,d,ld", [(1, 8, 2, 4096, 4096), (77, 8, 2, 4096, 4096), (4096, 8, 2, 4096, 4096),
+                                        (300, 6, 2, 512, 520), (129, 16, 4, 1024, 1024), (50, 8, 3, 256, 256)])
+def test_moe_router_matches_fp32(gpu, T, E, k, d, ld):
+    """The router GEMV fused with the top-k (K11a moe_router: TPW tokens per wave, wave reduce-scatter of
+    the E x TPW partial sums): logits within a bf16 rounding of the fp32 product (the kernel rounds them to
+    bf16 as F.linear would); the experts are the top-k of the kernel's own logits and match the fp32 top-k
+    wherever the fp32 logits are not within a rounding of a tie; weights = softmax of the selected logits;
+    the permutation as in moe_route.  E = 6 / row stride 520 cover a padded expert set and strided rows."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(31)
+    hb = (torch.randn(T, ld, device=gpu) * 0.5).to(torch.bfloat16)
+    h = hb[:, :d]
+    router = (torch.randn(E, d, device=gpu) * 0.05).to(torch.bfloat16)
+    ids, w, row_off, src, inv, lg = ops.moe_router(h, router, k, want_logits=True)
+    ref = h.float() @ router.float().t()
+    torch.testing.assert_close(lg.float(), ref, rtol=1.6e-2, atol=1e-3)
+    tid = ids.long()
+    lgf = lg.float()
+    top, _ = lgf.topk(k, dim=-1)
+    assert torch.equal(lgf.gather(1, tid), top)
+    assert all(len(set(r)) == k for r in tid.tolist())
+    torch.testing.assert_close(w, top.softmax(-1), rtol=1e-5, atol=1e-6)
+    # vs the fp32 oracle: the chosen set equals fp32's top-k unless the k-th / (k+1)-th logits nearly tie
+    rs, _ = ref.sort(-1, descending=True)
+    clear = (rs[:, k - 1] - rs[:, k]) > 0.02 * rs.abs().max(-1).values.clamp_min(1e-3) if k < E else \
+        torch.ones(T, dtype=torch.bool, device=gpu)
+    ref_set = ref.topk(k, -1).indices.sort(-1).values
+    assert torch.equal(tid.sort(-1).values[clear], ref_set[clear])
+    assert clear.float().mean() > 0.8
+    _check_permutation(gpu, ids, row_off, src, inv, T, E, k)
+    # the unfused pair on the same bf16 logits routes identically
+    ids2, w2, row_off2, _, _ = ops.moe_route(lg, k)
+    assert torch.equal(ids2, ids) and torch.equal(row_off2, row_off)
+    torch.testing.assert_close(w2, w, rtol=0, atol=0)
 
 
 def _mx_scale_map(mx: torch.Tensor, K: int) -> torch.Tensor:

@@ -167,7 +167,7 @@ def test_mixtral_moe_matches_reference_and_engine(gpu, fp8):
                    torch.tensor([P - 1], device=gpu), cache)
     # measured 0.99999 (bf16) / 0.9990 (fp8) over seeds 2-4 (scripts/mixtral_cos_probe.py); the bounds leave room
     # for a near-tie router flip.  (They were 0.99 / 0.985 while the router's softmax was wrong — README.)
-    assert _cos(lg[0], ref_logits[P - 1]) > (0.995 if fp8 else 0.999)
+    assert _cos(lg[0], ref_logits[P - 1]) > (0.998 if fp8 else 0.999)
     tok = ByteTokenizer(m.cfg.vocab_size)
     eng = LLMEngine(m, tok, num_blocks=1024, max_batch=160, max_model_len=512, cascade_min_batch=1)
     sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
