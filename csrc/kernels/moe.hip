@@ -76,13 +76,14 @@ __global__ void __launch_bounds__(256) moe_topk_kernel(const bf16_t* __restrict_
   route_token<EM, KM>(lv, E, k, t, topk_ids, topk_w);
 }
 
-// Router GEMV fused with the top-k (K11a): logits[t, e] = <h[t, :], router[e, :]> for TPW tokens per wave.
-// A lane walks the row in 16-byte chunks (lane, lane + 64, ...) keeping EM x TPW fp32 partials; the wave
-// then reduce-SCATTERS them (each xor step trades half of the remaining partials with the partner lane), so
-// after log2(EM*TPW) steps lane l holds the full sum of value (l >> (6 - log2(EM*TPW))) — 63 shuffles for
-// 64 sums instead of 6 per sum.  The logit is rounded to bf16 as the unfused F.linear (bf16 out) would
-// hold it, so both paths pick the same experts.  The router rows (E x d bf16, 64 KB for Mixtral) are
-// re-read by every wave from L1/L2; h is read once.  256 threads = 4 waves = 4 * TPW tokens per block.
+// Router GEMV fused with the top-k (K11a): logits[t, e] = <h[t, :], router[e, :]> for the TPW tokens of a
+// workgroup.  The 4 waves split the row (wave w takes 16-byte chunks w*64 + lane + 256 i), each lane keeps
+// EM x TPW fp32 partials, issuing all of its h / router loads of an iteration before the FMAs.  A wave then
+// reduce-SCATTERS its partials (each xor step trades half of the remaining values with the partner lane),
+// so after log2(EM*TPW) steps lane l holds the wave sum of value (l >> (6 - log2(EM*TPW))) — 31 shuffles
+// for 32 sums instead of 6 per sum — and the 4 wave sums meet in LDS.  The logit is rounded to bf16 as the
+// unfused F.linear (bf16 out) would hold it, so both paths pick the same experts.  The router rows (E x d
+// bf16, 64 KB for Mixtral) are L2-resident; h is read once.
 template <int EM, int KM, int TPW>
 __global__ void __launch_bounds__(256) moe_router_kernel(const bf16_t* __restrict__ h, int ldh,
                                                          const bf16_t* __restrict__ router, int T, int E, int d,
@@ -90,9 +91,10 @@ __global__ void __launch_bounds__(256) moe_router_kernel(const bf16_t* __restric
                                                          float* __restrict__ topk_w, bf16_t* __restrict__ logits) {
   constexpr int NV = EM * TPW;
   static_assert(NV <= 64 && (NV & (NV - 1)) == 0, "EM * TPW must be a power of two <= 64");
-  __shared__ float s_l[4][NV];
+  __shared__ float s_part[4][NV];
+  __shared__ float s_l[NV];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int t0 = (blockIdx.x * 4 + wv) * TPW;
+  const int t0 = blockIdx.x * TPW;
   float acc[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) acc[i] = 0.f;
@@ -101,15 +103,23 @@ __global__ void __launch_bounds__(256) moe_router_kernel(const bf16_t* __restric
   const bf16_t* hrow[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) hrow[j] = h + (size_t)min(t0 + j, T - 1) * ldh;
-#pragma unroll 1
-  for (int c = lane; c < nc; c += 64) {
+  const bf16_t* rrow[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) rrow[e] = router + (size_t)min(e, E - 1) * d;
+#pragma unroll 2
+  for (int c = wv * 64 + lane; c < nc; c += 256) {
+    uint4v hr[TPW], rr[EM];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) hr[j] = *reinterpret_cast<const uint4v*>(hrow[j] + c * 8);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) rr[e] = *reinterpret_cast<const uint4v*>(rrow[e] + c * 8);
     float hv[TPW][8];
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) unpack8(*reinterpret_cast<const uint4v*>(hrow[j] + c * 8), hv[j]);
+    for (int j = 0; j < TPW; ++j) unpack8(hr[j], hv[j]);
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
       float rv[8];
-      unpack8(*reinterpret_cast<const uint4v*>(router + (size_t)min(e, E - 1) * d + c * 8), rv);
+      unpack8(rr[e], rv);
 #pragma unroll
       for (int j = 0; j < TPW; ++j)
 #pragma unroll
@@ -130,17 +140,19 @@ __global__ void __launch_bounds__(256) moe_router_kernel(const bf16_t* __restric
   constexpr int SH = 64 / NV;  // lanes sharing one value after the scatter: finish with a plain xor-sum
 #pragma unroll
   for (int m = SH / 2; m >= 1; m >>= 1) acc[0] += __shfl_xor(acc[0], m);
-  if (lane % SH == 0) {
-    const int v = lane / SH;  // value index = token * EM + expert
-    s_l[wv][v] = bf2f(f2bf(acc[0]));
+  if (lane % SH == 0) s_part[wv][lane / SH] = acc[0];  // value index = token * EM + expert
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const int v = threadIdx.x;  // fixed summation order over the waves: deterministic
+    s_l[v] = bf2f(f2bf(((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v]));
   }
   __syncthreads();
-  if (lane < TPW && t0 + lane < T) {
-    const int t = t0 + lane;
+  if (threadIdx.x < TPW && t0 + (int)threadIdx.x < T) {
+    const int j = threadIdx.x, t = t0 + j;
     float lv[EM];
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
-      lv[e] = e < E ? s_l[wv][lane * EM + e] : -INFINITY;
+      lv[e] = e < E ? s_l[j * EM + e] : -INFINITY;
       if (logits != nullptr && e < E) logits[(size_t)t * E + e] = f2bf(lv[e]);
     }
     route_token<EM, KM>(lv, E, k, t, topk_ids, topk_w);
@@ -155,11 +167,23 @@ __global__ void __launch_bounds__(1024) moe_permute_kernel(const int* __restrict
                                                            int* __restrict__ inv) {
   __shared__ int s_count[kMaxExperts];
   __shared__ int s_cursor[kMaxExperts];
+  constexpr int PT = 8;  // n <= 8192 (the decode batches): every id read once, into registers
   const int tid = threadIdx.x;
+  const bool held = n <= 1024 * PT;
+  int ids[PT];
   if (tid < E) s_count[tid] = 0;
+  if (held) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) ids[i] = tid + 1024 * i < n ? topk_ids[tid + 1024 * i] : -1;
+  }
   __syncthreads();
-#pragma unroll 8
-  for (int i = tid; i < n; i += 1024) atomicAdd(&s_count[topk_ids[i]], 1);
+  if (held) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+      if (ids[i] >= 0) atomicAdd(&s_count[ids[i]], 1);
+  } else {
+    for (int i = tid; i < n; i += 1024) atomicAdd(&s_count[topk_ids[i]], 1);
+  }
   __syncthreads();
   if (tid == 0) {
     int acc = 0;
@@ -171,11 +195,22 @@ __global__ void __launch_bounds__(1024) moe_permute_kernel(const int* __restrict
     row_off[E] = acc;
   }
   __syncthreads();
-#pragma unroll 8
-  for (int i = tid; i < n; i += 1024) {
-    const int pos = atomicAdd(&s_cursor[topk_ids[i]], 1);
-    src_row[pos] = i / k;
-    inv[i] = pos;
+  if (held) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      if (ids[i] >= 0) {
+        const int idx = tid + 1024 * i;
+        const int pos = atomicAdd(&s_cursor[ids[i]], 1);
+        src_row[pos] = idx / k;
+        inv[idx] = pos;
+      }
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      const int pos = atomicAdd(&s_cursor[topk_ids[i]], 1);
+      src_row[pos] = i / k;
+      inv[i] = pos;
+    }
   }
 }
 
@@ -341,13 +376,13 @@ extern "C" int lwc_moe_router(const void* h, int ldh, const void* router, int T,
   const bf16_t* hp = (const bf16_t*)h;
   const bf16_t* rp = (const bf16_t*)router;
   if (E <= 8 && k <= 2)
-    moe_router_kernel<8, 2, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+    moe_router_kernel<8, 2, 4><<<(T + 3) / 4, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
                                                                 (bf16_t*)logits);
   else if (E <= 8)
-    moe_router_kernel<8, kMaxTopK, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+    moe_router_kernel<8, kMaxTopK, 4><<<(T + 3) / 4, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
                                                                        (bf16_t*)logits);
   else
-    moe_router_kernel<16, kMaxTopK, 4><<<(T + 15) / 16, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
+    moe_router_kernel<16, kMaxTopK, 4><<<(T + 3) / 4, 256, 0, s>>>(hp, ldh, rp, T, E, d, k, topk_ids, topk_w,
                                                                         (bf16_t*)logits);
   moe_permute_kernel<<<1, 1024, 0, s>>>(topk_ids, T * k, k, E, row_off, src_row, inv);
   return (int)hipGetLastError();

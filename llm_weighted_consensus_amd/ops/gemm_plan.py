@@ -6,7 +6,11 @@ Backends computing ``A . W^T`` for the dense projections:
 * ``g8``     — the hand-written 8-phase MFMA GEMM with a stream-K tail (``csrc/kernels/gemm8p.hip``);
 * ``g4``     — the hand-written 4-wave interleaved MFMA GEMM, 256 x 256 tiles (``csrc/kernels/gemm4w.hip``);
 * ``g4n192`` — the same core with 256 x 192 tiles (the qkv projection at decode batch 4096: 512 tiles =
-  two whole rounds of 256 CUs, where 256 x 256 tiles leave half of the second round idle).
+  two whole rounds of 256 CUs, where 256 x 256 tiles leave half of the second round idle);
+* ``g4p``    — gemm4w 256 x 256 with the VAR 64 schedule: each persistent workgroup prefetches its next
+  tile's first two K tiles under the current tile's (wave-local) epilogue — multi-round shapes with few
+  K tiles per output tile (the encoders' K = 768 / 1024 projections, mixed-prefill gate|up).  Not for the
+  plain residual epilogue (its VAR 64 form is the block-staged one: nothing to gain).
 
 The hand-written cores also fuse the SwiGLU of the gate|up projection, or the residual add of the o /
 down projections (:func:`linear_add_`), into their epilogue.  None wins everywhere
@@ -26,7 +30,7 @@ import torch.nn.functional as F
 from . import gemm4w, gemm8p, silu_mul
 
 MODE = os.environ.get("LWC_GEMM", "auto")
-BACKENDS = ("blas", "g8", "g4", "g4n192")
+BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p")
 # a hand-written core is chosen unless the library is faster by more than this fraction
 OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "0.01"))
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
@@ -61,13 +65,13 @@ def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
     """Whether hand-written backend ``b`` takes this call (layout and the cores' shape rules)."""
     if b == "blas" or not _g8_ok(N, K, epi) or x.stride(1) != 1:
         return False
-    return not (b == "g4n192" and epi == "swiglu")
+    return not ((b == "g4n192" and epi == "swiglu") or (b == "g4p" and epi == "residual"))
 
 
 def _own(b: str, x: torch.Tensor, w: torch.Tensor, ws=None, **kw) -> torch.Tensor:
     if b == "g8":
         return gemm8p(x, w, ws=ws, **kw)
-    return gemm4w(x, w, bn=192 if b == "g4n192" else 256, **kw)
+    return gemm4w(x, w, bn=192 if b == "g4n192" else 256, var=64 if b == "g4p" else 0, **kw)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, ws=None) -> torch.Tensor:
@@ -116,17 +120,19 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
     the fp32 erf-GELU at the bge-large FFN1 shape — the bf16 output's own rounding, 7.8e-3 for gemm8p's
     exact erf — where GEMM + the K9b bias_gelu pass rounds twice, 1.6e-2, and runs 657 vs 510 us at
     65536 tokens: scripts/gelu_epilogue_probe.py).  The backend is chosen per (token bucket, N, K,
-    epilogue) by timing the library and both hand-written cores (gemm8p, gemm4w) on the first call."""
+    epilogue) by timing the library and the hand-written cores (gemm8p, gemm4w, gemm4w VAR 64) on the first
+    call."""
     M, K = x.shape
     N = w.shape[0]
     epi = "bias_gelu" if gelu else "bias"
     key = (_m_bucket(M), N, K, epi)
-    c = MODE if MODE in ("blas", "g8", "g4") else _CHOICE.get(key)
+    c = MODE if MODE in ("blas", "g8", "g4", "g4p") else _CHOICE.get(key)
     # the hand-written cores address A through 32-bit buffer offsets: operands of 2 GiB or more take the
     # library path
     ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda and M * x.stride(0) * 2 < (1 << 31)
     runs = {"g8": lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws),
             "g4": lambda: gemm4w(x, w, bias=b, gelu=gelu),
+            "g4p": lambda: gemm4w(x, w, bias=b, gelu=gelu, var=64),
             "blas": ((lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu
                      else (lambda: F.linear(x, w, b)))}
     if c is None:
@@ -135,7 +141,7 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
         else:
             t = {name: _time(fn, iters=2, rounds=3) for name, fn in runs.items()}
             TIMINGS[key] = t
-            own = min(("g8", "g4"), key=lambda n: t[n])
+            own = min(("g8", "g4", "g4p"), key=lambda n: t[n])
             c = own if t[own] <= t["blas"] * (1 + OWN_MARGIN) else "blas"
         _CHOICE[key] = c
     return runs[c]() if c != "blas" and ok else runs["blas"]()

@@ -479,6 +479,37 @@ def small(dev):
         print(f"silu_mul T={T}: {us:6.1f} us", flush=True)
 
 
+def encoder_gemms(dev):
+    """The encoders' small-K projections (config 2 bge-base: d = 768, FFN 3072; bge-large: 1024 / 4096) at
+    ENC_M tokens: hipBLASLt (bias / bias+GELU epilogue) vs gemm8p, gemm4w (VAR 32) and gemm4w VAR 64 (next
+    tile's prologue under the epilogue).  Median of 5 interleaved rounds."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    M = int(os.environ.get("ENC_M", "524288"))  # config 2: 64 requests x 64 candidates x 128 tokens
+    d = int(os.environ.get("ENC_D", "768"))
+    shapes = [(3 * d, d, False), (d, d, False), (4 * d, d, True), (d, 4 * d, False)]
+    for N, K, gelu in shapes:
+        x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+        b = (torch.randn(N, device=dev) * 0.1).to(torch.bfloat16)
+        runs = {
+            "blas": (lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu else (lambda: F.linear(x, w, b)),
+            "g8": lambda: ops.gemm8p(x, w, bias=b, gelu=gelu),
+            "g4": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu),
+            "g4p": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu, var=64),
+            "g4p192": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu, var=64, bn=192),
+        }
+        res = {k: [] for k in runs}
+        for _ in range(5):
+            for k, fn in runs.items():
+                res[k].append(timeit(fn, iters=5, warm=1))
+        line = "  ".join(f"{k} {sorted(t)[2]:8.1f}" for k, t in res.items())
+        print(f"enc M={M} {N}x{K}{' gelu' if gelu else ''}: {line} us", flush=True)
+        del x, w
+
+
 def route_ab(dev):
     """Config-5 MoE plumbing at the decode batch (T = 4096 tokens, Mixtral d = 4096, 8 experts, top-2):
     the router projection + route (unfused: F.linear then moe_route) vs the fused moe_router kernel, and
@@ -584,6 +615,8 @@ def main():
         chain_ab(dev)
     if "route" in a.what:
         route_ab(dev)
+    if "enc" in a.what:
+        encoder_gemms(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:

@@ -1266,7 +1266,12 @@ def test_gemm8p_bias_gelu_epilogue(gpu, M, N, K, gelu):
                                        # > 256 tiles: every epilogue across persistent rounds (VAR 64's
                                        # cross-tile prefetch under the epilogue)
                                        (4096, 4352, 256, "res"), (4352, 4096, 128, "swiglu"),
-                                       (4352, 4096, 192, "gelu")])
+                                       (4352, 4096, 192, "gelu"),
+                                       # the encoders' small-K projections (config 2 bge-base K = 768, bge-large
+                                       # K = 1024): qkv / o / FFN1+GELU / FFN2 over several persistent rounds
+                                       (4352, 2304, 768, "bias"), (4352, 768, 768, "bias"),
+                                       (4352, 3072, 768, "gelu"), (4352, 768, 3072, "bias"),
+                                       (2100, 1024, 1024, "bias")])
 def test_gemm4w(gpu, M, N, K, epi, bn, var, monkeypatch):
     """4-wave interleaved MFMA GEMM (AGPR accumulators, in-place inline-asm MFMA) vs an fp32 matmul for every
     epilogue: ragged M / N tails, one / two / many K tiles (the peeled last iterations), both tile widths,
