@@ -11,6 +11,8 @@ namespace py = pybind11;
 using lwc::BlockManager;
 
 namespace lwc {
+void bind_json(py::module_& m);  // json_encode.cpp
+
 // Python face of the consensus core (kept out of consensus_core.cpp so the core also builds without
 // Python, e.g. the sanitizer self-test csrc/tests/runtime_selftest.cpp).
 void bind_consensus_core(py::module_& m) {
@@ -120,6 +122,7 @@ py::array_t<int32_t> slots_range(const BlockManager& bm, int64_t seq, int64_t st
 }  // namespace
 
 PYBIND11_MODULE(_runtime, m) {
+  lwc::bind_json(m);
   m.doc() = "llm_weighted_consensus_amd host runtime: paged-KV block manager and consensus core";
 
   py::class_<BlockManager>(m, "BlockManager")

@@ -136,7 +136,7 @@ class Wire(BaseModel):
         return f(self)
 
     def to_json(self) -> str:
-        return sjson.dumps(self.to_obj())
+        return sjson.dumps(self)
 
     def clone(self):
         """Deep copy.  Field-wise construction without validation — pydantic's generic deep copy
@@ -169,6 +169,21 @@ class Wire(BaseModel):
         _set(new, "__pydantic_extra__", None)
         _set(new, "__pydantic_private__", None)
         return new
+
+
+def _native_plan(cls):
+    """The native JSON encoder's view of a type (csrc/runtime/json_encode.cpp): a Wire class whose to_obj
+    is the generated field walk -> ((name, key, keep_none), ...); one with its own to_obj or flattened
+    fields -> None (the encoder writes its to_obj()); anything else -> False."""
+    if not (isinstance(cls, type) and issubclass(cls, Wire)):
+        return False
+    cur = cls.to_obj
+    if not (cur is Wire.to_obj or getattr(cur, "_lwc_generated", False)) or cls.__flatten__:
+        return None
+    return tuple((name, key, bool(keep)) for name, key, keep, _flat in _plan(cls))
+
+
+sjson.PLAN_OF = _native_plan
 
 
 # --- merge helpers (reference chat/completions/response.rs:812-872) -------------------------------

@@ -125,12 +125,37 @@ def _fix_float(m: "re.Match") -> str:
     return ryu_f64(float(t))
 
 
+try:  # the native encoder (csrc/runtime/json_encode.cpp): one C++ walk, ryu floats, no rewrite pass
+    from .._runtime import json_dumps as _native_dumps  # type: ignore
+except Exception:  # pragma: no cover - runtime not built
+    _native_dumps = None
+# schema/base.py installs the wire types' field plans here: the native encoder then writes Wire objects
+# straight from their fields (no to_obj dict tree)
+PLAN_OF = None
+
+
+def _maybe_exp(s: str) -> bool:
+    """Whether ``s`` may hold a number in exponent form: some "e-" / "e+" between two digits (str.find runs
+    in C; ids such as "fake-..." contain "e-" without digits around it)."""
+    for pat in ("e-", "e+"):
+        i = s.find(pat)
+        while i != -1:
+            if 0 < i and s[i - 1].isdigit() and i + 2 < len(s) and s[i + 2].isdigit():
+                return True
+            i = s.find(pat, i + 2)
+    return False
+
+
 def dumps(v: Any) -> str:
-    """Compact serde_json text (serde_json::to_string).  The C encoder's output equals serde_json's except for
-    floats in exponent form (Python ``1e-05``, ryu ``1e-5``) and non-finite floats (serde_json: null); those
-    are rewritten in one C-regex pass that skips string literals (logprobs of confident tokens are often in
-    exponent form, so this is the common case, not a fallback).  Values the C encoder refuses take the exact
-    Python encoder."""
+    """Compact serde_json text (serde_json::to_string).  The native encoder (C++, _runtime) writes it
+    directly.  Without it: Python's C encoder, whose output equals serde_json's except for floats in exponent
+    form (Python ``1e-05``, ryu ``1e-5``) and non-finite floats (serde_json: null); those are rewritten in one
+    C-regex pass that skips string literals.  Values neither C encoder takes use the exact Python encoder."""
+    if _native_dumps is not None and (PLAN_OF is not None or isinstance(v, (dict, list))):
+        try:
+            return _native_dumps(v, PLAN_OF)
+        except (TypeError, ValueError, UnicodeError):
+            pass
     s = None
     p = _plain(v)
     if isinstance(p, (dict, list)):  # (a bare scalar: the exact encoder)
@@ -139,7 +164,7 @@ def dumps(v: Any) -> str:
         except (TypeError, ValueError):
             s = None
     if s is not None:
-        if "e-" not in s and "e+" not in s and "NaN" not in s and "Infinity" not in s:
+        if not _maybe_exp(s) and "NaN" not in s and "Infinity" not in s:
             return s  # (Python writes every exponent with a sign): nothing anywhere to rewrite
         return _FIX_FLOATS.sub(_fix_float, s) if _NEEDS_RYU.search(s) else s
     out: list = []

@@ -1,4 +1,4 @@
-"""The serde-compatible JSON text: the C-encoder fast path of ``utils.json.dumps`` equals the exact
+"""The serde-compatible JSON text: the native (C++) encoder and the C-encoder fallback of ``utils.json.dumps`` equal the exact
 (pure-Python, ryu float) encoder on arbitrary nested values, including floats whose Python repr uses an
 exponent, non-finite floats and strings that merely look like numbers; Wire clone / to_obj keep the
 wire shape and never alias the source."""
@@ -103,3 +103,64 @@ def test_generated_to_obj_matches_the_field_walk():
         extra_note: str = "n"
     assert Extended(content="c").to_obj() == dict(_loop_to_obj(Extended(content="c")), extra_note="n")
     assert isinstance(Extended(content="c"), Wire) and "extra_note" not in C.Delta(content="c").to_obj()
+
+
+def test_native_float_text_equals_ryu_layout():
+    """csrc/runtime/json_encode.cpp formats f64 with std::to_chars' shortest digits in ryu's layout: the
+    same text as the Python ryu_f64 on random bit patterns, the layout's boundaries and the specials."""
+    import random
+    import struct
+
+    from llm_weighted_consensus_amd import _runtime as RT
+
+    rng = random.Random(7)
+    xs = [struct.unpack("<d", struct.pack("<Q", rng.getrandbits(64)))[0] for _ in range(20000)]
+    xs += [rng.uniform(-1, 1) * 10.0 ** rng.randint(-30, 30) for _ in range(20000)]
+    xs += [1e-5, 1e-4, 9.999e-5, 1e15, 1e16, 1e17, 123456789012345680.0, 0.1, 5e-324, 1.7976931348623157e308,
+           -0.0, 0.0, 1.0, 100.0, 0.3, 2.5e-7, math.inf, -math.inf, math.nan]
+    for x in xs:
+        assert RT.json_f64(x) == J.ryu_f64(x), repr(x)
+
+
+@settings(max_examples=300, deadline=None)
+@given(values)
+def test_python_fallback_equals_exact_encoder(v):
+    """Without the native encoder: the C json encoder + exponent rewrite path."""
+    native, J._native_dumps = J._native_dumps, None
+    try:
+        assert J.dumps(v) == _exact(v)
+    finally:
+        J._native_dumps = native
+
+
+def test_native_encoder_refuses_unknown_types_and_falls_back():
+    class Obj:
+        def to_obj(self):
+            return {"k": [1, 2.5e-7]}
+
+    assert J.dumps({"a": Obj()}) == '{"a":{"k":[1,2.5e-7]}}'
+    assert J.dumps({"s": "\u0000\u001f\u007f é \"q\" \\ \t"}) == _exact({"s": "\u0000\u001f\u007f é \"q\" \\ \t"})
+    assert J.dumps([10 ** 30, -10 ** 30, True, None]) == "[1000000000000000000000000000000,-1000000000000000000000000000000,true,null]"
+
+
+def test_native_wire_walk_equals_to_obj_text():
+    """The native encoder writes Wire objects from their field plans (no to_obj dict tree): the text equals
+    dumps(to_obj()) for generated-plan classes, classes with their own to_obj (score choices), instances
+    carrying extra fields, aliases and kept Nones."""
+    from llm_weighted_consensus_amd.schema import score as S
+
+    lp = C.Logprobs(content=[C.Logprob(token="a\\n", bytes=[97, 10], logprob=-1e-7,
+                                       top_logprobs=[C.TopLogprob(token="b", bytes=None, logprob=-1.5e-5)])])
+    chunk = C.ChatCompletionChunk(id="x", created=1, model="m", choices=[
+        C.StreamChoice(delta=C.Delta(content="hi", role="assistant"), index=0, logprobs=lp, finish_reason="stop")])
+    sc = S.ScoreStreamChoice(delta=S.ScoreDelta(content="k"), index=2, weight=1.5, model="v", model_index=0)
+    extra = C.Delta.model_validate({"content": "c"})
+    object.__setattr__(extra, "__pydantic_extra__", {"note": 1e-9})
+    for obj in (chunk, sc, lp, extra, [chunk, {"k": sc}]):
+        want = J.dumps(_obj(obj))
+        assert J.dumps(obj) == want == _exact(_obj(obj))
+
+
+def _obj(v):
+    from llm_weighted_consensus_amd.schema.base import to_obj
+    return to_obj(v)
