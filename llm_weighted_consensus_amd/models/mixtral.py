@@ -37,9 +37,9 @@ from dataclasses import dataclass
 from typing import Optional
 
 import torch
-import torch.nn.functional as F
 
 from .. import ops
+from ..ops import gemm_plan
 from .config import DecoderConfig
 from .llama import LlamaModel
 
@@ -93,6 +93,14 @@ class MixtralModel(LlamaModel):
 
             self.cfg = replace(cfg, heads=cfg.heads // tp_size, kv_heads=cfg.kv_heads // tp_size)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True) -> None:
+        """The bf16 vocabulary projection is the MoE decoder's one dense bf16 GEMM (attention projections and
+        experts are fp8, planned per shape in ops.linear_fp8_q): time the library against the hand-written
+        cores at decode batch M before the bucket's graph is captured (ops/gemm_plan.py)."""
+        if lm_head and self.g8_ws is not None and not isinstance(self.lm_head, ops.Fp8Weight):
+            x = torch.randn(M, self.cfg.hidden, device=self.device).to(self.dtype)
+            gemm_plan.tune(x, self.lm_head, ws=self.g8_ws, bucket=bucket)
 
     # ------------------------------------------------------------------ weights
     def _shard_layer(self, attn_norm, wq, wk, wv, wo, mlp_norm, router, w1, w3, w2) -> MoELayerWeights:
