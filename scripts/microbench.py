@@ -511,6 +511,38 @@ def encoder_gemms(dev):
         del x, w
 
 
+def serve_shapes(dev):
+    """Llama-3-8B projections at the serving path's mixed chunked-prefill row counts (2048 prompt rows + the
+    decode rows): every backend the planner times, median of 5 interleaved rounds (SERVE_M overrides)."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    d, Fd, QKV = 4096, 14336, 6144
+    r = lambda *s: ((torch.rand(*s, device=dev) * 2 - 1) / s[-1] ** 0.5).to(torch.bfloat16)  # noqa: E731
+    wqkv, wo, wgu, wd = r(QKV, d), r(d, d), ops.swiglu_interleave(r(2 * Fd, d)), r(d, Fd)
+    for M in [int(m) for m in os.environ.get("SERVE_M", "2048,2304,2560").split(",")]:
+        x, xa, xf = r(M, d) * 8, r(M, d) * 8, r(M, Fd) * 8
+        acc = torch.zeros(M, d, device=dev, dtype=torch.bfloat16)
+        runs = {
+            "qkv blas": lambda: F.linear(x, wqkv), "qkv g4": lambda: ops.gemm4w(x, wqkv),
+            "qkv g4n192": lambda: ops.gemm4w(x, wqkv, bn=192), "qkv g8": lambda: ops.gemm8p(x, wqkv),
+            "o blas": lambda: acc.addmm_(xa, wo.t()), "o g4": lambda: ops.gemm4w(xa, wo, residual=acc, out=acc),
+            "o g8": lambda: ops.gemm8p(xa, wo, residual=acc, out=acc),
+            "gu blas+silu": lambda: ops.silu_mul(F.linear(x, wgu), block=32),
+            "gu g4": lambda: ops.gemm4w(x, wgu, swiglu=True), "gu g4p": lambda: ops.gemm4w(x, wgu, swiglu=True, var=64),
+            "gu g8": lambda: ops.gemm8p(x, wgu, swiglu=True),
+            "down blas": lambda: acc.addmm_(xf, wd.t()), "down g4": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc),
+            "down g8": lambda: ops.gemm8p(xf, wd, residual=acc, out=acc),
+        }
+        res = {k: [] for k in runs}
+        for _ in range(5):
+            for k, fn in runs.items():
+                res[k].append(timeit(fn, iters=10, warm=2))
+        for k, t in res.items():
+            print(f"serve M={M} {k}: {sorted(t)[2]:8.1f} us", flush=True)
+
+
 def route_ab(dev):
     """Config-5 MoE plumbing at the decode batch (T = 4096 tokens, Mixtral d = 4096, 8 experts, top-2):
     the router projection + route (unfused: F.linear then moe_route) vs the fused moe_router kernel, and
@@ -618,6 +650,8 @@ def main():
         route_ab(dev)
     if "enc" in a.what:
         encoder_gemms(dev)
+    if "serve" in a.what:
+        serve_shapes(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:
