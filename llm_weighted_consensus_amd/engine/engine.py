@@ -765,20 +765,25 @@ class LLMEngine:
         return ch
 
     def _tune_mixed(self) -> None:
-        """Once, before the first mixed step (opt-in, ``LWC_GEMM_BUCKETS=1``): the GEMM backend per row-count
-        bucket of the mixed steps' projections (decode rows + up to ``chunked_prefill`` chunk rows), timed like
-        the decode buckets'.  Off by default: on the serving load (scripts/gpu_serve_bk.sh, interleaved runs)
-        it measured 28.0-28.9 vs 28.5-31.5 requests/s without — a bucket's choice is timed at its top row
-        count, and hipBLASLt's stream-K is the safer pick across the row counts below it."""
+        """Once, before the first mixed step: the GEMM backend per row-count bucket of the mixed steps'
+        projections (decode rows + up to ``chunked_prefill`` chunk rows), timed like the decode buckets'.
+        ``LWC_GEMM_BUCKETS``: ``swiglu`` (default) tunes the gate|up + SwiGLU projection only — the
+        hand-written cores win it at every serving row count (profiles/serve_load.md, round 5: 4-7 %, and no
+        separate silu_mul pass); ``1`` every projection (measured 28.0-28.9 vs 28.5-31.5 requests/s without in
+        round 3: a bucket's choice is timed at its top row count, and for the few-tile o / down shapes
+        hipBLASLt's stream-K is the safer pick across the row counts below it); ``0`` none."""
         self._mixed_tuned = True
-        if (not hasattr(self.model, "tune_gemms") or self.device.type != "cuda"
-                or os.environ.get("LWC_GEMM_BUCKETS", "0") != "1"):
+        mode = os.environ.get("LWC_GEMM_BUCKETS", "swiglu")
+        if not hasattr(self.model, "tune_gemms") or self.device.type != "cuda" or mode not in ("1", "swiglu"):
             return
         top = self.chunked_prefill + self.max_batch
         buckets = [m for m in (256, 512, 1024, 1536, 2048, 2560, 3072, 4096, 6144, 8192) if m < top] + [top]
         with span("tune_gemms"):
             for m in buckets:
-                self.model.tune_gemms(m, bucket=True, lm_head=False)
+                if mode == "1":
+                    self.model.tune_gemms(m, bucket=True, lm_head=False)
+                else:
+                    self.model.tune_gemms(m, bucket=True, lm_head=False, only=("swiglu",))
 
     def _chunk_items(self, budget: int):
         """This step's prompt chunks: (group, a, e) = prompt tokens [a, e), at most ``budget`` tokens, prompts

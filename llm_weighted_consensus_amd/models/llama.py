@@ -380,14 +380,20 @@ class LlamaModel:
     def comm_poll(self) -> None:
         """Tensor-parallel subclasses raise here once a failed collective is visible on the host."""
 
-    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True) -> None:
+    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True, only=None) -> None:
         """Pick the GEMM backend of every decode projection at batch M by timing both (before the
         bucket's hipGraph is captured; see ops/gemm_plan.py).  ``bucket``: M is a row-count bucket of the
         mixed chunked-prefill steps (their M varies step to step); ``lm_head``: tune the vocabulary
-        projection too (mixed steps only project the decode rows and completed prompts' last tokens)."""
+        projection too (mixed steps only project the decode rows and completed prompts' last tokens);
+        ``only``: the epilogues to tune (e.g. ("swiglu",): the gate|up projection alone)."""
         if self.g8_ws is None or not isinstance(self.layers[0], LayerWeights) or self.fp8_dense:
             return
         cfg, L = self.cfg, self.layers[0]
+        if only is not None:
+            if "swiglu" in only:
+                x = torch.randn(M, cfg.hidden, device=self.device).to(self.dtype)
+                gemm_plan.tune(x, L.w_gate_up, "swiglu", L.gu_block, ws=self.g8_ws, bucket=bucket)
+            return
         x = torch.randn(M, cfg.hidden, device=self.device).to(self.dtype)
         xa = torch.randn(M, cfg.heads * cfg.head_dim, device=self.device).to(self.dtype)
         xf = torch.randn(M, cfg.ffn, device=self.device).to(self.dtype)

@@ -94,11 +94,11 @@ class MixtralModel(LlamaModel):
             self.cfg = replace(cfg, heads=cfg.heads // tp_size, kv_heads=cfg.kv_heads // tp_size)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
-    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True) -> None:
+    def tune_gemms(self, M: int, bucket: bool = False, lm_head: bool = True, only=None) -> None:
         """The bf16 vocabulary projection is the MoE decoder's one dense bf16 GEMM (attention projections and
         experts are fp8, planned per shape in ops.linear_fp8_q): time the library against the hand-written
         cores at decode batch M before the bucket's graph is captured (ops/gemm_plan.py)."""
-        if lm_head and self.g8_ws is not None and not isinstance(self.lm_head, ops.Fp8Weight):
+        if lm_head and only is None and self.g8_ws is not None and not isinstance(self.lm_head, ops.Fp8Weight):
             x = torch.randn(M, self.cfg.hidden, device=self.device).to(self.dtype)
             gemm_plan.tune(x, self.lm_head, ws=self.g8_ws, bucket=bucket)
 

@@ -147,6 +147,11 @@ def main():
     from llm_weighted_consensus_amd.utils.tracing import STATS
 
     out["phases"] = {k: [v[0], round(v[1], 3)] for k, v in STATS.snapshot()["phases"].items()}
+    from llm_weighted_consensus_amd.ops import gemm_plan
+
+    # the planner's per-shape choices (decode buckets and mixed-step row buckets) with their timings
+    out["gemm_plan"] = {k: {b: (round(t, 1) if isinstance(t, float) else t) for b, t in v.items()}
+                        for k, v in gemm_plan.table().items()}
     out["engine_steps"] = stats["steps"]
     tb = getattr(state.score, "tally_batcher", None)
     if tb is not None:  # K10b: tallies batched into GPU launches (LWC_GPU_TALLY)
