@@ -551,6 +551,26 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
     // ---- epilogue: per wave 128 rows x CW bf16 columns through LDS, then 16 B stores
     bf16_t* ot = reinterpret_cast<bf16_t*>(smem) + wid * 128 * CW;
+    constexpr int CPR_ = CW / 8;
+    constexpr int kIt_ = 128 * CPR_ / 64;                                   // residual chunks per lane
+    constexpr int kGrp_ = kIt_ % 16 == 0 ? 16 : (kIt_ % 12 == 0 ? 12 : 8);  // whole groups only
+    // residual: the first group's loads go out before the accumulators are staged (into registers the main
+    // loop's fragments held), so their HBM round trip overlaps the staging instead of following it
+    uint4v rv0[EPI == EPI_RESIDUAL ? kGrp_ : 1];
+    const int erow0 = __builtin_amdgcn_readfirstlane(m0 + wm * 128);  // uniform: buffer resources in SGPRs
+    const int encol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
+    // (a valid pointer and an empty range for the epilogues without a residual operand)
+    const __amdgpu_buffer_rsrc_t rRes =
+        EPI == EPI_RESIDUAL ? uniform_rsrc(p.R + (size_t)erow0 * p.ldc, max(0, min(p.M - erow0, 128)) * p.ldc * 2)
+                            : uniform_rsrc(p.A, 0);
+    if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+      for (int u = 0; u < kGrp_; ++u) {
+        const int c = lane + 64 * u;
+        const int row = c / CPR_, gn = encol0 + (c % CPR_) * 8;
+        rv0[u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rRes, (row * p.ldc + gn) * 2, 0, 0));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float4v t[NT];
@@ -609,20 +629,24 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       // without a request; columns past N are never stored), kGrp of them in flight per lane before the
       // first add: loaded inside the store's bounds branch, every chunk waited its own HBM round trip
       // (vmcnt(0) per 16 B, the epilogue's whole latency).
-      const int row0 = __builtin_amdgcn_readfirstlane(m0 + wm * 128);  // uniform: buffer resources in SGPRs, no waterfall loops
-      const int rows_here = max(0, min(p.M - row0, 128));
-      const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.R + (size_t)row0 * p.ldc, rows_here * p.ldc * 2);
-      constexpr int kIt = 128 * CPR / 64;                         // chunks per lane: 32 (bn 256), 24 (bn 192)
-      constexpr int kGrp = kIt % 16 == 0 ? 16 : (kIt % 12 == 0 ? 12 : 8);  // whole groups only
+      const int row0 = erow0;
+      const __amdgpu_buffer_rsrc_t rR = rRes;
+      constexpr int kIt = kIt_;                                   // chunks per lane: 32 (bn 256), 24 (bn 192)
+      constexpr int kGrp = kGrp_;
       static_assert(kIt % kGrp == 0, "residual epilogue groups must tile the wave's chunks");
 #pragma unroll 1
       for (int g0 = 0; g0 < kIt; g0 += kGrp) {
         uint4v rv[kGrp];
+        if (g0 == 0) {
 #pragma unroll
-        for (int u = 0; u < kGrp; ++u) {
-          const int c = lane + 64 * (g0 + u);
-          const int row = c / CPR, gn = ncol0 + (c % CPR) * 8;
-          rv[u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
+          for (int u = 0; u < kGrp; ++u) rv[u] = rv0[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < kGrp; ++u) {
+            const int c = lane + 64 * (g0 + u);
+            const int row = c / CPR, gn = ncol0 + (c % CPR) * 8;
+            rv[u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
+          }
         }
 #pragma unroll
         for (int u = 0; u < kGrp; ++u) {
