@@ -42,15 +42,15 @@ def _assert_same_greedy(got, want, tol=2e-2):
     """Greedy continuations of two runs agree token for token, or up to a NEAR TIE: at the first
     differing step both runs' tokens are in the other's top-3 with log-probabilities within ``tol`` (decode
     rows that share a forward with prompt-chunk rows run other GEMM shapes: last-bit differences can flip
-    an exact tie of the random-init model, never a clear winner).  The first token (prompt logits) and the
-    log-probabilities up to the divergence must match within ``tol``."""
+    an exact tie of the random-init model, never a clear winner — the prompt logits too: a mixed step's
+    gate|up runs on the row-bucket planner's backend, so a first token can flip between two exactly tied
+    logits).  The log-probabilities up to the divergence must match within ``tol``."""
     for tg, tw in zip(got, want):
         for a, b in zip(tg, tw):
             assert len(a) == len(b)
             for step, ((ta, la, topa), (tb, lb, topb)) in enumerate(zip(a, b)):
                 assert abs(la - lb) < tol, (step, la, lb)
                 if ta != tb:
-                    assert step > 0, "first tokens differ"
                     assert tb in topa and abs(topa[tb] - la) < tol, (step, ta, tb, topa)
                     assert ta in topb and abs(topb[ta] - lb) < tol, (step, ta, tb, topb)
                     break
