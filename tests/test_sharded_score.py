@@ -386,3 +386,26 @@ def test_restarted_follower_rejoins_and_serves(tmp_path):
     assert g["t_rejoin"] < 60
     assert g["later_errors"] == [0, 0, 0] and all(n == len(KILL_LLMS) for n in g["later_n"])
     assert got[2][0] == "rejoined" and got[2][1] >= 3  # the replacement ran voters of every later request
+
+
+def test_timed_out_follower_is_told_to_cancel(monkeypatch):
+    """a live follower that never answers its share (slow, wedged) is given up after
+    LWC_SHARD_WAIT_S — its voters become error choices and the request completes — and the leader sends it
+    ("cancel", seq) so its voters stop using its GPU."""
+    from llm_weighted_consensus_amd.score.sharded import ShardedScoreClient
+
+    monkeypatch.setenv("LWC_SHARD_WAIT_S", "0.3")
+    link = _FakeLink()  # rank 1 live, never replies
+    client = ShardedScoreClient(FakeChatClient(_policy), link, world=2, rng_seed=1)
+
+    async def main():
+        return await client.create_unary(None, _request("mixed"))
+
+    out = asyncio.run(main())
+    scores = [m for m in link.sent if m[1][0] == "score"]
+    assert scores and all(r == 1 for r, _ in scores)
+    seq = scores[0][1][1]
+    assert (1, ("cancel", seq)) in link.sent
+    errs = [c for c in out.choices if c.error is not None]
+    assert errs and any("timed out" in str(c.error) for c in errs)
+    assert not client.hub.shares  # the share is closed
