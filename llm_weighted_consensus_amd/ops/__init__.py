@@ -634,6 +634,24 @@ def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Option
     return out
 
 
+def gemm4w8_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Optional[torch.Tensor] = None):
+    """Dense fp8 GEMM on the 4-wave schedule (csrc/kernels/gemm4w8.hip: one wave per SIMD, 128 x 128 wave tiles,
+    the LDS traffic of gemm8g's 2-waves-per-SIMD layout halved): (xq [M, K] e4m3 . w.q^T) * xs[row] * w.s[col]
+    -> bf16 [M, N].  Row blocks of < 2 GiB of A per launch (32-bit buffer range)."""
+    M = xq.shape[0]
+    N, K = w.q.shape
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+    if M == 0:
+        return out
+    s, ws = xs.reshape(-1).contiguous(), w.s.reshape(-1).contiguous()
+    step = max(256, (G8G_SPAN - 1) // xq.stride(0) // 256 * 256)
+    for r0 in range(0, M, step):
+        r1 = min(M, r0 + step)
+        kernels().gemm4w8(xq[r0:r1], w.q, out[r0:r1], s[r0:r1], ws)
+    return out
+
+
 def _fp8_blas(xq, xs, w):
     return torch._scaled_mm(xq, w.q.t(), scale_a=xs.view(-1, 1), scale_b=w.s, out_dtype=torch.bfloat16)
 

@@ -543,6 +543,33 @@ def serve_shapes(dev):
             print(f"serve M={M} {k}: {sorted(t)[2]:8.1f} us", flush=True)
 
 
+def g48_ab(dev):
+    """Dense fp8: the 4-wave gemm4w8 vs gemm8g (dense mode) vs hipBLASLt's row-scaled fp8 GEMM at config 5's
+    shapes (median of 5 interleaved rounds; G48_SHAPES picks a subset)."""
+    from llm_weighted_consensus_amd import ops
+
+    shapes = [(4096, 6144, 4096), (4096, 4096, 4096), (4096, 4096, 14336), (16384, 6144, 4096), (8192, 4096, 14336),
+              (65536, 6144, 4096)]
+    only = os.environ.get("G48_SHAPES")
+    if only:
+        shapes = [shapes[int(i)] for i in only.split(",")]
+    for M, N, K in shapes:
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        xq, xs = ops.quant_fp8_rows(x)
+        del x
+        w = ops.Fp8Weight((torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16))
+        runs = {"blas": lambda: ops._fp8_blas(xq, xs, w), "g8g": lambda: ops.gemm8g_dense(xq, xs, w),
+                "g4w8": lambda: ops.gemm4w8_dense(xq, xs, w)}
+        res = {k: [] for k in runs}
+        for _ in range(5):
+            for k, fn in runs.items():
+                res[k].append(timeit(fn, iters=5, warm=1))
+        fl = 2 * M * N * K / 1e12
+        line = "  ".join(f"{k} {sorted(t)[2]:8.1f} us ({fl / sorted(t)[2] * 1e6:5.0f})" for k, t in res.items())
+        print(f"g48 {M}x{N}x{K}: {line}", flush=True)
+        del xq, xs, w
+
+
 def route_ab(dev):
     """Config-5 MoE plumbing at the decode batch (T = 4096 tokens, Mixtral d = 4096, 8 experts, top-2):
     the router projection + route (unfused: F.linear then moe_route) vs the fused moe_router kernel, and
@@ -652,6 +679,8 @@ def main():
         encoder_gemms(dev)
     if "serve" in a.what:
         serve_shapes(dev)
+    if "g48" in a.what:
+        g48_ab(dev)
     if "g8ab" in a.what:
         gemm8p_ab(dev)
     if "g8" in a.what:

@@ -1389,3 +1389,25 @@ def test_knn_topk(gpu, n, d, k):
     if n > 10 and k > 1:
         r = rows.tolist()
         assert r.index(best) < r.index(n - 3)  # ties: lower row first
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 520, 256), (4096 + 37, 6144, 4096), (513, 1024, 128), (257, 768, 384),
+                                   (1000, 4096, 1280), (64, 256, 512)])
+def test_gemm4w8_dense_matches_fp32(gpu, M, N, K):
+    """The 4-wave fp8 GEMM (gemm4w8.hip: 16x16x128 e4m3 MFMAs, A fragments double-buffered by K tile, W
+    fragments by column half, clamped last-tile DMA) vs fp32 of the dequantised operands: ragged M / N tiles,
+    one K tile, odd and even K-tile counts (the loop's two parities), and a row stride larger than K."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(41)
+    x = torch.randn(M, K + 64, device=gpu)[:, :K]
+    xq, xs = ops.quant_fp8_rows(x.to(torch.bfloat16).contiguous())
+    xq_strided = torch.empty(M, K + 128, dtype=torch.uint8, device=gpu)
+    xq_strided[:, :K] = xq.view(torch.uint8)
+    xq2 = xq_strided[:, :K].view(torch.float8_e4m3fn)
+    w = ops.Fp8Weight((torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16))
+    ref = (xq.float() * xs.view(-1, 1)) @ (w.q.float() * w.s.view(-1, 1)).t()
+    for a in (xq, xq2):
+        out = ops.gemm4w8_dense(a, xs, w)
+        err = (out.float() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
