@@ -427,7 +427,17 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
             raise ValueError("gemm4w: gelu needs a bias")
         epi = 2 if swiglu else (1 if residual is not None else 0)
     if chain is None:
-        kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var))
+        # the kernel addresses A through one 32-bit buffer range: row blocks of < 2 GiB of A, one launch each
+        # (the encoders' FFN2 input at config 2's 0.5 M tokens is 3 GiB)
+        M = A.shape[0]
+        step = max(256, ((1 << 31) - 1) // max(1, A.stride(0) * 2) // 256 * 256)
+        if M <= step:
+            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var))
+        else:
+            for r0 in range(0, M, step):
+                r1 = min(M, r0 + step)
+                res = residual[r0:r1] if epi == 1 else residual
+                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var))
     elif epi == 1:
         kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var))
         chain.P = (N + 255) // 256

@@ -127,24 +127,27 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
     epi = "bias_gelu" if gelu else "bias"
     key = (_m_bucket(M), N, K, epi)
     c = MODE if MODE in ("blas", "g8", "g4", "g4p") else _CHOICE.get(key)
-    # the hand-written cores address A through 32-bit buffer offsets: operands of 2 GiB or more take the
-    # library path
-    ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda and M * x.stride(0) * 2 < (1 << 31)
-    runs = {"g8": lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws),
-            "g4": lambda: gemm4w(x, w, bias=b, gelu=gelu),
+    # gemm8p addresses A through one 32-bit buffer range (operands of 2 GiB or more take the other backends);
+    # gemm4w runs such an A as row blocks
+    ok = _g8_ok(N, K, epi) and x.stride(1) == 1 and x.is_cuda
+    small_a = M * x.stride(0) * 2 < (1 << 31)
+    runs = {"g4": lambda: gemm4w(x, w, bias=b, gelu=gelu),
             "g4p": lambda: gemm4w(x, w, bias=b, gelu=gelu, var=64),
             "blas": ((lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if gelu
                      else (lambda: F.linear(x, w, b)))}
+    if small_a:
+        runs["g8"] = lambda: gemm8p(x, w, bias=b, gelu=gelu, ws=ws)
     if c is None:
         if not ok or torch.cuda.is_current_stream_capturing():
             c = "blas"
         else:
             t = {name: _time(fn, iters=2, rounds=3) for name, fn in runs.items()}
             TIMINGS[key] = t
-            own = min(("g8", "g4", "g4p"), key=lambda n: t[n])
+            own = min((n for n in ("g8", "g4", "g4p") if n in t), key=lambda n: t[n])
             c = own if t[own] <= t["blas"] * (1 + OWN_MARGIN) else "blas"
         _CHOICE[key] = c
-    return runs[c]() if c != "blas" and ok else runs["blas"]()
+    # (a choice made for the token bucket at a smaller A may name gemm8p, which a 2 GiB A cannot take)
+    return runs[c]() if c != "blas" and ok and c in runs else runs["blas"]()
 
 
 def _time(fn, iters: int = 5, rounds: int = 3) -> float:

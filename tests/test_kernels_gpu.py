@@ -1411,3 +1411,26 @@ def test_gemm4w8_dense_matches_fp32(gpu, M, N, K):
         out = ops.gemm4w8_dense(a, xs, w)
         err = (out.float() - ref).abs().max().item()
         assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
+
+
+def test_gemm4w_row_blocks_past_2gib(gpu):
+    """gemm4w addresses A through one 32-bit buffer range; ops.gemm4w runs an A of 2 GiB or more (the encoders'
+    FFN2 input at config 2's 0.5 M tokens is 3 GiB) as row blocks: rows on both sides of the block boundary and
+    the ragged last rows match fp32, for the bias epilogue and the in-place residual one."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(43)
+    K, N = 8192, 256
+    step = ((1 << 31) - 1) // (K * 2) // 256 * 256
+    M = step + 300
+    A = (torch.rand(M, K, device=gpu) - 0.5).to(torch.bfloat16)
+    W = ((torch.rand(N, K, device=gpu) - 0.5) / K ** 0.5).to(torch.bfloat16)
+    b = (torch.rand(N, device=gpu) - 0.5).to(torch.bfloat16)
+    out = ops.gemm4w(A, W, bias=b, var=64)
+    R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    R0 = R.clone()
+    ops.gemm4w(A, W, residual=R, out=R)
+    for r0, r1 in ((0, 256), (step - 128, step + 128), (M - 300, M)):
+        ref = A[r0:r1].float() @ W.float().t()
+        _close(out[r0:r1], ref + b.float(), 3e-2, 1e-2)
+        _close(R[r0:r1], ref + R0[r0:r1].float(), 3e-2, 1e-2)
