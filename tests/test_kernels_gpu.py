@@ -984,7 +984,9 @@ def _check_permutation(gpu, ids, row_off, src, inv, T, E, k):
 
 
 @pytest.mark.parametrize("T,E,k,d,ld", [(1, 8, 2, 4096, 4096), (77, 8, 2, 4096, 4096), (4096, 8, 2, 4096, 4096),
-                                        (300, 6, 2, 512, 520), (129, 16, 4, 1024, 1024), (50, 8, 3, 256, 256)])
+                                        (300, 6, 2, 512, 520), (129, 16, 4, 1024, 1024), (50, 8, 3, 256, 256),
+                                        # > 8192 routed rows: the permutation's re-reading path (prefill batches)
+                                        (16500, 8, 2, 512, 512)])
 def test_moe_router_matches_fp32(gpu, T, E, k, d, ld):
     """The router GEMV fused with the top-k (K11a moe_router: TPW tokens per wave, wave reduce-scatter of
     the E x TPW partial sums): logits within a bf16 rounding of the fp32 product (the kernel rounds them to
