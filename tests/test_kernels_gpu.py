@@ -901,9 +901,10 @@ def test_gemm8g_grouped_fp8_matches_reference(gpu, gather, monkeypatch):
     _close(out, classic, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("sizes", [[300, 0, 77, 520], [100, 200, 129, 128]])
 @pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("moe_gemm", ["g8", "classic"])
-def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch):
+def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, sizes, monkeypatch):
     """MoE gate|up with the SwiGLU fused (gemm8g's epilogue; the 128x128 kernel + the SwiGLU pass when it
     takes the batch): gate / up rows interleaved in blocks of 32 per expert, ragged groups, A-row gather,
     per-row / per-channel scales -> silu(A Wg^T) * (A Wu^T) [rows, F] vs an fp32 reference."""
@@ -912,7 +913,6 @@ def test_grouped_fp8_swiglu_matches_reference(gpu, gather, moe_gemm, monkeypatch
     monkeypatch.setattr(ops, "MOE_GEMM", moe_gemm)
     torch.manual_seed(13)
     G, F, K = 4, 320, 512
-    sizes = [300, 0, 77, 520]
     rows = sum(sizes)
     off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
     A = torch.randn(rows + 11, K, device=gpu)
@@ -1030,7 +1030,9 @@ def _mx_scale_map(mx: torch.Tensor, K: int) -> torch.Tensor:
     return torch.exp2(mx.float() - 127.0)[kt, :, blk].t()
 
 
-@pytest.mark.parametrize("sizes", [[300, 0, 77, 520], [1024, 1003, 990, 1079]])
+@pytest.mark.parametrize("sizes", [[300, 0, 77, 520], [1024, 1003, 990, 1079],
+                                   # ragged tails of 65..128 rows (the wave rows' 128-row boundary)
+                                   [100, 200, 129, 128]])
 def test_grouped_fp8_mx_a_matches_reference(gpu, sizes):
     """The down-projection side of the MX expert FFN: gemm8g with A's e8m0 block scales applied by the
     block-scaled MFMA (the scale tile DMA'd beside A, one scale byte per lane and row fragment via op_sel)
@@ -1059,8 +1061,9 @@ def test_grouped_fp8_mx_a_matches_reference(gpu, sizes):
             assert ((out[o[g]:o[g + 1]].float() - ref_).norm() / ref_.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("sizes", [[300, 0, 77, 520], [100, 200, 129, 128]])
 @pytest.mark.parametrize("gather", [False, True])
-def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather):
+def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather, sizes):
     """The gate|up side of the MX expert FFN: SwiGLU in gemm8g's epilogue, the activation written as e4m3
     with one e8m0 scale per (row, block of 32; one quad of lanes per block) vs fp32; then the
     whole middle (MX gate|up -> MX down) vs fp32 silu(gate) * up through the down projection."""
@@ -1068,7 +1071,6 @@ def test_grouped_fp8_swiglu_mx_matches_reference(gpu, gather):
 
     torch.manual_seed(19)
     G, F, K, D = 4, 512, 512, 256
-    sizes = [300, 0, 77, 520]
     rows = sum(sizes)
     off = torch.tensor([0] + list(np.cumsum(sizes)), dtype=torch.int32, device=gpu)
     A = torch.randn(rows + 11, K, device=gpu)
