@@ -101,6 +101,22 @@ LWC_DEVICE void mfma(float4v& d, const uint4v& a, const uint4v& b) {
 #define G4_BAR() __builtin_amdgcn_s_barrier()
 #define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 #define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// Diagnostic build only (scripts/probes/g4_stamps.cpp defines LWC_G4_STAMPS): wave 0 of every workgroup
+// records s_memrealtime at four points of each persistent round (and s_memtime at the first and last) into
+// g4_stamps[block][round][4] with vector stores; the product build has no stamp code at all.
+#ifdef LWC_G4_STAMPS
+__device__ unsigned long long* g4_stamps;
+#define G4_STAMP(round, k)                                                                  \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && (round) < 64) {                                                 \
+      unsigned long long* sp_ = g4_stamps + ((size_t)blockIdx.x * 64 + (round)) * 8 + 2 * (k); \
+      if ((k) == 0 || (k) == 3) sp_[0] = __builtin_amdgcn_s_memtime();                      \
+      sp_[1] = __builtin_amdgcn_s_memrealtime();                                            \
+    }                                                                                       \
+  } while (0)
+#else
+#define G4_STAMP(round, k) ((void)0)
+#endif
 
 // x * sigmoid(x) with v_rcp_f32 (1 ulp) instead of the IEEE division sequence (v_div_scale x2, v_div_fmas,
 // v_div_fixup around an rcp: ~9 VALU per element in an epilogue of 256 per lane); the result is rounded
@@ -156,6 +172,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     int tm, tn;
     tile_mn(p, tile, tm, tn);
     const int m0 = tm * 256, n0 = tn * G::BN;
+    G4_STAMP(round, 0);
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -229,6 +246,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       G4_VM(0);
     }
     G4_BAR();
+    G4_STAMP(round, 1);
     if constexpr (RS == 1) {
       // row tid's scale from its partials (the main loop's first barrier publishes it to the epilogues)
       const float* part = reinterpret_cast<const float*>(smem + RSOFF);
@@ -402,6 +420,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
       for (int jj = 0; jj < NT; ++jj) asm volatile("" : "+a"(acc[i][jj]));
     __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
+    G4_STAMP(round, 2);
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
     if constexpr (PAP) {
@@ -546,6 +565,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           }
         }
       }
+      G4_STAMP(round, 3);
       continue;  // no block barrier: the next tile's first wait + barrier orders everything
     }
 
@@ -701,6 +721,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         }
       }
     }
+    G4_STAMP(round, 3);
   }
 }
 

@@ -1,0 +1,142 @@
+// Where a gemm4w tile's time goes: a diagnostic build of csrc/kernels/gemm4w.hip with LWC_G4_STAMPS, whose
+// wave 0 of every workgroup records (s_memtime, s_memrealtime) at four points of each persistent round:
+//   S0 tile start, S1 first K tiles landed (prologue wait + barrier), S2 main loop + drain + block barrier
+//   done, S3 epilogue done.
+// Per shape: the call time (events, 20 back-to-back calls after ~1.5 s of warm-up launches on random
+// operands), the in-kernel clock (memtime / realtime x 100 MHz) and, per round, the median over workgroups of
+// prologue (S1 - S0), main loop (S2 - S1), epilogue (S3 - S2) and the hand-off to the next round (next S0 - S3).
+//
+// Build (CPU container): hipcc --offload-arch=gfx950 -O3 -std=c++17 -DLWC_G4_STAMPS -I csrc/kernels \
+//   scripts/probes/g4_stamps.cpp -o scripts/probes/g4_stamps
+// Run (GPU box): timeout -k 10 120 scripts/probes/g4_stamps
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#include "gemm4w.hip"
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return 1;                                                                \
+    }                                                                          \
+  } while (0)
+
+__global__ void fill_rand(uint16_t* x, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    const float f = ((h & 0xffffff) / 16777216.0f) * 2.f - 1.f;  // [-1, 1)
+    x[i] = (uint16_t)(__float_as_uint(f) >> 16);
+  }
+}
+
+struct Shape {
+  const char* name;
+  int M, N, K, epi, var;
+};
+
+static double med(std::vector<double> v) {
+  if (v.empty()) return 0.0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+int main() {
+  const Shape shapes[] = {
+      {"gate_up+swiglu 4096x28672x4096 VAR64", 4096, 28672, 4096, 2, 64},
+      {"gate_up+swiglu 4096x28672x4096 VAR32", 4096, 28672, 4096, 2, 32},
+      {"lm_head 4096x128256x4096 VAR64", 4096, 128256, 4096, 0, 64},
+      {"lm_head 4096x128256x4096 VAR32", 4096, 128256, 4096, 0, 32},
+      {"o+res 4096x4096x4096 VAR32", 4096, 4096, 4096, 1, 32},
+      {"down+res 4096x4096x14336 VAR32", 4096, 4096, 14336, 1, 32},
+  };
+  const int blocks = lwc::g4w::device_cus();
+  unsigned long long* dst = nullptr;
+  CK(hipMalloc(&dst, (size_t)blocks * 64 * 8 * sizeof(unsigned long long)));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(lwc::g4w::g4_stamps), &dst, sizeof(dst)));
+  for (const Shape& sh : shapes) {
+    uint16_t *A, *W, *C, *R = nullptr;
+    CK(hipMalloc(&A, (size_t)sh.M * sh.K * 2));
+    CK(hipMalloc(&W, (size_t)sh.N * sh.K * 2));
+    CK(hipMalloc(&C, (size_t)sh.M * sh.N * 2));
+    fill_rand<<<1024, 256>>>(A, (size_t)sh.M * sh.K, 1);
+    fill_rand<<<1024, 256>>>(W, (size_t)sh.N * sh.K, 2);
+    if (sh.epi == 1) {
+      CK(hipMalloc(&R, (size_t)sh.M * sh.N * 2));
+      fill_rand<<<1024, 256>>>(R, (size_t)sh.M * sh.N, 3);
+    }
+    CK(hipDeviceSynchronize());
+    auto call = [&]() {
+      return lwc_gemm4w(A, W, C, R, sh.M, sh.N, sh.K, sh.K, sh.epi == 2 ? sh.N / 2 : sh.N, sh.epi, 256, nullptr, 0, 0,
+                        1, 1e-5f, sh.var, 0);
+    };
+    if (call() != 0) {
+      fprintf(stderr, "%s: launch refused\n", sh.name);
+      return 1;
+    }
+    CK(hipDeviceSynchronize());
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 1.5) {
+      for (int i = 0; i < 10; ++i) call();
+      CK(hipDeviceSynchronize());
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < 20; ++i) call();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    // the last call's stamps
+    std::vector<unsigned long long> h((size_t)blocks * 64 * 8);
+    CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
+    const int tiles = ((sh.M + 255) / 256) * ((sh.N + 255) / 256);
+    const int rounds = (tiles + blocks - 1) / blocks;
+    auto at = [&](int b, int r, int k, int which) { return h[((size_t)b * 64 + r) * 8 + 2 * k + which]; };
+    std::vector<double> clk;
+    for (int b = 0; b < blocks; ++b) {
+      const int last = std::min(rounds, 64) - 1;
+      const double dc = (double)(at(b, last, 3, 0) - at(b, 0, 0, 0));
+      const double dt = (double)(at(b, last, 3, 1) - at(b, 0, 0, 1));
+      if (dt > 0 && at(b, last, 3, 1) >= at(b, 0, 0, 1)) clk.push_back(dc / dt * 100.0);  // MHz
+    }
+    printf("== %s: %.1f us/call, %d tiles, %d rounds, in-kernel clock %.0f MHz (median over workgroups)\n", sh.name,
+           ms * 1e3 / 20, tiles, rounds, med(clk));
+    printf("   round | prologue us | main loop us | epilogue us | hand-off us | main loop us per K tile\n");
+    double sp = 0, sm = 0, se = 0, sh_ = 0;
+    for (int r = 0; r < std::min(rounds, 64); ++r) {
+      std::vector<double> p, m, e, o;
+      for (int b = 0; b < blocks; ++b) {
+        const int tile = r * blocks + (b & 7) * (blocks / 8) + (b >> 3);
+        if (tile >= tiles) continue;
+        p.push_back((at(b, r, 1, 1) - at(b, r, 0, 1)) * 0.01);
+        m.push_back((at(b, r, 2, 1) - at(b, r, 1, 1)) * 0.01);
+        e.push_back((at(b, r, 3, 1) - at(b, r, 2, 1)) * 0.01);
+        const int nt = (r + 1) * blocks + (b & 7) * (blocks / 8) + (b >> 3);
+        if (r + 1 < std::min(rounds, 64) && nt < tiles) o.push_back((at(b, r + 1, 0, 1) - at(b, r, 3, 1)) * 0.01);
+      }
+      sp += med(p), sm += med(m), se += med(e), sh_ += med(o);
+      if (r < 4 || r + 2 >= rounds)
+        printf("   %5d | %11.2f | %12.2f | %11.2f | %11.2f | %.3f\n", r, med(p), med(m), med(e), med(o),
+               med(m) / (sh.K / 64));
+    }
+    printf("   sum   | %11.2f | %12.2f | %11.2f | %11.2f |\n", sp, sm, se, sh_);
+    CK(hipFree(A));
+    CK(hipFree(W));
+    CK(hipFree(C));
+    if (R) CK(hipFree(R));
+  }
+  CK(hipFree(dst));
+  return 0;
+}
