@@ -102,15 +102,15 @@ LWC_DEVICE void mfma(float4v& d, const uint4v& a, const uint4v& b) {
 #define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 #define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 // Diagnostic build only (scripts/probes/g4_stamps.cpp defines LWC_G4_STAMPS): wave 0 of every workgroup
-// records s_memrealtime at four points of each persistent round (and s_memtime at the first and last) into
-// g4_stamps[block][round][4] with vector stores; the product build has no stamp code at all.
+// records s_memrealtime at up to eight points of each persistent round (and s_memtime at the first and last)
+// into g4_stamps[block][round][8] with vector stores (points: scripts/probes/g4_stamps.cpp); the product build has no stamp code at all.
 #ifdef LWC_G4_STAMPS
 __device__ unsigned long long* g4_stamps;
 #define G4_STAMP(round, k)                                                                  \
   do {                                                                                      \
     if (threadIdx.x == 0 && (round) < 64) {                                                 \
-      unsigned long long* sp_ = g4_stamps + ((size_t)blockIdx.x * 64 + (round)) * 8 + 2 * (k); \
-      if ((k) == 0 || (k) == 3) sp_[0] = __builtin_amdgcn_s_memtime();                      \
+      unsigned long long* sp_ = g4_stamps + ((size_t)blockIdx.x * 64 + (round)) * 16 + 2 * (k); \
+      if ((k) == 0 || (k) == 7) sp_[0] = __builtin_amdgcn_s_memtime();                      \
       sp_[1] = __builtin_amdgcn_s_memrealtime();                                            \
     }                                                                                       \
   } while (0)
@@ -486,6 +486,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           }
         }
       }
+      G4_STAMP(round, 3);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float4v t[NT];
@@ -553,6 +554,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         }
         G4_LGKM0();  // the staging reads are done before the next m-tile overwrites the slice
         __builtin_amdgcn_sched_barrier(0);
+        if (i == 0) G4_STAMP(round, 4);
+        if (i == 3) G4_STAMP(round, 5);
+        if (i == 7) G4_STAMP(round, 6);
       }
       if constexpr (RS == 2) {
         __syncthreads();  // both waves of each row half wrote their row sums
@@ -565,7 +569,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           }
         }
       }
-      G4_STAMP(round, 3);
+      G4_STAMP(round, 7);
       continue;  // no block barrier: the next tile's first wait + barrier orders everything
     }
 
@@ -721,7 +725,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         }
       }
     }
-    G4_STAMP(round, 3);
+    G4_STAMP(round, 7);
   }
 }
 

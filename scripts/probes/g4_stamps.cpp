@@ -1,10 +1,13 @@
 // Where a gemm4w tile's time goes: a diagnostic build of csrc/kernels/gemm4w.hip with LWC_G4_STAMPS, whose
-// wave 0 of every workgroup records (s_memtime, s_memrealtime) at four points of each persistent round:
+// wave 0 of every workgroup records s_memrealtime at up to eight points of each persistent round (s_memtime
+// at the first and last):
 //   S0 tile start, S1 first K tiles landed (prologue wait + barrier), S2 main loop + drain + block barrier
-//   done, S3 epilogue done.
+//   done, S7 epilogue done; the wave-local (VAR 64) epilogue also S3 next tile's DMA issued, S4 / S5 / S6
+//   m-tiles 0 / 0-3 / 0-7 staged and stored.
 // Per shape: the call time (events, 20 back-to-back calls after ~1.5 s of warm-up launches on random
 // operands), the in-kernel clock (memtime / realtime x 100 MHz) and, per round, the median over workgroups of
-// prologue (S1 - S0), main loop (S2 - S1), epilogue (S3 - S2) and the hand-off to the next round (next S0 - S3).
+// prologue (S1 - S0), main loop (S2 - S1), epilogue (S7 - S2) and the hand-off to the next round (next S0 - S7);
+// for VAR 64 the epilogue's parts.  (The residual epilogue's stamped build spills VGPRs: those arms are not here.)
 //
 // Build (CPU container): hipcc --offload-arch=gfx950 -O3 -std=c++17 -DLWC_G4_STAMPS -I csrc/kernels \
 //   scripts/probes/g4_stamps.cpp -o scripts/probes/g4_stamps
@@ -56,12 +59,10 @@ int main() {
       {"gate_up+swiglu 4096x28672x4096 VAR32", 4096, 28672, 4096, 2, 32},
       {"lm_head 4096x128256x4096 VAR64", 4096, 128256, 4096, 0, 64},
       {"lm_head 4096x128256x4096 VAR32", 4096, 128256, 4096, 0, 32},
-      {"o+res 4096x4096x4096 VAR32", 4096, 4096, 4096, 1, 32},
-      {"down+res 4096x4096x14336 VAR32", 4096, 4096, 14336, 1, 32},
   };
   const int blocks = lwc::g4w::device_cus();
   unsigned long long* dst = nullptr;
-  CK(hipMalloc(&dst, (size_t)blocks * 64 * 8 * sizeof(unsigned long long)));
+  CK(hipMalloc(&dst, (size_t)blocks * 64 * 16 * sizeof(unsigned long long)));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(lwc::g4w::g4_stamps), &dst, sizeof(dst)));
   for (const Shape& sh : shapes) {
     uint16_t *A, *W, *C, *R = nullptr;
@@ -99,39 +100,43 @@ int main() {
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, e0, e1));
     // the last call's stamps
-    std::vector<unsigned long long> h((size_t)blocks * 64 * 8);
+    std::vector<unsigned long long> h((size_t)blocks * 64 * 16);
     CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
     const int tiles = ((sh.M + 255) / 256) * ((sh.N + 255) / 256);
     const int rounds = (tiles + blocks - 1) / blocks;
-    auto at = [&](int b, int r, int k, int which) { return h[((size_t)b * 64 + r) * 8 + 2 * k + which]; };
+    auto at = [&](int b, int r, int k, int which) { return h[((size_t)b * 64 + r) * 16 + 2 * k + which]; };
     std::vector<double> clk;
     for (int b = 0; b < blocks; ++b) {
       const int last = std::min(rounds, 64) - 1;
-      const double dc = (double)(at(b, last, 3, 0) - at(b, 0, 0, 0));
-      const double dt = (double)(at(b, last, 3, 1) - at(b, 0, 0, 1));
-      if (dt > 0 && at(b, last, 3, 1) >= at(b, 0, 0, 1)) clk.push_back(dc / dt * 100.0);  // MHz
+      const double dc = (double)(at(b, last, 7, 0) - at(b, 0, 0, 0));
+      const double dt = (double)(at(b, last, 7, 1) - at(b, 0, 0, 1));
+      if (dt > 0 && at(b, last, 7, 1) >= at(b, 0, 0, 1)) clk.push_back(dc / dt * 100.0);  // MHz
     }
     printf("== %s: %.1f us/call, %d tiles, %d rounds, in-kernel clock %.0f MHz (median over workgroups)\n", sh.name,
            ms * 1e3 / 20, tiles, rounds, med(clk));
-    printf("   round | prologue us | main loop us | epilogue us | hand-off us | main loop us per K tile\n");
+    printf("   round | prologue | main loop | epilogue [DMA issue, m-tile 0, m-tiles 1-3, 4-7, tail] | hand-off | loop us/K tile\n");
     double sp = 0, sm = 0, se = 0, sh_ = 0;
     for (int r = 0; r < std::min(rounds, 64); ++r) {
-      std::vector<double> p, m, e, o;
+      std::vector<double> p, m, e, o, d[5];
       for (int b = 0; b < blocks; ++b) {
         const int tile = r * blocks + (b & 7) * (blocks / 8) + (b >> 3);
         if (tile >= tiles) continue;
-        p.push_back((at(b, r, 1, 1) - at(b, r, 0, 1)) * 0.01);
-        m.push_back((at(b, r, 2, 1) - at(b, r, 1, 1)) * 0.01);
-        e.push_back((at(b, r, 3, 1) - at(b, r, 2, 1)) * 0.01);
+        auto us = [&](int k1, int k0) { return ((double)at(b, r, k1, 1) - (double)at(b, r, k0, 1)) * 0.01; };
+        p.push_back(us(1, 0));
+        m.push_back(us(2, 1));
+        e.push_back(us(7, 2));
+        if (sh.var == 64)
+          for (int k = 0; k < 5; ++k) d[k].push_back(us(k + 3, k + 2));
         const int nt = (r + 1) * blocks + (b & 7) * (blocks / 8) + (b >> 3);
-        if (r + 1 < std::min(rounds, 64) && nt < tiles) o.push_back((at(b, r + 1, 0, 1) - at(b, r, 3, 1)) * 0.01);
+        if (r + 1 < std::min(rounds, 64) && nt < tiles)
+          o.push_back(((double)at(b, r + 1, 0, 1) - (double)at(b, r, 7, 1)) * 0.01);
       }
       sp += med(p), sm += med(m), se += med(e), sh_ += med(o);
-      if (r < 4 || r + 2 >= rounds)
-        printf("   %5d | %11.2f | %12.2f | %11.2f | %11.2f | %.3f\n", r, med(p), med(m), med(e), med(o),
-               med(m) / (sh.K / 64));
+      if (r < 3 || r + 2 >= rounds)
+        printf("   %5d | %8.2f | %9.2f | %8.2f [%5.2f %5.2f %5.2f %5.2f %5.2f] | %8.2f | %.3f\n", r, med(p), med(m),
+               med(e), med(d[0]), med(d[1]), med(d[2]), med(d[3]), med(d[4]), med(o), med(m) / (sh.K / 64));
     }
-    printf("   sum   | %11.2f | %12.2f | %11.2f | %11.2f |\n", sp, sm, se, sh_);
+    printf("   sum   | %8.2f | %9.2f | %8.2f | %8.2f\n", sp, sm, se, sh_);
     CK(hipFree(A));
     CK(hipFree(W));
     CK(hipFree(C));
