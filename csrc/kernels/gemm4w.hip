@@ -96,6 +96,16 @@ struct Geo {
 LWC_DEVICE void mfma(float4v& d, const uint4v& a, const uint4v& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
 }
+// TR: operands swapped — the MFMA computes the tile transposed (A operand = W rows, B = activation rows), so
+// a lane's accumulator quad holds 4 consecutive OUTPUT COLUMNS of one output row instead of 4 rows of one
+// column; the wave-local epilogue then packs rows in registers (no LDS staging), see TR below
+template <bool TR>
+LWC_DEVICE void mfma2(float4v& d, const uint4v& a, const uint4v& b) {
+  if constexpr (TR)
+    mfma(d, b, a);
+  else
+    mfma(d, a, b);
+}
 // the first non-MFMA read of an accumulator after the last (opaque) MFMA: 16 wait states
 #define G4_MFMA_DRAIN() asm volatile("s_nop 15" ::: "memory")
 #define G4_BAR() __builtin_amdgcn_s_barrier()
@@ -156,6 +166,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   // the wave-local epilogue (VAR 64) for the residual epilogue only with RS 2: the plain residual form of it
   // spilled (256 VGPRs + 220 B scratch), the RS 2 form compiles at 233 VGPRs
   constexpr bool PAP = VAR == 64 && (EPI != EPI_RESIDUAL || RS == 2);
+  // the wave-local epilogue of the plain and SwiGLU outputs on the transposed accumulator layout (mfma2)
+  constexpr bool TR = PAP && RS == 0 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU);
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
   // block-staged epilogue, VAR 32); RS 2: the four waves' 128 row sums (2 KiB) at the same place
   constexpr int RSOFF = PAP ? G::LdsPap : G::Lds, RSV = RSOFF + 16384;
@@ -281,16 +293,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
       rd1(cur, offA1, offB1, ya, yb, k);                                                            \
       _Pragma("unroll") for (int m = k * F1 / G::Reads; m < (k + 1) * F1 / G::Reads; ++m)           \
-        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
-    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
+    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
     G4_LGKM0();                                                                                     \
     G4_BAR();                                                                                       \
     _Pragma("unroll") for (int k = 0; k < P2; ++k) {                                                \
       if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
       _Pragma("unroll") for (int m = k * S2 / P2; m < (k + 1) * S2 / P2; ++m)                       \
-        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     if constexpr (STAGE) {                                                                          \
@@ -305,7 +317,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         if (k < P3) piece(cur, (R) + 2, P2 + k);                                                    \
       }                                                                                             \
       _Pragma("unroll") for (int m = S2 + k * S3 / G::Reads; m < S2 + (k + 1) * S3 / G::Reads; ++m) \
-        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -321,7 +333,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
       rd1(cur, offA1, offB1, ya, yb, k);                                                            \
       _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     G4_LGKM0();                                                                                     \
@@ -331,7 +343,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
       if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
       _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -350,7 +362,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
     _Pragma("unroll") for (int m = 0; m < HA; ++m) {                                                \
       if (m < G::Reads) rd1(cur, offA1, offB1, ya, yb, m);                                          \
-      mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                            \
+      mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                            \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     G4_LGKM0();                                                                                     \
@@ -362,9 +374,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       }                                                                                             \
       const int m = HA + q;                                                                         \
       if (m < M1)                                                                                   \
-        mfma(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       else                                                                                          \
-        mfma(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
+        mfma2<TR>(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     if constexpr (STAGE) {                                                                          \
@@ -379,7 +391,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         if (c < G::Reads) rd1(nxt, offA0, offB0, xa, xb, c);                                        \
       }                                                                                             \
       const int m = M1 - HC + c;                                                                    \
-      mfma(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                            \
+      mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                            \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -487,6 +499,54 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         }
       }
       G4_STAMP(round, 3);
+      if constexpr (TR) {
+        // TR layout: lane (r16, q) holds output row i * 16 + r16, columns g * 16 + 4 q + e of output group g
+        // (g = n-tile for the plain output, h * 2 + jj for SwiGLU's h-th 32-column block).  Per m-tile:
+        // SwiGLU / bf16 packing in registers (v_cvt_pk_bf16_f32 pairs), then groups (2 g2, 2 g2 + 1) pair up
+        // by v_permlane16_swap: row-of-16-lanes q keeps group 2 g2 + (q & 1), columns (q >> 1) * 8 .. + 7 —
+        // 16 contiguous bytes — and stores them with ONE buffer_store_dwordx4.  No LDS staging, no LDS waits
+        // (the block-staged image cost 16-32 ds_write_b16 + 2-4 ds_read_b128 + 2 lgkmcnt(0) per m-tile).
+        constexpr int NO = EPI == EPI_SWIGLU ? NT / 2 : NT;  // 16-column output groups
+        static_assert(NO % 2 == 0, "TR pairs output groups");
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          uint32_t o[NO][2];
+#pragma unroll
+          for (int g = 0; g < NO; ++g) {
+            float v[4];
+            if constexpr (EPI == EPI_SWIGLU) {
+              const int gate = (g >> 1) * 4 + (g & 1);  // n-tile of the gate half; the up half is 2 further
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = acc[i][g][e];
+            }
+            o[g][0] = pack_bf16x2(v[0], v[1]);
+            o[g][1] = pack_bf16x2(v[2], v[3]);
+          }
+          const int row = i * 16 + r16;
+#pragma unroll
+          for (int g2 = 0; g2 < NO / 2; ++g2) {
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto r = __builtin_amdgcn_permlane16_swap(o[2 * g2][d], o[2 * g2 + 1][d], false, false);
+              o[2 * g2][d] = r[0];
+              o[2 * g2 + 1][d] = r[1];
+            }
+            const uint4v v = {o[2 * g2][0], o[2 * g2][1], o[2 * g2 + 1][0], o[2 * g2 + 1][1]};
+            const int gn = ncol0 + g2 * 32 + (q & 1) * 16 + (q >> 1) * 8;
+            const uint32_t off = gn < ncols ? (uint32_t)((row * p.ldc + gn) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one m-tile's accumulators in flight at a time
+          if (i == 0) G4_STAMP(round, 4);
+          if (i == 3) G4_STAMP(round, 5);
+          if (i == 7) G4_STAMP(round, 6);
+        }
+        G4_STAMP(round, 7);
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float4v t[NT];
