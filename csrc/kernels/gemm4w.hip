@@ -163,11 +163,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  // the wave-local epilogue (VAR 64) for the residual epilogue only with RS 2: the plain residual form of it
-  // spilled (256 VGPRs + 220 B scratch), the RS 2 form compiles at 233 VGPRs
-  constexpr bool PAP = VAR == 64 && (EPI != EPI_RESIDUAL || RS == 2);
-  // the wave-local epilogue of the plain and SwiGLU outputs on the transposed accumulator layout (mfma2)
+  // the wave-local epilogue (VAR 64): every epilogue but the row-scaled consumers (RS 1)
+  constexpr bool PAP = VAR == 64 && RS != 1;
+  // the wave-local epilogue of the plain, SwiGLU (TR) and residual (TRR, RS 0 / 2) outputs on the transposed
+  // accumulator layout (mfma2); bias / GELU keep the staged image
   constexpr bool TR = PAP && RS == 0 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU);
+  constexpr bool TRR = PAP && EPI == EPI_RESIDUAL;
+  constexpr bool TRL = TR || TRR;
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
   // block-staged epilogue, VAR 32); RS 2: the four waves' 128 row sums (2 KiB) at the same place
   constexpr int RSOFF = PAP ? G::LdsPap : G::Lds, RSV = RSOFF + 16384;
@@ -242,9 +244,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
-    // (plain residual epilogues keep the block-staged path: o / down are single-round at the decode batch, so
-    // there is no next tile to prefetch, and its 32 up-front residual chunks per lane spilled; the RS 2 form of
-    // the chain takes this path: no block barriers between the staging and the stores)
+    // (the residual epilogue takes this path too — TRR: residual chunks loaded two m-tiles ahead, not all up
+    // front, which spilled — and so does its RS 2 form: no block barriers between the adds and the stores)
     if (!PAP || round == 0) {
       if constexpr (RS == 1) {  // the oldest VMEM ops of each wave: the counted wait below retires them
         for (int k = wid; k < p.P; k += 4) ss_dma(m0, k);
@@ -293,16 +294,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
       rd1(cur, offA1, offB1, ya, yb, k);                                                            \
       _Pragma("unroll") for (int m = k * F1 / G::Reads; m < (k + 1) * F1 / G::Reads; ++m)           \
-        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
-    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
+    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
     G4_LGKM0();                                                                                     \
     G4_BAR();                                                                                       \
     _Pragma("unroll") for (int k = 0; k < P2; ++k) {                                                \
       if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
       _Pragma("unroll") for (int m = k * S2 / P2; m < (k + 1) * S2 / P2; ++m)                       \
-        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     if constexpr (STAGE) {                                                                          \
@@ -317,7 +318,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         if (k < P3) piece(cur, (R) + 2, P2 + k);                                                    \
       }                                                                                             \
       _Pragma("unroll") for (int m = S2 + k * S3 / G::Reads; m < S2 + (k + 1) * S3 / G::Reads; ++m) \
-        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
       rd1(cur, offA1, offB1, ya, yb, k);                                                            \
       _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     G4_LGKM0();                                                                                     \
@@ -343,7 +344,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
       if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
       _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
     _Pragma("unroll") for (int m = 0; m < HA; ++m) {                                                \
       if (m < G::Reads) rd1(cur, offA1, offB1, ya, yb, m);                                          \
-      mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                            \
+      mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                            \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     G4_LGKM0();                                                                                     \
@@ -374,9 +375,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       }                                                                                             \
       const int m = HA + q;                                                                         \
       if (m < M1)                                                                                   \
-        mfma2<TR>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
+        mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
       else                                                                                          \
-        mfma2<TR>(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
+        mfma2<TRL>(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
     if constexpr (STAGE) {                                                                          \
@@ -391,7 +392,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         if (c < G::Reads) rd1(nxt, offA0, offB0, xa, xb, c);                                        \
       }                                                                                             \
       const int m = M1 - HC + c;                                                                    \
-      mfma2<TR>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                            \
+      mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                            \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
   }
@@ -436,8 +437,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
     if constexpr (PAP) {
-      // ---- epilogue, wave-local: per m-tile (16 rows) through this wave's own staging slice, no block
-      // barrier; residual chunks all loaded up front into the (dead) fragment registers
+      // ---- epilogue, wave-local: per m-tile (16 rows), no block barrier; plain / SwiGLU / residual pack rows
+      // in registers (TR, TRR), bias / GELU go through this wave's own staging slice
       constexpr int CPR = CW / 8;          // 16 B chunks per row
       constexpr int PER = 16 * CPR / 64;   // chunks per lane per m-tile: 4 (bn 256), 3 (bn 192), 2 (SwiGLU)
       bf16_t* st = reinterpret_cast<bf16_t*>(smem + G::Lds + wid * G::Stage);
@@ -451,7 +452,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       const __amdgpu_buffer_rsrc_t rC = uniform_rsrc(p.C + (size_t)row0 * p.ldc, rows_c * p.ldc * 2);
       // operand loads of the epilogue FIRST, then the next tile's DMA: loads return in issue order, so a
       // residual / bias value issued after the DMA pieces could only be used once they had landed
-      uint4v rv[8][PER];
       float bvals[NT];
       if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
@@ -460,17 +460,25 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           bvals[jj] = col < p.N ? bf2f(p.R[col]) : 0.f;
         }
       }
-      if constexpr (EPI == EPI_RESIDUAL) {
-        const int rows_here = max(0, min(p.M - row0, 128));
-        const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.R + (size_t)row0 * p.ldc, rows_here * p.ldc * 2);
+      // TR / TRR: the lane's 16 B chunk of column pair g2 of an m-tile (the layout of the TR stores below):
+      // the column part per lane (past the last column: an offset past the resource's end, dropped), the
+      // m-tile's row offset wave-uniform in soffset
+      uint32_t tr_vo[NT / 2];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+      for (int g2 = 0; g2 < NT / 2; ++g2) {
+        const int gn = ncol0 + g2 * 32 + (q & 1) * 16 + (q >> 1) * 8;
+        tr_vo[g2] = gn < ncols ? (uint32_t)((r16 * p.ldc + gn) * 2) : 0x80000000u;
+      }
+      auto tr_so = [&](int i) { return i * 32 * p.ldc; };  // (kernel argument x constant: SALU)
+      const __amdgpu_buffer_rsrc_t rR =
+          uniform_rsrc(EPI == EPI_RESIDUAL ? p.R + (size_t)row0 * p.ldc : p.A, EPI == EPI_RESIDUAL ? rows_c * p.ldc * 2 : 0);
+      uint4v rv[2][NT / 2];  // TRR: residual chunks of m-tiles i and i + 1 (two m-tiles ahead of the adds)
+      if constexpr (TRR) {
 #pragma unroll
-          for (int u = 0; u < PER; ++u) {
-            const int c = lane + 64 * u;
-            const int row = i * 16 + c / CPR, gn = ncol0 + (c % CPR) * 8;
-            rv[i][u] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, (row * p.ldc + gn) * 2, 0, 0));
-          }
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int g2 = 0; g2 < NT / 2; ++g2)
+            rv[i][g2] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, tr_vo[g2], tr_so(i), 0));
       }
       // ---- the next tile's first two K tiles into the (now free) K buffers, in flight under this epilogue
       const int ntile = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
@@ -499,6 +507,68 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         }
       }
       G4_STAMP(round, 3);
+      if constexpr (TRR) {
+        // residual on the TR layout: per column pair the fp32 accumulators swap halves by v_permlane16_swap
+        // (4 per pair), the lane adds its 16 B residual chunk (loaded two m-tiles ahead) to 8 consecutive
+        // columns and stores them in place; RS 2: the row's squares over the wave's 128 columns meet across
+        // the 4 lanes of the row (xor 16, 32)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          uint4v res[NT / 2];
+#pragma unroll
+          for (int g2 = 0; g2 < NT / 2; ++g2) res[g2] = rv[i & 1][g2];
+          if (i + 2 < 8) {
+#pragma unroll
+            for (int g2 = 0; g2 < NT / 2; ++g2)
+              rv[i & 1][g2] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, tr_vo[g2], tr_so(i + 2), 0));
+          }
+          float sq = 0.f;
+#pragma unroll
+          for (int g2 = 0; g2 < NT / 2; ++g2) {
+            float x[8], y[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * g2][e]),
+                                                              __float_as_uint(acc[i][2 * g2 + 1][e]), false, false);
+              x[e] = __uint_as_float(r[0]);
+              x[e + 4] = __uint_as_float(r[1]);
+            }
+            unpack8(res[g2], y);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] += y[e];
+            const uint4v v = pack8(x);
+            if constexpr (RS == 2) {  // the bf16-rounded values the stream now holds
+              float z[8];
+              unpack8(tr_vo[g2] != 0x80000000u ? v : uint4v{0u, 0u, 0u, 0u}, z);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) sq += z[e] * z[e];
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, tr_vo[g2], tr_so(i), 0);
+          }
+          if constexpr (RS == 2) {
+            sq += __shfl_xor(sq, 16);
+            sq += __shfl_xor(sq, 32);
+            if (q == 0) reinterpret_cast<float*>(smem + RSOFF)[wid * 128 + i * 16 + r16] = sq;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (i == 0) G4_STAMP(round, 4);
+          if (i == 3) G4_STAMP(round, 5);
+          if (i == 7) G4_STAMP(round, 6);
+        }
+        if constexpr (RS == 2) {
+          __syncthreads();  // both waves of each row half wrote their row sums
+          if (wn == 0) {
+            const float* rsum = reinterpret_cast<const float*>(smem + RSOFF);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int row = lane + 64 * h, gm = m0 + wm * 128 + row;
+              if (gm < p.M) p.ss[(size_t)tn * p.ssld + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
+            }
+          }
+        }
+        G4_STAMP(round, 7);
+        continue;
+      }
       if constexpr (TR) {
         // TR layout: lane (r16, q) holds output row i * 16 + r16, columns g * 16 + 4 q + e of output group g
         // (g = n-tile for the plain output, h * 2 + jj for SwiGLU's h-th 32-column block).  Per m-tile:
@@ -525,7 +595,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             o[g][0] = pack_bf16x2(v[0], v[1]);
             o[g][1] = pack_bf16x2(v[2], v[3]);
           }
-          const int row = i * 16 + r16;
 #pragma unroll
           for (int g2 = 0; g2 < NO / 2; ++g2) {
 #pragma unroll
@@ -535,9 +604,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
               o[2 * g2 + 1][d] = r[1];
             }
             const uint4v v = {o[2 * g2][0], o[2 * g2][1], o[2 * g2 + 1][0], o[2 * g2 + 1][1]};
-            const int gn = ncol0 + g2 * 32 + (q & 1) * 16 + (q >> 1) * 8;
-            const uint32_t off = gn < ncols ? (uint32_t)((row * p.ldc + gn) * 2) : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, tr_vo[g2], tr_so(i), 0);
           }
           __builtin_amdgcn_sched_barrier(0);  // one m-tile's accumulators in flight at a time
           if (i == 0) G4_STAMP(round, 4);
@@ -587,27 +654,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           const int c = lane + 64 * u;
           const int row = c / CPR, cch = c % CPR;
           const int gm = row0 + i * 16 + row, gn = ncol0 + cch * 8;
-          uint4v v = *reinterpret_cast<const uint4v*>(st + row * CW + swz<CW>(row, cch * 8));
-          if constexpr (EPI == EPI_RESIDUAL) {
-            float x[8], y[8];
-            unpack8(v, x);
-            unpack8(rv[i][u], y);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) x[e] += y[e];
-            v = pack8(x);
-          }
-          if constexpr (RS == 2) {  // as in the block-staged epilogue: the row's squares over the wave's columns
-            float z[8];
-            unpack8(gn < ncols ? v : uint4v{0u, 0u, 0u, 0u}, z);
-            float sq = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) sq += z[e] * z[e];
-            sq += __shfl_xor(sq, 8);
-            sq += __shfl_xor(sq, 4);
-            sq += __shfl_xor(sq, 2);
-            sq += __shfl_xor(sq, 1);
-            if ((lane & 15) == 0) reinterpret_cast<float*>(smem + RSOFF)[wid * 128 + i * 16 + row] = sq;
-          }
+          const uint4v v = *reinterpret_cast<const uint4v*>(st + row * CW + swz<CW>(row, cch * 8));
           (void)gm;
           const uint32_t off = gn < ncols ? (uint32_t)(((i * 16 + row) * p.ldc + gn) * 2) : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
@@ -617,17 +664,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         if (i == 0) G4_STAMP(round, 4);
         if (i == 3) G4_STAMP(round, 5);
         if (i == 7) G4_STAMP(round, 6);
-      }
-      if constexpr (RS == 2) {
-        __syncthreads();  // both waves of each row half wrote their row sums
-        if (wn == 0) {
-          const float* rsum = reinterpret_cast<const float*>(smem + RSOFF);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int row = lane + 64 * h, gm = m0 + wm * 128 + row;
-            if (gm < p.M) p.ss[(size_t)tn * p.ssld + gm] = rsum[wid * 128 + row] + rsum[(wid + 1) * 128 + row];
-          }
-        }
       }
       G4_STAMP(round, 7);
       continue;  // no block barrier: the next tile's first wait + barrier orders everything
@@ -791,7 +827,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = (VAR == 64 && (EPI != EPI_RESIDUAL || RS == 2) ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
+  constexpr int lds = (VAR == 64 && RS != 1 ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
                       (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
   static bool attr = false;
   if (!attr) {

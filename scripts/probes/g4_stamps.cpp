@@ -7,7 +7,8 @@
 // Per shape: the call time (events, 20 back-to-back calls after ~1.5 s of warm-up launches on random
 // operands), the in-kernel clock (memtime / realtime x 100 MHz) and, per round, the median over workgroups of
 // prologue (S1 - S0), main loop (S2 - S1), epilogue (S7 - S2) and the hand-off to the next round (next S0 - S7);
-// for VAR 64 the epilogue's parts.  (The residual epilogue's stamped build spills VGPRs: those arms are not here.)
+// for VAR 64 the epilogue's parts.  (The stamped build of the residual epilogue may spill a few VGPRs: compare
+// those arms by call time.)
 //
 // Build (CPU container): hipcc --offload-arch=gfx950 -O3 -std=c++17 -DLWC_G4_STAMPS -I csrc/kernels \
 //   scripts/probes/g4_stamps.cpp -o scripts/probes/g4_stamps
@@ -59,6 +60,10 @@ int main() {
       {"gate_up+swiglu 4096x28672x4096 VAR32", 4096, 28672, 4096, 2, 32},
       {"lm_head 4096x128256x4096 VAR64", 4096, 128256, 4096, 0, 64},
       {"lm_head 4096x128256x4096 VAR32", 4096, 128256, 4096, 0, 32},
+      {"o+res 4096x4096x4096 VAR64", 4096, 4096, 4096, 1, 64},
+      {"o+res 4096x4096x4096 VAR32", 4096, 4096, 4096, 1, 32},
+      {"down+res 4096x4096x14336 VAR64", 4096, 4096, 14336, 1, 64},
+      {"down+res 4096x4096x14336 VAR32", 4096, 4096, 14336, 1, 32},
   };
   const int blocks = lwc::g4w::device_cus();
   unsigned long long* dst = nullptr;
