@@ -164,10 +164,10 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   // the wave-local epilogue (VAR 64): every epilogue but the row-scaled consumers (RS 1)
-  constexpr bool PAP = VAR == 64 && RS != 1;
+  constexpr bool PAP = (VAR == 64 || VAR == 96) && RS != 1;  // 96: VAR 64 without TR (A/B knob)
   // the wave-local epilogue of the plain, SwiGLU (TR) and residual (TRR, RS 0 / 2) outputs on the transposed
   // accumulator layout (mfma2); bias / GELU keep the staged image
-  constexpr bool TR = PAP && RS == 0 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU);
+  constexpr bool TR = PAP && VAR == 64 && RS == 0 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU);
   constexpr bool TRR = PAP && EPI == EPI_RESIDUAL;
   constexpr bool TRL = TR || TRR;
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }                                                                                               \
   }
     int r = 0;
-    if constexpr (VAR == 32 || VAR == 64) {
+    if constexpr (VAR == 32 || VAR == 64 || VAR == 96) {
       for (; r + 2 < nt; ++r) G4_TILE_H(r, true, true)
       if (nt >= 2) {
         G4_TILE_H(r, false, true)
@@ -827,7 +827,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = (VAR == 64 && RS != 1 ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
+  constexpr int lds = ((VAR == 64 || VAR == 96) && RS != 1 ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
                       (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
   static bool attr = false;
   if (!attr) {
@@ -845,7 +845,7 @@ template <int EPI, int NT>
 int launch(const Params& p, hipStream_t s, int var, int rs) {
   // schedule variant (VAR bits, see the main loop): the caller's, else LWC_G4_VAR, an A/B knob
   // (scripts/microbench.py g4ab); default 32, the library-shaped schedule (faster than 1 at every headline
-  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants.
+  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants; 96 = 64 with the staged epilogue image instead of TR (plain / SwiGLU, A/B only).
   // rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sum-of-squares (see the file head)
   if (var <= 0) var = env_int("LWC_G4_VAR", 32);
   if (rs == 1) {
@@ -862,6 +862,9 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
   }
   if (var == 32) return launch3<EPI, NT, 32, 0>(p, s);
   if (var == 64) return launch3<EPI, NT, 64, 0>(p, s);
+  if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) {  // VAR 64 with the staged epilogue image (A/B)
+    if (var == 96) return launch3<EPI, NT, 96, 0>(p, s);
+  }
   if constexpr (EPI == EPI_PLAIN) {
     switch (var) {
       case 0: return launch3<EPI, NT, 0, 0>(p, s);
