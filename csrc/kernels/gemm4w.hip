@@ -139,6 +139,14 @@ LWC_DEVICE float erf_as(float x) {
   return copysignf(1.f - y * __expf(-a * a), x);
 }
 LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
+// GELU in the tanh form, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)) — the form hipBLASLt's bias+GELU
+// epilogue computes (the library arm the planner times against): 2 transcendentals + 4 VALU instead of
+// erf_as's 2 + ~12, within 8.1e-3 of the erf form at the bge-large FFN1 shape, the bf16 output's own rounding
+// being 7.8e-3 (ops/gemm_plan.py linear_bias).  The VAR 64 epilogue uses it; the other schedules keep erf.
+LWC_DEVICE float gelu_tanh(float x) {
+  const float z = x * (1.5957691216f + 0.0713548163f * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-z));
+}
 
 LWC_DEVICE void tile_mn(const Params& p, int t, int& m, int& n) {
   const int group = p.gm * p.tiles_n;
@@ -165,9 +173,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   // the wave-local epilogue (VAR 64): every epilogue but the row-scaled consumers (RS 1)
   constexpr bool PAP = (VAR == 64 || VAR == 96) && RS != 1;  // 96: VAR 64 without TR (A/B knob)
-  // the wave-local epilogue of the plain, SwiGLU (TR) and residual (TRR, RS 0 / 2) outputs on the transposed
-  // accumulator layout (mfma2); bias / GELU keep the staged image
-  constexpr bool TR = PAP && VAR == 64 && RS == 0 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU);
+  // the wave-local epilogue of every output on the transposed accumulator layout (mfma2): plain / SwiGLU /
+  // bias / GELU (TR) and residual (TRR, RS 0 / 2); VAR 96 keeps the staged image for all but the residual
+  constexpr bool TR = PAP && VAR == 64 && RS == 0 && EPI != EPI_RESIDUAL;
   constexpr bool TRR = PAP && EPI == EPI_RESIDUAL;
   constexpr bool TRL = TR || TRR;
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
@@ -437,8 +445,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
     if constexpr (PAP) {
-      // ---- epilogue, wave-local: per m-tile (16 rows), no block barrier; plain / SwiGLU / residual pack rows
-      // in registers (TR, TRR), bias / GELU go through this wave's own staging slice
+      // ---- epilogue, wave-local: per m-tile (16 rows), no block barrier; VAR 64 packs rows in registers (TR,
+      // TRR), VAR 96 (A/B) goes through this wave's own staging slice
       constexpr int CPR = CW / 8;          // 16 B chunks per row
       constexpr int PER = 16 * CPR / 64;   // chunks per lane per m-tile: 4 (bn 256), 3 (bn 192), 2 (SwiGLU)
       bf16_t* st = reinterpret_cast<bf16_t*>(smem + G::Lds + wid * G::Stage);
@@ -453,11 +461,26 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       // operand loads of the epilogue FIRST, then the next tile's DMA: loads return in issue order, so a
       // residual / bias value issued after the DMA pieces could only be used once they had landed
       float bvals[NT];
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+      if constexpr (!TR && (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
 #pragma unroll
         for (int jj = 0; jj < NT; ++jj) {
           const int col = n0 + wn * 16 * NT + r16 + jj * 16;
           bvals[jj] = col < p.N ? bf2f(p.R[col]) : 0.f;
+        }
+      }
+      // TR: the bias of the lane's 4 consecutive columns 16 g + 4 q .. + 3 of each n-tile g (8 B loads; N % 8
+      // == 0, so a group lies wholly inside or past the last column)
+      float tbias[NT][4];
+      if constexpr (TR && (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
+#pragma unroll
+        for (int g = 0; g < NT; ++g) {
+          const int col = n0 + wn * 16 * NT + g * 16 + 4 * q;
+          uint2 b2 = {0u, 0u};
+          if (col < p.N) b2 = *reinterpret_cast<const uint2*>(p.R + col);
+          tbias[g][0] = __uint_as_float(b2.x << 16);
+          tbias[g][1] = __uint_as_float(b2.x & 0xffff0000u);
+          tbias[g][2] = __uint_as_float(b2.y << 16);
+          tbias[g][3] = __uint_as_float(b2.y & 0xffff0000u);
         }
       }
       // TR / TRR: the lane's 16 B chunk of column pair g2 of an m-tile (the layout of the TR stores below):
@@ -571,8 +594,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       }
       if constexpr (TR) {
         // TR layout: lane (r16, q) holds output row i * 16 + r16, columns g * 16 + 4 q + e of output group g
-        // (g = n-tile for the plain output, h * 2 + jj for SwiGLU's h-th 32-column block).  Per m-tile:
-        // SwiGLU / bf16 packing in registers (v_cvt_pk_bf16_f32 pairs), then groups (2 g2, 2 g2 + 1) pair up
+        // (g = n-tile for the plain / bias output, h * 2 + jj for SwiGLU's h-th 32-column block).  Per m-tile:
+        // SwiGLU / bias (+ GELU) / bf16 packing in registers (v_cvt_pk_bf16_f32 pairs), then groups (2 g2, 2 g2 + 1) pair up
         // by v_permlane16_swap: row-of-16-lanes q keeps group 2 g2 + (q & 1), columns (q >> 1) * 8 .. + 7 —
         // 16 contiguous bytes — and stores them with ONE buffer_store_dwordx4.  No LDS staging, no LDS waits
         // (the block-staged image cost 16-32 ds_write_b16 + 2-4 ds_read_b128 + 2 lgkmcnt(0) per m-tile).
@@ -588,6 +611,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
               const int gate = (g >> 1) * 4 + (g & 1);  // n-tile of the gate half; the up half is 2 further
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
+            } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float y = acc[i][g][e] + tbias[g][e];
+                v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(y) : y;
+              }
             } else {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = acc[i][g][e];
@@ -845,7 +874,7 @@ template <int EPI, int NT>
 int launch(const Params& p, hipStream_t s, int var, int rs) {
   // schedule variant (VAR bits, see the main loop): the caller's, else LWC_G4_VAR, an A/B knob
   // (scripts/microbench.py g4ab); default 32, the library-shaped schedule (faster than 1 at every headline
-  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants; 96 = 64 with the staged epilogue image instead of TR (plain / SwiGLU, A/B only).
+  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants; 96 = 64 with the staged epilogue image instead of TR (and erf GELU; A/B only).
   // rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sum-of-squares (see the file head)
   if (var <= 0) var = env_int("LWC_G4_VAR", 32);
   if (rs == 1) {
@@ -862,7 +891,7 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
   }
   if (var == 32) return launch3<EPI, NT, 32, 0>(p, s);
   if (var == 64) return launch3<EPI, NT, 64, 0>(p, s);
-  if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) {  // VAR 64 with the staged epilogue image (A/B)
+  if constexpr (EPI != EPI_RESIDUAL) {  // VAR 64 with the staged epilogue image (and erf GELU): A/B
     if (var == 96) return launch3<EPI, NT, 96, 0>(p, s);
   }
   if constexpr (EPI == EPI_PLAIN) {
