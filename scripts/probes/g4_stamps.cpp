@@ -64,6 +64,9 @@ int main() {
       {"o+res 4096x4096x4096 VAR32", 4096, 4096, 4096, 1, 32},
       {"down+res 4096x4096x14336 VAR64", 4096, 4096, 14336, 1, 64},
       {"down+res 4096x4096x14336 VAR32", 4096, 4096, 14336, 1, 32},
+      {"enc o+bias 524288x768x768 VAR64", 524288, 768, 768, 3, 64},
+      {"enc o+bias 524288x768x768 VAR96", 524288, 768, 768, 3, 96},
+      {"enc FFN1+bias+GELU 524288x3072x768 VAR64", 524288, 3072, 768, 4, 64},
   };
   const int blocks = lwc::g4w::device_cus();
   unsigned long long* dst = nullptr;
@@ -76,9 +79,10 @@ int main() {
     CK(hipMalloc(&C, (size_t)sh.M * sh.N * 2));
     fill_rand<<<1024, 256>>>(A, (size_t)sh.M * sh.K, 1);
     fill_rand<<<1024, 256>>>(W, (size_t)sh.N * sh.K, 2);
-    if (sh.epi == 1) {
-      CK(hipMalloc(&R, (size_t)sh.M * sh.N * 2));
-      fill_rand<<<1024, 256>>>(R, (size_t)sh.M * sh.N, 3);
+    if (sh.epi == 1 || sh.epi == 3 || sh.epi == 4) {  // residual [M, N] / bias [N]
+      const size_t nr = sh.epi == 1 ? (size_t)sh.M * sh.N : (size_t)sh.N;
+      CK(hipMalloc(&R, nr * 2));
+      fill_rand<<<1024, 256>>>(R, nr, 3);
     }
     CK(hipDeviceSynchronize());
     auto call = [&]() {
