@@ -29,6 +29,7 @@ int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, int,
                float, int, hipStream_t);
 int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
+int lwc_skinny_gemm(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, int, int, const void*, void*, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
@@ -448,6 +449,19 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
                       (int)epi, (int)bn, ssp, ssp ? (int)ss->size(1) : 0, (int)rs_mode, (int)P, (float)eps, (int)var,
                       cur_stream()),
            "gemm4w");
+}
+
+// skinny GEMM (decode-sized M <= 64): C = A . W^T (epi 0), R + A . W^T (epi 1, R may be C) or the SwiGLU of
+// a 32-row gate/up interleaved W (epi 2, C [M, N / 2])
+void skinny_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R,
+                 int64_t epi) {
+  TORCH_CHECK(epi >= 0 && epi <= 2, "skinny_gemm: epi 0 (plain), 1 (residual) or 2 (SwiGLU)");
+  const void* r = gemm_operands(A, W, C, R, epi);
+  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
+  TORCH_CHECK(M <= 64 && K % 2048 == 0 && N % 16 == 0, "skinny_gemm: needs M <= 64, K % 2048 == 0, N % 16 == 0");
+  CHECK_RC(lwc_skinny_gemm(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
+                           (int)epi, cur_stream()),
+           "skinny_gemm");
 }
 
 // ss[r] = sum(x[r]^2): the single partial of the folded RMSNorm for the first projection of a chain
@@ -932,6 +946,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grouped_gemm", &grouped_gemm);
   m.def("gemm8p", &gemm8p);
   m.def("gemm4w", &gemm4w);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("rms_rowsumsq", &rms_rowsumsq);
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);

@@ -403,6 +403,25 @@ def gemm8p(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     return out
 
 
+def skinny_gemm(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, swiglu: bool = False) -> torch.Tensor:
+    """Decode-sized projection (K6, csrc/kernels/skinny.hip): ``A [M <= 64, K] . W[N, K]^T`` (+ ``residual``,
+    in place with ``out=residual``; or ``swiglu`` over a 32-row gate/up interleaved W, output [M, N / 2]) as a
+    weight stream — one workgroup per 16 output columns, its 8 waves splitting K, partials summed in LDS in a
+    fixed order.  Needs K % 2048 == 0 and N % 16 == 0 (SwiGLU: N % 64 == 0) (:func:`skinny_ok`)."""
+    if swiglu and residual is not None:
+        raise ValueError("skinny_gemm: swiglu and residual do not combine")
+    if out is None:
+        out = torch.empty(A.shape[0], W.shape[0] // 2 if swiglu else W.shape[0], dtype=torch.bfloat16,
+                          device=A.device)
+    kernels().skinny_gemm(A, W, out, residual, 2 if swiglu else (1 if residual is not None else 0))
+    return out
+
+
+def skinny_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
+    return 0 < M <= 64 and K % 2048 == 0 and N % (64 if swiglu else 16) == 0
+
+
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
            gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0) -> torch.Tensor:

@@ -9,8 +9,10 @@ Backends computing ``A . W^T`` for the dense projections:
   two whole rounds of 256 CUs, where 256 x 256 tiles leave half of the second round idle);
 * ``g4p``    — gemm4w 256 x 256 with the VAR 64 schedule: each persistent workgroup prefetches its next
   tile's first two K tiles under the current tile's (wave-local) epilogue — multi-round shapes with few
-  K tiles per output tile (the encoders' K = 768 / 1024 projections, mixed-prefill gate|up).  Not for the
-  plain residual epilogue (its VAR 64 form is the block-staged one: nothing to gain).
+  K tiles per output tile (the encoders' K = 768 / 1024 projections, mixed-prefill gate|up); its epilogues
+  run on the transposed accumulator layout (``profiles/gemm4w_stamps_r5.md``).
+* ``gv``     — the skinny weight-stream GEMM for decode-sized row counts (M <= 64; plain, residual and
+  SwiGLU epilogues; ``csrc/kernels/skinny.hip``): the serving path's small decode steps.
 
 The hand-written cores also fuse the SwiGLU of the gate|up projection, or the residual add of the o /
 down projections (:func:`linear_add_`), into their epilogue.  None wins everywhere
@@ -27,12 +29,14 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import gemm4w, gemm8p, silu_mul
+from . import gemm4w, gemm8p, silu_mul, skinny_gemm, skinny_ok
 
 MODE = os.environ.get("LWC_GEMM", "auto")
-BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p")
+BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p", "gv")
 # a hand-written core is chosen unless the library is faster by more than this fraction
 OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "0.01"))
+# LWC_GEMM_SKINNY=0 leaves the skinny decode GEMM out of the timing (A/B knob)
+SKINNY = os.environ.get("LWC_GEMM_SKINNY", "1") != "0"
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
 TIMINGS: Dict[Tuple[int, int, int, str], Dict[str, float]] = {}
 
@@ -65,12 +69,16 @@ def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
     """Whether hand-written backend ``b`` takes this call (layout and the cores' shape rules)."""
     if b == "blas" or not _g8_ok(N, K, epi) or x.stride(1) != 1:
         return False
-    return not ((b == "g4n192" and epi == "swiglu") or (b == "g4p" and epi == "residual"))
+    if b == "gv":
+        return SKINNY and skinny_ok(x.shape[0], N, K, swiglu=epi == "swiglu")
+    return not (b == "g4n192" and epi == "swiglu")
 
 
 def _own(b: str, x: torch.Tensor, w: torch.Tensor, ws=None, **kw) -> torch.Tensor:
     if b == "g8":
         return gemm8p(x, w, ws=ws, **kw)
+    if b == "gv":
+        return skinny_gemm(x, w, **kw)
     return gemm4w(x, w, bn=192 if b == "g4n192" else 256, var=64 if b == "g4p" else 0, **kw)
 
 

@@ -514,6 +514,47 @@ def encoder_gemms(dev):
         del x, w
 
 
+def skinny_ab(dev):
+    """Decode-sized projections (serving decode buckets): hipBLASLt vs the skinny weight-stream GEMM
+    (skinny.hip) for Llama-3-8B's projections, plain and residual, median of 5 interleaved rounds; TB/s = W
+    bytes / time."""
+    import torch.nn.functional as F
+
+    from llm_weighted_consensus_amd import ops
+
+    shapes = [(6144, 4096, False), (4096, 4096, True), (28672, 4096, False), (4096, 14336, True),
+              (128256, 4096, False)]  # (28672: gate|up with SwiGLU)
+    for M in [int(m) for m in os.environ.get("SKINNY_M", "2,8,16,32,64").split(",")]:
+        for N, K, res in shapes:
+            x = ((torch.rand(M, K, device=dev) * 2 - 1)).to(torch.bfloat16)
+            # rotate over enough weight copies to exceed the 256 MB last-level cache (a decode step streams
+            # 32 layers of different weights)
+            nw = max(1, min(16, (768 << 20) // (N * K * 2)))
+            ws = [((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16) for _ in range(nw)]
+            it = [0]
+
+            def nxt():
+                it[0] = (it[0] + 1) % nw
+                return ws[it[0]]
+            acc = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+            if res:
+                runs = {"blas": lambda: acc.addmm_(x, nxt().t()),
+                        "gv": lambda: ops.skinny_gemm(x, nxt(), residual=acc, out=acc)}
+            elif N == 28672:  # gate|up: library + silu_mul vs the skinny SwiGLU epilogue
+                runs = {"blas": lambda: ops.silu_mul(F.linear(x, nxt()), block=32),
+                        "gv": lambda: ops.skinny_gemm(x, nxt(), swiglu=True)}
+            else:
+                runs = {"blas": lambda: F.linear(x, nxt()), "gv": lambda: ops.skinny_gemm(x, nxt())}
+            t = {k: [] for k in runs}
+            for _ in range(5):
+                for k, fn in runs.items():
+                    t[k].append(timeit(fn, iters=20, warm=3))
+            gb = N * K * 2 / 1e12
+            line = "  ".join(f"{k} {sorted(v)[2]:7.1f} us ({gb / sorted(v)[2] * 1e6:4.1f} TB/s)" for k, v in t.items())
+            print(f"skinny M={M} {N}x{K}{' res' if res else ''}: {line}", flush=True)
+            del x, ws, acc
+
+
 def serve_shapes(dev):
     """Llama-3-8B projections at the serving path's mixed chunked-prefill row counts (2048 prompt rows + the
     decode rows): every backend the planner times, median of 5 interleaved rounds (SERVE_M overrides)."""
@@ -682,6 +723,8 @@ def main():
         encoder_gemms(dev)
     if "serve" in a.what:
         serve_shapes(dev)
+    if "skinny" in a.what:
+        skinny_ab(dev)
     if "g48" in a.what:
         g48_ab(dev)
     if "g8ab" in a.what:

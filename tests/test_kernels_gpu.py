@@ -1417,6 +1417,50 @@ def test_gemm4w8_dense_matches_fp32(gpu, M, N, K):
         assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
 
 
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1040, 2048)])
+@pytest.mark.parametrize("res", [False, True])
+def test_skinny_gemm_matches_fp32(gpu, M, N, K, res):
+    """Decode-sized weight-stream GEMM (skinny.hip): every m-tile count (1 / 2 / 4 with ragged rows), the
+    headline projections' N and K, a 65-workgroup N, plain and in-place residual epilogues vs fp32."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M * 7 + N + K + res)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    if res:
+        R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+        want = ref + R.float()
+        out = ops.skinny_gemm(A, W, residual=R, out=R)
+        assert out.data_ptr() == R.data_ptr()
+    else:
+        want = ref
+        out = ops.skinny_gemm(A, W)
+    _close(out, want, 3e-2, 1e-2)
+    # a view of rows (lda > K) takes the same path
+    if not res and M > 1:
+        big = torch.randn(M, K + 64, device=gpu).to(torch.bfloat16)
+        _close(ops.skinny_gemm(big[:, :K], W), big[:, :K].float() @ W.float().t(), 3e-2, 1e-2)
+
+
+
+@pytest.mark.parametrize("M", [1, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(28672, 4096), (1024, 2048)])
+def test_skinny_gemm_swiglu_matches_fp32(gpu, M, N, K):
+    """The skinny GEMM's SwiGLU epilogue over a 32-row gate/up interleaved W (each workgroup's gate and up
+    tiles on the same activation fragments) vs fp32 silu(x Wg^T) * (x Wu^T)."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    F = N // 2
+    out = ops.skinny_gemm(A, ops.swiglu_interleave(W), swiglu=True)
+    assert out.shape == (M, F)
+    _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
+
 def test_gemm4w_row_blocks_past_2gib(gpu):
     """gemm4w addresses A through one 32-bit buffer range; ops.gemm4w runs an A of 2 GiB or more (the encoders'
     FFN2 input at config 2's 0.5 M tokens is 3 GiB) as row blocks: rows on both sides of the block boundary and
