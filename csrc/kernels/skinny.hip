@@ -42,26 +42,29 @@ struct Params {
   int M, N, K, lda, ldc;
 };
 
-template <int MT, int EPI>
+// NW weight tiles of 16 rows per workgroup, on the same activation fragments: EPI 2 (SwiGLU, W = [gate; up]
+// interleaved in blocks of 32 rows, ops.swiglu_interleave) takes its 16 output columns' gate rows 64 (x / 2) +
+// 16 (x % 2) + [0, 16) and the up rows 32 further (NW = 2); the plain / residual forms take 16 (NW = 1) or 32
+// adjacent output columns (NW = 2: half the workgroups, so half the activation re-reads from L2 — past 16
+// rows those loads, M / 16 times the weight bytes, are what limits the NW = 1 form)
+template <int MT, int EPI, int NW>
 __global__ void __launch_bounds__(512) skinny_kernel(Params p) {
   constexpr int U = 4;  // k-steps per load batch: nb = K / 1024 batches, even for K % 2048 == 0
-  // EPI 2 (SwiGLU, W = [gate; up] interleaved in blocks of 32 rows, ops.swiglu_interleave): the workgroup's
-  // output columns 16 x .. 16 x + 15 need gate rows 64 (x / 2) + 16 (x % 2) + [0, 16) and the up rows 32
-  // further; each wave runs both tiles on the same activation fragments (NW = 2 weight tiles)
-  constexpr int NW = EPI == 2 ? 2 : 1;
+  static_assert(EPI != 2 || NW == 2, "SwiGLU pairs a gate and an up tile");
+  constexpr int TS = EPI == 2 ? 32 : 16;  // W rows between the NW tiles
   __shared__ float4v red[KS][NW][MT][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16;  // output columns
-  const int wrow = EPI == 2 ? 64 * (blockIdx.x >> 1) + 16 * (blockIdx.x & 1) : n0;  // first W row (gate)
+  const int n0 = blockIdx.x * (EPI == 2 ? 16 : 16 * NW);  // first output column
+  const int wrow = EPI == 2 ? 64 * (blockIdx.x >> 1) + 16 * (blockIdx.x & 1) : n0;  // first W row
   const int Kw = p.K / KS;          // this wave's K range [w Kw, (w + 1) Kw)
   const int nb = Kw / (32 * U);     // load batches
-  const __amdgpu_buffer_rsrc_t rW = uniform_rsrc(p.W + (size_t)wrow * p.K, (EPI == 2 ? 48 : 16) * p.K * 2);
+  const __amdgpu_buffer_rsrc_t rW = uniform_rsrc(p.W + (size_t)wrow * p.K, (16 + TS * (NW - 1)) * p.K * 2);
   const __amdgpu_buffer_rsrc_t rA = uniform_rsrc(p.A, p.M * p.lda * 2);
   uint32_t voW[NW];
 #pragma unroll
-  for (int t = 0; t < NW; ++t) voW[t] = (uint32_t)(((r16 + 32 * t) * p.K + w * Kw + 8 * g) * 2);
+  for (int t = 0; t < NW; ++t) voW[t] = (uint32_t)(((r16 + TS * t) * p.K + w * Kw + 8 * g) * 2);
   uint32_t voA[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) voA[mt] = (uint32_t)(((mt * 16 + r16) * p.lda + w * Kw + 8 * g) * 2);
@@ -118,47 +121,65 @@ __global__ void __launch_bounds__(512) skinny_kernel(Params p) {
     for (int mt = 0; mt < MT; ++mt) red[w][t][mt][lane] = acc[t][mt];
   __syncthreads();
   if (w < MT) {  // wave w finishes m-tile w: the 8 partials in wave order
-    float4v s = red[0][0][w][lane];
+    float4v sum[NW];
 #pragma unroll
-    for (int k = 1; k < KS; ++k) s += red[k][0][w][lane];
+    for (int t = 0; t < NW; ++t) {
+      sum[t] = red[0][t][w][lane];
+#pragma unroll
+      for (int k = 1; k < KS; ++k) sum[t] += red[k][t][w][lane];
+    }
+    constexpr int NO = EPI == 2 ? 1 : NW;  // 16-column output groups
     if constexpr (EPI == 2) {
-      float4v u = red[0][1][w][lane];
 #pragma unroll
-      for (int k = 1; k < KS; ++k) u += red[k][1][w][lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] = s[e] * __builtin_amdgcn_rcpf(1.f + __expf(-s[e])) * u[e];
+      for (int e = 0; e < 4; ++e) sum[0][e] = sum[0][e] * __builtin_amdgcn_rcpf(1.f + __expf(-sum[0][e])) * sum[1][e];
     }
     const int m = w * 16 + r16;
     if (m < p.M) {
-      const size_t off = (size_t)m * p.ldc + n0 + 4 * g;
-      float v[4] = {s[0], s[1], s[2], s[3]};
-      if constexpr (EPI == 1) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(p.R + off);
-        v[0] += __uint_as_float(rr.x << 16);
-        v[1] += __uint_as_float(rr.x & 0xffff0000u);
-        v[2] += __uint_as_float(rr.y << 16);
-        v[3] += __uint_as_float(rr.y & 0xffff0000u);
+#pragma unroll
+      for (int t = 0; t < NO; ++t) {
+        const size_t off = (size_t)m * p.ldc + n0 + 16 * t + 4 * g;
+        float v[4] = {sum[t][0], sum[t][1], sum[t][2], sum[t][3]};
+        if constexpr (EPI == 1) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(p.R + off);
+          v[0] += __uint_as_float(rr.x << 16);
+          v[1] += __uint_as_float(rr.x & 0xffff0000u);
+          v[2] += __uint_as_float(rr.y << 16);
+          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+        }
+        uint2 o;
+        o.x = pack_bf16x2(v[0], v[1]);
+        o.y = pack_bf16x2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(p.C + off) = o;
       }
-      uint2 o;
-      o.x = pack_bf16x2(v[0], v[1]);
-      o.y = pack_bf16x2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(p.C + off) = o;
     }
   }
 }
 
-template <int EPI>
-int launch(const Params& p, hipStream_t s) {
+template <int EPI, int NW>
+int launch_nw(const Params& p, hipStream_t s) {
   const int mt = (p.M + 15) / 16;
-  const dim3 grid(EPI == 2 ? p.N / 32 : p.N / 16);  // SwiGLU: N / 2 output columns
+  const dim3 grid(EPI == 2 ? p.N / 32 : p.N / (16 * NW));  // SwiGLU: N / 2 output columns, 16 per workgroup
   switch (mt) {
-    case 1: skinny_kernel<1, EPI><<<grid, 512, 0, s>>>(p); break;
-    case 2: skinny_kernel<2, EPI><<<grid, 512, 0, s>>>(p); break;
+    case 1: skinny_kernel<1, EPI, NW><<<grid, 512, 0, s>>>(p); break;
+    case 2: skinny_kernel<2, EPI, NW><<<grid, 512, 0, s>>>(p); break;
     case 3:
-    case 4: skinny_kernel<4, EPI><<<grid, 512, 0, s>>>(p); break;
+    case 4: skinny_kernel<4, EPI, NW><<<grid, 512, 0, s>>>(p); break;
     default: return -1;
   }
   return (int)hipGetLastError();
+}
+
+// plain / residual: 32 output columns per workgroup past 16 rows when that still leaves >= 192 workgroups
+// (M / 16 activation re-reads halved: qkv at M = 32 23.9 -> 17.9 us), else 16 (o, N = 4096: 128 workgroups
+// of 32 columns ran 17.6 us against 13.8 with 256 of 16 — too little of the weight stream in flight)
+template <int EPI>
+int launch(const Params& p, hipStream_t s) {
+  if constexpr (EPI == 2) {
+    return launch_nw<2, 2>(p, s);
+  } else {
+    if (p.M > 16 && p.N % 32 == 0 && p.N / 32 >= 192) return launch_nw<EPI, 2>(p, s);
+    return launch_nw<EPI, 1>(p, s);
+  }
 }
 
 }  // namespace skinny
