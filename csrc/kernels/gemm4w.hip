@@ -111,6 +111,7 @@ LWC_DEVICE void mfma2(float4v& d, const uint4v& a, const uint4v& b) {
 #define G4_BAR() __builtin_amdgcn_s_barrier()
 #define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 #define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
 // Diagnostic build only (scripts/probes/g4_stamps.cpp defines LWC_G4_STAMPS): wave 0 of every workgroup
 // records s_memrealtime at up to eight points of each persistent round (and s_memtime at the first and last)
 // into g4_stamps[block][round][8] with vector stores (points: scripts/probes/g4_stamps.cpp); the product build has no stamp code at all.
@@ -227,6 +228,28 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
       for (int k = 0; k < G::Pieces; ++k) piece(buf, kt, k);
     };
+    // VAR 64 / 96: the next persistent tile (its first two K tiles are DMA'd inside the last two main-loop
+    // iterations of this one).  Past the last tile the pieces re-read this tile's first two K tiles into
+    // the freed buffers instead: every piece a real memory request — pieces past a resource's end complete
+    // out of order with the real ones before them, and a counted vmcnt wait then passes too early
+    // (measured: wrong results at every K tile count past 2)
+    const int ntile = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
+    const bool pf = PAP && ntile < p.tiles;
+    int um = tm, un = tn;
+    if (pf) tile_mn(p, ntile, um, un);
+    const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.W + (size_t)un * G::BN * p.K), (short)0, min(p.N - un * G::BN, G::BN) * p.K * 2, 0x00020000);
+    auto npiece = [&](uint8_t* buf, int kt, int k) {  // piece k of the NEXT tile's K tile kt
+      if (k < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            nA, (__attribute__((address_space(3))) void*)(buf + k * 4096 + dst0), 16, voA, k * sA + kt * 128, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            nW, (__attribute__((address_space(3))) void*)(buf + kOpA + (k - 8) * 4096 + dst0), 16, voW,
+            (k - 8) * sW + kt * 128, 0, 0);
+    };
     // fragment reads: m-tile / n-tile i adds i * 16 rows = i * 2048 B; the swizzle only depends on r16
     const int sw = (r16 >> 1) & 7;
     const int offA0 = (wm * 128 + r16) * 128 + ((q ^ sw) << 4);
@@ -248,6 +271,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         fa[k - NT] = *reinterpret_cast<const uint4v*>(buf + oa + (k - NT) * 2048);
     };
 
+    // (VAR 64 / 96 take even K tile counts only — the host falls back to VAR 32 — so the next tile's first
+    // two K tiles, DMA'd inside the last two iterations, land in buffers 0 and 1)
     const int nt = KT;
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
@@ -376,10 +401,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }                                                                                               \
     G4_LGKM0();                                                                                     \
     G4_BAR();                                                                                       \
-    if constexpr (STAGE) __builtin_amdgcn_s_setprio(3);                                             \
+    if constexpr ((STAGE) != 0) __builtin_amdgcn_s_setprio(3);                                      \
     _Pragma("unroll") for (int q = 0; q < HB; ++q) {                                                \
-      if constexpr (STAGE) {                                                                        \
+      if constexpr ((STAGE) == 1) {                                                                 \
         if (q * G::Pieces / HB != (q + 1) * G::Pieces / HB) piece(cur, (R) + 2, q * G::Pieces / HB); \
+      } else if constexpr ((STAGE) == 2) {                                                          \
+        if (q * G::Pieces / HB != (q + 1) * G::Pieces / HB) npiece(cur, (R) + 2 - nt, q * G::Pieces / HB); \
       }                                                                                             \
       const int m = HA + q;                                                                         \
       if (m < M1)                                                                                   \
@@ -388,7 +415,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         mfma2<TRL>(acc[(m - M1) / NT][(m - M1) % NT], ya[(m - M1) / NT], yb[(m - M1) % NT]);              \
       __builtin_amdgcn_sched_barrier(0);                                                            \
     }                                                                                               \
-    if constexpr (STAGE) {                                                                          \
+    if constexpr ((STAGE) != 0) {                                                                   \
       __builtin_amdgcn_s_setprio(0);                                                                \
       G4_VM(G::Pieces);                                                                             \
     } else {                                                                                        \
@@ -406,12 +433,18 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   }
     int r = 0;
     if constexpr (VAR == 32 || VAR == 64 || VAR == 96) {
-      for (; r + 2 < nt; ++r) G4_TILE_H(r, true, true)
+      // VAR 64 / 96 (TAIL 2): the last two K tiles carry the NEXT tile's first two (into the buffers they
+      // free: buffer 0, then 1, as the prologue's stage(0) / stage(1) — KT is even for these variants): seg B
+      // pieces as in the steady state, no DMA burst left for the epilogue.  (The same control flow as the
+      // other variants' tail: a differently shaped tail made the register allocator rotate the accumulators
+      // through v_accvgpr_mov copies that read in-flight inline-asm MFMA results.)
+      constexpr int TAIL = PAP ? 2 : 0;
+      for (; r + 2 < nt; ++r) G4_TILE_H(r, 1, true)
       if (nt >= 2) {
-        G4_TILE_H(r, false, true)
+        G4_TILE_H(r, TAIL, true)
         ++r;
       }
-      G4_TILE_H(r, false, false)
+      G4_TILE_H(r, TAIL, false)
     } else if constexpr (VAR == 8) {
       for (; r + 2 < nt; ++r) G4_TILE1(r, true, true)
       if (nt >= 2) {
@@ -502,32 +535,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
           for (int g2 = 0; g2 < NT / 2; ++g2)
             rv[i][g2] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, tr_vo[g2], tr_so(i), 0));
-      }
-      // ---- the next tile's first two K tiles into the (now free) K buffers, in flight under this epilogue
-      const int ntile = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
-      if (ntile < p.tiles) {
-        int um, un;
-        tile_mn(p, ntile, um, un);
-
-        const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
-        const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p.W + (size_t)un * G::BN * p.K), (short)0, min(p.N - un * G::BN, G::BN) * p.K * 2, 0x00020000);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          if (kt == 1 && nt < 2) break;
-#pragma unroll
-          for (int k = 0; k < G::Pieces; ++k) {
-            uint8_t* buf = smem + kt * G::Buf;
-            if (k < 8)
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                  nA, (__attribute__((address_space(3))) void*)(buf + k * 4096 + dst0), 16, voA, k * sA + kt * 128, 0, 0);
-            else
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                  nW, (__attribute__((address_space(3))) void*)(buf + kOpA + (k - 8) * 4096 + dst0), 16, voW,
-                  (k - 8) * sW + kt * 128, 0, 0);
-          }
-        }
       }
       G4_STAMP(round, 3);
       if constexpr (TRR) {
@@ -852,6 +859,9 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }
     G4_STAMP(round, 7);
   }
+  // (VAR 64 / 96: the last tile's loop issued pieces nothing waited for; retire them before the
+  // workgroup's LDS is released)
+  if constexpr (PAP) G4_VM(0);
 }
 
 template <int EPI, int NT, int VAR, int RS>
@@ -877,6 +887,8 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
   // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants; 96 = 64 with the staged epilogue image instead of TR (and erf GELU; A/B only).
   // rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sum-of-squares (see the file head)
   if (var <= 0) var = env_int("LWC_G4_VAR", 32);
+  // VAR 64 / 96 DMA the next tile's first two K tiles inside the last two iterations: even K tile counts
+  if ((var == 64 || var == 96) && (p.KT & 1)) var = 32;
   if (rs == 1) {
     // (VAR 64 + RS 1 ran out of VGPRs in the wave-local epilogue: 256 + scratch; the row-scaled
     // consumers take the block-staged epilogue)

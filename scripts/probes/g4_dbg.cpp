@@ -1,4 +1,5 @@
-// Debug harness: gemm4w at var 64 on small shapes vs a CPU fp32 reference (built with -D switches).
+// Debug harness: gemm4w at var 32 / 64 on small shapes vs a CPU fp32 reference (build against any gemm4w.hip
+// with -I <dir>: scripts/probes/g4_dbg.cpp -> g4_dbg_*).
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstring>
