@@ -96,7 +96,21 @@ def build_kernels(jobs: int = 8, force: bool = False) -> Path:
         _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(KERNELS_SO),
               *tlibs])
         _check_kernel_stubs(KERNELS_SO)
+        _check_isa(hip_srcs, obj_dir)
     return KERNELS_SO
+
+
+def _check_isa(srcs: list[Path], obj_dir: Path) -> None:
+    """Fail the build when a kernel with inline-asm MFMAs (gemm4w) moves, reads or overwrites an accumulator
+    before the MFMA writing it has retired (llm_weighted_consensus_amd/_isa_guard.py): the compiler cannot see
+    the asm's latency, and such code computes wrong results without any diagnostic."""
+    from . import _isa_guard
+
+    bad = _isa_guard.check_objects((src, obj_dir / (src.stem + ".o")) for src in srcs)
+    if bad:
+        KERNELS_SO.unlink(missing_ok=True)
+        raise RuntimeError(f"ISA guard: {len(bad)} accumulator hazard(s) in the inline-asm MFMA kernels:\n  "
+                           + "\n  ".join(str(v) for v in bad[:20]))
 
 
 def _check_kernel_stubs(so: Path) -> None:

@@ -103,7 +103,8 @@ def build_embedding_service(name: str, spec: dict, dev) -> "EmbeddingService":
         dcfg = decoder_config(spec["arch"])
         mtok = int(spec.get("max_tokens", 4096))
         enc = DecoderEmbedder(LlamaModel(dcfg, device=dev, seed=seed, weights_path=path, max_position=mtok + 64,
-                                         fp8_dense=bool(spec.get("fp8", False))), max_tokens=mtok)
+                                         fp8_dense=bool(spec.get("fp8", False)), fold_norms=False),
+                              max_tokens=mtok)
     else:
         enc = BertEncoder(encoder_config(spec["arch"]), device=dev, seed=seed, weights_path=path,
                           dtype=torch.float32 if dev.type == "cpu" else torch.bfloat16)

@@ -498,7 +498,12 @@ class EngineGroup:
                 rid, msg = payload[:2]
                 fkind = payload[2] if len(payload) > 2 else "error"
                 with self._lock:
-                    req = self.requests.pop(rid, None)
+                    req = self.requests.get(rid)
+                    # only a worker that still owns an unfinished portion of the request may fail it
+                    if req is not None and any(p.worker == wid and p.finished < p.n for p in req.portions):
+                        self.requests.pop(rid, None)
+                    else:
+                        req = None
                 if req is not None:
                     if fkind != "deadline":
                         self.failures += 1
@@ -539,11 +544,14 @@ class EngineGroup:
                 if req is None:
                     continue
                 p = next((p for p in req.portions if p.worker == wid and p.offset <= idx < p.offset + p.n), None)
-                if p is not None:
-                    p.emitted += 1
-                    if fin:
-                        p.finished += 1
-                        self.load_of[wid] -= 1
+                if p is None:
+                    # no portion of this worker holds the row any more: a slot declared dead (its portions moved
+                    # to a survivor) whose process still pushed records before it was killed
+                    continue
+                p.emitted += 1
+                if fin:
+                    p.finished += 1
+                    self.load_of[wid] -= 1
                 per_loop.setdefault(req.loop, []).append((req.queue, GroupTokenEvent(idx, tid, text, lp, top, fin,
                                                                                      reason)))
                 if all(pp.finished == pp.n for pp in req.portions):
@@ -615,12 +623,19 @@ class EngineGroup:
                 return
             self.alive[w] = False
             self.ready[w] = False
+            # fence the slot at once: a process declared dead for a heartbeat timeout may still be running, and
+            # its late 'error' / deadline messages must not match the slot's generation while its portions are
+            # moved to survivors (the reader drops messages of an older generation); _respawn bumps it again
+            # for the replacement
+            self.gen[w] += 1
         self.failures += 1
         self.load_of[w] = 0
-        for fp, _ in self.followers[w]:  # a TP replica is one unit: its other ranks cannot go on alone
+        # every process of the dead unit is killed here, not only after the respawn backoff (a TP replica is one
+        # unit: its other ranks cannot go on alone; a hung tp=1 worker must not come back to life)
+        for fp, _ in self.followers[w]:
             if fp.is_alive():
                 fp.kill()
-        if self.followers[w] and self.procs[w].is_alive():
+        if self.procs[w] is not None and self.procs[w].is_alive():
             self.procs[w].kill()
         live = self.live_workers()
         with self._lock:

@@ -106,7 +106,8 @@ class _NullCache:
 
 class LlamaModel:
     def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
-                 weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8_dense: bool = False):
+                 weights_path: Optional[str] = None, max_position: Optional[int] = None, fp8_dense: bool = False,
+                 fold_norms: bool = True):
         if cfg.num_experts and type(self) is LlamaModel:
             raise NotImplementedError("MoE decoders use models.mixtral.MixtralModel")
         self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
@@ -141,15 +142,22 @@ class LlamaModel:
             blas_tuning.enable()  # offline-tuned hipBLASLt / rocBLAS solutions for the library GEMMs
         # folded RMSNorm (module docstring): the plain dense bf16 decoder on the GPU
         self.norm_folded = False
+        self.extra_bytes = 0  # device bytes the folded norms add (a tied lm_head's own copy)
+        self.final_norm_weight: Optional[torch.Tensor] = None  # the final norm's weight once lm_head holds it
         self.chain: Optional[ops.NormChain] = None
         self.chain_m: dict = {}  # decode batch M -> (use the chain, qkv tile width)
-        if (self.device.type == "cuda" and not self.fp8_dense and type(self) is LlamaModel
+        # ``fold_norms=False``: models that never decode through lm_head (the decoder-as-embedder) skip it
+        if (fold_norms and self.device.type == "cuda" and not self.fp8_dense and type(self) is LlamaModel
                 and os.environ.get("LWC_NORM_FOLD", "1") != "0" and isinstance(self.layers[0], LayerWeights)):
             self._fold_norms()
 
     def _fold_norms(self) -> None:
         """W diag(g) for every projection that reads a normalised row, then g = 1 (the unfolded path computes the
-        same function).  One bf16 rounding of each folded weight (exact for the random-init unit norm weights)."""
+        same function).  One bf16 rounding of each folded weight (exact for the random-init unit norm weights).
+
+        The final norm's weight is folded into lm_head only; :meth:`encode` (hidden states, no lm_head) keeps
+        applying it (``final_norm_weight``).  A tied lm_head becomes its own vocab x hidden copy (W_emb diag(g)):
+        ~1 GB more at Llama-3-8B shapes, reported by ``extra_bytes``."""
         def fold(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
             out = torch.empty_like(w)
             gf = g.float()
@@ -160,7 +168,10 @@ class LlamaModel:
         for L in self.layers:
             L.wqkv, L.attn_norm = fold(L.wqkv, L.attn_norm), torch.ones_like(L.attn_norm)
             L.w_gate_up, L.mlp_norm = fold(L.w_gate_up, L.mlp_norm), torch.ones_like(L.mlp_norm)
+        tied = self.lm_head is self.embed
         self.lm_head = fold(self.lm_head, self.final_norm)  # (a tied embedding table keeps its own copy)
+        self.extra_bytes = self.lm_head.numel() * self.lm_head.element_size() if tied else 0
+        self.final_norm_weight = self.final_norm  # what encode() applies
         self.final_norm = torch.ones_like(self.final_norm)
         self.norm_folded = True
         torch.cuda.empty_cache()
@@ -272,13 +283,14 @@ class LlamaModel:
         return bool(c and (c["attn"] or c["mlp"] or c["final"])) and self.chain is not None and M <= self.chain.max_rows
 
     def _layers(self, x_res: torch.Tensor, cache: KVCache, positions, slots, attn_fn, rope_q: bool = True,
-                keep: Optional[torch.Tensor] = None) -> torch.Tensor:
+                keep: Optional[torch.Tensor] = None, final_norm: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Runs every layer; x_res is the residual stream (updated in place); returns the final
         normalised hidden state.  ``rope_q=False``: q leaves the qkv projection un-rotated and ``attn_fn``
         rotates it (the decode kernels' load-time RoPE).  ``keep`` (row indices): only those rows' final
         states are wanted (a prefill's last tokens, an embedder's pooled token) — the last layer still runs
         qkv / RoPE / the cache write / attention over every row (later tokens' keys and values), then its
-        o projection, MLP and the final norm over the kept rows only; returns [len(keep), d]."""
+        o projection, MLP and the final norm over the kept rows only; returns [len(keep), d].  ``final_norm``:
+        the weight of the last norm (default ``self.final_norm``; ones once it is folded into lm_head)."""
         cfg = self.cfg
         T = x_res.shape[0]
         Hq, Hkv, D = cfg.heads, cfg.kv_heads, cfg.head_dim
@@ -304,7 +316,8 @@ class LlamaModel:
                     attn.reshape(T, Hq * D).index_select(0, keep)
                 x_res = x_res.index_select(0, keep)
                 T = x_res.shape[0]
-            nxt = self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else self.final_norm
+            nxt = (self.layers[li + 1].attn_norm if li + 1 < len(self.layers) else
+                   self.final_norm if final_norm is None else final_norm)
             if fused:
                 gemm_plan.linear_add_(attn.view(T, Hq * D), L.wo, x_res, ws=self.g8_ws)
                 h = ops.rmsnorm(x_res, L.mlp_norm, cfg.rms_eps)
@@ -541,7 +554,10 @@ class LlamaModel:
                 return ops.prefill_attention_mx(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, self.scale, causal=True)
             return ops.prefill_attention(q, k, v, cu_seqlens, max_seqlen, Hq, Hkv, D, self.scale, causal=True)
 
-        return self._layers(x, null, positions, None, attn_fn, keep=keep)
+        # the hidden states themselves are the output: the real final norm weight, also when it is folded
+        # into lm_head for decoding
+        return self._layers(x, null, positions, None, attn_fn, keep=keep,
+                            final_norm=self.final_norm_weight)
 
     def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, cu_seqlens: torch.Tensor,
                 max_seqlen: int, last_idx: torch.Tensor, cache: KVCache, ctx: Optional[dict] = None) -> torch.Tensor:

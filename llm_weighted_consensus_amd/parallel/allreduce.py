@@ -94,10 +94,14 @@ class CustomAllReduce:
             self.self_test()
 
     # ------------------------------------------------------------------ start-up self-test
+    def _pg_on_device(self) -> bool:
+        """Whether the process group's collectives take device tensors (RCCL) rather than host ones (gloo)."""
+        return dist.get_backend(self.group) == "nccl"
+
     def _gather_ref(self, x: torch.Tensor) -> List[torch.Tensor]:
-        """Every rank's ``x`` through the process group (host copies; any backend)."""
-        nccl = dist.get_backend(self.group) == "nccl"
-        src = x if nccl else x.cpu()
+        """Every rank's ``x`` through the process group (host copies; any backend).  ``x`` is built on the
+        host: RCCL (backend "nccl") takes device tensors only, gloo host tensors."""
+        src = x.to(self.device) if self._pg_on_device() else x.cpu()
         parts = [torch.empty_like(src) for _ in range(self.W)]
         dist.all_gather(parts, src, group=self.group)
         return [p.cpu() for p in parts]

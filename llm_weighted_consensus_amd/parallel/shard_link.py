@@ -362,13 +362,34 @@ class LinkClient:
             pass
 
 
+def link_host() -> str:
+    """The address the leader listens on: ``LWC_SHARD_LINK_HOST`` if set; loopback when every rank runs on this
+    node (WORLD_SIZE == LOCAL_WORLD_SIZE, or no torchrun sizes in the environment); otherwise ``MASTER_ADDR`` — the
+    address the other nodes already reach this node by.  A multi-node world with no usable address fails here
+    instead of leaving remote followers retrying a loopback address until the bring-up timeout."""
+    host = os.environ.get("LWC_SHARD_LINK_HOST")
+    if host:
+        return host
+    world = os.environ.get("WORLD_SIZE")
+    local = os.environ.get("LOCAL_WORLD_SIZE")
+    master = os.environ.get("MASTER_ADDR", "")
+    one_node = world is None or local is None or world == local
+    if one_node:
+        return "127.0.0.1"
+    if master in ("", "localhost", "::1") or master.startswith("127."):
+        raise RuntimeError("voter-sharded links span several nodes (WORLD_SIZE %s > LOCAL_WORLD_SIZE %s) but "
+                           "MASTER_ADDR is %r: set LWC_SHARD_LINK_HOST to this node's address reachable from "
+                           "the other nodes" % (world, local, master))
+    return master
+
+
 def open_links(group=None, hb_s: Optional[float] = None, dead_s: Optional[float] = None):
     """Bring-up (a collective over ``group``, once): rank 0 returns a :class:`LinkServer` with every follower
     connected, the others a :class:`LinkClient`.  Environment: ``LWC_SHARD_HB_S`` (heartbeat period, default
     0.5 s), ``LWC_SHARD_DEAD_S`` (silence after which a follower counts as dead, default 10 s),
-    ``LWC_SHARD_LINK_HOST`` (the interface the leader listens on and the followers reach; default loopback —
-    one node), ``LWC_SHARD_LINK_FILE`` (where the leader writes its address + secret for re-joining
-    followers)."""
+    ``LWC_SHARD_LINK_HOST`` (the interface the leader listens on and the followers reach; default: loopback
+    when every rank is on this node, else ``MASTER_ADDR`` — :func:`link_host`), ``LWC_SHARD_LINK_FILE``
+    (where the leader writes its address + secret for re-joining followers)."""
     import torch.distributed as dist
 
     from .dist import broadcast_object
@@ -377,7 +398,7 @@ def open_links(group=None, hb_s: Optional[float] = None, dead_s: Optional[float]
     dead = float(os.environ.get("LWC_SHARD_DEAD_S", "10")) if dead_s is None else dead_s
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     if rank == 0:
-        host = os.environ.get("LWC_SHARD_LINK_HOST", "127.0.0.1")
+        host = link_host()
         srv = LinkServer(world, host, hb, dead)
         join_file = os.environ.get("LWC_SHARD_LINK_FILE")
         if join_file:

@@ -15,6 +15,8 @@ STATS=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
 # GPU idle gaps (host stalls) over the whole run, before the trace is dropped
 TRACE=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
 [ -n "$TRACE" ] && python3 scripts/trace_gaps.py "$TRACE" ${GAP_MS:-0.2} > gpurun_out/prof_gaps.txt
+# per call site (kernel, predecessor): separates the library's o / down / lm_head calls
+[ -n "$TRACE" ] && python3 scripts/trace_shapes.py "$TRACE" 40 > gpurun_out/prof_shapes.md
 # keep the stats, drop the multi-MB per-dispatch trace (gpurun copies back <= 64 MiB)
 find gpurun_out/prof -name "*kernel_trace.csv" -delete
 exit $rc

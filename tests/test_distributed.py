@@ -317,3 +317,30 @@ def test_self_launch_spawns_ranks(tmp_path):
     with pytest.raises(SystemExit):
         launch.check_world(8, 1)
     launch.check_world(2, 2)
+
+
+def test_allreduce_selftest_gathers_device_tensors_on_rccl(monkeypatch):
+    """CustomAllReduce's start-up self-test builds its input on the host; on an RCCL process group (backend
+    "nccl") the all-gather must be handed a tensor on the communicator's device, on gloo a host tensor
+    (the NCCL branch passed the host tensor and raised on every multi-GPU bring-up).  No GPU: the
+    collective is replaced by a recorder and the device by "meta"."""
+    import torch
+    import torch.distributed as dist
+
+    from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
+
+    seen = []
+
+    def fake_all_gather(parts, src, group=None):
+        seen.append(src.device.type)
+        parts[:] = [torch.zeros(src.shape, dtype=src.dtype) for _ in parts]
+
+    ar = CustomAllReduce.__new__(CustomAllReduce)
+    ar.group, ar.W, ar.device = None, 2, torch.device("meta")
+    monkeypatch.setattr(dist, "all_gather", fake_all_gather)
+    x = torch.ones(16, dtype=torch.bfloat16)
+    for backend, want in (("nccl", "meta"), ("gloo", "cpu")):
+        monkeypatch.setattr(dist, "get_backend", lambda group=None, b=backend: b)
+        seen.clear()
+        out = ar._gather_ref(x)
+        assert seen == [want] and len(out) == 2 and all(p.device.type == "cpu" for p in out)

@@ -178,7 +178,8 @@ def test_dead_worker_is_respawned_and_serves_again():
         t0 = time.time()
         assert _wait_live(g, 2) == [0, 1]
         assert time.time() - t0 < 60
-        assert g.procs[0].pid != old_pid and g.gen[0] == 1 and g.respawns[0] == 1
+        # generation: +1 when the slot is fenced at death, +1 for the replacement
+        assert g.procs[0].pid != old_pid and g.gen[0] == 2 and g.respawns[0] == 1
         # the replacement serves: a request split over both workers completes with the usual seeds
         sp = SamplingParams(max_tokens=3, seed=8)
         toks, err = _collect(g, 6, sp)
@@ -227,5 +228,26 @@ def test_respawn_is_bounded():
                     time.sleep(0.05)
         time.sleep(1.0)
         assert g.respawns[0] == 2 and not g.alive[0] and g.live_workers() == [1]
+    finally:
+        g.close()
+
+
+def test_worker_declared_dead_is_fenced_and_killed():
+    """A worker declared dead while its process still runs (a heartbeat timeout on a hung, not exited, process)
+    is fenced at once: its slot's generation moves on, so late messages of the old process are dropped by the
+    reader, and the process is killed — also with respawning off, where no replacement ever bumps the
+    generation (a recovering hung worker could fail requests already moved to a survivor)."""
+    g = EngineGroup({"delay": 0.0}, devices=[0, 0], factory=FACTORY, heartbeat_timeout=60, respawn=False)
+    try:
+        victim = g.procs[0]
+        gen0 = g.gen[0]
+        assert victim.is_alive()
+        g._worker_died(0, "heartbeat timeout")
+        assert g.gen[0] == gen0 + 1 and not g.alive[0]
+        victim.join(timeout=30)
+        assert not victim.is_alive()
+        # the survivor still serves every candidate
+        toks, err = _collect(g, 4, SamplingParams(max_tokens=2, seed=3))
+        assert err is None and sorted(toks) == list(range(4))
     finally:
         g.close()

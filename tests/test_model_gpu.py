@@ -337,3 +337,42 @@ def test_folded_norm_chain_matches_unfolded(tiny, gpu, qkv_bn):
     assert _cos(got, base) > 0.9995
     assert (got - base).abs().max() < 0.05 * base.abs().max()
     assert _cos(got[B - 1], ref_logits[P]) > 0.995 and _cos(got[0], ref_logits[P]) > 0.995
+
+
+def test_folded_norms_keep_encode_and_logits_with_real_norm_weights(gpu):
+    """Norm folding with NON-unit norm weights (random init has unit ones, which hide a dropped weight): the
+    folded model's prefill logits and its encode() hidden states (the decoder-as-embedder output, which has
+    no lm_head to carry the final norm weight) equal the unfolded model's."""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import KVCache, LlamaModel
+
+    cfg = decoder_config("llama-tiny")
+    gen = torch.Generator(device="cpu").manual_seed(11)
+
+    def norm():
+        return (0.5 + torch.rand(cfg.hidden, generator=gen)).to(gpu, torch.bfloat16)
+
+    norms = [(norm(), norm()) for _ in range(cfg.layers)]
+    final = norm()
+    models = []
+    for fold in (False, True):
+        m = LlamaModel(cfg, device=gpu, seed=5, max_position=512, fold_norms=False)
+        for L, (na, nm) in zip(m.layers, norms):
+            L.attn_norm, L.mlp_norm = na.clone(), nm.clone()
+        m.final_norm = final.clone()
+        if fold:
+            m._fold_norms()
+            assert m.norm_folded and bool((m.final_norm == 1).all())
+        models.append(m)
+    a, b = models
+    P = 29
+    toks = torch.randint(0, cfg.vocab_size, (P,), generator=gen).to(gpu).int()
+    pos = torch.arange(P, dtype=torch.int32, device=gpu)
+    cu = torch.tensor([0, P], dtype=torch.int32, device=gpu)
+    ea = a.encode(toks, pos, cu, P).float()
+    eb = b.encode(toks, pos, cu, P).float()
+    assert _cos(ea, eb) > 0.9995 and (ea - eb).abs().max() < 0.05 * ea.abs().max()
+    last = torch.tensor([P - 1], device=gpu)
+    la = a.prefill(toks, pos, pos, cu, P, last, KVCache(cfg, 16, 16, gpu)).float()
+    lb = b.prefill(toks, pos, pos, cu, P, last, KVCache(cfg, 16, 16, gpu)).float()
+    assert _cos(la, lb) > 0.9995

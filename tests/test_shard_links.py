@@ -231,3 +231,26 @@ def test_failed_consensus_slice_is_recomputed_locally():
     assert sorted(calls) == [(0, 2), (2, 2)]  # the follower's slice [2, 4) ran on the leader
     assert [c.index for c in out.choices] == [0, 1, 2, 3]
     assert out.rows[2:].eq(2.0).all()
+
+
+def test_link_host_defaults(monkeypatch):
+    """The leader's listen address: loopback for a one-node world, MASTER_ADDR across nodes, an explicit
+    LWC_SHARD_LINK_HOST always; a multi-node world with only a loopback MASTER_ADDR fails fast."""
+    import pytest
+
+    from llm_weighted_consensus_amd.parallel.shard_link import link_host
+
+    for k in ("LWC_SHARD_LINK_HOST", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR"):
+        monkeypatch.delenv(k, raising=False)
+    assert link_host() == "127.0.0.1"
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("MASTER_ADDR", "10.0.0.5")
+    assert link_host() == "127.0.0.1"
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    assert link_host() == "10.0.0.5"
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    with pytest.raises(RuntimeError, match="LWC_SHARD_LINK_HOST"):
+        link_host()
+    monkeypatch.setenv("LWC_SHARD_LINK_HOST", "10.0.0.9")
+    assert link_host() == "10.0.0.9"
