@@ -74,6 +74,10 @@ def main():
     W, rank = info.world, info.rank
     launch.check_world(a.gpus, W)
     dev = torch.device("cuda", info.local_rank)
+    # multi-rank pre-flight (peer access matrix + a checked, timed RCCL all-gather): its result goes into the
+    # JSON so a first multi-GPU number explains itself
+    from llm_weighted_consensus_amd.parallel import preflight
+    pre = preflight.maybe_run(dev)
     N = a.candidates
     R = a.requests or max(1, 4096 // N)
     cp = a.cp or max(1, min(W, N // 32))
@@ -117,7 +121,8 @@ def main():
             # C4: prefill only this rank's R of the group's prompts, all-gather their KV blocks + last
             # logits inside the candidate group (RCCL)
             kv, lg, nbl = engine.export_prefill(prompts[crank * R:(crank + 1) * R])
-            shared = all_gather_prefills(kv, lg, nbl, group=cgroup)
+            with pdist.comm_tag("C4"):
+                shared = all_gather_prefills(kv, lg, nbl, group=cgroup)
         for gi, p in enumerate(prompts):
             sp = SamplingParams(temperature=0.8, top_p=0.95, max_tokens=a.gen_len, ignore_eos=True,
                                 seed=(step_idx * 1000003 + gidx * Rg + gi) * 131 + crank)
@@ -128,7 +133,8 @@ def main():
             engine.step()
         t1 = time.perf_counter()
         cands = [[s.tokens for s in g.seqs] for g in groups]
-        res = scorer.score(cands, gather=cp > 1, group=cgroup, defer=defer)
+        with pdist.comm_tag("C1"):
+            res = scorer.score(cands, gather=cp > 1, group=cgroup, defer=defer)
         if not defer:
             torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
@@ -143,6 +149,7 @@ def main():
     if res is not None:
         res.resolve()
     torch.cuda.synchronize(dev)
+    pdist.comm_report(reset=True)  # count the timed steps' collectives only
     pdist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
@@ -161,6 +168,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     elapsed = pdist.max_over_ranks(elapsed, dev)
+    comm_stats = pdist.comm_report(a.steps) if W > 1 else {}  # C1 / C4 bytes received + ms per step
     # self-check (untimed, after the clock stopped): the last step's first request re-scored from all of its
     # candidates on one device must match what the candidate-parallel path produced (C1 all-gather +
     # consensus); the verdict is a MIN over every rank, and a mismatch fails the run
@@ -172,6 +180,15 @@ def main():
     value = answers / elapsed
     emb_per_s = G * N * a.steps / elapsed
     seen = pdist.world_size_seen()  # collective: ranks that actually took part in an all-reduce
+    # which kernels the decode step ran (the largest decode bucket: the step every request goes through) and
+    # the engine's in-step A/B of whole captured steps behind that choice — on stderr in every run, and in
+    # the JSON record
+    Bdec = max(engine.buckets) if engine.buckets else 0
+    plan = model.plan_summary(Bdec) if Bdec else {}
+    step_ab = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in engine.step_ab.get(Bdec, {}).items()}
+    if rank == 0:
+        print(f"# decode plan at batch {Bdec}: {plan}; step A/B (ms per decode step): {step_ab}", file=sys.stderr,
+              flush=True)
     if a.profile_steps and rank == 0:
         print(f"# generate {gen_t / a.steps * 1e3:.1f} ms/step, score {score_t / a.steps * 1e3:.1f} ms/step, "
               f"decode steps {engine.stats['steps']}", file=sys.stderr)
@@ -198,6 +215,10 @@ def main():
             "embeddings_per_s": round(emb_per_s, 2),
             "verified": verified,
             "generated_tokens_per_s": round(G * N * a.gen_len * a.steps / elapsed, 1),
+            "decode_plan": plan,
+            "preflight": pre,
+            "comm_per_step": comm_stats,
+            "step_ab_ms": step_ab,
             "config": {
                 "model": f"{a.decoder} sampler + {a.encoder} scorer",
                 "global_batch": G,

@@ -80,8 +80,18 @@ def bench_moe(a):
     tp_group, dp_idx, tp_rank = pdist.candidate_groups(tp) if info.world > 1 else (None, 0, 0)
     dev = torch.device("cuda", info.local_rank)
     dcfg = decoder_config(a.decoder)
+    # multi-rank pre-flight (peer access matrix, a checked RCCL all-gather, the IPC self-test when the TP
+    # all-reduce is to run over IPC): a failed peer check runs the TP all-reduce on the process group instead,
+    # with the reason in the JSON
+    from llm_weighted_consensus_amd.parallel import preflight
+    pre = preflight.maybe_run(dev, want_ipc=tp > 1 and a.tp_comm == "ipc")
+    tp_comm = a.tp_comm
+    if pre is not None and pre["ipc_fallback"]:
+        tp_comm = "pg"
+        if info.rank == 0:
+            print(f"# pre-flight: {pre['ipc']} -> TP all-reduce on the process group", file=sys.stderr, flush=True)
     comm = None
-    if tp > 1 and a.tp_comm == "ipc":
+    if tp > 1 and tp_comm == "ipc":
         from llm_weighted_consensus_amd.parallel.allreduce import CustomAllReduce
 
         # C3 over IPC peer buffers: [decode batch, hidden] bf16 per call, inside the captured decode graph
@@ -126,19 +136,22 @@ def bench_moe(a):
             return scorer.score(last[0])
         n_loc = N // tp
         last[0] = [[s.tokens for s in gr.seqs[tp_rank * n_loc:(tp_rank + 1) * n_loc]] for gr in groups]
-        return scorer.score(last[0], gather=True, group=tp_group)
+        with pdist.comm_tag("C1"):
+            return scorer.score(last[0], gather=True, group=tp_group)
 
     last = [None]
 
     for i in range(a.warmup):
         step(i)
     _sync(dev, info.enabled)
+    pdist.comm_report(reset=True)  # count the timed steps' collectives only
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
         res = step(a.warmup + i)
     _sync(dev, info.enabled)
     dt = pdist.max_over_ranks((time.perf_counter() - t0) / a.steps, dev)
+    comm_stats = pdist.comm_report(a.steps) if info.world > 1 else {}
     if comm is not None:
         comm.check()
     # untimed self-check: the last step's first request re-scored from all of its candidates on one device
@@ -160,6 +173,9 @@ def bench_moe(a):
             "generated_tokens_per_s": round(dp * R * N * a.gen_len / dt, 1),
             "verified": verified,
             "embedder_allreduce_bytes_per_step": ar_bytes,
+            "world_size": pdist.world_size_seen(),
+            "preflight": pre,
+            "comm_per_step": comm_stats,
             "config": {"model": f"{a.decoder} + {a.embedder}", "global_batch": dp * R, "candidates_per_request": N,
                        "seq_len": a.prompt_len + a.gen_len,
                        "parallelism": f"tp{tp} x dp{dp}" + (" (ranks SHARE one GPU: a rehearsal of the protocol, "
@@ -167,7 +183,8 @@ def bench_moe(a):
                        "embedder": f"tp{emb_tp}" if emb_tp > 1 else (f"dp{tp} inside the TP group" if tp > 1 else
                                                                       "one GPU"),
                        "tp_allreduce": ("ipc one-shot kernel (hipGraph)" if comm is not None else
-                                        "process group (eager)" if tp > 1 else "none")}}
+                                        "process group (eager)" + (" (pre-flight fallback)" if tp_comm != a.tp_comm
+                                                                   else "") if tp > 1 else "none")}}
 
 
 def main():

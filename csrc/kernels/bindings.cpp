@@ -27,13 +27,12 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, int,
-               float, int, hipStream_t);
+               float, int, int, hipStream_t);
 int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
 int lwc_skinny_gemm(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
                    int, int, int, int, int, int, const void*, void*, int, hipStream_t);
 int lwc_moe_route(const void*, int, int, int, int*, float*, int*, int*, int*, hipStream_t);
-int lwc_gemm4w8(const void*, const void*, void*, const float*, const float*, int, int, int, int, int, hipStream_t);
 int lwc_moe_router(const void*, int, const void*, int, int, int, int, int*, float*, int*, int*, int*, void*,
                    hipStream_t);
 int lwc_moe_combine(const void*, const int*, const float*, int, int, int, void*, hipStream_t);
@@ -426,7 +425,8 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
 // Folded RMSNorm (gemm4w.hip head): rs_mode 1 (epi 0 / 2) reads ss [>= P, M] fp32 partial row sums of squares
 // and scales the accumulator rows by rsqrt(sum / K + eps); rs_mode 2 (epi 1, bn 256) writes ss [N/256, M].
 void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
-            int64_t bn, const c10::optional<at::Tensor>& ss, int64_t rs_mode, int64_t P, double eps, int64_t var) {
+            int64_t bn, const c10::optional<at::Tensor>& ss, int64_t rs_mode, int64_t P, double eps, int64_t var,
+            int64_t gm) {
   const void* r = gemm_operands(A, W, C, R, epi);
   const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
   TORCH_CHECK(bn == 256 || bn == 192, "gemm4w: bn must be 256 or 192");
@@ -447,7 +447,7 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
   }
   CHECK_RC(lwc_gemm4w(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
                       (int)epi, (int)bn, ssp, ssp ? (int)ss->size(1) : 0, (int)rs_mode, (int)P, (float)eps, (int)var,
-                      cur_stream()),
+                      (int)gm, cur_stream()),
            "gemm4w");
 }
 
@@ -470,22 +470,6 @@ void rms_rowsumsq(const at::Tensor& x, at::Tensor& ss) {
   TORCH_CHECK(x.dim() == 2 && ss.numel() >= x.size(0), "rms_rowsumsq: x [M, d], ss [>= M]");
   CHECK_RC(lwc_rms_rowsumsq(x.data_ptr(), ss.data_ptr<float>(), (int)x.size(0), (int)x.size(1), cur_stream()),
            "rms_rowsumsq");
-}
-
-void gemm4w8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const at::Tensor& a_scale,
-             const at::Tensor& w_scale) {
-  // dense fp8 GEMM on the 4-wave schedule (gemm4w8.hip): A [M, K] e4m3 (row stride allowed), W [N, K] e4m3,
-  // C [M, N] bf16 = (A . W^T) * a_scale[row] * w_scale[col]
-  CHECK_GPU(A); CHECK_GPU(W); CHECK_CONTIG(W); CHECK_BF16(C);
-  TORCH_CHECK(A.scalar_type() == at::kFloat8_e4m3fn && W.scalar_type() == at::kFloat8_e4m3fn, "gemm4w8: e4m3 A and W");
-  TORCH_CHECK(A.dim() == 2 && A.stride(1) == 1 && W.dim() == 2 && C.dim() == 2 && C.stride(1) == 1, "gemm4w8: layouts");
-  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
-  TORCH_CHECK(W.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm4w8: shape mismatch");
-  CHECK_DTYPE(a_scale, at::kFloat); CHECK_CONTIG(a_scale); CHECK_DTYPE(w_scale, at::kFloat); CHECK_CONTIG(w_scale);
-  TORCH_CHECK(a_scale.numel() >= M && w_scale.numel() == N, "gemm4w8: a_scale [M], w_scale [N]");
-  CHECK_RC(lwc_gemm4w8(A.data_ptr(), W.data_ptr(), C.data_ptr(), a_scale.data_ptr<float>(), w_scale.data_ptr<float>(), M,
-                       N, K, (int)A.stride(0), (int)C.stride(0), cur_stream()),
-           "gemm4w8");
 }
 
 void gemm8g_fp8(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& row_off,
@@ -951,7 +935,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm8p_slots", &lwc_gemm8p_slots);
   m.def("moe_route", &moe_route);
   m.def("moe_router", &moe_router);
-  m.def("gemm4w8", &gemm4w8);
   m.def("moe_combine", &moe_combine);
   m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("paged_decode_cascade", &paged_decode_cascade);

@@ -2,7 +2,7 @@
 //
 //   C[M, N]   = A[M, K] . W[N, K]^T (+ R)             EPI_PLAIN / EPI_RESIDUAL
 //   H[M, N/2] = silu(A . Wg^T) * (A . Wu^T)            EPI_SWIGLU (W rows gate/up interleaved in blocks of 32)
-//   C         = A . W^T + bias (then exact erf GELU)   EPI_BIAS / EPI_BIAS_GELU
+//   C         = A . W^T + bias (then GELU: exact erf on VAR 32, the tanh form on VAR 64)   EPI_BIAS / _GELU
 //
 // Why a second core next to gemm8p: gemm8p pairs two waves per SIMD and hands the matrix pipe back and
 // forth across s_barriers (compute segment of one wave || load segment of its partner).  Its load
@@ -15,20 +15,26 @@
 //
 // Per K tile (BK = 64) and wave: 16 NT MFMAs (8 m x NT n tiles x 2 k-steps of 32), 2 (8 + NT)
 // ds_read_b128 fragment reads, 8 + NT LDS-DMA pieces of 1 KiB (the workgroup moves the A | W tile).  LDS
-// holds two K tiles.  Register fragments are double-buffered by k-step: X = k-step 0, Y = k-step 1.
-//
-//   iteration r (tile r in LDS buffer r & 1):
-//     seg 1: 8 NT MFMAs k0(r) on X          || 8+NT ds_reads Y <- tile r           ; lgkmcnt(0), s_barrier
-//     seg 2: 4 NT MFMAs k1(r) on Y (m 0..3) || 8+NT DMA pieces tile r+2 -> buffer r & 1 ; vmcnt(8+NT), s_barrier
-//     seg 3: 4 NT MFMAs k1(r) on Y (m 4..7) || 8+NT ds_reads X <- tile r+1 (buffer (r+1) & 1)
-//   hazards: WAR — tile r+2 overwrites buffer r & 1 only after every wave's reads of tile r completed
-//            (lgkmcnt(0) + barrier closing seg 1).  RAW — tile r+1 is read in seg 3 after every wave's
-//            vmcnt wait for it (tile r+2's pieces, the youngest, may stay in flight) + the barrier closing
-//            seg 2.  vmcnt never reaches 0 inside the loop except for the last two tiles.
+// holds two K tiles.  Register fragments are double-buffered by k-step: X = k-step 0, Y = k-step 1.  The main
+// loop (G4_TILE_H, hipBLASLt's MT256x256x64 segment shape, disassembled): seg A = the Y reads of tile R, one
+// per k-step-0 MFMA, lgkmcnt(0), barrier; seg B = the rest of k-step 0 and most of k-step 1, carrying tile
+// R+2's DMA pieces one per ~5 MFMAs at raised wave priority, counted vmcnt, barrier; seg C = the last
+// k-step-1 MFMAs with the X reads of tile R+1.  vmcnt never reaches 0 inside the loop except for the last
+// two tiles.
+//   hazards: WAR — tile R+2 overwrites buffer R & 1 only after every wave's reads of tile R completed
+//            (lgkmcnt(0) + barrier closing seg A).  RAW — tile R+1 is read in seg C after every wave's
+//            counted vmcnt wait for it (tile R+2's pieces, the youngest, stay in flight) + the barrier
+//            closing seg B.
 //   interleave: each load is followed by its share of the segment's MFMAs, pinned by sched_barrier(0).
 //   MFMA: inline asm with the accumulator tied IN PLACE in an AGPR quad.  The builtin lets the register
 //         allocator pick the untied form (dst != srcC); with every AGPR live it then rotates the
-//         accumulators through VGPRs — ~300 v_accvgpr moves per K tile, measured in the .s.
+//         accumulators through VGPRs — ~300 v_accvgpr moves per K tile, measured in the .s.  The compiler
+//         cannot see the asm's latency: llm_weighted_consensus_amd/_isa_guard.py checks the built code
+//         object for accumulator moves / reads of in-flight MFMA results and fails the build on one.
+// Two schedules share that loop (the planner picks per shape, ops/gemm_plan.py): VAR 32 with the block-
+// staged epilogue (accumulators -> LDS image -> 16 B row stores), and VAR 64 — the wave-local epilogue on
+// the transposed accumulator layout (TR / TRR below), with the next persistent tile's first two K tiles
+// DMA'd inside this tile's last two iterations (even K tile counts).
 //
 // LDS image (per operand, per K tile): rows x 128 B, lane-linear DMA image; 16 B chunk c of row r is
 // stored at chunk c ^ ((r >> 1) & 7) (swizzle applied to the DMA source address and to the read: the 16
@@ -53,7 +59,8 @@
 //        pieces (1 KiB each) issued before the tile's first K-tile pieces (the prologue's counted wait
 //        retires them); after the prologue barrier thread t adds row t's partials in order and keeps
 //        r = rsqrt(sum / K + eps) in LDS; the epilogue scales its rows before SwiGLU / the store.  The
-//        first projection of a chain reads P = 1 partial from rms_rowsumsq (norm.hip).
+//        first projection of a chain reads P = 1 partial from rms_rowsumsq (norm.hip).  VAR 64: from the
+//        second persistent tile on, the tile's partials were DMA'd under the previous tile's main loop.
 #include <algorithm>
 #include <cstdlib>
 
@@ -87,8 +94,6 @@ struct Geo {
   static constexpr int OpB = BN * 128;          // W operand's K tile
   static constexpr int Buf = kOpA + OpB;        // one K tile
   static constexpr int Lds = 2 * Buf;           // two K tiles
-  static constexpr int Stage = 16 * 16 * NT * 2; // VAR 64: one wave's 16-row epilogue staging (bytes)
-  static constexpr int LdsPap = Lds + 4 * Stage;  // VAR 64: K buffers + the four waves' staging
   static constexpr int Pieces = 8 + NT;         // LDS-DMA pieces per wave per K tile
   static constexpr int Reads = 8 + NT;          // fragment reads per wave per k-step
 };
@@ -166,22 +171,30 @@ LWC_DEVICE int swz(int row, int col) {
   return col ^ (((row & 7) << 3) % CW);
 }
 
+// LDS bytes: the two K tiles, then the RS area (RS 1: P x 256 partials + 256 row scales; RS 2: row sums)
+template <int NT, int RS>
+constexpr int lds_bytes() {
+  return Geo<NT>::Lds + (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
+}
+
 template <int EPI, int NT, int VAR, int RS>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   using G = Geo<NT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  // the wave-local epilogue (VAR 64): every epilogue but the row-scaled consumers (RS 1)
-  constexpr bool PAP = (VAR == 64 || VAR == 96) && RS != 1;  // 96: VAR 64 without TR (A/B knob)
-  // the wave-local epilogue of every output on the transposed accumulator layout (mfma2): plain / SwiGLU /
-  // bias / GELU (TR) and residual (TRR, RS 0 / 2); VAR 96 keeps the staged image for all but the residual
-  constexpr bool TR = PAP && VAR == 64 && RS == 0 && EPI != EPI_RESIDUAL;
+  static_assert(VAR == 32 || VAR == 64, "gemm4w schedules: 32 (block-staged epilogue), 64 (wave-local)");
+  // VAR 64: the wave-local epilogue ("prefetch across persistent tiles") on the transposed accumulator layout
+  // (mfma2): plain / SwiGLU / bias / GELU (TR; RS 0, and the row-scaled consumers RS 1) and residual (TRR,
+  // RS 0 / 2)
+  constexpr bool PAP = VAR == 64;
+  constexpr bool TR = PAP && RS != 2 && EPI != EPI_RESIDUAL;
   constexpr bool TRR = PAP && EPI == EPI_RESIDUAL;
   constexpr bool TRL = TR || TRR;
-  // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers (RS 1 runs the
-  // block-staged epilogue, VAR 32); RS 2: the four waves' 128 row sums (2 KiB) at the same place
-  constexpr int RSOFF = PAP ? G::LdsPap : G::Lds, RSV = RSOFF + 16384;
+  static_assert(!PAP || TRL, "the wave-local epilogue runs on the transposed layout");
+  // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers; RS 2: the four
+  // waves' 128 row sums (2 KiB) at the same place
+  constexpr int RSOFF = G::Lds, RSV = RSOFF + 16384;
   // LDS-DMA piece k (64 lanes x 16 B = 256 rows x fp32) of partial k of m-tile rows [m, m + 256)
   auto ss_dma = [&](int m, int k) {
     const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.ssld + m, (p.M - m) * 4);
@@ -228,7 +241,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
       for (int k = 0; k < G::Pieces; ++k) piece(buf, kt, k);
     };
-    // VAR 64 / 96: the next persistent tile (its first two K tiles are DMA'd inside the last two main-loop
+    // VAR 64: the next persistent tile (its first two K tiles are DMA'd inside the last two main-loop
     // iterations of this one).  Past the last tile the pieces re-read this tile's first two K tiles into
     // the freed buffers instead: every piece a real memory request — pieces past a resource's end complete
     // out of order with the real ones before them, and a counted vmcnt wait then passes too early
@@ -271,7 +284,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         fa[k - NT] = *reinterpret_cast<const uint4v*>(buf + oa + (k - NT) * 2048);
     };
 
-    // (VAR 64 / 96 take even K tile counts only — the host falls back to VAR 32 — so the next tile's first
+    // (VAR 64 takes even K tile counts only — the host falls back to VAR 32 — so the next tile's first
     // two K tiles, DMA'd inside the last two iterations, land in buffers 0 and 1)
     const int nt = KT;
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
@@ -296,91 +309,35 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     if constexpr (RS == 1) {
       // row tid's scale from its partials (the main loop's first barrier publishes it to the epilogues)
       const float* part = reinterpret_cast<const float*>(smem + RSOFF);
-      float v[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = part[k * 256 + tid];  // all 16 in flight (the region is always 16 KiB)
       float sum = 0.f;
+      if constexpr (PAP) {
+        // (the accumulators and the fragment registers are live here: a few partials in flight at a time)
+#pragma unroll 4
+        for (int k = 0; k < p.P; ++k) sum += part[k * 256 + tid];  // fixed order: deterministic
+      } else {
+        float v[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) sum += k < p.P ? v[k] : 0.f;  // fixed order: deterministic
+        for (int k = 0; k < 16; ++k) v[k] = part[k * 256 + tid];  // all 16 in flight (the region is always 16 KiB)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sum += k < p.P ? v[k] : 0.f;  // fixed order: deterministic
+      }
       reinterpret_cast<float*>(smem + RSV)[tid] = rsqrtf(sum / (float)p.K + p.eps);
+      if constexpr (PAP) {
+        // the NEXT persistent tile's partials go out now, under this tile's main loop (its prologue is the
+        // previous tile's tail, which issues no partials): every thread has read this tile's first, then the
+        // DMA overwrites the region.  The oldest VMEM ops of the loop: its first counted wait retires them.
+        G4_LGKM0();
+        G4_BAR();
+        __builtin_amdgcn_sched_barrier(0);
+        if (pf) {
+          for (int k = wid; k < p.P; k += 4) ss_dma(um * 256, k);
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < G::Reads; ++k) rd1(smem, offA0, offB0, xa, xb, k);
 
-    // K tile R: seg 1 (k-step 0 on X || read Y), seg 2 (k-step 1, m 0..3 || DMA tile R+2), seg 3 (k-step 1,
-    // m 4..7 || read X of tile R+1).  STAGE / NEXT select the steady-state body or the last two tiles'
-    // (no DMA / no next tile): straight-line bodies, no branch inside.
-    constexpr int M1 = 8 * NT, M2 = 4 * NT;  // MFMAs of seg 1, of seg 2 and 3
-    // VAR bit 0: the DMA pieces of tile R+2 go P2 into seg 2 and the rest into seg 3 (beside the X reads);
-    // bit 1: the Y reads of seg 1 are spread over its first 3/4 only, so the lgkmcnt(0) closing seg 1
-    // does not wait on a read issued just before it; bit 2: seg 2 carries 1/4 of the k-step-1 MFMAs
-    // (not 1/2), seg 3 the other 3/4 — the X reads + DMA pieces of seg 3 get more MFMAs to hide behind.
-    constexpr bool SPLIT = VAR & 1, FRONT = VAR & 2, BAL = VAR & 4;
-    constexpr int P2 = SPLIT ? G::Pieces / 2 : G::Pieces, P3 = G::Pieces - P2;
-    constexpr int F1 = FRONT ? 3 * M1 / 4 : M1;      // seg-1 MFMAs that carry the Y reads
-    constexpr int S2 = BAL ? M2 / 2 : M2;  // seg-2 MFMAs (of the 2 M2 k-step-1 MFMAs)
-    constexpr int S3 = 2 * M2 - S2;
-#define G4_TILE(R, STAGE, NEXT)                                                                     \
-  {                                                                                                 \
-    uint8_t* cur = smem + ((R) & 1) * G::Buf;                                                       \
-    uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
-    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
-      rd1(cur, offA1, offB1, ya, yb, k);                                                            \
-      _Pragma("unroll") for (int m = k * F1 / G::Reads; m < (k + 1) * F1 / G::Reads; ++m)           \
-        mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                            \
-    }                                                                                               \
-    _Pragma("unroll") for (int m = F1; m < M1; ++m) mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]); \
-    G4_LGKM0();                                                                                     \
-    G4_BAR();                                                                                       \
-    _Pragma("unroll") for (int k = 0; k < P2; ++k) {                                                \
-      if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
-      _Pragma("unroll") for (int m = k * S2 / P2; m < (k + 1) * S2 / P2; ++m)                       \
-        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                            \
-    }                                                                                               \
-    if constexpr (STAGE) {                                                                          \
-      G4_VM(P2);                                                                                    \
-    } else {                                                                                        \
-      G4_VM(0);                                                                                     \
-    }                                                                                               \
-    G4_BAR();                                                                                       \
-    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
-      if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
-      if constexpr (STAGE && P3 > 0) {                                                              \
-        if (k < P3) piece(cur, (R) + 2, P2 + k);                                                    \
-      }                                                                                             \
-      _Pragma("unroll") for (int m = S2 + k * S3 / G::Reads; m < S2 + (k + 1) * S3 / G::Reads; ++m) \
-        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                            \
-    }                                                                                               \
-  }
-    // VAR 8: ONE barrier per K tile.  seg A = k-step 0 on X || Y reads of tile R; then lgkmcnt(0) (own Y
-    // reads done), vmcnt(0) (own pieces of tile R+1 landed: the only DMA in flight), barrier — after it
-    // every wave is done reading tile R's buffer (WAR) and tile R+1 is visible (RAW); seg B = k-step 1 on Y
-    // || X reads of tile R+1 AND the DMA of tile R+2 into tile R's buffer, both spread over all 8 NT
-    // MFMAs (LDS traffic per segment balanced: 2 segments x ~64 KiB instead of a 96 KiB third segment).
-#define G4_TILE1(R, STAGE, NEXT)                                                                    \
-  {                                                                                                 \
-    uint8_t* cur = smem + ((R) & 1) * G::Buf;                                                       \
-    uint8_t* nxt = smem + (((R) + 1) & 1) * G::Buf;                                                 \
-    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
-      rd1(cur, offA1, offB1, ya, yb, k);                                                            \
-      _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma2<TRL>(acc[m / NT][m % NT], xa[m / NT], xb[m % NT]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                            \
-    }                                                                                               \
-    G4_LGKM0();                                                                                     \
-    G4_VM(0);                                                                                       \
-    G4_BAR();                                                                                       \
-    _Pragma("unroll") for (int k = 0; k < G::Reads; ++k) {                                          \
-      if constexpr (NEXT) rd1(nxt, offA0, offB0, xa, xb, k);                                        \
-      if constexpr (STAGE) piece(cur, (R) + 2, k);                                                  \
-      _Pragma("unroll") for (int m = k * M1 / G::Reads; m < (k + 1) * M1 / G::Reads; ++m)           \
-        mfma2<TRL>(acc[m / NT][m % NT], ya[m / NT], yb[m % NT]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                            \
-    }                                                                                               \
-  }
+    constexpr int M1 = 8 * NT;  // MFMAs of one k-step
     // VAR 32: the library kernel's segment shape (hipBLASLt's MT256x256x64 DTL loop, disassembled: the same
     // 128 MFMA / 32 ds_read_b128 / 16 LDS-DMA per K tile, two barriers).  seg A: the Y reads of tile R back
     // to back, one per k-step-0 MFMA, then a few more MFMAs, lgkmcnt(0), barrier; seg B: the long middle —
@@ -432,8 +389,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     }                                                                                               \
   }
     int r = 0;
-    if constexpr (VAR == 32 || VAR == 64 || VAR == 96) {
-      // VAR 64 / 96 (TAIL 2): the last two K tiles carry the NEXT tile's first two (into the buffers they
+    {
+      // VAR 64 (TAIL 2): the last two K tiles carry the NEXT tile's first two (into the buffers they
       // free: buffer 0, then 1, as the prologue's stage(0) / stage(1) — KT is even for these variants): seg B
       // pieces as in the steady state, no DMA burst left for the epilogue.  (The same control flow as the
       // other variants' tail: a differently shaped tail made the register allocator rotate the accumulators
@@ -445,23 +402,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         ++r;
       }
       G4_TILE_H(r, TAIL, false)
-    } else if constexpr (VAR == 8) {
-      for (; r + 2 < nt; ++r) G4_TILE1(r, true, true)
-      if (nt >= 2) {
-        G4_TILE1(r, false, true)
-        ++r;
-      }
-      G4_TILE1(r, false, false)
-    } else {
-      for (; r + 2 < nt; ++r) G4_TILE(r, true, true)
-      if (nt >= 2) {
-        G4_TILE(r, false, true)
-        ++r;
-      }
-      G4_TILE(r, false, false)
     }
-#undef G4_TILE
-#undef G4_TILE1
 #undef G4_TILE_H
     // accumulators are read by VALU / stores from here on.  The MFMAs are opaque inline asm, so the compiler
     // takes their results as ready at once: without a barrier it hoisted v_accvgpr_read of the last MFMAs'
@@ -478,11 +419,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
     if constexpr (PAP) {
-      // ---- epilogue, wave-local: per m-tile (16 rows), no block barrier; VAR 64 packs rows in registers (TR,
-      // TRR), VAR 96 (A/B) goes through this wave's own staging slice
-      constexpr int CPR = CW / 8;          // 16 B chunks per row
-      constexpr int PER = 16 * CPR / 64;   // chunks per lane per m-tile: 4 (bn 256), 3 (bn 192), 2 (SwiGLU)
-      bf16_t* st = reinterpret_cast<bf16_t*>(smem + G::Lds + wid * G::Stage);
+      // ---- epilogue, wave-local: per m-tile (16 rows), no block barrier; rows packed in registers (TR, TRR)
       const int ncol0 = EPI == EPI_SWIGLU ? n0 / 2 + wn * 8 * NT : n0 + wn * 16 * NT;
       const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
       const int row0 = __builtin_amdgcn_readfirstlane(m0 + wm * 128);  // uniform: buffer resources in SGPRs, no waterfall loops
@@ -491,16 +428,6 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       // store branches between the epilogue's memory operations)
       const int rows_c = max(0, min(p.M - row0, 128));
       const __amdgpu_buffer_rsrc_t rC = uniform_rsrc(p.C + (size_t)row0 * p.ldc, rows_c * p.ldc * 2);
-      // operand loads of the epilogue FIRST, then the next tile's DMA: loads return in issue order, so a
-      // residual / bias value issued after the DMA pieces could only be used once they had landed
-      float bvals[NT];
-      if constexpr (!TR && (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
-#pragma unroll
-        for (int jj = 0; jj < NT; ++jj) {
-          const int col = n0 + wn * 16 * NT + r16 + jj * 16;
-          bvals[jj] = col < p.N ? bf2f(p.R[col]) : 0.f;
-        }
-      }
       // TR: the bias of the lane's 4 consecutive columns 16 g + 4 q .. + 3 of each n-tile g (8 B loads; N % 8
       // == 0, so a group lies wholly inside or past the last column)
       float tbias[NT][4];
@@ -611,13 +538,21 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           uint32_t o[NO][2];
+          // RS 1 (folded RMSNorm consumer): every value of the lane's row i * 16 + r16 takes the row's 1/rms
+          float sc = 1.f;
+          if constexpr (RS == 1) sc = reinterpret_cast<const float*>(smem + RSV)[wm * 128 + i * 16 + r16];
 #pragma unroll
           for (int g = 0; g < NO; ++g) {
             float v[4];
             if constexpr (EPI == EPI_SWIGLU) {
               const int gate = (g >> 1) * 4 + (g & 1);  // n-tile of the gate half; the up half is 2 further
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
+              for (int e = 0; e < 4; ++e) {
+                if constexpr (RS == 1)
+                  v[e] = silu(acc[i][gate][e] * sc) * (acc[i][gate + 2][e] * sc);
+                else
+                  v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
+              }
             } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -626,7 +561,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
               }
             } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = acc[i][g][e];
+              for (int e = 0; e < 4; ++e) v[e] = RS == 1 ? acc[i][g][e] * sc : acc[i][g][e];
             }
             o[g][0] = pack_bf16x2(v[0], v[1]);
             o[g][1] = pack_bf16x2(v[2], v[3]);
@@ -648,61 +583,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           if (i == 7) G4_STAMP(round, 6);
         }
         G4_STAMP(round, 7);
-        continue;
+        continue;  // no block barrier: the next tile's first wait + barrier orders everything
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float4v t[NT];
-#pragma unroll
-        for (int jj = 0; jj < NT; ++jj) t[jj] = acc[i][jj];
-        if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-          for (int h = 0; h < NT / 4; ++h)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) t[h * 4 + jj][e] = silu(t[h * 4 + jj][e]) * t[h * 4 + jj + 2][e];
-        }
-        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
-#pragma unroll
-          for (int jj = 0; jj < NT; ++jj)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float y = t[jj][e] + bvals[jj];
-              t[jj][e] = EPI == EPI_BIAS_GELU ? gelu_erf(y) : y;
-            }
-        }
-#pragma unroll
-        for (int jj = 0; jj < NT; ++jj) {
-          if constexpr (EPI == EPI_SWIGLU) {
-            if ((jj & 3) >= 2) continue;
-          }
-          const int oc = EPI == EPI_SWIGLU ? (jj >> 2) * 32 + (jj & 1) * 16 : jj * 16;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int row = 4 * q + e, col = oc + r16;
-            st[row * CW + swz<CW>(row, col)] = f2bf(t[jj][e]);
-          }
-        }
-        G4_LGKM0();  // the wave's staging writes landed before its lanes read each other's values
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-          const int c = lane + 64 * u;
-          const int row = c / CPR, cch = c % CPR;
-          const int gm = row0 + i * 16 + row, gn = ncol0 + cch * 8;
-          const uint4v v = *reinterpret_cast<const uint4v*>(st + row * CW + swz<CW>(row, cch * 8));
-          (void)gm;
-          const uint32_t off = gn < ncols ? (uint32_t)(((i * 16 + row) * p.ldc + gn) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(v, rC, off, 0, 0);
-        }
-        G4_LGKM0();  // the staging reads are done before the next m-tile overwrites the slice
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0) G4_STAMP(round, 4);
-        if (i == 3) G4_STAMP(round, 5);
-        if (i == 7) G4_STAMP(round, 6);
-      }
-      G4_STAMP(round, 7);
-      continue;  // no block barrier: the next tile's first wait + barrier orders everything
     }
 
     // ---- epilogue: per wave 128 rows x CW bf16 columns through LDS, then 16 B stores
@@ -866,8 +748,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
 template <int EPI, int NT, int VAR, int RS>
 int launch3(const Params& p, hipStream_t s) {
-  constexpr int lds = ((VAR == 64 || VAR == 96) && RS != 1 ? Geo<NT>::LdsPap : Geo<NT>::Lds) +
-                      (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
+  constexpr int lds = lds_bytes<NT, RS>();
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR, RS>,
@@ -878,21 +759,17 @@ int launch3(const Params& p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int env_int(const char* name, int dflt);
-
 template <int EPI, int NT>
 int launch(const Params& p, hipStream_t s, int var, int rs) {
-  // schedule variant (VAR bits, see the main loop): the caller's, else LWC_G4_VAR, an A/B knob
-  // (scripts/microbench.py g4ab); default 32, the library-shaped schedule (faster than 1 at every headline
-  // shape, profiles/gemm4w.md); every epilogue carries 1, 32 and 64, the plain one the other variants; 96 = 64 with the staged epilogue image instead of TR (and erf GELU; A/B only).
-  // rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sum-of-squares (see the file head)
-  if (var <= 0) var = env_int("LWC_G4_VAR", 32);
-  // VAR 64 / 96 DMA the next tile's first two K tiles inside the last two iterations: even K tile counts
-  if ((var == 64 || var == 96) && (p.KT & 1)) var = 32;
+  // schedule: 32 = the library-shaped main loop with the block-staged epilogue, 64 = the same loop with the
+  // wave-local transposed-layout epilogue and the next persistent tile's first K tiles DMA'd inside this
+  // one's last two iterations (even K tile counts only: odd ones run 32).  The planner picks per shape
+  // (ops/gemm_plan.py).  rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sums of squares.
+  if (var != 64 || (p.KT & 1)) var = 32;
   if (rs == 1) {
-    // (VAR 64 + RS 1 ran out of VGPRs in the wave-local epilogue: 256 + scratch; the row-scaled
-    // consumers take the block-staged epilogue)
-    if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) return launch3<EPI, NT, 32, 1>(p, s);
+    if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) {
+      return var == 64 ? launch3<EPI, NT, 64, 1>(p, s) : launch3<EPI, NT, 32, 1>(p, s);
+    }
     return -1;
   }
   if (rs == 2) {
@@ -901,22 +778,7 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
     }
     return -1;
   }
-  if (var == 32) return launch3<EPI, NT, 32, 0>(p, s);
-  if (var == 64) return launch3<EPI, NT, 64, 0>(p, s);
-  if constexpr (EPI != EPI_RESIDUAL) {  // VAR 64 with the staged epilogue image (and erf GELU): A/B
-    if (var == 96) return launch3<EPI, NT, 96, 0>(p, s);
-  }
-  if constexpr (EPI == EPI_PLAIN) {
-    switch (var) {
-      case 0: return launch3<EPI, NT, 0, 0>(p, s);
-      case 3: return launch3<EPI, NT, 3, 0>(p, s);
-      case 5: return launch3<EPI, NT, 5, 0>(p, s);
-      case 7: return launch3<EPI, NT, 7, 0>(p, s);
-      case 8: return launch3<EPI, NT, 8, 0>(p, s);
-      default: break;
-    }
-  }
-  return launch3<EPI, NT, 1, 0>(p, s);
+  return var == 64 ? launch3<EPI, NT, 64, 0>(p, s) : launch3<EPI, NT, 32, 0>(p, s);
 }
 
 template <int NT>
@@ -931,11 +793,6 @@ int dispatch(const Params& p, int epi, hipStream_t s, int var, int rs) {
       return -1;
   }
   return -1;
-}
-
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
 }
 
 int device_cus() {
@@ -955,9 +812,11 @@ int device_cus() {
 // 3 + bias, 4 gelu(. + bias)); bn = 256 or 192 (W rows per tile; SwiGLU needs 256).  Requires K % 64 == 0,
 // N % 8 == 0, lda / ldc % 8 == 0.  Folded RMSNorm (file head): ss [P][ssld] with P >= 1 partial row sums of
 // squares (epi 0 / 2) scales the accumulator rows by rsqrt(sum / K + eps); ss [N/256][ssld] (epi 1, bn 256)
-// makes the residual epilogue write those partials of its output.  var: schedule variant (0 = LWC_G4_VAR / 32).
+// makes the residual epilogue write those partials of its output.  var: schedule, 64 or 32 (anything else).
+// gm: m-tiles per group of the grouped tile order (an XCD's consecutive tiles run gm m-tiles down each n column).
 extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
-                          int epi, int bn, float* ss, int ssld, int rs_mode, int P, float eps, int var, hipStream_t s) {
+                          int epi, int bn, float* ss, int ssld, int rs_mode, int P, float eps, int var, int gm,
+                          hipStream_t s) {
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
@@ -971,6 +830,6 @@ extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, 
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
   const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
-           tiles_m, tiles_n, K / 64, std::max(1, env_int("LWC_G8_GM", 8)), wpx, tiles, ss, P, ssld, eps};
+           tiles_m, tiles_n, K / 64, std::max(1, gm), wpx, tiles, ss, P, ssld, eps};
   return bn == 256 ? dispatch<8>(p, epi, s, var, rs_mode) : dispatch<6>(p, epi, s, var, rs_mode);
 }

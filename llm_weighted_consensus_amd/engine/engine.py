@@ -27,6 +27,7 @@ import gc
 import itertools
 import os
 import random
+import sys
 import threading
 import time
 from array import array
@@ -334,6 +335,7 @@ class LLMEngine:
         # at a constrained key letter that is the restricted softmax over the sibling letters)
         self.constrained_logprobs = constrained_logprobs
         self.buckets: Dict[int, _GraphBucket] = {}
+        self.step_ab: Dict[int, dict] = {}  # bucket -> in-step A/B replay times per plan (_step_ab)
         self.inflight: Optional[_Step] = None
         # first tokens after a prefill are sampled asynchronously and processed by the next decode step
         self.async_first_tokens = True
@@ -984,6 +986,8 @@ class LLMEngine:
             bk.logits = fwd()
             return
         g = bk.graphs.get(cascade)
+        if g is None and not bk.graphs and bk.B not in self.step_ab:
+            self._step_ab(bk, fwd)
         if g is None:
             dev = self.device
             s = torch.cuda.Stream(device=dev)
@@ -1002,6 +1006,56 @@ class LLMEngine:
             bk.graph = g
         bk.logits = bk.graph_logits[cascade]
         g.replay()
+
+    def _step_ab(self, bk: _GraphBucket, fwd) -> None:
+        """In-step A/B of the model's candidate plans for this bucket (``step_plans``: the isolated planner's
+        choice, all-library, all-hand-written): each is captured into a graph of its own and replayed on this
+        step's real inputs (a decode replay rewrites the same KV slots with the same values, nothing else), the
+        fastest by median replay time becomes the bucket's plan.  Isolated per-GEMM timings do not see the
+        step's clock and cache state; this measures the thing that runs.  ``LWC_STEP_AB=0`` keeps the
+        planner's choice.  Results in ``self.step_ab[B]`` and on stderr."""
+        self.step_ab[bk.B] = {}
+        if os.environ.get("LWC_STEP_AB", "1") == "0" or not hasattr(self.model, "step_plans"):
+            return
+        # decided once per model and batch: every engine on the model then runs the same kernels (engines
+        # compared against each other, a re-created engine)
+        done = self.model.__dict__.setdefault("step_ab_done", {})
+        if bk.B in done:
+            self.step_ab[bk.B] = done[bk.B]
+            return
+        plans = self.model.step_plans(bk.B)
+        if len(plans) < 2:
+            return
+        dev = self.device
+        times = {}
+        s = torch.cuda.Stream(device=dev)
+        for name, plan in plans.items():
+            self.model.apply_step_plan(bk.B, plan)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                fwd()  # warm-up outside capture (first launches of new kernels set their attributes)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                out = fwd()
+            g.replay()
+            ts = []
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            times[name] = sorted(ts)[1]
+            del g, out
+        best = min(times, key=times.get)
+        self.model.apply_step_plan(bk.B, plans[best])
+        torch.cuda.empty_cache()
+        self.step_ab[bk.B] = done[bk.B] = dict(times, choice=best)
+        plan = self.model.plan_summary(bk.B) if hasattr(self.model, "plan_summary") else {}
+        print(f"# step A/B at batch {bk.B}: " + " ".join(f"{k}={v:.2f}ms" for k, v in times.items())
+              + f" -> {best} {plan}", file=sys.stderr, flush=True)
 
     def _launch(self, seqs: List[Sequence], sample: bool = True) -> _Step:
         """Stage inputs, replay the decode graph and launch the sampler for `seqs`; results are

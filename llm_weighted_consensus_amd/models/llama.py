@@ -258,9 +258,10 @@ class LlamaModel:
         if plan["attn"]:
             ops.rms_rowsumsq(x_res, ch)
         nl = len(self.layers)
+        qv, gv, lv = plan.get("qkv_var", 32), plan.get("gu_var", 32), plan.get("lm_var", 32)
         for li, L in enumerate(self.layers):
             if plan["attn"]:
-                qkv = ops.gemm4w(x_res, L.wqkv, bn=plan["qkv_bn"], chain=ch)
+                qkv = ops.gemm4w(x_res, L.wqkv, bn=plan["qkv_bn"], chain=ch, var=qv)
             else:
                 qkv = self._proj(ops.rmsnorm(x_res, ones, eps), L.wqkv)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, cache.k[li], cache.v[li], Hq, Hkv, D, slots=slots,
@@ -268,13 +269,13 @@ class LlamaModel:
             attn = attn_fn(qkv, li).reshape(T, Hq * D)
             self._residual_into(attn, L.wo, x_res, plan["o"] if plan["mlp"] else "plain")
             if plan["mlp"]:
-                act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch)
+                act = ops.gemm4w(x_res, L.w_gate_up, swiglu=True, chain=ch, var=gv)
             else:
                 act = gemm_plan.swiglu(ops.rmsnorm(x_res, ones, eps), L.w_gate_up, L.gu_block, ws=self.g8_ws)
             nxt = plan["attn"] if li + 1 < nl else plan["final"]
             self._residual_into(act, L.w_down, x_res, plan["down"] if nxt else "plain")
         if plan["final"]:
-            return ops.gemm4w(x_res, self.lm_head, chain=ch)
+            return ops.gemm4w(x_res, self.lm_head, chain=ch, var=lv)
         return self._proj(ops.rmsnorm(x_res, ones, eps), self.lm_head)
 
     def chain_ok(self, M: int) -> bool:
@@ -451,6 +452,12 @@ class LlamaModel:
                 ops.gemm4w(x, w[name], chain=ch, **kw)
             return run
 
+        # the row-scaled consumers at both schedules (VAR 32: block-staged epilogue; 64: wave-local, next tile
+        # prefetched) and, for qkv, both tile widths
+        cons = {"qkv": {f"qkv_rs{bn}v{v}": (bn, v) for bn in (192, 256) for v in (32, 64)},
+                "gu": {f"gu_rsv{v}": (256, v) for v in (32, 64)},
+                "lm": {f"lm_rsv{v}": (256, v) for v in (32, 64)}}
+
         def res(name, inp, var):
             return lambda: ops.gemm4w(inp, w[name], residual=x_res, out=x_res, chain=ch, var=var)
 
@@ -458,15 +465,16 @@ class LlamaModel:
             "norm": lambda: ops.rmsnorm(x_res, ones, eps),
             "sumsq": lambda: ops.rms_rowsumsq(x_res, ch),
             "qkv": lambda: self._proj(x, L.wqkv),
-            "qkv_rs192": fold("qkv", bn=192), "qkv_rs256": fold("qkv", bn=256),
             "o": lambda: gemm_plan.linear_add_(xa, L.wo, x_res, ws=self.g8_ws),
             "o_own32": res("o", xa, 32), "o_own64": res("o", xa, 64),
             "gu": lambda: gemm_plan.swiglu(x, L.w_gate_up, L.gu_block, ws=self.g8_ws),
-            "gu_rs": fold("gu", swiglu=True),
             "down": lambda: gemm_plan.linear_add_(xf, L.w_down, x_res, ws=self.g8_ws),
             "down_own32": res("down", xf, 32), "down_own64": res("down", xf, 64),
-            "lm": lambda: self._proj(x, self.lm_head), "lm_rs": fold("lm"),
+            "lm": lambda: self._proj(x, self.lm_head),
         }
+        for pt, cands in cons.items():
+            for k, (bn, v) in cands.items():
+                runs[k] = fold(pt, bn=bn, var=v, swiglu=pt == "gu")
         ts = {k: [] for k in runs}
         for _ in range(3):  # interleaved rounds (one process, one device: matched clocks and caches)
             for k, fn in runs.items():
@@ -475,29 +483,97 @@ class LlamaModel:
         ch.P = P0
 
         def producer(name):  # the cheapest way to leave partials, and its cost over the plain residual GEMM
-            # (a hand-written residual GEMM must beat the library + row-sum pass by 3 %: in isolation the
-            # down projection's gemm4w VAR 64 + RS 2 timed within that, inside the decode step it ran 332 us
-            # against ~308 — the planner's short interleaved rounds do not see the step's clock and caches)
-            opts = {"own32": t[f"{name}_own32"] * 1.03, "own64": t[f"{name}_own64"] * 1.03,
-                    "sumsq": t[name] + t["sumsq"]}
+            # (isolated timings; the engine's in-step A/B of whole captured decode steps then decides between
+            # this plan, the all-library one and the all-own one: LlamaModel.step_plans)
+            opts = {"own32": t[f"{name}_own32"], "own64": t[f"{name}_own64"], "sumsq": t[name] + t["sumsq"]}
             best = min(opts, key=opts.get)
-            return best, (opts[best] / 1.03 if best != "sumsq" else opts[best]) - t[name]
+            return best, opts[best] - t[name]
+
+        def consumer(pt):
+            k = min(cons[pt], key=lambda c: t[c])
+            return k, cons[pt][k]
 
         o_mode, o_extra = producer("o")
         d_mode, d_extra = producer("down")
-        qkv_bn = 192 if t["qkv_rs192"] <= t["qkv_rs256"] else 256
+        (qk, (qkv_bn, qv)), (gk, (_, gv)), (lk, (_, lv)) = consumer("qkv"), consumer("gu"), consumer("lm")
         # each point: folded (consumer + producer's extra) vs the norm kernel + the consumer's best backend
-        attn = t[f"qkv_rs{qkv_bn}"] + d_extra < t["norm"] + t["qkv"]
-        mlp = t["gu_rs"] + o_extra < t["norm"] + t["gu"]
-        final = t["lm_rs"] + d_extra < t["norm"] + t["lm"]
+        attn = t[qk] + d_extra < t["norm"] + t["qkv"]
+        mlp = t[gk] + o_extra < t["norm"] + t["gu"]
+        final = t[lk] + d_extra < t["norm"] + t["lm"]
         force = os.environ.get("LWC_NORM_CHAIN")
         if force is not None:
             attn = mlp = final = force == "1"
-        plan = {"attn": attn, "mlp": mlp, "final": final, "qkv_bn": qkv_bn, "o": o_mode, "down": d_mode}
+        plan = {"attn": attn, "mlp": mlp, "final": final, "qkv_bn": qkv_bn, "qkv_var": qv, "gu_var": gv,
+                "lm_var": lv, "o": o_mode, "down": d_mode}
         self.chain_m[M] = plan
         key = (M, cfg.hidden, 0, "norm_chain")
         gemm_plan.TIMINGS[key] = t
         gemm_plan._CHOICE[key] = ",".join(f"{k}={v}" for k, v in plan.items())
+
+    # ------------------------------------------------------------------ whole-step plans (engine in-step A/B)
+    def _plan_keys(self, M: int) -> dict:
+        cfg = self.cfg
+        epi = "residual" if self._dense_residual else "plain"
+        return {"qkv": (M, cfg.qkv_dim, cfg.hidden, "plain"), "o": (M, cfg.hidden, cfg.heads * cfg.head_dim, epi),
+                "gu": (M, 2 * cfg.ffn, cfg.hidden, "swiglu"), "down": (M, cfg.hidden, cfg.ffn, epi),
+                "lm": (M, cfg.vocab_size, cfg.hidden, "plain")}
+
+    def step_plans(self, M: int) -> dict:
+        """Candidate plans for a decode step of M rows, for the engine's in-step A/B (it captures the decode
+        graph under each and times replays: isolated per-GEMM timings misjudge the step's clock and cache
+        state, ``profiles/gemm4w_stamps_r5.md``).  ``planner``: the per-shape and norm-chain choices of
+        :meth:`tune_gemms`; ``library``: every projection on hipBLASLt, no folded norm; ``own``: every
+        projection on its fastest hand-written core with the whole norm chain folded.  {} when nothing was
+        tuned at M."""
+        keys = self._plan_keys(M)
+        if self.g8_ws is None or not any(k in gemm_plan._CHOICE for k in keys.values()):
+            return {}
+        plans = {"planner": {"choices": {n: gemm_plan._CHOICE.get(k) for n, k in keys.items()},
+                             "chain": self.chain_m.get(M)}}
+        none = {"attn": False, "mlp": False, "final": False, "qkv_bn": 192, "o": "plain", "down": "plain"}
+        plans["library"] = {"choices": {n: "blas" for n in keys}, "chain": none if M in self.chain_m else None}
+        own = {}
+        for n, k in keys.items():
+            t = {b: v for b, v in gemm_plan.TIMINGS.get(k, {}).items() if b != "blas" and isinstance(v, float)}
+            own[n] = min(t, key=t.get) if t else gemm_plan._CHOICE.get(k)
+        chain = self.chain_m.get(M)
+        t = gemm_plan.TIMINGS.get((M, self.cfg.hidden, 0, "norm_chain"))
+        if chain is not None and t:
+            def best(cands):
+                return min(cands, key=lambda c: t.get(c, float("inf")))
+            q = best([f"qkv_rs{bn}v{v}" for bn in (192, 256) for v in (32, 64)])
+            chain = {"attn": True, "mlp": True, "final": True, "qkv_bn": int(q[6:9]), "qkv_var": int(q[10:]),
+                     "gu_var": int(best(["gu_rsv32", "gu_rsv64"])[6:]), "lm_var": int(best(["lm_rsv32", "lm_rsv64"])[6:]),
+                     "o": best(["o_own32", "o_own64"])[2:], "down": best(["down_own32", "down_own64"])[5:]}
+        plans["own"] = {"choices": own, "chain": chain}
+        return plans
+
+    def apply_step_plan(self, M: int, plan: dict) -> None:
+        """Make ``plan`` (one of :meth:`step_plans`) the choice of every projection at M (and of the norm chain)."""
+        keys = self._plan_keys(M)
+        for n, c in plan["choices"].items():
+            if c is not None:
+                gemm_plan._CHOICE[keys[n]] = c
+        if plan.get("chain") is not None:
+            self.chain_m[M] = dict(plan["chain"])
+
+    def plan_summary(self, M: int) -> dict:
+        """The kernels a decode step of M rows runs, compactly (bench JSON / logs)."""
+        keys = self._plan_keys(M)
+        out = {n: gemm_plan._CHOICE.get(k, "blas") for n, k in keys.items()}
+        c = self.chain_m.get(M)
+        if c and self.chain_ok(M):
+            if c["attn"]:
+                out["qkv"] = f"g4 rs{c['qkv_bn']} v{c.get('qkv_var', 32)}"
+            if c["mlp"]:
+                out["gu"] = f"g4 rs v{c.get('gu_var', 32)}"
+            if c["final"]:
+                out["lm"] = f"g4 rs v{c.get('lm_var', 32)}"
+            if c["mlp"] and c["o"] != "plain":
+                out["o"] = out["o"] + "+sumsq" if c["o"] == "sumsq" else f"g4 rs2 v{c['o'][3:]}"
+            if (c["attn"] or c["final"]) and c["down"] != "plain":
+                out["down"] = out["down"] + "+sumsq" if c["down"] == "sumsq" else f"g4 rs2 v{c['down'][3:]}"
+        return out
 
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor,
                ctx_lens: torch.Tensor, cache: KVCache, num_splits: int = 1,

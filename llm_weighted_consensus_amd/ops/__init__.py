@@ -424,7 +424,8 @@ def skinny_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
 
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
-           gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0) -> torch.Tensor:
+           gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0,
+           gm: int = 8) -> torch.Tensor:
     """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
     a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
     workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
@@ -433,7 +434,8 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     Folded RMSNorm (the decode chain, :class:`NormChain`): with ``chain`` a plain / SwiGLU projection scales
     its accumulator rows by 1/rms of its input rows from the chain's partial row sums of squares (the norm
     weight folded into W: rmsnorm(x) . W^T), and a residual projection writes the partials of its output for
-    the next one.  ``var``: schedule variant (0 = default)."""
+    the next one.  ``var``: schedule (64: wave-local epilogue + next-tile prefetch, else 32: block-staged
+    epilogue); ``gm``: m-tiles per group of the grouped tile order."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
@@ -451,17 +453,17 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
         M = A.shape[0]
         step = max(256, ((1 << 31) - 1) // max(1, A.stride(0) * 2) // 256 * 256)
         if M <= step:
-            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var))
+            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm))
         else:
             for r0 in range(0, M, step):
                 r1 = min(M, r0 + step)
                 res = residual[r0:r1] if epi == 1 else residual
-                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var))
+                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm))
     elif epi == 1:
-        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var))
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var), int(gm))
         chain.P = (N + 255) // 256
     elif epi in (0, 2):
-        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 1, chain.P, chain.eps, int(var))
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 1, chain.P, chain.eps, int(var), int(gm))
     else:
         raise ValueError("gemm4w: chain= goes with the plain, SwiGLU or residual epilogue")
     return out
@@ -660,24 +662,6 @@ def gemm8g_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Option
         r1 = min(M, r0 + step)
         kernels().gemm8g_fp8(xq[r0:r1], wq, out[r0:r1], None, -(-(r1 - r0) // 256), None, s[r0:r1], ws,
                              int(bool(swiglu)), None, None)
-    return out
-
-
-def gemm4w8_dense(xq: torch.Tensor, xs: torch.Tensor, w: "Fp8Weight", out: Optional[torch.Tensor] = None):
-    """Dense fp8 GEMM on the 4-wave schedule (csrc/kernels/gemm4w8.hip: one wave per SIMD, 128 x 128 wave tiles,
-    the LDS traffic of gemm8g's 2-waves-per-SIMD layout halved): (xq [M, K] e4m3 . w.q^T) * xs[row] * w.s[col]
-    -> bf16 [M, N].  Row blocks of < 2 GiB of A per launch (32-bit buffer range)."""
-    M = xq.shape[0]
-    N, K = w.q.shape
-    if out is None:
-        out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
-    if M == 0:
-        return out
-    s, ws = xs.reshape(-1).contiguous(), w.s.reshape(-1).contiguous()
-    step = max(256, (G8G_SPAN - 1) // xq.stride(0) // 256 * 256)
-    for r0 in range(0, M, step):
-        r1 = min(M, r0 + step)
-        kernels().gemm4w8(xq[r0:r1], w.q, out[r0:r1], s[r0:r1], ws)
     return out
 
 

@@ -7,10 +7,9 @@ Backends computing ``A . W^T`` for the dense projections:
 * ``g4``     — the hand-written 4-wave interleaved MFMA GEMM, 256 x 256 tiles (``csrc/kernels/gemm4w.hip``);
 * ``g4n192`` — the same core with 256 x 192 tiles (the qkv projection at decode batch 4096: 512 tiles =
   two whole rounds of 256 CUs, where 256 x 256 tiles leave half of the second round idle);
-* ``g4p``    — gemm4w 256 x 256 with the VAR 64 schedule: each persistent workgroup prefetches its next
-  tile's first two K tiles under the current tile's (wave-local) epilogue — multi-round shapes with few
-  K tiles per output tile (the encoders' K = 768 / 1024 projections, mixed-prefill gate|up); its epilogues
-  run on the transposed accumulator layout (``profiles/gemm4w_stamps_r5.md``).
+* ``g4p``    — gemm4w 256 x 256 with the VAR 64 schedule: each persistent workgroup DMAs its next tile's
+  first two K tiles inside its last two main-loop iterations and runs the wave-local epilogue on the
+  transposed accumulator layout (``profiles/gemm4w_stamps_r5.md``).
 * ``gv``     — the skinny weight-stream GEMM for decode-sized row counts (M <= 64; plain, residual and
   SwiGLU epilogues; ``csrc/kernels/skinny.hip``): the serving path's small decode steps.
 
@@ -18,7 +17,8 @@ The hand-written cores also fuse the SwiGLU of the gate|up projection, or the re
 down projections (:func:`linear_add_`), into their epilogue.  None wins everywhere
 (``profiles/gemm4w.md``), so the choice is made per (M, N, K, epilogue) by timing every applicable
 backend on the device, once, before a decode bucket's hipGraph is captured (:meth:`LlamaModel.tune_gemms`);
-a hand-written core is taken when it beats the library by ``-OWN_MARGIN`` (2 %; isolated timings flatter it).  Untuned shapes (prefill,
+a hand-written core is taken when it is at least as fast as the library (``OWN_MARGIN``, 0); for a decode bucket
+the engine then A/Bs whole captured steps (planner / all-library / all-own, ``LlamaModel.step_plans``).  Untuned shapes (prefill,
 encode) use hipBLASLt.  ``LWC_GEMM=blas|g8|g4|g4n192`` forces one backend (``auto`` = measured, the default).
 """
 from __future__ import annotations
@@ -33,10 +33,10 @@ from . import gemm4w, gemm8p, silu_mul, skinny_gemm, skinny_ok
 
 MODE = os.environ.get("LWC_GEMM", "auto")
 BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p", "gv")
-# a hand-written core is chosen when it beats the library by at least this fraction: the planner times
-# isolated calls, and a core within a percent of the library there ran slower inside the decode step
-# (lm_head on gemm4w VAR 64 chosen at +1 % in isolation: ~2 % slower in the bench, profiles/gemm4w_stamps_r5.md)
-OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "-0.02"))
+# a hand-written core is chosen when it is at least as fast as the library in the isolated timings (no
+# bias either way: the decode step's plan is then settled by the engine's in-step A/B of whole captured steps,
+# engine.LLMEngine._step_ab, which sees the step's clock and cache state)
+OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "0"))
 # LWC_GEMM_SKINNY=0 leaves the skinny decode GEMM out of the timing (A/B knob)
 SKINNY = os.environ.get("LWC_GEMM_SKINNY", "1") != "0"
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -90,10 +91,82 @@ def group_size(group=None) -> int:
     return dist.get_world_size(group) if _INFO.enabled else 1
 
 
+# Per-collective accounting (bench JSON at W > 1): tag -> calls, bytes this rank receives, and the
+# (start, end) events bracketing each call on the issuing stream; ms are read once, after a synchronize
+_COMM: dict = {}
+_TAG: list = [None]
+
+
+class comm_tag:
+    """``with comm_tag("C1"):`` — the collectives issued inside count under that tag (:func:`comm_report`)."""
+
+    def __init__(self, tag: str):
+        self.tag = tag
+
+    def __enter__(self):
+        self.prev, _TAG[0] = _TAG[0], self.tag
+        return self
+
+    def __exit__(self, *exc):
+        _TAG[0] = self.prev
+        return False
+
+
+def _comm_begin(nbytes: int, device):
+    tag = _TAG[0]
+    if tag is None:
+        return None
+    rec = _COMM.setdefault(tag, {"calls": 0, "bytes": 0, "events": []})
+    rec["calls"] += 1
+    rec["bytes"] += int(nbytes)
+    if device is not None and device.type == "cuda":
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return rec, e0
+    return rec, time.perf_counter()
+
+
+def _comm_end(tok) -> None:
+    if tok is None:
+        return
+    rec, start = tok
+    if isinstance(start, float):
+        rec["events"].append((start, time.perf_counter()))
+    else:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        rec["events"].append((start, e1))
+
+
+def comm_report(steps: int = 1, reset: bool = True) -> dict:
+    """{tag: {"calls", "bytes", "ms"}} per step (divided by ``steps``) of the tagged collectives since the last
+    reset; synchronizes the device first (call outside timed regions or at their end)."""
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    out = {}
+    for tag, rec in _COMM.items():
+        ms = 0.0
+        for a, b in rec["events"]:
+            ms += (b - a) * 1e3 if isinstance(a, float) else a.elapsed_time(b)
+        n = max(1, steps)
+        out[tag] = {"calls": rec["calls"] / n, "bytes": rec["bytes"] // n, "ms": round(ms / n, 3)}
+    if reset:
+        _COMM.clear()
+    return out
+
+
 def all_gather_flat(t: torch.Tensor, group=None) -> torch.Tensor:
     """[*] per rank -> [group size, *]: one all_gather_into_tensor on the flattened buffer (the 1-D form
     works for RCCL and gloo alike; GPU tensors under gloo are staged through host memory)."""
     W = group_size(group)
+    tok = _comm_begin(W * t.numel() * t.element_size(), t.device)
+    try:
+        return _all_gather_flat(t, W, group)
+    finally:
+        _comm_end(tok)
+
+
+def _all_gather_flat(t: torch.Tensor, W: int, group=None) -> torch.Tensor:
     flat = t.contiguous().view(-1)
     if _INFO.backend == "gloo" and flat.is_cuda:
         host = flat.cpu()

@@ -6,7 +6,7 @@
 #   bench         the driver's bench command (BENCH_ARGS overrides: default --steps 20 --warmup 5)
 #   quick         bench.py --steps 2 --warmup 1 --profile-steps ($QUICK_ARGS appended)
 #   prof          rocprofv3 kernel-trace + stats of bench.py (scripts/gpu_profile.sh; BENCH_ARGS)
-#   g4ab          scripts/microbench.py g4ab (G4_SHAPES / G4_VARS / G4_VARS_EPI select)
+#   g4ab          scripts/microbench.py g4ab (G4_SHAPES / G4_VARS select)
 #   kernels       tests/test_kernels_gpu.py (-k $KSEL)
 #   pytest:<path> one test file / node id
 #   micro:<what>  scripts/microbench.py <what>

@@ -223,32 +223,38 @@ def gemm4w_ab(dev):
         w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = (torch.rand(N, device=dev) - 0.5).to(torch.bfloat16)
         acc = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+        # gemm4w at both schedules (32: block-staged epilogue, 64: wave-local epilogue + next-tile prefetch;
+        # G4_VARS selects) and both tile widths
+        vars_ = [int(v) for v in os.environ.get("G4_VARS", "32,64").split(",")]
+        gms = [int(v) for v in os.environ.get("G4_GMS", "8").split(",")]
+        vg = [(v, gm) for v in vars_ for gm in gms]
+
+        def nm(p, v, gm):
+            return f"{p}v{v}" + (f"g{gm}" if len(gms) > 1 else "")
+        no_g8 = os.environ.get("G4_NO_G8") == "1"
         if epi == "swiglu":
             wi = ops.swiglu_interleave(w)
             runs = {"blas": lambda: ops.silu_mul(F.linear(x, wi), block=32),
-                    "g8": lambda: ops.gemm8p(x, wi, swiglu=True, ws=ws),
-                    "g4": lambda: ops.gemm4w(x, wi, swiglu=True)}
+                    "g8": lambda: ops.gemm8p(x, wi, swiglu=True, ws=ws)}
+            runs.update({nm("g4", v, gm): (lambda v=v, gm=gm: ops.gemm4w(x, wi, swiglu=True, var=v, gm=gm)) for v, gm in vg})
         elif epi == "res":
-            runs = {"blas": lambda: acc.addmm_(x, w.t()), "g8": lambda: ops.gemm8p(x, w, residual=acc, out=acc, ws=ws),
-                    "g4": lambda: ops.gemm4w(x, w, residual=acc, out=acc),
-                    "g4n192": lambda: ops.gemm4w(x, w, residual=acc, out=acc, bn=192)}
+            runs = {"blas": lambda: acc.addmm_(x, w.t()), "g8": lambda: ops.gemm8p(x, w, residual=acc, out=acc, ws=ws)}
+            runs.update({nm("g4", v, gm): (lambda v=v, gm=gm: ops.gemm4w(x, w, residual=acc, out=acc, var=v, gm=gm))
+                         for v, gm in vg})
         elif epi in ("bias", "gelu"):
             g = epi == "gelu"
             runs = {"blas": (lambda: torch._addmm_activation(b, x, w.t(), use_gelu=True)) if g
                     else (lambda: F.linear(x, w, b)),
-                    "g8": lambda: ops.gemm8p(x, w, bias=b, gelu=g, ws=ws),
-                    "g4": lambda: ops.gemm4w(x, w, bias=b, gelu=g),
-                    "g4n192": lambda: ops.gemm4w(x, w, bias=b, gelu=g, bn=192)}
+                    "g8": lambda: ops.gemm8p(x, w, bias=b, gelu=g, ws=ws)}
+            runs.update({nm("g4", v, gm): (lambda v=v, gm=gm: ops.gemm4w(x, w, bias=b, gelu=g, var=v, gm=gm))
+                         for v, gm in vg})
         else:
-            runs = {"blas": lambda: F.linear(x, w), "g8": lambda: ops.gemm8p(x, w, ws=ws),
-                    "g4": lambda: ops.gemm4w(x, w), "g4n192": lambda: ops.gemm4w(x, w, bn=192)}
-        # gemm4w schedule variants (LWC_G4_VAR bits: 1 split DMA, 2 front-load seg-1 reads, 4 seg-2/3 balance;
-        # only the plain epilogue carries every variant)
-        for k in [k for k in runs if k.startswith("g4")]:
-            fn = runs.pop(k)
-            for v in (os.environ.get("G4_VARS", "1,3,5,7") if epi == "plain"
-                      else os.environ.get("G4_VARS_EPI", "1")).split(","):
-                runs[f"{k}v{v}"] = (lambda fn=fn, v=v: (os.environ.__setitem__("LWC_G4_VAR", v), fn()))
+            runs = {"blas": lambda: F.linear(x, w), "g8": lambda: ops.gemm8p(x, w, ws=ws)}
+            runs.update({nm("g4", v, gm): (lambda v=v, gm=gm: ops.gemm4w(x, w, var=v, gm=gm)) for v, gm in vg})
+            runs.update({nm("g4n192", v, gm): (lambda v=v, gm=gm: ops.gemm4w(x, w, bn=192, var=v, gm=gm))
+                         for v, gm in vg})
+        if no_g8:
+            runs.pop("g8", None)
         res = {k: [] for k in runs}
         for _ in range(5):
             for k, fn in runs.items():
@@ -588,8 +594,9 @@ def serve_shapes(dev):
 
 
 def g48_ab(dev):
-    """Dense fp8: the 4-wave gemm4w8 vs gemm8g (dense mode) vs hipBLASLt's row-scaled fp8 GEMM at config 5's
-    shapes (median of 5 interleaved rounds; G48_SHAPES picks a subset)."""
+    """Dense fp8: gemm8g (dense mode) vs hipBLASLt's row-scaled fp8 GEMM at config 5's shapes (median of 5
+    interleaved rounds; G48_SHAPES picks a subset).  (The 4-wave gemm4w8 arm was removed in round 6: 3-13 %
+    behind gemm8g, profiles/fp8_4wave_r5.md, and its accumulators rotated through in-flight copies.)"""
     from llm_weighted_consensus_amd import ops
 
     shapes = [(4096, 6144, 4096), (4096, 4096, 4096), (4096, 4096, 14336), (16384, 6144, 4096), (8192, 4096, 14336),
@@ -602,8 +609,7 @@ def g48_ab(dev):
         xq, xs = ops.quant_fp8_rows(x)
         del x
         w = ops.Fp8Weight((torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16))
-        runs = {"blas": lambda: ops._fp8_blas(xq, xs, w), "g8g": lambda: ops.gemm8g_dense(xq, xs, w),
-                "g4w8": lambda: ops.gemm4w8_dense(xq, xs, w)}
+        runs = {"blas": lambda: ops._fp8_blas(xq, xs, w), "g8g": lambda: ops.gemm8g_dense(xq, xs, w)}
         res = {k: [] for k in runs}
         for _ in range(5):
             for k, fn in runs.items():

@@ -87,7 +87,7 @@ int main() {
     CK(hipDeviceSynchronize());
     auto call = [&]() {
       return lwc_gemm4w(A, W, C, R, sh.M, sh.N, sh.K, sh.K, sh.epi == 2 ? sh.N / 2 : sh.N, sh.epi, 256, nullptr, 0, 0,
-                        1, 1e-5f, sh.var, 0);
+                        1, 1e-5f, sh.var, 8, 0);
     };
     if (call() != 0) {
       fprintf(stderr, "%s: launch refused\n", sh.name);

@@ -1,10 +1,14 @@
 """Why does the down projection's K tile cost more cycles than o's?  gemm4w (plain epilogue, VAR 64) on the
 decode batch with A rows 8 KB apart (o), 28 KB apart (a K = 4096 slice of the [4096, 14336] activation) and
 the full down shape, per K tile, interleaved rounds in one process; hipBLASLt beside each."""
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
 
-from llm_weighted_consensus_amd import ops
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from llm_weighted_consensus_amd import ops  # noqa: E402
 
 
 def t(fn, it=10):

@@ -186,7 +186,16 @@ def _world8_worker(rank, world, port, out_q):
     from llm_weighted_consensus_amd.parallel import dist as pdist
     from llm_weighted_consensus_amd.parallel.prefill_share import all_gather_prefills
 
+    from llm_weighted_consensus_amd.parallel import preflight
+
     pdist.init_from_env("cpu")
+    # the benches' start-up pre-flight: a checked all-gather at world 8 (CPU: no devices, no peer pairs);
+    # with a forced peer failure the IPC path falls back with the reason
+    pre = preflight.run(torch.device("cpu"))
+    pre_ok = (pre["world_size_rccl"] == world and pre["rccl_allgather"]["ok"] and pre["peer_access"] == "all"
+              and pre["ipc"] == "not requested" and not pre["ipc_fallback"])
+    forced = preflight.run(torch.device("cpu"), want_ipc=True, force_peer_fail=True)
+    pre_ok &= forced["ipc_fallback"] and forced["ipc"].startswith("fallback: no peer access on forced")
     cp = 2
     cgroup, gidx, crank = pdist.candidate_groups(cp)
     ok = (gidx, crank) == (rank // cp, rank % cp)
@@ -194,7 +203,9 @@ def _world8_worker(rank, world, port, out_q):
     R, L, E, V, nb = 2, 2, 4, 5, 3
     kv = torch.stack([torch.full((L, 2, E), 1000.0 * rank + b) for b in range(R * nb)], dim=2)
     lg = torch.stack([torch.full((V,), 10.0 * rank + i) for i in range(R)])
-    shared = all_gather_prefills(kv, lg, [nb] * R, group=cgroup)
+    pdist.comm_report(reset=True)
+    with pdist.comm_tag("C4"):
+        shared = all_gather_prefills(kv, lg, [nb] * R, group=cgroup)
     ok &= len(shared) == R * cp
     for j, (k, l) in enumerate(shared):
         src = gidx * cp + j // R          # global rank that prefilled group prompt j
@@ -205,8 +216,16 @@ def _world8_worker(rank, world, port, out_q):
     g = torch.Generator().manual_seed(7 + gidx)   # one candidate set per request group
     full = torch.nn.functional.normalize(torch.randn(R * cp, N, d, generator=g), dim=-1)
     n_local = N // cp
-    got = gather_candidates(full[:, crank * n_local:(crank + 1) * n_local].contiguous(), cgroup)
+    with pdist.comm_tag("C1"):
+        got = gather_candidates(full[:, crank * n_local:(crank + 1) * n_local].contiguous(), cgroup)
     ok &= torch.equal(got, full)
+    # the per-step accounting the bench JSON reports: bytes received per tag (kv + logits + 2 count gathers
+    # for C4, the embeddings for C1), calls, and a time for each
+    comm = pdist.comm_report(1)
+    c4_bytes = cp * (kv.numel() + lg.numel()) * 4 + cp * 2 * 8 + cp * R * 8
+    ok &= comm["C4"]["calls"] == 4 and comm["C4"]["bytes"] == c4_bytes and comm["C4"]["ms"] >= 0
+    ok &= comm["C1"]["calls"] == 1 and comm["C1"]["bytes"] == R * cp * N * d * 4
+    ok &= pre_ok
     ok &= consensus_reference(got, 0.1).best == consensus_reference(full, 0.1).best
     seen = pdist.world_size_seen()
     ok &= pdist.max_over_ranks(float(rank)) == world - 1

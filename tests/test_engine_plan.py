@@ -56,3 +56,50 @@ def test_cascade_tiles_overflow_raises_only_without_room():
     tiles = np.zeros((1, 3), dtype=np.int32)
     with pytest.raises(RuntimeError):
         cascade_tiles([(0, 40, 0)], 32, tiles)
+
+
+def test_step_plans_candidates_and_apply(monkeypatch):
+    """LlamaModel.step_plans (the engine's in-step A/B candidates) from recorded planner state, on CPU: the
+    planner's own choice, all-library (norm chain off) and all-hand-written (fastest own backend per shape, the
+    chain fully folded with the fastest consumer / producer variants); apply_step_plan installs one and
+    plan_summary reports it."""
+    from llm_weighted_consensus_amd.models.config import decoder_config
+    from llm_weighted_consensus_amd.models.llama import LlamaModel
+    from llm_weighted_consensus_amd.ops import gemm_plan
+
+    m = LlamaModel.__new__(LlamaModel)
+    m.cfg = decoder_config("llama-3-8b")
+    m.g8_ws = object()
+    m.fp8_dense = False
+    m.chain = type("Ch", (), {"max_rows": 8192})()
+    M = 4096
+    keys = m._plan_keys(M)
+    choices, timings = dict(gemm_plan._CHOICE), dict(gemm_plan.TIMINGS)
+    try:
+        for n, k in keys.items():
+            gemm_plan._CHOICE[k] = "blas"
+            gemm_plan.TIMINGS[k] = {"blas": 100.0, "g4": 101.0, "g4p": 99.0, "g8": 120.0}
+        t = {f"qkv_rs{bn}v{v}": 150.0 + bn / 100 + v / 100 for bn in (192, 256) for v in (32, 64)}
+        t.update({"gu_rsv32": 660.0, "gu_rsv64": 650.0, "lm_rsv32": 3000.0, "lm_rsv64": 2990.0,
+                  "o_own32": 110.0, "o_own64": 101.0, "down_own32": 330.0, "down_own64": 320.0})
+        gemm_plan.TIMINGS[(M, m.cfg.hidden, 0, "norm_chain")] = t
+        m.chain_m = {M: {"attn": True, "mlp": False, "final": False, "qkv_bn": 192, "qkv_var": 32, "o": "own64",
+                         "down": "sumsq"}}
+        plans = m.step_plans(M)
+        assert set(plans) == {"planner", "library", "own"}
+        assert plans["library"]["choices"] == {n: "blas" for n in keys}
+        assert not plans["library"]["chain"]["attn"]
+        assert plans["own"]["choices"] == {n: "g4p" for n in keys}
+        assert plans["own"]["chain"] == {"attn": True, "mlp": True, "final": True, "qkv_bn": 192, "qkv_var": 32,
+                                         "gu_var": 64, "lm_var": 64, "o": "own64", "down": "own64"}
+        m.apply_step_plan(M, plans["own"])
+        assert all(gemm_plan._CHOICE[k] == "g4p" for k in keys.values()) and m.chain_m[M]["mlp"]
+        s = m.plan_summary(M)
+        assert s["gu"] == "g4 rs v64" and s["o"] == "g4 rs2 v64" and s["qkv"] == "g4 rs192 v32"
+        m.apply_step_plan(M, plans["library"])
+        assert m.plan_summary(M) == {n: "blas" for n in keys}
+    finally:
+        gemm_plan._CHOICE.clear()
+        gemm_plan._CHOICE.update(choices)
+        gemm_plan.TIMINGS.clear()
+        gemm_plan.TIMINGS.update(timings)

@@ -44,16 +44,20 @@ def test_prefill_and_decode_match_reference(tiny, gpu):
         assert _cos(dl[0], ref_logits[t]) > 0.995, t
 
 
-def test_engine_greedy_graph_equivalence_and_fork(tiny, gpu):
+@pytest.mark.parametrize("step_ab", ["0", "1"])
+def test_engine_greedy_graph_equivalence_and_fork(tiny, gpu, step_ab, monkeypatch):
+    """Graph replay == eager decode, greedy.  With the in-step A/B on (engine._step_ab), the graph engine runs
+    first: its A/B installs the winning plan in the model, which the eager engine then runs too."""
     from llm_weighted_consensus_amd.engine.engine import LLMEngine
     from llm_weighted_consensus_amd.engine.sampling import SamplingParams
     from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
 
+    monkeypatch.setenv("LWC_STEP_AB", step_ab)
     tok = ByteTokenizer(tiny.cfg.vocab_size)
     prompts = [tok.encode("hello world, this is a prompt of some length " * 2), tok.encode("short")]
     sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
     outs = []
-    for graphs in (False, True):
+    for graphs in ((True, False) if step_ab == "1" else (False, True)):
         eng = LLMEngine(tiny, tok, num_blocks=256, max_batch=16, max_model_len=512, use_graphs=graphs)
         outs.append(eng.generate(prompts, sp, n=3))
         assert eng.bm.num_free == 256  # everything released
