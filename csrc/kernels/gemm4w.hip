@@ -414,7 +414,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int jj = 0; jj < NT; ++jj) asm volatile("" : "+a"(acc[i][jj]));
-    __syncthreads();  // every wave is done with the K buffers: LDS is reused by the epilogue
+    // VAR 32: every wave is done with the K buffers, which the block-staged epilogue reuses.  VAR 64's
+    // wave-local epilogue touches no K buffer (its LDS use, the RS areas, is ordered by the main loop's
+    // barriers and the next tile's prologue barrier), so no block barrier here: a __syncthreads() would also
+    // drain vmcnt(0) — the next tile's K-tile DMA issued in the last iteration — before the epilogue starts
+    if constexpr (!PAP) __syncthreads();
     G4_STAMP(round, 2);
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
@@ -430,17 +434,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       const __amdgpu_buffer_rsrc_t rC = uniform_rsrc(p.C + (size_t)row0 * p.ldc, rows_c * p.ldc * 2);
       // TR: the bias of the lane's 4 consecutive columns 16 g + 4 q .. + 3 of each n-tile g (8 B loads; N % 8
       // == 0, so a group lies wholly inside or past the last column)
-      float tbias[NT][4];
+      // (kept packed, 2 VGPRs per group, unpacked per use; the column base is made opaque so the loads are not
+      // hoisted above the main loop, where 32 live floats made this kernel spill)
+      uint2 tbias[NT];
       if constexpr (TR && (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
+        int cb = n0 + wn * 16 * NT + 4 * q;
+        asm volatile("" : "+v"(cb));
 #pragma unroll
         for (int g = 0; g < NT; ++g) {
-          const int col = n0 + wn * 16 * NT + g * 16 + 4 * q;
-          uint2 b2 = {0u, 0u};
-          if (col < p.N) b2 = *reinterpret_cast<const uint2*>(p.R + col);
-          tbias[g][0] = __uint_as_float(b2.x << 16);
-          tbias[g][1] = __uint_as_float(b2.x & 0xffff0000u);
-          tbias[g][2] = __uint_as_float(b2.y << 16);
-          tbias[g][3] = __uint_as_float(b2.y & 0xffff0000u);
+          const int col = cb + g * 16;
+          tbias[g] = col < p.N ? *reinterpret_cast<const uint2*>(p.R + col) : uint2{0u, 0u};
         }
       }
       // TR / TRR: the lane's 16 B chunk of column pair g2 of an m-tile (the layout of the TR stores below):
@@ -554,9 +557,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
                   v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
               }
             } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+              const float tb[4] = {__uint_as_float(tbias[g].x << 16), __uint_as_float(tbias[g].x & 0xffff0000u),
+                                   __uint_as_float(tbias[g].y << 16), __uint_as_float(tbias[g].y & 0xffff0000u)};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float y = acc[i][g][e] + tbias[g][e];
+                const float y = acc[i][g][e] + tb[e];
                 v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(y) : y;
               }
             } else {
@@ -829,6 +834,10 @@ extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, 
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
   const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
+  // grouped tile order: an XCD's wpx consecutive tiles run gm m-tiles down each n column.  Auto (gm <= 0): 4
+  // for the decode projections (up to 128 n-tiles: o / down / qkv / gate|up at M = 4096 read 1-4 % faster
+  // than with 8 in scripts/microbench.py g4ab, G4_GMS), 8 for the vocabulary projection's 501 n-tiles
+  if (gm <= 0) gm = tiles_n > 128 ? 8 : 4;
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
            tiles_m, tiles_n, K / 64, std::max(1, gm), wpx, tiles, ss, P, ssld, eps};
   return bn == 256 ? dispatch<8>(p, epi, s, var, rs_mode) : dispatch<6>(p, epi, s, var, rs_mode);

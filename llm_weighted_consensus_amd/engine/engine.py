@@ -1008,17 +1008,21 @@ class LLMEngine:
         g.replay()
 
     def _step_ab(self, bk: _GraphBucket, fwd) -> None:
-        """In-step A/B of the model's candidate plans for this bucket (``step_plans``: the isolated planner's
-        choice, all-library, all-hand-written): each is captured into a graph of its own and replayed on this
-        step's real inputs (a decode replay rewrites the same KV slots with the same values, nothing else), the
-        fastest by median replay time becomes the bucket's plan.  Isolated per-GEMM timings do not see the
-        step's clock and cache state; this measures the thing that runs.  ``LWC_STEP_AB=0`` keeps the
-        planner's choice.  Results in ``self.step_ab[B]`` and on stderr."""
+        """In-step A/B of the model's plans for this bucket: every candidate is captured into a graph of its own
+        and replayed on this step's real inputs (a decode replay rewrites the same KV slots with the same
+        values, nothing else); the median of 5 replays ranks it.  Round 1 ranks whole plans (``step_plans``: the
+        isolated planner's choice, all-library, all-hand-written); then one coordinate-descent pass over
+        single-decision moves from the best (``step_moves``: one projection's backend, one norm point folded or
+        not, a consumer's schedule, a producer's mode), each kept when it beats the incumbent by more than
+        0.2 %.  Isolated per-GEMM timings do not see the step's clock and cache state (they flipped choices
+        that lost 0.5 % in the bench); this measures the thing that runs.  ``LWC_STEP_AB=0`` keeps the
+        planner's choice, ``LWC_STEP_AB=plans`` skips the moves, ``LWC_STEP_PLAN=<name>`` runs that whole plan
+        (profiling).  Decided once per model and batch; results in ``self.step_ab[B]`` and on stderr."""
         self.step_ab[bk.B] = {}
-        if os.environ.get("LWC_STEP_AB", "1") == "0" or not hasattr(self.model, "step_plans"):
+        mode = os.environ.get("LWC_STEP_AB", "1")
+        if mode == "0" or not hasattr(self.model, "step_plans"):
             return
-        # decided once per model and batch: every engine on the model then runs the same kernels (engines
-        # compared against each other, a re-created engine)
+        # every engine on the model then runs the same kernels (engines compared against each other)
         done = self.model.__dict__.setdefault("step_ab_done", {})
         if bk.B in done:
             self.step_ab[bk.B] = done[bk.B]
@@ -1027,9 +1031,9 @@ class LLMEngine:
         if len(plans) < 2:
             return
         dev = self.device
-        times = {}
         s = torch.cuda.Stream(device=dev)
-        for name, plan in plans.items():
+
+        def capture(plan):
             self.model.apply_step_plan(bk.B, plan)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
@@ -1039,23 +1043,55 @@ class LLMEngine:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 out = fwd()
             g.replay()
-            ts = []
-            for _ in range(3):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                g.replay()
-                e1.record()
-                e1.synchronize()
-                ts.append(e0.elapsed_time(e1))
-            times[name] = sorted(ts)[1]
-            del g, out
+            return g, out
+
+        def replay_ms(g) -> float:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1)
+
+        def race(graphs: dict, rounds: int = 4) -> dict:
+            # interleaved replays (ABAB...): the clock's drift hits every candidate alike; median per candidate
+            ts = {k: [] for k in graphs}
+            for _ in range(rounds):
+                for k, (g, _) in graphs.items():
+                    ts[k].append(replay_ms(g))
+            return {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
+
+        graphs = {name: capture(plan) for name, plan in plans.items()}
+        times = race(graphs, 5)
         best = min(times, key=times.get)
-        self.model.apply_step_plan(bk.B, plans[best])
+        cur, t_cur = plans[best], times[best]
+        inc = graphs.pop(best)
+        del graphs
+        kept = []
+        if mode != "plans" and hasattr(self.model, "step_moves"):
+            # coordinate descent: each move raced against the incumbent (both graphs alive); kept when the
+            # incumbent / move ratio says > 0.25 % faster, and the incumbent becomes the new plan
+            for label, delta in self.model.step_moves(bk.B, cur):
+                cand = self.model.with_move(cur, delta)
+                gm = capture(cand)
+                r = race({"inc": inc, "mv": gm})
+                times[label] = r["mv"] * t_cur / r["inc"]  # on the incumbent's scale
+                if r["mv"] < r["inc"] * 0.9975:
+                    cur, inc, t_cur = cand, gm, times[label]
+                    kept.append(label)
+                else:
+                    del gm
+        del inc
+        forced = os.environ.get("LWC_STEP_PLAN")
+        if forced in plans:
+            cur, kept = plans[forced], [f"forced {forced}"]
+        self.model.apply_step_plan(bk.B, cur)
         torch.cuda.empty_cache()
-        self.step_ab[bk.B] = done[bk.B] = dict(times, choice=best)
+        self.step_ab[bk.B] = done[bk.B] = dict({k: round(v, 3) for k, v in times.items()}, choice=best,
+                                                moves=kept, final=round(t_cur, 3))
         plan = self.model.plan_summary(bk.B) if hasattr(self.model, "plan_summary") else {}
         print(f"# step A/B at batch {bk.B}: " + " ".join(f"{k}={v:.2f}ms" for k, v in times.items())
-              + f" -> {best} {plan}", file=sys.stderr, flush=True)
+              + f" -> {best} + {kept} ({t_cur:.2f} ms) {plan}", file=sys.stderr, flush=True)
 
     def _launch(self, seqs: List[Sequence], sample: bool = True) -> _Step:
         """Stage inputs, replay the decode graph and launch the sampler for `seqs`; results are

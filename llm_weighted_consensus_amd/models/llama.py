@@ -548,6 +548,55 @@ class LlamaModel:
         plans["own"] = {"choices": own, "chain": chain}
         return plans
 
+    def step_moves(self, M: int, plan: dict) -> list:
+        """Single-decision changes of ``plan`` (the engine's coordinate-descent A/B, after the whole-plan
+        round): each projection's backend (hipBLASLt <-> its fastest hand-written core) where the norm chain
+        does not own it, each norm point folded or not, the consumers' schedule / tile width, the producers'
+        mode.  [(label, delta)]: ``with_move(plan, delta)`` applies one."""
+        keys = self._plan_keys(M)
+        own = {}
+        for n, k in keys.items():
+            t = {b: v for b, v in gemm_plan.TIMINGS.get(k, {}).items() if b != "blas" and isinstance(v, float)}
+            own[n] = min(t, key=t.get) if t else None
+        ch = plan.get("chain")
+        owned = set()
+        if ch is not None and self.chain is not None and M <= self.chain.max_rows:
+            owned = {n for n, pt in (("qkv", "attn"), ("gu", "mlp"), ("lm", "final")) if ch.get(pt)}
+            if ch.get("mlp") and ch.get("o") in ("own32", "own64"):
+                owned.add("o")
+            if (ch.get("attn") or ch.get("final")) and ch.get("down") in ("own32", "own64"):
+                owned.add("down")
+        moves = []
+
+        def variant(label, choices=None, chain=None):
+            moves.append((label, {"choices": dict(choices or {}), "chain": dict(chain or {})}))
+
+        for n in keys:
+            c = plan["choices"].get(n)
+            if n in owned or own[n] is None:
+                continue
+            variant(f"{n}={'blas' if c != 'blas' else own[n]}", {n: "blas" if c != "blas" else own[n]})
+        if ch is not None and self.chain is not None and M <= self.chain.max_rows:
+            for pt in ("attn", "mlp", "final"):
+                variant(f"{pt}_fold={not ch.get(pt)}", chain={pt: not ch.get(pt)})
+            for key, alts in (("qkv_var", (32, 64)), ("gu_var", (32, 64)), ("lm_var", (32, 64)), ("qkv_bn", (192, 256))):
+                cur = ch.get(key, alts[0])
+                for v in alts:
+                    if v != cur:
+                        variant(f"{key}={v}", chain={key: v})
+            for key in ("o", "down"):
+                for v in ("own32", "own64", "sumsq"):
+                    if v != ch.get(key):
+                        variant(f"{key}_producer={v}", chain={key: v})
+        return moves
+
+    @staticmethod
+    def with_move(plan: dict, delta: dict) -> dict:
+        """``plan`` with one :meth:`step_moves` delta applied (choices and chain entries overridden)."""
+        ch = plan.get("chain")
+        return {"choices": dict(plan["choices"], **delta.get("choices", {})),
+                "chain": dict(ch, **delta.get("chain", {})) if ch is not None else None}
+
     def apply_step_plan(self, M: int, plan: dict) -> None:
         """Make ``plan`` (one of :meth:`step_plans`) the choice of every projection at M (and of the norm chain)."""
         keys = self._plan_keys(M)

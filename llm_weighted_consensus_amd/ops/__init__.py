@@ -425,7 +425,7 @@ def skinny_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
            gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0,
-           gm: int = 8) -> torch.Tensor:
+           gm: int = 0) -> torch.Tensor:
     """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
     a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
     workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
@@ -435,7 +435,7 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     its accumulator rows by 1/rms of its input rows from the chain's partial row sums of squares (the norm
     weight folded into W: rmsnorm(x) . W^T), and a residual projection writes the partials of its output for
     the next one.  ``var``: schedule (64: wave-local epilogue + next-tile prefetch, else 32: block-staged
-    epilogue); ``gm``: m-tiles per group of the grouped tile order."""
+    epilogue); ``gm``: m-tiles per group of the grouped tile order (0: by shape, see gemm4w.hip)."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)

@@ -226,7 +226,7 @@ def gemm4w_ab(dev):
         # gemm4w at both schedules (32: block-staged epilogue, 64: wave-local epilogue + next-tile prefetch;
         # G4_VARS selects) and both tile widths
         vars_ = [int(v) for v in os.environ.get("G4_VARS", "32,64").split(",")]
-        gms = [int(v) for v in os.environ.get("G4_GMS", "8").split(",")]
+        gms = [int(v) for v in os.environ.get("G4_GMS", "0").split(",")]  # 0: the kernel's choice by shape
         vg = [(v, gm) for v in vars_ for gm in gms]
 
         def nm(p, v, gm):

@@ -96,6 +96,17 @@ def test_step_plans_candidates_and_apply(monkeypatch):
         assert all(gemm_plan._CHOICE[k] == "g4p" for k in keys.values()) and m.chain_m[M]["mlp"]
         s = m.plan_summary(M)
         assert s["gu"] == "g4 rs v64" and s["o"] == "g4 rs2 v64" and s["qkv"] == "g4 rs192 v32"
+        # coordinate-descent moves: from the all-own plan (chain owns every projection) only chain decisions
+        labels = [lb for lb, _ in m.step_moves(M, plans["own"])]
+        assert "attn_fold=False" in labels and "gu_var=32" in labels and "o_producer=sumsq" in labels
+        assert not any(lb.startswith(("qkv=", "gu=", "lm=")) for lb in labels)
+        # from the planner's plan: the projections the chain does not own can switch backend
+        mv = dict(m.step_moves(M, plans["planner"]))
+        assert "gu=g4p" in mv and "qkv=g4p" not in mv
+        p1 = m.with_move(plans["planner"], mv["gu=g4p"])
+        assert p1["choices"]["gu"] == "g4p" and p1["chain"] == plans["planner"]["chain"]
+        p2 = m.with_move(p1, mv["mlp_fold=True"])  # moves compose
+        assert p2["chain"]["mlp"] and p2["choices"]["gu"] == "g4p" and not plans["planner"]["chain"]["mlp"]
         m.apply_step_plan(M, plans["library"])
         assert m.plan_summary(M) == {n: "blas" for n in keys}
     finally:
