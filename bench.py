@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cp", type=int, default=0,
                     help="candidate-parallel degree (ranks sharing one request's candidates); 0 = auto: "
                          "min(world, candidates // 32) so every GPU keeps >= 32 candidates per request")
+    ap.add_argument("--kv-fraction", type=float, default=0.5,
+                    help="share of the free device memory the engine's paged KV cache takes")
     ap.add_argument("--profile-steps", action="store_true", help="print a per-phase breakdown")
     return ap.parse_args()
 
@@ -100,7 +102,8 @@ def main():
     # memory at the same time, so each takes its share of the fraction
     shared = os.environ.get("LWC_SHARE_ONE_GPU") == "1" and W > 1
     engine = LLMEngine(model, tok, max_batch=Rg * n_local, max_model_len=max_len, use_graphs=not a.no_graphs,
-                       kv_memory_fraction=0.5 / W if shared else 0.5, prefix_sharing=not a.no_prefix_sharing)
+                       kv_memory_fraction=a.kv_fraction / W if shared else a.kv_fraction,
+                       prefix_sharing=not a.no_prefix_sharing)
     scorer = EmbeddingConsensus(encoder, tau=0.05, max_tokens=512)
     gen = torch.Generator().manual_seed(99)
 

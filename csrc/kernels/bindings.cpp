@@ -27,7 +27,7 @@ int lwc_grouped_gemm(const void*, const void*, void*, const int*, const float*, 
 int lwc_gemm8p(const void*, const void*, void*, const void*, float*, int*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8p_slots();
 int lwc_gemm4w(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, float*, int, int, int,
-               float, int, int, hipStream_t);
+               float, int, int, int, int, float*, int*, hipStream_t);
 int lwc_rms_rowsumsq(const void*, float*, int, int, hipStream_t);
 int lwc_skinny_gemm(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 int lwc_gemm8g_fp8(const void*, const void*, void*, const int*, const int*, const float*, const float*, int, int, int,
@@ -426,7 +426,8 @@ void gemm8p(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
 // and scales the accumulator rows by rsqrt(sum / K + eps); rs_mode 2 (epi 1, bn 256) writes ss [N/256, M].
 void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::optional<at::Tensor>& R, int64_t epi,
             int64_t bn, const c10::optional<at::Tensor>& ss, int64_t rs_mode, int64_t P, double eps, int64_t var,
-            int64_t gm) {
+            int64_t gm, int64_t splits, int64_t split_from, const c10::optional<at::Tensor>& part,
+            const c10::optional<at::Tensor>& cnt) {
   const void* r = gemm_operands(A, W, C, R, epi);
   const int M = (int)A.size(0), K = (int)A.size(1), N = (int)W.size(0);
   TORCH_CHECK(bn == 256 || bn == 192, "gemm4w: bn must be 256 or 192");
@@ -445,9 +446,21 @@ void gemm4w(const at::Tensor& A, const at::Tensor& W, at::Tensor& C, const c10::
     }
     ssp = ss->data_ptr<float>();
   }
+  if (splits > 1) {
+    // split-K workspace, checked here against what the kernel will index (a short buffer would fault)
+    const long long tiles = (long long)((M + 255) / 256) * ((N + bn - 1) / bn);
+    const long long split_tiles = tiles - std::min<long long>(std::max<long long>(split_from, 0), tiles);
+    TORCH_CHECK(part.has_value() && cnt.has_value(), "gemm4w: split-K needs part and cnt");
+    CHECK_GPU(*part); CHECK_DTYPE(*part, at::kFloat); CHECK_CONTIG(*part);
+    CHECK_GPU(*cnt); CHECK_DTYPE(*cnt, at::kInt); CHECK_CONTIG(*cnt);
+    TORCH_CHECK(part->numel() >= split_tiles * (splits - 1) * 256 * bn, "gemm4w: split-K partial slab too small");
+    TORCH_CHECK(cnt->numel() >= 2 * tiles, "gemm4w: split-K counters too small");
+  }
   CHECK_RC(lwc_gemm4w(A.data_ptr(), W.data_ptr(), C.data_ptr(), r, M, N, K, (int)A.stride(0), (int)C.stride(0),
                       (int)epi, (int)bn, ssp, ssp ? (int)ss->size(1) : 0, (int)rs_mode, (int)P, (float)eps, (int)var,
-                      (int)gm, cur_stream()),
+                      (int)gm, (int)splits, (int)split_from,
+                      part.has_value() ? part->data_ptr<float>() : nullptr,
+                      cnt.has_value() ? cnt->data_ptr<int>() : nullptr, cur_stream()),
            "gemm4w");
 }
 

@@ -86,6 +86,15 @@ struct Params {
   int P;            // RS 1: partials per row (<= 16)
   int ssld;         // floats between partials (a multiple of 4: 16-byte aligned LDS-DMA sources)
   float eps;        // RS 1
+  // split-K (VAR 64): tiles [0, full) run whole; every tile t >= full runs as S units over K ranges of KT / S
+  // K tiles.  The first S - 1 arrivers (a ticket from cnt[t]) store their fp32 accumulators into part, then
+  // count themselves in done[t]; the last arriver waits for those (they already run: no deadlock), adds
+  // the partials and runs the epilogue.  cnt / done are zero between calls (zeroed once, reset by each
+  // tile's last arriver).
+  int full, S, units;
+  float* part;      // [(tiles - full) * (S - 1)][8 NT][256] float4
+  int* cnt;         // [tiles]
+  int* done;        // [tiles]
 };
 
 template <int NT>
@@ -116,6 +125,16 @@ LWC_DEVICE void mfma2(float4v& d, const uint4v& a, const uint4v& b) {
 #define G4_BAR() __builtin_amdgcn_s_barrier()
 #define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 #define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// the wave-local epilogue's accumulators of m-tile I into AV[NT] (VGPRs): the tile's own, plus the partial
+// sums of the other split-K units when this workgroup is a split tile's last arriver (nsl slabs at pslab)
+#define G4_ACC_LOAD(AV, I)                                                                     \
+  do {                                                                                         \
+    _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];                     \
+    for (int u_ = 0; u_ < nsl; ++u_) {                                                         \
+      _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_)                                        \
+        AV[g_] += pslab[((size_t)u_ * 8 * NT + (I) * NT + g_) * 256 + tid];                    \
+    }                                                                                          \
+  } while (0)
 
 // Diagnostic build only (scripts/probes/g4_stamps.cpp defines LWC_G4_STAMPS): wave 0 of every workgroup
 // records s_memrealtime at up to eight points of each persistent round (and s_memtime at the first and last)
@@ -154,6 +173,17 @@ LWC_DEVICE float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __expf(-z));
 }
 
+// work unit u -> (tile, first K tile, K tile count): whole tiles first, then the split tiles' S units each
+// (consecutive: one tile's units land on one XCD's wpx consecutive units, its partials stay in that L2)
+LWC_DEVICE void unit_tile(const Params& p, int u, int& t, int& kt0, int& nkt) {
+  if (u < p.full) {
+    t = u, kt0 = 0, nkt = p.KT;
+  } else {
+    const int v = u - p.full, per = p.KT / p.S;
+    t = p.full + v / p.S, kt0 = (v % p.S) * per, nkt = per;
+  }
+}
+
 LWC_DEVICE void tile_mn(const Params& p, int t, int& m, int& n) {
   const int group = p.gm * p.tiles_n;
   const int first_m = (t / group) * p.gm;
@@ -174,7 +204,7 @@ LWC_DEVICE int swz(int row, int col) {
 // LDS bytes: the two K tiles, then the RS area (RS 1: P x 256 partials + 256 row scales; RS 2: row sums)
 template <int NT, int RS>
 constexpr int lds_bytes() {
-  return Geo<NT>::Lds + (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0));
+  return Geo<NT>::Lds + (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0)) + 16;  // (+ the split-K ticket word)
 }
 
 template <int EPI, int NT, int VAR, int RS>
@@ -195,6 +225,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   // RS 1: the P x 256 partials (16 KiB) and the 256 row scales (1 KiB) after the K buffers; RS 2: the four
   // waves' 128 row sums (2 KiB) at the same place
   constexpr int RSOFF = G::Lds, RSV = RSOFF + 16384;
+  constexpr int SKOFF = lds_bytes<NT, RS>() - 16;  // split-K: the workgroup's arrival ticket
   // LDS-DMA piece k (64 lanes x 16 B = 256 rows x fp32) of partial k of m-tile rows [m, m + 256)
   auto ss_dma = [&](int m, int k) {
     const __amdgpu_buffer_rsrc_t rR = uniform_rsrc(p.ss + (size_t)k * p.ssld + m, (p.M - m) * 4);
@@ -203,8 +234,10 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   };
 
   for (int round = 0;; ++round) {
-    const int tile = round * 8 * p.wpx + xcd * p.wpx + j;
-    if (tile >= p.tiles) break;
+    const int unit = round * 8 * p.wpx + xcd * p.wpx + j;
+    if (unit >= p.units) break;
+    int tile, kt0, nkt;
+    unit_tile(p, unit, tile, kt0, nkt);
     int tm, tn;
     tile_mn(p, tile, tm, tn);
     const int m0 = tm * 256, n0 = tn * G::BN;
@@ -223,10 +256,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     const uint32_t voW = (uint32_t)((drow * p.K + dchk) * 2);
     const int sA = 32 * p.lda * 2, sW = 32 * p.K * 2;  // bytes between pieces
     const int dst0 = wid * 1024;
+    // (a split unit's K range starts kt0 K tiles in: the resources start there)
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.A + (size_t)m0 * p.lda), (short)0, (p.M - m0) * p.lda * 2, 0x00020000);
+        (void*)(p.A + (size_t)m0 * p.lda + kt0 * 64), (short)0, (p.M - m0) * p.lda * 2 - kt0 * 128, 0x00020000);
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.W + (size_t)n0 * p.K), (short)0, min(p.N - n0, G::BN) * p.K * 2, 0x00020000);
+        (void*)(p.W + (size_t)n0 * p.K + kt0 * 64), (short)0, min(p.N - n0, G::BN) * p.K * 2 - kt0 * 128, 0x00020000);
     // LDS-DMA piece k of one K tile (k < 8: A rows, else W rows)
     auto piece = [&](uint8_t* buf, int kt, int k) {
       if (k < 8)
@@ -246,14 +280,20 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // the freed buffers instead: every piece a real memory request — pieces past a resource's end complete
     // out of order with the real ones before them, and a counted vmcnt wait then passes too early
     // (measured: wrong results at every K tile count past 2)
-    const int ntile = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
-    const bool pf = PAP && ntile < p.tiles;
-    int um = tm, un = tn;
-    if (pf) tile_mn(p, ntile, um, un);
+    const int nunit = (round + 1) * 8 * p.wpx + xcd * p.wpx + j;
+    const bool pf = PAP && nunit < p.units;
+    int um = tm, un = tn, ukt0 = kt0;
+    if (pf) {
+      int ut, unkt;
+      unit_tile(p, nunit, ut, ukt0, unkt);
+      tile_mn(p, ut, um, un);
+    }
     const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.A + (size_t)um * 256 * p.lda), (short)0, (p.M - um * 256) * p.lda * 2, 0x00020000);
+        (void*)(p.A + (size_t)um * 256 * p.lda + ukt0 * 64), (short)0, (p.M - um * 256) * p.lda * 2 - ukt0 * 128,
+        0x00020000);
     const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.W + (size_t)un * G::BN * p.K), (short)0, min(p.N - un * G::BN, G::BN) * p.K * 2, 0x00020000);
+        (void*)(p.W + (size_t)un * G::BN * p.K + ukt0 * 64), (short)0,
+        min(p.N - un * G::BN, G::BN) * p.K * 2 - ukt0 * 128, 0x00020000);
     auto npiece = [&](uint8_t* buf, int kt, int k) {  // piece k of the NEXT tile's K tile kt
       if (k < 8)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -286,7 +326,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 
     // (VAR 64 takes even K tile counts only — the host falls back to VAR 32 — so the next tile's first
     // two K tiles, DMA'd inside the last two iterations, land in buffers 0 and 1)
-    const int nt = KT;
+    const int nt = nkt;  // (a split unit: its share of the K tiles; even, like every VAR 64 count)
+    (void)KT;
     // VAR 64 ("prefetch across persistent tiles"): from the second tile on, this tile's first two K tiles
     // were issued by the previous tile right after its main loop, under its epilogue; the waits below then
     // also cover the previous epilogue's memory ops issued after them (stricter, still exact for the data)
@@ -420,6 +461,56 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // drain vmcnt(0) — the next tile's K-tile DMA issued in the last iteration — before the epilogue starts
     if constexpr (!PAP) __syncthreads();
     G4_STAMP(round, 2);
+    int nsl = 0;                    // split-K last arriver: partial slabs to add in the epilogue
+    const float4v* pslab = nullptr;
+    if constexpr (PAP) {
+      // split-K (tile >= full, wave-uniform): arrival ticket; the first S - 1 arrivers publish their partial
+      // sums and leave, the last one adds them and runs the epilogue.  Publication: plain stores, every wave's
+      // vmcnt(0), the block barrier, lane 0's agent release fence + vmcnt(0), then the relaxed count in
+      // done[tile]; the last arriver polls done[tile] relaxed, takes one agent acquire fence, and the block
+      // barrier orders its plain loads (MI355X_MICROARCH.md, Workgroup dispatch: valid forms)
+      if (tile >= p.full) {
+        int* tk = reinterpret_cast<int*>(smem + SKOFF);
+        if (tid == 0) tk[0] = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int ticket = __builtin_amdgcn_readfirstlane(tk[0]);
+        float4v* slab = reinterpret_cast<float4v*>(p.part) + (size_t)(tile - p.full) * (p.S - 1) * (8 * NT * 256);
+        if (ticket < p.S - 1) {
+          float4v* mine = slab + (size_t)ticket * (8 * NT * 256);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int jj = 0; jj < NT; ++jj) mine[(i * NT + jj) * 256 + tid] = acc[i][jj];
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(p.done + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          continue;  // this unit's work is in the partial: no epilogue
+        }
+        if (tid == 0) {
+          // the units waited for hold earlier tickets: they are running and wait on nothing.  Bounded anyway
+          // (~0.3 s), so a broken hand-off cannot hang the GPU
+          for (int it = 0; it < (1 << 21); ++it) {
+            if (__hip_atomic_load(p.done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= p.S - 1) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // every unit of this tile has counted itself: reset for the next call
+          __hip_atomic_store(p.done + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        // the partials are added where the epilogue reads the accumulators (G4_ACC): the accumulators stay
+        // as the MFMAs left them (rewriting them here made the register allocator rotate all of them through
+        // v_accvgpr_mov copies, caught by the build's ISA guard)
+        nsl = p.S - 1;
+        pslab = slab;
+      }
+    }
 
     constexpr int CW = EPI == EPI_SWIGLU ? 8 * NT : 16 * NT;
     if constexpr (PAP) {
@@ -474,6 +565,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         // the 4 lanes of the row (xor 16, 32)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
+          float4v av[NT];  // the m-tile's accumulators (+ the split-K partials of the other units)
+          G4_ACC_LOAD(av, i);
           uint4v res[NT / 2];
 #pragma unroll
           for (int g2 = 0; g2 < NT / 2; ++g2) res[g2] = rv[i & 1][g2];
@@ -488,8 +581,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             float x[8], y[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * g2][e]),
-                                                              __float_as_uint(acc[i][2 * g2 + 1][e]), false, false);
+              const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(av[2 * g2][e]),
+                                                              __float_as_uint(av[2 * g2 + 1][e]), false, false);
               x[e] = __uint_as_float(r[0]);
               x[e + 4] = __uint_as_float(r[1]);
             }
@@ -541,6 +634,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           uint32_t o[NO][2];
+          float4v av[NT];  // the m-tile's accumulators (+ the split-K partials of the other units)
+          G4_ACC_LOAD(av, i);
           // RS 1 (folded RMSNorm consumer): every value of the lane's row i * 16 + r16 takes the row's 1/rms
           float sc = 1.f;
           if constexpr (RS == 1) sc = reinterpret_cast<const float*>(smem + RSV)[wm * 128 + i * 16 + r16];
@@ -552,21 +647,21 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 if constexpr (RS == 1)
-                  v[e] = silu(acc[i][gate][e] * sc) * (acc[i][gate + 2][e] * sc);
+                  v[e] = silu(av[gate][e] * sc) * (av[gate + 2][e] * sc);
                 else
-                  v[e] = silu(acc[i][gate][e]) * acc[i][gate + 2][e];
+                  v[e] = silu(av[gate][e]) * av[gate + 2][e];
               }
             } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
               const float tb[4] = {__uint_as_float(tbias[g].x << 16), __uint_as_float(tbias[g].x & 0xffff0000u),
                                    __uint_as_float(tbias[g].y << 16), __uint_as_float(tbias[g].y & 0xffff0000u)};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float y = acc[i][g][e] + tb[e];
+                const float y = av[g][e] + tb[e];
                 v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(y) : y;
               }
             } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = RS == 1 ? acc[i][g][e] * sc : acc[i][g][e];
+              for (int e = 0; e < 4; ++e) v[e] = RS == 1 ? av[g][e] * sc : av[g][e];
             }
             o[g][0] = pack_bf16x2(v[0], v[1]);
             o[g][1] = pack_bf16x2(v[2], v[3]);
@@ -819,9 +914,10 @@ int device_cus() {
 // squares (epi 0 / 2) scales the accumulator rows by rsqrt(sum / K + eps); ss [N/256][ssld] (epi 1, bn 256)
 // makes the residual epilogue write those partials of its output.  var: schedule, 64 or 32 (anything else).
 // gm: m-tiles per group of the grouped tile order (an XCD's consecutive tiles run gm m-tiles down each n column).
+// splits / split_from / part / cnt: split-K of the tiles from split_from on (VAR 64; see Params).
 extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldc,
                           int epi, int bn, float* ss, int ssld, int rs_mode, int P, float eps, int var, int gm,
-                          hipStream_t s) {
+                          int splits, int split_from, float* part, int* cnt, hipStream_t s) {
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
@@ -833,12 +929,24 @@ extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, 
   if (rs_mode == 2 && (epi != EPI_RESIDUAL || bn != 256)) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
-  const int wpx = std::min(device_cus() / 8, (tiles + 7) / 8);
+  // split-K (VAR 64 only): tiles [split_from, tiles) run as `splits` units of K / splits each (an even K tile
+  // count, like every VAR 64 unit); workspace part [(tiles - split_from) * (splits - 1) * 256 * bn] fp32,
+  // cnt [2 * tiles] int32 zeroed once
+  const int KT = K / 64;
+  if (splits > 1) {
+    if (var != 64 || KT % splits != 0 || (KT / splits) % 2 != 0 || part == nullptr || cnt == nullptr) return -1;
+  } else {
+    splits = 1;
+  }
+  const int full = splits > 1 ? std::max(0, std::min(split_from, tiles)) : tiles;
+  const int units = full + (tiles - full) * splits;
+  const int wpx = std::min(device_cus() / 8, (units + 7) / 8);
   // grouped tile order: an XCD's wpx consecutive tiles run gm m-tiles down each n column.  Auto (gm <= 0): 4
   // for the decode projections (up to 128 n-tiles: o / down / qkv / gate|up at M = 4096 read 1-4 % faster
   // than with 8 in scripts/microbench.py g4ab, G4_GMS), 8 for the vocabulary projection's 501 n-tiles
   if (gm <= 0) gm = tiles_n > 128 ? 8 : 4;
   Params p{(const lwc::bf16_t*)A, (const lwc::bf16_t*)W, (lwc::bf16_t*)C, (const lwc::bf16_t*)R, M, N, K, lda, ldc,
-           tiles_m, tiles_n, K / 64, std::max(1, gm), wpx, tiles, ss, P, ssld, eps};
+           tiles_m, tiles_n, KT, std::max(1, gm), wpx, tiles, ss, P, ssld, eps, full, splits, units, part, cnt,
+           cnt ? cnt + tiles : nullptr};
   return bn == 256 ? dispatch<8>(p, epi, s, var, rs_mode) : dispatch<6>(p, epi, s, var, rs_mode);
 }

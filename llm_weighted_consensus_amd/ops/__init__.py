@@ -425,7 +425,7 @@ def skinny_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
 def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, swiglu: bool = False, bias: Optional[torch.Tensor] = None,
            gelu: bool = False, bn: int = 256, chain: "Optional[NormChain]" = None, var: int = 0,
-           gm: int = 0) -> torch.Tensor:
+           gm: int = 0, splits: int = 1, split_from: int = 0) -> torch.Tensor:
     """4-wave interleaved MFMA GEMM (K6, csrc/kernels/gemm4w.hip): one wave per SIMD owns a 128 x bn/2 slice of
     a 256 x ``bn`` tile (bn 256 or 192) with its 256 (192) fp32 accumulators in AGPRs; data-parallel tiles, no
     workspace.  Same epilogues as :func:`gemm8p`: ``residual`` (in place with ``out=residual``), ``swiglu``
@@ -435,7 +435,13 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     its accumulator rows by 1/rms of its input rows from the chain's partial row sums of squares (the norm
     weight folded into W: rmsnorm(x) . W^T), and a residual projection writes the partials of its output for
     the next one.  ``var``: schedule (64: wave-local epilogue + next-tile prefetch, else 32: block-staged
-    epilogue); ``gm``: m-tiles per group of the grouped tile order (0: by shape, see gemm4w.hip)."""
+    epilogue); ``gm``: m-tiles per group of the grouped tile order (0: by shape, see gemm4w.hip).
+
+    Split-K (``splits`` > 1, schedule 64): the output tiles from ``split_from`` on run as ``splits`` units over
+    K / splits each; the first arrivers publish fp32 partials, the last adds them and runs the epilogue (no
+    workgroup waits on one that has not started).  For shapes whose tile count leaves CUs idle (the serving
+    path's mid-size row counts: :func:`split_plan`) and a ragged last round (``split_from`` = the whole
+    rounds).  The workspace is this module's, sized before graph capture (:func:`split_workspace`)."""
     N = W.shape[0] // 2 if swiglu else W.shape[0]
     if out is None:
         out = torch.empty(A.shape[0], N, dtype=torch.bfloat16, device=A.device)
@@ -447,26 +453,68 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
         if gelu:
             raise ValueError("gemm4w: gelu needs a bias")
         epi = 2 if swiglu else (1 if residual is not None else 0)
+    sk = (int(splits), int(split_from), None, None)
+    if splits > 1:
+        part, cnt = split_workspace(A.shape[0], W.shape[0], bn, splits, split_from, A.device)
+        sk = (int(splits), int(split_from), part, cnt)
     if chain is None:
         # the kernel addresses A through one 32-bit buffer range: row blocks of < 2 GiB of A, one launch each
         # (the encoders' FFN2 input at config 2's 0.5 M tokens is 3 GiB)
         M = A.shape[0]
         step = max(256, ((1 << 31) - 1) // max(1, A.stride(0) * 2) // 256 * 256)
         if M <= step:
-            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm))
+            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm), *sk)
         else:
             for r0 in range(0, M, step):
                 r1 = min(M, r0 + step)
                 res = residual[r0:r1] if epi == 1 else residual
-                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm))
+                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm),
+                                 1, 0, None, None)
     elif epi == 1:
-        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var), int(gm))
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var), int(gm), *sk)
         chain.P = (N + 255) // 256
     elif epi in (0, 2):
-        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 1, chain.P, chain.eps, int(var), int(gm))
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 1, chain.P, chain.eps, int(var), int(gm), *sk)
     else:
         raise ValueError("gemm4w: chain= goes with the plain, SwiGLU or residual epilogue")
     return out
+
+
+# split-K workspace of gemm4w (per device): fp32 partial slabs + the per-tile ticket / done counters (zeroed
+# once; each tile's last arriver resets its pair).  Grown only outside graph capture.
+_SPLIT_WS: dict = {}
+
+
+def split_workspace(M: int, N: int, bn: int, splits: int, split_from: int, device):
+    """(part, cnt) big enough for a split-K gemm4w call of this shape (W rows N: for SwiGLU the interleaved
+    gate|up rows).  Allocated / grown here, never under graph capture (a capture then needs it pre-sized by an
+    eager call of the same shape: the planners time every backend before capturing)."""
+    tiles = ((M + 255) // 256) * ((N + bn - 1) // bn)
+    need_p = max(0, tiles - max(0, min(split_from, tiles))) * (splits - 1) * 256 * bn
+    need_c = 2 * tiles
+    key = str(device)
+    ws = _SPLIT_WS.get(key)
+    if ws is None or ws[0].numel() < need_p or ws[1].numel() < need_c:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gemm4w split-K workspace must be sized before graph capture")
+        old_p = ws[0].numel() if ws is not None else 0
+        old_c = ws[1].numel() if ws is not None else 0
+        ws = (torch.empty(max(need_p, old_p, 1), dtype=torch.float32, device=device),
+              torch.zeros(max(need_c, old_c), dtype=torch.int32, device=device))
+        _SPLIT_WS[key] = ws
+    return ws
+
+
+def split_plan(M: int, N: int, K: int, bn: int = 256) -> tuple:
+    """(splits, split_from) for a gemm4w call whose tiles leave CUs idle: the whole call split 2 or 4 ways
+    while that fills the GPU at most ~1.25x over (the serving path's mid-size row counts), or (1, 0)."""
+    tiles = ((M + 255) // 256) * ((N + bn - 1) // bn)
+    KT = K // 64
+    cus = 256
+    s = 1
+    while s < 4 and tiles * s * 2 <= cus * 5 // 4 and KT % (2 * s) == 0 and (KT // (2 * s)) % 2 == 0:
+        s *= 2
+    return (s, 0) if s > 1 else (1, 0)
 
 
 class NormChain:

@@ -11,5 +11,7 @@ rc=$?; echo "rocprof rc=$rc"; grep "score requests" gpurun_out/prof_serve.log | 
 STATS=$(find gpurun_out/prof_serve -name "*kernel_stats.csv" | head -1)
 [ -n "$STATS" ] && python3 scripts/summarize_profile.py "$STATS" "serve_load.py (rocprofv3 --kernel-trace --stats)" \
     gpurun_out/prof_serve_summary.md > /dev/null
+TRACE=$(find gpurun_out/prof_serve -name "*kernel_trace.csv" | head -1)
+[ -n "$TRACE" ] && python3 scripts/trace_shapes.py "$TRACE" 40 > gpurun_out/prof_serve_shapes.md
 find gpurun_out/prof_serve -name "*kernel_trace.csv" -delete
 exit $rc

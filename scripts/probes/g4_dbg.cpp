@@ -23,7 +23,7 @@ int main() {
     (void)hipMemcpy(dw, w.data(), w.size() * 2, hipMemcpyHostToDevice);
     for (int var : {32, 64}) {
       (void)hipMemset(dc, 0, c.size() * 2);
-      int rc = lwc_gemm4w(da, dw, dc, nullptr, M, N, K, K, N, 0, 256, nullptr, 0, 0, 1, 1e-5f, var, 8, 0);
+      int rc = lwc_gemm4w(da, dw, dc, nullptr, M, N, K, K, N, 0, 256, nullptr, 0, 0, 1, 1e-5f, var, 8, 1, 0, nullptr, nullptr, 0);
       (void)hipDeviceSynchronize();
       (void)hipMemcpy(c.data(), dc, c.size() * 2, hipMemcpyDeviceToHost);
       double maxe = 0;

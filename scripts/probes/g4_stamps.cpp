@@ -57,15 +57,10 @@ static double med(std::vector<double> v) {
 int main() {
   const Shape shapes[] = {
       {"gate_up+swiglu 4096x28672x4096 VAR64", 4096, 28672, 4096, 2, 64},
-      {"gate_up+swiglu 4096x28672x4096 VAR32", 4096, 28672, 4096, 2, 32},
       {"lm_head 4096x128256x4096 VAR64", 4096, 128256, 4096, 0, 64},
-      {"lm_head 4096x128256x4096 VAR32", 4096, 128256, 4096, 0, 32},
       {"o+res 4096x4096x4096 VAR64", 4096, 4096, 4096, 1, 64},
-      {"o+res 4096x4096x4096 VAR32", 4096, 4096, 4096, 1, 32},
       {"down+res 4096x4096x14336 VAR64", 4096, 4096, 14336, 1, 64},
-      {"down+res 4096x4096x14336 VAR32", 4096, 4096, 14336, 1, 32},
       {"enc o+bias 524288x768x768 VAR64", 524288, 768, 768, 3, 64},
-      {"enc o+bias 524288x768x768 VAR96", 524288, 768, 768, 3, 96},
       {"enc FFN1+bias+GELU 524288x3072x768 VAR64", 524288, 3072, 768, 4, 64},
   };
   const int blocks = lwc::g4w::device_cus();
@@ -87,7 +82,7 @@ int main() {
     CK(hipDeviceSynchronize());
     auto call = [&]() {
       return lwc_gemm4w(A, W, C, R, sh.M, sh.N, sh.K, sh.K, sh.epi == 2 ? sh.N / 2 : sh.N, sh.epi, 256, nullptr, 0, 0,
-                        1, 1e-5f, sh.var, 8, 0);
+                        1, 1e-5f, sh.var, 0, 1, 0, nullptr, nullptr, 0);
     };
     if (call() != 0) {
       fprintf(stderr, "%s: launch refused\n", sh.name);
@@ -146,6 +141,36 @@ int main() {
                med(e), med(d[0]), med(d[1]), med(d[2]), med(d[3]), med(d[4]), med(o), med(m) / (sh.K / 64));
     }
     printf("   sum   | %8.2f | %9.2f | %8.2f | %8.2f\n", sp, sm, se, sh_);
+    // dispatch skew and tail: first / last workgroup start (round 0 S0) and first / last end (last round S7),
+    // relative to the first start
+    {
+      const int last = std::min(rounds, 64) - 1;
+      double s0min = 1e30, s0max = 0, s7min = 1e30, s7max = 0;
+      for (int b = 0; b < blocks; ++b) {
+        const double a0 = (double)at(b, 0, 0, 1);
+        int lr = last;
+        while (lr > 0 && (lr * blocks + (b & 7) * (blocks / 8) + (b >> 3)) >= tiles) --lr;
+        const double a7 = (double)at(b, lr, 7, 1);
+        s0min = std::min(s0min, a0), s0max = std::max(s0max, a0);
+        s7min = std::min(s7min, a7), s7max = std::max(s7max, a7);
+      }
+      printf("   starts %.2f .. %.2f us, ends %.2f .. %.2f us (from the first start)\n", 0.0, (s0max - s0min) * 0.01,
+             (s7min - s0min) * 0.01, (s7max - s0min) * 0.01);
+      // per XCD group (blockIdx % 8: the blocks that share an XCD's L2 under round-robin dispatch): the ends'
+      // spread inside the group, and the group's last end — how much a per-XCD work queue could balance
+      printf("   per XCD group: ");
+      for (int x = 0; x < 8; ++x) {
+        double lo = 1e30, hi = 0;
+        for (int b = x; b < blocks; b += 8) {
+          int lr = last;
+          while (lr > 0 && (lr * blocks + (b & 7) * (blocks / 8) + (b >> 3)) >= tiles) --lr;
+          const double a7 = (double)at(b, lr, 7, 1);
+          lo = std::min(lo, a7), hi = std::max(hi, a7);
+        }
+        printf("[%.0f..%.0f] ", (lo - s0min) * 0.01, (hi - s0min) * 0.01);
+      }
+      printf("\n");
+    }
     CK(hipFree(A));
     CK(hipFree(W));
     CK(hipFree(C));

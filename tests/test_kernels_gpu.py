@@ -1463,3 +1463,58 @@ def test_gemm4w_row_blocks_past_2gib(gpu):
         ref = A[r0:r1].float() @ W.float().t()
         _close(out[r0:r1], ref + b.float(), 3e-2, 1e-2)
         _close(R[r0:r1], ref + R0[r0:r1].float(), 3e-2, 1e-2)
+
+
+@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("M,N,K,epi,split_from", [(2048, 4096, 4096, "res", 0), (700, 2048, 1024, "swiglu", 0),
+                                                  (1000, 128256 // 16, 512, "plain", 64), (300, 6144, 512, "plain", 0),
+                                                  (4352, 4096, 512, "res", 200)])
+def test_gemm4w_split_k(gpu, M, N, K, epi, split_from, splits):
+    """gemm4w split-K (VAR 64): the tiles from split_from on run as `splits` units over K / splits; the first
+    arrivers publish fp32 partials, the last adds them in its epilogue.  Plain / residual / SwiGLU, all tiles
+    or only a tail (whole tiles and split tiles in one launch, several persistent rounds), ragged M / N; three
+    launches in a row (the ticket counters reset by each tile's last arriver); vs fp32."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + N + K + splits)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    for _ in range(3):
+        if epi == "swiglu":
+            F = N // 2
+            out = ops.gemm4w(A, ops.swiglu_interleave(W), swiglu=True, var=64, splits=splits, split_from=split_from)
+            _close(out, torch.nn.functional.silu(ref[:, :F]) * ref[:, F:], 3e-2, 1e-2)
+        elif epi == "res":
+            R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+            want = ref + R.float()
+            _close(ops.gemm4w(A, W, residual=R, out=R, var=64, splits=splits, split_from=split_from), want, 3e-2, 1e-2)
+        else:
+            _close(ops.gemm4w(A, W, var=64, splits=splits, split_from=split_from), ref, 3e-2, 1e-2)
+    torch.cuda.synchronize()
+    _, cnt = ops.split_workspace(M, N, 256, splits, split_from, A.device)
+    assert int(cnt.abs().sum()) == 0  # every tile's counters were reset by its last arriver
+
+
+@pytest.mark.parametrize("splits", [2, 4])
+def test_gemm4w_split_k_norm_chain(gpu, splits):
+    """Split-K with the folded-RMSNorm epilogues: a row-scaled consumer (RS 1) and a residual producer that
+    writes the row sums of squares (RS 2) — only the last arriver of a tile runs them."""
+    from llm_weighted_consensus_amd import ops
+
+    M, N, K, P = 1000, 4096, 1024, 4
+    torch.manual_seed(7 + splits)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    chain = ops.NormChain(M + 64, 256 * 16, 1e-5, gpu)
+    chain.ss[:P, :M] = torch.rand(P, M, device=gpu) * K / P + 0.01
+    chain.P = P
+    rs = torch.rsqrt(chain.ss[:P, :M].sum(0) / K + 1e-5)
+    _close(ops.gemm4w(A, W, chain=chain, var=64, splits=splits), rs[:, None] * (A.float() @ W.float().t()), 3e-2, 1e-2)
+    R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    want = R.float() + A.float() @ W.float().t()
+    C = ops.gemm4w(A, W, residual=R, out=R, chain=chain, var=64, splits=splits)
+    torch.cuda.synchronize()
+    _close(C, want, 3e-2, 1e-2)
+    parts = C.float().pow(2).view(M, N // 256, 256).sum(-1).t()
+    assert torch.allclose(chain.ss[:N // 256, :M], parts, rtol=1e-5, atol=1e-4)
