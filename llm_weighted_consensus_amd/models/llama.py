@@ -275,7 +275,8 @@ class LlamaModel:
             nxt = plan["attn"] if li + 1 < nl else plan["final"]
             self._residual_into(act, L.w_down, x_res, plan["down"] if nxt else "plain")
         if plan["final"]:
-            return ops.gemm4w(x_res, self.lm_head, chain=ch, var=lv)
+            sk = ops.split_plan(T, self.lm_head.shape[0], cfg.hidden) if plan.get("lm_split") and lv == 64 else (1, 0)
+            return ops.gemm4w(x_res, self.lm_head, chain=ch, var=lv, splits=sk[0], split_from=sk[1])
         return self._proj(ops.rmsnorm(x_res, ones, eps), self.lm_head)
 
     def chain_ok(self, M: int) -> bool:
@@ -457,6 +458,7 @@ class LlamaModel:
         cons = {"qkv": {f"qkv_rs{bn}v{v}": (bn, v) for bn in (192, 256) for v in (32, 64)},
                 "gu": {f"gu_rsv{v}": (256, v) for v in (32, 64)},
                 "lm": {f"lm_rsv{v}": (256, v) for v in (32, 64)}}
+        lm_sk = ops.split_plan(M, self.lm_head.shape[0], cfg.hidden)  # lm_head's ragged last round, split
 
         def res(name, inp, var):
             return lambda: ops.gemm4w(inp, w[name], residual=x_res, out=x_res, chain=ch, var=var)
@@ -475,6 +477,8 @@ class LlamaModel:
         for pt, cands in cons.items():
             for k, (bn, v) in cands.items():
                 runs[k] = fold(pt, bn=bn, var=v, swiglu=pt == "gu")
+        if lm_sk[0] > 1:
+            runs["lm_rsv64s"] = fold("lm", bn=256, var=64, splits=lm_sk[0], split_from=lm_sk[1])
         ts = {k: [] for k in runs}
         for _ in range(3):  # interleaved rounds (one process, one device: matched clocks and caches)
             for k, fn in runs.items():
@@ -493,18 +497,22 @@ class LlamaModel:
             k = min(cons[pt], key=lambda c: t[c])
             return k, cons[pt][k]
 
+        lm_split = "lm_rsv64s" in t and t["lm_rsv64s"] < min(t["lm_rsv32"], t["lm_rsv64"])
+
         o_mode, o_extra = producer("o")
         d_mode, d_extra = producer("down")
         (qk, (qkv_bn, qv)), (gk, (_, gv)), (lk, (_, lv)) = consumer("qkv"), consumer("gu"), consumer("lm")
         # each point: folded (consumer + producer's extra) vs the norm kernel + the consumer's best backend
         attn = t[qk] + d_extra < t["norm"] + t["qkv"]
         mlp = t[gk] + o_extra < t["norm"] + t["gu"]
+        if lm_split:
+            lk, lv = "lm_rsv64s", 64
         final = t[lk] + d_extra < t["norm"] + t["lm"]
         force = os.environ.get("LWC_NORM_CHAIN")
         if force is not None:
             attn = mlp = final = force == "1"
         plan = {"attn": attn, "mlp": mlp, "final": final, "qkv_bn": qkv_bn, "qkv_var": qv, "gu_var": gv,
-                "lm_var": lv, "o": o_mode, "down": d_mode}
+                "lm_var": lv, "lm_split": lm_split, "o": o_mode, "down": d_mode}
         self.chain_m[M] = plan
         key = (M, cfg.hidden, 0, "norm_chain")
         gemm_plan.TIMINGS[key] = t
@@ -542,9 +550,11 @@ class LlamaModel:
             def best(cands):
                 return min(cands, key=lambda c: t.get(c, float("inf")))
             q = best([f"qkv_rs{bn}v{v}" for bn in (192, 256) for v in (32, 64)])
+            lm = best(["lm_rsv32", "lm_rsv64", "lm_rsv64s"])
             chain = {"attn": True, "mlp": True, "final": True, "qkv_bn": int(q[6:9]), "qkv_var": int(q[10:]),
-                     "gu_var": int(best(["gu_rsv32", "gu_rsv64"])[6:]), "lm_var": int(best(["lm_rsv32", "lm_rsv64"])[6:]),
-                     "o": best(["o_own32", "o_own64"])[2:], "down": best(["down_own32", "down_own64"])[5:]}
+                     "gu_var": int(best(["gu_rsv32", "gu_rsv64"])[6:]), "lm_var": int(lm[6:8]),
+                     "lm_split": lm.endswith("s"), "o": best(["o_own32", "o_own64"])[2:],
+                     "down": best(["down_own32", "down_own64"])[5:]}
         plans["own"] = {"choices": own, "chain": chain}
         return plans
 
@@ -579,6 +589,8 @@ class LlamaModel:
         if ch is not None and self.chain is not None and M <= self.chain.max_rows:
             for pt in ("attn", "mlp", "final"):
                 variant(f"{pt}_fold={not ch.get(pt)}", chain={pt: not ch.get(pt)})
+            variant(f"lm_split={not ch.get('lm_split', False)}", chain={"lm_split": not ch.get("lm_split", False),
+                                                                        "lm_var": 64})
             for key, alts in (("qkv_var", (32, 64)), ("gu_var", (32, 64)), ("lm_var", (32, 64)), ("qkv_bn", (192, 256))):
                 cur = ch.get(key, alts[0])
                 for v in alts:
@@ -617,7 +629,7 @@ class LlamaModel:
             if c["mlp"]:
                 out["gu"] = f"g4 rs v{c.get('gu_var', 32)}"
             if c["final"]:
-                out["lm"] = f"g4 rs v{c.get('lm_var', 32)}"
+                out["lm"] = f"g4 rs v{c.get('lm_var', 32)}" + (" split-K tail" if c.get("lm_split") else "")
             if c["mlp"] and c["o"] != "plain":
                 out["o"] = out["o"] + "+sumsq" if c["o"] == "sumsq" else f"g4 rs2 v{c['o'][3:]}"
             if (c["attn"] or c["final"]) and c["down"] != "plain":

@@ -505,16 +505,28 @@ def split_workspace(M: int, N: int, bn: int, splits: int, split_from: int, devic
     return ws
 
 
-def split_plan(M: int, N: int, K: int, bn: int = 256) -> tuple:
-    """(splits, split_from) for a gemm4w call whose tiles leave CUs idle: the whole call split 2 or 4 ways
-    while that fills the GPU at most ~1.25x over (the serving path's mid-size row counts), or (1, 0)."""
+def split_plan(M: int, N: int, K: int, bn: int = 256, cus: int = 256) -> tuple:
+    """(splits, split_from) for gemm4w's split-K (VAR 64 units: an even K tile count each), or (1, 0):
+    * fewer tiles than ~3/4 of the CUs (the serving path's mid-size row counts: o / down at M = 2048 are 128
+      tiles): the whole call split 2 or 4 ways, while that stays within ~1.25 rounds;
+    * a ragged last round of at most half the CUs (lm_head at M = 4096: 8016 tiles = 31 rounds + 80): only that
+      round's tiles split, 2 or 4 ways, into at most one round of shorter units."""
     tiles = ((M + 255) // 256) * ((N + bn - 1) // bn)
     KT = K // 64
-    cus = 256
-    s = 1
-    while s < 4 and tiles * s * 2 <= cus * 5 // 4 and KT % (2 * s) == 0 and (KT // (2 * s)) % 2 == 0:
-        s *= 2
-    return (s, 0) if s > 1 else (1, 0)
+
+    def ok(s):
+        return KT % s == 0 and (KT // s) % 2 == 0
+
+    if tiles <= cus * 3 // 4:
+        s = 1
+        while s < 4 and tiles * s * 2 <= cus * 5 // 4 and ok(2 * s):
+            s *= 2
+        return (s, 0) if s > 1 else (1, 0)
+    tail = tiles % cus
+    if 0 < tail <= cus // 2:
+        s = 4 if tail * 4 <= cus and ok(4) else (2 if ok(2) else 1)
+        return (s, tiles - tail) if s > 1 else (1, 0)
+    return (1, 0)
 
 
 class NormChain:

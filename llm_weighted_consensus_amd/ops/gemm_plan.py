@@ -12,6 +12,9 @@ Backends computing ``A . W^T`` for the dense projections:
   transposed accumulator layout (``profiles/gemm4w_stamps_r5.md``).
 * ``gv``     — the skinny weight-stream GEMM for decode-sized row counts (M <= 64; plain, residual and
   SwiGLU epilogues; ``csrc/kernels/skinny.hip``): the serving path's small decode steps.
+* ``g4s``    — gemm4w VAR 64 with split-K (``ops.split_plan``): shapes whose tiles leave CUs idle (the
+  serving path's mid-size row counts: o / down at M = 2048 are 128 tiles for 256 CUs) run every tile as 2-4
+  K-range units, a ragged last round (lm_head) splits only that round's tiles.
 
 The hand-written cores also fuse the SwiGLU of the gate|up projection, or the residual add of the o /
 down projections (:func:`linear_add_`), into their epilogue.  None wins everywhere
@@ -29,10 +32,10 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import gemm4w, gemm8p, silu_mul, skinny_gemm, skinny_ok
+from . import gemm4w, gemm8p, silu_mul, skinny_gemm, skinny_ok, split_plan
 
 MODE = os.environ.get("LWC_GEMM", "auto")
-BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p", "gv")
+BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p", "gv", "g4s")
 # a hand-written core is chosen when it is at least as fast as the library in the isolated timings (no
 # bias either way: the decode step's plan is then settled by the engine's in-step A/B of whole captured steps,
 # engine.LLMEngine._step_ab, which sees the step's clock and cache state)
@@ -73,6 +76,8 @@ def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
         return False
     if b == "gv":
         return SKINNY and skinny_ok(x.shape[0], N, K, swiglu=epi == "swiglu")
+    if b == "g4s":
+        return x.is_cuda and split_plan(x.shape[0], N, K)[0] > 1
     return not (b == "g4n192" and epi == "swiglu")
 
 
@@ -81,6 +86,9 @@ def _own(b: str, x: torch.Tensor, w: torch.Tensor, ws=None, **kw) -> torch.Tenso
         return gemm8p(x, w, ws=ws, **kw)
     if b == "gv":
         return skinny_gemm(x, w, **kw)
+    if b == "g4s":
+        s_, f_ = split_plan(x.shape[0], w.shape[0], x.shape[1])
+        return gemm4w(x, w, var=64, splits=s_, split_from=f_, **kw)
     return gemm4w(x, w, bn=192 if b == "g4n192" else 256, var=64 if b == "g4p" else 0, **kw)
 
 

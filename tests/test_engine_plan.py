@@ -91,7 +91,8 @@ def test_step_plans_candidates_and_apply(monkeypatch):
         assert not plans["library"]["chain"]["attn"]
         assert plans["own"]["choices"] == {n: "g4p" for n in keys}
         assert plans["own"]["chain"] == {"attn": True, "mlp": True, "final": True, "qkv_bn": 192, "qkv_var": 32,
-                                         "gu_var": 64, "lm_var": 64, "o": "own64", "down": "own64"}
+                                         "gu_var": 64, "lm_var": 64, "lm_split": False, "o": "own64",
+                                         "down": "own64"}
         m.apply_step_plan(M, plans["own"])
         assert all(gemm_plan._CHOICE[k] == "g4p" for k in keys.values()) and m.chain_m[M]["mlp"]
         s = m.plan_summary(M)
@@ -99,6 +100,7 @@ def test_step_plans_candidates_and_apply(monkeypatch):
         # coordinate-descent moves: from the all-own plan (chain owns every projection) only chain decisions
         labels = [lb for lb, _ in m.step_moves(M, plans["own"])]
         assert "attn_fold=False" in labels and "gu_var=32" in labels and "o_producer=sumsq" in labels
+        assert "lm_split=True" in labels
         assert not any(lb.startswith(("qkv=", "gu=", "lm=")) for lb in labels)
         # from the planner's plan: the projections the chain does not own can switch backend
         mv = dict(m.step_moves(M, plans["planner"]))
