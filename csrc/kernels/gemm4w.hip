@@ -70,6 +70,8 @@ namespace lwc {
 namespace g4w {
 
 constexpr int kOpA = 256 * 128;  // A operand's K tile: 256 rows x 128 B
+// buffer load / store cache policy sc1 (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16): write-through stores, L1-bypassing loads
+constexpr int kSC1 = 16;
 
 enum Epi { EPI_PLAIN = 0, EPI_RESIDUAL = 1, EPI_SWIGLU = 2, EPI_BIAS = 3, EPI_BIAS_GELU = 4 };
 
@@ -126,14 +128,39 @@ LWC_DEVICE void mfma2(float4v& d, const uint4v& a, const uint4v& b) {
 #define G4_VM(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 #define G4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 // the wave-local epilogue's accumulators of m-tile I into AV[NT] (VGPRs): the tile's own, plus the partial
-// sums of the other split-K units when this workgroup is a split tile's last arriver (nsl slabs at pslab)
-#define G4_ACC_LOAD(AV, I)                                                                     \
-  do {                                                                                         \
-    _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];                     \
-    for (int u_ = 0; u_ < nsl; ++u_) {                                                         \
-      _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_)                                        \
-        AV[g_] += pslab[((size_t)u_ * 8 * NT + (I) * NT + g_) * 256 + tid];                    \
-    }                                                                                          \
+// sums of the other split-K units when this workgroup is a split tile's last arriver (nsl slabs behind the
+// resource pslab, read with sc1 loads: L2, never a stale L1 line).  The first slab's values come from PP,
+// loaded one m-tile ahead (G4_ACC_PREFETCH0 before the loop; each G4_ACC_LOAD issues the next m-tile's), so
+// the loads of m-tile i + 1 are in flight under m-tile i's epilogue.  The residual epilogue (TRR) prefetches;
+// the TR epilogues load each m-tile's partials in place (G4_ACC_LOAD_SYNC: 32 more live VGPRs made them spill)
+#define G4_SLAB(U, I, G) \
+  __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(pslab, (((I) * NT + (G)) * 256 + tid) * 16, \
+                                                                    (U) * (8 * NT * 256 * 16), kSC1))
+#define G4_ACC_PREFETCH0(PP)                                      \
+  do {                                                            \
+    if (nsl > 0) {                                                \
+      _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) PP[g_] = G4_SLAB(0, 0, g_); \
+    }                                                             \
+  } while (0)
+#define G4_ACC_LOAD_SYNC(AV, I)                                                  \
+  do {                                                                           \
+    _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];       \
+    for (int u_ = 0; u_ < nsl; ++u_) {                                           \
+      _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] += G4_SLAB(u_, I, g_); \
+    }                                                                            \
+  } while (0)
+#define G4_ACC_LOAD(AV, PP, I)                                                   \
+  do {                                                                           \
+    _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];       \
+    if (nsl > 0) {                                                               \
+      _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] += PP[g_];        \
+      if ((I) + 1 < 8) {                                                         \
+        _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) PP[g_] = G4_SLAB(0, (I) + 1, g_); \
+      }                                                                          \
+      for (int u_ = 1; u_ < nsl; ++u_) {                                         \
+        _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] += G4_SLAB(u_, I, g_); \
+      }                                                                          \
+    }                                                                            \
   } while (0)
 
 // Diagnostic build only (scripts/probes/g4_stamps.cpp defines LWC_G4_STAMPS): wave 0 of every workgroup
@@ -461,33 +488,34 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     // drain vmcnt(0) — the next tile's K-tile DMA issued in the last iteration — before the epilogue starts
     if constexpr (!PAP) __syncthreads();
     G4_STAMP(round, 2);
-    int nsl = 0;                    // split-K last arriver: partial slabs to add in the epilogue
-    const float4v* pslab = nullptr;
+    int nsl = 0;  // split-K last arriver: partial slabs to add in the epilogue
+    __amdgpu_buffer_rsrc_t pslab = __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000);
     if constexpr (PAP) {
       // split-K (tile >= full, wave-uniform): arrival ticket; the first S - 1 arrivers publish their partial
-      // sums and leave, the last one adds them and runs the epilogue.  Publication: plain stores, every wave's
-      // vmcnt(0), the block barrier, lane 0's agent release fence + vmcnt(0), then the relaxed count in
-      // done[tile]; the last arriver polls done[tile] relaxed, takes one agent acquire fence, and the block
-      // barrier orders its plain loads (MI355X_MICROARCH.md, Workgroup dispatch: valid forms)
+      // sums and leave, the last one adds them and runs the epilogue.  Hand-off (MI355X_MICROARCH.md,
+      // inter-workgroup visibility, the sc1 table's first row): every slab byte is stored write-through (sc1,
+      // 16 B) and loaded sc1 (L2, bypassing L1), every storing wave waits vmcnt(0), a block barrier, then one
+      // lane's agent-scope add to done[tile]; the last arriver's lane 0 polls done[tile] with sc1 loads and the
+      // block barrier releases the other waves.  No release / acquire fences: a release fence writes back the
+      // whole XCD L2 — here 256 KB of fresh partials per workgroup — and cost ~30 us per call
       if (tile >= p.full) {
         int* tk = reinterpret_cast<int*>(smem + SKOFF);
         if (tid == 0) tk[0] = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         const int ticket = __builtin_amdgcn_readfirstlane(tk[0]);
-        float4v* slab = reinterpret_cast<float4v*>(p.part) + (size_t)(tile - p.full) * (p.S - 1) * (8 * NT * 256);
+        pslab = uniform_rsrc(p.part + (size_t)(tile - p.full) * (p.S - 1) * (8 * NT * 256 * 4),
+                             (p.S - 1) * (8 * NT * 256 * 16));
         if (ticket < p.S - 1) {
-          float4v* mine = slab + (size_t)ticket * (8 * NT * 256);
 #pragma unroll
           for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int jj = 0; jj < NT; ++jj) mine[(i * NT + jj) * 256 + tid] = acc[i][jj];
+            for (int jj = 0; jj < NT; ++jj)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, acc[i][jj]), pslab,
+                                                     ((i * NT + jj) * 256 + tid) * 16, ticket * (8 * NT * 256 * 16),
+                                                     kSC1);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
-          if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(p.done + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          if (tid == 0) __hip_atomic_fetch_add(p.done + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           continue;  // this unit's work is in the partial: no epilogue
         }
         if (tid == 0) {
@@ -497,18 +525,15 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             if (__hip_atomic_load(p.done + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= p.S - 1) break;
             __builtin_amdgcn_s_sleep(2);
           }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           // every unit of this tile has counted itself: reset for the next call
           __hip_atomic_store(p.done + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        // the partials are added where the epilogue reads the accumulators (G4_ACC): the accumulators stay
-        // as the MFMAs left them (rewriting them here made the register allocator rotate all of them through
-        // v_accvgpr_mov copies, caught by the build's ISA guard)
+        // the partials are added where the epilogue reads the accumulators (G4_ACC_LOAD): the accumulators
+        // stay as the MFMAs left them (rewriting them here made the register allocator rotate all of them
+        // through v_accvgpr_mov copies, caught by the build's ISA guard)
         nsl = p.S - 1;
-        pslab = slab;
       }
     }
 
@@ -557,6 +582,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
           for (int g2 = 0; g2 < NT / 2; ++g2)
             rv[i][g2] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, tr_vo[g2], tr_so(i), 0));
       }
+      float4v pp[NT];  // split-K (TRR): the first partial slab's values of the next m-tile
+      if constexpr (TRR) G4_ACC_PREFETCH0(pp);
       G4_STAMP(round, 3);
       if constexpr (TRR) {
         // residual on the TR layout: per column pair the fp32 accumulators swap halves by v_permlane16_swap
@@ -566,7 +593,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float4v av[NT];  // the m-tile's accumulators (+ the split-K partials of the other units)
-          G4_ACC_LOAD(av, i);
+          G4_ACC_LOAD(av, pp, i);
           uint4v res[NT / 2];
 #pragma unroll
           for (int g2 = 0; g2 < NT / 2; ++g2) res[g2] = rv[i & 1][g2];
@@ -635,7 +662,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
         for (int i = 0; i < 8; ++i) {
           uint32_t o[NO][2];
           float4v av[NT];  // the m-tile's accumulators (+ the split-K partials of the other units)
-          G4_ACC_LOAD(av, i);
+          G4_ACC_LOAD_SYNC(av, i);
           // RS 1 (folded RMSNorm consumer): every value of the lane's row i * 16 + r16 takes the row's 1/rms
           float sc = 1.f;
           if constexpr (RS == 1) sc = reinterpret_cast<const float*>(smem + RSV)[wm * 128 + i * 16 + r16];

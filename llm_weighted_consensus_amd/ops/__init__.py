@@ -507,8 +507,9 @@ def split_workspace(M: int, N: int, bn: int, splits: int, split_from: int, devic
 
 def split_plan(M: int, N: int, K: int, bn: int = 256, cus: int = 256) -> tuple:
     """(splits, split_from) for gemm4w's split-K (VAR 64 units: an even K tile count each), or (1, 0):
-    * fewer tiles than ~3/4 of the CUs (the serving path's mid-size row counts: o / down at M = 2048 are 128
-      tiles): the whole call split 2 or 4 ways, while that stays within ~1.25 rounds;
+    * at most half as many tiles as CUs (the serving path's mid-size row counts: o / down at M = 2048 are 128
+      tiles): the whole call split 2 or 4 ways while the units fit one round (a second round of half-K units
+      costs what one round of whole tiles does: M = 2304's 144 tiles measured 136 vs 86 us split);
     * a ragged last round of at most half the CUs (lm_head at M = 4096: 8016 tiles = 31 rounds + 80): only that
       round's tiles split, 2 or 4 ways, into at most one round of shorter units."""
     tiles = ((M + 255) // 256) * ((N + bn - 1) // bn)
@@ -517,9 +518,9 @@ def split_plan(M: int, N: int, K: int, bn: int = 256, cus: int = 256) -> tuple:
     def ok(s):
         return KT % s == 0 and (KT // s) % 2 == 0
 
-    if tiles <= cus * 3 // 4:
+    if tiles <= cus // 2:
         s = 1
-        while s < 4 and tiles * s * 2 <= cus * 5 // 4 and ok(2 * s):
+        while s < 4 and tiles * s * 2 <= cus and ok(2 * s):
             s *= 2
         return (s, 0) if s > 1 else (1, 0)
     tail = tiles % cus

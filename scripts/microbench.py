@@ -571,7 +571,7 @@ def serve_shapes(dev):
     d, Fd, QKV = 4096, 14336, 6144
     r = lambda *s: ((torch.rand(*s, device=dev) * 2 - 1) / s[-1] ** 0.5).to(torch.bfloat16)  # noqa: E731
     wqkv, wo, wgu, wd = r(QKV, d), r(d, d), ops.swiglu_interleave(r(2 * Fd, d)), r(d, Fd)
-    for M in [int(m) for m in os.environ.get("SERVE_M", "2048,2304,2560").split(",")]:
+    for M in [int(m) for m in os.environ.get("SERVE_M", "512,1024,2048,2304,2560,3072").split(",")]:
         x, xa, xf = r(M, d) * 8, r(M, d) * 8, r(M, Fd) * 8
         acc = torch.zeros(M, d, device=dev, dtype=torch.bfloat16)
         runs = {
@@ -585,6 +585,14 @@ def serve_shapes(dev):
             "down blas": lambda: acc.addmm_(xf, wd.t()), "down g4": lambda: ops.gemm4w(xf, wd, residual=acc, out=acc),
             "down g8": lambda: ops.gemm8p(xf, wd, residual=acc, out=acc),
         }
+        # split-K (VAR 64) where ops.split_plan splits the call or its ragged tail
+        for k, (w, K, kw) in {"qkv": (wqkv, d, {}), "o": (wo, d, {"residual": acc, "out": acc}),
+                              "gu": (wgu, d, {"swiglu": True}), "down": (wd, Fd, {"residual": acc, "out": acc})}.items():
+            S, f = ops.split_plan(M, w.shape[0], K)
+            if S > 1:
+                a_ = xf if k == "down" else (xa if k == "o" else x)
+                runs[f"{k} g4s{S}@{f}"] = (lambda a_=a_, w=w, kw=kw, S=S, f=f:
+                                           ops.gemm4w(a_, w, var=64, splits=S, split_from=f, **kw))
         res = {k: [] for k in runs}
         for _ in range(5):
             for k, fn in runs.items():

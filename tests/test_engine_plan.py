@@ -116,3 +116,17 @@ def test_step_plans_candidates_and_apply(monkeypatch):
         gemm_plan._CHOICE.update(choices)
         gemm_plan.TIMINGS.clear()
         gemm_plan.TIMINGS.update(timings)
+
+
+def test_split_plan():
+    """gemm4w split-K planning: whole-call splits only while the units fit one round; ragged last rounds of at
+    most half the CUs split their tiles; every unit an even K tile count."""
+    from llm_weighted_consensus_amd.ops import split_plan
+
+    assert split_plan(2048, 4096, 4096) == (2, 0)  # 128 tiles -> 256 units
+    assert split_plan(512, 4096, 4096) == (4, 0)  # 32 tiles -> 128 units
+    assert split_plan(2304, 4096, 4096) == (1, 0)  # 144 tiles: a split would need a second round
+    assert split_plan(4096, 128256, 4096) == (2, 7936)  # lm_head: 31 rounds + 80 tiles
+    assert split_plan(3072, 6144, 4096) == (4, 256)  # 288 tiles: 32-tile tail
+    assert split_plan(4096, 28672, 4096) == (1, 0)  # 7 whole rounds
+    assert split_plan(2048, 4096, 192) == (1, 0)  # 3 K tiles: no even split
