@@ -9,7 +9,7 @@
 extern "C" {
 int lwc_rmsnorm(const void*, void*, const void*, void*, int, int, float, hipStream_t);
 int lwc_rmsnorm_quant_fp8(const void*, void*, const void*, void*, int, int, float, void*, float*, hipStream_t);
-int lwc_layernorm(const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
+int lwc_layernorm(const void*, const void*, const void*, const void*, const void*, void*, int, int, float, hipStream_t);
 int lwc_rope_kv_write(void*, const int*, const int*, const float*, const float*, void*, void*, int, int, int, int,
                       int, int, hipStream_t);
 int lwc_silu_mul(const void*, void*, int, int, int, hipStream_t);
@@ -136,7 +136,7 @@ void rmsnorm_quant_fp8(const at::Tensor& x, const c10::optional<at::Tensor>& res
 }
 
 void layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& g,
-               const at::Tensor& b, at::Tensor& out, double eps) {
+               const at::Tensor& b, at::Tensor& out, double eps, const c10::optional<at::Tensor>& pre_bias) {
   CHECK_BF16(x); CHECK_BF16(g); CHECK_BF16(b); CHECK_BF16(out);
   CHECK_CONTIG(x); CHECK_CONTIG(out);
   const int d = (int)x.size(-1);
@@ -148,7 +148,13 @@ void layernorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, c
     TORCH_CHECK(residual->numel() == x.numel(), "layernorm: residual shape mismatch");
     r = residual->data_ptr();
   }
-  CHECK_RC(lwc_layernorm(x.data_ptr(), r, g.data_ptr(), b.data_ptr(), out.data_ptr(), rows, d, (float)eps,
+  const void* pb = nullptr;
+  if (pre_bias.has_value() && pre_bias->defined()) {
+    CHECK_BF16(*pre_bias); CHECK_CONTIG(*pre_bias);
+    TORCH_CHECK(pre_bias->numel() == d, "layernorm: pre-norm bias shape mismatch");
+    pb = pre_bias->data_ptr();
+  }
+  CHECK_RC(lwc_layernorm(x.data_ptr(), r, pb, g.data_ptr(), b.data_ptr(), out.data_ptr(), rows, d, (float)eps,
                          cur_stream()),
            "layernorm");
 }

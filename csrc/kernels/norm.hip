@@ -172,10 +172,13 @@ static void launch_rmsnorm_wave_q(const void* x, void* residual, const void* w, 
 
 // LayerNorm with affine: y = (h - mean)/sqrt(var+eps) * g + b, h = x (+ residual);
 // residual (if given) is NOT updated: BERT post-norm writes y back as the new stream.
+// pb (optional): a pre-norm bias, h = x (+ residual) + pb — the residual projection's bias when its GEMM
+// fused the residual add instead (x then already holds the stream).
 template <bool kResidual>
 __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual,
-                                                        const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
-                                                        bf16_t* __restrict__ y, int d, float eps) {
+                                                        const bf16_t* __restrict__ pb, const bf16_t* __restrict__ g,
+                                                        const bf16_t* __restrict__ b, bf16_t* __restrict__ y, int d,
+                                                        float eps) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = d >> 3;
@@ -196,6 +199,12 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restric
         unpack8(rr[i], r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+      }
+      if (pb) {
+        float c[8];
+        unpack8(reinterpret_cast<const uint4v*>(pb)[i], c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += c[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[k][j];
@@ -222,6 +231,84 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16_t* __restric
       float gf[8], bf[8], o[8];
       unpack8(gr[i], gf);
       unpack8(br[i], bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * inv * gf[j] + bf[j];
+      yr[i] = pack8(o);
+    }
+  }
+}
+
+// LayerNorm for rows of at most 1024 elements (bge-base 768, bge-large 1024): one wave per row, lane l owning
+// the row's 16-byte vectors l and l + 64, four rows per 256-thread workgroup, wave shuffles for the two sums
+// (no LDS, no block barriers: the one-workgroup-per-row kernel ran 768-wide rows at ~4.9 TB/s).  x and y may
+// be the same tensor (every lane loads its vectors before the first shuffle).
+template <bool kResidual>
+__global__ void __launch_bounds__(256) layernorm_wave_kernel(const bf16_t* x, const bf16_t* __restrict__ residual,
+                                                             const bf16_t* __restrict__ pb, const bf16_t* __restrict__ g,
+                                                             const bf16_t* __restrict__ b, bf16_t* y, int rows, int d,
+                                                             float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nvec = d >> 3;
+  const uint4v* xr = reinterpret_cast<const uint4v*>(x + (size_t)row * d);
+  const uint4v* rr = reinterpret_cast<const uint4v*>(residual + (size_t)row * d);
+  float v[2][8];
+  uint4v raw[2], rraw[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nvec) {
+      raw[k] = xr[i];
+      if (kResidual) rraw[k] = rr[i];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nvec) {
+      unpack8(raw[k], v[k]);
+      if (kResidual) {
+        float r[8];
+        unpack8(rraw[k], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+      }
+      if (pb) {
+        float c[8];
+        unpack8(reinterpret_cast<const uint4v*>(pb)[i], c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += c[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[k][j];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (lane + 64 * k < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = v[k][j] - mean;
+        s2 += c * c;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+  const float inv = rsqrtf(s2 / (float)d + eps);
+  uint4v* yr = reinterpret_cast<uint4v*>(y + (size_t)row * d);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nvec) {
+      float gf[8], bf[8], o[8];
+      unpack8(reinterpret_cast<const uint4v*>(g)[i], gf);
+      unpack8(reinterpret_cast<const uint4v*>(b)[i], bf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * inv * gf[j] + bf[j];
       yr[i] = pack8(o);
@@ -292,16 +379,29 @@ extern "C" int lwc_rmsnorm_quant_fp8(const void* x, void* residual, const void* 
   return (int)hipGetLastError();
 }
 
-extern "C" int lwc_layernorm(const void* x, const void* residual, const void* g, const void* b, void* y, int rows,
-                             int d, float eps, hipStream_t s) {
+extern "C" int lwc_layernorm(const void* x, const void* residual, const void* pre_bias, const void* g, const void* b,
+                             void* y, int rows, int d, float eps, hipStream_t s) {
   using namespace lwc;
   if (d % 8 != 0 || d > kMaxVec * 8 * 1024) return -1;
+  if (rows == 0) return 0;
+  const bf16_t* pb = (const bf16_t*)pre_bias;
+  if (d <= 1024) {
+    const int grid = (rows + 3) / 4;
+    if (residual)
+      layernorm_wave_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)residual, pb, (const bf16_t*)g,
+                                                       (const bf16_t*)b, (bf16_t*)y, rows, d, eps);
+    else
+      layernorm_wave_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)x, nullptr, pb, (const bf16_t*)g,
+                                                        (const bf16_t*)b, (bf16_t*)y, rows, d, eps);
+    return (int)hipGetLastError();
+  }
+  if (x == y) return -1;  // the workgroup-per-row kernel is not in-place safe across its vector loop
   const int t = norm_threads(d);
   if (residual)
-    layernorm_kernel<true><<<rows, t, 0, s>>>((const bf16_t*)x, (const bf16_t*)residual, (const bf16_t*)g,
+    layernorm_kernel<true><<<rows, t, 0, s>>>((const bf16_t*)x, (const bf16_t*)residual, pb, (const bf16_t*)g,
                                               (const bf16_t*)b, (bf16_t*)y, d, eps);
   else
-    layernorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, (const bf16_t*)g, (const bf16_t*)b,
+    layernorm_kernel<false><<<rows, t, 0, s>>>((const bf16_t*)x, nullptr, pb, (const bf16_t*)g, (const bf16_t*)b,
                                                (bf16_t*)y, d, eps);
   return (int)hipGetLastError();
 }

@@ -1017,10 +1017,15 @@ class LLMEngine:
         0.2 %.  Isolated per-GEMM timings do not see the step's clock and cache state (they flipped choices
         that lost 0.5 % in the bench); this measures the thing that runs.  ``LWC_STEP_AB=0`` keeps the
         planner's choice, ``LWC_STEP_AB=plans`` skips the moves, ``LWC_STEP_PLAN=<name>`` runs that whole plan
-        (profiling).  Decided once per model and batch; results in ``self.step_ab[B]`` and on stderr."""
+        (profiling).  Decided once per model and batch; results in ``self.step_ab[B]`` and on stderr.
+        Only for buckets of at least ``LWC_STEP_AB_MIN`` rows (default 1024): below, the projections are few-tile
+        or weight-streaming shapes the planner's isolated timings rank the same way, and a serving engine
+        meets many small buckets — each A/B captures ~20 graphs (measured: ~10 s of a 256-request load test)."""
         self.step_ab[bk.B] = {}
         mode = os.environ.get("LWC_STEP_AB", "1")
         if mode == "0" or not hasattr(self.model, "step_plans"):
+            return
+        if bk.B < int(os.environ.get("LWC_STEP_AB_MIN", "1024")) and not os.environ.get("LWC_STEP_PLAN"):
             return
         # every engine on the model then runs the same kernels (engines compared against each other)
         done = self.model.__dict__.setdefault("step_ab_done", {})

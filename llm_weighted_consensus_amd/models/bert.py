@@ -21,6 +21,7 @@ GPU whose kernels failed to load.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -62,6 +63,7 @@ class BertEncoder:
         else:
             self._random_init(seed)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.fused_residual = os.environ.get("LWC_ENC_FUSED_RESIDUAL", "ffn2")
 
     def _random_init(self, seed: int) -> None:
         c, dev, dt = self.cfg, self.device, self.dtype
@@ -150,21 +152,36 @@ class BertEncoder:
         x = ops.layernorm(ops.embedding(self.word, ids), self.emb_ln_g, self.emb_ln_b, c.ln_eps,
                           residual=ops.embedding(self.pos_type, positions))
         lin = gemm_plan.linear_bias  # bias (+ GELU) in the GEMM epilogue (gemm8p) or hipBLASLt, per shape
+        # post-LN residual: a projection whose GEMM adds its product into the stream x (residual epilogue) hands
+        # its bias to the LayerNorm that follows as a pre-norm bias, in place: the norm reads one [T, d] tensor
+        # instead of the projection output and the stream.  LWC_ENC_FUSED_RESIDUAL: "ffn2" (default) for FFN2
+        # only, "all" for o too, "0" for neither.  Measured (bge-base, 0.5 M tokens): hipBLASLt's beta = 1 GEMM
+        # reads the stream under FFN2's K = 3072 loop almost free (+29 us vs the bias GEMM, the norm -134 us)
+        # but not under o's K = 768 (+119 us): profiles/round6_ab.md
+        mode = self.fused_residual if d <= 1024 else "0"
+        fuse_o, fuse_f = mode == "all", mode in ("all", "ffn2")
         for L in self.layers:
             qkv = lin(x, L.wqkv, L.bqkv)
             a = ops.prefill_attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], cu, max_len, H, H, Dh, self.scale,
                                       causal=False)
-            o = lin(a, L.wo, L.bo)
-            x = ops.layernorm(o, L.ln1_g, L.ln1_b, c.ln_eps, residual=x)
+            if fuse_o:
+                gemm_plan.linear_residual_(a, L.wo, x)
+                ops.layernorm(x, L.ln1_g, L.ln1_b, c.ln_eps, out=x, pre_bias=L.bo)
+            else:
+                x = ops.layernorm(lin(a, L.wo, L.bo), L.ln1_g, L.ln1_b, c.ln_eps, residual=x)
             h = lin(x, L.w1, L.b1, gelu=True)
-            y = lin(h, L.w2, L.b2)
-            x = ops.layernorm(y, L.ln2_g, L.ln2_b, c.ln_eps, residual=x)
+            if fuse_f:
+                gemm_plan.linear_residual_(h, L.w2, x)
+                ops.layernorm(x, L.ln2_g, L.ln2_b, c.ln_eps, out=x, pre_bias=L.b2)
+            else:
+                x = ops.layernorm(lin(h, L.w2, L.b2), L.ln2_g, L.ln2_b, c.ln_eps, residual=x)
         return x
 
     def to(self, device, dtype=None) -> "BertEncoder":
         """Copy of this encoder on another device (e.g. a GPU model's weights on CPU for the oracle)."""
         out = BertEncoder.__new__(BertEncoder)
         out.cfg, out.device, out.scale = self.cfg, torch.device(device), self.scale
+        out.fused_residual = self.fused_residual
         out.dtype = dtype or self.dtype
         mv = lambda t: t.to(device=device, dtype=out.dtype)
         out.word, out.pos_type, out.emb_ln_g, out.emb_ln_b = (mv(self.word), mv(self.pos_type), mv(self.emb_ln_g),

@@ -432,7 +432,9 @@ class LlamaModel:
             return
         cfg, L = self.cfg, self.layers[0]
         none = {"attn": False, "mlp": False, "final": False, "qkv_bn": 192, "o": "plain", "down": "plain"}
-        if (cfg.hidden + 255) // 256 > 16:
+        # below 256 rows the chain's 256-row tiles run mostly empty and the weight-streaming cores win every
+        # projection: not timed (a serving engine meets many such buckets)
+        if (cfg.hidden + 255) // 256 > 16 or M < 256:
             self.chain_m[M] = none
             return
         if self.chain is None:  # once, for every decode bucket (captured graphs keep these addresses)

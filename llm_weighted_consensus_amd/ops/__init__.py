@@ -86,11 +86,14 @@ def rmsnorm_quant_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Op
 
 
 def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
-              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = layernorm(x [+ residual]) * g + b (K9a)."""
+              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+              pre_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = layernorm(x [+ residual] [+ pre_bias]) * g + b (K9a).  ``pre_bias`` [d]: the bias of a projection
+    whose GEMM already added the residual stream into x (the encoder's fused o / FFN2 residual).  ``out`` may
+    be x itself for rows of at most 1024 elements (one wave per row loads before it stores)."""
     if out is None:
         out = torch.empty_like(x)
-    kernels().layernorm(x, residual, g, b, out, float(eps))
+    kernels().layernorm(x, residual, g, b, out, float(eps), pre_bias)
     return out
 
 

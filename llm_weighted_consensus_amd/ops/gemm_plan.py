@@ -76,8 +76,8 @@ def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
         return False
     if b == "gv":
         return SKINNY and skinny_ok(x.shape[0], N, K, swiglu=epi == "swiglu")
-    if b == "g4s":
-        return x.is_cuda and split_plan(x.shape[0], N, K)[0] > 1
+    if b == "g4s":  # (256-row tiles: below 256 rows the weight-streaming cores win)
+        return x.is_cuda and x.shape[0] >= 256 and split_plan(x.shape[0], N, K)[0] > 1
     return not (b == "g4n192" and epi == "swiglu")
 
 
@@ -166,6 +166,41 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
         _CHOICE[key] = c
     # (a choice made for the token bucket at a smaller A may name gemm8p, which a 2 GiB A cannot take)
     return runs[c]() if c != "blas" and ok and c in runs else runs["blas"]()
+
+
+def linear_residual_(x: torch.Tensor, w: torch.Tensor, acc: torch.Tensor, ws=None) -> torch.Tensor:
+    """acc += x . w^T in place — the post-LN encoder's o / FFN2 projections with the residual stream added in
+    the GEMM epilogue (their bias then enters the LayerNorm that follows as its pre-norm bias, so that norm
+    reads one [M, d] tensor instead of two).  Backend per (token bucket, N, K), timed on the first call on a
+    copy of acc: hipBLASLt with beta = 1 (``addmm_``), gemm4w's residual epilogue (VAR 32 / 64) or gemm8p's."""
+    M, K = x.shape
+    N = w.shape[0]
+    key = (_m_bucket(M), N, K, "enc_residual")
+    c = MODE if MODE in ("blas", "g8", "g4", "g4p") else _CHOICE.get(key)
+    ok = _g8_ok(N, K, "residual") and x.stride(1) == 1 and x.is_cuda and acc.is_contiguous()
+    small_a = M * x.stride(0) * 2 < (1 << 31)
+
+    def runs_on(a):
+        r = {"g4": lambda: gemm4w(x, w, residual=a, out=a), "g4p": lambda: gemm4w(x, w, residual=a, out=a, var=64),
+             "blas": lambda: a.addmm_(x, w.t())}
+        if small_a:
+            r["g8"] = lambda: gemm8p(x, w, residual=a, out=a, ws=ws)
+        return r
+
+    if c is None:
+        if not ok or torch.cuda.is_current_stream_capturing():
+            c = "blas"
+        else:
+            scratch = acc.clone()  # the timing runs add into a copy, never into the stream
+            t = {name: _time(fn, iters=2, rounds=3) for name, fn in runs_on(scratch).items()}
+            del scratch
+            TIMINGS[key] = t
+            own = min((n for n in ("g8", "g4", "g4p") if n in t), key=lambda n: t[n])
+            c = own if t[own] <= t["blas"] * (1 + OWN_MARGIN) else "blas"
+        _CHOICE[key] = c
+    runs = runs_on(acc)
+    runs[c if c != "blas" and ok and c in runs else "blas"]()
+    return acc
 
 
 def _time(fn, iters: int = 5, rounds: int = 3) -> float:

@@ -52,6 +52,11 @@ def test_layernorm(gpu, d):
     _close(y, ref.layernorm(x.float() + r.float(), g, b, 1e-12), 4e-2, 2e-2)
     y2 = ops.layernorm(x, g, b, 1e-12)
     _close(y2, ref.layernorm(x, g, b, 1e-12), 4e-2, 2e-2)
+    # pre-norm bias (the encoder's residual-fused projections), in place
+    pb = _bf(d, dev=gpu)
+    x3 = x.clone()
+    ops.layernorm(x3, g, b, 1e-12, out=x3, pre_bias=pb)
+    _close(x3, ref.layernorm(x.float() + pb.float(), g, b, 1e-12), 4e-2, 2e-2)
 
 
 def test_silu_mul_embedding(gpu):

@@ -53,6 +53,7 @@ def test_engine_greedy_graph_equivalence_and_fork(tiny, gpu, step_ab, monkeypatc
     from llm_weighted_consensus_amd.engine.tokenizer import ByteTokenizer
 
     monkeypatch.setenv("LWC_STEP_AB", step_ab)
+    monkeypatch.setenv("LWC_STEP_AB_MIN", "1")  # the tiny model's buckets are small
     tok = ByteTokenizer(tiny.cfg.vocab_size)
     prompts = [tok.encode("hello world, this is a prompt of some length " * 2), tok.encode("short")]
     sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
@@ -129,14 +130,17 @@ def test_engine_export_import_prefill_equivalence(tiny, gpu):
     assert b.bm.num_free == 256
 
 
+@pytest.mark.parametrize("fused", ["ffn2", "all", "0"])
 @pytest.mark.parametrize("arch", ["bge-small-en-v1.5", "bert-tiny"])
-def test_bert_encoder_matches_reference(gpu, arch):
+def test_bert_encoder_matches_reference(gpu, arch, fused):
     """HIP encoder (LN, varlen bidirectional attention incl. head_dim 32, bias+GELU, pooling) vs the
-    fp32 PyTorch reference forward of the same weights."""
+    fp32 PyTorch reference forward of the same weights; ``fused``: which of o / FFN2 add into the residual stream
+    in their GEMM epilogue, the LayerNorm then taking their bias (default "ffn2"), else projection + LN(x + r)."""
     from llm_weighted_consensus_amd.models.bert import BertEncoder
     from llm_weighted_consensus_amd.models.config import encoder_config
 
     m = BertEncoder(encoder_config(arch), device=gpu, seed=5)
+    m.fused_residual = fused
     lists = [[101] + list(range(1000, 1000 + n)) + [102] for n in (3, 40, 77, 130)]
     ids, pos, cu, max_len = m.pack(lists)
     h = m.forward_packed(ids, pos, cu, max_len)
