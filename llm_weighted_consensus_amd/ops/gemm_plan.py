@@ -40,6 +40,7 @@ BACKENDS = ("blas", "g8", "g4", "g4n192", "g4p", "gv", "g4s")
 # bias either way: the decode step's plan is then settled by the engine's in-step A/B of whole captured steps,
 # engine.LLMEngine._step_ab, which sees the step's clock and cache state)
 OWN_MARGIN = float(os.environ.get("LWC_GEMM_OWN_MARGIN", "0"))
+EXCLUDE = {b for b in os.environ.get("LWC_GEMM_NO", "").split(",") if b}
 # LWC_GEMM_SKINNY=0 leaves the skinny decode GEMM out of the timing (A/B knob)
 SKINNY = os.environ.get("LWC_GEMM_SKINNY", "1") != "0"
 _CHOICE: Dict[Tuple[int, int, int, str], str] = {}
@@ -71,13 +72,14 @@ def _g8_ok(N: int, K: int, epi: str) -> bool:
 
 
 def _own_ok(b: str, x: torch.Tensor, N: int, K: int, epi: str) -> bool:
-    """Whether hand-written backend ``b`` takes this call (layout and the cores' shape rules)."""
-    if b == "blas" or not _g8_ok(N, K, epi) or x.stride(1) != 1:
+    """Whether hand-written backend ``b`` takes this call (layout and the cores' shape rules; ``LWC_GEMM_NO``:
+    a comma list of backends the planner leaves out, for A/B runs)."""
+    if b == "blas" or not _g8_ok(N, K, epi) or x.stride(1) != 1 or b in EXCLUDE:
         return False
     if b == "gv":
         return SKINNY and skinny_ok(x.shape[0], N, K, swiglu=epi == "swiglu")
-    if b == "g4s":  # (256-row tiles: below 256 rows the weight-streaming cores win)
-        return x.is_cuda and x.shape[0] >= 256 and split_plan(x.shape[0], N, K)[0] > 1
+    if b == "g4s":  # VAR 64, split-K wherever split_plan splits this M (else unsplit: a bucket's M varies)
+        return x.is_cuda
     return not (b == "g4n192" and epi == "swiglu")
 
 
@@ -233,7 +235,15 @@ def tune(x: torch.Tensor, w: torch.Tensor, epi: str = "plain", block: int = 0, w
         if bucket:
             _add_bucket(M, N, K, epi, _CHOICE[key])
         return _CHOICE[key]
-    c = _tune(x, w, epi, block, ws, M, N, K, key)
+    lo = None
+    if bucket:
+        # a bucket's choice serves every row count down to the next smaller bucket: time at its top and at the
+        # middle of its range (256-row-tile cores cost in whole m-tiles, the library more smoothly; a choice
+        # timed at the top alone took a split-K core that lost at the bucket's smaller row counts)
+        prev = max((mb for mb, _ in _BUCKETS.get((N, K, epi), []) if mb < M), default=M // 2)
+        lo = max(1, (prev + M) // 2)
+        lo = lo if lo < M else None
+    c = _tune(x, w, epi, block, ws, M, N, K, key, lo)
     if bucket:
         _add_bucket(M, N, K, epi, c)
     return c
@@ -246,29 +256,43 @@ def _add_bucket(M: int, N: int, K: int, epi: str, c: str) -> None:
         bl.sort()
 
 
-def _tune(x, w, epi, block, ws, M, N, K, key) -> str:
+def _tune(x, w, epi, block, ws, M, N, K, key, lo=None) -> str:
+    """``lo``: also time every backend at that row count (the bucket's middle); the choice minimises the sum."""
     if not _g8_ok(N, K, epi) or (epi == "swiglu" and block != 32):
         _CHOICE[key] = "blas"
         return "blas"
     acc = torch.zeros(M, N, dtype=x.dtype, device=x.device) if epi == "residual" else None
+
+    def run(b, xx):
+        aa = acc[:xx.shape[0]] if acc is not None else None
+        if epi == "swiglu":
+            return (lambda: silu_mul(F.linear(xx, w), block=block)) if b == "blas" else \
+                (lambda: _own(b, xx, w, ws, swiglu=True))
+        if epi == "residual":
+            return (lambda: aa.addmm_(xx, w.t())) if b == "blas" else \
+                (lambda: _own(b, xx, w, ws, residual=aa, out=aa))
+        return (lambda: F.linear(xx, w)) if b == "blas" else (lambda: _own(b, xx, w, ws))
+
     runs = {}
     for b in BACKENDS:
         if b != "blas" and not _own_ok(b, x, N, K, epi):
             continue
-        if epi == "swiglu":
-            runs[b] = (lambda: silu_mul(F.linear(x, w), block=block)) if b == "blas" else \
-                (lambda b=b: _own(b, x, w, ws, swiglu=True))
-        elif epi == "residual":
-            runs[b] = (lambda: acc.addmm_(x, w.t())) if b == "blas" else \
-                (lambda b=b: _own(b, x, w, ws, residual=acc, out=acc))
-        else:
-            runs[b] = (lambda: F.linear(x, w)) if b == "blas" else (lambda b=b: _own(b, x, w, ws))
+        if b == "g4s" and (M < 256 or split_plan(M, N, K)[0] == 1 or lo is not None):
+            # (unsplit at the top it is g4p.)  Not for the mixed steps' row-count buckets: timed 3-7 % ahead of
+            # g4p at the buckets' rows, it ran the serving load's mixed steps 0.6-2 % slower (profiles/round6_ab.md)
+            continue
+        fns = [run(b, x)]
+        if lo is not None:
+            if b != "blas" and not _own_ok(b, x[:lo], N, K, epi):
+                continue  # a backend must take the whole bucket
+            fns.append(run(b, x[:lo]))
+        runs[b] = fns
     ts = {b: [] for b in runs}
     # 5 interleaved rounds of 5 calls: o and gate|up are within 1-3 % between backends, and 3 x 3 calls
     # flipped the choice from run to run (profiles/bench_r64_round3.md); runs before graph capture only
     for _ in range(5):
-        for b, fn in runs.items():
-            ts[b].append(_time(fn, iters=5, rounds=1))
+        for b, fns in runs.items():
+            ts[b].append(sum(_time(fn, iters=5, rounds=1) for fn in fns))
     med = {b: sorted(t)[len(t) // 2] for b, t in ts.items()}
     TIMINGS[key] = med
     own = min((b for b in med if b != "blas"), key=lambda b: med[b], default=None)
