@@ -138,21 +138,21 @@ LWC_DEVICE void mfma2(float4v& d, const uint4v& a, const uint4v& b) {
                                                                     (U) * (8 * NT * 256 * 16), kSC1))
 #define G4_ACC_PREFETCH0(PP)                                      \
   do {                                                            \
-    if (nsl > 0) {                                                \
+    if (SK && nsl > 0) {                                          \
       _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) PP[g_] = G4_SLAB(0, 0, g_); \
     }                                                             \
   } while (0)
 #define G4_ACC_LOAD_SYNC(AV, I)                                                  \
   do {                                                                           \
     _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];       \
-    for (int u_ = 0; u_ < nsl; ++u_) {                                           \
+    for (int u_ = 0; SK && u_ < nsl; ++u_) {                                     \
       _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] += G4_SLAB(u_, I, g_); \
     }                                                                            \
   } while (0)
 #define G4_ACC_LOAD(AV, PP, I)                                                   \
   do {                                                                           \
     _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] = acc[I][g_];       \
-    if (nsl > 0) {                                                               \
+    if (SK && nsl > 0) {                                                         \
       _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) AV[g_] += PP[g_];        \
       if ((I) + 1 < 8) {                                                         \
         _Pragma("unroll") for (int g_ = 0; g_ < NT; ++g_) PP[g_] = G4_SLAB(0, (I) + 1, g_); \
@@ -202,8 +202,9 @@ LWC_DEVICE float gelu_tanh(float x) {
 
 // work unit u -> (tile, first K tile, K tile count): whole tiles first, then the split tiles' S units each
 // (consecutive: one tile's units land on one XCD's wpx consecutive units, its partials stay in that L2)
+template <bool SK>
 LWC_DEVICE void unit_tile(const Params& p, int u, int& t, int& kt0, int& nkt) {
-  if (u < p.full) {
+  if (!SK || u < p.full) {
     t = u, kt0 = 0, nkt = p.KT;
   } else {
     const int v = u - p.full, per = p.KT / p.S;
@@ -234,13 +235,16 @@ constexpr int lds_bytes() {
   return Geo<NT>::Lds + (RS == 1 ? 16384 + 1024 : (RS == 2 ? 2048 : 0)) + 16;  // (+ the split-K ticket word)
 }
 
-template <int EPI, int NT, int VAR, int RS>
+// SK: the split-K build (VAR 64; chosen per call only when the call splits): the other builds carry none of
+// its code (its epilogue paths cost the unsplit VAR 64 kernels ~1 % at the serving shapes when they did)
+template <int EPI, int NT, int VAR, int RS, bool SK>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   using G = Geo<NT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int KT = p.KT;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   static_assert(VAR == 32 || VAR == 64, "gemm4w schedules: 32 (block-staged epilogue), 64 (wave-local)");
+  static_assert(!SK || VAR == 64, "split-K runs on the VAR 64 schedule");
   // VAR 64: the wave-local epilogue ("prefetch across persistent tiles") on the transposed accumulator layout
   // (mfma2): plain / SwiGLU / bias / GELU (TR; RS 0, and the row-scaled consumers RS 1) and residual (TRR,
   // RS 0 / 2)
@@ -264,7 +268,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     const int unit = round * 8 * p.wpx + xcd * p.wpx + j;
     if (unit >= p.units) break;
     int tile, kt0, nkt;
-    unit_tile(p, unit, tile, kt0, nkt);
+    unit_tile<SK>(p, unit, tile, kt0, nkt);
     int tm, tn;
     tile_mn(p, tile, tm, tn);
     const int m0 = tm * 256, n0 = tn * G::BN;
@@ -312,7 +316,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     int um = tm, un = tn, ukt0 = kt0;
     if (pf) {
       int ut, unkt;
-      unit_tile(p, nunit, ut, ukt0, unkt);
+      unit_tile<SK>(p, nunit, ut, ukt0, unkt);
       tile_mn(p, ut, um, un);
     }
     const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
@@ -490,7 +494,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     G4_STAMP(round, 2);
     int nsl = 0;  // split-K last arriver: partial slabs to add in the epilogue
     __amdgpu_buffer_rsrc_t pslab = __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000);
-    if constexpr (PAP) {
+    if constexpr (SK) {
       // split-K (tile >= full, wave-uniform): arrival ticket; the first S - 1 arrivers publish their partial
       // sums and leave, the last one adds them and runs the epilogue.  Hand-off (MI355X_MICROARCH.md,
       // inter-workgroup visibility, the sc1 table's first row): every slab byte is stored write-through (sc1,
@@ -583,7 +587,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
             rv[i][g2] = __builtin_bit_cast(uint4v, __builtin_amdgcn_raw_buffer_load_b128(rR, tr_vo[g2], tr_so(i), 0));
       }
       float4v pp[NT];  // split-K (TRR): the first partial slab's values of the next m-tile
-      if constexpr (TRR) G4_ACC_PREFETCH0(pp);
+      if constexpr (TRR && SK) G4_ACC_PREFETCH0(pp);
       G4_STAMP(round, 3);
       if constexpr (TRR) {
         // residual on the TR layout: per column pair the fp32 accumulators swap halves by v_permlane16_swap
@@ -873,16 +877,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
   if constexpr (PAP) G4_VM(0);
 }
 
-template <int EPI, int NT, int VAR, int RS>
+template <int EPI, int NT, int VAR, int RS, bool SK = false>
 int launch3(const Params& p, hipStream_t s) {
   constexpr int lds = lds_bytes<NT, RS>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR, RS>,
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, NT, VAR, RS, SK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  gemm4w_kernel<EPI, NT, VAR, RS><<<8 * p.wpx, 256, lds, s>>>(p);
+  gemm4w_kernel<EPI, NT, VAR, RS, SK><<<8 * p.wpx, 256, lds, s>>>(p);
   return (int)hipGetLastError();
 }
 
@@ -893,6 +897,19 @@ int launch(const Params& p, hipStream_t s, int var, int rs) {
   // one's last two iterations (even K tile counts only: odd ones run 32).  The planner picks per shape
   // (ops/gemm_plan.py).  rs: 1 = row-scaled epilogue (plain / SwiGLU), 2 = residual + row sums of squares.
   if (var != 64 || (p.KT & 1)) var = 32;
+  if (p.S > 1) {
+    // split-K builds: bn 256; plain / SwiGLU (RS 0, or 1: the row-scaled consumers of the folded chain, e.g.
+    // the vocabulary projection's ragged last round) and residual (RS 0, or 2: the chain's producers)
+    if constexpr (NT == 8 && (EPI == EPI_PLAIN || EPI == EPI_SWIGLU)) {
+      if (rs == 0) return launch3<EPI, NT, 64, 0, true>(p, s);
+      if (rs == 1) return launch3<EPI, NT, 64, 1, true>(p, s);
+    }
+    if constexpr (NT == 8 && EPI == EPI_RESIDUAL) {
+      if (rs == 0) return launch3<EPI, NT, 64, 0, true>(p, s);
+      if (rs == 2) return launch3<EPI, NT, 64, 2, true>(p, s);
+    }
+    return -1;
+  }
   if (rs == 1) {
     if constexpr (EPI == EPI_PLAIN || EPI == EPI_SWIGLU) {
       return var == 64 ? launch3<EPI, NT, 64, 1>(p, s) : launch3<EPI, NT, 32, 1>(p, s);
