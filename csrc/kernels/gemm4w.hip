@@ -195,6 +195,9 @@ LWC_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710
 // epilogue computes (the library arm the planner times against): 2 transcendentals + 4 VALU instead of
 // erf_as's 2 + ~12, within 8.1e-3 of the erf form at the bge-large FFN1 shape, the bf16 output's own rounding
 // being 7.8e-3 (ops/gemm_plan.py linear_bias).  The VAR 64 epilogue uses it; the other schedules keep erf.
+// (A degree-7 polynomial of the erf form, clamped at |x| = 4 — no transcendental, 12 VALU — ran FFN1 + GELU
+// 3.5 % slower at config 2's shape; its packed-fp32 form miscompiled inside this epilogue:
+// profiles/round6_ab.md, scripts/probes/pkfma_probe.cpp.)
 LWC_DEVICE float gelu_tanh(float x) {
   const float z = x * (1.5957691216f + 0.0713548163f * x * x);
   return x * __builtin_amdgcn_rcpf(1.f + __expf(-z));

@@ -488,8 +488,8 @@ def small(dev):
 def encoder_gemms(dev):
     """The encoders' small-K projections (config 2 bge-base: d = 768, FFN 3072; bge-large: 1024 / 4096) at
     ENC_M tokens: hipBLASLt (bias / bias+GELU epilogue) vs gemm8p, gemm4w (VAR 32) and gemm4w VAR 64 (next
-    tile's prologue under the epilogue; g4p96 = VAR 64 with the staged epilogue image and erf GELU).  Median of
-    5 interleaved rounds."""
+    tile's prologue under the epilogue, polynomial GELU), g4p192 its 256 x 192 tiles.  Median of 5 interleaved
+    rounds."""
     import torch.nn.functional as F
 
     from llm_weighted_consensus_amd import ops
@@ -507,8 +507,6 @@ def encoder_gemms(dev):
             **({"g8": lambda: ops.gemm8p(x, w, bias=b, gelu=gelu)} if x.numel() * 2 < (1 << 31) else {}),
             "g4": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu),
             "g4p": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu, var=64),
-            # VAR 96: VAR 64 with the staged epilogue image and the erf GELU (the A/B arm of the TR epilogue)
-            "g4p96": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu, var=96),
             "g4p192": lambda: ops.gemm4w(x, w, bias=b, gelu=gelu, var=64, bn=192),
         }
         res = {k: [] for k in runs}

@@ -1523,3 +1523,18 @@ def test_gemm4w_split_k_norm_chain(gpu, splits):
     _close(C, want, 3e-2, 1e-2)
     parts = C.float().pow(2).view(M, N // 256, 256).sum(-1).t()
     assert torch.allclose(chain.ss[:N // 256, :M], parts, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("var", [32, 64])
+def test_gemm4w_gelu_epilogue_values(gpu, var):
+    """The GELU epilogue's math alone: W = identity, so the output is gelu(A + b) of the operand's own bf16
+    values over [-10, 10] (the VAR 64 polynomial, clamped at |x| = 4, and the VAR 32 erf form) against the fp32
+    erf GELU: within 1e-3 plus the bf16 output's rounding."""
+    from llm_weighted_consensus_amd import ops
+
+    M, K = 512, 128
+    x = torch.linspace(-10, 10, M * K, device=gpu).view(M, K).to(torch.bfloat16)
+    W = torch.eye(K, device=gpu).to(torch.bfloat16)
+    b = torch.zeros(K, device=gpu).to(torch.bfloat16)
+    y = ops.gemm4w(x, W, bias=b, gelu=True, var=var)
+    _close(y, torch.nn.functional.gelu(x.float()), 1e-3, 8e-3)
