@@ -160,7 +160,9 @@ extern "C" int lwc_rope_kv_write(void* qkv, const int* positions, const int* slo
                                  int rope_q, hipStream_t s) {
   using namespace lwc;
   if (D % 16 != 0 || T <= 0) return T == 0 ? 0 : -1;
-  // (320 threads — every rotated pair of a Llama-3 token in one round — measured 27.9 vs 26.3 us at T = 4096)
+  // (320 threads — every rotated pair of a Llama-3 token in one round — measured 27.9 vs 26.3 us at T = 4096;
+  // a wave per token with 8 dims per lane, 2 B V stores 32 B apart across lanes, 23.4 vs 10.7 us k-only at
+  // T = 3072: the V scatter wants consecutive lanes on consecutive dims)
   // k only: Hkv * D/16 rotations (64 for Llama-3) + the V scatter, 128 threads
   rope_kv_write_kernel<<<T, rope_q ? 256 : 128, 0, s>>>((bf16_t*)qkv, positions, slots, cos_t, sin_t, (bf16_t*)kc,
                                                         (bf16_t*)vc, Hq, Hkv, D, BS, rope_q);

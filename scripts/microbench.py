@@ -464,7 +464,7 @@ def small(dev):
 
     cfg = decoder_config("llama-3-8b")
     cos, sin = rope_tables(cfg, dev, 4096)
-    for T in (512, 3072):
+    for T in (512, 3072, 4096):
         cache = KVCache(cfg, T + 64, 16, dev)
         qkv = torch.randn(T, cfg.qkv_dim, device=dev).to(torch.bfloat16)
         pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)

@@ -102,6 +102,19 @@ def test_rope_kv_write(gpu):
     blk, off = (slots // BS).long(), (slots % BS).long()
     _close(kc[blk, :, off, :], k_ref, 2e-2, 1e-2)
     _close(ops.v_token(vc, blk, off), v_ref, 0)
+    # padding rows of a decode bucket (slot -1) on the k-only path: no cache write, k rotated in place, q as is
+    sl3 = slots.clone()
+    sl3[::3] = -1
+    q3 = q0.clone()
+    kc3, vc3 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ops.rope_kv_write(q3, pos, cos, sin, kc3, vc3, Hq, Hkv, D, slots=sl3, rope_q=False)
+    pad, real = sl3 < 0, sl3 >= 0
+    assert torch.equal(q3[:, : Hq * D], q0[:, : Hq * D]) and torch.equal(q3[real], q0[real])
+    assert torch.equal(q3[pad, Hq * D:(Hq + Hkv) * D], qkv[pad, Hq * D:(Hq + Hkv) * D])
+    b3, o3 = blk[real], off[real]
+    assert torch.equal(kc3[b3, :, o3, :], kc[b3, :, o3, :])
+    assert torch.equal(ops.v_token(vc3, b3, o3), ops.v_token(vc, b3, o3))
+    assert int((kc3 != 0).sum()) == int((kc3[b3, :, o3, :] != 0).sum())
 
 
 @pytest.fixture(params=["wg4", "wave"])
