@@ -1027,6 +1027,10 @@ class LLMEngine:
             return
         if bk.B < int(os.environ.get("LWC_STEP_AB_MIN", "1024")) and not os.environ.get("LWC_STEP_PLAN"):
             return
+        if getattr(self.model, "tp_size", 1) > 1 or getattr(self.model, "ep_size", 1) > 1:
+            # a tensor- / expert-parallel step holds collectives: every rank would have to capture and replay
+            # the same candidates in the same order, and each rank's candidates come from its own timings
+            return
         # every engine on the model then runs the same kernels (engines compared against each other)
         done = self.model.__dict__.setdefault("step_ab_done", {})
         if bk.B in done:
