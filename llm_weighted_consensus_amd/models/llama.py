@@ -139,7 +139,7 @@ class LlamaModel:
                     L.w_gate_up = ops.swiglu_interleave(L.w_gate_up)
                     L.gu_block = 32
             self.g8_ws = ops.new_gemm8p_workspace(self.device)
-            blas_tuning.enable()  # offline-tuned hipBLASLt / rocBLAS solutions for the library GEMMs
+            blas_tuning.enable()  # offline-tuned library solutions: only with LWC_TUNED_BLAS=1 (off by default)
         # folded RMSNorm (module docstring): the plain dense bf16 decoder on the GPU
         self.norm_folded = False
         self.extra_bytes = 0  # device bytes the folded norms add (a tied lm_head's own copy)

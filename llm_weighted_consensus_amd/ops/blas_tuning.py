@@ -14,7 +14,13 @@ capture).
 
 TunableOp validates the table against the running PyTorch / HIP / hipBLASLt / rocBLAS versions and the
 GCN arch and ignores it on any mismatch, so a different image falls back to the defaults.
-``LWC_TUNED_BLAS=0`` disables the table (A/B runs).
+
+Off by default since round 6 (``LWC_TUNED_BLAS=1`` turns it on).  With TunableOp enabled, every eager library
+GEMM pays its per-call signature lookup on the host, ~126 us per call (serve_load cProfile).  In a same-box
+ABBA run (profiles/round6_ab.md):
+- serving: mixed chunked-prefill steps 9.81-9.90 s off vs 10.75-10.96 s on; 33.07-33.49 vs 32.74-32.91
+  requests/s;
+- headline bench, whose decode steps replay graphs: 9.027 off vs 9.046 on answers/s.
 """
 from __future__ import annotations
 
@@ -35,7 +41,7 @@ def enable(table: Path = TABLE) -> bool:
     if _STATE["enabled"] is not None:
         return _STATE["enabled"]
     ok = False
-    if os.environ.get("LWC_TUNED_BLAS", "1") != "0" and torch.cuda.is_available() and table.exists():
+    if os.environ.get("LWC_TUNED_BLAS", "0") == "1" and torch.cuda.is_available() and table.exists():
         tun = torch.cuda.tunable
         # TunableOp may write its results file back at exit: point it at a private copy so the shipped
         # table is never rewritten
