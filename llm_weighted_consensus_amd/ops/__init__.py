@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import importlib
 import os
+import threading
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -483,9 +484,12 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     return out
 
 
-# split-K workspace of gemm4w (per device): fp32 partial slabs + the per-tile ticket / done counters (zeroed
-# once; each tile's last arriver resets its pair).  Grown only outside graph capture.
+# split-K workspace of gemm4w (per device and host thread: two engines on two threads never share counters):
+# fp32 partial slabs + the per-tile ticket / done counters (zeroed once; each tile's last arriver resets its
+# pair).  Grown only outside graph capture; a replaced workspace is kept alive (_SPLIT_WS_RETIRED), since
+# graphs captured before the growth still address it.
 _SPLIT_WS: dict = {}
+_SPLIT_WS_RETIRED: list = []
 
 
 def split_workspace(M: int, N: int, bn: int, splits: int, split_from: int, device):
@@ -495,9 +499,11 @@ def split_workspace(M: int, N: int, bn: int, splits: int, split_from: int, devic
     tiles = ((M + 255) // 256) * ((N + bn - 1) // bn)
     need_p = max(0, tiles - max(0, min(split_from, tiles))) * (splits - 1) * 256 * bn
     need_c = 2 * tiles
-    key = str(device)
+    key = (str(device), threading.get_ident())
     ws = _SPLIT_WS.get(key)
     if ws is None or ws[0].numel() < need_p or ws[1].numel() < need_c:
+        if ws is not None:
+            _SPLIT_WS_RETIRED.append(ws)
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             raise RuntimeError("gemm4w split-K workspace must be sized before graph capture")
         old_p = ws[0].numel() if ws is not None else 0
