@@ -1114,7 +1114,19 @@ class LLMEngine:
                     ts[k].append(replay_ms(g))
             return {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
 
-        graphs = {name: capture(plan) for name, plan in plans.items()}
+        def try_capture(name, plan):
+            # a candidate that fails to build or capture (a kernel refusing its shape, say) drops out of the
+            # race instead of failing the engine; the planner's own plan is what ran before the A/B existed
+            try:
+                return capture(plan)
+            except RuntimeError as e:
+                print(f"# step A/B at batch {bk.B}: candidate {name} dropped ({e})", file=sys.stderr, flush=True)
+                return None
+
+        graphs = {name: g for name, g in ((n, try_capture(n, p)) for n, p in plans.items()) if g is not None}
+        if not graphs:
+            self.model.apply_step_plan(bk.B, plans["planner"])
+            return
         times = race(graphs, 5)
         best = min(times, key=times.get)
         cur, t_cur = plans[best], times[best]
@@ -1126,7 +1138,9 @@ class LLMEngine:
             # incumbent / move ratio says > 0.25 % faster, and the incumbent becomes the new plan
             for label, delta in self.model.step_moves(bk.B, cur):
                 cand = self.model.with_move(cur, delta)
-                gm = capture(cand)
+                gm = try_capture(label, cand)
+                if gm is None:
+                    continue
                 r = race({"inc": inc, "mv": gm})
                 times[label] = r["mv"] * t_cur / r["inc"]  # on the incumbent's scale
                 if r["mv"] < r["inc"] * 0.9975:
