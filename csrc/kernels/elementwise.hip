@@ -10,6 +10,8 @@
 
 namespace lwc {
 
+constexpr int kRopeVMax = 4096;  // V row elements staged in LDS (Hkv * D; Llama-3-8B: 1024)
+
 // qkv: [T, (Hq + 2*Hkv) * D]; cos/sin: [max_pos, D/2] f32; K cache [NB, Hkv, BS, D];
 // V cache [NB, Hkv, BS/4, D, 4] (4-token interleaved)
 __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ positions,
@@ -64,11 +66,20 @@ __global__ void __launch_bounds__(512) rope_kv_write_kernel(bf16_t* __restrict__
   // V is cached 4-token interleaved per block ([NB, Hkv, BS/4, D, 4]) so the decode kernels' P.V MFMA
   // reads 4 consecutive tokens of a dim as one 8 B load (see attention_decode.hip).  One element per
   // thread, consecutive threads = consecutive dims: a wave's 64 stores cover 16 32-byte sectors.
+  // The row's V comes in through LDS: 16 B loads (one per 8 dims), then the 2 B stores with consecutive threads
+  // on consecutive dims (2 B global loads took 8x the load instructions).
   if (slot >= 0) {
     const bf16_t* vsrc = row + (Hq + Hkv) * D;
-    for (int i = threadIdx.x; i < Hkv * D; i += blockDim.x) {
+    __shared__ uint4v vrow[kRopeVMax / 8];
+    const int nv = Hkv * D;
+    if (nv <= kRopeVMax) {
+      for (int i = threadIdx.x; i < (nv >> 3); i += blockDim.x) vrow[i] = reinterpret_cast<const uint4v*>(vsrc)[i];
+      __syncthreads();
+    }
+    const bf16_t* vl = nv <= kRopeVMax ? reinterpret_cast<const bf16_t*>(vrow) : vsrc;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) {
       const int vh = i / D, d = i - vh * D;
-      vc[((size_t)blk * Hkv + vh) * D * BS + ((off >> 2) * D + d) * 4 + (off & 3)] = vsrc[i];
+      vc[((size_t)blk * Hkv + vh) * D * BS + ((off >> 2) * D + d) * 4 + (off & 3)] = vl[i];
     }
   }
 }
