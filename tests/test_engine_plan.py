@@ -2,6 +2,7 @@
 keep shared tiles inside one group, and degrade gracefully when the table is small."""
 import numpy as np
 import pytest
+import torch
 from hypothesis import given, settings, strategies as st
 
 from llm_weighted_consensus_amd.engine.engine import cascade_tiles
@@ -130,3 +131,24 @@ def test_split_plan():
     assert split_plan(3072, 6144, 4096) == (4, 256)  # 288 tiles: 32-tile tail
     assert split_plan(4096, 28672, 4096) == (1, 0)  # 7 whole rounds
     assert split_plan(2048, 4096, 192) == (1, 0)  # 3 K tiles: no even split
+
+
+def test_split_workspace_grows_and_keeps_old_buffers():
+    """gemm4w split-K workspace: per (device, thread); growing it keeps the old buffers alive (graphs captured
+    before the growth still address them); a smaller request reuses the current one."""
+    import threading
+
+    from llm_weighted_consensus_amd import ops
+
+    dev = torch.device("cpu")
+    p1, c1 = ops.split_workspace(2048, 4096, 256, 2, 0, dev)
+    assert p1.numel() >= 128 * 256 * 256 and c1.numel() >= 2 * 128 and int(c1.abs().sum()) == 0
+    assert ops.split_workspace(512, 4096, 256, 2, 0, dev)[0] is p1  # fits: same buffer
+    p2, _ = ops.split_workspace(2048, 4096, 256, 4, 0, dev)  # 3 slabs per tile: grows
+    assert p2 is not p1 and p2.numel() >= 3 * 128 * 256 * 256
+    assert any(ws[0] is p1 for ws in ops._SPLIT_WS_RETIRED)
+    other = {}
+    t = threading.Thread(target=lambda: other.setdefault("ws", ops.split_workspace(2048, 4096, 256, 2, 0, dev)))
+    t.start()
+    t.join()
+    assert other["ws"][0] is not p2  # another host thread gets its own counters
