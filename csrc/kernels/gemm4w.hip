@@ -290,9 +290,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
     const uint32_t voW = (uint32_t)((drow * p.K + dchk) * 2);
     const int sA = 32 * p.lda * 2, sW = 32 * p.K * 2;  // bytes between pieces
     const int dst0 = wid * 1024;
-    // (a split unit's K range starts kt0 K tiles in: the resources start there)
+    // (a split unit's K range starts kt0 K tiles in: the resources start there.  A's resource spans only the
+    // tile's own 256 rows, so A of any size takes one launch: the 32-bit range is per tile)
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.A + (size_t)m0 * p.lda + kt0 * 64), (short)0, (p.M - m0) * p.lda * 2 - kt0 * 128, 0x00020000);
+        (void*)(p.A + (size_t)m0 * p.lda + kt0 * 64), (short)0, min(p.M - m0, 256) * p.lda * 2 - kt0 * 128,
+        0x00020000);
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.W + (size_t)n0 * p.K + kt0 * 64), (short)0, min(p.N - n0, G::BN) * p.K * 2 - kt0 * 128, 0x00020000);
     // LDS-DMA piece k of one K tile (k < 8: A rows, else W rows)
@@ -323,8 +325,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(Params p) {
       tile_mn(p, ut, um, un);
     }
     const __amdgpu_buffer_rsrc_t nA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.A + (size_t)um * 256 * p.lda + ukt0 * 64), (short)0, (p.M - um * 256) * p.lda * 2 - ukt0 * 128,
-        0x00020000);
+        (void*)(p.A + (size_t)um * 256 * p.lda + ukt0 * 64), (short)0,
+        min(p.M - um * 256, 256) * p.lda * 2 - ukt0 * 128, 0x00020000);
     const __amdgpu_buffer_rsrc_t nW = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.W + (size_t)un * G::BN * p.K + ukt0 * 64), (short)0,
         min(p.N - un * G::BN, G::BN) * p.K * 2 - ukt0 * 128, 0x00020000);
@@ -968,7 +970,8 @@ extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, 
   using namespace lwc::g4w;
   if (K % 64 != 0 || K < 64 || N % 8 != 0 || lda % 8 != 0 || ldc % 8 != 0) return -1;
   if (bn != 256 && bn != 192) return -1;
-  if ((long long)M * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
+  // (A: every buffer resource spans one tile's 256 rows, so any M; W: one tile's bn rows)
+  if ((long long)256 * lda * 2 >= (1LL << 31) || (long long)bn * K * 2 >= (1LL << 31)) return -1;
   if (epi == EPI_SWIGLU && (N % 64 != 0 || bn != 256)) return -1;
   if ((epi == EPI_RESIDUAL || epi == EPI_BIAS || epi == EPI_BIAS_GELU) && R == nullptr) return -1;
   if (rs_mode < 0 || rs_mode > 2 || (rs_mode && (ss == nullptr || ssld < M || ssld % 4 != 0))) return -1;

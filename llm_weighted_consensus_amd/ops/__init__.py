@@ -462,18 +462,9 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
         part, cnt = split_workspace(A.shape[0], W.shape[0], bn, splits, split_from, A.device)
         sk = (int(splits), int(split_from), part, cnt)
     if chain is None:
-        # the kernel addresses A through one 32-bit buffer range: row blocks of < 2 GiB of A, one launch each
-        # (the encoders' FFN2 input at config 2's 0.5 M tokens is 3 GiB)
-        M = A.shape[0]
-        step = max(256, ((1 << 31) - 1) // max(1, A.stride(0) * 2) // 256 * 256)
-        if M <= step:
-            kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm), *sk)
-        else:
-            for r0 in range(0, M, step):
-                r1 = min(M, r0 + step)
-                res = residual[r0:r1] if epi == 1 else residual
-                kernels().gemm4w(A[r0:r1], W, out[r0:r1], res, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm),
-                                 1, 0, None, None)
+        # (one launch for any M: the kernel's A resource spans one tile's rows.  Config 2's FFN2 input, 3 GiB at
+        # 0.5 M tokens, ran as two row blocks before — 16 + 9 rounds, the second's last round holding one tile)
+        kernels().gemm4w(A, W, out, residual, epi, int(bn), None, 0, 0, 0.0, int(var), int(gm), *sk)
     elif epi == 1:
         kernels().gemm4w(A, W, out, residual, epi, int(bn), chain.ss, 2, 0, 0.0, int(var), int(gm), *sk)
         chain.P = (N + 255) // 256

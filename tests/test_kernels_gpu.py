@@ -1551,3 +1551,23 @@ def test_gemm4w_gelu_epilogue_values(gpu, var):
     b = torch.zeros(K, device=gpu).to(torch.bfloat16)
     y = ops.gemm4w(x, W, bias=b, gelu=True, var=var)
     _close(y, torch.nn.functional.gelu(x.float()), 1e-3, 8e-3)
+
+
+@pytest.mark.parametrize("var", [32, 64])
+def test_gemm4w_operand_past_2gib_one_launch(gpu, var):
+    """A of more than 2 GiB in one launch (the kernel's A buffer resource spans one tile's rows): the first
+    and the last rows of a [1049088, 1024] bf16 operand (2.0 GiB + 1 MiB) against fp32, residual epilogue."""
+    from llm_weighted_consensus_amd import ops
+
+    M, K, N = (1 << 20) + 512, 1024, 256
+    A = torch.empty(M, K, device=gpu, dtype=torch.bfloat16)
+    A[:1024] = torch.randn(1024, K, device=gpu).to(torch.bfloat16)
+    A[-1024:] = torch.randn(1024, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    R = torch.zeros(M, N, device=gpu, dtype=torch.bfloat16)
+    R[-1024:] = torch.randn(1024, N, device=gpu).to(torch.bfloat16)
+    out = ops.gemm4w(A, W, residual=R, var=var)
+    for sl in (slice(0, 1024), slice(M - 1024, M)):
+        want = R[sl].float() + A[sl].float() @ W.float().t()
+        _close(out[sl], want, 3e-2, 1e-2)
+    del A, R, out
