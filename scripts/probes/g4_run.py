@@ -1,6 +1,5 @@
 """Run gate|up + SwiGLU (M = 4096, N = 28672, K = 4096) on one backend ITERS times, for rocprofv3 --pmc passes:
-g4_run.py {g4v64|g4v96|g4v32|blas} ITERS  (g4v96 = VAR 64 with the staged epilogue image; blas = hipBLASLt +
-silu_mul)"""
+g4_run.py {g4v64|g4v32|blas} ITERS  (blas = hipBLASLt + silu_mul)"""
 import os
 import sys
 
