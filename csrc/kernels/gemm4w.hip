@@ -210,8 +210,9 @@ LWC_DEVICE void unit_tile(const Params& p, int u, int& t, int& kt0, int& nkt) {
   if (!SK || u < p.full) {
     t = u, kt0 = 0, nkt = p.KT;
   } else {
-    const int v = u - p.full, per = p.KT / p.S;
-    t = p.full + v / p.S, kt0 = (v % p.S) * per, nkt = per;
+    // (unit s of S: K tile pairs [s * H / S, (s + 1) * H / S) of the tile's H = KT / 2 — S need not divide KT)
+    const int v = u - p.full, s = v % p.S, h = p.KT >> 1;
+    t = p.full + v / p.S, kt0 = 2 * (s * h / p.S), nkt = 2 * ((s + 1) * h / p.S) - kt0;
   }
 }
 
@@ -979,12 +980,12 @@ extern "C" int lwc_gemm4w(const void* A, const void* W, void* C, const void* R, 
   if (rs_mode == 2 && (epi != EPI_RESIDUAL || bn != 256)) return -1;
   if (M == 0 || N == 0) return 0;
   const int tiles_m = (M + 255) / 256, tiles_n = (N + bn - 1) / bn, tiles = tiles_m * tiles_n;
-  // split-K (VAR 64 only): tiles [split_from, tiles) run as `splits` units of K / splits each (an even K tile
-  // count, like every VAR 64 unit); workspace part [(tiles - split_from) * (splits - 1) * 256 * bn] fp32,
+  // split-K (VAR 64 only): tiles [split_from, tiles) run as `splits` units of about K / splits each (an even K
+  // tile count, like every VAR 64 unit: KT even, KT / 2 >= splits); workspace part [(tiles - split_from) * (splits - 1) * 256 * bn] fp32,
   // cnt [2 * tiles] int32 zeroed once
   const int KT = K / 64;
   if (splits > 1) {
-    if (var != 64 || KT % splits != 0 || (KT / splits) % 2 != 0 || part == nullptr || cnt == nullptr) return -1;
+    if (var != 64 || KT % 2 != 0 || KT / 2 < splits || part == nullptr || cnt == nullptr) return -1;
   } else {
     splits = 1;
   }

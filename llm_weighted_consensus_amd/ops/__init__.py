@@ -442,7 +442,7 @@ def gemm4w(A: torch.Tensor, W: torch.Tensor, residual: Optional[torch.Tensor] = 
     epilogue); ``gm``: m-tiles per group of the grouped tile order (0: by shape, see gemm4w.hip).
 
     Split-K (``splits`` > 1, schedule 64): the output tiles from ``split_from`` on run as ``splits`` units over
-    K / splits each; the first arrivers publish fp32 partials, the last adds them and runs the epilogue (no
+    about K / splits each (even K tile counts: K / 64 even and >= 2 * splits); the first arrivers publish fp32 partials, the last adds them and runs the epilogue (no
     workgroup waits on one that has not started).  For shapes whose tile count leaves CUs idle (the serving
     path's mid-size row counts: :func:`split_plan`) and a ragged last round (``split_from`` = the whole
     rounds).  The workspace is this module's, sized before graph capture (:func:`split_workspace`)."""

@@ -591,6 +591,15 @@ def serve_shapes(dev):
                 a_ = xf if k == "down" else (xa if k == "o" else x)
                 runs[f"{k} g4s{S}@{f}"] = (lambda a_=a_, w=w, kw=kw, S=S, f=f:
                                            ops.gemm4w(a_, w, var=64, splits=S, split_from=f, **kw))
+            # SERVE_SPLITS: forced whole-call splits (any S: uneven K shares) for qkv / o / down
+            for S in [int(v) for v in os.environ.get("SERVE_SPLITS", "").split(",") if v]:
+                if k != "gu" and (K // 64) // 2 >= S:
+                    a_ = xf if k == "down" else (xa if k == "o" else x)
+                    runs[f"{k} g4s{S}"] = (lambda a_=a_, w=w, kw=kw, S=S:
+                                           ops.gemm4w(a_, w, var=64, splits=S, split_from=0, **kw))
+        if os.environ.get("SERVE_ONLY"):  # e.g. "o ,down ": arms whose name starts with one of these
+            pre = tuple(os.environ["SERVE_ONLY"].split(","))
+            runs = {k: v for k, v in runs.items() if k.startswith(pre)}
         res = {k: [] for k in runs}
         for _ in range(5):
             for k, fn in runs.items():

@@ -1483,7 +1483,7 @@ def test_gemm4w_row_blocks_past_2gib(gpu):
         _close(R[r0:r1], ref + R0[r0:r1].float(), 3e-2, 1e-2)
 
 
-@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("splits", [2, 3, 4])
 @pytest.mark.parametrize("M,N,K,epi,split_from", [(2048, 4096, 4096, "res", 0), (700, 2048, 1024, "swiglu", 0),
                                                   (1000, 128256 // 16, 512, "plain", 64), (300, 6144, 512, "plain", 0),
                                                   (4352, 4096, 512, "res", 200)])
@@ -1514,7 +1514,27 @@ def test_gemm4w_split_k(gpu, M, N, K, epi, split_from, splits):
     assert int(cnt.abs().sum()) == 0  # every tile's counters were reset by its last arriver
 
 
-@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("M,N,K,splits", [(2560, 4096, 1024, 7), (2304, 4096, 1792, 3), (2560, 4096, 3584, 6)])
+def test_gemm4w_split_k_uneven(gpu, M, N, K, splits):
+    """Split-K with S not dividing the K tile count (units of K tile pairs [s H / S, (s + 1) H / S), H = K / 128)
+    and more units than one round of CUs (144-160 tiles x 3-7 units): residual epilogue, twice in a row, vs
+    fp32; the counters end reset."""
+    from llm_weighted_consensus_amd import ops
+
+    torch.manual_seed(M + K + splits)
+    A = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    for _ in range(2):
+        R = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+        want = ref + R.float()
+        _close(ops.gemm4w(A, W, residual=R, out=R, var=64, splits=splits), want, 3e-2, 1e-2)
+    torch.cuda.synchronize()
+    _, cnt = ops.split_workspace(M, N, 256, splits, 0, A.device)
+    assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("splits", [2, 3, 4])
 def test_gemm4w_split_k_norm_chain(gpu, splits):
     """Split-K with the folded-RMSNorm epilogues: a row-scaled consumer (RS 1) and a residual producer that
     writes the row sums of squares (RS 2) — only the last arriver of a tile runs them."""
@@ -1541,7 +1561,7 @@ def test_gemm4w_split_k_norm_chain(gpu, splits):
 @pytest.mark.parametrize("var", [32, 64])
 def test_gemm4w_gelu_epilogue_values(gpu, var):
     """The GELU epilogue's math alone: W = identity, so the output is gelu(A + b) of the operand's own bf16
-    values over [-10, 10] (the VAR 64 polynomial, clamped at |x| = 4, and the VAR 32 erf form) against the fp32
+    values over [-10, 10] (the VAR 64 tanh form and the VAR 32 erf form) against the fp32
     erf GELU: within 1e-3 plus the bf16 output's rounding."""
     from llm_weighted_consensus_amd import ops
 
