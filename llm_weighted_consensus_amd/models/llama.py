@@ -591,16 +591,21 @@ class LlamaModel:
         if ch is not None and self.chain is not None and M <= self.chain.max_rows:
             for pt in ("attn", "mlp", "final"):
                 variant(f"{pt}_fold={not ch.get(pt)}", chain={pt: not ch.get(pt)})
-            variant(f"lm_split={not ch.get('lm_split', False)}", chain={"lm_split": not ch.get("lm_split", False),
-                                                                        "lm_var": 64})
-            for key, alts in (("qkv_var", (32, 64)), ("gu_var", (32, 64)), ("lm_var", (32, 64)), ("qkv_bn", (192, 256))):
+            # (only moves that change the step: a consumer's schedule / tile width where its norm point is
+            # folded, a producer's mode where a folded point reads it — plan_summary's rules.  A no-op move
+            # once "won" by 0.3 % of replay noise)
+            if ch.get("final"):
+                variant(f"lm_split={not ch.get('lm_split', False)}", chain={"lm_split": not ch.get("lm_split", False),
+                                                                            "lm_var": 64})
+            for key, pt, alts in (("qkv_var", "attn", (32, 64)), ("gu_var", "mlp", (32, 64)),
+                                  ("lm_var", "final", (32, 64)), ("qkv_bn", "attn", (192, 256))):
                 cur = ch.get(key, alts[0])
                 for v in alts:
-                    if v != cur:
+                    if v != cur and ch.get(pt):
                         variant(f"{key}={v}", chain={key: v})
-            for key in ("o", "down"):
+            for key, live in (("o", ch.get("mlp")), ("down", ch.get("attn") or ch.get("final"))):
                 for v in ("own32", "own64", "sumsq"):
-                    if v != ch.get(key):
+                    if v != ch.get(key) and live:
                         variant(f"{key}_producer={v}", chain={key: v})
         return moves
 

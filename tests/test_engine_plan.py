@@ -108,6 +108,12 @@ def test_step_plans_candidates_and_apply(monkeypatch):
         assert "gu=g4p" in mv and "qkv=g4p" not in mv
         p1 = m.with_move(plans["planner"], mv["gu=g4p"])
         assert p1["choices"]["gu"] == "g4p" and p1["chain"] == plans["planner"]["chain"]
+        # no move that leaves the step unchanged: a schedule / tile width / producer mode only where its norm
+        # point is folded
+        pc = plans["planner"]["chain"]
+        assert ("gu_var=32" in mv or "gu_var=64" in mv) == bool(pc["mlp"])
+        assert any(k.startswith("lm_") and k != "lm=g4p" for k in mv) == bool(pc["final"])
+        assert any(k.startswith("o_producer=") for k in mv) == bool(pc["mlp"])
         p2 = m.with_move(p1, mv["mlp_fold=True"])  # moves compose
         assert p2["chain"]["mlp"] and p2["choices"]["gu"] == "g4p" and not plans["planner"]["chain"]["mlp"]
         m.apply_step_plan(M, plans["library"])
