@@ -1106,13 +1106,13 @@ class LLMEngine:
             e1.synchronize()
             return e0.elapsed_time(e1)
 
-        def race(graphs: dict, rounds: int = 4) -> dict:
+        def race(graphs: dict, rounds: int = 4, raw: bool = False) -> dict:
             # interleaved replays (ABAB...): the clock's drift hits every candidate alike; median per candidate
             ts = {k: [] for k in graphs}
             for _ in range(rounds):
                 for k, (g, _) in graphs.items():
                     ts[k].append(replay_ms(g))
-            return {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
+            return ts if raw else {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
 
         def try_capture(name, plan):
             # a candidate that fails to build or capture (a kernel refusing its shape, say) drops out of the
@@ -1134,16 +1134,20 @@ class LLMEngine:
         del graphs
         kept = []
         if mode != "plans" and hasattr(self.model, "step_moves"):
-            # coordinate descent: each move raced against the incumbent (both graphs alive); kept when the
-            # incumbent / move ratio says > 0.25 % faster, and the incumbent becomes the new plan
+            # coordinate descent: each move raced against the incumbent (both graphs alive, 6 paired rounds);
+            # kept when the median move / incumbent ratio says > 0.25 % faster, and it becomes the incumbent
             for label, delta in self.model.step_moves(bk.B, cur):
                 cand = self.model.with_move(cur, delta)
                 gm = try_capture(label, cand)
                 if gm is None:
                     continue
-                r = race({"inc": inc, "mv": gm})
-                times[label] = r["mv"] * t_cur / r["inc"]  # on the incumbent's scale
-                if r["mv"] < r["inc"] * 0.9975:
+                # paired: the median of the per-round move / incumbent ratios (back-to-back replays share the
+                # clock state; separate medians let a no-op move "win" by 0.3 %)
+                r = race({"inc": inc, "mv": gm}, 6, raw=True)
+                ratios = sorted(a / b for a, b in zip(r["mv"], r["inc"]))
+                ratio = 0.5 * (ratios[len(ratios) // 2 - 1] + ratios[len(ratios) // 2])
+                times[label] = ratio * t_cur  # on the incumbent's scale
+                if ratio < 0.9975:
                     cur, inc, t_cur = cand, gm, times[label]
                     kept.append(label)
                 else:
