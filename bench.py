@@ -175,7 +175,7 @@ def main():
     # self-check (untimed, after the clock stopped): the last step's first request re-scored from all of its
     # candidates on one device must match what the candidate-parallel path produced (C1 all-gather +
     # consensus); the verdict is a MIN over every rank, and a mismatch fails the run
-    from llm_weighted_consensus_amd.embeddings.consensus import verify_sharded
+    from llm_weighted_consensus_amd.embeddings.consensus import LAST_VERIFY, verify_sharded
     verified = True
     if res is not None and last_cands[0]:
         verified = verify_sharded(scorer, last_cands[0][0], res, group=cgroup if cp > 1 else None)
@@ -217,6 +217,7 @@ def main():
             "data": "synthetic prompts (random token ids), random-init weights",
             "embeddings_per_s": round(emb_per_s, 2),
             "verified": verified,
+            "verify_detail": dict(LAST_VERIFY),
             "generated_tokens_per_s": round(G * N * a.gen_len * a.steps / elapsed, 1),
             "decode_plan": plan,
             "preflight": pre,

@@ -156,12 +156,16 @@ def bench_moe(a):
         comm.check()
     # untimed self-check: the last step's first request re-scored from all of its candidates on one device
     # (a MIN over every rank; a mismatch fails the run, see bench.py)
-    from llm_weighted_consensus_amd.embeddings.consensus import verify_sharded
+    from llm_weighted_consensus_amd.embeddings.consensus import LAST_VERIFY, verify_sharded
     gathered = not (emb_tp > 1 or tp == 1)
-    verified = verify_sharded(scorer, last[0][0], res, group=tp_group if gathered else None)
     # the TP embedder's per-layer all-reduces: 2 per layer of [tokens, d] bf16 over the process group
     ecfg = decoder_config(a.embedder)
     emb_tokens = R * N * (a.gen_len + 1)
+    # (the re-embedding takes the fp8 dense-MLP path the batch took: MX from DENSE_MX_MIN_ROWS rows on)
+    from llm_weighted_consensus_amd import ops as _ops
+    batch_rows = emb_tokens // (tp if gathered else 1)
+    with _ops.dense_mx_min_rows(0 if batch_rows >= _ops.DENSE_MX_MIN_ROWS else _ops.DENSE_MX_MIN_ROWS):
+        verified = verify_sharded(scorer, last[0][0], res, group=tp_group if gathered else None)
     ar_bytes = 2 * ecfg.layers * emb_tokens * ecfg.hidden * 2 if emb_tp > 1 else 0
     return {"metric": "consensus answers/sec (config 5: Mixtral-8x7B sampler + e5-mistral-7b embedder)",
             "value": round(dp * R / dt, 4), "unit": "answers/s", "n_gpus": 1 if shared else info.world,
@@ -172,6 +176,7 @@ def bench_moe(a):
             "data": "synthetic prompts (random token ids), random-init weights",
             "generated_tokens_per_s": round(dp * R * N * a.gen_len / dt, 1),
             "verified": verified,
+            "verify_detail": dict(LAST_VERIFY),
             "embedder_allreduce_bytes_per_step": ar_bytes,
             "world_size": pdist.world_size_seen(),
             "preflight": pre,

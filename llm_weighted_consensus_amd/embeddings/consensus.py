@@ -61,6 +61,9 @@ def gather_candidates(E_local: torch.Tensor, group=None) -> torch.Tensor:
     return G.permute(1, 0, 2, 3).reshape(R, -1, d).contiguous()
 
 
+LAST_VERIFY: dict = {}  # this process's last verify_sharded numbers (the benches put them in their JSON)
+
+
 def verify_sharded(scorer: "EmbeddingConsensus", local: Sequence[Sequence[int]], res: ConsensusResult,
                    group=None, request: int = 0, atol: float = 0.03) -> bool:
     """Self-check of a candidate-parallel consensus (a collective over every rank of the job).
@@ -87,11 +90,15 @@ def verify_sharded(scorer: "EmbeddingConsensus", local: Sequence[Sequence[int]],
     cen = res.centrality[request].float().cpu()
     best = res.best[request] if not isinstance(res.best, torch.Tensor) else int(res.best[request])
     ok = not res.partial and S.shape == ref.similarity[0].shape
+    LAST_VERIFY.clear()
     if ok:
-        ok = bool((S - ref.similarity[0]).abs().max() <= atol)
+        d_s = float((S - ref.similarity[0]).abs().max())
         top = torch.topk(ref.centrality[0], min(2, len(full))).values
-        ok = ok and (best == ref.best[0] or bool(top[0] - top[-1] <= atol))
-        ok = ok and bool((cen - ref.centrality[0]).abs().max() <= atol)
+        d_c = float((cen - ref.centrality[0]).abs().max())
+        same_best = best == int(ref.best[0])
+        LAST_VERIFY.update(similarity_max_abs=round(d_s, 5), centrality_max_abs=round(d_c, 5), same_best=same_best,
+                           top2_gap=round(float(top[0] - top[-1]), 5), atol=atol)
+        ok = d_s <= atol and (same_best or bool(top[0] - top[-1] <= atol)) and d_c <= atol
     if not on:
         return ok
     flag = torch.tensor([1.0 if ok else 0.0], device=eb.device if eb.is_cuda else "cpu")

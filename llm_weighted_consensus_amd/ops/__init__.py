@@ -11,6 +11,7 @@ Layout conventions shared with the engine:
 """
 from __future__ import annotations
 
+import contextlib
 import importlib
 import os
 import threading
@@ -794,6 +795,19 @@ def linear_fp8_swiglu(x, w: Fp8Weight, block: int):
 # rows, where gemm8g wins both projections (profiles/moe_round4.md); "LWC_DENSE_MX=0" keeps the row-scaled path
 DENSE_MX = os.environ.get("LWC_DENSE_MX", "1") != "0"
 DENSE_MX_MIN_ROWS = 16384
+
+
+@contextlib.contextmanager
+def dense_mx_min_rows(rows: int):
+    """Temporarily take the MX dense-MLP path from ``rows`` rows on (the benches' self-check re-embeds one
+    request's candidates — a few thousand rows — on the path the whole batch took, so it compares sharding,
+    not the MX vs row-quantised fp8 numerics: ~0.026 apart in cosine at config 5)."""
+    global DENSE_MX_MIN_ROWS
+    old, DENSE_MX_MIN_ROWS = DENSE_MX_MIN_ROWS, int(rows)
+    try:
+        yield
+    finally:
+        DENSE_MX_MIN_ROWS = old
 
 
 def dense_mx_ok(x, w_gu: Fp8Weight, w_down: Fp8Weight, block: int) -> bool:

@@ -158,3 +158,20 @@ def test_split_workspace_grows_and_keeps_old_buffers():
     t.start()
     t.join()
     assert other["ws"][0] is not p2  # another host thread gets its own counters
+
+
+def test_dense_mx_min_rows_context():
+    """The benches' self-check re-embeds on the batch's fp8 MLP path: the MX threshold is overridden inside the
+    context only, and restored on the way out (also after an exception)."""
+    from llm_weighted_consensus_amd import ops
+
+    base = ops.DENSE_MX_MIN_ROWS
+    with ops.dense_mx_min_rows(0):
+        assert ops.DENSE_MX_MIN_ROWS == 0
+    assert ops.DENSE_MX_MIN_ROWS == base
+    try:
+        with ops.dense_mx_min_rows(7):
+            raise ValueError
+    except ValueError:
+        pass
+    assert ops.DENSE_MX_MIN_ROWS == base
